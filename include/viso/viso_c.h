@@ -1,0 +1,196 @@
+/* viso_amd — MI355X-native (gfx950) visual-odometry hot path, C ABI.
+ *
+ * This is the drop-in boundary for the reference's per-frame path
+ * (Seasandwpy/viso).  Each entry point names the reference interface it
+ * replaces (file:line under the reference tree).  Conventions:
+ *   - every function returns int: VISO_OK (0) or a negative VISO_ERR_*;
+ *     nothing throws across this boundary;
+ *   - the caller owns host buffers; inputs are consumed (uploaded) before a
+ *     call returns unless the name says "_device" (then the pointers are HIP
+ *     device pointers that must stay valid until viso_synchronize());
+ *   - a viso_ctx is bound to one HIP device and one HIP stream; it is not
+ *     thread-safe; distinct contexts may run concurrently;
+ *   - no C++ or torch types cross this boundary.
+ */
+#ifndef VISO_C_H
+#define VISO_C_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VISO_OK 0
+#define VISO_ERR_ARG (-1)
+#define VISO_ERR_HIP (-2)
+#define VISO_ERR_CAPACITY (-3)
+#define VISO_ERR_STATE (-4)
+#define VISO_ERR_NODEVICE (-5)
+
+/* include/viso.h:13-17 */
+#define VISO_STATE_INITIALIZATION 0
+#define VISO_STATE_RUNNING 1
+#define VISO_STATE_FINISHED 2
+
+/* Constructor arguments Viso(fx, fy, cx, cy) (include/viso.h:47) plus the
+ * reference's hard-coded constants (include/viso.h:20-26) and the switches
+ * the reference does not have. */
+typedef struct viso_params {
+    double fx, fy, cx, cy;            /* include/viso.h:47-50 */
+    int32_t width, height;            /* level-0 frame size (continuous rows) */
+    int32_t reinitialize_after;       /* 10     include/viso.h:20 */
+    int32_t fast_thresh;              /* 50     include/viso.h:21 */
+    double projection_error_thresh;   /* 0.3    include/viso.h:22 */
+    double parallax_thresh;           /* 1 deg  include/viso.h:23 */
+    double disparity_squared_thresh;  /* 225    include/viso.h:24 */
+    double photometric_error_thresh;  /* 14400  include/viso.h:26 */
+    int32_t enable_tracking;          /* 0: as shipped (kFinished after init,
+                                         src/viso.cpp:97); 1: kRunning */
+    int32_t ransac_e_iters;           /* 1000 (OpenCV findEssentialMat default) */
+    int32_t ransac_h_iters;           /* 2000 (src/viso.cpp:240) */
+    double ransac_confidence;         /* 0.99 (src/viso.cpp:222,240) */
+    uint64_t ransac_seed;             /* counter-RNG seed of the samplers */
+    int32_t max_features;             /* capacity of FAST / KLT arrays */
+    int32_t max_poses;                /* capacity of the pose log */
+    int32_t batch_frames;             /* frames per viso_process_frames_device
+                                         chunk (frame-slot pool size) */
+    int32_t reserved[7];
+} viso_params;
+
+typedef struct viso_ctx viso_ctx;
+
+/* Defaults = the reference's constants (include/viso.h:20-26). */
+int viso_default_params(viso_params* p, double fx, double fy, double cx, double cy,
+                        int32_t width, int32_t height);
+
+/* Viso::Viso(fx,fy,cx,cy) (include/viso.h:47-52) on HIP device `device`. */
+int viso_create(const viso_params* p, int device, viso_ctx** out);
+int viso_destroy(viso_ctx* ctx);
+
+/* FrameSequence::FrameHandler::OnNewFrame(Keyframe::Ptr)
+ * (include/frame_sequence.h:13-16, implemented by Viso::OnNewFrame,
+ * src/viso.cpp:7-145).  `grey`: width x height u8 rows, `stride` bytes apart.
+ * Builds the 4-level pyramid (Keyframe ctor, include/keyframe.h:28-46). */
+int viso_process_frame(viso_ctx* ctx, const uint8_t* grey, int32_t width, int32_t height,
+                       int32_t stride);
+
+/* North-star facade VisualOdometryStereo::process(left, right, dims):
+ * dims = {width, height, stride}.  The left image drives the reference path;
+ * the right image is ingested into the same frame slot (pyramid) and fed to
+ * the stereo stage (viso_stereo_match).  (No reference counterpart: the
+ * reference is monocular) */
+int viso_process_stereo(viso_ctx* ctx, const uint8_t* left, const uint8_t* right,
+                        const int32_t dims[3]);
+
+/* Batched ingest of n consecutive frames already resident in HBM (device
+ * pointers, frame f at d_left + f * frame_stride, rows continuous).  Builds
+ * all pyramids of the chunk in one batched launch, then runs OnNewFrame per
+ * frame in order.  d_right may be NULL (mono). */
+int viso_process_frames_device(viso_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right,
+                               int32_t n, size_t frame_stride);
+
+/* Wait for all queued work of the context. */
+int viso_synchronize(viso_ctx* ctx);
+
+/* State (include/viso.h:44) */
+int viso_get_state(viso_ctx* ctx, int32_t* state);
+/* Viso::poses (include/viso.h:54): Tcw per tracked frame, 12 doubles each
+ * (R row-major, t).  *n receives the total count. */
+int viso_get_poses(viso_ctx* ctx, double* Tcw12, size_t cap, size_t* n);
+/* Viso::GetPoints() (include/viso.h:60-67): map points, 3 doubles each. */
+int viso_get_points(viso_ctx* ctx, double* xyz, size_t cap, size_t* n);
+/* Initialisation tracks: init_.kp1 / init_.kp2 (float x,y) and
+ * init_.success (include/viso.h:33-41). */
+int viso_get_init_tracks(viso_ctx* ctx, float* kp1, float* kp2, uint8_t* success, size_t cap,
+                         size_t* n);
+/* Last LKAlignment outputs (src/viso.cpp:768-843), dense over map points:
+ * pair_kf (-1 = no pair), success, uv_before, uv_after (2 doubles each). */
+int viso_get_alignment(viso_ctx* ctx, int32_t* pair_kf, uint8_t* success, double* uv_before,
+                       double* uv_after, size_t cap, size_t* n);
+/* Per-frame statistics of the last processed frame (16 doubles):
+ * [0] state, [1] tracked points, [2] nr_inliers, [3] best motion,
+ * [4] candidates, [5] init frame_cnt, [6] alignment pairs,
+ * [7] alignment successes, [8] disparity_squared, [9] direct-pose nGood
+ * (level 0), [10] direct-pose cost (level 0), [11] frames processed,
+ * [12] init succeeded on this frame, [13..15] reserved. */
+int viso_get_frame_stats(viso_ctx* ctx, double stats[16]);
+
+/* Kernel timing (HIP events on the context stream) for roofline accounting.
+ * kernel ids: see VISO_KERNEL_*.  When enabled, every launch of the kernel
+ * is bracketed by events; viso_timing_get returns the launch count and the
+ * summed milliseconds. */
+#define VISO_KERNEL_PYRAMID 0
+#define VISO_KERNEL_FAST 1
+#define VISO_KERNEL_KLT 2
+#define VISO_KERNEL_RANSAC 3
+#define VISO_KERNEL_SELECT 4
+#define VISO_KERNEL_DIRECT 5
+#define VISO_KERNEL_LKALIGN 6
+#define VISO_KERNEL_STEREO 7
+#define VISO_KERNEL_COUNT 8
+int viso_timing_enable(viso_ctx* ctx, int32_t enable);
+int viso_timing_get(viso_ctx* ctx, int32_t kernel, int64_t* launches, double* total_ms);
+
+/* ------------------------------------------------------------------------
+ * Stage-level entry points (host buffers in/out; synchronous).  Used by the
+ * parity tests; each runs the same device kernels as the frame path.
+ * ---------------------------------------------------------------------- */
+
+/* Sizes of the 4 pyramid levels: dims[2l] = w_l, dims[2l+1] = h_l;
+ * w_l = (int)(w_{l-1} * 0.5) (include/keyframe.h:42-43). */
+int viso_pyramid_dims(int32_t width, int32_t height, int32_t dims[8], size_t* total_bytes);
+
+/* Keyframe::Keyframe pyramid (include/keyframe.h:28-46) for n images at once:
+ * in: n * w * h bytes; out: n * total_bytes (levels concatenated). */
+int viso_pyramid(viso_ctx* ctx, const uint8_t* images, int32_t n, int32_t width, int32_t height,
+                 uint8_t* out);
+
+/* cv::FAST(img, kps, thresh) with NMS (src/viso.cpp:104): row-major
+ * keypoints; *n = total count (only cap written). */
+int viso_fast(viso_ctx* ctx, const uint8_t* image, int32_t width, int32_t height, int32_t thresh,
+              int32_t* xs, int32_t* ys, int32_t* scores, size_t cap, size_t* n);
+
+/* OpticalFlowMultiLevel(ref, cur, kp1, kp2, success, inverse=true)
+ * (src/viso.cpp:353-391): pyramids as produced by viso_pyramid. */
+int viso_klt(viso_ctx* ctx, const uint8_t* ref_pyr, const uint8_t* cur_pyr, int32_t width,
+             int32_t height, const float* kp1, float* kp2, uint8_t* success, int32_t n);
+
+/* DirectPoseEstimationMultiLayer (src/viso.cpp:760-766, one GN step per
+ * level as shipped).  poses: 12 doubles (R row-major, t). */
+int viso_direct_pose(viso_ctx* ctx, const uint8_t* last_pyr, const uint8_t* cur_pyr,
+                     int32_t width, int32_t height, const double* points, int32_t n_points,
+                     const double pose_last[12], double pose_io[12]);
+
+/* LKAlignment (src/viso.cpp:768-843) against n_kf keyframes. */
+int viso_lk_align(viso_ctx* ctx, const uint8_t* kf_pyrs, const double* kf_poses, int32_t n_kf,
+                  const uint8_t* cur_pyr, const double cur_pose[12], int32_t width,
+                  int32_t height, const double* points, int32_t n_points, int32_t* pair_kf,
+                  uint8_t* success, double* uv_before, double* uv_after);
+
+/* Viso::PoseEstimation2d2d (src/viso.cpp:178-256) followed by SelectMotion
+ * (src/viso.cpp:520-638) on normalised coordinates p1, p2 (n x 3 doubles,
+ * z = 1).  Outputs: R, T (T normalised by mean depth), inliers (n),
+ * points3d (n x 3; rows of outliers are zero), candidates (<= 5 x 12),
+ * stats = {nr_inliers, best_motion, n_candidates, disparity_sq,
+ *          e_inliers, h_inliers, e_iters, h_iters}. */
+int viso_pose_2d2d(viso_ctx* ctx, const double* p1, const double* p2, int32_t n, double R[9],
+                   double T[3], uint8_t* inliers, double* points3d, double* candidates,
+                   double stats[8]);
+
+/* North-star stereo stage: for each left keypoint (x, y integer pixels) find
+ * the right-image column by 8x8 SAD along the same row, disparities
+ * 0..max_disp (winner = smallest SAD, ties -> smallest disparity).  Outputs
+ * disparity (-1 = invalid) and best SAD.  No reference counterpart. */
+int viso_stereo_match(viso_ctx* ctx, const uint8_t* left, const uint8_t* right, int32_t width,
+                      int32_t height, const int32_t* xs, const int32_t* ys, int32_t n,
+                      int32_t max_disp, int32_t* disparity, int32_t* sad);
+
+/* Library build/version string (e.g. "viso_amd 0.1 gfx950"). */
+const char* viso_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VISO_C_H */

@@ -1,0 +1,126 @@
+// TEST INFRASTRUCTURE ONLY — shared helpers of the CPU oracle (see viso_oracle.h).
+#ifndef VISO_ORACLE_COMMON_HPP
+#define VISO_ORACLE_COMMON_HPP
+
+#include <cmath>
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+namespace oracle {
+
+constexpr int kLevels = 4;
+constexpr double kScales[kLevels] = {1.0, 0.5, 0.25, 0.125};  // include/keyframe.h:22
+constexpr int kHalfPatch = 4;                                  // include/viso.h:25
+
+struct PyrView {
+    const uint8_t* base;
+    int w[kLevels], h[kLevels];
+    size_t off[kLevels];
+    const uint8_t* level(int l) const { return base + off[l]; }
+};
+
+inline void pyramid_dims(int w, int h, int* ws, int* hs, size_t* offs) {
+    size_t off = 0;
+    for (int l = 0; l < kLevels; ++l) {
+        if (l > 0) {
+            // cv::Size(cols * 0.5, rows * 0.5): double -> int truncation (keyframe.h:43)
+            w = (int)(w * 0.5);
+            h = (int)(h * 0.5);
+        }
+        ws[l] = w;
+        hs[l] = h;
+        offs[l] = off;
+        off += (size_t)w * (size_t)h;
+    }
+}
+
+inline PyrView make_view(const uint8_t* base, int w, int h) {
+    PyrView v;
+    v.base = base;
+    pyramid_dims(w, h, v.w, v.h, v.off);
+    return v;
+}
+
+// Canonical pairwise tree sum over n leaves padded with +0.0 to a power of two.
+inline double tree_sum(const double* v, int n) {
+    if (n <= 0) return 0.0;
+    int p = 1;
+    while (p < n) p <<= 1;
+    std::vector<double> t((size_t)p, 0.0);
+    for (int i = 0; i < n; ++i) t[(size_t)i] = v[i];
+    for (int s = 1; s < p; s <<= 1)
+        for (int i = 0; i < p; i += 2 * s) t[(size_t)i] = t[(size_t)i] + t[(size_t)(i + s)];
+    return t[0];
+}
+
+// GetPixelValue (include/common.h:35-42, include/keyframe.h:50-57).  Base
+// pointer uses int() truncation, weights use x - floor(x).  Taps outside the
+// continuous level buffer read 0 (reference: reads outside the cv::Mat).
+inline double sample(const uint8_t* img, int w, int h, double x, double y) {
+    long long base;
+    bool finite = (x > -1e9 && x < 1e9 && y > -1e9 && y < 1e9);
+    long long n = (long long)w * (long long)h;
+    if (finite)
+        base = (long long)(int)y * (long long)w + (long long)(int)x;
+    else
+        base = -(1LL << 40);
+    auto tap = [&](long long idx) -> double {
+        return (idx >= 0 && idx < n) ? (double)img[idx] : 0.0;
+    };
+    double xx = x - std::floor(x);
+    double yy = y - std::floor(y);
+    double d0 = tap(base), d1 = tap(base + 1), d2 = tap(base + w), d3 = tap(base + w + 1);
+    return double((1 - xx) * (1 - yy) * d0 + xx * (1 - yy) * d1 + (1 - xx) * yy * d2 +
+                  xx * yy * d3);
+}
+
+inline void gradient(const uint8_t* img, int w, int h, double u, double v, double& gx,
+                     double& gy) {
+    // include/common.h:44-49
+    gx = 0.5 * (sample(img, w, h, u + 1, v) - sample(img, w, h, u - 1, v));
+    gy = 0.5 * (sample(img, w, h, u, v + 1) - sample(img, w, h, u, v - 1));
+}
+
+// Pose as (R row-major, t).  Tcw convention: Pc = R * Pw + t (keyframe.h:84).
+struct Pose {
+    double R[9];
+    double t[3];
+};
+
+inline void mat3_vec(const double* R, const double* p, double* out) {
+    // Eigen coefficient order: (R(i,0)*p0 + R(i,1)*p1) + R(i,2)*p2
+    for (int i = 0; i < 3; ++i) out[i] = R[3 * i + 0] * p[0] + R[3 * i + 1] * p[1] + R[3 * i + 2] * p[2];
+}
+
+// Keyframe::Project (include/keyframe.h:82-89)
+inline void project(const Pose& T, const double K[4], const double* P, int level, double& u,
+                    double& v) {
+    double uv1[3];
+    mat3_vec(T.R, P, uv1);
+    uv1[0] = uv1[0] + T.t[0];
+    uv1[1] = uv1[1] + T.t[1];
+    uv1[2] = uv1[2] + T.t[2];
+    double z = uv1[2];
+    uv1[0] = uv1[0] / z;
+    uv1[1] = uv1[1] / z;
+    u = kScales[level] * (uv1[0] * K[0] + K[2]);
+    v = kScales[level] * (uv1[1] * K[1] + K[3]);
+}
+
+// Keyframe::IsInside(u, v, level) (include/keyframe.h:77-80)
+inline bool is_inside(double u, double v, int w, int h) {
+    return u >= 0 && u < w && v >= 0 && v < h;
+}
+
+// counter-based RNG used by the RANSAC samplers (identical on the device)
+inline uint64_t mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+}  // namespace oracle
+
+#endif

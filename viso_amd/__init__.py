@@ -1,0 +1,11 @@
+"""viso_amd — MI355X-native (gfx950) hot path of the Seasandwpy/viso
+visual-odometry engine, behind the C ABI of include/viso/viso_c.h.
+
+Everything that touches pixels or points runs in hand-written HIP kernels in
+``viso_amd/libviso_amd.so``; this package is the thin host mirror of the
+reference interface.  There is no CPU fallback.
+"""
+from . import _lib  # noqa: F401
+from .api import Context, default_context, default_params, pyramid_dims  # noqa: F401
+
+__all__ = ["Context", "default_context", "default_params", "pyramid_dims"]

@@ -1,0 +1,111 @@
+"""ctypes binding of the C ABI (include/viso/viso_c.h).
+
+The product path loads ``viso_amd/libviso_amd.so`` (built in-tree by
+``viso_amd/build.py``).  There is no CPU fallback: if the library is missing
+or a call fails, an exception is raised.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libviso_amd.so")
+
+VISO_OK = 0
+ERRORS = {-1: "VISO_ERR_ARG", -2: "VISO_ERR_HIP", -3: "VISO_ERR_CAPACITY",
+          -4: "VISO_ERR_STATE", -5: "VISO_ERR_NODEVICE"}
+
+STATE_INITIALIZATION, STATE_RUNNING, STATE_FINISHED = 0, 1, 2
+KERNEL_IDS = {"pyramid": 0, "fast": 1, "klt": 2, "ransac": 3, "select": 4, "direct": 5,
+              "lkalign": 6, "stereo": 7}
+
+
+class VisoError(RuntimeError):
+    def __init__(self, fn: str, rc: int):
+        super().__init__(f"{fn} failed: {ERRORS.get(rc, rc)}")
+        self.rc = rc
+
+
+class viso_params(ctypes.Structure):
+    _fields_ = [
+        ("fx", ctypes.c_double), ("fy", ctypes.c_double),
+        ("cx", ctypes.c_double), ("cy", ctypes.c_double),
+        ("width", ctypes.c_int32), ("height", ctypes.c_int32),
+        ("reinitialize_after", ctypes.c_int32), ("fast_thresh", ctypes.c_int32),
+        ("projection_error_thresh", ctypes.c_double), ("parallax_thresh", ctypes.c_double),
+        ("disparity_squared_thresh", ctypes.c_double),
+        ("photometric_error_thresh", ctypes.c_double),
+        ("enable_tracking", ctypes.c_int32), ("ransac_e_iters", ctypes.c_int32),
+        ("ransac_h_iters", ctypes.c_int32), ("ransac_confidence", ctypes.c_double),
+        ("ransac_seed", ctypes.c_uint64), ("max_features", ctypes.c_int32),
+        ("max_poses", ctypes.c_int32), ("batch_frames", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 7),
+    ]
+
+
+_vp = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_sz = ctypes.c_size_t
+_d = ctypes.c_double
+
+# name -> argtypes (restype int unless listed in _RESTYPES)
+SIGNATURES = {
+    "viso_default_params": [_vp, _d, _d, _d, _d, _i32, _i32],
+    "viso_create": [_vp, ctypes.c_int, _vp],
+    "viso_destroy": [_vp],
+    "viso_process_frame": [_vp, _vp, _i32, _i32, _i32],
+    "viso_process_stereo": [_vp, _vp, _vp, _vp],
+    "viso_process_frames_device": [_vp, _vp, _vp, _i32, _sz],
+    "viso_synchronize": [_vp],
+    "viso_get_state": [_vp, _vp],
+    "viso_get_poses": [_vp, _vp, _sz, _vp],
+    "viso_get_points": [_vp, _vp, _sz, _vp],
+    "viso_get_init_tracks": [_vp, _vp, _vp, _vp, _sz, _vp],
+    "viso_get_alignment": [_vp, _vp, _vp, _vp, _vp, _sz, _vp],
+    "viso_get_frame_stats": [_vp, _vp],
+    "viso_timing_enable": [_vp, _i32],
+    "viso_timing_get": [_vp, _i32, _vp, _vp],
+    "viso_pyramid_dims": [_i32, _i32, _vp, _vp],
+    "viso_pyramid": [_vp, _vp, _i32, _i32, _i32, _vp],
+    "viso_fast": [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _sz, _vp],
+    "viso_klt": [_vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _i32],
+    "viso_direct_pose": [_vp, _vp, _vp, _i32, _i32, _vp, _i32, _vp, _vp],
+    "viso_lk_align": [_vp, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _vp, _i32, _vp, _vp, _vp,
+                      _vp],
+    "viso_pose_2d2d": [_vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp],
+    "viso_stereo_match": [_vp, _vp, _vp, _i32, _i32, _vp, _vp, _i32, _i32, _vp, _vp],
+    "viso_version": [],
+}
+_RESTYPES = {"viso_version": ctypes.c_char_p}
+
+_lib = None
+
+
+def load(path: str | None = None):
+    """Load the HIP library (raises if it has not been built)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise ImportError(
+            f"viso_amd: {p} not found — build it with `python -m viso_amd.build` "
+            "(there is no CPU fallback)")
+    lib = ctypes.CDLL(p)
+    for name, args in SIGNATURES.items():
+        fn = getattr(lib, name, None)
+        if fn is None:  # reported by tests/test_abi.py::test_exports
+            continue
+        fn.argtypes = args
+        fn.restype = _RESTYPES.get(name, ctypes.c_int)
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def call(name: str, *args) -> int:
+    rc = getattr(load(), name)(*args)
+    if rc != VISO_OK:
+        raise VisoError(name, rc)
+    return rc

@@ -1,0 +1,82 @@
+"""Build the gfx950 HIP library in-tree: viso_amd/libviso_amd.so.
+
+Every ``csrc/*.hip`` / ``csrc/*.cpp`` file is compiled by hipcc for
+``--offload-arch=gfx950`` with ``-ffp-contract=off`` (the numerics contract
+of DESIGN.md §Numerics) and linked into one shared library exporting the C
+ABI of ``include/viso/viso_c.h``.  Objects are rebuilt only when a source or
+header is newer than the object.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+OBJ = os.path.join(HERE, "_obj")
+LIB = os.path.join(HERE, "libviso_amd.so")
+HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("VISO_OFFLOAD_ARCH", "gfx950")
+
+COMMON = ["-std=c++17", "-O3", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}",
+          "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-Wall", "-Wno-unused-function",
+          "-Wno-unused-variable", "-Wno-unused-result"]
+
+
+def _headers():
+    hs = []
+    for d in (CSRC, os.path.join(ROOT, "include", "viso")):
+        for f in os.listdir(d):
+            if f.endswith((".hpp", ".h")):
+                hs.append(os.path.join(d, f))
+    return hs
+
+
+def _sources():
+    return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC)
+                  if f.endswith((".hip", ".cpp")))
+
+
+def _compile(src, hdr_mtime, verbose):
+    obj = os.path.join(OBJ, os.path.basename(src) + ".o")
+    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hdr_mtime):
+        return obj
+    cmd = [HIPCC, *COMMON, "-c", src, "-o", obj]
+    if src.endswith(".cpp"):
+        cmd = [HIPCC, *COMMON, "-x", "hip", "-c", src, "-o", obj]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError(f"hipcc failed on {src}")
+    return obj
+
+
+def build(verbose: bool = False) -> str:
+    os.makedirs(OBJ, exist_ok=True)
+    srcs = _sources()
+    hdr_mtime = max([os.path.getmtime(h) for h in _headers()] + [0.0])
+    jobs = min(len(srcs), int(os.environ.get("MAX_JOBS", "8")))
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        objs = list(ex.map(lambda s: _compile(s, hdr_mtime, verbose), srcs))
+    if os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(o) for o in objs):
+        return LIB
+    tmp = LIB + ".tmp"
+    cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", tmp, *objs, "-lpthread"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError("link failed")
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(verbose=True))

@@ -1,0 +1,114 @@
+// viso_amd — shared definitions for the gfx950 kernels and the host context.
+//
+// Numerics contract: fp64 everywhere the reference is
+// fp64, operand order as in the reference source, compiled with
+// -ffp-contract=off; every sum over patch pixels or points is the canonical
+// pairwise tree (xor-butterfly with ascending offsets on a wave64), so the
+// device reproduces the CPU oracle bit for bit.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <cstdio>
+
+namespace viso {
+
+constexpr int kLevels = 4;
+constexpr int kHalfPatch = 4;    // include/viso.h:25
+constexpr int kPatch = 64;       // (2*4)^2 pixels, one per wave64 lane
+constexpr int kMaxWidth = 4096;  // FAST row kernel LDS bound
+
+struct PyrGeom {
+    int w[kLevels], h[kLevels];
+    size_t off[kLevels];
+    size_t bytes;  // all levels
+    size_t slot;   // bytes per frame slot (bytes rounded up to 256)
+};
+
+inline PyrGeom make_geom(int w, int h) {
+    PyrGeom g{};
+    size_t off = 0;
+    for (int l = 0; l < kLevels; ++l) {
+        if (l > 0) {
+            w = (int)(w * 0.5);  // include/keyframe.h:43 (truncating Size(cols*0.5, rows*0.5))
+            h = (int)(h * 0.5);
+        }
+        g.w[l] = w;
+        g.h[l] = h;
+        g.off[l] = off;
+        off += (size_t)w * (size_t)h;
+    }
+    g.bytes = off;
+    g.slot = (off + 255) & ~(size_t)255;
+    return g;
+}
+
+// Pose: R row-major + t (Tcw: Pc = R*Pw + t, include/keyframe.h:84)
+struct Pose12 {
+    double v[12];
+};
+
+__host__ __device__ inline void mat3_vec(const double* R, const double* p, double* o) {
+    o[0] = R[0] * p[0] + R[1] * p[1] + R[2] * p[2];
+    o[1] = R[3] * p[0] + R[4] * p[1] + R[5] * p[2];
+    o[2] = R[6] * p[0] + R[7] * p[1] + R[8] * p[2];
+}
+
+// GetPixelValue (include/common.h:35-42): int() base, floor() weights,
+// taps outside the continuous level buffer read 0.
+__device__ inline double sample_px(const uint8_t* __restrict__ img, int w, int h, double x,
+                                   double y) {
+    const long long n = (long long)w * (long long)h;
+    const bool finite = (x > -1e9 && x < 1e9 && y > -1e9 && y < 1e9);
+    long long base = finite ? (long long)(int)y * (long long)w + (long long)(int)x : -(1LL << 40);
+    double d0 = (base >= 0 && base < n) ? (double)img[base] : 0.0;
+    double d1 = (base + 1 >= 0 && base + 1 < n) ? (double)img[base + 1] : 0.0;
+    double d2 = (base + w >= 0 && base + w < n) ? (double)img[base + w] : 0.0;
+    double d3 = (base + w + 1 >= 0 && base + w + 1 < n) ? (double)img[base + w + 1] : 0.0;
+    double xx = x - floor(x);
+    double yy = y - floor(y);
+    return double((1 - xx) * (1 - yy) * d0 + xx * (1 - yy) * d1 + (1 - xx) * yy * d2 +
+                  xx * yy * d3);
+}
+
+__device__ inline void gradient_px(const uint8_t* __restrict__ img, int w, int h, double u,
+                                   double v, double& gx, double& gy) {
+    gx = 0.5 * (sample_px(img, w, h, u + 1, v) - sample_px(img, w, h, u - 1, v));
+    gy = 0.5 * (sample_px(img, w, h, u, v + 1) - sample_px(img, w, h, u, v - 1));
+}
+
+// Canonical pairwise tree over the 64 lanes of a wave: ascending xor offsets.
+// Every lane ends with the same bits (a + b == b + a in IEEE arithmetic).
+__device__ inline double wave_tree_sum(double v) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) v = v + __shfl_xor(v, off, 64);
+    return v;
+}
+
+__device__ inline int wave_sum_int(int v) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// counter-based RNG of the RANSAC samplers (identical to the oracle's)
+__host__ __device__ inline uint64_t mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+}  // namespace viso
+
+#define VISO_HIP_CHECK(expr)                                                              \
+    do {                                                                                  \
+        hipError_t _e = (expr);                                                           \
+        if (_e != hipSuccess) {                                                           \
+            std::fprintf(stderr, "viso_amd: HIP error %s at %s:%d: %s\n", hipGetErrorName(_e), \
+                         __FILE__, __LINE__, #expr);                                      \
+            return VISO_ERR_HIP;                                                          \
+        }                                                                                 \
+    } while (0)

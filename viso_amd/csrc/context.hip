@@ -1,0 +1,219 @@
+// viso_amd — host context and C ABI (include/viso/viso_c.h).
+//
+// The context owns one HIP stream and all device memory of one sequence.
+// Host code here is the orchestration the reference does in
+// Viso::OnNewFrame (src/viso.cpp:7-145); every pixel/point loop runs in the
+// gfx950 kernels of image.hip / track.hip / direct.hip / geometry.hip.
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "context.hpp"
+
+using namespace viso;
+
+namespace viso {
+
+int DevBuf::ensure(size_t need) {
+    if (need <= bytes) return VISO_OK;
+    if (ptr) {
+        VISO_HIP_CHECK(hipFree(ptr));
+        ptr = nullptr;
+        bytes = 0;
+    }
+    size_t b = std::max<size_t>(need, 256);
+    VISO_HIP_CHECK(hipMalloc(&ptr, b));
+    bytes = b;
+    return VISO_OK;
+}
+
+void DevBuf::release() {
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    bytes = 0;
+}
+
+}  // namespace viso
+
+static int check_device_present() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return VISO_ERR_NODEVICE;
+    return VISO_OK;
+}
+
+extern "C" {
+
+const char* viso_version(void) { return "viso_amd 0.1 gfx950 (HIP)"; }
+
+int viso_default_params(viso_params* p, double fx, double fy, double cx, double cy, int32_t width,
+                        int32_t height) {
+    if (!p) return VISO_ERR_ARG;
+    std::memset(p, 0, sizeof(*p));
+    p->fx = fx;
+    p->fy = fy;
+    p->cx = cx;
+    p->cy = cy;
+    p->width = width;
+    p->height = height;
+    p->reinitialize_after = 10;          // include/viso.h:20
+    p->fast_thresh = 50;                 // include/viso.h:21
+    p->projection_error_thresh = 0.3;    // include/viso.h:22
+    p->parallax_thresh = 1.0;            // include/viso.h:23
+    p->disparity_squared_thresh = 225.0; // include/viso.h:24
+    p->photometric_error_thresh = (4.0 * 2) * (4.0 * 2) * 15 * 15;  // include/viso.h:26
+    p->enable_tracking = 0;
+    p->ransac_e_iters = 1000;
+    p->ransac_h_iters = 2000;
+    p->ransac_confidence = 0.99;
+    p->ransac_seed = 0x5eed5eedULL;
+    p->max_features = 32768;
+    p->max_poses = 65536;
+    p->batch_frames = 64;
+    return VISO_OK;
+}
+
+int viso_pyramid_dims(int32_t width, int32_t height, int32_t dims[8], size_t* total_bytes) {
+    if (width < 8 || height < 8 || !dims) return VISO_ERR_ARG;
+    PyrGeom g = make_geom(width, height);
+    for (int l = 0; l < kLevels; ++l) {
+        dims[2 * l] = g.w[l];
+        dims[2 * l + 1] = g.h[l];
+    }
+    if (total_bytes) *total_bytes = g.bytes;
+    return VISO_OK;
+}
+
+int viso_create(const viso_params* p, int device, viso_ctx** out) {
+    if (!p || !out) return VISO_ERR_ARG;
+    *out = nullptr;
+    if (p->width < 16 || p->height < 16 || p->width > kMaxWidth) return VISO_ERR_ARG;
+    if (p->max_features <= 0 || p->batch_frames <= 0) return VISO_ERR_ARG;
+    int rc = check_device_present();
+    if (rc != VISO_OK) return rc;
+    VISO_HIP_CHECK(hipSetDevice(device));
+    viso_ctx* c = new (std::nothrow) viso_ctx();
+    if (!c) return VISO_ERR_ARG;
+    c->p = *p;
+    c->device = device;
+    c->geom = make_geom(p->width, p->height);
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return VISO_ERR_HIP;
+    }
+    rc = c->init();
+    if (rc != VISO_OK) {
+        viso_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return VISO_OK;
+}
+
+int viso_destroy(viso_ctx* c) {
+    if (!c) return VISO_ERR_ARG;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    c->release();
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return VISO_OK;
+}
+
+int viso_synchronize(viso_ctx* c) {
+    if (!c) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipStreamSynchronize(c->stream));
+    return VISO_OK;
+}
+
+int viso_timing_enable(viso_ctx* c, int32_t enable) {
+    if (!c) return VISO_ERR_ARG;
+    c->timing.enabled = enable != 0;
+    return VISO_OK;
+}
+
+int viso_timing_get(viso_ctx* c, int32_t kernel, int64_t* launches, double* total_ms) {
+    if (!c || kernel < 0 || kernel >= VISO_KERNEL_COUNT) return VISO_ERR_ARG;
+    int rc = c->timing.collect();
+    if (rc != VISO_OK) return rc;
+    if (launches) *launches = c->timing.launches[kernel];
+    if (total_ms) *total_ms = c->timing.total_ms[kernel];
+    return VISO_OK;
+}
+
+// ----------------------------------------------------------- stage entry points
+int viso_pyramid(viso_ctx* c, const uint8_t* images, int32_t n, int32_t width, int32_t height,
+                 uint8_t* out) {
+    if (!c || !images || !out || n <= 0 || width < 8 || height < 8) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipSetDevice(c->device));
+    PyrGeom g = make_geom(width, height);
+    int rc = c->scratch_a.ensure(g.slot * (size_t)n);
+    if (rc) return rc;
+    uint8_t* d = (uint8_t*)c->scratch_a.ptr;
+    const size_t l0 = (size_t)width * height;
+    for (int i = 0; i < n; ++i)
+        VISO_HIP_CHECK(hipMemcpyAsync(d + g.slot * i, images + l0 * i, l0, hipMemcpyHostToDevice,
+                                      c->stream));
+    {
+        TimedRegion t(c->timing, VISO_KERNEL_PYRAMID, c->stream);
+        launch_pyramid(g, d, n, g.slot, c->stream);
+    }
+    VISO_HIP_CHECK(hipGetLastError());
+    for (int i = 0; i < n; ++i)
+        VISO_HIP_CHECK(hipMemcpyAsync(out + g.bytes * i, d + g.slot * i, g.bytes,
+                                      hipMemcpyDeviceToHost, c->stream));
+    VISO_HIP_CHECK(hipStreamSynchronize(c->stream));
+    return VISO_OK;
+}
+
+int viso_fast(viso_ctx* c, const uint8_t* image, int32_t width, int32_t height, int32_t thresh,
+              int32_t* xs, int32_t* ys, int32_t* scores, size_t cap, size_t* n) {
+    if (!c || !image || width < 8 || height < 8 || width > kMaxWidth) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipSetDevice(c->device));
+    const size_t npx = (size_t)width * height;
+    const size_t row_cap = fast_row_cap(width);
+    const size_t kcap = std::max<size_t>(cap, 1);
+    int rc = c->scratch_a.ensure(npx);
+    if (!rc) rc = c->scratch_b.ensure(sizeof(int) * (height + 1) + sizeof(int4) * row_cap * height);
+    if (!rc) rc = c->scratch_c.ensure(sizeof(int4) * kcap + sizeof(int));
+    if (rc) return rc;
+    uint8_t* d_img = (uint8_t*)c->scratch_a.ptr;
+    FastScratch s;
+    s.row_count = (int*)c->scratch_b.ptr;
+    s.row_list = (int4*)((char*)c->scratch_b.ptr + ((sizeof(int) * (height + 1) + 15) & ~(size_t)15));
+    int4* d_raw = (int4*)c->scratch_c.ptr;
+    int* d_n = (int*)((char*)c->scratch_c.ptr + sizeof(int4) * kcap);
+    VISO_HIP_CHECK(hipMemcpyAsync(d_img, image, npx, hipMemcpyHostToDevice, c->stream));
+    {
+        TimedRegion t(c->timing, VISO_KERNEL_FAST, c->stream);
+        launch_fast(d_img, width, height, thresh, s, nullptr, d_raw, (int)kcap, d_n, c->stream);
+    }
+    VISO_HIP_CHECK(hipGetLastError());
+    int total = 0;
+    VISO_HIP_CHECK(hipMemcpyAsync(&total, d_n, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    VISO_HIP_CHECK(hipStreamSynchronize(c->stream));
+    size_t m = std::min<size_t>((size_t)total, cap);
+    if (m > 0) {
+        std::vector<int4> raw(m);
+        VISO_HIP_CHECK(hipMemcpy(raw.data(), d_raw, sizeof(int4) * m, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < m; ++i) {
+            if (xs) xs[i] = raw[i].x;
+            if (ys) ys[i] = raw[i].y;
+            if (scores) scores[i] = raw[i].z;
+        }
+    }
+    if (n) *n = (size_t)total;
+    return VISO_OK;
+}
+
+}  // extern "C"
+
+int viso_ctx::init() { return VISO_OK; }
+
+void viso_ctx::release() {
+    timing.destroy();
+    scratch_a.release();
+    scratch_b.release();
+    scratch_c.release();
+    scratch_d.release();
+}
