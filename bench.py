@@ -1,0 +1,212 @@
+#!/usr/bin/env python3
+"""Benchmark: stereo frames/sec at 1242x375 grey through the HIP hot path.
+
+Workload (BASELINE.json configs[1]): one stereo sequence per GPU, 1242x375
+grey pairs, KITTI seq-00 intrinsics.  KITTI is not available offline, so the
+frames come from the repo's deterministic KITTI-like renderer (viso_amd.synth,
+seed = rank); they are rendered on the host and uploaded to HBM before the
+timed region.  A "step" is one stereo frame through
+viso_process_frames_device (batched pyramid build of left+right, then
+Viso::OnNewFrame on the left image, src/viso.cpp:7-145, with tracking
+enabled so the direct-pose GN and LK alignment run every frame).  The W warmup
+frames include the 2D-2D initialisation; the K timed frames are tracking
+frames.
+
+Multi-GPU (torchrun, one process per GPU): independent sequences, no
+data-path collective; after the timed frames the per-rank pose logs are
+all-gathered over RCCL (the trivial result gather of BASELINE.json config 4).
+value = total frames / max-over-ranks time (weak scaling).
+
+Prints ONE JSON line on rank 0 (the driver's contract), including:
+  roofline     — the HBM-bound image pass (pyramid),
+                 HIP-event timed inside this run;
+  cpu_baseline — the CPU oracle (single thread) on a bounded sample of the
+                 same sequence, timed on this host;
+  parity       — GPU vs oracle pose rel-Frobenius on the sampled frames.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "stereo frames/sec at 1242x375 grey, 1/2/4/8 GPUs; pose RMSE vs reference"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--width", type=int, default=1242)
+    ap.add_argument("--height", type=int, default=375)
+    ap.add_argument("--batch", type=int, default=50, help="frames per batched ingest call")
+    ap.add_argument("--cpu-frames", type=int, default=60,
+                    help="timed tracking frames of the CPU oracle sample (0 = skip)")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    distributed = world > 1
+    if distributed:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import viso_amd
+    from viso_amd import _lib
+    from viso_amd.synth import Sequence
+
+    W, H = args.width, args.height
+    n_total = args.warmup + args.steps
+    seq = Sequence(W, H, seed=rank)
+    t0 = time.time()
+    left = np.stack([seq.image(f, 0) for f in range(n_total)])
+    right = np.stack([seq.image(f, 1) for f in range(n_total)])
+    log(f"[rank {rank}] rendered {n_total} stereo pairs in {time.time() - t0:.1f}s")
+    d_left = torch.from_numpy(left).to(f"cuda:{local}")
+    d_right = torch.from_numpy(right).to(f"cuda:{local}")
+    torch.cuda.synchronize()
+    frame_bytes = W * H
+
+    v = viso_amd.Viso(*seq.K, width=W, height=H, device=local, enable_tracking=1,
+                      batch_frames=args.batch, max_poses=max(1024, n_total + 16))
+
+    def run(f0, n):
+        f = f0
+        while f < f0 + n:
+            m = min(args.batch, f0 + n - f)
+            v.process_device(d_left.data_ptr() + f * frame_bytes,
+                             d_right.data_ptr() + f * frame_bytes, m, frame_bytes)
+            f += m
+
+    # ---------------------------------------------------------- warmup
+    run(0, args.warmup)
+    v.synchronize()
+    n_pose_before = len(v.poses)
+    if v.state != 1:
+        log(f"[rank {rank}] warning: not tracking after warmup (state {v.state})")
+    v.ctx.timing_enable(True)
+
+    # ---------------------------------------------------------- timed
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    v.synchronize()
+    t_start = time.perf_counter()
+    run(args.warmup, args.steps)
+    v.synchronize()
+    poses = v.poses
+    pose_t = torch.from_numpy(poses[n_pose_before:].astype(np.float64)).to(f"cuda:{local}")
+    if distributed:
+        # result gather over RCCL (pad to the same length)
+        n_max = torch.tensor([pose_t.shape[0]], device=pose_t.device)
+        dist.all_reduce(n_max, op=dist.ReduceOp.MAX)
+        pad = torch.zeros((int(n_max.item()), 12), dtype=torch.float64, device=pose_t.device)
+        pad[:pose_t.shape[0]] = pose_t
+        gathered = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(gathered, pad)
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    if distributed:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    # ---------------------------------------------------------- kernel timing
+    timing = {}
+    for k in ("pyramid", "fast", "klt", "ransac", "direct", "lkalign"):
+        n_l, ms = v.ctx.timing(k)
+        if n_l:
+            timing[k] = {"launches": n_l, "avg_ms": ms / n_l, "total_ms": ms}
+    dims, total_bytes = viso_amd.pyramid_dims(W, H)
+    algo_bytes_img = dims[0][0] * dims[0][1] + sum(w * h for w, h in dims[1:])
+    roofline = None
+    if "pyramid" in timing:
+        # one timed launch group = the 3-level pyramid of every image of one
+        # ingest chunk (left + right)
+        imgs_per_launch = 2 * args.steps / timing["pyramid"]["launches"]
+        bytes_per_launch = algo_bytes_img * imgs_per_launch
+        achieved = bytes_per_launch / (timing["pyramid"]["avg_ms"] * 1e-3) / 1e9
+        roofline = {"kernel": "pyr_down_kernel x3 (batched image pass)", "bound": "hbm",
+                    "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "algorithmic_bytes_per_launch": int(bytes_per_launch),
+                    "images_per_launch": imgs_per_launch}
+    st = v.stats()
+    n_map = len(v.GetPoints())
+    value = world * args.steps / elapsed
+
+    # ---------------------------------------------------------- CPU baseline + parity
+    cpu = None
+    parity = None
+    if rank == 0 and not args.no_cpu and args.cpu_frames > 0:
+        from tests import oracle_lib
+        ov = oracle_lib.Viso(seq.K, W, H, enable_tracking=1)
+        for f in range(args.warmup):
+            ov.on_new_frame(left[f])
+        n_cpu = min(args.cpu_frames, args.steps)
+        t0 = time.perf_counter()
+        for f in range(args.warmup, args.warmup + n_cpu):
+            ov.on_new_frame(left[f])
+        cpu_s = time.perf_counter() - t0
+        cpu = {"value": round(n_cpu / cpu_s, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+               "sample": f"oracle/ C++ restatement, single thread, frames {args.warmup}-"
+                         f"{args.warmup + n_cpu - 1} (tracking) of the same synthetic sequence, "
+                         f"left image only (the reference is monocular)"}
+        oP = ov.poses()
+        gP = poses
+        m = min(len(oP), len(gP))
+        if m:
+            diff = np.linalg.norm(gP[:m] - oP[:m], axis=1) / np.maximum(np.linalg.norm(oP[:m], axis=1), 1e-300)
+            parity = {"frames": int(m), "max_rel_frobenius": float(diff.max()),
+                      "rmse_translation": float(np.sqrt(np.mean(np.sum((gP[:m, 9:] - oP[:m, 9:]) ** 2, 1))))}
+
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": "configs[1]: one 1242x375 grey stereo sequence per GPU, "
+                                   "KITTI seq-00 intrinsics, synthetic KITTI-like frames "
+                                   "(KITTI absent offline), tracking enabled",
+                       "width": W, "height": H, "map_points": n_map,
+                       "ingest_batch": args.batch, "parallelism": f"independent sequences x{world}"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "parity_vs_oracle": parity,
+            "speedup_vs_cpu": round(value / world / cpu["value"], 1) if cpu else None,
+            "kernels": {k: {"launches": t["launches"], "avg_ms": round(t["avg_ms"], 5)}
+                        for k, t in timing.items()},
+            "last_frame_stats": {"direct_nGood": st[9], "lk_pairs": st[6], "lk_success": st[7]},
+        }
+        print(json.dumps(out), flush=True)
+    if distributed:
+        dist.destroy_process_group()
+    del _lib
+
+
+if __name__ == "__main__":
+    main()

@@ -290,6 +290,15 @@ int oracle_viso_tracks(const oracle_viso* v, float* kp1, float* kp2, uint8_t* su
     return n;
 }
 
+int oracle_viso_keyframe_poses(const oracle_viso* v, double* out12, int cap) {
+    int n = (int)v->keyframes.size();
+    for (int j = 0; j < n && j < cap; ++j) {
+        std::memcpy(out12 + 12 * j, v->keyframes[(size_t)j]->R, 9 * sizeof(double));
+        std::memcpy(out12 + 12 * j + 9, v->keyframes[(size_t)j]->T, 3 * sizeof(double));
+    }
+    return n;
+}
+
 int oracle_viso_alignment(const oracle_viso* v, int32_t* pair_kf, uint8_t* success,
                           double* uv_before, double* uv_after, int cap) {
     int n = (int)v->al_kf.size();

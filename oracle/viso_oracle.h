@@ -160,6 +160,8 @@ void oracle_viso_points(const oracle_viso* v, double* out3);
 void oracle_viso_last_stats(const oracle_viso* v, double* out16);
 // Current init tracks (kp1, kp2 float x,y) and success flags.
 int oracle_viso_tracks(const oracle_viso* v, float* kp1, float* kp2, uint8_t* success, int cap);
+// Map keyframe poses (12 doubles each); returns the keyframe count.
+int oracle_viso_keyframe_poses(const oracle_viso* v, double* out12, int cap);
 // Last LK alignment outputs (dense over map points).
 int oracle_viso_alignment(const oracle_viso* v, int32_t* pair_kf, uint8_t* success,
                           double* uv_before, double* uv_after, int cap);

@@ -40,6 +40,7 @@ SIG = {
     "oracle_select_motion": ([_vp, _vp, _i, _vp, _vp, _i, _vp, _d, _d, _vp, _vp, _vp, _vp, _vp],
                              _i),
     "oracle_pose_2d2d": ([_vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], _i),
+    "oracle_recover_pose": ([_vp, _vp, _vp, _i, _vp, _vp, _vp], _i),
     "oracle_default_params": ([_vp, _d, _d, _d, _d, _i, _i], None),
     "oracle_viso_create": ([_vp], _vp),
     "oracle_viso_destroy": ([_vp], None),
@@ -52,6 +53,7 @@ SIG = {
     "oracle_viso_last_stats": ([_vp, _vp], None),
     "oracle_viso_tracks": ([_vp, _vp, _vp, _vp, _i], _i),
     "oracle_viso_alignment": ([_vp, _vp, _vp, _vp, _vp, _i], _i),
+    "oracle_viso_keyframe_poses": ([_vp, _vp, _i], _i),
 }
 
 _lib = None
@@ -101,6 +103,198 @@ def pyramid(img: np.ndarray) -> np.ndarray:
     out = np.zeros(lib.oracle_pyramid_bytes(w, h), np.uint8)
     lib.oracle_pyramid(ptr(img), w, h, ptr(out))
     return out
+
+
+def klt(ref_pyr, cur_pyr, w, h, kp1, kp2, thresh=14400.0):
+    lib = load()
+    kp1 = np.ascontiguousarray(kp1, np.float32)
+    kp2 = np.ascontiguousarray(kp2, np.float32).copy()
+    n = kp1.shape[0]
+    succ = np.zeros(n, np.uint8)
+    lib.oracle_klt(ptr(np.ascontiguousarray(ref_pyr)), ptr(np.ascontiguousarray(cur_pyr)), w, h,
+                   ptr(kp1), ptr(kp2), ptr(succ), n, thresh)
+    return kp2, succ
+
+
+def direct_pose(last_pyr, cur_pyr, w, h, K, points, pose_last, pose_init):
+    lib = load()
+    pts = np.ascontiguousarray(points, np.float64).reshape(-1, 3)
+    Kd = np.asarray(K, np.float64)
+    pl = np.ascontiguousarray(pose_last, np.float64).reshape(12)
+    pio = np.ascontiguousarray(pose_init, np.float64).reshape(12).copy()
+    lib.oracle_direct_pose(ptr(np.ascontiguousarray(last_pyr)), ptr(np.ascontiguousarray(cur_pyr)),
+                           w, h, ptr(Kd), ptr(pts), pts.shape[0], ptr(pl), ptr(pio))
+    return pio
+
+
+def lk_align(kf_pyrs, kf_poses, cur_pyr, cur_pose, w, h, K, points, thresh=14400.0):
+    lib = load()
+    kfs = [np.ascontiguousarray(k, np.uint8) for k in kf_pyrs]
+    arr = (ctypes.c_void_p * len(kfs))(*[k.ctypes.data for k in kfs])
+    kposes = np.ascontiguousarray(kf_poses, np.float64).reshape(-1, 12)
+    pts = np.ascontiguousarray(points, np.float64).reshape(-1, 3)
+    n = pts.shape[0]
+    pk = np.zeros(n, np.int32)
+    sc = np.zeros(n, np.uint8)
+    ub = np.zeros((n, 2))
+    ua = np.zeros((n, 2))
+    Kd = np.asarray(K, np.float64)
+    cp = np.ascontiguousarray(cur_pose, np.float64).reshape(12)
+    lib.oracle_lk_align(ctypes.cast(arr, ctypes.c_void_p), ptr(kposes), len(kfs),
+                        ptr(np.ascontiguousarray(cur_pyr)), ptr(cp), w, h, ptr(Kd), ptr(pts), n,
+                        thresh, ptr(pk), ptr(sc), ptr(ub), ptr(ua))
+    return pk, sc, ub, ua
+
+
+def pose_2d2d(p1, p2, K, w=1242, h=375, R0=None, T0=None, **kw):
+    lib = load()
+    p1 = np.ascontiguousarray(p1, np.float64).reshape(-1, 3)
+    p2 = np.ascontiguousarray(p2, np.float64).reshape(-1, 3)
+    n = p1.shape[0]
+    prm = params(K, w, h, **kw)
+    R = np.ascontiguousarray(np.eye(3) if R0 is None else R0, np.float64).reshape(9).copy()
+    T = np.ascontiguousarray(np.zeros(3) if T0 is None else T0, np.float64).reshape(3).copy()
+    inl = np.zeros(max(n, 1), np.uint8)
+    pts = np.zeros((max(n, 1), 3))
+    cand = np.zeros((5, 12))
+    st = np.zeros(8)
+    Kd = np.asarray(K, np.float64)
+    ran = lib.oracle_pose_2d2d(ptr(p1), ptr(p2), n, ptr(Kd), ctypes.byref(prm), ptr(R), ptr(T),
+                               ptr(inl), ptr(pts), ptr(cand), ptr(st))
+    return {"ran": ran, "R": R.reshape(3, 3), "T": T, "inliers": inl[:n], "points3d": pts[:n],
+            "candidates": cand[:int(st[2])], "stats": st}
+
+
+def triangulate(R, T, x1, x2):
+    lib = load()
+    R = np.ascontiguousarray(R, np.float64).reshape(9)
+    T = np.ascontiguousarray(T, np.float64).reshape(3)
+    a = np.ascontiguousarray(x1, np.float64).reshape(3)
+    b = np.ascontiguousarray(x2, np.float64).reshape(3)
+    P = np.zeros(3)
+    lib.oracle_triangulate(ptr(R), ptr(T), ptr(a), ptr(b), ptr(P))
+    return P
+
+
+def decompose_homography(H):
+    lib = load()
+    H = np.ascontiguousarray(H, np.float64).reshape(9)
+    Rs = np.zeros((4, 3, 3))
+    ts = np.zeros((4, 3))
+    ns = np.zeros((4, 3))
+    m = lib.oracle_decompose_homography(ptr(H), ptr(Rs), ptr(ts), ptr(ns))
+    return Rs[:m], ts[:m], ns[:m]
+
+
+def ransac(kind, q1, q2, thresh, conf=0.99, iters=1000, seed=0x5eed5eed):
+    lib = load()
+    q1 = np.ascontiguousarray(q1, np.float64).reshape(-1, 2)
+    q2 = np.ascontiguousarray(q2, np.float64).reshape(-1, 2)
+    n = q1.shape[0]
+    M = np.zeros(9)
+    mask = np.zeros(max(n, 1), np.uint8)
+    it = ctypes.c_int32(0)
+    fn = lib.oracle_ransac_essential if kind == "E" else lib.oracle_ransac_homography
+    good = fn(ptr(q1), ptr(q2), n, thresh, conf, iters, seed, ptr(M), ptr(mask), ctypes.byref(it))
+    return good, M.reshape(3, 3), mask[:n], it.value
+
+
+def recover_pose(E, q1, q2, mask):
+    lib = load()
+    q1 = np.ascontiguousarray(q1, np.float64).reshape(-1, 2)
+    q2 = np.ascontiguousarray(q2, np.float64).reshape(-1, 2)
+    mask = np.ascontiguousarray(mask, np.uint8).copy()
+    E = np.ascontiguousarray(E, np.float64).reshape(9)
+    R = np.zeros(9)
+    t = np.zeros(3)
+    good = lib.oracle_recover_pose(ptr(E), ptr(q1), ptr(q2), q1.shape[0], ptr(mask), ptr(R), ptr(t))
+    return good, R.reshape(3, 3), t, mask
+
+
+class OracleParams(ctypes.Structure):
+    _fields_ = [("fx", ctypes.c_double), ("fy", ctypes.c_double), ("cx", ctypes.c_double),
+                ("cy", ctypes.c_double), ("width", ctypes.c_int32), ("height", ctypes.c_int32),
+                ("reinitialize_after", ctypes.c_int32), ("fast_thresh", ctypes.c_int32),
+                ("projection_error_thresh", ctypes.c_double), ("parallax_thresh", ctypes.c_double),
+                ("disparity_squared_thresh", ctypes.c_double),
+                ("photometric_error_thresh", ctypes.c_double),
+                ("enable_tracking", ctypes.c_int32), ("ransac_e_iters", ctypes.c_int32),
+                ("ransac_h_iters", ctypes.c_int32), ("ransac_confidence", ctypes.c_double),
+                ("ransac_seed", ctypes.c_uint64)]
+
+
+def params(K, w, h, **kw):
+    p = OracleParams()
+    load().oracle_default_params(ctypes.byref(p), K[0], K[1], K[2], K[3], w, h)
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+class Viso:
+    """Oracle of the whole per-frame path (Viso::OnNewFrame)."""
+
+    def __init__(self, K, w, h, **kw):
+        self.lib = load()
+        self.p = params(K, w, h, **kw)
+        self.v = self.lib.oracle_viso_create(ctypes.byref(self.p))
+        self.w, self.h = w, h
+
+    def __del__(self):
+        try:
+            self.lib.oracle_viso_destroy(self.v)
+        except Exception:
+            pass
+
+    def on_new_frame(self, img):
+        img = np.ascontiguousarray(img, np.uint8)
+        assert img.shape == (self.h, self.w)
+        self.lib.oracle_viso_on_new_frame(self.v, ptr(img))
+
+    @property
+    def state(self):
+        return self.lib.oracle_viso_state(self.v)
+
+    def poses(self):
+        n = self.lib.oracle_viso_num_poses(self.v)
+        out = np.zeros((n, 12))
+        if n:
+            self.lib.oracle_viso_poses(self.v, ptr(out))
+        return out
+
+    def points(self):
+        n = self.lib.oracle_viso_num_points(self.v)
+        out = np.zeros((n, 3))
+        if n:
+            self.lib.oracle_viso_points(self.v, ptr(out))
+        return out
+
+    def stats(self):
+        out = np.zeros(16)
+        self.lib.oracle_viso_last_stats(self.v, ptr(out))
+        return out
+
+    def tracks(self):
+        cap = 1 << 16
+        k1 = np.zeros((cap, 2), np.float32)
+        k2 = np.zeros((cap, 2), np.float32)
+        s = np.zeros(cap, np.uint8)
+        n = self.lib.oracle_viso_tracks(self.v, ptr(k1), ptr(k2), ptr(s), cap)
+        return k1[:n].copy(), k2[:n].copy(), s[:n].copy()
+
+    def alignment(self):
+        cap = 1 << 16
+        pk = np.zeros(cap, np.int32)
+        s = np.zeros(cap, np.uint8)
+        ub = np.zeros((cap, 2))
+        ua = np.zeros((cap, 2))
+        n = self.lib.oracle_viso_alignment(self.v, ptr(pk), ptr(s), ptr(ub), ptr(ua), cap)
+        return pk[:n].copy(), s[:n].copy(), ub[:n].copy(), ua[:n].copy()
+
+    def keyframe_poses(self):
+        out = np.zeros((8, 12))
+        n = self.lib.oracle_viso_keyframe_poses(self.v, ptr(out), 8)
+        return out[:n].copy()
 
 
 def fast(img: np.ndarray, thresh: int, cap: int = 1 << 20):

@@ -7,5 +7,7 @@ reference interface.  There is no CPU fallback.
 """
 from . import _lib  # noqa: F401
 from .api import Context, default_context, default_params, pyramid_dims  # noqa: F401
+from .frontend import FrameHandler, FrameSequence, Keyframe, Viso  # noqa: F401
 
-__all__ = ["Context", "default_context", "default_params", "pyramid_dims"]
+__all__ = ["Context", "default_context", "default_params", "pyramid_dims", "Viso", "Keyframe",
+           "FrameSequence", "FrameHandler"]

@@ -92,6 +92,14 @@ def load(path: str | None = None):
         raise ImportError(
             f"viso_amd: {p} not found — build it with `python -m viso_amd.build` "
             "(there is no CPU fallback)")
+    # One HIP runtime per process: torch ships its own libamdhip64.so.7.  If
+    # torch is importable, load it first so that our NEEDED libamdhip64.so.7
+    # binds to the already-loaded copy (soname match); loading ours first
+    # would make torch map a second runtime that cannot open the device.
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
     lib = ctypes.CDLL(p)
     for name, args in SIGNATURES.items():
         fn = getattr(lib, name, None)

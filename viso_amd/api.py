@@ -92,6 +92,64 @@ class Context:
         m = min(n.value, cap)
         return xs[:m].copy(), ys[:m].copy(), sc[:m].copy()
 
+    def klt(self, ref_pyr: np.ndarray, cur_pyr: np.ndarray, width: int, height: int,
+            kp1: np.ndarray, kp2: np.ndarray):
+        """OpticalFlowMultiLevel(..., inverse=true) (src/viso.cpp:353-391).
+        kp1, kp2: (n,2) float32; returns (kp2_out, success)."""
+        kp1 = np.ascontiguousarray(kp1, dtype=np.float32)
+        kp2 = np.ascontiguousarray(kp2, dtype=np.float32).copy()
+        n = kp1.shape[0]
+        succ = np.zeros(n, np.uint8)
+        _lib.call("viso_klt", self.h, _p(np.ascontiguousarray(ref_pyr)),
+                  _p(np.ascontiguousarray(cur_pyr)), width, height, _p(kp1), _p(kp2), _p(succ), n)
+        return kp2, succ
+
+    def direct_pose(self, last_pyr, cur_pyr, width, height, points, pose_last, pose_init):
+        """DirectPoseEstimationMultiLayer (src/viso.cpp:760-766); poses 12 doubles."""
+        pts = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 3)
+        pl = np.ascontiguousarray(pose_last, dtype=np.float64).reshape(12)
+        pio = np.ascontiguousarray(pose_init, dtype=np.float64).reshape(12).copy()
+        _lib.call("viso_direct_pose", self.h, _p(np.ascontiguousarray(last_pyr)),
+                  _p(np.ascontiguousarray(cur_pyr)), width, height, _p(pts), pts.shape[0],
+                  _p(pl), _p(pio))
+        return pio
+
+    def lk_align(self, kf_pyrs, kf_poses, cur_pyr, cur_pose, width, height, points):
+        """LKAlignment (src/viso.cpp:768-843): dense per-map-point outputs
+        (pair_kf, success, uv_before (n,2), uv_after (n,2))."""
+        kfp = np.ascontiguousarray(np.stack(kf_pyrs) if isinstance(kf_pyrs, (list, tuple))
+                                   else kf_pyrs, dtype=np.uint8)
+        kposes = np.ascontiguousarray(kf_poses, dtype=np.float64).reshape(-1, 12)
+        pts = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 3)
+        n = pts.shape[0]
+        pk = np.zeros(n, np.int32)
+        sc = np.zeros(n, np.uint8)
+        ub = np.zeros((n, 2), np.float64)
+        ua = np.zeros((n, 2), np.float64)
+        cp = np.ascontiguousarray(cur_pose, dtype=np.float64).reshape(12)
+        _lib.call("viso_lk_align", self.h, _p(kfp), _p(kposes), kposes.shape[0],
+                  _p(np.ascontiguousarray(cur_pyr)), _p(cp), width, height, _p(pts), n, _p(pk),
+                  _p(sc), _p(ub), _p(ua))
+        return pk, sc, ub, ua
+
+    def pose_2d2d(self, p1: np.ndarray, p2: np.ndarray, R0=None, T0=None):
+        """PoseEstimation2d2d + SelectMotion (src/viso.cpp:178-256, 520-638) on
+        normalised (n,3) points.  Returns dict(R, T, inliers, points3d,
+        candidates, stats)."""
+        p1 = np.ascontiguousarray(p1, dtype=np.float64).reshape(-1, 3)
+        p2 = np.ascontiguousarray(p2, dtype=np.float64).reshape(-1, 3)
+        n = p1.shape[0]
+        R = np.ascontiguousarray(np.eye(3) if R0 is None else R0, dtype=np.float64).reshape(9).copy()
+        T = np.ascontiguousarray(np.zeros(3) if T0 is None else T0, dtype=np.float64).reshape(3).copy()
+        inl = np.zeros(max(n, 1), np.uint8)
+        pts = np.zeros((max(n, 1), 3), np.float64)
+        cand = np.zeros((5, 12), np.float64)
+        st = np.zeros(8, np.float64)
+        _lib.call("viso_pose_2d2d", self.h, _p(p1), _p(p2), n, _p(R), _p(T), _p(inl), _p(pts),
+                  _p(cand), _p(st))
+        return {"R": R.reshape(3, 3), "T": T, "inliers": inl[:n], "points3d": pts[:n],
+                "candidates": cand[:int(st[2])], "stats": st}
+
     # ------------------------------------------------------------ timing
     def timing_enable(self, on: bool = True):
         _lib.call("viso_timing_enable", self.h, 1 if on else 0)
@@ -107,10 +165,15 @@ class Context:
         _lib.call("viso_synchronize", self.h)
 
 
-def default_context(width: int = 640, height: int = 480, device: int = 0) -> Context:
-    key = (device,)
+def default_context(width: int = 640, height: int = 480, device: int = 0, K=None) -> Context:
+    """A cached context per (device, intrinsics).  The stage functions that
+    project points (direct_pose, lk_align, pose_2d2d) use the context's K,
+    as the reference's Viso members do (include/viso.h:28-29)."""
+    K = tuple(K) if K is not None else (517.3, 516.5, 325.1, 249.7)
+    key = (device, K)
     c = _ctx_cache.get(key)
     if c is None:
-        c = Context(default_params(width=width, height=height), device=device)
+        c = Context(default_params(fx=K[0], fy=K[1], cx=K[2], cy=K[3], width=width,
+                                   height=height), device=device)
         _ctx_cache[key] = c
     return c

@@ -45,6 +45,19 @@ inline PyrGeom make_geom(int w, int h) {
     return g;
 }
 
+// One frame's pyramid as per-level pointers.  Level 0 may live in the
+// caller's device buffer (batched ingest) while levels 1..3 live in a frame
+// slot of the context; every level is continuous (step == width).
+struct FrameDev {
+    const uint8_t* l[kLevels];
+};
+
+inline FrameDev frame_from_base(const uint8_t* base, const PyrGeom& g) {
+    FrameDev f;
+    for (int i = 0; i < kLevels; ++i) f.l[i] = base + g.off[i];
+    return f;
+}
+
 // Pose: R row-major + t (Tcw: Pc = R*Pw + t, include/keyframe.h:84)
 struct Pose12 {
     double v[12];

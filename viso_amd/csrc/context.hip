@@ -208,12 +208,140 @@ int viso_fast(viso_ctx* c, const uint8_t* image, int32_t width, int32_t height, 
 
 }  // extern "C"
 
-int viso_ctx::init() { return VISO_OK; }
 
-void viso_ctx::release() {
-    timing.destroy();
-    scratch_a.release();
-    scratch_b.release();
-    scratch_c.release();
-    scratch_d.release();
+// ----------------------------------------------------------- tracking stages
+extern "C" {
+
+int viso_klt(viso_ctx* c, const uint8_t* ref_pyr, const uint8_t* cur_pyr, int32_t width,
+             int32_t height, const float* kp1, float* kp2, uint8_t* success, int32_t n) {
+    if (!c || !ref_pyr || !cur_pyr || n < 0 || width < 16 || height < 16) return VISO_ERR_ARG;
+    if (n == 0) return VISO_OK;
+    if (!kp1 || !kp2 || !success) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipSetDevice(c->device));
+    PyrGeom g = make_geom(width, height);
+    Bump b;
+    size_t o_ref = b.take(g.bytes), o_cur = b.take(g.bytes), o_k1 = b.take(8 * (size_t)n),
+           o_k2 = b.take(8 * (size_t)n), o_s = b.take((size_t)n);
+    int rc = c->scratch_a.ensure(b.off);
+    if (rc) return rc;
+    char* base = (char*)c->scratch_a.ptr;
+    VISO_HIP_CHECK(hipMemcpyAsync(base + o_ref, ref_pyr, g.bytes, hipMemcpyHostToDevice, c->stream));
+    VISO_HIP_CHECK(hipMemcpyAsync(base + o_cur, cur_pyr, g.bytes, hipMemcpyHostToDevice, c->stream));
+    VISO_HIP_CHECK(hipMemcpyAsync(base + o_k1, kp1, 8 * (size_t)n, hipMemcpyHostToDevice, c->stream));
+    VISO_HIP_CHECK(hipMemcpyAsync(base + o_k2, kp2, 8 * (size_t)n, hipMemcpyHostToDevice, c->stream));
+    {
+        TimedRegion t(c->timing, VISO_KERNEL_KLT, c->stream);
+        launch_klt(frame_from_base((const uint8_t*)(base + o_ref), g),
+                   frame_from_base((const uint8_t*)(base + o_cur), g), g,
+                   (const float2*)(base + o_k1), (float2*)(base + o_k2), (uint8_t*)(base + o_s), n,
+                   c->p.photometric_error_thresh, c->stream);
+    }
+    VISO_HIP_CHECK(hipGetLastError());
+    VISO_HIP_CHECK(hipMemcpyAsync(kp2, base + o_k2, 8 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    VISO_HIP_CHECK(hipMemcpyAsync(success, base + o_s, (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    VISO_HIP_CHECK(hipStreamSynchronize(c->stream));
+    return VISO_OK;
 }
+
+int viso_direct_pose(viso_ctx* c, const uint8_t* last_pyr, const uint8_t* cur_pyr, int32_t width,
+                     int32_t height, const double* points, int32_t n, const double pose_last[12],
+                     double pose_io[12]) {
+    if (!c || !last_pyr || !cur_pyr || !pose_last || !pose_io || n < 0 || n > kMaxMapPoints)
+        return VISO_ERR_ARG;
+    if (n > 0 && !points) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipSetDevice(c->device));
+    PyrGeom g = make_geom(width, height);
+    Bump b;
+    size_t o_l = b.take(g.bytes), o_c = b.take(g.bytes), o_p = b.take(24 * (size_t)std::max(n, 1)),
+           o_pl = b.take(96), o_pio = b.take(96), o_se3 = b.take(56), o_tp = b.take(256 * 28 * 8),
+           o_tg = b.take(256 * 4);
+    int rc = c->scratch_a.ensure(b.off);
+    if (rc) return rc;
+    char* base = (char*)c->scratch_a.ptr;
+    VISO_HIP_CHECK(hipMemcpyAsync(base + o_l, last_pyr, g.bytes, hipMemcpyHostToDevice, c->stream));
+    VISO_HIP_CHECK(hipMemcpyAsync(base + o_c, cur_pyr, g.bytes, hipMemcpyHostToDevice, c->stream));
+    if (n > 0)
+        VISO_HIP_CHECK(hipMemcpyAsync(base + o_p, points, 24 * (size_t)n, hipMemcpyHostToDevice, c->stream));
+    VISO_HIP_CHECK(hipMemcpyAsync(base + o_pl, pose_last, 96, hipMemcpyHostToDevice, c->stream));
+    VISO_HIP_CHECK(hipMemcpyAsync(base + o_pio, pose_io, 96, hipMemcpyHostToDevice, c->stream));
+    DirectScratch ds;
+    ds.tile_part = (double*)(base + o_tp);
+    ds.tile_good = (int*)(base + o_tg);
+    const double K[4] = {c->p.fx, c->p.fy, c->p.cx, c->p.cy};
+    double* se3 = (double*)(base + o_se3);
+    launch_se3_from_pose((const double*)(base + o_pio), se3, c->stream);
+    {
+        TimedRegion t(c->timing, VISO_KERNEL_DIRECT, c->stream);
+        for (int level = kLevels - 1; level >= 0; --level)
+            launch_direct_level(frame_from_base((const uint8_t*)(base + o_l), g),
+                                frame_from_base((const uint8_t*)(base + o_c), g), g, K,
+                                (const double*)(base + o_p), n, (const double*)(base + o_pl), se3,
+                                level, ds, nullptr, c->stream);
+    }
+    launch_se3_to_pose(se3, (double*)(base + o_pio), nullptr, nullptr, c->stream);
+    VISO_HIP_CHECK(hipGetLastError());
+    VISO_HIP_CHECK(hipMemcpyAsync(pose_io, base + o_pio, 96, hipMemcpyDeviceToHost, c->stream));
+    VISO_HIP_CHECK(hipStreamSynchronize(c->stream));
+    return VISO_OK;
+}
+
+int viso_lk_align(viso_ctx* c, const uint8_t* kf_pyrs, const double* kf_poses, int32_t n_kf,
+                  const uint8_t* cur_pyr, const double cur_pose[12], int32_t width, int32_t height,
+                  const double* points, int32_t n, int32_t* pair_kf, uint8_t* success,
+                  double* uv_before, double* uv_after) {
+    if (!c || !kf_pyrs || !kf_poses || n_kf <= 0 || n_kf > kMaxKeyframes || !cur_pyr || !cur_pose ||
+        n < 0)
+        return VISO_ERR_ARG;
+    if (n == 0) return VISO_OK;
+    if (!points || !pair_kf || !success || !uv_before || !uv_after) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipSetDevice(c->device));
+    PyrGeom g = make_geom(width, height);
+    Bump b;
+    size_t o_kf = b.take(g.bytes * (size_t)n_kf), o_kp = b.take(96 * (size_t)n_kf),
+           o_c = b.take(g.bytes), o_cp = b.take(96), o_p = b.take(24 * (size_t)n),
+           o_pk = b.take(4 * (size_t)n), o_s = b.take((size_t)n), o_ub = b.take(16 * (size_t)n),
+           o_ua = b.take(16 * (size_t)n);
+    int rc = c->scratch_a.ensure(b.off);
+    if (rc) return rc;
+    char* base = (char*)c->scratch_a.ptr;
+    VISO_HIP_CHECK(hipMemcpyAsync(base + o_kf, kf_pyrs, g.bytes * (size_t)n_kf, hipMemcpyHostToDevice, c->stream));
+    VISO_HIP_CHECK(hipMemcpyAsync(base + o_kp, kf_poses, 96 * (size_t)n_kf, hipMemcpyHostToDevice, c->stream));
+    VISO_HIP_CHECK(hipMemcpyAsync(base + o_c, cur_pyr, g.bytes, hipMemcpyHostToDevice, c->stream));
+    VISO_HIP_CHECK(hipMemcpyAsync(base + o_cp, cur_pose, 96, hipMemcpyHostToDevice, c->stream));
+    VISO_HIP_CHECK(hipMemcpyAsync(base + o_p, points, 24 * (size_t)n, hipMemcpyHostToDevice, c->stream));
+    LkAlignArgs a{};
+    for (int j = 0; j < n_kf; ++j) a.kf[j] = frame_from_base((const uint8_t*)(base + o_kf + g.bytes * j), g);
+    a.kf_poses = (const double*)(base + o_kp);
+    a.n_kf = n_kf;
+    a.cur = frame_from_base((const uint8_t*)(base + o_c), g);
+    a.cur_pose = (const double*)(base + o_cp);
+    a.points = (const double*)(base + o_p);
+    a.n = n;
+    a.K[0] = c->p.fx;
+    a.K[1] = c->p.fy;
+    a.K[2] = c->p.cx;
+    a.K[3] = c->p.cy;
+    a.thresh = c->p.photometric_error_thresh;
+    for (int l = 0; l < kLevels; ++l) {
+        a.g.w[l] = g.w[l];
+        a.g.h[l] = g.h[l];
+        a.g.off[l] = g.off[l];
+    }
+    a.pair_kf = (int32_t*)(base + o_pk);
+    a.success = (uint8_t*)(base + o_s);
+    a.uv_before = (double*)(base + o_ub);
+    a.uv_after = (double*)(base + o_ua);
+    {
+        TimedRegion t(c->timing, VISO_KERNEL_LKALIGN, c->stream);
+        launch_lk_align(a, c->stream);
+    }
+    VISO_HIP_CHECK(hipGetLastError());
+    VISO_HIP_CHECK(hipMemcpyAsync(pair_kf, base + o_pk, 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    VISO_HIP_CHECK(hipMemcpyAsync(success, base + o_s, (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    VISO_HIP_CHECK(hipMemcpyAsync(uv_before, base + o_ub, 16 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    VISO_HIP_CHECK(hipMemcpyAsync(uv_after, base + o_ua, 16 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    VISO_HIP_CHECK(hipStreamSynchronize(c->stream));
+    return VISO_OK;
+}
+
+}  // extern "C"

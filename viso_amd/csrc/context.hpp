@@ -4,6 +4,7 @@
 #include <vector>
 
 #include "../../include/viso/viso_c.h"
+#include "geometry.hpp"
 #include "kernels.hpp"
 
 namespace viso {
@@ -65,6 +66,16 @@ struct Timing {
     }
 };
 
+// Bump sub-allocator over one DevBuf (stage entry points).
+struct Bump {
+    size_t off = 0;
+    size_t take(size_t bytes) {
+        size_t o = off;
+        off += (bytes + 255) & ~(size_t)255;
+        return o;
+    }
+};
+
 struct TimedRegion {
     Timing& t;
     int kernel;
@@ -87,6 +98,16 @@ struct TimedRegion {
 
 }  // namespace viso
 
+namespace viso {
+// One pyramid slot of the frame pool.  Level 0 is either in the slot or
+// borrowed from the caller's device buffer (batched ingest).
+struct SlotRec {
+    const uint8_t* l0 = nullptr;
+    bool borrowed = false;
+    int refs = 0;
+};
+}  // namespace viso
+
 struct viso_ctx {
     viso_params p{};
     int device = 0;
@@ -96,6 +117,66 @@ struct viso_ctx {
     // scratch for the stage-level entry points
     viso::DevBuf scratch_a, scratch_b, scratch_c, scratch_d;
 
+    // ---------------- frame pool (Keyframe objects; include/keyframe.h:10-123)
+    int n_slots = 0;
+    viso::DevBuf slot_pool;   // n_slots x geom.slot bytes
+    viso::DevBuf slot_pose;   // n_slots x 12 doubles (Keyframe R_, T_)
+    std::vector<viso::SlotRec> slots;
+    std::vector<int> free_slots;
+    int ref_slot = -1, last_slot = -1;  // init_.ref_frame, last_frame
+    std::vector<int> kf_slots;          // Map::keyframes_
+
+    // ---------------- initialisation tracks (Viso::Initialization, include/viso.h:33-41)
+    viso::DevBuf kp1, kp2, kp1b, kp2b, track_success, n_track_dev;
+    viso::FastScratch fast;
+    viso::DevBuf fast_rows;
+    int n_track = 0;
+    bool success_valid = false;
+    int frame_cnt = 0;
+    double initR[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    double initT[3] = {0, 0, 0};
+    double Kinv[9] = {0};
+
+    // ---------------- geometry (PoseEstimation2d2d + SelectMotion)
+    viso::DevBuf geo_buf;
+    viso::GeoArgs geo{};
+    viso::GeoCtl* h_ctl = nullptr;  // pinned
+    int* h_int = nullptr;           // pinned scratch ints
+    double* h_dbl = nullptr;        // pinned scratch doubles (64)
+
+    // ---------------- map (Map / MapPoint, include/map.h, map_point.h)
+    viso::DevBuf map_pts;  // kMaxMapPoints x 3
+    int n_map = 0;
+    viso::DevBuf kf_poses;  // kMaxKeyframes x 12
+
+    // ---------------- tracking (kRunning)
+    viso::DevBuf se3;           // 7 doubles
+    viso::DevBuf direct_tiles;  // 256 x 28 doubles + 256 ints
+    viso::DirectScratch direct{};
+    viso::DevBuf direct_stats;  // 4 levels x 50 doubles
+    viso::DevBuf lk_pair, lk_succ, lk_before, lk_after;
+    viso::DevBuf pose_log;  // max_poses x 12
+    viso::DevBuf pose_count;
+    int n_poses = 0;
+
+    // ---------------- state (include/viso.h:44)
+    int state = VISO_STATE_INITIALIZATION;
+    int64_t frames = 0;
+    double stats[16] = {0};
+    bool ran_tracking = false;
+
     int init();
     void release();
+    // frame pool
+    int acquire_slot();
+    void hold(int slot);
+    void drop(int slot);
+    void set_role(int& role, int slot);
+    viso::FrameDev frame(int slot) const;
+    uint8_t* slot_base(int slot) const;
+    double* pose_of(int slot) const;
+    int own_level0(int slot);
+    // OnNewFrame on a frame whose pyramid is already built in `slot`
+    int on_new_frame(int slot);
+    int ingest_host(const uint8_t* grey, int32_t w, int32_t h, int32_t stride, int* slot_out);
 };

@@ -1,0 +1,652 @@
+// viso_amd — the per-frame path: Viso::OnNewFrame (src/viso.cpp:7-145) as a
+// host state machine over device-resident state.
+//
+// All pixel/point work is on the GPU; the host only sequences launches.
+// Tracking frames (kRunning) never synchronise: direct pose (4 levels x 2
+// launches), SE3 -> pose, and LK alignment (1 launch) are queued back to
+// back and the pose stays in HBM (pose log).  Initialisation frames
+// synchronise once (to read the PoseEstimation2d2d result block) because the
+// state transition (src/viso.cpp:76-98) decides which kernels the next frame
+// runs.  Frames live in a slot pool (device pyramids + device poses); the
+// reference's shared_ptr<Keyframe> roles (ref_frame, last_frame, map
+// keyframes) are slot reference counts.
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "context.hpp"
+
+using namespace viso;
+
+namespace {
+
+// Eigen 3x3 inverse (compute_inverse<..., 3>): cofactors times 1/det;
+// K_inv = K.inverse() (include/viso.h:50).
+void eigen_inverse3(const double* m, double* inv) {
+    auto M = [&](int i, int j) { return m[3 * i + j]; };
+    auto cof = [&](int i, int j) {
+        int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+        return M(i1, j1) * M(i2, j2) - M(i1, j2) * M(i2, j1);
+    };
+    double c0[3] = {cof(0, 0), cof(1, 0), cof(2, 0)};
+    double det = (c0[0] * M(0, 0) + c0[1] * M(1, 0)) + c0[2] * M(2, 0);
+    double invdet = 1.0 / det;
+    inv[0] = c0[0] * invdet;
+    inv[1] = c0[1] * invdet;
+    inv[2] = c0[2] * invdet;
+    inv[3] = cof(0, 1) * invdet;
+    inv[4] = cof(1, 1) * invdet;
+    inv[5] = cof(2, 1) * invdet;
+    inv[6] = cof(0, 2) * invdet;
+    inv[7] = cof(1, 2) * invdet;
+    inv[8] = cof(2, 2) * invdet;
+}
+
+const double kIdentityPose[12] = {1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0};
+
+}  // namespace
+
+// ------------------------------------------------------------------ lifecycle
+int viso_ctx::init() {
+    const PyrGeom& g = geom;
+    const int cap = p.max_features;
+    n_slots = 2 * p.batch_frames + 8;
+    int rc = slot_pool.ensure(g.slot * (size_t)n_slots);
+    if (!rc) rc = slot_pose.ensure(sizeof(double) * 12 * (size_t)n_slots);
+    if (rc) return rc;
+    slots.assign((size_t)n_slots, SlotRec{});
+    free_slots.clear();
+    for (int s = n_slots - 1; s >= 0; --s) free_slots.push_back(s);
+    // tracks
+    const size_t kbytes = sizeof(float2) * (size_t)cap;
+    if (!rc) rc = kp1.ensure(kbytes);
+    if (!rc) rc = kp2.ensure(kbytes);
+    if (!rc) rc = kp1b.ensure(kbytes);
+    if (!rc) rc = kp2b.ensure(kbytes);
+    if (!rc) rc = track_success.ensure((size_t)cap);
+    if (!rc) rc = n_track_dev.ensure(256);
+    const size_t row_cap = fast_row_cap(g.w[0]);
+    const size_t rows_off = ((sizeof(int) * (g.h[0] + 1)) + 255) & ~(size_t)255;
+    if (!rc) rc = fast_rows.ensure(rows_off + sizeof(int4) * row_cap * g.h[0]);
+    if (rc) return rc;
+    fast.row_count = (int*)fast_rows.ptr;
+    fast.row_list = (int4*)((char*)fast_rows.ptr + rows_off);
+    // geometry
+    {
+        Bump b;
+        const size_t o_p1 = b.take(24 * (size_t)cap), o_p2 = b.take(24 * (size_t)cap),
+                     o_q1 = b.take(16 * (size_t)cap), o_q2 = b.take(16 * (size_t)cap),
+                     o_ctl = b.take(sizeof(GeoCtl)),
+                     o_em = b.take(72 * (size_t)std::max(p.ransac_e_iters, 1)),
+                     o_ev = b.take((size_t)std::max(p.ransac_e_iters, 1)),
+                     o_ec = b.take(4 * (size_t)std::max(p.ransac_e_iters, 1)),
+                     o_emk = b.take((size_t)cap),
+                     o_hm = b.take(72 * (size_t)std::max(p.ransac_h_iters, 1)),
+                     o_hv = b.take((size_t)std::max(p.ransac_h_iters, 1)),
+                     o_hc = b.take(4 * (size_t)std::max(p.ransac_h_iters, 1)),
+                     o_hmk = b.take((size_t)cap), o_si = b.take((size_t)kMaxCandidates * cap),
+                     o_sp = b.take(24 * (size_t)kMaxCandidates * cap), o_in = b.take((size_t)cap),
+                     o_po = b.take(24 * (size_t)cap);
+        rc = geo_buf.ensure(b.off);
+        if (rc) return rc;
+        char* base = (char*)geo_buf.ptr;
+        GeoArgs& a = geo;
+        std::memset(&a, 0, sizeof(a));
+        a.n_dev = (const int*)n_track_dev.ptr;
+        a.p1 = (double*)(base + o_p1);
+        a.p2 = (double*)(base + o_p2);
+        a.q1 = (double*)(base + o_q1);
+        a.q2 = (double*)(base + o_q2);
+        a.ctl = (GeoCtl*)(base + o_ctl);
+        a.e_models = (double*)(base + o_em);
+        a.e_valid = (uint8_t*)(base + o_ev);
+        a.e_counts = (int*)(base + o_ec);
+        a.e_mask = (uint8_t*)(base + o_emk);
+        a.h_models = (double*)(base + o_hm);
+        a.h_valid = (uint8_t*)(base + o_hv);
+        a.h_counts = (int*)(base + o_hc);
+        a.h_mask = (uint8_t*)(base + o_hmk);
+        a.sel_in = (uint8_t*)(base + o_si);
+        a.sel_pts = (double*)(base + o_sp);
+        a.inliers = (uint8_t*)(base + o_in);
+        a.points_out = (double*)(base + o_po);
+        a.cap = cap;
+        const double K[9] = {p.fx, 0, p.cx, 0, p.fy, p.cy, 0, 0, 1};
+        eigen_inverse3(K, Kinv);
+        for (int k = 0; k < 9; ++k) a.Kinv[k] = Kinv[k];
+        a.K[0] = p.fx;
+        a.K[1] = p.fy;
+        a.K[2] = p.cx;
+        a.K[3] = p.cy;
+        a.disparity_thresh = p.disparity_squared_thresh;
+        a.proj_thresh = p.projection_error_thresh;
+        a.parallax_thresh = p.parallax_thresh;
+        a.confidence = p.ransac_confidence;
+        // thresh = projection_error_thresh / sqrt(fx^2 + fy^2) (src/viso.cpp:191);
+        // OpenCV findInliers compares against (float)(thresh * thresh)
+        const double thr = p.projection_error_thresh / std::sqrt(p.fx * p.fx + p.fy * p.fy);
+        a.t2 = (float)(thr * thr);
+        a.seed = p.ransac_seed;
+        a.e_iters = p.ransac_e_iters;
+        a.h_iters = p.ransac_h_iters;
+    }
+    VISO_HIP_CHECK(hipHostMalloc((void**)&h_ctl, sizeof(GeoCtl)));
+    VISO_HIP_CHECK(hipHostMalloc((void**)&h_int, 64 * sizeof(int)));
+    VISO_HIP_CHECK(hipHostMalloc((void**)&h_dbl, 256 * sizeof(double)));
+    // map + tracking
+    if (!rc) rc = map_pts.ensure(24 * (size_t)kMaxMapPoints);
+    if (!rc) rc = kf_poses.ensure(96 * (size_t)kMaxKeyframes);
+    if (!rc) rc = se3.ensure(64);
+    if (!rc) rc = direct_tiles.ensure(256 * 28 * 8 + 256 * 4);
+    if (!rc) rc = direct_stats.ensure(4 * 50 * 8);
+    if (!rc) rc = lk_pair.ensure(4 * (size_t)kMaxMapPoints);
+    if (!rc) rc = lk_succ.ensure((size_t)kMaxMapPoints);
+    if (!rc) rc = lk_before.ensure(16 * (size_t)kMaxMapPoints);
+    if (!rc) rc = lk_after.ensure(16 * (size_t)kMaxMapPoints);
+    if (!rc) rc = pose_log.ensure(96 * (size_t)std::max(p.max_poses, 1));
+    if (!rc) rc = pose_count.ensure(256);
+    if (rc) return rc;
+    direct.tile_part = (double*)direct_tiles.ptr;
+    direct.tile_good = (int*)((char*)direct_tiles.ptr + 256 * 28 * 8);
+    VISO_HIP_CHECK(hipMemsetAsync(pose_count.ptr, 0, 256, stream));
+    VISO_HIP_CHECK(hipMemsetAsync(n_track_dev.ptr, 0, 256, stream));
+    VISO_HIP_CHECK(hipStreamSynchronize(stream));
+    return VISO_OK;
+}
+
+void viso_ctx::release() {
+    timing.destroy();
+    DevBuf* bufs[] = {&scratch_a, &scratch_b, &scratch_c, &scratch_d, &slot_pool, &slot_pose,
+                      &kp1, &kp2, &kp1b, &kp2b, &track_success, &n_track_dev, &fast_rows,
+                      &geo_buf, &map_pts, &kf_poses, &se3, &direct_tiles, &direct_stats,
+                      &lk_pair, &lk_succ, &lk_before, &lk_after, &pose_log, &pose_count};
+    for (DevBuf* b : bufs) b->release();
+    if (h_ctl) (void)hipHostFree(h_ctl);
+    if (h_int) (void)hipHostFree(h_int);
+    if (h_dbl) (void)hipHostFree(h_dbl);
+    h_ctl = nullptr;
+    h_int = nullptr;
+    h_dbl = nullptr;
+}
+
+// ------------------------------------------------------------------ frame pool
+int viso_ctx::acquire_slot() {
+    if (free_slots.empty()) return -1;
+    int s = free_slots.back();
+    free_slots.pop_back();
+    slots[(size_t)s] = SlotRec{};
+    slots[(size_t)s].l0 = slot_base(s);
+    return s;
+}
+
+void viso_ctx::hold(int s) {
+    if (s >= 0) slots[(size_t)s].refs += 1;
+}
+
+void viso_ctx::drop(int s) {
+    if (s < 0) return;
+    SlotRec& r = slots[(size_t)s];
+    if (--r.refs == 0) free_slots.push_back(s);
+}
+
+void viso_ctx::set_role(int& role, int s) {
+    if (role == s) return;
+    hold(s);
+    drop(role);
+    role = s;
+}
+
+uint8_t* viso_ctx::slot_base(int s) const { return (uint8_t*)slot_pool.ptr + geom.slot * (size_t)s; }
+
+double* viso_ctx::pose_of(int s) const { return (double*)slot_pose.ptr + 12 * (size_t)s; }
+
+FrameDev viso_ctx::frame(int s) const {
+    FrameDev f = frame_from_base(slot_base(s), geom);
+    f.l[0] = slots[(size_t)s].l0;
+    return f;
+}
+
+// A retained frame must not keep pointing into the caller's buffer.
+int viso_ctx::own_level0(int s) {
+    if (s < 0) return VISO_OK;
+    SlotRec& r = slots[(size_t)s];
+    if (!r.borrowed) return VISO_OK;
+    VISO_HIP_CHECK(hipMemcpyAsync(slot_base(s), r.l0, (size_t)geom.w[0] * geom.h[0],
+                                  hipMemcpyDeviceToDevice, stream));
+    r.l0 = slot_base(s);
+    r.borrowed = false;
+    return VISO_OK;
+}
+
+int viso_ctx::ingest_host(const uint8_t* grey, int32_t w, int32_t h, int32_t stride, int* slot_out) {
+    if (w != p.width || h != p.height || stride < w || !grey) return VISO_ERR_ARG;
+    int s = acquire_slot();
+    if (s < 0) return VISO_ERR_CAPACITY;
+    VISO_HIP_CHECK(hipMemcpy2DAsync(slot_base(s), (size_t)w, grey, (size_t)stride, (size_t)w, (size_t)h,
+                                    hipMemcpyHostToDevice, stream));
+    *slot_out = s;
+    return VISO_OK;
+}
+
+// ------------------------------------------------------------------ OnNewFrame
+int viso_ctx::on_new_frame(int cur) {
+    const PyrGeom& g = geom;
+    hold(cur);  // the "cur_frame" shared_ptr
+    for (int k = 0; k < 16; ++k) stats[k] = 0;
+    launch_set_pose(pose_of(cur), kIdentityPose, stream);  // Keyframe ctor: R = I, T = 0
+    const double K[4] = {p.fx, p.fy, p.cx, p.cy};
+    bool counted = true;  // ++init_.frame_cnt at the end of kInitialization
+    switch (state) {
+        case VISO_STATE_INITIALIZATION: {
+            if (frame_cnt > 0 && frame_cnt <= p.reinitialize_after) {
+                stats[3] = -1;
+                const int n = n_track;
+                if (n > 0) {
+                    TimedRegion t(timing, VISO_KERNEL_KLT, stream);
+                    launch_klt(frame(ref_slot), frame(cur), g, (const float2*)kp1.ptr,
+                               (float2*)kp2.ptr, (uint8_t*)track_success.ptr, n,
+                               p.photometric_error_thresh, stream);
+                }
+                // erase failed tracks (src/viso.cpp:23-40)
+                launch_compact_tracks((const float2*)kp1.ptr, (const float2*)kp2.ptr,
+                                      (const uint8_t*)track_success.ptr, n, (float2*)kp1b.ptr,
+                                      (float2*)kp2b.ptr, (int*)n_track_dev.ptr, stream);
+                std::swap(kp1, kp1b);
+                std::swap(kp2, kp2b);
+                success_valid = false;
+                geo.kp1 = (const float2*)kp1.ptr;
+                geo.kp2 = (const float2*)kp2.ptr;
+                geo.p1_in = geo.p2_in = nullptr;
+                {
+                    TimedRegion t(timing, VISO_KERNEL_RANSAC, stream);
+                    launch_pose_2d2d(geo, stream, &timing);
+                }
+                VISO_HIP_CHECK(hipGetLastError());
+                VISO_HIP_CHECK(hipMemcpyAsync(h_ctl, geo.ctl, sizeof(GeoCtl), hipMemcpyDeviceToHost, stream));
+                VISO_HIP_CHECK(hipStreamSynchronize(stream));
+                const GeoCtl& c = *h_ctl;
+                n_track = c.n;
+                int nr_inliers = 0;
+                if (c.gate) {
+                    nr_inliers = c.nr_inliers;
+                    if (c.best_motion >= 0) {
+                        std::memcpy(initR, c.R, sizeof(initR));
+                        std::memcpy(initT, c.T, sizeof(initT));
+                        success_valid = true;  // init_.success = best_inliers
+                    }
+                    stats[3] = c.best_motion;
+                    stats[4] = c.n_cand;
+                }
+                stats[1] = n_track;
+                stats[2] = nr_inliers;
+                stats[8] = c.disparity;
+                const double thresh = 0.9;
+                if (n_track > 50 && nr_inliers > 0 && (nr_inliers / (double)n_track) > thresh) {
+                    // map creation (src/viso.cpp:79-96)
+                    for (int s : kf_slots) drop(s);
+                    kf_slots.clear();
+                    kf_slots.push_back(ref_slot);
+                    kf_slots.push_back(cur);
+                    hold(ref_slot);
+                    hold(cur);
+                    double pose[12];
+                    std::memcpy(pose, initR, sizeof(initR));
+                    std::memcpy(pose + 9, initT, sizeof(initT));
+                    launch_set_pose(pose_of(cur), pose, stream);
+                    n_map = std::min(nr_inliers, kMaxMapPoints);
+                    VISO_HIP_CHECK(hipMemcpyAsync(map_pts.ptr, geo.points_out, 24 * (size_t)n_map,
+                                                  hipMemcpyDeviceToDevice, stream));
+                    for (size_t j = 0; j < kf_slots.size(); ++j)
+                        VISO_HIP_CHECK(hipMemcpyAsync((char*)kf_poses.ptr + 96 * j, pose_of(kf_slots[j]),
+                                                      96, hipMemcpyDeviceToDevice, stream));
+                    state = p.enable_tracking ? VISO_STATE_RUNNING : VISO_STATE_FINISHED;
+                    stats[12] = 1;
+                    counted = false;  // `break` skips ++frame_cnt (src/viso.cpp:98)
+                }
+            } else {
+                // re-detect (src/viso.cpp:100-108)
+                {
+                    TimedRegion t(timing, VISO_KERNEL_FAST, stream);
+                    launch_fast(frame(cur).l[0], g.w[0], g.h[0], p.fast_thresh, fast,
+                                (float2*)kp1.ptr, nullptr, p.max_features, (int*)n_track_dev.ptr,
+                                stream);
+                }
+                VISO_HIP_CHECK(hipGetLastError());
+                VISO_HIP_CHECK(hipMemcpyAsync(h_int, n_track_dev.ptr, sizeof(int), hipMemcpyDeviceToHost, stream));
+                VISO_HIP_CHECK(hipStreamSynchronize(stream));
+                n_track = std::min(h_int[0], p.max_features);
+                h_int[1] = n_track;
+                VISO_HIP_CHECK(hipMemcpyAsync(n_track_dev.ptr, &h_int[1], sizeof(int), hipMemcpyHostToDevice, stream));
+                if (n_track > 0)
+                    VISO_HIP_CHECK(hipMemcpyAsync(kp2.ptr, kp1.ptr, sizeof(float2) * (size_t)n_track,
+                                                  hipMemcpyDeviceToDevice, stream));
+                success_valid = false;
+                set_role(ref_slot, cur);
+                frame_cnt = 0;
+                stats[1] = n_track;
+            }
+            if (counted) ++frame_cnt;
+            break;
+        }
+        case VISO_STATE_RUNNING: {
+            // Sophus::SE3d X(last_frame->GetR(), last_frame->GetT()) (src/viso.cpp:114)
+            launch_se3_from_pose(pose_of(last_slot), (double*)se3.ptr, stream);
+            {
+                TimedRegion t(timing, VISO_KERNEL_DIRECT, stream);
+                for (int level = kLevels - 1; level >= 0; --level)
+                    launch_direct_level(frame(last_slot), frame(cur), g, K, (const double*)map_pts.ptr,
+                                        n_map, pose_of(last_slot), (double*)se3.ptr, level, direct,
+                                        (double*)direct_stats.ptr + 50 * level, stream);
+            }
+            // cur_frame->SetR/SetT(X); poses.push_back(X) (src/viso.cpp:117-118, 137)
+            const bool log = n_poses < p.max_poses;
+            launch_se3_to_pose((const double*)se3.ptr, pose_of(cur), log ? (double*)pose_log.ptr : nullptr,
+                               log ? (int*)pose_count.ptr : nullptr, stream);
+            if (log) ++n_poses;
+            // LKAlignment (src/viso.cpp:121, 768-843)
+            LkAlignArgs a{};
+            a.n_kf = (int)kf_slots.size();
+            for (int j = 0; j < a.n_kf; ++j) a.kf[j] = frame(kf_slots[(size_t)j]);
+            a.kf_poses = (const double*)kf_poses.ptr;
+            a.cur = frame(cur);
+            a.cur_pose = pose_of(cur);
+            a.points = (const double*)map_pts.ptr;
+            a.n = n_map;
+            a.K[0] = p.fx;
+            a.K[1] = p.fy;
+            a.K[2] = p.cx;
+            a.K[3] = p.cy;
+            a.thresh = p.photometric_error_thresh;
+            for (int l = 0; l < kLevels; ++l) {
+                a.g.w[l] = g.w[l];
+                a.g.h[l] = g.h[l];
+                a.g.off[l] = g.off[l];
+            }
+            a.pair_kf = (int32_t*)lk_pair.ptr;
+            a.success = (uint8_t*)lk_succ.ptr;
+            a.uv_before = (double*)lk_before.ptr;
+            a.uv_after = (double*)lk_after.ptr;
+            {
+                TimedRegion t(timing, VISO_KERNEL_LKALIGN, stream);
+                launch_lk_align(a, stream);
+            }
+            ran_tracking = true;
+            break;
+        }
+        default:
+            break;
+    }
+    VISO_HIP_CHECK(hipGetLastError());
+    set_role(last_slot, cur);  // last_frame = cur_frame (src/viso.cpp:144)
+    drop(cur);
+    ++frames;
+    stats[0] = state;
+    stats[5] = frame_cnt;
+    stats[11] = (double)frames;
+    stats[13] = success_valid ? 1 : 0;
+    return VISO_OK;
+}
+
+// ------------------------------------------------------------------ C ABI
+extern "C" {
+
+int viso_process_frame(viso_ctx* c, const uint8_t* grey, int32_t width, int32_t height,
+                       int32_t stride) {
+    if (!c) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipSetDevice(c->device));
+    int s = -1;
+    int rc = c->ingest_host(grey, width, height, stride, &s);
+    if (rc) return rc;
+    uint8_t* slot = c->slot_base(s);
+    const uint8_t* l0 = slot;
+    {
+        TimedRegion t(c->timing, VISO_KERNEL_PYRAMID, c->stream);
+        launch_pyramid_frames(c->geom, &l0, &slot, 1, c->stream);
+    }
+    VISO_HIP_CHECK(hipGetLastError());
+    rc = c->on_new_frame(s);
+    return rc;
+}
+
+int viso_process_stereo(viso_ctx* c, const uint8_t* left, const uint8_t* right,
+                        const int32_t dims[3]) {
+    if (!c || !left || !right || !dims) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipSetDevice(c->device));
+    int sl = -1, sr = -1;
+    int rc = c->ingest_host(left, dims[0], dims[1], dims[2], &sl);
+    if (rc) return rc;
+    rc = c->ingest_host(right, dims[0], dims[1], dims[2], &sr);
+    if (rc) {
+        c->hold(sl);
+        c->drop(sl);
+        return rc;
+    }
+    uint8_t* slots[2] = {c->slot_base(sl), c->slot_base(sr)};
+    const uint8_t* l0s[2] = {slots[0], slots[1]};
+    {
+        TimedRegion t(c->timing, VISO_KERNEL_PYRAMID, c->stream);
+        launch_pyramid_frames(c->geom, l0s, slots, 2, c->stream);
+    }
+    VISO_HIP_CHECK(hipGetLastError());
+    // the right pyramid is the stereo stage's input (viso_stereo_match); the
+    // reference path runs on the left image only
+    c->hold(sr);
+    c->drop(sr);
+    return c->on_new_frame(sl);
+}
+
+int viso_process_frames_device(viso_ctx* c, const uint8_t* d_left, const uint8_t* d_right,
+                               int32_t n, size_t frame_stride) {
+    if (!c || !d_left || n < 0) return VISO_ERR_ARG;
+    if (frame_stride < (size_t)c->geom.w[0] * c->geom.h[0]) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipSetDevice(c->device));
+    const int B = c->p.batch_frames;
+    for (int f0 = 0; f0 < n; f0 += B) {
+        const int nb = std::min(B, n - f0);
+        const int sides = d_right ? 2 : 1;
+        std::vector<int> sl;
+        std::vector<const uint8_t*> l0;
+        std::vector<uint8_t*> dst;
+        for (int i = 0; i < nb * sides; ++i) {
+            const int s = c->acquire_slot();
+            if (s < 0) {
+                for (int x : sl) {
+                    c->hold(x);
+                    c->drop(x);
+                }
+                return VISO_ERR_CAPACITY;
+            }
+            const int f = f0 + (i % nb);
+            const uint8_t* src = (i < nb ? d_left : d_right) + frame_stride * (size_t)f;
+            c->slots[(size_t)s].l0 = src;
+            c->slots[(size_t)s].borrowed = true;
+            c->hold(s);  // pending in this chunk
+            sl.push_back(s);
+            l0.push_back(src);
+            dst.push_back(c->slot_base(s));
+        }
+        {
+            TimedRegion t(c->timing, VISO_KERNEL_PYRAMID, c->stream);
+            launch_pyramid_frames(c->geom, l0.data(), dst.data(), (int)l0.size(), c->stream);
+        }
+        VISO_HIP_CHECK(hipGetLastError());
+        for (int i = 0; i < nb; ++i) {
+            int rc = c->on_new_frame(sl[(size_t)i]);
+            if (rc) return rc;
+        }
+        // frames still referenced after the chunk get their own level 0
+        int roles[3] = {c->ref_slot, c->last_slot, -1};
+        for (int r : roles) {
+            int rc = c->own_level0(r);
+            if (rc) return rc;
+        }
+        for (int s : c->kf_slots) {
+            int rc = c->own_level0(s);
+            if (rc) return rc;
+        }
+        for (int s : sl) c->drop(s);
+    }
+    return VISO_OK;
+}
+
+int viso_get_state(viso_ctx* c, int32_t* state) {
+    if (!c || !state) return VISO_ERR_ARG;
+    *state = c->state;
+    return VISO_OK;
+}
+
+int viso_get_poses(viso_ctx* c, double* Tcw12, size_t cap, size_t* n) {
+    if (!c) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipSetDevice(c->device));
+    const size_t m = std::min(cap, (size_t)c->n_poses);
+    if (m > 0 && Tcw12) {
+        VISO_HIP_CHECK(hipMemcpyAsync(Tcw12, c->pose_log.ptr, 96 * m, hipMemcpyDeviceToHost, c->stream));
+    }
+    VISO_HIP_CHECK(hipStreamSynchronize(c->stream));
+    if (n) *n = (size_t)c->n_poses;
+    return VISO_OK;
+}
+
+int viso_get_points(viso_ctx* c, double* xyz, size_t cap, size_t* n) {
+    if (!c) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipSetDevice(c->device));
+    const size_t m = std::min(cap, (size_t)c->n_map);
+    if (m > 0 && xyz)
+        VISO_HIP_CHECK(hipMemcpyAsync(xyz, c->map_pts.ptr, 24 * m, hipMemcpyDeviceToHost, c->stream));
+    VISO_HIP_CHECK(hipStreamSynchronize(c->stream));
+    if (n) *n = (size_t)c->n_map;
+    return VISO_OK;
+}
+
+int viso_get_init_tracks(viso_ctx* c, float* kp1, float* kp2, uint8_t* success, size_t cap,
+                         size_t* n) {
+    if (!c) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipSetDevice(c->device));
+    const size_t m = std::min(cap, (size_t)c->n_track);
+    if (m > 0) {
+        if (kp1) VISO_HIP_CHECK(hipMemcpyAsync(kp1, c->kp1.ptr, 8 * m, hipMemcpyDeviceToHost, c->stream));
+        if (kp2) VISO_HIP_CHECK(hipMemcpyAsync(kp2, c->kp2.ptr, 8 * m, hipMemcpyDeviceToHost, c->stream));
+        if (success) {
+            if (c->success_valid)
+                VISO_HIP_CHECK(hipMemcpyAsync(success, c->geo.inliers, m, hipMemcpyDeviceToHost, c->stream));
+            else
+                std::memset(success, 0, m);
+        }
+    }
+    VISO_HIP_CHECK(hipStreamSynchronize(c->stream));
+    if (n) *n = (size_t)c->n_track;
+    return VISO_OK;
+}
+
+int viso_get_alignment(viso_ctx* c, int32_t* pair_kf, uint8_t* success, double* uv_before,
+                       double* uv_after, size_t cap, size_t* n) {
+    if (!c) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipSetDevice(c->device));
+    const size_t m = c->ran_tracking ? std::min(cap, (size_t)c->n_map) : 0;
+    if (m > 0) {
+        if (pair_kf) VISO_HIP_CHECK(hipMemcpyAsync(pair_kf, c->lk_pair.ptr, 4 * m, hipMemcpyDeviceToHost, c->stream));
+        if (success) VISO_HIP_CHECK(hipMemcpyAsync(success, c->lk_succ.ptr, m, hipMemcpyDeviceToHost, c->stream));
+        if (uv_before) VISO_HIP_CHECK(hipMemcpyAsync(uv_before, c->lk_before.ptr, 16 * m, hipMemcpyDeviceToHost, c->stream));
+        if (uv_after) VISO_HIP_CHECK(hipMemcpyAsync(uv_after, c->lk_after.ptr, 16 * m, hipMemcpyDeviceToHost, c->stream));
+    }
+    VISO_HIP_CHECK(hipStreamSynchronize(c->stream));
+    if (n) *n = c->ran_tracking ? (size_t)c->n_map : 0;
+    return VISO_OK;
+}
+
+int viso_get_frame_stats(viso_ctx* c, double out[16]) {
+    if (!c || !out) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipSetDevice(c->device));
+    std::memcpy(out, c->stats, sizeof(c->stats));
+    if (c->state == VISO_STATE_RUNNING && c->stats[12] == 0 && c->ran_tracking) {
+        // last frame was a tracking frame: level-0 direct stats + LK counts
+        const int m = c->n_map;
+        std::vector<int32_t> pk((size_t)m);
+        std::vector<uint8_t> sc((size_t)m);
+        if (m > 0) {
+            VISO_HIP_CHECK(hipMemcpyAsync(pk.data(), c->lk_pair.ptr, 4 * (size_t)m, hipMemcpyDeviceToHost, c->stream));
+            VISO_HIP_CHECK(hipMemcpyAsync(sc.data(), c->lk_succ.ptr, (size_t)m, hipMemcpyDeviceToHost, c->stream));
+        }
+        VISO_HIP_CHECK(hipMemcpyAsync(c->h_dbl, c->direct_stats.ptr, 2 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        VISO_HIP_CHECK(hipStreamSynchronize(c->stream));
+        int pairs = 0, succ = 0;
+        for (int i = 0; i < m; ++i) {
+            pairs += pk[(size_t)i] >= 0;
+            succ += sc[(size_t)i];
+        }
+        out[6] = pairs;
+        out[7] = succ;
+        out[9] = c->h_dbl[0];
+        out[10] = c->h_dbl[1];
+    }
+    return VISO_OK;
+}
+
+int viso_pose_2d2d(viso_ctx* c, const double* p1, const double* p2, int32_t n, double R[9],
+                   double T[3], uint8_t* inliers, double* points3d, double* candidates,
+                   double stats[8]) {
+    if (!c || n < 0 || n > c->p.max_features || !R || !T || !stats) return VISO_ERR_ARG;
+    if (n > 0 && (!p1 || !p2)) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipSetDevice(c->device));
+    int rc = c->scratch_d.ensure(48 * (size_t)std::max(n, 1) + 512);
+    if (rc) return rc;
+    double* d_p1 = (double*)c->scratch_d.ptr;
+    double* d_p2 = d_p1 + 3 * (size_t)std::max(n, 1);
+    if (n > 0) {
+        VISO_HIP_CHECK(hipMemcpyAsync(d_p1, p1, 24 * (size_t)n, hipMemcpyHostToDevice, c->stream));
+        VISO_HIP_CHECK(hipMemcpyAsync(d_p2, p2, 24 * (size_t)n, hipMemcpyHostToDevice, c->stream));
+    }
+    c->h_int[2] = n;
+    VISO_HIP_CHECK(hipMemcpyAsync(c->n_track_dev.ptr, &c->h_int[2], sizeof(int), hipMemcpyHostToDevice, c->stream));
+    GeoArgs a = c->geo;
+    a.p1_in = d_p1;
+    a.p2_in = d_p2;
+    {
+        TimedRegion t(c->timing, VISO_KERNEL_RANSAC, c->stream);
+        launch_pose_2d2d(a, c->stream, &c->timing);
+    }
+    VISO_HIP_CHECK(hipGetLastError());
+    VISO_HIP_CHECK(hipMemcpyAsync(c->h_ctl, a.ctl, sizeof(GeoCtl), hipMemcpyDeviceToHost, c->stream));
+    VISO_HIP_CHECK(hipStreamSynchronize(c->stream));
+    const GeoCtl& g = *c->h_ctl;
+    for (int k = 0; k < 8; ++k) stats[k] = 0;
+    stats[3] = g.disparity;
+    if (!g.gate) {
+        // early return (src/viso.cpp:184, 216): R, T, inliers untouched; the
+        // disparity gate's value is still reported when it was computed
+        if (n < 10) stats[3] = 0;
+        return VISO_OK;
+    }
+    stats[0] = g.nr_inliers;
+    stats[1] = g.best_motion;
+    stats[2] = g.n_cand;
+    stats[4] = g.e_count;
+    stats[5] = g.h_count;
+    stats[6] = g.e_iters;
+    stats[7] = g.h_iters;
+    if (g.best_motion >= 0) {
+        std::memcpy(R, g.R, sizeof(g.R));
+        std::memcpy(T, g.T, sizeof(g.T));
+    }
+    if (candidates)
+        for (int m = 0; m < g.n_cand; ++m) std::memcpy(candidates + 12 * m, g.cand[m], 96);
+    if (n > 0 && (inliers || points3d)) {
+        std::vector<uint8_t> in((size_t)n);
+        VISO_HIP_CHECK(hipMemcpy(in.data(), a.inliers, (size_t)n, hipMemcpyDeviceToHost));
+        if (inliers) std::memcpy(inliers, in.data(), (size_t)n);
+        if (points3d) {
+            std::vector<double> comp(3 * (size_t)std::max(g.nr_inliers, 1));
+            if (g.nr_inliers > 0)
+                VISO_HIP_CHECK(hipMemcpy(comp.data(), a.points_out, 24 * (size_t)g.nr_inliers,
+                                         hipMemcpyDeviceToHost));
+            int k = 0;
+            for (int i = 0; i < n; ++i) {
+                for (int j = 0; j < 3; ++j) points3d[3 * i + j] = in[(size_t)i] ? comp[(size_t)3 * k + j] : 0.0;
+                k += in[(size_t)i] ? 1 : 0;
+            }
+        }
+    }
+    return VISO_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,719 @@
+// viso_amd — 2D-2D initialisation geometry for gfx950:
+// Viso::PoseEstimation2d2d (src/viso.cpp:178-256) with the repo's
+// deterministic RANSAC for E and H (stand-ins for cv::findEssentialMat /
+// cv::findHomography, see oracle_geom.cpp), cv::recoverPose and
+// cv::decomposeHomographyMat restated, then Viso::SelectMotion (:520-638).
+//
+// Parallel structure:
+//  * hypothesis kernels: one lane per RANSAC hypothesis (minimal solver);
+//  * scoring kernels: one workgroup per hypothesis, points strided over the
+//    256 lanes, inliers counted with __ballot/__popcll per wave;
+//  * scan kernel: one lane replays OpenCV's sequential loop
+//    (RANSACUpdateNumIters) over the per-hypothesis counts — identical to a
+//    sequential RANSAC whose i-th sample is hypothesis i;
+//  * select-motion: one lane per (candidate, point) triangulation + tests,
+//    one workgroup for the strict-max choice and the mean-depth tree.
+#include <cfloat>
+
+#include "device_math.hpp"
+#include "geometry.hpp"
+#include "linalg.hpp"
+
+namespace viso {
+
+namespace {
+
+__device__ inline uint64_t sample_hash(uint64_t seed, int h, int t, int k, int a) {
+    uint64_t z = seed + 0x632BE59BD9B4E019ULL * (uint64_t)(h + 1) +
+                 0x9E3779B97F4A7C15ULL * (uint64_t)(t + 1) +
+                 0xD1B54A32D192ED03ULL * (uint64_t)(k * 64 + a + 1);
+    return mix64(z);
+}
+
+template <int M>
+__device__ inline void draw_subset(uint64_t seed, int h, int t, int n, int* idx) {
+    for (int k = 0; k < M; ++k) {
+        int chosen = -1;
+        for (int a = 0; a < 64 && chosen < 0; ++a) {
+            const int c = (int)(sample_hash(seed, h, t, k, a) % (uint64_t)n);
+            bool dup = false;
+            for (int j = 0; j < k; ++j) dup |= (idx[j] == c);
+            if (!dup) chosen = c;
+        }
+        if (chosen < 0) {
+            for (int c = 0; c < n && chosen < 0; ++c) {
+                bool dup = false;
+                for (int j = 0; j < k; ++j) dup |= (idx[j] == c);
+                if (!dup) chosen = c;
+            }
+        }
+        idx[k] = chosen;
+    }
+}
+
+// ---------------------------------------------------------------- normalise
+// p = K_inv * (x, y, 1) (src/viso.cpp:45-48); q = float-rounded (cv::Point2f,
+// :204-205); disparity = canonical tree of |p2 - p1|^2 (:199-211).
+__global__ __launch_bounds__(256) void normalize_kernel(GeoArgs a) {
+    __shared__ double s_red[4];
+    const int n = *a.n_dev;
+    const double* Ki = a.Kinv;
+    for (int i = threadIdx.x; i < n; i += 256) {
+        double p1[3], p2[3];
+        if (a.p1_in) {
+            for (int r = 0; r < 3; ++r) {
+                p1[r] = a.p1_in[3 * i + r];
+                p2[r] = a.p2_in[3 * i + r];
+            }
+        } else {
+            const float2 k1 = a.kp1[i], k2 = a.kp2[i];
+            const double u1[3] = {(double)k1.x, (double)k1.y, 1};
+            const double u2[3] = {(double)k2.x, (double)k2.y, 1};
+            for (int r = 0; r < 3; ++r) {
+                p1[r] = Ki[3 * r] * u1[0] + Ki[3 * r + 1] * u1[1] + Ki[3 * r + 2] * u1[2];
+                p2[r] = Ki[3 * r] * u2[0] + Ki[3 * r + 1] * u2[1] + Ki[3 * r + 2] * u2[2];
+            }
+        }
+        for (int r = 0; r < 3; ++r) {
+            a.p1[3 * i + r] = p1[r];
+            a.p2[3 * i + r] = p2[r];
+        }
+        a.q1[2 * i] = (double)(float)p1[0];
+        a.q1[2 * i + 1] = (double)(float)p1[1];
+        a.q2[2 * i] = (double)(float)p2[0];
+        a.q2[2 * i + 1] = (double)(float)p2[1];
+    }
+    __syncthreads();
+    const double s = block_tree_sum(n, [&](int i) {
+        const double dx = a.p2[3 * i] - a.p1[3 * i];
+        const double dy = a.p2[3 * i + 1] - a.p1[3 * i + 1];
+        return dx * dx + dy * dy;
+    }, s_red);
+    if (threadIdx.x == 0) {
+        double d = s;
+        const double f = (a.K[0] + a.K[1]) / 2;
+        if (d != 0) {
+            d /= n;
+            d *= f * f;
+        }
+        GeoCtl* c = a.ctl;
+        c->n = n;
+        c->disparity = d;
+        c->gate = (n >= 10 && !(d < a.disparity_thresh)) ? 1 : 0;
+        c->n_cand = 0;
+        c->e_count = c->h_count = 0;
+        c->e_best = c->h_best = -1;
+        c->e_iters = c->h_iters = 0;
+        c->nr_inliers = 0;
+        c->best_motion = -1;
+    }
+}
+
+// ---------------------------------------------------------------- E RANSAC
+__device__ inline bool essential_from_8(const double* q1, const double* q2, const int* idx,
+                                        double* E) {
+    double A[72];
+    for (int r = 0; r < 8; ++r) {
+        const double x1 = q1[2 * idx[r]], y1 = q1[2 * idx[r] + 1];
+        const double x2 = q2[2 * idx[r]], y2 = q2[2 * idx[r] + 1];
+        double* row = A + 9 * r;
+        row[0] = x2 * x1;
+        row[1] = x2 * y1;
+        row[2] = x2;
+        row[3] = y2 * x1;
+        row[4] = y2 * y1;
+        row[5] = y2;
+        row[6] = x1;
+        row[7] = y1;
+        row[8] = 1.0;
+    }
+    double e[9];
+    if (!null_vector_8x9(A, e)) return false;
+    double U[9], s[3], V[9];
+    svd3(e, U, s, V);
+    if (!(s[1] > 0)) return false;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) E[3 * i + j] = U[3 * i + 0] * V[3 * j + 0] + U[3 * i + 1] * V[3 * j + 1];
+    return true;
+}
+
+__device__ inline float sampson_err(const double* E, double x1, double y1, double x2, double y2) {
+    const double ex0 = E[0] * x1 + E[1] * y1 + E[2];
+    const double ex1 = E[3] * x1 + E[4] * y1 + E[5];
+    const double ex2 = E[6] * x1 + E[7] * y1 + E[8];
+    const double et0 = E[0] * x2 + E[3] * y2 + E[6];
+    const double et1 = E[1] * x2 + E[4] * y2 + E[7];
+    const double x2tEx1 = x2 * ex0 + y2 * ex1 + ex2;
+    const double aa = ex0 * ex0, b = ex1 * ex1, c = et0 * et0, d = et1 * et1;
+    return (float)(x2tEx1 * x2tEx1 / (aa + b + c + d));
+}
+
+__global__ __launch_bounds__(64) void e_hyp_kernel(GeoArgs a) {
+    const int h = blockIdx.x * 64 + threadIdx.x;
+    if (h >= a.e_iters) return;
+    const GeoCtl* c = a.ctl;
+    if (!c->gate) return;
+    const int n = c->n;
+    double* E = a.e_models + 9 * (size_t)h;
+    int idx[8];
+    if (n == 8)
+        for (int k = 0; k < 8; ++k) idx[k] = k;
+    else
+        draw_subset<8>(a.seed, h, 0, n, idx);
+    a.e_valid[h] = essential_from_8(a.q1, a.q2, idx, E) ? 1 : 0;
+}
+
+// ---------------------------------------------------------------- H RANSAC
+__device__ inline bool subset_ok_h(const double* p1, const double* p2, const int* idx) {
+    const int tt[4][3] = {{0, 1, 2}, {1, 2, 3}, {0, 2, 3}, {0, 1, 3}};
+    const float eps = FLT_EPSILON;
+    for (int img = 0; img < 2; ++img) {
+        const double* p = img == 0 ? p1 : p2;
+        for (int q = 0; q < 4; ++q) {
+            const int* t = tt[q];
+            const double dx1 = p[2 * idx[t[1]]] - p[2 * idx[t[0]]], dy1 = p[2 * idx[t[1]] + 1] - p[2 * idx[t[0]] + 1];
+            const double dx2 = p[2 * idx[t[2]]] - p[2 * idx[t[0]]], dy2 = p[2 * idx[t[2]] + 1] - p[2 * idx[t[0]] + 1];
+            if (fabs(dx2 * dy1 - dy2 * dx1) <= eps * (fabs(dx1) + fabs(dy1) + fabs(dx2) + fabs(dy2)))
+                return false;
+        }
+    }
+    int negative = 0;
+    for (int q = 0; q < 4; ++q) {
+        const int* t = tt[q];
+        double A[9], B[9];
+        for (int r = 0; r < 3; ++r) {
+            A[3 * r] = p1[2 * idx[t[r]]];
+            A[3 * r + 1] = p1[2 * idx[t[r]] + 1];
+            A[3 * r + 2] = 1.0;
+            B[3 * r] = p2[2 * idx[t[r]]];
+            B[3 * r + 1] = p2[2 * idx[t[r]] + 1];
+            B[3 * r + 2] = 1.0;
+        }
+        negative += det3(A) * det3(B) < 0;
+    }
+    return negative == 0 || negative == 4;
+}
+
+__device__ inline void h_rows(double x1, double y1, double x2, double y2, double* ra, double* rb) {
+    ra[0] = x1;
+    ra[1] = y1;
+    ra[2] = 1.0;
+    ra[3] = 0.0;
+    ra[4] = 0.0;
+    ra[5] = 0.0;
+    ra[6] = -x2 * x1;
+    ra[7] = -x2 * y1;
+    ra[8] = -x2;
+    rb[0] = 0.0;
+    rb[1] = 0.0;
+    rb[2] = 0.0;
+    rb[3] = x1;
+    rb[4] = y1;
+    rb[5] = 1.0;
+    rb[6] = -y2 * x1;
+    rb[7] = -y2 * y1;
+    rb[8] = -y2;
+}
+
+__device__ inline float transfer_err(const double* H, double x1, double y1, double x2, double y2) {
+    const double w = H[6] * x1 + H[7] * y1 + H[8];
+    const double px = (H[0] * x1 + H[1] * y1 + H[2]) / w;
+    const double py = (H[3] * x1 + H[4] * y1 + H[5]) / w;
+    const double dx = px - x2, dy = py - y2;
+    return (float)(dx * dx + dy * dy);
+}
+
+__global__ __launch_bounds__(64) void h_hyp_kernel(GeoArgs a) {
+    const int h = blockIdx.x * 64 + threadIdx.x;
+    if (h >= a.h_iters) return;
+    const GeoCtl* c = a.ctl;
+    if (!c->gate) return;
+    const int n = c->n;
+    int idx[4];
+    bool ok = false;
+    for (int t = 0; t < 100 && !ok; ++t) {
+        if (n == 4)
+            for (int k = 0; k < 4; ++k) idx[k] = k;
+        else
+            draw_subset<4>(a.seed ^ 0x4848484848484848ULL, h, t, n, idx);
+        ok = subset_ok_h(a.q1, a.q2, idx);
+        if (n == 4) break;
+    }
+    if (!ok) {
+        a.h_valid[h] = 0;
+        return;
+    }
+    double A[72];
+    for (int r = 0; r < 4; ++r)
+        h_rows(a.q1[2 * idx[r]], a.q1[2 * idx[r] + 1], a.q2[2 * idx[r]], a.q2[2 * idx[r] + 1],
+               A + 18 * r, A + 18 * r + 9);
+    a.h_valid[h] = null_vector_8x9(A, a.h_models + 9 * (size_t)h) ? 1 : 0;
+}
+
+// ---------------------------------------------------------------- scoring
+template <bool IS_E>
+__global__ __launch_bounds__(256) void score_kernel(GeoArgs a) {
+    __shared__ int s_cnt;
+    const int h = blockIdx.x;
+    const GeoCtl* c = a.ctl;
+    int* counts = IS_E ? a.e_counts : a.h_counts;
+    const uint8_t* valid = IS_E ? a.e_valid : a.h_valid;
+    if (!c->gate) return;
+    if (!valid[h]) {
+        if (threadIdx.x == 0) counts[h] = -1;
+        return;
+    }
+    const double* M = (IS_E ? a.e_models : a.h_models) + 9 * (size_t)h;
+    double m[9];
+    for (int k = 0; k < 9; ++k) m[k] = M[k];
+    const float t2 = a.t2;
+    const int n = c->n;
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+    int cnt = 0;
+    for (int i0 = 0; i0 < n; i0 += 256) {
+        const int i = i0 + threadIdx.x;
+        bool in = false;
+        if (i < n) {
+            const double x1 = a.q1[2 * i], y1 = a.q1[2 * i + 1], x2 = a.q2[2 * i], y2 = a.q2[2 * i + 1];
+            in = (IS_E ? sampson_err(m, x1, y1, x2, y2) : transfer_err(m, x1, y1, x2, y2)) <= t2;
+        }
+        cnt += __popcll(__ballot(in));
+    }
+    if ((threadIdx.x & 63) == 0) atomicAdd(&s_cnt, cnt);
+    __syncthreads();
+    if (threadIdx.x == 0) counts[h] = s_cnt;
+}
+
+// cv::RANSACUpdateNumIters
+__device__ inline int update_num_iters(double p, double ep, int modelPoints, int maxIters) {
+    p = fmax(p, 0.);
+    p = fmin(p, 1.);
+    ep = fmax(ep, 0.);
+    ep = fmin(ep, 1.);
+    double num = fmax(1. - p, DBL_MIN);
+    double denom = 1. - pow(1. - ep, (double)modelPoints);
+    if (denom < DBL_MIN) return 0;
+    num = log(num);
+    denom = log(denom);
+    return denom >= 0 || -num >= maxIters * (-denom) ? maxIters : (int)rint(num / denom);
+}
+
+// OpenCV's sequential RANSAC loop over the precomputed counts (one lane),
+// then the winner's inlier mask (all lanes).
+template <bool IS_E>
+__global__ __launch_bounds__(256) void scan_kernel(GeoArgs a) {
+    __shared__ int s_best;
+    GeoCtl* c = a.ctl;
+    if (!c->gate) return;
+    const int n = c->n;
+    const int modelPoints = IS_E ? 8 : 4;
+    const int maxIters = IS_E ? a.e_iters : a.h_iters;
+    const int* counts = IS_E ? a.e_counts : a.h_counts;
+    if (threadIdx.x == 0) {
+        int niters = maxIters, maxGood = 0, best = -1, h = 0;
+        const bool enough = n >= modelPoints && (!IS_E || n >= 8);
+        if (enough) {
+            for (h = 0; h < niters; ++h) {
+                const int cc = counts[h];
+                if (cc < 0) continue;
+                if (cc > max(maxGood, modelPoints - 1)) {
+                    maxGood = cc;
+                    best = h;
+                    niters = update_num_iters(a.confidence, (double)(n - cc) / n, modelPoints, niters);
+                }
+            }
+        }
+        if (IS_E) {
+            c->e_count = best >= 0 ? maxGood : 0;
+            c->e_best = best;
+            c->e_iters = enough ? h : 0;
+        } else {
+            c->h_count = best >= 0 ? maxGood : 0;
+            c->h_best = best;
+            c->h_iters = enough ? h : 0;
+        }
+        s_best = best;
+    }
+    __syncthreads();
+    const int best = s_best;
+    if (best < 0) return;
+    const double* M = (IS_E ? a.e_models : a.h_models) + 9 * (size_t)best;
+    uint8_t* mask = IS_E ? a.e_mask : a.h_mask;
+    for (int i = threadIdx.x; i < n; i += 256) {
+        const double x1 = a.q1[2 * i], y1 = a.q1[2 * i + 1], x2 = a.q2[2 * i], y2 = a.q2[2 * i + 1];
+        mask[i] = (IS_E ? sampson_err(M, x1, y1, x2, y2) : transfer_err(M, x1, y1, x2, y2)) <= a.t2;
+    }
+}
+
+// ---------------------------------------------------------------- recoverPose
+__global__ __launch_bounds__(256) void recover_pose_kernel(GeoArgs a) {
+    __shared__ double s_R[2][9], s_t[3];
+    __shared__ int s_good[4][4];
+    GeoCtl* c = a.ctl;
+    if (!c->gate || c->e_best < 0) return;
+    const int n = c->n;
+    if (threadIdx.x == 0) {
+        const double* E = a.e_models + 9 * (size_t)c->e_best;
+        double U[9], s[3], V[9];
+        svd3(E, U, s, V);
+        if (det3(U) < 0)
+            for (int k = 0; k < 9; ++k) U[k] = -U[k];
+        double Vt[9];
+        transpose3(V, Vt);
+        if (det3(Vt) < 0)
+            for (int k = 0; k < 9; ++k) Vt[k] = -Vt[k];
+        const double W[9] = {0, 1, 0, -1, 0, 0, 0, 0, 1};
+        double Wt[9], UW[9];
+        transpose3(W, Wt);
+        matmul3(U, W, UW);
+        matmul3(UW, Vt, s_R[0]);
+        matmul3(U, Wt, UW);
+        matmul3(UW, Vt, s_R[1]);
+        s_t[0] = U[2] * 1.0;
+        s_t[1] = U[5] * 1.0;
+        s_t[2] = U[8] * 1.0;
+    }
+    __syncthreads();
+    const double sg[4] = {1, 1, -1, -1};
+    int good[4] = {0, 0, 0, 0};
+    for (int i = threadIdx.x; i < n; i += 256) {
+        const double x1 = a.q1[2 * i], y1 = a.q1[2 * i + 1], x2 = a.q2[2 * i], y2 = a.q2[2 * i + 1];
+        uint8_t m4 = 0;
+        for (int m = 0; m < 4; ++m) {
+            const double* R = s_R[m & 1];
+            const double tt[3] = {sg[m] * s_t[0], sg[m] * s_t[1], sg[m] * s_t[2]};
+            double X[4];
+            triangulate_h(R, tt, x1, y1, x2, y2, X);
+            bool ok = X[2] * X[3] > 0;
+            const double Q[3] = {X[0] / X[3], X[1] / X[3], X[2] / X[3]};
+            ok = (Q[2] < 50.0) && ok;
+            const double z2 = R[6] * Q[0] + R[7] * Q[1] + R[8] * Q[2] + tt[2] * 1.0;
+            ok = (z2 > 0) && ok;
+            ok = (z2 < 50.0) && ok;
+            ok = ok && a.e_mask[i];
+            good[m] += ok ? 1 : 0;
+        }
+        (void)m4;
+    }
+    for (int m = 0; m < 4; ++m) {
+        int g = wave_sum_int(good[m]);
+        if ((threadIdx.x & 63) == 0) s_good[m][threadIdx.x >> 6] = g;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int G[4];
+        for (int m = 0; m < 4; ++m) G[m] = (s_good[m][0] + s_good[m][1]) + (s_good[m][2] + s_good[m][3]);
+        int pick;
+        if (G[0] >= G[1] && G[0] >= G[2] && G[0] >= G[3])
+            pick = 0;
+        else if (G[1] >= G[0] && G[1] >= G[2] && G[1] >= G[3])
+            pick = 1;
+        else if (G[2] >= G[0] && G[2] >= G[1] && G[2] >= G[3])
+            pick = 2;
+        else
+            pick = 3;
+        double* cand = c->cand[c->n_cand];
+        for (int k = 0; k < 9; ++k) cand[k] = s_R[pick & 1][k];
+        for (int k = 0; k < 3; ++k) cand[9 + k] = pick >= 2 ? -s_t[k] : s_t[k];
+        c->n_cand += 1;
+    }
+}
+
+// ---------------------------------------------------------------- H refine + decompose
+__global__ __launch_bounds__(256) void h_refine_decompose_kernel(GeoArgs a) {
+    __shared__ double s_red[4];
+    __shared__ double s_M[81];
+    GeoCtl* c = a.ctl;
+    if (!c->gate || c->h_best < 0) return;
+    const int n = c->n;
+    const int good = c->h_count;
+    if (good >= 4) {
+        for (int r = 0; r < 9; ++r)
+            for (int col = r; col < 9; ++col) {
+                const double s = block_tree_sum(n, [&](int i) {
+                    double ra[9], rb[9];
+                    h_rows(a.q1[2 * i], a.q1[2 * i + 1], a.q2[2 * i], a.q2[2 * i + 1], ra, rb);
+                    return a.h_mask[i] ? ra[r] * ra[col] + rb[r] * rb[col] : 0.0;
+                }, s_red);
+                if (threadIdx.x == 0) {
+                    s_M[9 * r + col] = s;
+                    s_M[9 * col + r] = s;
+                }
+            }
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    double H[9];
+    const double* Hb = a.h_models + 9 * (size_t)c->h_best;
+    for (int k = 0; k < 9; ++k) H[k] = Hb[k];
+    if (good >= 4) {
+        double M[81], ev[9], V[81];
+        for (int k = 0; k < 81; ++k) M[k] = s_M[k];
+        jacobi_eigen<9>(M, ev, V);
+        for (int k = 0; k < 9; ++k) H[k] = V[9 * k + 8];
+    }
+    if (fabs(H[8]) > 1e-12) {
+        const double d = H[8];
+        for (int k = 0; k < 9; ++k) H[k] = H[k] / d;
+    }
+    for (int k = 0; k < 9; ++k) c->H[k] = H[k];
+    // cv::decomposeHomographyMat(H, I) — HomographyDecompInria
+    double U[9], s[3], V[9];
+    svd3(H, U, s, V);
+    double Hn[9];
+    const double inv = 1.0 / s[1];
+    for (int k = 0; k < 9; ++k) Hn[k] = H[k] * inv;
+    double Ht[9], S[9];
+    transpose3(Hn, Ht);
+    matmul3(Ht, Hn, S);
+    S[0] -= 1.0;
+    S[4] -= 1.0;
+    S[8] -= 1.0;
+    double mx = 0;
+    for (int k = 0; k < 9; ++k) mx = fmax(mx, fabs(S[k]));
+    if (mx < 0.001) {
+        double* cand = c->cand[c->n_cand];
+        for (int k = 0; k < 9; ++k) cand[k] = Hn[k];
+        cand[9] = cand[10] = cand[11] = 0;
+        c->n_cand += 1;
+        return;
+    }
+    auto minor = [&](int row, int col) {
+        const int x1 = col == 0 ? 1 : 0, x2 = col == 2 ? 1 : 2;
+        const int y1 = row == 0 ? 1 : 0, y2 = row == 2 ? 1 : 2;
+        return S[3 * y1 + x2] * S[3 * y2 + x1] - S[3 * y1 + x1] * S[3 * y2 + x2];
+    };
+    auto signd = [](double x) { return x >= 0 ? 1 : -1; };
+    const double M00 = minor(0, 0), M11 = minor(1, 1), M22 = minor(2, 2);
+    const double rtM00 = sqrt(M00), rtM11 = sqrt(M11), rtM22 = sqrt(M22);
+    const double M01 = minor(0, 1), M12 = minor(1, 2), M02 = minor(0, 2);
+    const int e12 = signd(M12), e02 = signd(M02), e01 = signd(M01);
+    const double nS00 = fabs(S[0]), nS11 = fabs(S[4]), nS22 = fabs(S[8]);
+    int indx = 0;
+    if (nS00 < nS11) {
+        indx = 1;
+        if (nS11 < nS22) indx = 2;
+    } else {
+        if (nS00 < nS22) indx = 2;
+    }
+    double npa[3], npb[3];
+    if (indx == 0) {
+        npa[0] = S[0], npb[0] = S[0];
+        npa[1] = S[1] + rtM22, npb[1] = S[1] - rtM22;
+        npa[2] = S[2] + e12 * rtM11, npb[2] = S[2] - e12 * rtM11;
+    } else if (indx == 1) {
+        npa[0] = S[1] + rtM22, npb[0] = S[1] - rtM22;
+        npa[1] = S[4], npb[1] = S[4];
+        npa[2] = S[5] - e02 * rtM00, npb[2] = S[5] + e02 * rtM00;
+    } else {
+        npa[0] = S[2] + e01 * rtM11, npb[0] = S[2] - e01 * rtM11;
+        npa[1] = S[5] + rtM00, npb[1] = S[5] - rtM00;
+        npa[2] = S[8], npb[2] = S[8];
+    }
+    const double traceS = S[0] + S[4] + S[8];
+    const double v = 2.0 * (double)sqrtf((float)(1 + traceS - M00 - M11 - M22));
+    const double ESii = signd(S[3 * indx + indx]);
+    const double r = sqrt(2 + traceS + v);
+    const double n_t = sqrt(2 + traceS - v);
+    const double na_n = sqrt((npa[0] * npa[0] + npa[1] * npa[1]) + npa[2] * npa[2]);
+    const double nb_n = sqrt((npb[0] * npb[0] + npb[1] * npb[1]) + npb[2] * npb[2]);
+    double na[3], nb[3];
+    for (int k = 0; k < 3; ++k) {
+        na[k] = npa[k] / na_n;
+        nb[k] = npb[k] / nb_n;
+    }
+    const double half_nt = 0.5 * n_t;
+    const double esii_t_r = ESii * r;
+    double ta_star[3], tb_star[3];
+    for (int k = 0; k < 3; ++k) {
+        ta_star[k] = half_nt * (esii_t_r * nb[k] - n_t * na[k]);
+        tb_star[k] = half_nt * (esii_t_r * na[k] - n_t * nb[k]);
+    }
+    auto rmat = [&](const double* tstar, const double* nn, double* R) {
+        double Mx[9];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) Mx[3 * i + j] = (i == j ? 1.0 : 0.0) - (2 / v) * tstar[i] * nn[j];
+        matmul3(Hn, Mx, R);
+        if (det3(R) < 0)
+            for (int k = 0; k < 9; ++k) R[k] = -R[k];
+    };
+    double Ra[9], Rb[9], ta[3], tb[3];
+    rmat(ta_star, na, Ra);
+    mat3_vec(Ra, ta_star, ta);
+    rmat(tb_star, nb, Rb);
+    mat3_vec(Rb, tb_star, tb);
+    const double* Rs[4] = {Ra, Ra, Rb, Rb};
+    const double* ts[4] = {ta, ta, tb, tb};
+    const double sg[4] = {1, -1, 1, -1};
+    for (int m = 0; m < 4; ++m) {
+        double* cand = c->cand[c->n_cand];
+        for (int k = 0; k < 9; ++k) cand[k] = Rs[m][k];
+        for (int k = 0; k < 3; ++k) cand[9 + k] = sg[m] > 0 ? ts[m][k] : -ts[m][k];
+        c->n_cand += 1;
+    }
+}
+
+// ---------------------------------------------------------------- SelectMotion
+__global__ __launch_bounds__(256) void select_points_kernel(GeoArgs a) {
+    const GeoCtl* c = a.ctl;
+    if (!c->gate) return;
+    const int n = c->n, m = c->n_cand;
+    const int gid = blockIdx.x * 256 + threadIdx.x;
+    const int mi = gid / a.cap, i = gid - mi * a.cap;
+    if (mi >= m || i >= n) return;
+    const double kPi = 3.14159265358979323846;
+    const double* R = c->cand[mi];
+    const double* T = c->cand[mi] + 9;
+    uint8_t* inl = a.sel_in + (size_t)mi * a.cap;
+    double* pts = a.sel_pts + (size_t)mi * a.cap * 3;
+    inl[i] = 0;
+    pts[3 * i] = pts[3 * i + 1] = pts[3 * i + 2] = 0.0;
+    double O2[3];
+    for (int r = 0; r < 3; ++r) O2[r] = (-R[3 * r]) * T[0] + (-R[3 * r + 1]) * T[1] + (-R[3 * r + 2]) * T[2];
+    const double x1 = a.p1[3 * i], y1 = a.p1[3 * i + 1], x2 = a.p2[3 * i], y2 = a.p2[3 * i + 1];
+    double X[4];
+    triangulate_h(R, T, x1, y1, x2, y2, X);
+    const double P1[3] = {X[0] / X[3], X[1] / X[3], X[2] / X[3]};
+    if (P1[2] < 0) return;
+    const double n2[3] = {P1[0] - O2[0], P1[1] - O2[1], P1[2] - O2[2]};
+    const double d1 = sqrt((P1[0] * P1[0] + P1[1] * P1[1]) + P1[2] * P1[2]);
+    const double d2 = sqrt((n2[0] * n2[0] + n2[1] * n2[1]) + n2[2] * n2[2]);
+    double parallax = (P1[0] * n2[0] + P1[1] * n2[1]) + P1[2] * n2[2];
+    parallax /= (d1 * d2);
+    parallax = acos(parallax) * 180 / kPi;
+    if (parallax > a.parallax_thresh) return;
+    double dx = (P1[0] / P1[2] - x1) * a.K[0];
+    double dy = (P1[1] / P1[2] - y1) * a.K[1];
+    if (sqrt(dx * dx + dy * dy) > a.proj_thresh) return;
+    double P2[3];
+    mat3_vec(R, P1, P2);
+    P2[0] = P2[0] + T[0];
+    P2[1] = P2[1] + T[1];
+    P2[2] = P2[2] + T[2];
+    if (P2[2] < 0) return;
+    dx = (P2[0] / P2[2] - x2) * a.K[0];
+    dy = (P2[1] / P2[2] - y2) * a.K[1];
+    if (sqrt(dx * dx + dy * dy) > a.proj_thresh) return;
+    inl[i] = 1;
+    pts[3 * i] = P1[0];
+    pts[3 * i + 1] = P1[1];
+    pts[3 * i + 2] = P1[2];
+}
+
+__global__ __launch_bounds__(256) void select_reduce_kernel(GeoArgs a) {
+    __shared__ double s_red[4];
+    __shared__ int s_cnt[4];
+    __shared__ int s_best, s_bestn;
+    GeoCtl* c = a.ctl;
+    if (!c->gate) return;
+    const int n = c->n, m = c->n_cand;
+    if (threadIdx.x == 0) {
+        s_best = -1;
+        s_bestn = 0;
+    }
+    __syncthreads();
+    for (int mi = 0; mi < m; ++mi) {
+        int cnt = 0;
+        for (int i = threadIdx.x; i < n; i += 256) cnt += a.sel_in[(size_t)mi * a.cap + i];
+        cnt = wave_sum_int(cnt);
+        if ((threadIdx.x & 63) == 0) s_cnt[threadIdx.x >> 6] = cnt;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const int tot = (s_cnt[0] + s_cnt[1]) + (s_cnt[2] + s_cnt[3]);
+            if (tot > s_bestn) {  // strict: the first maximum wins (src/viso.cpp:605)
+                s_bestn = tot;
+                s_best = mi;
+            }
+        }
+        __syncthreads();
+    }
+    const int best = s_best, nr = s_bestn;
+    double mean = 0.0;
+    if (best >= 0) {
+        const uint8_t* inl = a.sel_in + (size_t)best * a.cap;
+        const double* pts = a.sel_pts + (size_t)best * a.cap * 3;
+        mean = block_tree_sum(n, [&](int i) { return inl[i] ? pts[3 * i + 2] : 0.0; }, s_red);
+    }
+    if (threadIdx.x == 0) {
+        c->nr_inliers = nr;
+        c->best_motion = best;
+        if (best >= 0) {
+            for (int k = 0; k < 9; ++k) c->R[k] = c->cand[best][k];
+            for (int k = 0; k < 3; ++k) c->T[k] = c->cand[best][9 + k];
+        }
+        c->mean_depth = mean;
+        c->mean_nonzero = mean != 0 ? 1 : 0;
+        if (mean != 0) {
+            c->mean_depth = mean / nr;
+            for (int k = 0; k < 3; ++k) c->T[k] = c->T[k] / c->mean_depth;
+        }
+    }
+}
+
+// normalised inlier points in order (the reference's points3d after
+// SelectMotion's depth normalisation) -> map points; inlier flags -> mask
+__global__ __launch_bounds__(256) void select_output_kernel(GeoArgs a) {
+    __shared__ int s_wave[4];
+    __shared__ int s_base;
+    const GeoCtl* c = a.ctl;
+    if (!c->gate) return;
+    const int best = c->best_motion, n = c->n;
+    if (threadIdx.x == 0) s_base = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int i0 = 0; i0 < n; i0 += 256) {
+        const int i = i0 + threadIdx.x;
+        bool in = false;
+        if (i < n && best >= 0) in = a.sel_in[(size_t)best * a.cap + i] != 0;
+        if (i < n) a.inliers[i] = in ? 1 : 0;
+        const unsigned long long msk = __ballot(in);
+        const int before = __popcll(msk & ((1ULL << lane) - 1ULL));
+        if (lane == 0) s_wave[wave] = __popcll(msk);
+        __syncthreads();
+        int off = s_base;
+        for (int k = 0; k < wave; ++k) off += s_wave[k];
+        if (in) {
+            const double* P = a.sel_pts + ((size_t)best * a.cap + i) * 3;
+            const double md = c->mean_depth;
+            double* o = a.points_out + 3 * (size_t)(off + before);
+            if (c->mean_nonzero) {
+                o[0] = P[0] / md;
+                o[1] = P[1] / md;
+                o[2] = P[2] / md;
+            } else {
+                o[0] = P[0];
+                o[1] = P[1];
+                o[2] = P[2];
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) s_base += (s_wave[0] + s_wave[1]) + (s_wave[2] + s_wave[3]);
+        __syncthreads();
+    }
+}
+
+}  // namespace
+
+void launch_pose_2d2d(const GeoArgs& a, hipStream_t stream, Timing* timing) {
+    normalize_kernel<<<1, 256, 0, stream>>>(a);
+    if (a.e_iters > 0) {
+        e_hyp_kernel<<<(a.e_iters + 63) / 64, 64, 0, stream>>>(a);
+        score_kernel<true><<<a.e_iters, 256, 0, stream>>>(a);
+        scan_kernel<true><<<1, 256, 0, stream>>>(a);
+        recover_pose_kernel<<<1, 256, 0, stream>>>(a);
+    }
+    if (a.h_iters > 0) {
+        h_hyp_kernel<<<(a.h_iters + 63) / 64, 64, 0, stream>>>(a);
+        score_kernel<false><<<a.h_iters, 256, 0, stream>>>(a);
+        scan_kernel<false><<<1, 256, 0, stream>>>(a);
+        h_refine_decompose_kernel<<<1, 256, 0, stream>>>(a);
+    }
+    const int total = 5 * a.cap;
+    select_points_kernel<<<(total + 255) / 256, 256, 0, stream>>>(a);
+    select_reduce_kernel<<<1, 256, 0, stream>>>(a);
+    select_output_kernel<<<1, 256, 0, stream>>>(a);
+    (void)timing;
+}
+
+}  // namespace viso

@@ -1,0 +1,68 @@
+// viso_amd — device state and launcher of the 2D-2D initialisation geometry
+// (PoseEstimation2d2d + SelectMotion, src/viso.cpp:178-256, 520-638).
+#pragma once
+
+#include "common.hpp"
+
+namespace viso {
+
+struct Timing;
+
+constexpr int kMaxCandidates = 5;
+
+// Device-resident result block of one PoseEstimation2d2d call (read back by
+// the host once per initialisation frame).
+struct GeoCtl {
+    int n;
+    int gate;  // N >= 10 and disparity >= threshold (src/viso.cpp:184, 216)
+    double disparity;
+    int e_count, e_best, e_iters;
+    int h_count, h_best, h_iters;
+    int n_cand;
+    double cand[kMaxCandidates][12];
+    double H[9];
+    int nr_inliers, best_motion;
+    double R[9], T[3];
+    double mean_depth;
+    int mean_nonzero;
+    int pad;
+};
+
+struct GeoArgs {
+    const int* n_dev;  // tracked point count (device)
+    const float2* kp1;
+    const float2* kp2;
+    const double* p1_in;  // optional normalised inputs (n x 3) instead of kp1/kp2
+    const double* p2_in;
+    double Kinv[9];
+    double K[4];
+    double* p1;  // cap x 3
+    double* p2;
+    double* q1;  // cap x 2 (float-rounded)
+    double* q2;
+    GeoCtl* ctl;
+    double disparity_thresh;
+    double proj_thresh;
+    double parallax_thresh;
+    double confidence;
+    float t2;  // (float)(thresh^2), thresh = 0.3 / sqrt(fx^2 + fy^2)
+    uint64_t seed;
+    int e_iters, h_iters;
+    double* e_models;
+    uint8_t* e_valid;
+    int* e_counts;
+    uint8_t* e_mask;
+    double* h_models;
+    uint8_t* h_valid;
+    int* h_counts;
+    uint8_t* h_mask;
+    int cap;
+    uint8_t* sel_in;   // kMaxCandidates x cap
+    double* sel_pts;   // kMaxCandidates x cap x 3
+    uint8_t* inliers;  // cap (best motion's inlier flags)
+    double* points_out;  // cap x 3 (normalised inlier points, compacted)
+};
+
+void launch_pose_2d2d(const GeoArgs& a, hipStream_t stream, Timing* timing);
+
+}  // namespace viso

@@ -14,6 +14,8 @@
 // surviving corners in ascending x with a ballot/popcount prefix (row-major
 // order is then restored across rows by fast_compact, an exclusive prefix
 // over per-row counts).
+#include <vector>
+
 #include "kernels.hpp"
 
 namespace viso {
@@ -31,14 +33,17 @@ __device__ inline int reflect101(int p, int len) {
     return p;
 }
 
-__global__ __launch_bounds__(256) void pyr_down_kernel(const uint8_t* __restrict__ src_base,
-                                                       uint8_t* __restrict__ dst_base,
-                                                       size_t img_stride, int sw, int sh, int dw,
+struct PyrPtrs {
+    const uint8_t* src[kPyrBatch];
+    uint8_t* dst[kPyrBatch];
+};
+
+__global__ __launch_bounds__(256) void pyr_down_kernel(PyrPtrs ptrs, int sw, int sh, int dw,
                                                        int dh) {
     __shared__ uint8_t s_in[kPyrInH][kPyrInW + 1];
     __shared__ int s_h[kPyrInH][kPyrTileW + 1];
-    const uint8_t* src = src_base + (size_t)blockIdx.z * img_stride;
-    uint8_t* dst = dst_base + (size_t)blockIdx.z * img_stride;
+    const uint8_t* __restrict__ src = ptrs.src[blockIdx.z];
+    uint8_t* __restrict__ dst = ptrs.dst[blockIdx.z];
     const int ox0 = blockIdx.x * kPyrTileW;
     const int oy0 = blockIdx.y * kPyrTileH;
     const int tid = threadIdx.x;
@@ -234,14 +239,31 @@ __global__ __launch_bounds__(256) void fast_compact_kernel(const int* __restrict
 
 }  // namespace
 
+void launch_pyramid_frames(const PyrGeom& g, const uint8_t* const* l0, uint8_t* const* slot,
+                           int n, hipStream_t stream) {
+    for (int b0 = 0; b0 < n; b0 += kPyrBatch) {
+        const int nb = (n - b0) < kPyrBatch ? (n - b0) : kPyrBatch;
+        for (int l = 1; l < kLevels; ++l) {
+            PyrPtrs p;
+            for (int i = 0; i < nb; ++i) {
+                p.src[i] = l == 1 ? l0[b0 + i] : slot[b0 + i] + g.off[l - 1];
+                p.dst[i] = slot[b0 + i] + g.off[l];
+            }
+            dim3 grid((g.w[l] + kPyrTileW - 1) / kPyrTileW, (g.h[l] + kPyrTileH - 1) / kPyrTileH, nb);
+            pyr_down_kernel<<<grid, 256, 0, stream>>>(p, g.w[l - 1], g.h[l - 1], g.w[l], g.h[l]);
+        }
+    }
+}
+
 void launch_pyramid(const PyrGeom& g, uint8_t* base, int n_images, size_t img_stride,
                     hipStream_t stream) {
-    for (int l = 1; l < kLevels; ++l) {
-        dim3 grid((g.w[l] + kPyrTileW - 1) / kPyrTileW, (g.h[l] + kPyrTileH - 1) / kPyrTileH,
-                  n_images);
-        pyr_down_kernel<<<grid, 256, 0, stream>>>(base + g.off[l - 1], base + g.off[l], img_stride,
-                                                  g.w[l - 1], g.h[l - 1], g.w[l], g.h[l]);
+    std::vector<const uint8_t*> l0((size_t)n_images);
+    std::vector<uint8_t*> slot((size_t)n_images);
+    for (int i = 0; i < n_images; ++i) {
+        slot[(size_t)i] = base + img_stride * (size_t)i;
+        l0[(size_t)i] = slot[(size_t)i];
     }
+    launch_pyramid_frames(g, l0.data(), slot.data(), n_images, stream);
 }
 
 size_t fast_row_cap(int w) { return (size_t)(w / 2 + 2); }

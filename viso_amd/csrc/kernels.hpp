@@ -10,6 +10,11 @@ namespace viso {
 // base + i*img_stride (levels follow, PyrGeom offsets).
 void launch_pyramid(const PyrGeom& g, uint8_t* base, int n_images, size_t img_stride,
                     hipStream_t stream);
+// Batched pyramid over frames whose level 0 is at l0[i] and whose levels
+// 1..3 go to slot[i] + g.off[l] (n <= kPyrBatch per launch; more are split).
+constexpr int kPyrBatch = 64;
+void launch_pyramid_frames(const PyrGeom& g, const uint8_t* const* l0, uint8_t* const* slot,
+                           int n, hipStream_t stream);
 
 struct FastScratch {
     int* row_count = nullptr;   // [h]
@@ -20,5 +25,58 @@ size_t fast_row_cap(int w);
 // raw int4 {x, y, score, 0}) and the total count to *n_out (device).
 void launch_fast(const uint8_t* img, int w, int h, int thresh, FastScratch& s, float2* kp_out,
                  int4* raw_out, int cap, int* n_out, hipStream_t stream);
+
+// ---------------------------------------------------------------- tracking
+// OpticalFlowMultiLevel(inverse=true): kp2 in/out, success out (level 0).
+void launch_klt(const FrameDev& ref, const FrameDev& cur, const PyrGeom& g, const float2* kp1,
+                float2* kp2, uint8_t* success, int n, double thresh, hipStream_t stream);
+// Order-preserving erase of failed tracks (src/viso.cpp:23-40):
+// kp1/kp2[0..n) with success -> out arrays; *n_out = survivors.
+void launch_compact_tracks(const float2* kp1, const float2* kp2, const uint8_t* success, int n,
+                           float2* kp1_out, float2* kp2_out, int* n_out, hipStream_t stream);
+
+constexpr int kMaxKeyframes = 8;
+struct LkAlignArgs {
+    FrameDev kf[kMaxKeyframes];
+    const double* kf_poses;  // n_kf x 12 (device)
+    int n_kf;
+    FrameDev cur;
+    const double* cur_pose;  // 12 (device)
+    const double* points;    // n x 3
+    int n;
+    double K[4];
+    double thresh;
+    struct {
+        int w[4], h[4];
+        unsigned long long off[4];
+    } g;
+    int32_t* pair_kf;
+    uint8_t* success;
+    double* uv_before;
+    double* uv_after;
+};
+void launch_lk_align(const LkAlignArgs& a, hipStream_t stream);
+
+// ---------------------------------------------------------------- direct pose
+constexpr int kMaxMapPoints = 16384;
+struct DirectScratch {
+    double* tile_part = nullptr;  // [256 * 28]
+    int* tile_good = nullptr;     // [256]
+};
+// SE3 state on the device: 7 doubles (qx, qy, qz, qw, tx, ty, tz).
+// One DirectPoseEstimationSingleLayer call (faithful: one GN step).
+// stats (device, may be null): [nGood, cost, H(36), b(6), update(6)].
+void launch_direct_level(const FrameDev& last, const FrameDev& cur, const PyrGeom& g,
+                         const double K[4], const double* points, int n,
+                         const double* pose_last12, double* se3_state, int level,
+                         DirectScratch& s, double* stats, hipStream_t stream);
+// dst (12 doubles, device) <- src (host values, passed by value)
+void launch_set_pose(double* dst, const double src[12], hipStream_t stream);
+// se3_state <- SE3(R, t) of a 12-double pose (Sophus::SE3d(R, t)).
+void launch_se3_from_pose(const double* pose12, double* se3_state, hipStream_t stream);
+// pose12 <- rotationMatrix(), translation() of se3_state (optionally also
+// appended to a pose log at *log_count).
+void launch_se3_to_pose(const double* se3_state, double* pose12, double* log, int* log_count,
+                        hipStream_t stream);
 
 }  // namespace viso

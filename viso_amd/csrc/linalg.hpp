@@ -1,0 +1,259 @@
+// viso_amd — small dense linear algebra for the geometry kernels, one lane
+// each: one-sided Jacobi null vector (Triangulate's JacobiSVD,
+// src/viso.cpp:425), cyclic Jacobi symmetric eigen-decomposition, complete-
+// pivot Gauss-Jordan null vector of an 8x9 system, 3x3 SVD via A^T A.
+// Same algorithms and operation order as the oracle's.
+#pragma once
+
+#include "common.hpp"
+
+namespace viso {
+
+template <int N>
+__device__ inline void null_vector_jacobi(const double* Ain, double* v_out) {
+    double U[N * N], V[N * N];
+#pragma unroll
+    for (int i = 0; i < N * N; ++i) {
+        U[i] = Ain[i];
+        V[i] = (i % (N + 1) == 0) ? 1.0 : 0.0;
+    }
+    for (int sweep = 0; sweep < 40; ++sweep) {
+        bool rotated = false;
+#pragma unroll
+        for (int p = 0; p < N - 1; ++p)
+#pragma unroll
+            for (int q = p + 1; q < N; ++q) {
+                double alpha = 0, beta = 0, gamma = 0;
+#pragma unroll
+                for (int i = 0; i < N; ++i) {
+                    alpha = alpha + U[N * i + p] * U[N * i + p];
+                    beta = beta + U[N * i + q] * U[N * i + q];
+                    gamma = gamma + U[N * i + p] * U[N * i + q];
+                }
+                if (gamma == 0.0 || fabs(gamma) <= 1e-15 * sqrt(alpha * beta)) continue;
+                rotated = true;
+                const double zeta = (beta - alpha) / (2.0 * gamma);
+                const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+                const double c = 1.0 / sqrt(1.0 + t * t);
+                const double s = c * t;
+#pragma unroll
+                for (int i = 0; i < N; ++i) {
+                    const double up = U[N * i + p], uq = U[N * i + q];
+                    U[N * i + p] = c * up - s * uq;
+                    U[N * i + q] = s * up + c * uq;
+                    const double vp = V[N * i + p], vq = V[N * i + q];
+                    V[N * i + p] = c * vp - s * vq;
+                    V[N * i + q] = s * vp + c * vq;
+                }
+            }
+        if (!rotated) break;
+    }
+    int k = 0;
+    double best = 0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        double nn = 0;
+#pragma unroll
+        for (int i = 0; i < N; ++i) nn = nn + U[N * i + j] * U[N * i + j];
+        if (j == 0 || nn < best) {
+            best = nn;
+            k = j;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+        if (j == k)
+#pragma unroll
+            for (int i = 0; i < N; ++i) v_out[i] = V[N * i + j];
+}
+
+template <int N>
+__device__ inline void jacobi_eigen(const double* Ain, double* evals, double* evecs) {
+    double A[N * N], V[N * N];
+    for (int i = 0; i < N * N; ++i) {
+        A[i] = Ain[i];
+        V[i] = (i % (N + 1) == 0) ? 1.0 : 0.0;
+    }
+    for (int sweep = 0; sweep < 50; ++sweep) {
+        double off = 0, diag = 0;
+        for (int p = 0; p < N; ++p) {
+            diag = diag + A[N * p + p] * A[N * p + p];
+            for (int q = p + 1; q < N; ++q) off = off + A[N * p + q] * A[N * p + q];
+        }
+        if (off <= 1e-30 * diag || off == 0.0) break;
+        for (int p = 0; p < N - 1; ++p)
+            for (int q = p + 1; q < N; ++q) {
+                const double apq = A[N * p + q];
+                if (apq == 0.0) continue;
+                const double theta = (A[N * q + q] - A[N * p + p]) / (2.0 * apq);
+                const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                const double c = 1.0 / sqrt(t * t + 1.0);
+                const double s = t * c;
+                for (int k = 0; k < N; ++k) {
+                    const double akp = A[N * k + p], akq = A[N * k + q];
+                    A[N * k + p] = c * akp - s * akq;
+                    A[N * k + q] = s * akp + c * akq;
+                }
+                for (int k = 0; k < N; ++k) {
+                    const double apk = A[N * p + k], aqk = A[N * q + k];
+                    A[N * p + k] = c * apk - s * aqk;
+                    A[N * q + k] = s * apk + c * aqk;
+                }
+                for (int k = 0; k < N; ++k) {
+                    const double vkp = V[N * k + p], vkq = V[N * k + q];
+                    V[N * k + p] = c * vkp - s * vkq;
+                    V[N * k + q] = s * vkp + c * vkq;
+                }
+            }
+    }
+    int idx[N];
+    for (int i = 0; i < N; ++i) idx[i] = i;
+    for (int i = 0; i < N; ++i) {
+        int m = i;
+        for (int j = i + 1; j < N; ++j)
+            if (A[N * idx[j] + idx[j]] > A[N * idx[m] + idx[m]]) m = j;
+        const int tmp = idx[i];
+        idx[i] = idx[m];
+        idx[m] = tmp;
+    }
+    for (int j = 0; j < N; ++j) {
+        evals[j] = A[N * idx[j] + idx[j]];
+        for (int i = 0; i < N; ++i) evecs[N * i + j] = V[N * i + idx[j]];
+    }
+}
+
+__device__ inline bool null_vector_8x9(const double* Ain, double* e) {
+    double M[8 * 9];
+    for (int i = 0; i < 72; ++i) M[i] = Ain[i];
+    int cp[9];
+    for (int j = 0; j < 9; ++j) cp[j] = j;
+    for (int k = 0; k < 8; ++k) {
+        int pr = k, pc = k;
+        double best = -1.0;
+        for (int r = k; r < 8; ++r)
+            for (int c = k; c < 9; ++c) {
+                const double a = fabs(M[9 * r + c]);
+                if (a > best) {
+                    best = a;
+                    pr = r;
+                    pc = c;
+                }
+            }
+        if (!(best > 1e-300)) return false;
+        if (pr != k)
+            for (int j = 0; j < 9; ++j) {
+                const double tmp = M[9 * k + j];
+                M[9 * k + j] = M[9 * pr + j];
+                M[9 * pr + j] = tmp;
+            }
+        if (pc != k) {
+            for (int r = 0; r < 8; ++r) {
+                const double tmp = M[9 * r + k];
+                M[9 * r + k] = M[9 * r + pc];
+                M[9 * r + pc] = tmp;
+            }
+            const int tmp = cp[k];
+            cp[k] = cp[pc];
+            cp[pc] = tmp;
+        }
+        const double piv = M[9 * k + k];
+        for (int j = k + 1; j < 9; ++j) M[9 * k + j] = M[9 * k + j] / piv;
+        M[9 * k + k] = 1.0;
+        for (int r = 0; r < 8; ++r) {
+            if (r == k) continue;
+            const double f = M[9 * r + k];
+            if (f == 0.0) continue;
+            for (int j = k + 1; j < 9; ++j) M[9 * r + j] = M[9 * r + j] - f * M[9 * k + j];
+            M[9 * r + k] = 0.0;
+        }
+    }
+    double ep[9];
+    for (int k = 0; k < 8; ++k) ep[k] = -M[9 * k + 8];
+    ep[8] = 1.0;
+    for (int j = 0; j < 9; ++j) e[cp[j]] = ep[j];
+    return true;
+}
+
+__device__ inline double det3(const double* m) {
+    return m[0] * (m[4] * m[8] - m[5] * m[7]) - m[1] * (m[3] * m[8] - m[5] * m[6]) +
+           m[2] * (m[3] * m[7] - m[4] * m[6]);
+}
+
+__device__ inline void matmul3(const double* a, const double* b, double* o) {
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            o[3 * i + j] = (a[3 * i + 0] * b[0 + j] + a[3 * i + 1] * b[3 + j]) + a[3 * i + 2] * b[6 + j];
+}
+
+__device__ inline void transpose3(const double* a, double* o) {
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) o[3 * j + i] = a[3 * i + j];
+}
+
+__device__ inline void svd3(const double* A, double* U, double* s, double* V) {
+    double At[9], AtA[9], ev[3];
+    transpose3(A, At);
+    matmul3(At, A, AtA);
+    jacobi_eigen<3>(AtA, ev, V);
+    for (int i = 0; i < 3; ++i) s[i] = sqrt(ev[i] > 0 ? ev[i] : 0.0);
+    for (int j = 0; j < 2; ++j) {
+        const double v0 = V[j], v1 = V[3 + j], v2 = V[6 + j];
+        const double u0 = A[0] * v0 + A[1] * v1 + A[2] * v2;
+        const double u1 = A[3] * v0 + A[4] * v1 + A[5] * v2;
+        const double u2 = A[6] * v0 + A[7] * v1 + A[8] * v2;
+        const double inv = s[j] > 0 ? 1.0 / s[j] : 0.0;
+        U[j] = u0 * inv;
+        U[3 + j] = u1 * inv;
+        U[6 + j] = u2 * inv;
+    }
+    U[2] = U[3] * U[7] - U[6] * U[4];
+    U[5] = U[6] * U[1] - U[0] * U[7];
+    U[8] = U[0] * U[4] - U[3] * U[1];
+}
+
+// Viso::Triangulate with P1 = [I|0], P2 = [R|T]: homogeneous null vector.
+__device__ inline void triangulate_h(const double* R, const double* T, double x1, double y1,
+                                     double x2, double y2, double* X) {
+    const double P2[12] = {R[0], R[1], R[2], T[0], R[3], R[4], R[5], T[1], R[6], R[7], R[8], T[2]};
+    const double P1[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+    double A[16];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        A[j] = x1 * P1[8 + j] - P1[j];
+        A[4 + j] = y1 * P1[8 + j] - P1[4 + j];
+        A[8 + j] = x2 * P2[8 + j] - P2[j];
+        A[12 + j] = y2 * P2[8 + j] - P2[4 + j];
+    }
+    null_vector_jacobi<4>(A, X);
+}
+
+// Block-wide (256 threads) canonical pairwise tree over n leaves: leaf(i)
+// for i < n, +0.0 beyond.  Each thread reduces an aligned chunk of
+// C = max(1, P/256) leaves with the binary-counter form of the same tree,
+// then lanes and waves combine in index order.  Result valid in thread 0.
+template <class F>
+__device__ inline double block_tree_sum(int n, F leaf, double* s_red4) {
+    int P = 1;
+    while (P < n) P <<= 1;
+    const int C = P > 256 ? P / 256 : 1;
+    const int t = threadIdx.x;
+    double stack[16];
+    int sp = 0;
+    for (int j = 0; j < C; ++j) {
+        const int i = t * C + j;
+        double x = i < n ? leaf(i) : 0.0;
+        for (int k = j; k & 1; k >>= 1) x = stack[--sp] + x;
+        stack[sp++] = x;
+    }
+    double v = stack[0];
+    v = wave_tree_sum(v);
+    const int wave = t >> 6;
+    __syncthreads();
+    if ((t & 63) == 0) s_red4[wave] = v;
+    __syncthreads();
+    const double r = (s_red4[0] + s_red4[1]) + (s_red4[2] + s_red4[3]);
+    __syncthreads();
+    return r;
+}
+
+}  // namespace viso

@@ -1,0 +1,246 @@
+// viso_amd — per-point Lucas-Kanade engines for gfx950.
+//
+//  * klt_kernel: OpticalFlowMultiLevel(ref, cur, kp1, kp2, success,
+//    inverse=true) (src/viso.cpp:353-391) with OpticalFlowSingleLevel
+//    (:259-350) inside, all four levels in one launch.
+//  * lk_align_kernel: LKAlignment + LKAlignmentSingle (src/viso.cpp:768-925):
+//    best-viewing-angle keyframe selection, then four levels of <= 100
+//    inverse-compositional iterations per pair.
+//
+// Mapping: one wave64 per point, lane p = one pixel of the 8x8 patch
+// (p = (x+4)*8 + (y+4), the reference's x-outer / y-inner order).  Because
+// the Jacobian is taken on the reference image (inverse compositional), the
+// per-lane template value, gradient and the 2x2 Hessian are computed once per
+// level; each GN iteration is one bilinear sample of the current image plus
+// three canonical wave-tree sums (b0, b1, cost).  All lanes hold identical
+// sums, so the iteration control flow is wave-uniform.  Working set: two
+// pyramids (cache-resident); the bound is VALU/latency, not HBM.
+#include "device_math.hpp"
+#include "kernels.hpp"
+
+namespace viso {
+
+namespace {
+
+struct LkResult {
+    double dx, dy;
+    bool succ;
+};
+
+// One level of the inverse-compositional LK used by both engines.
+//   ref_x/ref_y: template coordinate of THIS lane's pixel (already offset);
+//   cur_x/cur_y: current-image coordinate of this lane's pixel without d;
+//   bound_x/bound_y: coordinate whose +d is bounds-checked (per engine).
+template <int MAXIT, bool KLT_BOUNDS>
+__device__ inline LkResult lk_level(const uint8_t* __restrict__ img1, int w1, int h1,
+                                    const uint8_t* __restrict__ img2, int w2, int h2,
+                                    double ref_x, double ref_y, double cur_x, double cur_y,
+                                    double bx, double by, double dx, double dy, double thresh) {
+    const double hp = 4.0;
+    double gx, gy;
+    gradient_px(img1, w1, h1, ref_x, ref_y, gx, gy);
+    const double J0 = -gx, J1 = -gy;
+    const double I1 = sample_px(img1, w1, h1, ref_x, ref_y);
+    const double H00 = wave_tree_sum(J0 * J0);
+    const double H01 = wave_tree_sum(J0 * J1);
+    const double H11 = wave_tree_sum(J1 * J1);
+    const double H10 = H01;  // J1*J0 == J0*J1 leaf by leaf
+    const double invdet = 1.0 / (H00 * H11 - H10 * H01);
+    const double i00 = H11 * invdet, i10 = -H10 * invdet, i01 = -H01 * invdet, i11 = H00 * invdet;
+    double cost = 0, lastCost = 0;
+    bool succ = true;
+    for (int iter = 0; iter < MAXIT; ++iter) {
+        bool out;
+        if (KLT_BOUNDS) {  // src/viso.cpp:286
+            out = bx + dx <= hp || bx + dx >= w1 - hp || by + dy <= hp || by + dy >= h1 - hp;
+        } else {  // src/viso.cpp:869-873 (ref coords + d, both corners)
+            out = !inside_px(bx + dx - hp, by + dy - hp, w1, h1) ||
+                  !inside_px(bx + dx + hp, by + dy + hp, w1, h1);
+        }
+        if (out) {
+            succ = false;
+            break;
+        }
+        const double e = I1 - sample_px(img2, w2, h2, cur_x + dx, cur_y + dy);
+        const double B0 = wave_tree_sum(-J0 * e);
+        const double B1 = wave_tree_sum(-J1 * e);
+        cost = wave_tree_sum(e * e);
+        const double u0 = i00 * B0 + i01 * B1;
+        const double u1 = i10 * B0 + i11 * B1;
+        if (isnan(u0)) {
+            succ = false;
+            break;
+        }
+        if (iter > 0 && cost > lastCost) break;
+        dx += u0;
+        dy += u1;
+        lastCost = cost;
+        succ = !(lastCost > thresh);
+    }
+    return {dx, dy, succ};
+}
+
+__global__ __launch_bounds__(256) void klt_kernel(FrameDev ref, FrameDev cur, PyrDev g,
+                                                  const float2* __restrict__ kp1,
+                                                  float2* __restrict__ kp2,
+                                                  uint8_t* __restrict__ success, int n,
+                                                  double thresh) {
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= n) return;  // wave-uniform
+    const int lane = threadIdx.x & 63;
+    const int px = (lane >> 3) - 4, py = (lane & 7) - 4;
+    const float2 k1 = kp1[i];
+    float2 k2 = kp2[i];
+    // kp2[j].pt *= scales[3]  (saturate_cast<float>(x * 0.125))
+    k2.x = (float)((double)k2.x * kScale[3]);
+    k2.y = (float)((double)k2.y * kScale[3]);
+    bool succ = true;
+    for (int level = kLevels - 1; level >= 0; --level) {
+        const float kx = (float)((double)k1.x * kScale[level]);
+        const float ky = (float)((double)k1.y * kScale[level]);
+        const double dx0 = (double)(k2.x - kx), dy0 = (double)(k2.y - ky);
+        const float fx = kx + (float)px, fy = ky + (float)py;  // float + int
+        const int w = g.w[level], h = g.h[level];
+        LkResult r = lk_level<10, true>(ref.l[level], w, h, cur.l[level], w, h,
+                                        (double)fx, (double)fy, (double)fx, (double)fy,
+                                        (double)kx, (double)ky, dx0, dy0, thresh);
+        succ = r.succ;
+        k2.x = kx + (float)r.dx;
+        k2.y = ky + (float)r.dy;
+        if (level != 0) {
+            k2.x = (float)((double)k2.x / 0.5);
+            k2.y = (float)((double)k2.y / 0.5);
+        }
+    }
+    if (lane == 0) {
+        kp2[i] = k2;
+        success[i] = succ ? 1 : 0;
+    }
+}
+
+__global__ __launch_bounds__(256) void lk_align_kernel(LkAlignArgs a) {
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= a.n) return;
+    const int lane = threadIdx.x & 63;
+    const int px = (lane >> 3) - 4, py = (lane & 7) - 4;
+    const double P[3] = {a.points[3 * i], a.points[3 * i + 1], a.points[3 * i + 2]};
+    const Intrinsics K{a.K[0], a.K[1], a.K[2], a.K[3]};
+    const int w0 = a.g.w[0], h0 = a.g.h[0];
+    int32_t kf = -1;
+    uint8_t succ_out = 0;
+    double ub[2] = {0.0, 0.0}, ua[2] = {0.0, 0.0};
+    double uc, vc;
+    project_px(a.cur_pose, K, P, 1.0, uc, vc);
+    if (inside_px(uc, vc, w0, h0)) {  // current_frame->IsInside(Pw, 0)
+        double best_angle = 180.0;
+        double bu = 0, bv = 0;
+        const double kPi = 3.14159265358979323846;
+        for (int j = 0; j < a.n_kf; ++j) {
+            const double* kp = a.kf_poses + 12 * j;
+            double ur, vr;
+            project_px(kp, K, P, 1.0, ur, vr);
+            if (!inside_px(ur, vr, w0, h0)) continue;
+            double Pc[3];
+            mat3_vec(kp, P, Pc);
+            Pc[0] = Pc[0] + kp[9];
+            Pc[1] = Pc[1] + kp[10];
+            Pc[2] = Pc[2] + kp[11];
+            const double nrm = (Pc[0] * Pc[0] + Pc[1] * Pc[1]) + Pc[2] * Pc[2];
+            if (nrm > 0) {
+                const double s = sqrt(nrm);
+                Pc[0] = Pc[0] / s;
+                Pc[1] = Pc[1] / s;
+                Pc[2] = Pc[2] / s;
+            }
+            const double angle = fabs(acos(Pc[2]) / kPi * 180);
+            if (angle > 180.0 || angle > best_angle) continue;
+            best_angle = angle;
+            kf = j;
+            bu = ur;
+            bv = vr;
+        }
+        if (kf >= 0) {
+            ub[0] = uc;
+            ub[1] = vc;
+            double cu = uc, cv = vc;
+            const FrameDev refp = a.kf[kf];
+            bool succ = false;
+            for (int level = kLevels - 1; level >= 0; --level) {
+                const double s = kScale[level];
+                const int w = a.g.w[level], h = a.g.h[level];
+                const double rx = bu * s + px, ry = bv * s + py;
+                const double cx = cu * s + px, cy = cv * s + py;
+                LkResult r = lk_level<100, false>(refp.l[level], w, h, a.cur.l[level], w, h, rx,
+                                                  ry, cx,
+                                                  cy, bu * s, bv * s, 0.0, 0.0, a.thresh);
+                succ = r.succ;
+                cu = cu + r.dx / s;  // pair.uv_cur += V2d{dx/s, dy/s}
+                cv = cv + r.dy / s;
+            }
+            succ_out = succ ? 1 : 0;
+            ua[0] = cu;
+            ua[1] = cv;
+        }
+    }
+    if (lane == 0) {
+        a.pair_kf[i] = kf;
+        a.success[i] = succ_out;
+        a.uv_before[2 * i] = ub[0];
+        a.uv_before[2 * i + 1] = ub[1];
+        a.uv_after[2 * i] = ua[0];
+        a.uv_after[2 * i + 1] = ua[1];
+    }
+}
+
+// One workgroup: ballot/popcount prefix in chunks of 256 keeps the order.
+__global__ __launch_bounds__(256) void compact_tracks_kernel(const float2* __restrict__ kp1,
+                                                             const float2* __restrict__ kp2,
+                                                             const uint8_t* __restrict__ success,
+                                                             int n, float2* __restrict__ o1,
+                                                             float2* __restrict__ o2,
+                                                             int* __restrict__ n_out) {
+    __shared__ int s_wave[4];
+    __shared__ int s_base;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (threadIdx.x == 0) s_base = 0;
+    __syncthreads();
+    for (int i0 = 0; i0 < n; i0 += 256) {
+        const int i = i0 + threadIdx.x;
+        const bool keep = i < n && success[i] != 0;
+        const unsigned long long m = __ballot(keep);
+        const int before = __popcll(m & ((1ULL << lane) - 1ULL));
+        if (lane == 0) s_wave[wave] = __popcll(m);
+        __syncthreads();
+        int off = s_base;
+        for (int k = 0; k < wave; ++k) off += s_wave[k];
+        if (keep) {
+            o1[off + before] = kp1[i];
+            o2[off + before] = kp2[i];
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) s_base += (s_wave[0] + s_wave[1]) + (s_wave[2] + s_wave[3]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *n_out = s_base;
+}
+
+}  // namespace
+
+void launch_compact_tracks(const float2* kp1, const float2* kp2, const uint8_t* success, int n,
+                           float2* kp1_out, float2* kp2_out, int* n_out, hipStream_t stream) {
+    compact_tracks_kernel<<<1, 256, 0, stream>>>(kp1, kp2, success, n, kp1_out, kp2_out, n_out);
+}
+
+void launch_klt(const FrameDev& ref, const FrameDev& cur, const PyrGeom& g, const float2* kp1,
+                float2* kp2, uint8_t* success, int n, double thresh, hipStream_t stream) {
+    if (n <= 0) return;
+    klt_kernel<<<(n + 3) / 4, 256, 0, stream>>>(ref, cur, make_pyrdev(g), kp1, kp2, success, n,
+                                                 thresh);
+}
+
+void launch_lk_align(const LkAlignArgs& a, hipStream_t stream) {
+    if (a.n <= 0) return;
+    lk_align_kernel<<<(a.n + 3) / 4, 256, 0, stream>>>(a);
+}
+
+}  // namespace viso

@@ -1,0 +1,163 @@
+"""Host mirror of the reference's classes over the C ABI.
+
+* ``Viso(fx, fy, cx, cy, ...)`` — include/viso.h:11-125: ``OnNewFrame``,
+  ``poses``, ``GetPoints()``; plus the north-star ``process(left, right)``.
+* ``Keyframe(image)`` — include/keyframe.h:28-46 (pyramid built on device by
+  ``OnNewFrame``; ``Pyramids()`` computes it on demand for inspection).
+* ``FrameSequence(location, handler)`` — include/frame_sequence.h:11-43:
+  ``RunOnce()`` loads ``<location><next_id+1>.png`` and calls
+  ``handler.OnNewFrame``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from . import _lib
+from .api import Context, default_params
+
+
+class Keyframe:
+    """A grey frame handed to ``FrameHandler.OnNewFrame``."""
+
+    next_id_ = 0  # Keyframe::next_id_ (src/keyframe.cpp:7)
+
+    def __init__(self, mat: np.ndarray):
+        mat = np.ascontiguousarray(mat, dtype=np.uint8)
+        if mat.ndim != 2:
+            raise ValueError("Keyframe expects a single-channel (grey) image")
+        self.mat_ = mat
+        self.id_ = Keyframe.next_id_
+        Keyframe.next_id_ += 1
+
+    @classmethod
+    def GetNextId(cls) -> int:
+        return cls.next_id_
+
+    def GetId(self) -> int:
+        return self.id_
+
+    def Mat(self) -> np.ndarray:
+        return self.mat_
+
+
+class FrameHandler:
+    """FrameSequence::FrameHandler (include/frame_sequence.h:13-16)."""
+
+    def OnNewFrame(self, keyframe: Keyframe) -> None:  # pragma: no cover - interface
+        raise NotImplementedError
+
+
+class Viso(FrameHandler):
+    """Viso (include/viso.h:11): one device context per sequence."""
+
+    def __init__(self, fx: float, fy: float, cx: float, cy: float, width: int = 640,
+                 height: int = 480, device: int = 0, **params):
+        self.params = default_params(fx=fx, fy=fy, cx=cx, cy=cy, width=width, height=height,
+                                     **params)
+        self.ctx = Context(self.params, device=device)
+        self.width, self.height = width, height
+
+    # ----------------------------------------------------------- reference API
+    def OnNewFrame(self, cur_frame) -> None:
+        img = cur_frame.Mat() if isinstance(cur_frame, Keyframe) else cur_frame
+        img = np.ascontiguousarray(img, dtype=np.uint8)
+        h, w = img.shape
+        _lib.call("viso_process_frame", self.ctx.h, img.ctypes.data, w, h, w)
+
+    @property
+    def poses(self) -> np.ndarray:
+        """Viso::poses (include/viso.h:54): (n, 3, 4) Tcw."""
+        n = ctypes.c_size_t(0)
+        _lib.call("viso_get_poses", self.ctx.h, None, 0, ctypes.byref(n))
+        out = np.zeros((n.value, 12), np.float64)
+        if n.value:
+            _lib.call("viso_get_poses", self.ctx.h, out.ctypes.data, n.value, ctypes.byref(n))
+        return out
+
+    def GetPoints(self) -> np.ndarray:
+        """Viso::GetPoints (include/viso.h:60-67): (n, 3)."""
+        n = ctypes.c_size_t(0)
+        _lib.call("viso_get_points", self.ctx.h, None, 0, ctypes.byref(n))
+        out = np.zeros((n.value, 3), np.float64)
+        if n.value:
+            _lib.call("viso_get_points", self.ctx.h, out.ctypes.data, n.value, ctypes.byref(n))
+        return out
+
+    # ----------------------------------------------------------- north-star API
+    def process(self, left: np.ndarray, right: np.ndarray) -> None:
+        """VisualOdometryStereo::process(left, right) facade."""
+        left = np.ascontiguousarray(left, dtype=np.uint8)
+        right = np.ascontiguousarray(right, dtype=np.uint8)
+        h, w = left.shape
+        dims = (ctypes.c_int32 * 3)(w, h, w)
+        _lib.call("viso_process_stereo", self.ctx.h, left.ctypes.data, right.ctypes.data, dims)
+
+    def process_device(self, d_left: int, d_right: int | None, n: int, frame_stride: int):
+        """Batched ingest of n frames resident in HBM (device pointers)."""
+        _lib.call("viso_process_frames_device", self.ctx.h, d_left, d_right, n, frame_stride)
+
+    # ----------------------------------------------------------- inspection
+    @property
+    def state(self) -> int:
+        s = ctypes.c_int32(0)
+        _lib.call("viso_get_state", self.ctx.h, ctypes.byref(s))
+        return s.value
+
+    def stats(self) -> np.ndarray:
+        out = np.zeros(16)
+        _lib.call("viso_get_frame_stats", self.ctx.h, out.ctypes.data)
+        return out
+
+    def tracks(self):
+        """init_.kp1, init_.kp2 (float32 (n,2)) and init_.success."""
+        n = ctypes.c_size_t(0)
+        _lib.call("viso_get_init_tracks", self.ctx.h, None, None, None, 0, ctypes.byref(n))
+        m = n.value
+        k1 = np.zeros((m, 2), np.float32)
+        k2 = np.zeros((m, 2), np.float32)
+        s = np.zeros(m, np.uint8)
+        if m:
+            _lib.call("viso_get_init_tracks", self.ctx.h, k1.ctypes.data, k2.ctypes.data,
+                      s.ctypes.data, m, ctypes.byref(n))
+        return k1, k2, s
+
+    def alignment(self):
+        """Last LKAlignment (dense per map point)."""
+        n = ctypes.c_size_t(0)
+        _lib.call("viso_get_alignment", self.ctx.h, None, None, None, None, 0, ctypes.byref(n))
+        m = n.value
+        pk = np.zeros(m, np.int32)
+        sc = np.zeros(m, np.uint8)
+        ub = np.zeros((m, 2))
+        ua = np.zeros((m, 2))
+        if m:
+            _lib.call("viso_get_alignment", self.ctx.h, pk.ctypes.data, sc.ctypes.data,
+                      ub.ctypes.data, ua.ctypes.data, m, ctypes.byref(n))
+        return pk, sc, ub, ua
+
+    def synchronize(self):
+        self.ctx.synchronize()
+
+    def close(self):
+        self.ctx.close()
+
+
+class FrameSequence:
+    """FrameSequence (include/frame_sequence.h:11-43): reads
+    ``<location><Keyframe.GetNextId()+1>.png`` (grey) per RunOnce()."""
+
+    def __init__(self, location: str, handler: FrameHandler):
+        self.location_ = location
+        self.handler_ = handler
+
+    def RunOnce(self) -> bool:
+        path = os.path.join(self.location_, f"{Keyframe.GetNextId() + 1}.png")
+        if not os.path.exists(path):
+            return False  # the reference silently skips a missing file
+        from PIL import Image
+        img = np.asarray(Image.open(path).convert("L"), dtype=np.uint8)
+        self.handler_.OnNewFrame(Keyframe(img))
+        return True
