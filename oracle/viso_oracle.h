@@ -116,6 +116,13 @@ int oracle_select_motion(const double* p1, const double* p2, int n, const double
                          double parallax_thresh, int32_t* best_out, double R_out[9],
                          double T_out[3], uint8_t* inliers, double* points3d);
 
+// North-star stereo SAD stage (no reference counterpart; the repo's own spec,
+// viso_amd/csrc/stereo.hip): 8x8 SAD along the row, d = 0..max_disp while
+// x - d - 4 >= 0, smallest SAD wins, ties -> smallest d; -1 when the left
+// patch leaves the image.
+void oracle_stereo_match(const uint8_t* L, const uint8_t* R, int w, int h, const int32_t* xs,
+                         const int32_t* ys, int n, int max_disp, int32_t* disp, int32_t* best_sad);
+
 // ---------------------------------------------------------------- full path
 struct oracle_params;
 // Viso::PoseEstimation2d2d (src/viso.cpp:178-256) + SelectMotion on n x 3

@@ -54,6 +54,7 @@ SIG = {
     "oracle_viso_tracks": ([_vp, _vp, _vp, _vp, _i], _i),
     "oracle_viso_alignment": ([_vp, _vp, _vp, _vp, _vp, _i], _i),
     "oracle_viso_keyframe_poses": ([_vp, _vp, _i], _i),
+    "oracle_stereo_match": ([_vp, _vp, _i, _i, _vp, _vp, _i, _i, _vp, _vp], None),
 }
 
 _lib = None
@@ -163,6 +164,21 @@ def pose_2d2d(p1, p2, K, w=1242, h=375, R0=None, T0=None, **kw):
                                ptr(inl), ptr(pts), ptr(cand), ptr(st))
     return {"ran": ran, "R": R.reshape(3, 3), "T": T, "inliers": inl[:n], "points3d": pts[:n],
             "candidates": cand[:int(st[2])], "stats": st}
+
+
+def stereo_match(left, right, xs, ys, max_disp):
+    lib = load()
+    left = np.ascontiguousarray(left, np.uint8)
+    right = np.ascontiguousarray(right, np.uint8)
+    h, w = left.shape
+    xs = np.ascontiguousarray(xs, np.int32)
+    ys = np.ascontiguousarray(ys, np.int32)
+    n = len(xs)
+    d = np.zeros(n, np.int32)
+    s = np.zeros(n, np.int32)
+    lib.oracle_stereo_match(ptr(left), ptr(right), w, h, ptr(xs), ptr(ys), n, max_disp, ptr(d),
+                            ptr(s))
+    return d, s
 
 
 def triangulate(R, T, x1, x2):

@@ -150,6 +150,20 @@ class Context:
         return {"R": R.reshape(3, 3), "T": T, "inliers": inl[:n], "points3d": pts[:n],
                 "candidates": cand[:int(st[2])], "stats": st}
 
+    def stereo_match(self, left, right, xs, ys, max_disp: int = 128):
+        """North-star stereo SAD stage: (disparity, sad) per left keypoint."""
+        left = np.ascontiguousarray(left, dtype=np.uint8)
+        right = np.ascontiguousarray(right, dtype=np.uint8)
+        h, w = left.shape
+        xs = np.ascontiguousarray(xs, dtype=np.int32)
+        ys = np.ascontiguousarray(ys, dtype=np.int32)
+        n = len(xs)
+        d = np.zeros(n, np.int32)
+        s = np.zeros(n, np.int32)
+        _lib.call("viso_stereo_match", self.h, _p(left), _p(right), w, h, _p(xs), _p(ys), n,
+                  max_disp, _p(d), _p(s))
+        return d, s
+
     # ------------------------------------------------------------ timing
     def timing_enable(self, on: bool = True):
         _lib.call("viso_timing_enable", self.h, 1 if on else 0)

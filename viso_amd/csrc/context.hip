@@ -345,3 +345,36 @@ int viso_lk_align(viso_ctx* c, const uint8_t* kf_pyrs, const double* kf_poses, i
 }
 
 }  // extern "C"
+
+extern "C" int viso_stereo_match(viso_ctx* c, const uint8_t* left, const uint8_t* right,
+                                 int32_t width, int32_t height, const int32_t* xs,
+                                 const int32_t* ys, int32_t n, int32_t max_disp,
+                                 int32_t* disparity, int32_t* sad) {
+    if (!c || !left || !right || width < 8 || height < 8 || n < 0 || max_disp < 0)
+        return VISO_ERR_ARG;
+    if (n == 0) return VISO_OK;
+    if (!xs || !ys || !disparity || !sad) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipSetDevice(c->device));
+    const size_t npx = (size_t)width * height;
+    Bump b;
+    const size_t o_l = b.take(npx), o_r = b.take(npx), o_x = b.take(4 * (size_t)n),
+                 o_y = b.take(4 * (size_t)n), o_d = b.take(4 * (size_t)n), o_s = b.take(4 * (size_t)n);
+    int rc = c->scratch_a.ensure(b.off);
+    if (rc) return rc;
+    char* base = (char*)c->scratch_a.ptr;
+    VISO_HIP_CHECK(hipMemcpyAsync(base + o_l, left, npx, hipMemcpyHostToDevice, c->stream));
+    VISO_HIP_CHECK(hipMemcpyAsync(base + o_r, right, npx, hipMemcpyHostToDevice, c->stream));
+    VISO_HIP_CHECK(hipMemcpyAsync(base + o_x, xs, 4 * (size_t)n, hipMemcpyHostToDevice, c->stream));
+    VISO_HIP_CHECK(hipMemcpyAsync(base + o_y, ys, 4 * (size_t)n, hipMemcpyHostToDevice, c->stream));
+    {
+        TimedRegion t(c->timing, VISO_KERNEL_STEREO, c->stream);
+        launch_stereo_sad((const uint8_t*)(base + o_l), (const uint8_t*)(base + o_r), width, height,
+                          (const int*)(base + o_x), (const int*)(base + o_y), n, max_disp,
+                          (int*)(base + o_d), (int*)(base + o_s), c->stream);
+    }
+    VISO_HIP_CHECK(hipGetLastError());
+    VISO_HIP_CHECK(hipMemcpyAsync(disparity, base + o_d, 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    VISO_HIP_CHECK(hipMemcpyAsync(sad, base + o_s, 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    VISO_HIP_CHECK(hipStreamSynchronize(c->stream));
+    return VISO_OK;
+}

@@ -57,6 +57,11 @@ struct LkAlignArgs {
 };
 void launch_lk_align(const LkAlignArgs& a, hipStream_t stream);
 
+// ---------------------------------------------------------------- stereo (north star)
+void launch_stereo_sad(const uint8_t* left, const uint8_t* right, int w, int h, const int* xs,
+                       const int* ys, int n, int max_disp, int* disp, int* sad,
+                       hipStream_t stream);
+
 // ---------------------------------------------------------------- direct pose
 constexpr int kMaxMapPoints = 16384;
 struct DirectScratch {
