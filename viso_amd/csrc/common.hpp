@@ -100,6 +100,38 @@ __device__ inline double wave_tree_sum(double v) {
     return v;
 }
 
+// DPP move of both halves of a double (all 64 lanes must be active).
+template <int CTRL>
+__device__ inline double dpp_f64(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffLL), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+__device__ inline double readlane_f64(double v, int lane) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), lane);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// The same canonical tree as wave_tree_sum, built from DPP row operations:
+// xor-1 and xor-2 by quad_perm; then, because every lane of an aligned 4-
+// (8-) group already holds the same partial, row_half_mirror (row_mirror)
+// pairs each group with its sibling exactly like xor-4 (xor-8); the last two
+// levels read the four row sums with v_readlane: (r0 + r1) + (r2 + r3).
+// Result is wave-uniform.  Requires EXEC = all 64 lanes.
+__device__ inline double wave_tree_sum_dpp(double v) {
+    v = v + dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]  (xor 1)
+    v = v + dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]  (xor 2)
+    v = v + dpp_f64<0x141>(v);  // row_half_mirror      (xor 4 on uniform quads)
+    v = v + dpp_f64<0x140>(v);  // row_mirror           (xor 8 on uniform octets)
+    const double r0 = readlane_f64(v, 0), r1 = readlane_f64(v, 16);
+    const double r2 = readlane_f64(v, 32), r3 = readlane_f64(v, 48);
+    return (r0 + r1) + (r2 + r3);
+}
+
 __device__ inline int wave_sum_int(int v) {
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);

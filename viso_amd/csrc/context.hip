@@ -253,8 +253,8 @@ int viso_direct_pose(viso_ctx* c, const uint8_t* last_pyr, const uint8_t* cur_py
     PyrGeom g = make_geom(width, height);
     Bump b;
     size_t o_l = b.take(g.bytes), o_c = b.take(g.bytes), o_p = b.take(24 * (size_t)std::max(n, 1)),
-           o_pl = b.take(96), o_pio = b.take(96), o_se3 = b.take(56), o_tp = b.take(256 * 28 * 8),
-           o_tg = b.take(256 * 4);
+           o_pl = b.take(96), o_pio = b.take(96), o_se3 = b.take(56),
+           o_tp = b.take(direct_scratch_bytes()), o_tg = b.take(4 * 4096);
     int rc = c->scratch_a.ensure(b.off);
     if (rc) return rc;
     char* base = (char*)c->scratch_a.ptr;

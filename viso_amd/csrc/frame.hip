@@ -137,7 +137,7 @@ int viso_ctx::init() {
     if (!rc) rc = map_pts.ensure(24 * (size_t)kMaxMapPoints);
     if (!rc) rc = kf_poses.ensure(96 * (size_t)kMaxKeyframes);
     if (!rc) rc = se3.ensure(64);
-    if (!rc) rc = direct_tiles.ensure(256 * 28 * 8 + 256 * 4);
+    if (!rc) rc = direct_tiles.ensure(direct_scratch_bytes());
     if (!rc) rc = direct_stats.ensure(4 * 50 * 8);
     if (!rc) rc = lk_pair.ensure(4 * (size_t)kMaxMapPoints);
     if (!rc) rc = lk_succ.ensure((size_t)kMaxMapPoints);
@@ -147,7 +147,7 @@ int viso_ctx::init() {
     if (!rc) rc = pose_count.ensure(256);
     if (rc) return rc;
     direct.tile_part = (double*)direct_tiles.ptr;
-    direct.tile_good = (int*)((char*)direct_tiles.ptr + 256 * 28 * 8);
+    direct.tile_good = (int*)((char*)direct_tiles.ptr + 28 * 4096 * 8);
     VISO_HIP_CHECK(hipMemsetAsync(pose_count.ptr, 0, 256, stream));
     VISO_HIP_CHECK(hipMemsetAsync(n_track_dev.ptr, 0, 256, stream));
     VISO_HIP_CHECK(hipStreamSynchronize(stream));
@@ -233,7 +233,8 @@ int viso_ctx::on_new_frame(int cur) {
     const PyrGeom& g = geom;
     hold(cur);  // the "cur_frame" shared_ptr
     for (int k = 0; k < 16; ++k) stats[k] = 0;
-    launch_set_pose(pose_of(cur), kIdentityPose, stream);  // Keyframe ctor: R = I, T = 0
+    // Keyframe ctor: R = I, T = 0 (a tracking frame overwrites it below)
+    if (state != VISO_STATE_RUNNING) launch_set_pose(pose_of(cur), kIdentityPose, stream);
     const double K[4] = {p.fx, p.fy, p.cx, p.cy};
     bool counted = true;  // ++init_.frame_cnt at the end of kInitialization
     switch (state) {
@@ -329,19 +330,20 @@ int viso_ctx::on_new_frame(int cur) {
             break;
         }
         case VISO_STATE_RUNNING: {
-            // Sophus::SE3d X(last_frame->GetR(), last_frame->GetT()) (src/viso.cpp:114)
-            launch_se3_from_pose(pose_of(last_slot), (double*)se3.ptr, stream);
+            // Sophus::SE3d X(last_frame->GetR(), last_frame->GetT()) (src/viso.cpp:114) is
+            // seeded inside level 3; level 0 writes cur_frame->SetR/SetT(X) and
+            // poses.push_back(X) (src/viso.cpp:117-118, 137)
+            const bool log = n_poses < p.max_poses;
             {
                 TimedRegion t(timing, VISO_KERNEL_DIRECT, stream);
                 for (int level = kLevels - 1; level >= 0; --level)
                     launch_direct_level(frame(last_slot), frame(cur), g, K, (const double*)map_pts.ptr,
                                         n_map, pose_of(last_slot), (double*)se3.ptr, level, direct,
-                                        (double*)direct_stats.ptr + 50 * level, stream);
+                                        (double*)direct_stats.ptr + 50 * level, stream,
+                                        level == kLevels - 1, level == 0 ? pose_of(cur) : nullptr,
+                                        level == 0 && log ? (double*)pose_log.ptr : nullptr,
+                                        level == 0 && log ? (int*)pose_count.ptr : nullptr);
             }
-            // cur_frame->SetR/SetT(X); poses.push_back(X) (src/viso.cpp:117-118, 137)
-            const bool log = n_poses < p.max_poses;
-            launch_se3_to_pose((const double*)se3.ptr, pose_of(cur), log ? (double*)pose_log.ptr : nullptr,
-                               log ? (int*)pose_count.ptr : nullptr, stream);
             if (log) ++n_poses;
             // LKAlignment (src/viso.cpp:121, 768-843)
             LkAlignArgs a{};

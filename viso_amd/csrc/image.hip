@@ -75,6 +75,157 @@ __global__ __launch_bounds__(256) void pyr_down_kernel(PyrPtrs ptrs, int sw, int
     }
 }
 
+// ---------------------------------------------------------------- fused pyramid
+// One workgroup owns a level-3 tile of 16x8 and the matching level-2 (32x16)
+// and level-1 (64x32) tiles.  It stages the level-0 window that feeds them
+// (149 x 85, recursive 5-tap halos) in LDS with 16-byte loads, then runs
+// horizontal/vertical passes level by level entirely in LDS.  Every level's
+// border uses reflect-101 against that level's own (truncated) size, so
+// halo samples are read at reflected coordinates, which always fall inside
+// the window.  Integer math: identical to three separate pyrDown passes.
+constexpr int kF3W = 16, kF3H = 8;
+constexpr int kF2W = 2 * kF3W + 3, kF2H = 2 * kF3H + 3;  // 35 x 19
+constexpr int kF1W = 2 * kF2W + 3, kF1H = 2 * kF2H + 3;  // 73 x 41
+constexpr int kF0W = 2 * kF1W + 3, kF0H = 2 * kF1H + 3;  // 149 x 85
+constexpr int kF0P = 160;                                // LDS pitch of the level-0 window
+
+struct PyrFusedArgs {
+    const uint8_t* l0[kPyrBatch];
+    uint8_t* slot[kPyrBatch];
+    int w[4], h[4];
+    unsigned long long off[4];
+};
+
+__global__ __launch_bounds__(256) void pyr_fused_kernel(PyrFusedArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t s0[kF0H][kF0P];
+    __shared__ short hs0[kF0H][kF1W];
+    __shared__ uint8_t s1[kF1H][kF1W + 3];
+    __shared__ short hs1[kF1H][kF2W];
+    __shared__ uint8_t s2[kF2H][kF2W + 1];
+    const uint8_t* __restrict__ src = a.l0[blockIdx.z];
+    uint8_t* __restrict__ base = a.slot[blockIdx.z];
+    const int tid = threadIdx.x;
+    const int X3 = blockIdx.x * kF3W, Y3 = blockIdx.y * kF3H;
+    const int ox2 = 2 * X3 - 2, oy2 = 2 * Y3 - 2;
+    const int ox1 = 2 * ox2 - 2, oy1 = 2 * oy2 - 2;
+    const int ox0 = 2 * ox1 - 2, oy0 = 2 * oy1 - 2;
+    const int w0 = a.w[0], h0 = a.h[0], w1 = a.w[1], h1 = a.h[1];
+    const int w2 = a.w[2], h2 = a.h[2], w3 = a.w[3], h3 = a.h[3];
+    // ---- stage the level-0 window (in-range part), 16-byte aligned chunks
+    {
+        const int c_lo = max(ox0, 0), c_hi = min(ox0 + kF0W, w0);
+        const uintptr_t img_lo = (uintptr_t)src, img_hi = img_lo + (uintptr_t)w0 * h0;
+        const int nchunk = (c_hi > c_lo) ? ((c_hi - c_lo) + 15 + 15) / 16 : 0;
+        for (int it = tid; it < kF0H * nchunk; it += 256) {
+            const int r = it / nchunk, k = it - r * nchunk;
+            const int y = oy0 + r;
+            if (y < 0 || y >= h0) continue;
+            const uintptr_t row = img_lo + (uintptr_t)y * w0;
+            const uintptr_t a0 = ((row + c_lo) & ~(uintptr_t)15) + 16 * (uintptr_t)k;
+            const uintptr_t lo = row + c_lo, hi = row + c_hi;
+            if (a0 >= hi) continue;
+            if (a0 >= img_lo && a0 + 16 <= img_hi) {
+                const uint4 v = *reinterpret_cast<const uint4*>(a0);
+                const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int b = 0; b < 16; ++b) {
+                    const uintptr_t ad = a0 + b;
+                    if (ad >= lo && ad < hi) s0[r][(int)(ad - row) - ox0] = (uint8_t)(wv[b >> 2] >> (8 * (b & 3)));
+                }
+            } else {
+                for (int b = 0; b < 16; ++b) {
+                    const uintptr_t ad = a0 + b;
+                    if (ad >= lo && ad < hi) s0[r][(int)(ad - row) - ox0] = *reinterpret_cast<const uint8_t*>(ad);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // ---- level 1: horizontal pass on every staged row
+    for (int it = tid; it < kF0H * kF1W; it += 256) {
+        const int r = it / kF1W, c = it - r * kF1W;
+        const int y = oy0 + r, x1 = ox1 + c;
+        if (y < 0 || y >= h0 || x1 < 0 || x1 >= w1) continue;
+        int s = 0;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const int wgt = j == 2 ? 6 : ((j & 1) ? 4 : 1);
+            s += wgt * (int)s0[r][reflect101(2 * x1 - 2 + j, w0) - ox0];
+        }
+        hs0[r][c] = (short)s;
+    }
+    __syncthreads();
+    uint8_t* d1 = base + a.off[1];
+    for (int it = tid; it < kF1H * kF1W; it += 256) {
+        const int r = it / kF1W, c = it - r * kF1W;
+        const int y1 = oy1 + r, x1 = ox1 + c;
+        if (y1 < 0 || y1 >= h1 || x1 < 0 || x1 >= w1) continue;
+        int s = 0;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const int wgt = i == 2 ? 6 : ((i & 1) ? 4 : 1);
+            s += wgt * (int)hs0[reflect101(2 * y1 - 2 + i, h0) - oy0][c];
+        }
+        const uint8_t v = (uint8_t)((s + 128) >> 8);
+        s1[r][c] = v;
+        if (x1 >= 4 * X3 && x1 < 4 * X3 + 4 * kF3W && y1 >= 4 * Y3 && y1 < 4 * Y3 + 4 * kF3H)
+            d1[(size_t)y1 * w1 + x1] = v;
+    }
+    __syncthreads();
+    // ---- level 2
+    for (int it = tid; it < kF1H * kF2W; it += 256) {
+        const int r = it / kF2W, c = it - r * kF2W;
+        const int y1 = oy1 + r, x2 = ox2 + c;
+        if (y1 < 0 || y1 >= h1 || x2 < 0 || x2 >= w2) continue;
+        int s = 0;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const int wgt = j == 2 ? 6 : ((j & 1) ? 4 : 1);
+            s += wgt * (int)s1[r][reflect101(2 * x2 - 2 + j, w1) - ox1];
+        }
+        hs1[r][c] = (short)s;
+    }
+    __syncthreads();
+    uint8_t* d2 = base + a.off[2];
+    for (int it = tid; it < kF2H * kF2W; it += 256) {
+        const int r = it / kF2W, c = it - r * kF2W;
+        const int y2 = oy2 + r, x2 = ox2 + c;
+        if (y2 < 0 || y2 >= h2 || x2 < 0 || x2 >= w2) continue;
+        int s = 0;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const int wgt = i == 2 ? 6 : ((i & 1) ? 4 : 1);
+            s += wgt * (int)hs1[reflect101(2 * y2 - 2 + i, h1) - oy1][c];
+        }
+        const uint8_t v = (uint8_t)((s + 128) >> 8);
+        s2[r][c] = v;
+        if (x2 >= 2 * X3 && x2 < 2 * X3 + 2 * kF3W && y2 >= 2 * Y3 && y2 < 2 * Y3 + 2 * kF3H)
+            d2[(size_t)y2 * w2 + x2] = v;
+    }
+    __syncthreads();
+    // ---- level 3 (128 outputs, 25 taps each; integer sums are exact)
+    uint8_t* d3 = base + a.off[3];
+    if (tid < kF3W * kF3H) {
+        const int x3 = X3 + (tid & (kF3W - 1)), y3 = Y3 + tid / kF3W;
+        if (x3 < w3 && y3 < h3) {
+            int s = 0;
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+                const int wi = i == 2 ? 6 : ((i & 1) ? 4 : 1);
+                const int rr = reflect101(2 * y3 - 2 + i, h2) - oy2;
+                int hsum = 0;
+#pragma unroll
+                for (int j = 0; j < 5; ++j) {
+                    const int wj = j == 2 ? 6 : ((j & 1) ? 4 : 1);
+                    hsum += wj * (int)s2[rr][reflect101(2 * x3 - 2 + j, w2) - ox2];
+                }
+                s += wi * hsum;
+            }
+            d3[(size_t)y3 * w3 + x3] = (uint8_t)((s + 128) >> 8);
+        }
+    }
+}
+
 // ---------------------------------------------------------------- FAST
 __constant__ int c_circle_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
 __constant__ int c_circle_dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
@@ -241,6 +392,28 @@ __global__ __launch_bounds__(256) void fast_compact_kernel(const int* __restrict
 
 void launch_pyramid_frames(const PyrGeom& g, const uint8_t* const* l0, uint8_t* const* slot,
                            int n, hipStream_t stream) {
+    auto cdiv = [](int a, int b) { return (a + b - 1) / b; };
+    const int tx = std::max(cdiv(g.w[3], kF3W), std::max(cdiv(g.w[2], 2 * kF3W), cdiv(g.w[1], 4 * kF3W)));
+    const int ty = std::max(cdiv(g.h[3], kF3H), std::max(cdiv(g.h[2], 2 * kF3H), cdiv(g.h[1], 4 * kF3H)));
+    for (int b0 = 0; b0 < n; b0 += kPyrBatch) {
+        const int nb = (n - b0) < kPyrBatch ? (n - b0) : kPyrBatch;
+        PyrFusedArgs a;
+        for (int l = 0; l < kLevels; ++l) {
+            a.w[l] = g.w[l];
+            a.h[l] = g.h[l];
+            a.off[l] = g.off[l];
+        }
+        for (int i = 0; i < nb; ++i) {
+            a.l0[i] = l0[b0 + i];
+            a.slot[i] = slot[b0 + i];
+        }
+        pyr_fused_kernel<<<dim3(tx, ty, nb), 256, 0, stream>>>(a);
+    }
+}
+
+// Reference (unfused) form: one launch per level; kept for A/B timing.
+void launch_pyramid_frames_unfused(const PyrGeom& g, const uint8_t* const* l0,
+                                   uint8_t* const* slot, int n, hipStream_t stream) {
     for (int b0 = 0; b0 < n; b0 += kPyrBatch) {
         const int nb = (n - b0) < kPyrBatch ? (n - b0) : kPyrBatch;
         for (int l = 1; l < kLevels; ++l) {

@@ -65,16 +65,21 @@ void launch_stereo_sad(const uint8_t* left, const uint8_t* right, int w, int h, 
 // ---------------------------------------------------------------- direct pose
 constexpr int kMaxMapPoints = 16384;
 struct DirectScratch {
-    double* tile_part = nullptr;  // [256 * 28]
-    int* tile_good = nullptr;     // [256]
+    double* tile_part = nullptr;  // [28 x 4096] k-major
+    int* tile_good = nullptr;     // [4096]
 };
+size_t direct_scratch_bytes();
 // SE3 state on the device: 7 doubles (qx, qy, qz, qw, tx, ty, tz).
 // One DirectPoseEstimationSingleLayer call (faithful: one GN step).
 // stats (device, may be null): [nGood, cost, H(36), b(6), update(6)].
+// seed_from_last: start from SE3(R, t) of pose_last12 instead of se3_state.
+// pose_out (may be null): receives R, t of the result; log/log_count append.
 void launch_direct_level(const FrameDev& last, const FrameDev& cur, const PyrGeom& g,
                          const double K[4], const double* points, int n,
                          const double* pose_last12, double* se3_state, int level,
-                         DirectScratch& s, double* stats, hipStream_t stream);
+                         DirectScratch& s, double* stats, hipStream_t stream,
+                         bool seed_from_last = false, double* pose_out = nullptr,
+                         double* log = nullptr, int* log_count = nullptr);
 // dst (12 doubles, device) <- src (host values, passed by value)
 void launch_set_pose(double* dst, const double src[12], hipStream_t stream);
 // se3_state <- SE3(R, t) of a 12-double pose (Sophus::SE3d(R, t)).

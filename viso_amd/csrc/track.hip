@@ -41,9 +41,9 @@ __device__ inline LkResult lk_level(const uint8_t* __restrict__ img1, int w1, in
     gradient_px(img1, w1, h1, ref_x, ref_y, gx, gy);
     const double J0 = -gx, J1 = -gy;
     const double I1 = sample_px(img1, w1, h1, ref_x, ref_y);
-    const double H00 = wave_tree_sum(J0 * J0);
-    const double H01 = wave_tree_sum(J0 * J1);
-    const double H11 = wave_tree_sum(J1 * J1);
+    const double H00 = wave_tree_sum_dpp(J0 * J0);
+    const double H01 = wave_tree_sum_dpp(J0 * J1);
+    const double H11 = wave_tree_sum_dpp(J1 * J1);
     const double H10 = H01;  // J1*J0 == J0*J1 leaf by leaf
     const double invdet = 1.0 / (H00 * H11 - H10 * H01);
     const double i00 = H11 * invdet, i10 = -H10 * invdet, i01 = -H01 * invdet, i11 = H00 * invdet;
@@ -62,9 +62,9 @@ __device__ inline LkResult lk_level(const uint8_t* __restrict__ img1, int w1, in
             break;
         }
         const double e = I1 - sample_px(img2, w2, h2, cur_x + dx, cur_y + dy);
-        const double B0 = wave_tree_sum(-J0 * e);
-        const double B1 = wave_tree_sum(-J1 * e);
-        cost = wave_tree_sum(e * e);
+        const double B0 = wave_tree_sum_dpp(-J0 * e);
+        const double B1 = wave_tree_sum_dpp(-J1 * e);
+        cost = wave_tree_sum_dpp(e * e);
         const double u0 = i00 * B0 + i01 * B1;
         const double u1 = i10 * B0 + i11 * B1;
         if (isnan(u0)) {
