@@ -50,6 +50,32 @@ def test_version_and_host_only_calls():
     assert p.photometric_error_thresh == 14400.0 and p.disparity_squared_thresh == 225.0
 
 
+def _build_facade(tmp_path):
+    import subprocess
+    exe = str(tmp_path / "facade_check")
+    libdir = os.path.join(ROOT, "viso_amd")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cpp", "facade_check.cpp"), "-L", libdir,
+                    "-lviso_amd", f"-Wl,-rpath,{libdir}", "-o", exe], check=True)
+    return exe
+
+
+def test_cpp_facade_compiles_and_links(tmp_path):
+    import subprocess
+    exe = _build_facade(tmp_path)
+    out = subprocess.run([exe], capture_output=True, text=True, check=True)
+    assert "facade ok" in out.stdout
+
+
+@pytest.mark.gpu
+def test_gpu_cpp_facade_runs(tmp_path):
+    import subprocess
+    exe = _build_facade(tmp_path)
+    out = subprocess.run([exe, "run"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "poses" in out.stdout
+
+
 def test_oracle_stereo_recovers_known_disparity():
     rng = np.random.default_rng(0)
     left = rng.integers(0, 256, (60, 200), dtype=np.uint8)

@@ -123,6 +123,7 @@ int viso_destroy(viso_ctx* c) {
 int viso_synchronize(viso_ctx* c) {
     if (!c) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipStreamSynchronize(c->stream));
+    if (c->lk_stream) VISO_HIP_CHECK(hipStreamSynchronize(c->lk_stream));
     return VISO_OK;
 }
 

@@ -105,7 +105,9 @@ struct SlotRec {
     const uint8_t* l0 = nullptr;
     bool borrowed = false;
     int refs = 0;
+    int64_t lk_use = -1;  // last LK-alignment launch (on the LK stream) that reads it
 };
+constexpr int kLkRing = 64;
 }  // namespace viso
 
 struct viso_ctx {
@@ -155,6 +157,12 @@ struct viso_ctx {
     viso::DirectScratch direct{};
     viso::DevBuf direct_stats;  // 4 levels x 50 doubles
     viso::DevBuf lk_pair, lk_succ, lk_before, lk_after;
+    // LKAlignment only feeds the display (src/viso.cpp:121-135): it runs on
+    // its own stream and overlaps the next frame's direct pose.
+    hipStream_t lk_stream = nullptr;
+    hipEvent_t ev_pose = nullptr;
+    hipEvent_t lk_ring[viso::kLkRing] = {};
+    int64_t lk_seq = 0;
     viso::DevBuf pose_log;  // max_poses x 12
     viso::DevBuf pose_count;
     int n_poses = 0;

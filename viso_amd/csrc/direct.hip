@@ -3,20 +3,24 @@
 // src/viso.cpp:640-766).
 //
 // One level = two launches:
-//  1. direct_tiles_kernel: one wave per map point, lane = patch pixel.  The
-//     wave forms J = -grad^T * dPixel/dXi for its 64 pixels and reduces the
-//     28 sums (21 upper-triangle J J^T, 6 -e J, e^2) with the canonical DPP
-//     wave tree; a workgroup's 4 points form one tile, (p0 + p1) + (p2 + p3).
-//  2. direct_solve_kernel (one workgroup): canonical tree over the tiles
-//     (independent coalesced loads, k-major layout), then on one lane:
-//     H^-1 (PartialPivLU), SE3::exp(update) * T21, cost / nGood and the
-//     NaN / cost-increase / relative-decrease checks of :741-753.
+//  1. direct_tiles_kernel (8 waves): one wave per map point at a time, lane =
+//     patch pixel.  The wave forms J = -grad^T * dPixel/dXi for its 64 pixels
+//     and reduces the 28 sums (21 upper-triangle J J^T, 6 -e J, e^2) with the
+//     canonical DPP wave tree.  A workgroup owns an aligned tile of
+//     T = max(8, P/256) points (P = next pow2 of the point count), so there
+//     are at most 256 tiles; the tile's 28 sums are a tree over its points,
+//     stored tile-major.
+//  2. direct_solve_kernel (one workgroup): thread t loads tile t's 28 sums in
+//     one burst; canonical tree over tiles (DPP wave tree, then the 4 waves);
+//     PartialPivLU of H on one lane, the six inverse columns on six lanes
+//     (column-oriented forward/backward substitution), update rows on six
+//     lanes, SE3::exp(update) * T21, cost / nGood and the checks of :741-753.
 // The sum order is the canonical pairwise tree over (point, pixel), so the
 // result is independent of the launch geometry and equal to the oracle's.
 // As shipped the loop takes exactly one GN step per level (cost is never
 // reset, src/viso.cpp:673); the rare continuation (a level
 // whose photometric cost is exactly 0) is executed faithfully by the solve
-// workgroup itself, re-running the tiles.
+// workgroup itself, re-running every tile.
 // Frame-level fusions: level 3 seeds T21 = SE3(last R, last t)
 // (src/viso.cpp:114) inside both kernels; level 0's solve writes
 // cur_frame R,t and appends the pose log (src/viso.cpp:117-118, 137).
@@ -28,9 +32,9 @@ namespace viso {
 namespace {
 
 constexpr int kSums = 28;
-constexpr int kTile = 4;           // points per tile = waves per workgroup
-constexpr int kMaxTiles = 4096;    // kMaxMapPoints / kTile
-constexpr int kChunk = kMaxTiles / 256;
+constexpr int kWaves = 8;         // waves per tiles workgroup
+constexpr int kMaxTiles = 256;
+constexpr int kMaxTile = kMaxMapPoints / kMaxTiles;  // 64 points
 
 struct DirectArgs {
     FrameDev last;
@@ -43,9 +47,9 @@ struct DirectArgs {
     double* se3;  // 7 doubles in/out
     int seed_from_last;
     int level;
-    int n_tiles;
-    int tile_stride;  // k-major layout: tile_part[k * tile_stride + tile]
-    double* tile_part;
+    int tile;     // points per tile (power of two, >= kWaves)
+    int n_tiles;  // <= 256
+    double* tile_part;  // tile-major [tile][28]
     int* tile_good;
     double* stats;
     double* pose_out;  // level 0: cur pose (12)
@@ -138,35 +142,42 @@ __device__ inline void state_to_pose(const double* st, double* pose) {
     pose[11] = st[6];
 }
 
-// Tile b (kTile points): 28 sums -> tile_part (k-major), good count -> tile_good.
-// Called by a whole 256-thread workgroup.
-__device__ void direct_tile(const DirectArgs& a, const double* cur_pose, int b, double* s_pts,
-                            int* s_good4) {
+// Tile b (a.tile points): 28 sums -> tile_part[b], good count -> tile_good[b].
+// Called by every thread of a workgroup of `nwaves` waves.
+__device__ void direct_tile(const DirectArgs& a, const double* cur_pose, int b, int nwaves,
+                            double* s_pts, int* s_good) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int i = b * kTile + wave;
-    double s[kSums];
-    bool good = false;
-    if (i < a.n) good = direct_point(a, cur_pose, i, s);
-    if (lane == 0) {
-#pragma unroll
-        for (int k = 0; k < kSums; ++k) s_pts[wave * kSums + k] = good ? s[k] : 0.0;
-        s_good4[wave] = good ? 1 : 0;
-    }
+    const int T = a.tile;
+    if (threadIdx.x == 0) *s_good = 0;
     __syncthreads();
-    if (threadIdx.x < kSums) {
-        const int k = threadIdx.x;
-        const double v = (s_pts[0 * kSums + k] + s_pts[1 * kSums + k]) +
-                         (s_pts[2 * kSums + k] + s_pts[3 * kSums + k]);
-        a.tile_part[(size_t)k * a.tile_stride + b] = v;
+    int good_cnt = 0;
+    for (int local = wave; local < T; local += nwaves) {
+        const int i = b * T + local;
+        double s[kSums];
+        bool good = false;
+        if (i < a.n) good = direct_point(a, cur_pose, i, s);
+        if (lane == 0) {
+#pragma unroll
+            for (int k = 0; k < kSums; ++k) s_pts[local * kSums + k] = good ? s[k] : 0.0;
+        }
+        good_cnt += good ? 1 : 0;
     }
-    if (threadIdx.x == 0) a.tile_good[b] = (s_good4[0] + s_good4[1]) + (s_good4[2] + s_good4[3]);
+    if (lane == 0 && good_cnt) atomicAdd(s_good, good_cnt);
+    __syncthreads();
+    // tree over the tile's T points (lanes >= T hold +0.0)
+    for (int k = wave; k < kSums; k += nwaves) {
+        const double v = lane < T ? s_pts[lane * kSums + k] : 0.0;
+        const double r = wave_tree_sum_dpp(v);
+        if (lane == 0) a.tile_part[(size_t)b * kSums + k] = r;
+    }
+    if (threadIdx.x == 0) a.tile_good[b] = *s_good;
     __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void direct_tiles_kernel(DirectArgs a) {
+__global__ __launch_bounds__(kWaves * 64) void direct_tiles_kernel(DirectArgs a) {
     __shared__ double s_pose[12];
-    __shared__ double s_pts[kTile * kSums];
-    __shared__ int s_good4[kTile];
+    __shared__ double s_pts[kMaxTile * kSums];
+    __shared__ int s_good;
     if (threadIdx.x == 0) {
         double st[7];
         start_state(a, st);
@@ -176,48 +187,41 @@ __global__ __launch_bounds__(256) void direct_tiles_kernel(DirectArgs a) {
     double pose[12];
 #pragma unroll
     for (int k = 0; k < 12; ++k) pose[k] = s_pose[k];
-    direct_tile(a, pose, blockIdx.x, s_pts, s_good4);
+    direct_tile(a, pose, blockIdx.x, kWaves, s_pts, &s_good);
 }
 
-// Canonical tree over the tiles: thread t owns the aligned chunk
-// [t*C, (t+1)*C) (C = P_tiles/256, a power of two <= kChunk; a 16-leaf tree
-// whose extra leaves are +0.0 equals the C-leaf tree), then lanes and waves.
-__device__ void reduce_tiles(const DirectArgs& a, double* S, int* n_good, double* s_red) {
+// Canonical tree over <= 256 tiles: thread t holds tile t (zeros beyond).
+__device__ void reduce_tiles(const DirectArgs& a, double* S, int* n_good, double* s_red,
+                             int* s_g) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int t = threadIdx.x;
-    int P = 256;
-    while (P < a.n_tiles) P <<= 1;
-    const int C = P / 256;
-    for (int k = 0; k < kSums; ++k) {
-        const double* src = a.tile_part + (size_t)k * a.tile_stride;
-        double v[kChunk];
+    double v[kSums];
+    if (t < a.n_tiles) {
+        const double2* src = reinterpret_cast<const double2*>(a.tile_part + (size_t)t * kSums);
 #pragma unroll
-        for (int j = 0; j < kChunk; ++j) {
-            const int tile = t * C + j;
-            v[j] = (j < C && tile < a.n_tiles) ? src[tile] : 0.0;
+        for (int k = 0; k < kSums / 2; ++k) {
+            const double2 d = src[k];
+            v[2 * k] = d.x;
+            v[2 * k + 1] = d.y;
         }
+    } else {
 #pragma unroll
-        for (int sft = 1; sft < kChunk; sft <<= 1)
+        for (int k = 0; k < kSums; ++k) v[k] = 0.0;
+    }
+    int g = t < a.n_tiles ? a.tile_good[t] : 0;
 #pragma unroll
-            for (int j = 0; j < kChunk; j += 2 * sft) v[j] = v[j] + v[j + sft];
-        const double r = wave_tree_sum_dpp(v[0]);
+    for (int k = 0; k < kSums; ++k) {
+        const double r = wave_tree_sum_dpp(v[k]);
         if (lane == 0) s_red[wave * kSums + k] = r;
     }
-    int gsum = 0;
-    for (int j = 0; j < C; ++j) {
-        const int tile = t * C + j;
-        gsum += tile < a.n_tiles ? a.tile_good[tile] : 0;
-    }
-    gsum = wave_sum_int(gsum);
-    __shared__ int s_g[4];
-    if (lane == 0) s_g[wave] = gsum;
+    g = wave_sum_int(g);
+    if (lane == 0) s_g[wave] = g;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int k = 0; k < kSums; ++k)
-            S[k] = (s_red[0 * kSums + k] + s_red[1 * kSums + k]) +
-                   (s_red[2 * kSums + k] + s_red[3 * kSums + k]);
-        *n_good = (s_g[0] + s_g[1]) + (s_g[2] + s_g[3]);
+    if (threadIdx.x < kSums) {
+        const int k = threadIdx.x;
+        S[k] = (s_red[0 * kSums + k] + s_red[1 * kSums + k]) + (s_red[2 * kSums + k] + s_red[3 * kSums + k]);
     }
+    if (threadIdx.x == 0) *n_good = (s_g[0] + s_g[1]) + (s_g[2] + s_g[3]);
     __syncthreads();
 }
 
@@ -225,12 +229,15 @@ __global__ __launch_bounds__(256) void direct_solve_kernel(DirectArgs a) {
     __shared__ double s_red[4 * kSums];
     __shared__ double S[kSums];
     __shared__ int s_ngood;
+    __shared__ int s_g[4];
     __shared__ double s_pose[12];
-    __shared__ double s_pts[kTile * kSums];
-    __shared__ int s_good4[kTile];
+    __shared__ double s_pts[kMaxTile * kSums];
+    __shared__ int s_good;
     __shared__ int s_continue;
     __shared__ double s_state[7], s_best[7];
     __shared__ double s_cost, s_lastCost;
+    __shared__ double s_lu[36], s_inv[36], s_upd[6];
+    __shared__ int s_tr[6];
     if (threadIdx.x == 0) {
         start_state(a, s_state);
         for (int k = 0; k < 7; ++k) s_best[k] = s_state[k];
@@ -245,29 +252,81 @@ __global__ __launch_bounds__(256) void direct_solve_kernel(DirectArgs a) {
             __syncthreads();
             double pose[12];
             for (int k = 0; k < 12; ++k) pose[k] = s_pose[k];
-            for (int b = 0; b < a.n_tiles; ++b) direct_tile(a, pose, b, s_pts, s_good4);
+            for (int b = 0; b < a.n_tiles; ++b) direct_tile(a, pose, b, 4, s_pts, &s_good);
             __threadfence_block();
             __syncthreads();
         }
-        reduce_tiles(a, S, &s_ngood, s_red);
+        reduce_tiles(a, S, &s_ngood, s_red, s_g);
+        // ---- H.inverse() (Eigen PartialPivLU): factor on lane 0 ...
         if (threadIdx.x == 0) {
-            double H[36], b[6];
+            double lu[36];
             int idx = 0;
             for (int r = 0; r < 6; ++r)
                 for (int c = r; c < 6; ++c) {
-                    H[6 * r + c] = S[idx];
-                    H[6 * c + r] = S[idx];
+                    lu[6 * r + c] = S[idx];
+                    lu[6 * c + r] = S[idx];
                     ++idx;
                 }
-            for (int k = 0; k < 6; ++k) b[k] = S[21 + k];
-            double cost = s_cost + S[27];
-            double inv[36], update[6];
-            inverse6(H, inv);
-            for (int r = 0; r < 6; ++r) {
-                double s = inv[6 * r] * b[0];
-                for (int c = 1; c < 6; ++c) s = s + inv[6 * r + c] * b[c];
-                update[r] = s;
+            for (int k = 0; k < 6; ++k) {
+                int p = k;
+                double best = fabs(lu[6 * k + k]);
+                for (int i = k + 1; i < 6; ++i) {
+                    const double s = fabs(lu[6 * i + k]);
+                    if (s > best) {
+                        best = s;
+                        p = i;
+                    }
+                }
+                s_tr[k] = p;
+                if (best != 0.0) {
+                    if (p != k)
+                        for (int j = 0; j < 6; ++j) {
+                            const double tmp = lu[6 * k + j];
+                            lu[6 * k + j] = lu[6 * p + j];
+                            lu[6 * p + j] = tmp;
+                        }
+                    for (int i = k + 1; i < 6; ++i) lu[6 * i + k] = lu[6 * i + k] / lu[6 * k + k];
+                }
+                for (int i = k + 1; i < 6; ++i)
+                    for (int j = k + 1; j < 6; ++j) lu[6 * i + j] = lu[6 * i + j] - lu[6 * i + k] * lu[6 * k + j];
             }
+            for (int e = 0; e < 36; ++e) s_lu[e] = lu[e];
+        }
+        __syncthreads();
+        // ... one lane per column: X = P*I, forward (unit L), backward (U)
+        if (threadIdx.x < 6) {
+            const int c = threadIdx.x;
+            double x[6];
+            for (int i = 0; i < 6; ++i) x[i] = (i == c) ? 1.0 : 0.0;
+            for (int k = 0; k < 6; ++k) {
+                const int p = s_tr[k];
+                if (p != k) {
+                    const double tmp = x[k];
+                    x[k] = x[p];
+                    x[p] = tmp;
+                }
+            }
+            for (int j = 0; j < 6; ++j)
+                for (int i = j + 1; i < 6; ++i) x[i] = x[i] - s_lu[6 * i + j] * x[j];
+            for (int j = 5; j >= 0; --j) {
+                x[j] = x[j] / s_lu[6 * j + j];
+                for (int i = 0; i < j; ++i) x[i] = x[i] - s_lu[6 * i + j] * x[j];
+            }
+            for (int i = 0; i < 6; ++i) s_inv[6 * i + c] = x[i];
+        }
+        __syncthreads();
+        // update = H^-1 * b, one lane per row
+        if (threadIdx.x < 6) {
+            const int r = threadIdx.x;
+            double s = s_inv[6 * r] * S[21];
+            for (int c = 1; c < 6; ++c) s = s + s_inv[6 * r + c] * S[21 + c];
+            s_upd[r] = s;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double update[6];
+            for (int k = 0; k < 6; ++k) update[k] = s_upd[k];
+            double cost = s_cost + S[27];
             SE3d T21;
             for (int k = 0; k < 4; ++k) T21.q[k] = s_state[k];
             for (int k = 0; k < 3; ++k) T21.t[k] = s_state[4 + k];
@@ -279,8 +338,14 @@ __global__ __launch_bounds__(256) void direct_solve_kernel(DirectArgs a) {
             if (a.stats) {
                 a.stats[0] = s_ngood;
                 a.stats[1] = cost;
-                for (int k = 0; k < 36; ++k) a.stats[2 + k] = H[k];
-                for (int k = 0; k < 6; ++k) a.stats[38 + k] = b[k];
+                int idx = 0;
+                for (int r = 0; r < 6; ++r)
+                    for (int c = r; c < 6; ++c) {
+                        a.stats[2 + 6 * r + c] = S[idx];
+                        a.stats[2 + 6 * c + r] = S[idx];
+                        ++idx;
+                    }
+                for (int k = 0; k < 6; ++k) a.stats[38 + k] = S[21 + k];
                 for (int k = 0; k < 6; ++k) a.stats[44 + k] = update[k];
             }
             int cont = 1;
@@ -371,19 +436,21 @@ void launch_direct_level(const FrameDev& last_pyr, const FrameDev& cur_pyr, cons
     a.se3 = se3_state;
     a.seed_from_last = seed_from_last ? 1 : 0;
     a.level = level;
-    a.n_tiles = (n + kTile - 1) / kTile;
-    a.tile_stride = kMaxTiles;
+    int P = 1;
+    while (P < n) P <<= 1;
+    a.tile = P / kMaxTiles > kWaves ? P / kMaxTiles : kWaves;
+    a.n_tiles = (n + a.tile - 1) / a.tile;
     a.tile_part = s.tile_part;
     a.tile_good = s.tile_good;
     a.stats = stats;
     a.pose_out = pose_out;
     a.log = log;
     a.log_count = log_count;
-    if (a.n_tiles > 0) direct_tiles_kernel<<<a.n_tiles, 256, 0, stream>>>(a);
+    if (a.n_tiles > 0) direct_tiles_kernel<<<a.n_tiles, kWaves * 64, 0, stream>>>(a);
     direct_solve_kernel<<<1, 256, 0, stream>>>(a);
 }
 
-size_t direct_scratch_bytes() { return (size_t)kSums * kMaxTiles * 8 + (size_t)kMaxTiles * 4; }
+size_t direct_scratch_bytes() { return (size_t)kSums * kMaxTiles * 8 + (size_t)kMaxTiles * 4 + 256; }
 
 void launch_se3_from_pose(const double* pose12, double* se3_state, hipStream_t stream) {
     se3_from_pose_kernel<<<1, 64, 0, stream>>>(pose12, se3_state);

@@ -147,7 +147,10 @@ int viso_ctx::init() {
     if (!rc) rc = pose_count.ensure(256);
     if (rc) return rc;
     direct.tile_part = (double*)direct_tiles.ptr;
-    direct.tile_good = (int*)((char*)direct_tiles.ptr + 28 * 4096 * 8);
+    direct.tile_good = (int*)((char*)direct_tiles.ptr + 28 * 256 * 8);
+    VISO_HIP_CHECK(hipStreamCreateWithFlags(&lk_stream, hipStreamNonBlocking));
+    VISO_HIP_CHECK(hipEventCreateWithFlags(&ev_pose, hipEventDisableTiming));
+    for (int i = 0; i < kLkRing; ++i) VISO_HIP_CHECK(hipEventCreateWithFlags(&lk_ring[i], hipEventDisableTiming));
     VISO_HIP_CHECK(hipMemsetAsync(pose_count.ptr, 0, 256, stream));
     VISO_HIP_CHECK(hipMemsetAsync(n_track_dev.ptr, 0, 256, stream));
     VISO_HIP_CHECK(hipStreamSynchronize(stream));
@@ -155,7 +158,16 @@ int viso_ctx::init() {
 }
 
 void viso_ctx::release() {
+    if (lk_stream) (void)hipStreamSynchronize(lk_stream);
     timing.destroy();
+    if (ev_pose) (void)hipEventDestroy(ev_pose);
+    ev_pose = nullptr;
+    for (auto& e : lk_ring) {
+        if (e) (void)hipEventDestroy(e);
+        e = nullptr;
+    }
+    if (lk_stream) (void)hipStreamDestroy(lk_stream);
+    lk_stream = nullptr;
     DevBuf* bufs[] = {&scratch_a, &scratch_b, &scratch_c, &scratch_d, &slot_pool, &slot_pose,
                       &kp1, &kp2, &kp1b, &kp2b, &track_success, &n_track_dev, &fast_rows,
                       &geo_buf, &map_pts, &kf_poses, &se3, &direct_tiles, &direct_stats,
@@ -174,6 +186,13 @@ int viso_ctx::acquire_slot() {
     if (free_slots.empty()) return -1;
     int s = free_slots.back();
     free_slots.pop_back();
+    // the LK stream may still read this slot's previous frame: order the
+    // reuse behind that launch (a no-op wait in steady state)
+    const int64_t use = slots[(size_t)s].lk_use;
+    if (use >= 0 && lk_seq > use) {
+        const int64_t e = (lk_seq - use <= kLkRing) ? use : lk_seq - 1;
+        (void)hipStreamWaitEvent(stream, lk_ring[e % kLkRing], 0);
+    }
     slots[(size_t)s] = SlotRec{};
     slots[(size_t)s].l0 = slot_base(s);
     return s;
@@ -368,10 +387,16 @@ int viso_ctx::on_new_frame(int cur) {
             a.success = (uint8_t*)lk_succ.ptr;
             a.uv_before = (double*)lk_before.ptr;
             a.uv_after = (double*)lk_after.ptr;
+            VISO_HIP_CHECK(hipEventRecord(ev_pose, stream));
+            VISO_HIP_CHECK(hipStreamWaitEvent(lk_stream, ev_pose, 0));
             {
-                TimedRegion t(timing, VISO_KERNEL_LKALIGN, stream);
-                launch_lk_align(a, stream);
+                TimedRegion t(timing, VISO_KERNEL_LKALIGN, lk_stream);
+                launch_lk_align(a, lk_stream);
             }
+            VISO_HIP_CHECK(hipEventRecord(lk_ring[lk_seq % kLkRing], lk_stream));
+            slots[(size_t)cur].lk_use = lk_seq;
+            for (int s : kf_slots) slots[(size_t)s].lk_use = lk_seq;
+            ++lk_seq;
             ran_tracking = true;
             break;
         }
@@ -544,6 +569,7 @@ int viso_get_alignment(viso_ctx* c, int32_t* pair_kf, uint8_t* success, double* 
                        double* uv_after, size_t cap, size_t* n) {
     if (!c) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(c->device));
+    VISO_HIP_CHECK(hipStreamSynchronize(c->lk_stream));
     const size_t m = c->ran_tracking ? std::min(cap, (size_t)c->n_map) : 0;
     if (m > 0) {
         if (pair_kf) VISO_HIP_CHECK(hipMemcpyAsync(pair_kf, c->lk_pair.ptr, 4 * m, hipMemcpyDeviceToHost, c->stream));
@@ -562,6 +588,7 @@ int viso_get_frame_stats(viso_ctx* c, double out[16]) {
     std::memcpy(out, c->stats, sizeof(c->stats));
     if (c->state == VISO_STATE_RUNNING && c->stats[12] == 0 && c->ran_tracking) {
         // last frame was a tracking frame: level-0 direct stats + LK counts
+        VISO_HIP_CHECK(hipStreamSynchronize(c->lk_stream));
         const int m = c->n_map;
         std::vector<int32_t> pk((size_t)m);
         std::vector<uint8_t> sc((size_t)m);
