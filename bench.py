@@ -74,11 +74,12 @@ def main():
 
     import viso_amd
     from viso_amd import _lib
+    from viso_amd.shard import gather_poses, sequence_seed
     from viso_amd.synth import Sequence
 
     W, H = args.width, args.height
     n_total = args.warmup + args.steps
-    seq = Sequence(W, H, seed=rank)
+    seq = Sequence(W, H, seed=sequence_seed(rank))
     t0 = time.time()
     left = np.stack([seq.image(f, 0) for f in range(n_total)])
     right = np.stack([seq.image(f, 1) for f in range(n_total)])
@@ -116,15 +117,9 @@ def main():
     run(args.warmup, args.steps)
     v.synchronize()
     poses = v.poses
-    pose_t = torch.from_numpy(poses[n_pose_before:].astype(np.float64)).to(f"cuda:{local}")
     if distributed:
-        # result gather over RCCL (pad to the same length)
-        n_max = torch.tensor([pose_t.shape[0]], device=pose_t.device)
-        dist.all_reduce(n_max, op=dist.ReduceOp.MAX)
-        pad = torch.zeros((int(n_max.item()), 12), dtype=torch.float64, device=pose_t.device)
-        pad[:pose_t.shape[0]] = pose_t
-        gathered = [torch.empty_like(pad) for _ in range(world)]
-        dist.all_gather(gathered, pad)
+        # the trivial result gather over RCCL (viso_amd/shard.py)
+        gathered = gather_poses(poses[n_pose_before:], device=f"cuda:{local}")
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
@@ -144,12 +139,12 @@ def main():
     algo_bytes_img = dims[0][0] * dims[0][1] + sum(w * h for w, h in dims[1:])
     roofline = None
     if "pyramid" in timing:
-        # one timed launch group = the 3-level pyramid of every image of one
-        # ingest chunk (left + right)
+        # one timed region = one pyr_fused_kernel launch building levels 1..3
+        # of every image of one ingest chunk (left + right; <= 128 images)
         imgs_per_launch = 2 * args.steps / timing["pyramid"]["launches"]
         bytes_per_launch = algo_bytes_img * imgs_per_launch
         achieved = bytes_per_launch / (timing["pyramid"]["avg_ms"] * 1e-3) / 1e9
-        roofline = {"kernel": "pyr_down_kernel x3 (batched image pass)", "bound": "hbm",
+        roofline = {"kernel": "pyr_fused_kernel (batched image pass, L0 read + L1..L3 write)", "bound": "hbm",
                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                     "algorithmic_bytes_per_launch": int(bytes_per_launch),

@@ -132,6 +132,72 @@ __device__ inline double wave_tree_sum_dpp(double v) {
     return (r0 + r1) + (r2 + r3);
 }
 
+// 28 canonical wave trees at once by reduce-scatter: at butterfly level s
+// (partner lane ^ 2^s, ascending) every lane keeps half of its remaining
+// values and adds the partner's copy of that half, so each value's partial
+// sums follow exactly the ascending-xor tree of wave_tree_sum.  Partners:
+// xor 1/2 by DPP quad_perm; xor 4/8 by DPP row_shl/row_shr + select; xor 16
+// by ds_swizzle; xor 32 by a lane shuffle.  On return, lane l (and l^32)
+// holds value index 14*b0 + 7*b1 + 4*b2 + 2*b3 + b4 (b = bits of l) when
+// 4*b2 + 2*b3 + b4 < 7; the other 4 lane classes hold garbage.
+__device__ inline double dsel(bool c, double a, double b) { return c ? a : b; }
+
+template <int CTRL>
+__device__ inline double dpp_or0(double v) {
+    return dpp_f64<CTRL>(v);
+}
+
+__device__ inline double swizzle_xor16_f64(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_ds_swizzle((int)(b & 0xffffffffLL), 0x401F);
+    const int hi = __builtin_amdgcn_ds_swizzle((int)(b >> 32), 0x401F);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+__device__ inline double reduce_scatter_28(const double* v, int* value_index) {
+    const int lane = threadIdx.x & 63;
+    const bool b0 = lane & 1, b1 = lane & 2, b2 = lane & 4, b3 = lane & 8, b4 = lane & 16;
+    double a[14];
+#pragma unroll
+    for (int k = 0; k < 14; ++k) {
+        const double send = dsel(b0, v[k], v[14 + k]);
+        const double keep = dsel(b0, v[14 + k], v[k]);
+        a[k] = keep + dpp_f64<0xB1>(send);
+    }
+    double c[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+        const double send = dsel(b1, a[k], a[7 + k]);
+        const double keep = dsel(b1, a[7 + k], a[k]);
+        c[k] = keep + dpp_f64<0x4E>(send);
+    }
+    double d[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const double hi = k < 3 ? c[4 + k] : 0.0;
+        const double send = dsel(b2, c[k], hi);
+        const double keep = dsel(b2, hi, c[k]);
+        const double recv = dsel(b2, dpp_f64<0x114>(send), dpp_f64<0x104>(send));  // row_shr:4 / row_shl:4
+        d[k] = keep + recv;
+    }
+    double e[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const double send = dsel(b3, d[k], d[2 + k]);
+        const double keep = dsel(b3, d[2 + k], d[k]);
+        const double recv = dsel(b3, dpp_f64<0x118>(send), dpp_f64<0x108>(send));  // row_shr:8 / row_shl:8
+        e[k] = keep + recv;
+    }
+    const double send = dsel(b4, e[0], e[1]);
+    const double keep = dsel(b4, e[1], e[0]);
+    double f = keep + swizzle_xor16_f64(send);
+    f = f + __shfl_xor(f, 32, 64);
+    *value_index = (b0 ? 14 : 0) + (b1 ? 7 : 0) + (b2 ? 4 : 0) + (b3 ? 2 : 0) + (b4 ? 1 : 0);
+    const int local = (b2 ? 4 : 0) + (b3 ? 2 : 0) + (b4 ? 1 : 0);
+    if (local >= 7) *value_index = -1;
+    return f;
+}
+
 __device__ inline int wave_sum_int(int v) {
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);

@@ -123,7 +123,8 @@ int viso_destroy(viso_ctx* c) {
 int viso_synchronize(viso_ctx* c) {
     if (!c) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipStreamSynchronize(c->stream));
-    if (c->lk_stream) VISO_HIP_CHECK(hipStreamSynchronize(c->lk_stream));
+    for (auto s : c->lk_streams)
+        if (s) VISO_HIP_CHECK(hipStreamSynchronize(s));
     return VISO_OK;
 }
 
@@ -279,7 +280,7 @@ int viso_direct_pose(viso_ctx* c, const uint8_t* last_pyr, const uint8_t* cur_py
                                 (const double*)(base + o_p), n, (const double*)(base + o_pl), se3,
                                 level, ds, nullptr, c->stream);
     }
-    launch_se3_to_pose(se3, (double*)(base + o_pio), nullptr, nullptr, c->stream);
+    launch_se3_to_pose(se3, (double*)(base + o_pio), nullptr, -1, c->stream);
     VISO_HIP_CHECK(hipGetLastError());
     VISO_HIP_CHECK(hipMemcpyAsync(pose_io, base + o_pio, 96, hipMemcpyDeviceToHost, c->stream));
     VISO_HIP_CHECK(hipStreamSynchronize(c->stream));

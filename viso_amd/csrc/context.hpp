@@ -156,10 +156,12 @@ struct viso_ctx {
     viso::DevBuf direct_tiles;  // 256 x 28 doubles + 256 ints
     viso::DirectScratch direct{};
     viso::DevBuf direct_stats;  // 4 levels x 50 doubles
-    viso::DevBuf lk_pair, lk_succ, lk_before, lk_after;
-    // LKAlignment only feeds the display (src/viso.cpp:121-135): it runs on
-    // its own stream and overlaps the next frame's direct pose.
-    hipStream_t lk_stream = nullptr;
+    // LKAlignment only feeds the display (src/viso.cpp:121-135): launch f
+    // runs on lk_streams[f % kLkStreams] (its own output buffer set), after
+    // direct(f), overlapping later frames' direct pose and other LK launches.
+    static constexpr int kLkStreams = 4;
+    viso::DevBuf lk_pair, lk_succ, lk_before, lk_after;  // kLkStreams x kMaxMapPoints
+    hipStream_t lk_streams[kLkStreams] = {};
     hipEvent_t ev_pose = nullptr;
     hipEvent_t lk_ring[viso::kLkRing] = {};
     int64_t lk_seq = 0;

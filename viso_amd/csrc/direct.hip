@@ -54,7 +54,7 @@ struct DirectArgs {
     double* stats;
     double* pose_out;  // level 0: cur pose (12)
     double* log;
-    int* log_count;
+    int log_index;  // < 0: no log append
 };
 
 // dPixeldXi (src/viso.cpp:640-658)
@@ -80,6 +80,46 @@ __device__ inline void d_pixel_d_xi(const Intrinsics& K, const double* pose, con
     J[9] = -fy - fy * y * y / zz;
     J[10] = fy * xy / zz;
     J[11] = fy * x / z;
+}
+
+// The 28 sums of one map point by reduce-scatter: returns good; lane l < 32
+// with *idx >= 0 holds sum *idx in *out.
+__device__ inline bool direct_point_rs(const DirectArgs& a, const double* cur_pose, int i,
+                                       double* out, int* idx) {
+    const int lane = threadIdx.x & 63;
+    const int px = (lane >> 3) - 4, py = (lane & 7) - 4;
+    const int l = a.level;
+    const double scale = kScale[l];
+    const int w = a.g.w[l], h = a.g.h[l];
+    const double P[3] = {a.points[3 * i], a.points[3 * i + 1], a.points[3 * i + 2]};
+    double ur, vr, uc, vc;
+    project_px(a.pose_last, a.K, P, scale, ur, vr);
+    project_px(cur_pose, a.K, P, scale, uc, vc);
+    const double hp = 4.0;
+    const bool good = inside_px(ur - hp, vr - hp, w, h) && inside_px(ur + hp, vr + hp, w, h) &&
+                      inside_px(uc - hp, vc - hp, w, h) && inside_px(uc + hp, vc + hp, w, h);
+    if (!good) return false;
+    double Jp[12];
+    d_pixel_d_xi(a.K, cur_pose, P, scale, Jp);
+    const uint8_t* L = a.last.l[l];
+    const uint8_t* C = a.cur.l[l];
+    const double error = sample_px(L, w, h, ur + px, vr + py) - sample_px(C, w, h, uc + px, vc + py);
+    double g0, g1;
+    gradient_px(C, w, h, uc + px, vc + py, g0, g1);
+    double J[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) J[k] = -g0 * Jp[k] + -g1 * Jp[6 + k];
+    double leaf[kSums];
+    int e = 0;
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int c = r; c < 6; ++c) leaf[e++] = J[r] * J[c];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) leaf[21 + k] = -error * J[k];
+    leaf[27] = error * error;
+    *out = reduce_scatter_28(leaf, idx);
+    return true;
 }
 
 // The 28 sums of one map point (wave-wide; identical in every lane).
@@ -153,12 +193,14 @@ __device__ void direct_tile(const DirectArgs& a, const double* cur_pose, int b, 
     int good_cnt = 0;
     for (int local = wave; local < T; local += nwaves) {
         const int i = b * T + local;
-        double s[kSums];
+        double f = 0.0;
+        int idx = -1;
         bool good = false;
-        if (i < a.n) good = direct_point(a, cur_pose, i, s);
-        if (lane == 0) {
-#pragma unroll
-            for (int k = 0; k < kSums; ++k) s_pts[local * kSums + k] = good ? s[k] : 0.0;
+        if (i < a.n) good = direct_point_rs(a, cur_pose, i, &f, &idx);
+        if (!good) {
+            if (lane < kSums) s_pts[local * kSums + lane] = 0.0;
+        } else if (lane < 32 && idx >= 0) {
+            s_pts[local * kSums + idx] = f;
         }
         good_cnt += good ? 1 : 0;
     }
@@ -373,11 +415,8 @@ __global__ __launch_bounds__(256) void direct_solve_kernel(DirectArgs a) {
             double p[12];
             state_to_pose(s_state, p);
             for (int k = 0; k < 12; ++k) a.pose_out[k] = p[k];
-            if (a.log && a.log_count) {
-                const int c = *a.log_count;
-                for (int k = 0; k < 12; ++k) a.log[12 * c + k] = p[k];
-                *a.log_count = c + 1;
-            }
+            if (a.log && a.log_index >= 0)
+                for (int k = 0; k < 12; ++k) a.log[12 * (size_t)a.log_index + k] = p[k];
         }
     }
 }
@@ -392,16 +431,13 @@ __global__ void se3_from_pose_kernel(const double* pose, double* se3) {
     se3[6] = pose[11];
 }
 
-__global__ void se3_to_pose_kernel(const double* se3, double* pose, double* log, int* log_count) {
+__global__ void se3_to_pose_kernel(const double* se3, double* pose, double* log, int log_index) {
     if (threadIdx.x != 0) return;
     double p[12];
     state_to_pose(se3, p);
     for (int k = 0; k < 12; ++k) pose[k] = p[k];
-    if (log && log_count) {
-        const int c = *log_count;
-        for (int k = 0; k < 12; ++k) log[12 * c + k] = p[k];
-        *log_count = c + 1;
-    }
+    if (log && log_index >= 0)
+        for (int k = 0; k < 12; ++k) log[12 * (size_t)log_index + k] = p[k];
 }
 
 struct Pose12v {
@@ -424,7 +460,7 @@ void launch_direct_level(const FrameDev& last_pyr, const FrameDev& cur_pyr, cons
                          const double K[4], const double* points, int n,
                          const double* pose_last12, double* se3_state, int level,
                          DirectScratch& s, double* stats, hipStream_t stream,
-                         bool seed_from_last, double* pose_out, double* log, int* log_count) {
+                         bool seed_from_last, double* pose_out, double* log, int log_index) {
     DirectArgs a;
     a.last = last_pyr;
     a.cur = cur_pyr;
@@ -445,7 +481,7 @@ void launch_direct_level(const FrameDev& last_pyr, const FrameDev& cur_pyr, cons
     a.stats = stats;
     a.pose_out = pose_out;
     a.log = log;
-    a.log_count = log_count;
+    a.log_index = log ? log_index : -1;
     if (a.n_tiles > 0) direct_tiles_kernel<<<a.n_tiles, kWaves * 64, 0, stream>>>(a);
     direct_solve_kernel<<<1, 256, 0, stream>>>(a);
 }
@@ -456,9 +492,9 @@ void launch_se3_from_pose(const double* pose12, double* se3_state, hipStream_t s
     se3_from_pose_kernel<<<1, 64, 0, stream>>>(pose12, se3_state);
 }
 
-void launch_se3_to_pose(const double* se3_state, double* pose12, double* log, int* log_count,
+void launch_se3_to_pose(const double* se3_state, double* pose12, double* log, int log_index,
                         hipStream_t stream) {
-    se3_to_pose_kernel<<<1, 64, 0, stream>>>(se3_state, pose12, log, log_count);
+    se3_to_pose_kernel<<<1, 64, 0, stream>>>(se3_state, pose12, log, log ? log_index : -1);
 }
 
 }  // namespace viso

@@ -139,16 +139,16 @@ int viso_ctx::init() {
     if (!rc) rc = se3.ensure(64);
     if (!rc) rc = direct_tiles.ensure(direct_scratch_bytes());
     if (!rc) rc = direct_stats.ensure(4 * 50 * 8);
-    if (!rc) rc = lk_pair.ensure(4 * (size_t)kMaxMapPoints);
-    if (!rc) rc = lk_succ.ensure((size_t)kMaxMapPoints);
-    if (!rc) rc = lk_before.ensure(16 * (size_t)kMaxMapPoints);
-    if (!rc) rc = lk_after.ensure(16 * (size_t)kMaxMapPoints);
+    if (!rc) rc = lk_pair.ensure(4 * (size_t)kMaxMapPoints * kLkStreams);
+    if (!rc) rc = lk_succ.ensure((size_t)kMaxMapPoints * kLkStreams);
+    if (!rc) rc = lk_before.ensure(16 * (size_t)kMaxMapPoints * kLkStreams);
+    if (!rc) rc = lk_after.ensure(16 * (size_t)kMaxMapPoints * kLkStreams);
     if (!rc) rc = pose_log.ensure(96 * (size_t)std::max(p.max_poses, 1));
     if (!rc) rc = pose_count.ensure(256);
     if (rc) return rc;
     direct.tile_part = (double*)direct_tiles.ptr;
     direct.tile_good = (int*)((char*)direct_tiles.ptr + 28 * 256 * 8);
-    VISO_HIP_CHECK(hipStreamCreateWithFlags(&lk_stream, hipStreamNonBlocking));
+    for (auto& s : lk_streams) VISO_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     VISO_HIP_CHECK(hipEventCreateWithFlags(&ev_pose, hipEventDisableTiming));
     for (int i = 0; i < kLkRing; ++i) VISO_HIP_CHECK(hipEventCreateWithFlags(&lk_ring[i], hipEventDisableTiming));
     VISO_HIP_CHECK(hipMemsetAsync(pose_count.ptr, 0, 256, stream));
@@ -158,7 +158,8 @@ int viso_ctx::init() {
 }
 
 void viso_ctx::release() {
-    if (lk_stream) (void)hipStreamSynchronize(lk_stream);
+    for (auto s : lk_streams)
+        if (s) (void)hipStreamSynchronize(s);
     timing.destroy();
     if (ev_pose) (void)hipEventDestroy(ev_pose);
     ev_pose = nullptr;
@@ -166,8 +167,10 @@ void viso_ctx::release() {
         if (e) (void)hipEventDestroy(e);
         e = nullptr;
     }
-    if (lk_stream) (void)hipStreamDestroy(lk_stream);
-    lk_stream = nullptr;
+    for (auto& s : lk_streams) {
+        if (s) (void)hipStreamDestroy(s);
+        s = nullptr;
+    }
     DevBuf* bufs[] = {&scratch_a, &scratch_b, &scratch_c, &scratch_d, &slot_pool, &slot_pose,
                       &kp1, &kp2, &kp1b, &kp2b, &track_success, &n_track_dev, &fast_rows,
                       &geo_buf, &map_pts, &kf_poses, &se3, &direct_tiles, &direct_stats,
@@ -190,7 +193,9 @@ int viso_ctx::acquire_slot() {
     // reuse behind that launch (a no-op wait in steady state)
     const int64_t use = slots[(size_t)s].lk_use;
     if (use >= 0 && lk_seq > use) {
-        const int64_t e = (lk_seq - use <= kLkRing) ? use : lk_seq - 1;
+        // a later launch on the same LK stream also implies completion
+        const int64_t e = (lk_seq - use <= kLkRing) ? use
+                                                    : use + kLkStreams * ((lk_seq - 1 - use) / kLkStreams);
         (void)hipStreamWaitEvent(stream, lk_ring[e % kLkRing], 0);
     }
     slots[(size_t)s] = SlotRec{};
@@ -361,7 +366,7 @@ int viso_ctx::on_new_frame(int cur) {
                                         (double*)direct_stats.ptr + 50 * level, stream,
                                         level == kLevels - 1, level == 0 ? pose_of(cur) : nullptr,
                                         level == 0 && log ? (double*)pose_log.ptr : nullptr,
-                                        level == 0 && log ? (int*)pose_count.ptr : nullptr);
+                                        n_poses);
             }
             if (log) ++n_poses;
             // LKAlignment (src/viso.cpp:121, 768-843)
@@ -383,17 +388,20 @@ int viso_ctx::on_new_frame(int cur) {
                 a.g.h[l] = g.h[l];
                 a.g.off[l] = g.off[l];
             }
-            a.pair_kf = (int32_t*)lk_pair.ptr;
-            a.success = (uint8_t*)lk_succ.ptr;
-            a.uv_before = (double*)lk_before.ptr;
-            a.uv_after = (double*)lk_after.ptr;
+            const int ring = (int)(lk_seq % kLkStreams);
+            const size_t o = (size_t)ring * kMaxMapPoints;
+            a.pair_kf = (int32_t*)lk_pair.ptr + o;
+            a.success = (uint8_t*)lk_succ.ptr + o;
+            a.uv_before = (double*)lk_before.ptr + 2 * o;
+            a.uv_after = (double*)lk_after.ptr + 2 * o;
+            hipStream_t ls = lk_streams[ring];
             VISO_HIP_CHECK(hipEventRecord(ev_pose, stream));
-            VISO_HIP_CHECK(hipStreamWaitEvent(lk_stream, ev_pose, 0));
+            VISO_HIP_CHECK(hipStreamWaitEvent(ls, ev_pose, 0));
             {
-                TimedRegion t(timing, VISO_KERNEL_LKALIGN, lk_stream);
-                launch_lk_align(a, lk_stream);
+                TimedRegion t(timing, VISO_KERNEL_LKALIGN, ls);
+                launch_lk_align(a, ls);
             }
-            VISO_HIP_CHECK(hipEventRecord(lk_ring[lk_seq % kLkRing], lk_stream));
+            VISO_HIP_CHECK(hipEventRecord(lk_ring[lk_seq % kLkRing], ls));
             slots[(size_t)cur].lk_use = lk_seq;
             for (int s : kf_slots) slots[(size_t)s].lk_use = lk_seq;
             ++lk_seq;
@@ -569,13 +577,14 @@ int viso_get_alignment(viso_ctx* c, int32_t* pair_kf, uint8_t* success, double* 
                        double* uv_after, size_t cap, size_t* n) {
     if (!c) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(c->device));
-    VISO_HIP_CHECK(hipStreamSynchronize(c->lk_stream));
+    for (auto s : c->lk_streams) VISO_HIP_CHECK(hipStreamSynchronize(s));
     const size_t m = c->ran_tracking ? std::min(cap, (size_t)c->n_map) : 0;
+    const size_t o = c->lk_seq > 0 ? (size_t)((c->lk_seq - 1) % viso_ctx::kLkStreams) * kMaxMapPoints : 0;
     if (m > 0) {
-        if (pair_kf) VISO_HIP_CHECK(hipMemcpyAsync(pair_kf, c->lk_pair.ptr, 4 * m, hipMemcpyDeviceToHost, c->stream));
-        if (success) VISO_HIP_CHECK(hipMemcpyAsync(success, c->lk_succ.ptr, m, hipMemcpyDeviceToHost, c->stream));
-        if (uv_before) VISO_HIP_CHECK(hipMemcpyAsync(uv_before, c->lk_before.ptr, 16 * m, hipMemcpyDeviceToHost, c->stream));
-        if (uv_after) VISO_HIP_CHECK(hipMemcpyAsync(uv_after, c->lk_after.ptr, 16 * m, hipMemcpyDeviceToHost, c->stream));
+        if (pair_kf) VISO_HIP_CHECK(hipMemcpyAsync(pair_kf, (int32_t*)c->lk_pair.ptr + o, 4 * m, hipMemcpyDeviceToHost, c->stream));
+        if (success) VISO_HIP_CHECK(hipMemcpyAsync(success, (uint8_t*)c->lk_succ.ptr + o, m, hipMemcpyDeviceToHost, c->stream));
+        if (uv_before) VISO_HIP_CHECK(hipMemcpyAsync(uv_before, (double*)c->lk_before.ptr + 2 * o, 16 * m, hipMemcpyDeviceToHost, c->stream));
+        if (uv_after) VISO_HIP_CHECK(hipMemcpyAsync(uv_after, (double*)c->lk_after.ptr + 2 * o, 16 * m, hipMemcpyDeviceToHost, c->stream));
     }
     VISO_HIP_CHECK(hipStreamSynchronize(c->stream));
     if (n) *n = c->ran_tracking ? (size_t)c->n_map : 0;
@@ -588,13 +597,14 @@ int viso_get_frame_stats(viso_ctx* c, double out[16]) {
     std::memcpy(out, c->stats, sizeof(c->stats));
     if (c->state == VISO_STATE_RUNNING && c->stats[12] == 0 && c->ran_tracking) {
         // last frame was a tracking frame: level-0 direct stats + LK counts
-        VISO_HIP_CHECK(hipStreamSynchronize(c->lk_stream));
+        for (auto s : c->lk_streams) VISO_HIP_CHECK(hipStreamSynchronize(s));
         const int m = c->n_map;
+        const size_t o = c->lk_seq > 0 ? (size_t)((c->lk_seq - 1) % viso_ctx::kLkStreams) * kMaxMapPoints : 0;
         std::vector<int32_t> pk((size_t)m);
         std::vector<uint8_t> sc((size_t)m);
         if (m > 0) {
-            VISO_HIP_CHECK(hipMemcpyAsync(pk.data(), c->lk_pair.ptr, 4 * (size_t)m, hipMemcpyDeviceToHost, c->stream));
-            VISO_HIP_CHECK(hipMemcpyAsync(sc.data(), c->lk_succ.ptr, (size_t)m, hipMemcpyDeviceToHost, c->stream));
+            VISO_HIP_CHECK(hipMemcpyAsync(pk.data(), (int32_t*)c->lk_pair.ptr + o, 4 * (size_t)m, hipMemcpyDeviceToHost, c->stream));
+            VISO_HIP_CHECK(hipMemcpyAsync(sc.data(), (uint8_t*)c->lk_succ.ptr + o, (size_t)m, hipMemcpyDeviceToHost, c->stream));
         }
         VISO_HIP_CHECK(hipMemcpyAsync(c->h_dbl, c->direct_stats.ptr, 2 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
         VISO_HIP_CHECK(hipStreamSynchronize(c->stream));

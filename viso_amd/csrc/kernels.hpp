@@ -12,7 +12,7 @@ void launch_pyramid(const PyrGeom& g, uint8_t* base, int n_images, size_t img_st
                     hipStream_t stream);
 // Batched pyramid over frames whose level 0 is at l0[i] and whose levels
 // 1..3 go to slot[i] + g.off[l] (n <= kPyrBatch per launch; more are split).
-constexpr int kPyrBatch = 64;
+constexpr int kPyrBatch = 128;
 void launch_pyramid_frames(const PyrGeom& g, const uint8_t* const* l0, uint8_t* const* slot,
                            int n, hipStream_t stream);
 
@@ -73,20 +73,21 @@ size_t direct_scratch_bytes();
 // One DirectPoseEstimationSingleLayer call (faithful: one GN step).
 // stats (device, may be null): [nGood, cost, H(36), b(6), update(6)].
 // seed_from_last: start from SE3(R, t) of pose_last12 instead of se3_state.
-// pose_out (may be null): receives R, t of the result; log/log_count append.
+// pose_out (may be null): receives R, t of the result, also stored at
+// log[12*log_index] when log is non-null.
 void launch_direct_level(const FrameDev& last, const FrameDev& cur, const PyrGeom& g,
                          const double K[4], const double* points, int n,
                          const double* pose_last12, double* se3_state, int level,
                          DirectScratch& s, double* stats, hipStream_t stream,
                          bool seed_from_last = false, double* pose_out = nullptr,
-                         double* log = nullptr, int* log_count = nullptr);
+                         double* log = nullptr, int log_index = -1);
 // dst (12 doubles, device) <- src (host values, passed by value)
 void launch_set_pose(double* dst, const double src[12], hipStream_t stream);
 // se3_state <- SE3(R, t) of a 12-double pose (Sophus::SE3d(R, t)).
 void launch_se3_from_pose(const double* pose12, double* se3_state, hipStream_t stream);
 // pose12 <- rotationMatrix(), translation() of se3_state (optionally also
-// appended to a pose log at *log_count).
-void launch_se3_to_pose(const double* se3_state, double* pose12, double* log, int* log_count,
+// stored at log[12*log_index]).
+void launch_se3_to_pose(const double* se3_state, double* pose12, double* log, int log_index,
                         hipStream_t stream);
 
 }  // namespace viso

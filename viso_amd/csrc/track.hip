@@ -27,6 +27,58 @@ struct LkResult {
     bool succ;
 };
 
+// Per-wave LDS window of the current image around the patch's starting
+// position.  A sample whose four taps lie inside the window (which itself
+// lies inside the image, so no tap wraps a row or leaves the buffer) reads
+// the same bytes from LDS; any other sample takes sample_px's global path.
+constexpr int kWinW = 24, kWinH = 24;
+
+struct Window {
+    const uint8_t* lds;  // nullptr: disabled
+    int x0, y0;
+};
+
+__device__ inline Window load_window(uint8_t* lds, const uint8_t* img, int w, int h, double cx,
+                                     double cy) {
+    Window win{nullptr, 0, 0};
+    if (w < kWinW || h < kWinH || !(cx > -1e6 && cx < 1e6 && cy > -1e6 && cy < 1e6)) return win;
+    int x0 = (int)floor(cx) - kWinW / 2 + 1;
+    int y0 = (int)floor(cy) - kWinH / 2 + 1;
+    x0 = min(max(x0, 0), w - kWinW);
+    y0 = min(max(y0, 0), h - kWinH);
+    const int lane = threadIdx.x & 63;
+    for (int e = lane; e < kWinW * kWinH; e += 64) {
+        const int r = e / kWinW, c = e - r * kWinW;
+        lds[e] = img[(size_t)(y0 + r) * w + (x0 + c)];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    win.lds = lds;
+    win.x0 = x0;
+    win.y0 = y0;
+    return win;
+}
+
+// sample_px with the tap fetch served from the window when possible
+__device__ inline double sample_win(const uint8_t* __restrict__ img, int w, int h, double x,
+                                    double y, const Window& win) {
+    const bool finite = (x > -1e9 && x < 1e9 && y > -1e9 && y < 1e9);
+    if (finite && win.lds) {
+        const int ix = (int)x, iy = (int)y;
+        if (ix >= win.x0 && ix + 1 < win.x0 + kWinW && iy >= win.y0 && iy + 1 < win.y0 + kWinH) {
+            const uint8_t* p = win.lds + (iy - win.y0) * kWinW + (ix - win.x0);
+            const double d0 = (double)p[0], d1 = (double)p[1];
+            const double d2 = (double)p[kWinW], d3 = (double)p[kWinW + 1];
+            const double xx = x - floor(x);
+            const double yy = y - floor(y);
+            return double((1 - xx) * (1 - yy) * d0 + xx * (1 - yy) * d1 + (1 - xx) * yy * d2 +
+                          xx * yy * d3);
+        }
+    }
+    return sample_px(img, w, h, x, y);
+}
+
 // One level of the inverse-compositional LK used by both engines.
 //   ref_x/ref_y: template coordinate of THIS lane's pixel (already offset);
 //   cur_x/cur_y: current-image coordinate of this lane's pixel without d;
@@ -35,7 +87,8 @@ template <int MAXIT, bool KLT_BOUNDS>
 __device__ inline LkResult lk_level(const uint8_t* __restrict__ img1, int w1, int h1,
                                     const uint8_t* __restrict__ img2, int w2, int h2,
                                     double ref_x, double ref_y, double cur_x, double cur_y,
-                                    double bx, double by, double dx, double dy, double thresh) {
+                                    double bx, double by, double dx, double dy, double thresh,
+                                    const Window& win) {
     const double hp = 4.0;
     double gx, gy;
     gradient_px(img1, w1, h1, ref_x, ref_y, gx, gy);
@@ -61,7 +114,7 @@ __device__ inline LkResult lk_level(const uint8_t* __restrict__ img1, int w1, in
             succ = false;
             break;
         }
-        const double e = I1 - sample_px(img2, w2, h2, cur_x + dx, cur_y + dy);
+        const double e = I1 - sample_win(img2, w2, h2, cur_x + dx, cur_y + dy, win);
         const double B0 = wave_tree_sum_dpp(-J0 * e);
         const double B1 = wave_tree_sum_dpp(-J1 * e);
         cost = wave_tree_sum_dpp(e * e);
@@ -85,10 +138,12 @@ __global__ __launch_bounds__(256) void klt_kernel(FrameDev ref, FrameDev cur, Py
                                                   float2* __restrict__ kp2,
                                                   uint8_t* __restrict__ success, int n,
                                                   double thresh) {
+    __shared__ uint8_t s_win[4][kWinW * kWinH];
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= n) return;  // wave-uniform
     const int lane = threadIdx.x & 63;
     const int px = (lane >> 3) - 4, py = (lane & 7) - 4;
+    uint8_t* my_win = s_win[threadIdx.x >> 6];
     const float2 k1 = kp1[i];
     float2 k2 = kp2[i];
     // kp2[j].pt *= scales[3]  (saturate_cast<float>(x * 0.125))
@@ -101,9 +156,10 @@ __global__ __launch_bounds__(256) void klt_kernel(FrameDev ref, FrameDev cur, Py
         const double dx0 = (double)(k2.x - kx), dy0 = (double)(k2.y - ky);
         const float fx = kx + (float)px, fy = ky + (float)py;  // float + int
         const int w = g.w[level], h = g.h[level];
+        const Window win = load_window(my_win, cur.l[level], w, h, (double)kx + dx0, (double)ky + dy0);
         LkResult r = lk_level<10, true>(ref.l[level], w, h, cur.l[level], w, h,
                                         (double)fx, (double)fy, (double)fx, (double)fy,
-                                        (double)kx, (double)ky, dx0, dy0, thresh);
+                                        (double)kx, (double)ky, dx0, dy0, thresh, win);
         succ = r.succ;
         k2.x = kx + (float)r.dx;
         k2.y = ky + (float)r.dy;
@@ -119,9 +175,11 @@ __global__ __launch_bounds__(256) void klt_kernel(FrameDev ref, FrameDev cur, Py
 }
 
 __global__ __launch_bounds__(256) void lk_align_kernel(LkAlignArgs a) {
+    __shared__ uint8_t s_win[4][kWinW * kWinH];
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= a.n) return;
     const int lane = threadIdx.x & 63;
+    uint8_t* my_win = s_win[threadIdx.x >> 6];
     const int px = (lane >> 3) - 4, py = (lane & 7) - 4;
     const double P[3] = {a.points[3 * i], a.points[3 * i + 1], a.points[3 * i + 2]};
     const Intrinsics K{a.K[0], a.K[1], a.K[2], a.K[3]};
@@ -170,9 +228,10 @@ __global__ __launch_bounds__(256) void lk_align_kernel(LkAlignArgs a) {
                 const int w = a.g.w[level], h = a.g.h[level];
                 const double rx = bu * s + px, ry = bv * s + py;
                 const double cx = cu * s + px, cy = cv * s + py;
+                const Window win = load_window(my_win, a.cur.l[level], w, h, cu * s, cv * s);
                 LkResult r = lk_level<100, false>(refp.l[level], w, h, a.cur.l[level], w, h, rx,
-                                                  ry, cx,
-                                                  cy, bu * s, bv * s, 0.0, 0.0, a.thresh);
+                                                  ry, cx, cy, bu * s, bv * s, 0.0, 0.0, a.thresh,
+                                                  win);
                 succ = r.succ;
                 cu = cu + r.dx / s;  // pair.uv_cur += V2d{dx/s, dy/s}
                 cv = cv + r.dy / s;
