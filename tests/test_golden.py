@@ -116,24 +116,24 @@ def test_gpu_stages_golden():
     import viso_amd
 
     g = golden()
-    with viso_amd.default_context(160, 120) as ctx:
-        pyr = ctx.pyramid(g["pyr_in"])[0]
-        assert np.array_equal(pyr, g["pyr_out"])
-        for t in (20, 50):
-            xs, ys, sc = ctx.fast(g["fast_in"], t)
-            assert np.array_equal(np.stack([xs, ys, sc], 1), g[f"fast_t{t}"]), t
-        ref, cur = ctx.pyramid(g["klt_ref"])[0], ctx.pyramid(g["klt_cur"])[0]
-        kp2, succ = ctx.klt(ref, cur, 160, 120, g["klt_kp1"], g["klt_kp1"].copy())
-        assert np.array_equal(kp2.view(np.uint32), g["klt_kp2"].view(np.uint32))
-        assert np.array_equal(succ, g["klt_success"])
-        d, s = ctx.stereo_match(g["st_left"], g["st_right"], g["st_xs"], g["st_ys"], 32)
-        assert np.array_equal(d, g["st_disp"]) and np.array_equal(s, g["st_sad"])
-    with viso_amd.default_context(W, H, K=tuple(g["p2d_K"])) as ctx:
-        out = ctx.pose_2d2d(g["p2d_p1"], g["p2d_p2"])
-        assert np.array_equal(out["inliers"], g["p2d_inliers"])
-        st = out["stats"]
-        assert all(st[k] == g["p2d_stats"][k] for k in (0, 1, 2, 4, 5, 6, 7))
-        assert _rel(out["R"], g["p2d_R"]) < 1e-12 and _rel(out["T"], g["p2d_T"]) < 1e-10
+    ctx = viso_amd.default_context(160, 120)
+    pyr = ctx.pyramid(g["pyr_in"])[0]
+    assert np.array_equal(pyr, g["pyr_out"])
+    for t in (20, 50):
+        xs, ys, sc = ctx.fast(g["fast_in"], t)
+        assert np.array_equal(np.stack([xs, ys, sc], 1), g[f"fast_t{t}"]), t
+    ref, cur = ctx.pyramid(g["klt_ref"])[0], ctx.pyramid(g["klt_cur"])[0]
+    kp2, succ = ctx.klt(ref, cur, 160, 120, g["klt_kp1"], g["klt_kp1"].copy())
+    assert np.array_equal(kp2.view(np.uint32), g["klt_kp2"].view(np.uint32))
+    assert np.array_equal(succ, g["klt_success"])
+    d, s = ctx.stereo_match(g["st_left"], g["st_right"], g["st_xs"], g["st_ys"], 32)
+    assert np.array_equal(d, g["st_disp"]) and np.array_equal(s, g["st_sad"])
+    ctx = viso_amd.default_context(W, H, K=tuple(g["p2d_K"]))
+    out = ctx.pose_2d2d(g["p2d_p1"], g["p2d_p2"])
+    assert np.array_equal(out["inliers"], g["p2d_inliers"])
+    st = out["stats"]
+    assert all(st[k] == g["p2d_stats"][k] for k in (0, 1, 2, 4, 5, 6, 7))
+    assert _rel(out["R"], g["p2d_R"]) < 1e-12 and _rel(out["T"], g["p2d_T"]) < 1e-10
 
 
 @pytest.mark.gpu

@@ -10,7 +10,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libviso_amd.so")
+LIB_PATH = os.environ.get("VISO_LIB") or os.path.join(_HERE, "libviso_amd.so")
 
 VISO_OK = 0
 ERRORS = {-1: "VISO_ERR_ARG", -2: "VISO_ERR_HIP", -3: "VISO_ERR_CAPACITY",

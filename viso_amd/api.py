@@ -186,7 +186,7 @@ def default_context(width: int = 640, height: int = 480, device: int = 0, K=None
     K = tuple(K) if K is not None else (517.3, 516.5, 325.1, 249.7)
     key = (device, K)
     c = _ctx_cache.get(key)
-    if c is None:
+    if c is None or c.h is None:  # absent or closed by a caller
         c = Context(default_params(fx=K[0], fy=K[1], cx=K[2], cy=K[3], width=width,
                                    height=height), device=device)
         _ctx_cache[key] = c

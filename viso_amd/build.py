@@ -17,14 +17,20 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
-OBJ = os.path.join(HERE, "_obj")
-LIB = os.path.join(HERE, "libviso_amd.so")
+# VISO_VARIANT=probe builds an instrumented copy (-DVISO_PROBE) next to the
+# product library (libviso_amd_probe.so, objects in _obj_probe); the product
+# path never loads it (viso_amd/_lib.py loads it only when VISO_LIB names it).
+VARIANT = os.environ.get("VISO_VARIANT", "")
+OBJ = os.path.join(HERE, "_obj" + (f"_{VARIANT}" if VARIANT else ""))
+LIB = os.path.join(HERE, "libviso_amd" + (f"_{VARIANT}" if VARIANT else "") + ".so")
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("VISO_OFFLOAD_ARCH", "gfx950")
 
 COMMON = ["-std=c++17", "-O3", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}",
           "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-Wall", "-Wno-unused-function",
           "-Wno-unused-variable", "-Wno-unused-result"]
+if VARIANT == "probe":
+    COMMON.append("-DVISO_PROBE")
 
 
 def _headers():

@@ -123,8 +123,7 @@ int viso_destroy(viso_ctx* c) {
 int viso_synchronize(viso_ctx* c) {
     if (!c) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipStreamSynchronize(c->stream));
-    for (auto s : c->lk_streams)
-        if (s) VISO_HIP_CHECK(hipStreamSynchronize(s));
+    if (c->lk_stream) VISO_HIP_CHECK(hipStreamSynchronize(c->lk_stream));
     return VISO_OK;
 }
 
@@ -255,8 +254,7 @@ int viso_direct_pose(viso_ctx* c, const uint8_t* last_pyr, const uint8_t* cur_py
     PyrGeom g = make_geom(width, height);
     Bump b;
     size_t o_l = b.take(g.bytes), o_c = b.take(g.bytes), o_p = b.take(24 * (size_t)std::max(n, 1)),
-           o_pl = b.take(96), o_pio = b.take(96), o_se3 = b.take(56),
-           o_tp = b.take(direct_scratch_bytes()), o_tg = b.take(4 * 4096);
+           o_pl = b.take(96), o_pio = b.take(96), o_ds = b.take(direct_scratch_bytes());
     int rc = c->scratch_a.ensure(b.off);
     if (rc) return rc;
     char* base = (char*)c->scratch_a.ptr;
@@ -266,21 +264,15 @@ int viso_direct_pose(viso_ctx* c, const uint8_t* last_pyr, const uint8_t* cur_py
         VISO_HIP_CHECK(hipMemcpyAsync(base + o_p, points, 24 * (size_t)n, hipMemcpyHostToDevice, c->stream));
     VISO_HIP_CHECK(hipMemcpyAsync(base + o_pl, pose_last, 96, hipMemcpyHostToDevice, c->stream));
     VISO_HIP_CHECK(hipMemcpyAsync(base + o_pio, pose_io, 96, hipMemcpyHostToDevice, c->stream));
-    DirectScratch ds;
-    ds.tile_part = (double*)(base + o_tp);
-    ds.tile_good = (int*)(base + o_tg);
     const double K[4] = {c->p.fx, c->p.fy, c->p.cx, c->p.cy};
-    double* se3 = (double*)(base + o_se3);
-    launch_se3_from_pose((const double*)(base + o_pio), se3, c->stream);
     {
         TimedRegion t(c->timing, VISO_KERNEL_DIRECT, c->stream);
-        for (int level = kLevels - 1; level >= 0; --level)
-            launch_direct_level(frame_from_base((const uint8_t*)(base + o_l), g),
-                                frame_from_base((const uint8_t*)(base + o_c), g), g, K,
-                                (const double*)(base + o_p), n, (const double*)(base + o_pl), se3,
-                                level, ds, nullptr, c->stream);
+        launch_direct_pose(frame_from_base((const uint8_t*)(base + o_l), g),
+                           frame_from_base((const uint8_t*)(base + o_c), g), g, K,
+                           (const double*)(base + o_p), n, (const double*)(base + o_pl),
+                           (const double*)(base + o_pio), direct_scratch_at(base + o_ds), nullptr,
+                           (double*)(base + o_pio), nullptr, -1, c->stream);
     }
-    launch_se3_to_pose(se3, (double*)(base + o_pio), nullptr, -1, c->stream);
     VISO_HIP_CHECK(hipGetLastError());
     VISO_HIP_CHECK(hipMemcpyAsync(pose_io, base + o_pio, 96, hipMemcpyDeviceToHost, c->stream));
     VISO_HIP_CHECK(hipStreamSynchronize(c->stream));
@@ -315,8 +307,10 @@ int viso_lk_align(viso_ctx* c, const uint8_t* kf_pyrs, const double* kf_poses, i
     for (int j = 0; j < n_kf; ++j) a.kf[j] = frame_from_base((const uint8_t*)(base + o_kf + g.bytes * j), g);
     a.kf_poses = (const double*)(base + o_kp);
     a.n_kf = n_kf;
-    a.cur = frame_from_base((const uint8_t*)(base + o_c), g);
-    a.cur_pose = (const double*)(base + o_cp);
+    a.n_frames = 1;
+    a.frames[0].cur = frame_from_base((const uint8_t*)(base + o_c), g);
+    a.frames[0].pose = (const double*)(base + o_cp);
+    a.out_stride = 0;
     a.points = (const double*)(base + o_p);
     a.n = n;
     a.K[0] = c->p.fx;

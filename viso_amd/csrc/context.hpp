@@ -105,7 +105,7 @@ struct SlotRec {
     const uint8_t* l0 = nullptr;
     bool borrowed = false;
     int refs = 0;
-    int64_t lk_use = -1;  // last LK-alignment launch (on the LK stream) that reads it
+    int64_t lk_use = -1;  // last lk_stream batch that reads it (lk_seq numbering)
 };
 constexpr int kLkRing = 64;
 }  // namespace viso
@@ -152,21 +152,22 @@ struct viso_ctx {
     viso::DevBuf kf_poses;  // kMaxKeyframes x 12
 
     // ---------------- tracking (kRunning)
-    viso::DevBuf se3;           // 7 doubles
-    viso::DevBuf direct_tiles;  // 256 x 28 doubles + 256 ints
+    viso::DevBuf direct_buf;  // direct-pose scratch (kernels.hpp DirectScratch)
     viso::DirectScratch direct{};
     viso::DevBuf direct_stats;  // 4 levels x 50 doubles
-    // LKAlignment only feeds the display (src/viso.cpp:121-135): launch f
-    // runs on lk_streams[f % kLkStreams] (its own output buffer set), after
-    // direct(f), overlapping later frames' direct pose and other LK launches.
-    static constexpr int kLkStreams = 4;
-    viso::DevBuf lk_pair, lk_succ, lk_before, lk_after;  // kLkStreams x kMaxMapPoints
-    hipStream_t lk_streams[kLkStreams] = {};
-    hipEvent_t ev_pose = nullptr;
-    hipEvent_t lk_ring[viso::kLkRing] = {};
-    int64_t lk_seq = 0;
+    // LKAlignment only feeds the display (src/viso.cpp:121-135): tracking
+    // frames queue in lk_pending (slot held) and run as one batched launch
+    // (up to kLkBatch frames) when the ingest call ends; outputs of batch
+    // frame f at row f.  Batches of viso_process_frames_device run on the
+    // context stream after the chunk's direct-pose chain; single-frame calls
+    // use lk_stream so the host's next frame overlaps them.
+    std::vector<int> lk_pending;
+    int lk_last_rows = 0;  // frames in the last launched batch
+    viso::DevBuf lk_pair, lk_succ, lk_before, lk_after;  // kLkBatch x kMaxMapPoints
+    hipStream_t lk_stream = nullptr;
+    hipEvent_t lk_ring[viso::kLkRing] = {};  // recorded after each lk_stream batch
+    int64_t lk_seq = 0;                      // lk_stream batches launched
     viso::DevBuf pose_log;  // max_poses x 12
-    viso::DevBuf pose_count;
     int n_poses = 0;
 
     // ---------------- state (include/viso.h:44)
@@ -189,4 +190,6 @@ struct viso_ctx {
     // OnNewFrame on a frame whose pyramid is already built in `slot`
     int on_new_frame(int slot);
     int ingest_host(const uint8_t* grey, int32_t w, int32_t h, int32_t stride, int* slot_out);
+    // launch LKAlignment of every pending tracking frame (on `s`)
+    int flush_lk(hipStream_t s);
 };

@@ -2,39 +2,72 @@
 // (DirectPoseEstimationSingleLayer / MultiLayer + dPixeldXi,
 // src/viso.cpp:640-766).
 //
-// One level = two launches:
-//  1. direct_tiles_kernel (8 waves): one wave per map point at a time, lane =
-//     patch pixel.  The wave forms J = -grad^T * dPixel/dXi for its 64 pixels
-//     and reduces the 28 sums (21 upper-triangle J J^T, 6 -e J, e^2) with the
-//     canonical DPP wave tree.  A workgroup owns an aligned tile of
-//     T = max(8, P/256) points (P = next pow2 of the point count), so there
-//     are at most 256 tiles; the tile's 28 sums are a tree over its points,
-//     stored tile-major.
-//  2. direct_solve_kernel (one workgroup): thread t loads tile t's 28 sums in
-//     one burst; canonical tree over tiles (DPP wave tree, then the 4 waves);
-//     PartialPivLU of H on one lane, the six inverse columns on six lanes
-//     (column-oriented forward/backward substitution), update rows on six
-//     lanes, SE3::exp(update) * T21, cost / nGood and the checks of :741-753.
-// The sum order is the canonical pairwise tree over (point, pixel), so the
-// result is independent of the launch geometry and equal to the oracle's.
+// One frame = five launches on one stream:
+//   L(3), L(2), L(1), L(0), F
+// L(l) (one workgroup of 8 waves per tile):
+//   prologue — every workgroup solves level l+1 from that level's tile
+//     partials (written by L(l+1)) and gets T21 for level l.  All workgroups
+//     compute the same bits, so no grid-wide hand-off is needed beyond the
+//     kernel boundary.  L(3) instead seeds T21 = SE3(R, t) of the last
+//     frame's pose (src/viso.cpp:114).
+//     Work that does not depend on T21 is issued first: the tile partial
+//     loads of level l+1, the wave's map point, its projection into the last
+//     frame and the `last` patch sample.
+//   tiles — one wave per map point, lane = patch pixel: J = -grad^T *
+//     dPixel/dXi, the 28 sums (21 upper-triangle J J^T, 6 -e J, e^2) by
+//     reduce-scatter (the canonical wave tree, common.hpp).  A workgroup owns
+//     an aligned tile of T = max(8, P/256) points (P = next pow2 of the point
+//     count), so there are at most 256 tiles; the tile's 28 sums are a tree
+//     over its points, stored tile-major per level.
+// F (one workgroup): solves level 0 and writes the pose (+ pose log).
+//
+// The solve (one level, one workgroup): tile t's partials in thread t, a
+// canonical tree over the tiles (reduce-scatter per wave, then the 4 waves);
+// then on wave 0 alone: Eigen PartialPivLU of H with one lane per matrix
+// element, the inverse by column-parallel forward / backward substitution
+// (one lane per element), update = H^-1 b, SE3::exp(update) * T21 (sin/cos
+// of theta/2 and theta in two lanes at once), cost / nGood and the checks of
+// :741-753.  Every element sees the same operations in the same order as the
+// sequential oracle, so the result is bit-identical.
 // As shipped the loop takes exactly one GN step per level (cost is never
 // reset, src/viso.cpp:673); the rare continuation (a level
-// whose photometric cost is exactly 0) is executed faithfully by the solve
-// workgroup itself, re-running every tile.
-// Frame-level fusions: level 3 seeds T21 = SE3(last R, last t)
-// (src/viso.cpp:114) inside both kernels; level 0's solve writes
-// cur_frame R,t and appends the pose log (src/viso.cpp:117-118, 137).
+// whose photometric cost is exactly 0) is executed faithfully by each
+// workgroup on its own, re-evaluating every tile into private scratch.
 #include "device_math.hpp"
 #include "kernels.hpp"
+
+// Phase probes (build with VISO_VARIANT=probe; tools/probe_direct.py): block
+// 0, thread 0 accumulates s_memrealtime (100 MHz) deltas from kernel entry
+// and records absolute entry/exit stamps of the last frame's launches.
+#ifdef VISO_PROBE
+__device__ unsigned long long g_probe[128];
+#define PROBE_T0() const unsigned long long probe_t0 = __builtin_amdgcn_s_memrealtime()
+#define PROBE(i)                                                                        \
+    do {                                                                                \
+        if (threadIdx.x == 0 && blockIdx.x == 0)                                        \
+            g_probe[(i)] += __builtin_amdgcn_s_memrealtime() - probe_t0;                \
+    } while (0)
+#define PROBE_ABS(i)                                                                    \
+    do {                                                                                \
+        if (threadIdx.x == 0 && blockIdx.x == 0) g_probe[(i)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define PROBE_T0()
+#define PROBE(i)
+#define PROBE_ABS(i)
+#endif
 
 namespace viso {
 
 namespace {
 
 constexpr int kSums = 28;
-constexpr int kWaves = 8;         // waves per tiles workgroup
+constexpr int kWaves = 8;  // waves per workgroup
+constexpr int kThreads = kWaves * 64;
 constexpr int kMaxTiles = 256;
 constexpr int kMaxTile = kMaxMapPoints / kMaxTiles;  // 64 points
+constexpr int kStats = 50;
+constexpr int kStateStride = 8;
 
 struct DirectArgs {
     FrameDev last;
@@ -43,16 +76,14 @@ struct DirectArgs {
     Intrinsics K;
     const double* points;
     int n;
-    const double* pose_last;
-    double* se3;  // 7 doubles in/out
-    int seed_from_last;
-    int level;
-    int tile;     // points per tile (power of two, >= kWaves)
-    int n_tiles;  // <= 256
-    double* tile_part;  // tile-major [tile][28]
-    int* tile_good;
-    double* stats;
-    double* pose_out;  // level 0: cur pose (12)
+    const double* pose_last;  // `last` frame pose: patch reference (12)
+    const double* pose_seed;  // level 3 starts at SE3(R, t) of this pose (12)
+    int level;                // tiles of this level; -1: final solve only
+    int tile;                 // points per tile (power of two, >= kWaves)
+    int n_tiles;              // <= 256
+    DirectScratch s;
+    double* stats;     // [kLevels][kStats] or null
+    double* pose_out;  // result pose (12) or null
     double* log;
     int log_index;  // < 0: no log append
 };
@@ -82,28 +113,46 @@ __device__ inline void d_pixel_d_xi(const Intrinsics& K, const double* pose, con
     J[11] = fy * x / z;
 }
 
-// The 28 sums of one map point by reduce-scatter: returns good; lane l < 32
-// with *idx >= 0 holds sum *idx in *out.
-__device__ inline bool direct_point_rs(const DirectArgs& a, const double* cur_pose, int i,
-                                       double* out, int* idx) {
+// The part of one map point that does not depend on T21: the point, its
+// projection into the last frame (src/viso.cpp:697) and the `last` sample.
+struct RefSample {
+    double P[3];
+    double ur, vr;
+    double lval;
+    bool ok;
+};
+
+__device__ inline void ref_sample(const DirectArgs& a, int lv, int i, RefSample& r) {
     const int lane = threadIdx.x & 63;
     const int px = (lane >> 3) - 4, py = (lane & 7) - 4;
-    const int l = a.level;
-    const double scale = kScale[l];
-    const int w = a.g.w[l], h = a.g.h[l];
-    const double P[3] = {a.points[3 * i], a.points[3 * i + 1], a.points[3 * i + 2]};
-    double ur, vr, uc, vc;
-    project_px(a.pose_last, a.K, P, scale, ur, vr);
-    project_px(cur_pose, a.K, P, scale, uc, vc);
+    const double scale = kScale[lv];
+    const int w = a.g.w[lv], h = a.g.h[lv];
+    r.P[0] = a.points[3 * i];
+    r.P[1] = a.points[3 * i + 1];
+    r.P[2] = a.points[3 * i + 2];
+    project_px(a.pose_last, a.K, r.P, scale, r.ur, r.vr);
     const double hp = 4.0;
-    const bool good = inside_px(ur - hp, vr - hp, w, h) && inside_px(ur + hp, vr + hp, w, h) &&
-                      inside_px(uc - hp, vc - hp, w, h) && inside_px(uc + hp, vc + hp, w, h);
+    r.ok = inside_px(r.ur - hp, r.vr - hp, w, h) && inside_px(r.ur + hp, r.vr + hp, w, h);
+    r.lval = r.ok ? sample_px(a.last.l[lv], w, h, r.ur + px, r.vr + py) : 0.0;
+}
+
+// The 28 sums of one map point by reduce-scatter: returns good; lane l < 32
+// with *idx >= 0 holds sum *idx in *out.
+__device__ inline bool direct_point_rs(const DirectArgs& a, int lv, const double* cur_pose,
+                                       const RefSample& r, double* out, int* idx) {
+    const int lane = threadIdx.x & 63;
+    const int px = (lane >> 3) - 4, py = (lane & 7) - 4;
+    const double scale = kScale[lv];
+    const int w = a.g.w[lv], h = a.g.h[lv];
+    double uc, vc;
+    project_px(cur_pose, a.K, r.P, scale, uc, vc);
+    const double hp = 4.0;
+    const bool good = r.ok && inside_px(uc - hp, vc - hp, w, h) && inside_px(uc + hp, vc + hp, w, h);
     if (!good) return false;
     double Jp[12];
-    d_pixel_d_xi(a.K, cur_pose, P, scale, Jp);
-    const uint8_t* L = a.last.l[l];
-    const uint8_t* C = a.cur.l[l];
-    const double error = sample_px(L, w, h, ur + px, vr + py) - sample_px(C, w, h, uc + px, vc + py);
+    d_pixel_d_xi(a.K, cur_pose, r.P, scale, Jp);
+    const uint8_t* C = a.cur.l[lv];
+    const double error = r.lval - sample_px(C, w, h, uc + px, vc + py);
     double g0, g1;
     gradient_px(C, w, h, uc + px, vc + py, g0, g1);
     double J[6];
@@ -112,9 +161,9 @@ __device__ inline bool direct_point_rs(const DirectArgs& a, const double* cur_po
     double leaf[kSums];
     int e = 0;
 #pragma unroll
-    for (int r = 0; r < 6; ++r)
+    for (int rr = 0; rr < 6; ++rr)
 #pragma unroll
-        for (int c = r; c < 6; ++c) leaf[e++] = J[r] * J[c];
+        for (int c = rr; c < 6; ++c) leaf[e++] = J[rr] * J[c];
 #pragma unroll
     for (int k = 0; k < 6; ++k) leaf[21 + k] = -error * J[k];
     leaf[27] = error * error;
@@ -122,56 +171,47 @@ __device__ inline bool direct_point_rs(const DirectArgs& a, const double* cur_po
     return true;
 }
 
-// The 28 sums of one map point (wave-wide; identical in every lane).
-__device__ inline bool direct_point(const DirectArgs& a, const double* cur_pose, int i,
-                                    double* s) {
-    const int lane = threadIdx.x & 63;
-    const int px = (lane >> 3) - 4, py = (lane & 7) - 4;
-    const int l = a.level;
-    const double scale = kScale[l];
-    const int w = a.g.w[l], h = a.g.h[l];
-    const double P[3] = {a.points[3 * i], a.points[3 * i + 1], a.points[3 * i + 2]};
-    double ur, vr, uc, vc;
-    project_px(a.pose_last, a.K, P, scale, ur, vr);
-    project_px(cur_pose, a.K, P, scale, uc, vc);
-    const double hp = 4.0;
-    const bool good = inside_px(ur - hp, vr - hp, w, h) && inside_px(ur + hp, vr + hp, w, h) &&
-                      inside_px(uc - hp, vc - hp, w, h) && inside_px(uc + hp, vc + hp, w, h);
-    if (!good) return false;
-    double Jp[12];
-    d_pixel_d_xi(a.K, cur_pose, P, scale, Jp);
-    const uint8_t* L = a.last.l[l];
-    const uint8_t* C = a.cur.l[l];
-    const double error = sample_px(L, w, h, ur + px, vr + py) - sample_px(C, w, h, uc + px, vc + py);
-    double g0, g1;
-    gradient_px(C, w, h, uc + px, vc + py, g0, g1);
-    double J[6];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) J[k] = -g0 * Jp[k] + -g1 * Jp[6 + k];
-    int idx = 0;
-#pragma unroll
-    for (int r = 0; r < 6; ++r)
-#pragma unroll
-        for (int c = r; c < 6; ++c) s[idx++] = wave_tree_sum_dpp(J[r] * J[c]);
-#pragma unroll
-    for (int k = 0; k < 6; ++k) s[21 + k] = wave_tree_sum_dpp(-error * J[k]);
-    s[27] = wave_tree_sum_dpp(error * error);
-    return true;
-}
-
-// T21 at the start of this launch: the running state, or SE3(R, t) of the
-// last frame's pose for the first level (Sophus::SE3d(R, t): R -> quaternion)
-__device__ inline void start_state(const DirectArgs& a, double* st) {
-    if (a.seed_from_last) {
-        double q[4];
-        quat_from_matrix(a.pose_last, q);
-        for (int k = 0; k < 4; ++k) st[k] = q[k];
-        st[4] = a.pose_last[9];
-        st[5] = a.pose_last[10];
-        st[6] = a.pose_last[11];
-    } else {
-        for (int k = 0; k < 7; ++k) st[k] = a.se3[k];
+// Tile b of level lv (a.tile points) -> part[b][28], good[b].  Called by
+// every thread of the workgroup.  `pre` (may be null) is the prefetched
+// RefSample of this wave's first point of the tile (valid when has_pre).
+__device__ void direct_tile(const DirectArgs& a, int lv, const double* cur_pose, int b,
+                            const RefSample& pre, bool has_pre, double* part, int* good,
+                            double* s_pts, int* s_good) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int T = a.tile;
+    if (threadIdx.x == 0) *s_good = 0;
+    __syncthreads();
+    int good_cnt = 0;
+    for (int local = wave; local < T; local += kWaves) {
+        const int i = b * T + local;
+        double f = 0.0;
+        int idx = -1;
+        bool ok = false;
+        if (i < a.n) {
+            RefSample r;
+            if (has_pre && local == wave)
+                r = pre;
+            else
+                ref_sample(a, lv, i, r);
+            ok = direct_point_rs(a, lv, cur_pose, r, &f, &idx);
+        }
+        if (!ok) {
+            if (lane < kSums) s_pts[local * kSums + lane] = 0.0;
+        } else if (lane < 32 && idx >= 0) {
+            s_pts[local * kSums + idx] = f;
+        }
+        good_cnt += ok ? 1 : 0;
     }
+    if (lane == 0 && good_cnt) atomicAdd(s_good, good_cnt);
+    __syncthreads();
+    // tree over the tile's T points (lanes >= T hold +0.0)
+    for (int k = wave; k < kSums; k += kWaves) {
+        const double v = lane < T ? s_pts[lane * kSums + k] : 0.0;
+        const double r = wave_tree_sum_dpp(v);
+        if (lane == 0) part[(size_t)b * kSums + k] = r;
+    }
+    if (threadIdx.x == 0) good[b] = *s_good;
+    __syncthreads();
 }
 
 __device__ inline void state_to_pose(const double* st, double* pose) {
@@ -182,262 +222,329 @@ __device__ inline void state_to_pose(const double* st, double* pose) {
     pose[11] = st[6];
 }
 
-// Tile b (a.tile points): 28 sums -> tile_part[b], good count -> tile_good[b].
-// Called by every thread of a workgroup of `nwaves` waves.
-__device__ void direct_tile(const DirectArgs& a, const double* cur_pose, int b, int nwaves,
-                            double* s_pts, int* s_good) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int T = a.tile;
-    if (threadIdx.x == 0) *s_good = 0;
-    __syncthreads();
-    int good_cnt = 0;
-    for (int local = wave; local < T; local += nwaves) {
-        const int i = b * T + local;
-        double f = 0.0;
-        int idx = -1;
-        bool good = false;
-        if (i < a.n) good = direct_point_rs(a, cur_pose, i, &f, &idx);
-        if (!good) {
-            if (lane < kSums) s_pts[local * kSums + lane] = 0.0;
-        } else if (lane < 32 && idx >= 0) {
-            s_pts[local * kSums + idx] = f;
-        }
-        good_cnt += good ? 1 : 0;
-    }
-    if (lane == 0 && good_cnt) atomicAdd(s_good, good_cnt);
-    __syncthreads();
-    // tree over the tile's T points (lanes >= T hold +0.0)
-    for (int k = wave; k < kSums; k += nwaves) {
-        const double v = lane < T ? s_pts[lane * kSums + k] : 0.0;
-        const double r = wave_tree_sum_dpp(v);
-        if (lane == 0) a.tile_part[(size_t)b * kSums + k] = r;
-    }
-    if (threadIdx.x == 0) a.tile_good[b] = *s_good;
-    __syncthreads();
-}
+// ---------------------------------------------------------------- solve
+struct SolveLds {
+    double red[4][kSums];
+    double S[kSums];
+    int g[4];
+    int ngood;
+    double state[kStateStride], best[kStateStride];
+    double cost, last_cost;
+    int cont;
+};
 
-__global__ __launch_bounds__(kWaves * 64) void direct_tiles_kernel(DirectArgs a) {
-    __shared__ double s_pose[12];
-    __shared__ double s_pts[kMaxTile * kSums];
-    __shared__ int s_good;
-    if (threadIdx.x == 0) {
-        double st[7];
-        start_state(a, st);
-        state_to_pose(st, s_pose);
-    }
-    __syncthreads();
-    double pose[12];
-#pragma unroll
-    for (int k = 0; k < 12; ++k) pose[k] = s_pose[k];
-    direct_tile(a, pose, blockIdx.x, kWaves, s_pts, &s_good);
-}
-
-// Canonical tree over <= 256 tiles: thread t holds tile t (zeros beyond).
-__device__ void reduce_tiles(const DirectArgs& a, double* S, int* n_good, double* s_red,
-                             int* s_g) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+// Thread t < 256 loads tile t's partials (zeros beyond n_tiles).
+__device__ inline void load_partials(const double* __restrict__ part, const int* __restrict__ good,
+                                     int n_tiles, double* v, int& gg) {
     const int t = threadIdx.x;
-    double v[kSums];
-    if (t < a.n_tiles) {
-        const double2* src = reinterpret_cast<const double2*>(a.tile_part + (size_t)t * kSums);
+    if (t < n_tiles) {
+        const double2* src = reinterpret_cast<const double2*>(part + (size_t)t * kSums);
 #pragma unroll
         for (int k = 0; k < kSums / 2; ++k) {
             const double2 d = src[k];
             v[2 * k] = d.x;
             v[2 * k + 1] = d.y;
         }
+        gg = good[t];
     } else {
 #pragma unroll
         for (int k = 0; k < kSums; ++k) v[k] = 0.0;
+        gg = 0;
     }
-    int g = t < a.n_tiles ? a.tile_good[t] : 0;
-#pragma unroll
-    for (int k = 0; k < kSums; ++k) {
-        const double r = wave_tree_sum_dpp(v[k]);
-        if (lane == 0) s_red[wave * kSums + k] = r;
+}
+
+// Canonical tree over <= 256 tiles (thread t holds tile t) -> L.S, L.ngood.
+__device__ inline void reduce_partials(const double* v, int gg, SolveLds& L) {
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+    if (t < 256) {
+        int idx;
+        const double f = reduce_scatter_28(v, &idx);
+        if (lane < 32 && idx >= 0) L.red[wave][idx] = f;
+        const int g = wave_sum_int(gg);
+        if (lane == 0) L.g[wave] = g;
     }
-    g = wave_sum_int(g);
-    if (lane == 0) s_g[wave] = g;
     __syncthreads();
-    if (threadIdx.x < kSums) {
-        const int k = threadIdx.x;
-        S[k] = (s_red[0 * kSums + k] + s_red[1 * kSums + k]) + (s_red[2 * kSums + k] + s_red[3 * kSums + k]);
-    }
-    if (threadIdx.x == 0) *n_good = (s_g[0] + s_g[1]) + (s_g[2] + s_g[3]);
+    if (t < kSums) L.S[t] = (L.red[0][t] + L.red[1][t]) + (L.red[2][t] + L.red[3][t]);
+    if (t == 0) L.ngood = (L.g[0] + L.g[1]) + (L.g[2] + L.g[3]);
     __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void direct_solve_kernel(DirectArgs a) {
-    __shared__ double s_red[4 * kSums];
-    __shared__ double S[kSums];
-    __shared__ int s_ngood;
-    __shared__ int s_g[4];
-    __shared__ double s_pose[12];
-    __shared__ double s_pts[kMaxTile * kSums];
-    __shared__ int s_good;
-    __shared__ int s_continue;
-    __shared__ double s_state[7], s_best[7];
-    __shared__ double s_cost, s_lastCost;
-    __shared__ double s_lu[36], s_inv[36], s_upd[6];
-    __shared__ int s_tr[6];
-    if (threadIdx.x == 0) {
-        start_state(a, s_state);
-        for (int k = 0; k < 7; ++k) s_best[k] = s_state[k];
-        s_cost = 0.0;
-        s_lastCost = 0.0;
+__device__ inline double shfl_f64(double v, int src) { return __shfl(v, src, 64); }
+
+// One GN step of one level on wave 0 (all 64 lanes): L.S -> update, the new
+// L.state and the loop decision L.cont (src/viso.cpp:731-753).
+__device__ void solve_wave0(SolveLds& L, int iter, double* stats) {
+    const int lane = threadIdx.x & 63;
+    const int row = lane / 6, col = lane - 6 * (lane / 6);
+    const bool in = lane < 36;
+    // H (symmetric) from the 21 upper-triangle sums, one element per lane
+    const int r0 = row < col ? row : col, c0 = row < col ? col : row;
+    const double h = in ? L.S[r0 * 6 - (r0 * (r0 - 1)) / 2 + (c0 - r0)] : 0.0;
+    // ---- Eigen PartialPivLU (first maximal |pivot| wins)
+    double v = h;
+    int tr[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        int p = k;
+        double best = fabs(readlane_f64(v, 7 * k));
+#pragma unroll
+        for (int i = k + 1; i < 6; ++i) {
+            const double s = fabs(readlane_f64(v, 6 * i + k));
+            if (s > best) {
+                best = s;
+                p = i;
+            }
+        }
+        tr[k] = p;
+        if (best != 0.0) {
+            if (p != k) {
+                const double vk = shfl_f64(v, 6 * k + col);
+                const double vp = shfl_f64(v, 6 * p + col);
+                if (row == k) v = vp;
+                else if (row == p) v = vk;
+            }
+            const double piv = readlane_f64(v, 7 * k);
+            if (in && row > k && col == k) v = v / piv;
+        }
+        const double lik = shfl_f64(v, (6 * row + k) & 63);
+        const double ukj = shfl_f64(v, 6 * k + col);
+        if (in && row > k && col > k) v = v - lik * ukj;
     }
-    __syncthreads();
-    for (int iter = 0; iter < 100; ++iter) {
-        if (iter > 0) {
-            // continuation (faithful, rare): this workgroup recomputes every tile
-            if (threadIdx.x == 0) state_to_pose(s_state, s_pose);
-            __syncthreads();
-            double pose[12];
-            for (int k = 0; k < 12; ++k) pose[k] = s_pose[k];
-            for (int b = 0; b < a.n_tiles; ++b) direct_tile(a, pose, b, 4, s_pts, &s_good);
-            __threadfence_block();
-            __syncthreads();
+    // ---- inverse: lane (row, col) holds X[row][col], X = P * I then
+    // forward (unit L) and backward (U) substitution per column
+    int pos = col;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        if (pos == k) pos = tr[k];
+        else if (pos == tr[k]) pos = k;
+    }
+    double x = (row == pos) ? 1.0 : 0.0;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        const double xj = shfl_f64(x, 6 * j + col);
+        const double lij = shfl_f64(v, (6 * row + j) & 63);
+        if (in && row > j) x = x - lij * xj;
+    }
+#pragma unroll
+    for (int j = 5; j >= 0; --j) {
+        const double ujj = readlane_f64(v, 7 * j);
+        if (in && row == j) x = x / ujj;
+        const double xj = shfl_f64(x, 6 * j + col);
+        const double uij = shfl_f64(v, (6 * row + j) & 63);
+        if (in && row < j) x = x - uij * xj;
+    }
+    // ---- update = H^-1 * b (row-wise, ascending columns)
+    double update[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+        double s = readlane_f64(x, 6 * r) * L.S[21];
+#pragma unroll
+        for (int c = 1; c < 6; ++c) s = s + readlane_f64(x, 6 * r + c) * L.S[21 + c];
+        update[r] = s;
+    }
+    // ---- SE3::exp(update) (Sophus), sin/cos of theta/2 and theta in lanes 0/1
+    SE3d E;
+    {
+        const double eps = 1e-10;
+        const double* w = update + 3;
+        const double theta_sq = (w[0] * w[0] + w[1] * w[1]) + w[2] * w[2];
+        const double theta = sqrt(theta_sq);
+        const double half_theta = 0.5 * theta;
+        double sn, cs;
+        sincos((lane & 1) ? theta : half_theta, &sn, &cs);
+        const double s_half = readlane_f64(sn, 0), c_half = readlane_f64(cs, 0);
+        const double s_th = readlane_f64(sn, 1), c_th = readlane_f64(cs, 1);
+        double imag, real;
+        if (theta < eps) {
+            const double theta_po4 = theta_sq * theta_sq;
+            imag = 0.5 - (1.0 / 48.0) * theta_sq + (1.0 / 3840.0) * theta_po4;
+            real = 1.0 - 0.5 * theta_sq + (1.0 / 384.0) * theta_po4;
+        } else {
+            imag = s_half / theta;
+            real = c_half;
         }
-        reduce_tiles(a, S, &s_ngood, s_red, s_g);
-        // ---- H.inverse() (Eigen PartialPivLU): factor on lane 0 ...
-        if (threadIdx.x == 0) {
-            double lu[36];
-            int idx = 0;
-            for (int r = 0; r < 6; ++r)
-                for (int c = r; c < 6; ++c) {
-                    lu[6 * r + c] = S[idx];
-                    lu[6 * c + r] = S[idx];
-                    ++idx;
-                }
-            for (int k = 0; k < 6; ++k) {
-                int p = k;
-                double best = fabs(lu[6 * k + k]);
-                for (int i = k + 1; i < 6; ++i) {
-                    const double s = fabs(lu[6 * i + k]);
-                    if (s > best) {
-                        best = s;
-                        p = i;
-                    }
-                }
-                s_tr[k] = p;
-                if (best != 0.0) {
-                    if (p != k)
-                        for (int j = 0; j < 6; ++j) {
-                            const double tmp = lu[6 * k + j];
-                            lu[6 * k + j] = lu[6 * p + j];
-                            lu[6 * p + j] = tmp;
-                        }
-                    for (int i = k + 1; i < 6; ++i) lu[6 * i + k] = lu[6 * i + k] / lu[6 * k + k];
-                }
-                for (int i = k + 1; i < 6; ++i)
-                    for (int j = k + 1; j < 6; ++j) lu[6 * i + j] = lu[6 * i + j] - lu[6 * i + k] * lu[6 * k + j];
+        E.q[0] = imag * w[0];
+        E.q[1] = imag * w[1];
+        E.q[2] = imag * w[2];
+        E.q[3] = real;
+        double V[9];
+        if (theta < eps) {
+            quat_to_matrix(E.q, V);
+        } else {
+            const double O[9] = {0.0, -w[2], w[1], w[2], 0.0, -w[0], -w[1], w[0], 0.0};
+            double O2[9];
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j)
+                    O2[3 * i + j] = (O[3 * i + 0] * O[0 + j] + O[3 * i + 1] * O[3 + j]) + O[3 * i + 2] * O[6 + j];
+            const double th2 = theta * theta;
+            const double c1 = (1.0 - c_th) / th2;
+            const double c2 = (theta - s_th) / (th2 * theta);
+#pragma unroll
+            for (int i = 0; i < 9; ++i) {
+                const double id = (i % 4 == 0) ? 1.0 : 0.0;
+                V[i] = (id + c1 * O[i]) + c2 * O2[i];
             }
-            for (int e = 0; e < 36; ++e) s_lu[e] = lu[e];
         }
-        __syncthreads();
-        // ... one lane per column: X = P*I, forward (unit L), backward (U)
-        if (threadIdx.x < 6) {
-            const int c = threadIdx.x;
-            double x[6];
-            for (int i = 0; i < 6; ++i) x[i] = (i == c) ? 1.0 : 0.0;
-            for (int k = 0; k < 6; ++k) {
-                const int p = s_tr[k];
-                if (p != k) {
-                    const double tmp = x[k];
-                    x[k] = x[p];
-                    x[p] = tmp;
-                }
-            }
-            for (int j = 0; j < 6; ++j)
-                for (int i = j + 1; i < 6; ++i) x[i] = x[i] - s_lu[6 * i + j] * x[j];
-            for (int j = 5; j >= 0; --j) {
-                x[j] = x[j] / s_lu[6 * j + j];
-                for (int i = 0; i < j; ++i) x[i] = x[i] - s_lu[6 * i + j] * x[j];
-            }
-            for (int i = 0; i < 6; ++i) s_inv[6 * i + c] = x[i];
+        mat3_vec(V, update, E.t);
+    }
+    SE3d T21;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) T21.q[k] = L.state[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) T21.t[k] = L.state[4 + k];
+    T21 = se3_mul(E, T21);
+    const int ngood = L.ngood;
+    double cost = L.cost + L.S[27];
+    cost /= ngood;
+    const double lastCost = L.last_cost;
+    if (stats) {
+        if (in) stats[2 + lane] = h;
+        if (lane == 0) {
+            stats[0] = ngood;
+            stats[1] = cost;
+            for (int k = 0; k < 6; ++k) stats[38 + k] = L.S[21 + k];
+            for (int k = 0; k < 6; ++k) stats[44 + k] = update[k];
         }
-        __syncthreads();
-        // update = H^-1 * b, one lane per row
-        if (threadIdx.x < 6) {
-            const int r = threadIdx.x;
-            double s = s_inv[6 * r] * S[21];
-            for (int c = 1; c < 6; ++c) s = s + s_inv[6 * r + c] * S[21 + c];
-            s_upd[r] = s;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            double update[6];
-            for (int k = 0; k < 6; ++k) update[k] = s_upd[k];
-            double cost = s_cost + S[27];
-            SE3d T21;
-            for (int k = 0; k < 4; ++k) T21.q[k] = s_state[k];
-            for (int k = 0; k < 3; ++k) T21.t[k] = s_state[4 + k];
-            T21 = se3_mul(se3_exp(update), T21);
-            for (int k = 0; k < 4; ++k) s_state[k] = T21.q[k];
-            for (int k = 0; k < 3; ++k) s_state[4 + k] = T21.t[k];
-            cost /= s_ngood;
-            const double lastCost = s_lastCost;
-            if (a.stats) {
-                a.stats[0] = s_ngood;
-                a.stats[1] = cost;
-                int idx = 0;
-                for (int r = 0; r < 6; ++r)
-                    for (int c = r; c < 6; ++c) {
-                        a.stats[2 + 6 * r + c] = S[idx];
-                        a.stats[2 + 6 * c + r] = S[idx];
-                        ++idx;
-                    }
-                for (int k = 0; k < 6; ++k) a.stats[38 + k] = S[21 + k];
-                for (int k = 0; k < 6; ++k) a.stats[44 + k] = update[k];
-            }
-            int cont = 1;
-            if (isnan(update[0])) {
-                for (int k = 0; k < 7; ++k) s_state[k] = s_best[k];
-                cont = 0;
-            } else if (iter > 0 && cost > lastCost) {
-                for (int k = 0; k < 7; ++k) s_state[k] = s_best[k];
+    }
+    if (lane == 0) {
+        int cont = 1;
+        if (isnan(update[0])) {
+            for (int k = 0; k < 7; ++k) L.state[k] = L.best[k];
+            cont = 0;
+        } else {
+            for (int k = 0; k < 4; ++k) L.state[k] = T21.q[k];
+            for (int k = 0; k < 3; ++k) L.state[4 + k] = T21.t[k];
+            if (iter > 0 && cost > lastCost) {
+                for (int k = 0; k < 7; ++k) L.state[k] = L.best[k];
                 cont = 0;
             } else if ((1 - cost / (double)lastCost) < 0.005) {
                 cont = 0;
             } else {
-                for (int k = 0; k < 7; ++k) s_best[k] = s_state[k];
-                s_lastCost = cost;
+                for (int k = 0; k < 7; ++k) L.best[k] = L.state[k];
+                L.last_cost = cost;
             }
-            s_cost = cost;
-            s_continue = cont;
         }
-        __syncthreads();
-        if (!s_continue) break;
+        L.cost = cost;
+        L.cont = cont;
     }
-    if (threadIdx.x == 0) {
-        for (int k = 0; k < 7; ++k) a.se3[k] = s_state[k];
-        if (a.pose_out) {
+}
+
+// Continuation (faithful, rare): this workgroup re-evaluates every tile of
+// level lv at T21 = state into its own scratch.  Out of line: it keeps the
+// common path's register allocation small.
+__device__ void continue_tiles(const DirectArgs& a, int lv,
+                                                         const double* state, double* s_pose,
+                                                         double* s_pts, int* s_good) {
+    double* part = a.s.cont_part + (size_t)blockIdx.x * kMaxTiles * kSums;
+    int* good = a.s.cont_good + (size_t)blockIdx.x * kMaxTiles;
+    if (threadIdx.x == 0) state_to_pose(state, s_pose);
+    __syncthreads();
+    double pose[12];
+    for (int k = 0; k < 12; ++k) pose[k] = s_pose[k];
+    RefSample none{};
+    for (int b = 0; b < a.n_tiles; ++b)
+        direct_tile(a, lv, pose, b, none, false, part, good, s_pts, s_good);
+    __threadfence_block();
+    __syncthreads();
+}
+
+// The GN loop of level lv on its tile partials (thread t < 256 already holds
+// tile t's in v / gg); L.state holds the T21 the tiles were evaluated at and
+// is left holding the level's result.
+__device__ void solve_level(const DirectArgs& a, int lv, SolveLds& L, double* v, int gg,
+                            double* stats, double* s_pose, double* s_pts, int* s_good) {
+    const int t = threadIdx.x, wave = t >> 6;
+    if (t == 0) {
+        for (int k = 0; k < 7; ++k) L.best[k] = L.state[k];
+        L.cost = 0.0;
+        L.last_cost = 0.0;
+    }
+    __syncthreads();
+    for (int iter = 0; iter < 100; ++iter) {
+        if (iter > 0) {
+            continue_tiles(a, lv, L.state, s_pose, s_pts, s_good);
+            if (t < 256)
+                load_partials(a.s.cont_part + (size_t)blockIdx.x * kMaxTiles * kSums,
+                              a.s.cont_good + (size_t)blockIdx.x * kMaxTiles, a.n_tiles, v, gg);
+        }
+        reduce_partials(v, gg, L);
+        if (wave == 0) solve_wave0(L, iter, stats);
+        __syncthreads();
+        if (!L.cont) break;
+    }
+}
+
+// L(level) and F (level = -1).
+__global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
+    PROBE_T0();
+    PROBE_ABS(64 + 4 * (a.level + 1));
+    __shared__ SolveLds L;
+    __shared__ double s_pose[12];
+    __shared__ double s_pts[kMaxTile * kSums];
+    __shared__ int s_good;
+    const int lv = a.level;
+    const int prev = lv + 1;  // level solved in the prologue (kLevels: seeded)
+    const int t = threadIdx.x, wave = t >> 6;
+    const bool tiles = lv >= 0 && (int)blockIdx.x < a.n_tiles;
+
+    // ---- independent of T21: partials of `prev`, this wave's point
+    double v[kSums];
+    int gg = 0;
+    if (prev < kLevels && t < 256)
+        load_partials(a.s.part + (size_t)prev * kMaxTiles * kSums, a.s.good + prev * kMaxTiles,
+                      a.n_tiles, v, gg);
+    RefSample pre;
+    const int i0 = (int)blockIdx.x * a.tile + wave;
+    const bool has_pre = tiles && wave < a.tile && i0 < a.n;
+    if (has_pre) ref_sample(a, lv, i0, pre);
+    // ---- T21 the prologue starts from
+    if (t == 0) {
+        if (prev == kLevels) {
+            // Sophus::SE3d(R, t): R -> quaternion
+            double q[4];
+            quat_from_matrix(a.pose_seed, q);
+            for (int k = 0; k < 4; ++k) L.state[k] = q[k];
+            L.state[4] = a.pose_seed[9];
+            L.state[5] = a.pose_seed[10];
+            L.state[6] = a.pose_seed[11];
+        } else {
+            for (int k = 0; k < 7; ++k) L.state[k] = a.s.state[prev * kStateStride + k];
+        }
+    }
+    __syncthreads();
+    if (prev < kLevels) {
+        double* st = (a.stats && blockIdx.x == 0) ? a.stats + (size_t)kStats * prev : nullptr;
+        solve_level(a, prev, L, v, gg, st, s_pose, s_pts, &s_good);
+    }
+    PROBE(lv + 1);
+    const int out = lv >= 0 ? lv : kLevels;
+    if (blockIdx.x == 0 && t == 0) {
+        for (int k = 0; k < 7; ++k) a.s.state[out * kStateStride + k] = L.state[k];
+        if (lv < 0 && a.pose_out) {
             double p[12];
-            state_to_pose(s_state, p);
+            state_to_pose(L.state, p);
             for (int k = 0; k < 12; ++k) a.pose_out[k] = p[k];
             if (a.log && a.log_index >= 0)
                 for (int k = 0; k < 12; ++k) a.log[12 * (size_t)a.log_index + k] = p[k];
         }
     }
-}
-
-__global__ void se3_from_pose_kernel(const double* pose, double* se3) {
-    if (threadIdx.x != 0) return;
-    double q[4];
-    quat_from_matrix(pose, q);
-    for (int k = 0; k < 4; ++k) se3[k] = q[k];
-    se3[4] = pose[9];
-    se3[5] = pose[10];
-    se3[6] = pose[11];
-}
-
-__global__ void se3_to_pose_kernel(const double* se3, double* pose, double* log, int log_index) {
-    if (threadIdx.x != 0) return;
-    double p[12];
-    state_to_pose(se3, p);
-    for (int k = 0; k < 12; ++k) pose[k] = p[k];
-    if (log && log_index >= 0)
-        for (int k = 0; k < 12; ++k) log[12 * (size_t)log_index + k] = p[k];
+    if (tiles) {
+        if (t == 0) state_to_pose(L.state, s_pose);
+        __syncthreads();
+        double pose[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) pose[k] = s_pose[k];
+        direct_tile(a, lv, pose, blockIdx.x, pre, has_pre,
+                    a.s.part + (size_t)lv * kMaxTiles * kSums, a.s.good + lv * kMaxTiles, s_pts,
+                    &s_good);
+    }
+    PROBE(8 + lv + 1);
+    PROBE_ABS(65 + 4 * (a.level + 1));
+#ifdef VISO_PROBE
+    if (threadIdx.x == 0 && blockIdx.x == 0) g_probe[16 + lv + 1] += 1;
+#endif
 }
 
 struct Pose12v {
@@ -456,11 +563,34 @@ void launch_set_pose(double* dst, const double src[12], hipStream_t stream) {
     set_pose_kernel<<<1, 64, 0, stream>>>(dst, p);
 }
 
-void launch_direct_level(const FrameDev& last_pyr, const FrameDev& cur_pyr, const PyrGeom& g,
-                         const double K[4], const double* points, int n,
-                         const double* pose_last12, double* se3_state, int level,
-                         DirectScratch& s, double* stats, hipStream_t stream,
-                         bool seed_from_last, double* pose_out, double* log, int log_index) {
+size_t direct_scratch_bytes() {
+    return (size_t)kLevels * kMaxTiles * kSums * 8 + (size_t)kLevels * kMaxTiles * 4 +
+           (size_t)(kLevels + 1) * kStateStride * 8 + (size_t)kMaxTiles * kMaxTiles * kSums * 8 +
+           (size_t)kMaxTiles * kMaxTiles * 4 + 5 * 256;
+}
+
+DirectScratch direct_scratch_at(void* base) {
+    auto align = [](size_t o) { return (o + 255) & ~(size_t)255; };
+    char* b = (char*)base;
+    size_t o = 0;
+    DirectScratch s;
+    s.part = (double*)(b + o);
+    o = align(o + (size_t)kLevels * kMaxTiles * kSums * 8);
+    s.good = (int*)(b + o);
+    o = align(o + (size_t)kLevels * kMaxTiles * 4);
+    s.state = (double*)(b + o);
+    o = align(o + (size_t)(kLevels + 1) * kStateStride * 8);
+    s.cont_part = (double*)(b + o);
+    o = align(o + (size_t)kMaxTiles * kMaxTiles * kSums * 8);
+    s.cont_good = (int*)(b + o);
+    return s;
+}
+
+void launch_direct_pose(const FrameDev& last_pyr, const FrameDev& cur_pyr, const PyrGeom& g,
+                        const double K[4], const double* points, int n,
+                        const double* pose_last12, const double* pose_seed12,
+                        const DirectScratch& s, double* stats, double* pose_out, double* log,
+                        int log_index, hipStream_t stream) {
     DirectArgs a;
     a.last = last_pyr;
     a.cur = cur_pyr;
@@ -469,32 +599,36 @@ void launch_direct_level(const FrameDev& last_pyr, const FrameDev& cur_pyr, cons
     a.points = points;
     a.n = n;
     a.pose_last = pose_last12;
-    a.se3 = se3_state;
-    a.seed_from_last = seed_from_last ? 1 : 0;
-    a.level = level;
+    a.pose_seed = pose_seed12;
     int P = 1;
     while (P < n) P <<= 1;
     a.tile = P / kMaxTiles > kWaves ? P / kMaxTiles : kWaves;
     a.n_tiles = (n + a.tile - 1) / a.tile;
-    a.tile_part = s.tile_part;
-    a.tile_good = s.tile_good;
+    a.s = s;
     a.stats = stats;
     a.pose_out = pose_out;
     a.log = log;
     a.log_index = log ? log_index : -1;
-    if (a.n_tiles > 0) direct_tiles_kernel<<<a.n_tiles, kWaves * 64, 0, stream>>>(a);
-    direct_solve_kernel<<<1, 256, 0, stream>>>(a);
-}
-
-size_t direct_scratch_bytes() { return (size_t)kSums * kMaxTiles * 8 + (size_t)kMaxTiles * 4 + 256; }
-
-void launch_se3_from_pose(const double* pose12, double* se3_state, hipStream_t stream) {
-    se3_from_pose_kernel<<<1, 64, 0, stream>>>(pose12, se3_state);
-}
-
-void launch_se3_to_pose(const double* se3_state, double* pose12, double* log, int log_index,
-                        hipStream_t stream) {
-    se3_to_pose_kernel<<<1, 64, 0, stream>>>(se3_state, pose12, log, log ? log_index : -1);
+    const int grid = a.n_tiles > 0 ? a.n_tiles : 1;
+    for (int level = kLevels - 1; level >= 0; --level) {
+        a.level = level;
+        direct_level_kernel<<<grid, kThreads, 0, stream>>>(a);
+    }
+    a.level = -1;
+    direct_level_kernel<<<1, kThreads, 0, stream>>>(a);
 }
 
 }  // namespace viso
+
+#ifdef VISO_PROBE
+extern "C" int viso_debug_probe(unsigned long long* out, int n, int reset) {
+    if (n > 128) n = 128;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_probe), sizeof(unsigned long long) * n) != hipSuccess)
+        return -2;
+    if (reset) {
+        static unsigned long long zero[128] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_probe), zero, sizeof(zero)) != hipSuccess) return -2;
+    }
+    return 0;
+}
+#endif

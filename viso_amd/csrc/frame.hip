@@ -2,9 +2,10 @@
 // host state machine over device-resident state.
 //
 // All pixel/point work is on the GPU; the host only sequences launches.
-// Tracking frames (kRunning) never synchronise: direct pose (4 levels x 2
-// launches), SE3 -> pose, and LK alignment (1 launch) are queued back to
-// back and the pose stays in HBM (pose log).  Initialisation frames
+// Tracking frames (kRunning) never synchronise: the direct pose (5 launches,
+// direct.hip) is queued back to back and the pose stays in HBM (pose log);
+// LK alignment of the call's tracking frames runs as one batched launch when
+// the ingest call ends (flush_lk).  Initialisation frames
 // synchronise once (to read the PoseEstimation2d2d result block) because the
 // state transition (src/viso.cpp:76-98) decides which kernels the next frame
 // runs.  Frames live in a slot pool (device pyramids + device poses); the
@@ -136,45 +137,35 @@ int viso_ctx::init() {
     // map + tracking
     if (!rc) rc = map_pts.ensure(24 * (size_t)kMaxMapPoints);
     if (!rc) rc = kf_poses.ensure(96 * (size_t)kMaxKeyframes);
-    if (!rc) rc = se3.ensure(64);
-    if (!rc) rc = direct_tiles.ensure(direct_scratch_bytes());
+    if (!rc) rc = direct_buf.ensure(direct_scratch_bytes());
     if (!rc) rc = direct_stats.ensure(4 * 50 * 8);
-    if (!rc) rc = lk_pair.ensure(4 * (size_t)kMaxMapPoints * kLkStreams);
-    if (!rc) rc = lk_succ.ensure((size_t)kMaxMapPoints * kLkStreams);
-    if (!rc) rc = lk_before.ensure(16 * (size_t)kMaxMapPoints * kLkStreams);
-    if (!rc) rc = lk_after.ensure(16 * (size_t)kMaxMapPoints * kLkStreams);
+    if (!rc) rc = lk_pair.ensure(4 * (size_t)kMaxMapPoints * kLkBatch);
+    if (!rc) rc = lk_succ.ensure((size_t)kMaxMapPoints * kLkBatch);
+    if (!rc) rc = lk_before.ensure(16 * (size_t)kMaxMapPoints * kLkBatch);
+    if (!rc) rc = lk_after.ensure(16 * (size_t)kMaxMapPoints * kLkBatch);
     if (!rc) rc = pose_log.ensure(96 * (size_t)std::max(p.max_poses, 1));
-    if (!rc) rc = pose_count.ensure(256);
     if (rc) return rc;
-    direct.tile_part = (double*)direct_tiles.ptr;
-    direct.tile_good = (int*)((char*)direct_tiles.ptr + 28 * 256 * 8);
-    for (auto& s : lk_streams) VISO_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    VISO_HIP_CHECK(hipEventCreateWithFlags(&ev_pose, hipEventDisableTiming));
+    direct = direct_scratch_at(direct_buf.ptr);
+    VISO_HIP_CHECK(hipStreamCreateWithFlags(&lk_stream, hipStreamNonBlocking));
     for (int i = 0; i < kLkRing; ++i) VISO_HIP_CHECK(hipEventCreateWithFlags(&lk_ring[i], hipEventDisableTiming));
-    VISO_HIP_CHECK(hipMemsetAsync(pose_count.ptr, 0, 256, stream));
     VISO_HIP_CHECK(hipMemsetAsync(n_track_dev.ptr, 0, 256, stream));
     VISO_HIP_CHECK(hipStreamSynchronize(stream));
     return VISO_OK;
 }
 
 void viso_ctx::release() {
-    for (auto s : lk_streams)
-        if (s) (void)hipStreamSynchronize(s);
+    if (lk_stream) (void)hipStreamSynchronize(lk_stream);
     timing.destroy();
-    if (ev_pose) (void)hipEventDestroy(ev_pose);
-    ev_pose = nullptr;
     for (auto& e : lk_ring) {
         if (e) (void)hipEventDestroy(e);
         e = nullptr;
     }
-    for (auto& s : lk_streams) {
-        if (s) (void)hipStreamDestroy(s);
-        s = nullptr;
-    }
+    if (lk_stream) (void)hipStreamDestroy(lk_stream);
+    lk_stream = nullptr;
     DevBuf* bufs[] = {&scratch_a, &scratch_b, &scratch_c, &scratch_d, &slot_pool, &slot_pose,
                       &kp1, &kp2, &kp1b, &kp2b, &track_success, &n_track_dev, &fast_rows,
-                      &geo_buf, &map_pts, &kf_poses, &se3, &direct_tiles, &direct_stats,
-                      &lk_pair, &lk_succ, &lk_before, &lk_after, &pose_log, &pose_count};
+                      &geo_buf, &map_pts, &kf_poses, &direct_buf, &direct_stats,
+                      &lk_pair, &lk_succ, &lk_before, &lk_after, &pose_log};
     for (DevBuf* b : bufs) b->release();
     if (h_ctl) (void)hipHostFree(h_ctl);
     if (h_int) (void)hipHostFree(h_int);
@@ -189,13 +180,12 @@ int viso_ctx::acquire_slot() {
     if (free_slots.empty()) return -1;
     int s = free_slots.back();
     free_slots.pop_back();
-    // the LK stream may still read this slot's previous frame: order the
-    // reuse behind that launch (a no-op wait in steady state)
+    // lk_stream may still read this slot's previous frame: order the reuse
+    // behind that batch (a no-op wait in steady state; a later batch on the
+    // same stream also implies completion)
     const int64_t use = slots[(size_t)s].lk_use;
     if (use >= 0 && lk_seq > use) {
-        // a later launch on the same LK stream also implies completion
-        const int64_t e = (lk_seq - use <= kLkRing) ? use
-                                                    : use + kLkStreams * ((lk_seq - 1 - use) / kLkStreams);
+        const int64_t e = (lk_seq - use <= kLkRing) ? use : lk_seq - 1;
         (void)hipStreamWaitEvent(stream, lk_ring[e % kLkRing], 0);
     }
     slots[(size_t)s] = SlotRec{};
@@ -249,6 +239,63 @@ int viso_ctx::ingest_host(const uint8_t* grey, int32_t w, int32_t h, int32_t str
     VISO_HIP_CHECK(hipMemcpy2DAsync(slot_base(s), (size_t)w, grey, (size_t)stride, (size_t)w, (size_t)h,
                                     hipMemcpyHostToDevice, stream));
     *slot_out = s;
+    return VISO_OK;
+}
+
+// ------------------------------------------------------------------ LKAlignment batch
+int viso_ctx::flush_lk(hipStream_t ls) {
+    if (lk_pending.empty()) return VISO_OK;
+    const PyrGeom& g = geom;
+    LkAlignArgs a{};
+    a.n_kf = (int)kf_slots.size();
+    for (int j = 0; j < a.n_kf; ++j) a.kf[j] = frame(kf_slots[(size_t)j]);
+    a.kf_poses = (const double*)kf_poses.ptr;
+    a.n_frames = (int)lk_pending.size();
+    for (int f = 0; f < a.n_frames; ++f) {
+        a.frames[f].cur = frame(lk_pending[(size_t)f]);
+        a.frames[f].pose = pose_of(lk_pending[(size_t)f]);
+    }
+    a.points = (const double*)map_pts.ptr;
+    a.n = n_map;
+    a.K[0] = p.fx;
+    a.K[1] = p.fy;
+    a.K[2] = p.cx;
+    a.K[3] = p.cy;
+    a.thresh = p.photometric_error_thresh;
+    for (int l = 0; l < kLevels; ++l) {
+        a.g.w[l] = g.w[l];
+        a.g.h[l] = g.h[l];
+        a.g.off[l] = g.off[l];
+    }
+    a.out_stride = kMaxMapPoints;
+    a.pair_kf = (int32_t*)lk_pair.ptr;
+    a.success = (uint8_t*)lk_succ.ptr;
+    a.uv_before = (double*)lk_before.ptr;
+    a.uv_after = (double*)lk_after.ptr;
+    const bool side = ls != stream;
+    if (side) {
+        // the frames' poses come from the context stream
+        VISO_HIP_CHECK(hipEventRecord(lk_ring[lk_seq % kLkRing], stream));
+        VISO_HIP_CHECK(hipStreamWaitEvent(ls, lk_ring[lk_seq % kLkRing], 0));
+    } else if (lk_seq > 0) {
+        // the outputs may still be read by the last side batch's getters:
+        // order behind the last side batch
+        VISO_HIP_CHECK(hipStreamWaitEvent(stream, lk_ring[(lk_seq - 1) % kLkRing], 0));
+    }
+    {
+        TimedRegion t(timing, VISO_KERNEL_LKALIGN, ls);
+        launch_lk_align(a, ls);
+    }
+    VISO_HIP_CHECK(hipGetLastError());
+    lk_last_rows = a.n_frames;
+    if (side) {
+        VISO_HIP_CHECK(hipEventRecord(lk_ring[lk_seq % kLkRing], ls));
+        for (int s : lk_pending) slots[(size_t)s].lk_use = lk_seq;
+        for (int s : kf_slots) slots[(size_t)s].lk_use = lk_seq;
+        ++lk_seq;
+    }
+    for (int s : lk_pending) drop(s);
+    lk_pending.clear();
     return VISO_OK;
 }
 
@@ -360,51 +407,20 @@ int viso_ctx::on_new_frame(int cur) {
             const bool log = n_poses < p.max_poses;
             {
                 TimedRegion t(timing, VISO_KERNEL_DIRECT, stream);
-                for (int level = kLevels - 1; level >= 0; --level)
-                    launch_direct_level(frame(last_slot), frame(cur), g, K, (const double*)map_pts.ptr,
-                                        n_map, pose_of(last_slot), (double*)se3.ptr, level, direct,
-                                        (double*)direct_stats.ptr + 50 * level, stream,
-                                        level == kLevels - 1, level == 0 ? pose_of(cur) : nullptr,
-                                        level == 0 && log ? (double*)pose_log.ptr : nullptr,
-                                        n_poses);
+                launch_direct_pose(frame(last_slot), frame(cur), g, K, (const double*)map_pts.ptr,
+                                   n_map, pose_of(last_slot), pose_of(last_slot), direct,
+                                   (double*)direct_stats.ptr, pose_of(cur),
+                                   log ? (double*)pose_log.ptr : nullptr, n_poses, stream);
             }
             if (log) ++n_poses;
-            // LKAlignment (src/viso.cpp:121, 768-843)
-            LkAlignArgs a{};
-            a.n_kf = (int)kf_slots.size();
-            for (int j = 0; j < a.n_kf; ++j) a.kf[j] = frame(kf_slots[(size_t)j]);
-            a.kf_poses = (const double*)kf_poses.ptr;
-            a.cur = frame(cur);
-            a.cur_pose = pose_of(cur);
-            a.points = (const double*)map_pts.ptr;
-            a.n = n_map;
-            a.K[0] = p.fx;
-            a.K[1] = p.fy;
-            a.K[2] = p.cx;
-            a.K[3] = p.cy;
-            a.thresh = p.photometric_error_thresh;
-            for (int l = 0; l < kLevels; ++l) {
-                a.g.w[l] = g.w[l];
-                a.g.h[l] = g.h[l];
-                a.g.off[l] = g.off[l];
+            // LKAlignment (src/viso.cpp:121, 768-843): queued for the batched
+            // launch at the end of this ingest call
+            hold(cur);
+            lk_pending.push_back(cur);
+            if ((int)lk_pending.size() == kLkBatch) {
+                int rc = flush_lk(stream);
+                if (rc) return rc;
             }
-            const int ring = (int)(lk_seq % kLkStreams);
-            const size_t o = (size_t)ring * kMaxMapPoints;
-            a.pair_kf = (int32_t*)lk_pair.ptr + o;
-            a.success = (uint8_t*)lk_succ.ptr + o;
-            a.uv_before = (double*)lk_before.ptr + 2 * o;
-            a.uv_after = (double*)lk_after.ptr + 2 * o;
-            hipStream_t ls = lk_streams[ring];
-            VISO_HIP_CHECK(hipEventRecord(ev_pose, stream));
-            VISO_HIP_CHECK(hipStreamWaitEvent(ls, ev_pose, 0));
-            {
-                TimedRegion t(timing, VISO_KERNEL_LKALIGN, ls);
-                launch_lk_align(a, ls);
-            }
-            VISO_HIP_CHECK(hipEventRecord(lk_ring[lk_seq % kLkRing], ls));
-            slots[(size_t)cur].lk_use = lk_seq;
-            for (int s : kf_slots) slots[(size_t)s].lk_use = lk_seq;
-            ++lk_seq;
             ran_tracking = true;
             break;
         }
@@ -440,7 +456,8 @@ int viso_process_frame(viso_ctx* c, const uint8_t* grey, int32_t width, int32_t 
     }
     VISO_HIP_CHECK(hipGetLastError());
     rc = c->on_new_frame(s);
-    return rc;
+    if (rc) return rc;
+    return c->flush_lk(c->lk_stream);
 }
 
 int viso_process_stereo(viso_ctx* c, const uint8_t* left, const uint8_t* right,
@@ -467,7 +484,9 @@ int viso_process_stereo(viso_ctx* c, const uint8_t* left, const uint8_t* right,
     // reference path runs on the left image only
     c->hold(sr);
     c->drop(sr);
-    return c->on_new_frame(sl);
+    rc = c->on_new_frame(sl);
+    if (rc) return rc;
+    return c->flush_lk(c->lk_stream);
 }
 
 int viso_process_frames_device(viso_ctx* c, const uint8_t* d_left, const uint8_t* d_right,
@@ -509,14 +528,17 @@ int viso_process_frames_device(viso_ctx* c, const uint8_t* d_left, const uint8_t
             int rc = c->on_new_frame(sl[(size_t)i]);
             if (rc) return rc;
         }
+        // the chunk's LKAlignment batch, behind its direct-pose chain
+        int rc = c->flush_lk(c->stream);
+        if (rc) return rc;
         // frames still referenced after the chunk get their own level 0
         int roles[3] = {c->ref_slot, c->last_slot, -1};
         for (int r : roles) {
-            int rc = c->own_level0(r);
+            rc = c->own_level0(r);
             if (rc) return rc;
         }
         for (int s : c->kf_slots) {
-            int rc = c->own_level0(s);
+            rc = c->own_level0(s);
             if (rc) return rc;
         }
         for (int s : sl) c->drop(s);
@@ -577,9 +599,9 @@ int viso_get_alignment(viso_ctx* c, int32_t* pair_kf, uint8_t* success, double* 
                        double* uv_after, size_t cap, size_t* n) {
     if (!c) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(c->device));
-    for (auto s : c->lk_streams) VISO_HIP_CHECK(hipStreamSynchronize(s));
+    VISO_HIP_CHECK(hipStreamSynchronize(c->lk_stream));
     const size_t m = c->ran_tracking ? std::min(cap, (size_t)c->n_map) : 0;
-    const size_t o = c->lk_seq > 0 ? (size_t)((c->lk_seq - 1) % viso_ctx::kLkStreams) * kMaxMapPoints : 0;
+    const size_t o = (size_t)std::max(c->lk_last_rows - 1, 0) * kMaxMapPoints;
     if (m > 0) {
         if (pair_kf) VISO_HIP_CHECK(hipMemcpyAsync(pair_kf, (int32_t*)c->lk_pair.ptr + o, 4 * m, hipMemcpyDeviceToHost, c->stream));
         if (success) VISO_HIP_CHECK(hipMemcpyAsync(success, (uint8_t*)c->lk_succ.ptr + o, m, hipMemcpyDeviceToHost, c->stream));
@@ -597,9 +619,9 @@ int viso_get_frame_stats(viso_ctx* c, double out[16]) {
     std::memcpy(out, c->stats, sizeof(c->stats));
     if (c->state == VISO_STATE_RUNNING && c->stats[12] == 0 && c->ran_tracking) {
         // last frame was a tracking frame: level-0 direct stats + LK counts
-        for (auto s : c->lk_streams) VISO_HIP_CHECK(hipStreamSynchronize(s));
+        VISO_HIP_CHECK(hipStreamSynchronize(c->lk_stream));
         const int m = c->n_map;
-        const size_t o = c->lk_seq > 0 ? (size_t)((c->lk_seq - 1) % viso_ctx::kLkStreams) * kMaxMapPoints : 0;
+        const size_t o = (size_t)std::max(c->lk_last_rows - 1, 0) * kMaxMapPoints;
         std::vector<int32_t> pk((size_t)m);
         std::vector<uint8_t> sc((size_t)m);
         if (m > 0) {

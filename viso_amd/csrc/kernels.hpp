@@ -36,12 +36,18 @@ void launch_compact_tracks(const float2* kp1, const float2* kp2, const uint8_t* 
                            float2* kp1_out, float2* kp2_out, int* n_out, hipStream_t stream);
 
 constexpr int kMaxKeyframes = 8;
+// One frame of a batched LKAlignment launch: its pyramid and pose (device).
+struct LkFrame {
+    FrameDev cur;
+    const double* pose;  // 12 doubles
+};
+constexpr int kLkBatch = 64;  // frames per launch (kernel arguments stay < 4 KB)
 struct LkAlignArgs {
     FrameDev kf[kMaxKeyframes];
     const double* kf_poses;  // n_kf x 12 (device)
     int n_kf;
-    FrameDev cur;
-    const double* cur_pose;  // 12 (device)
+    int n_frames;            // <= kLkBatch
+    LkFrame frames[kLkBatch];
     const double* points;    // n x 3
     int n;
     double K[4];
@@ -50,9 +56,11 @@ struct LkAlignArgs {
         int w[4], h[4];
         unsigned long long off[4];
     } g;
+    // outputs of frame f at f * out_stride (elements)
+    size_t out_stride;
     int32_t* pair_kf;
     uint8_t* success;
-    double* uv_before;
+    double* uv_before;  // 2 per point
     double* uv_after;
 };
 void launch_lk_align(const LkAlignArgs& a, hipStream_t stream);
@@ -64,30 +72,32 @@ void launch_stereo_sad(const uint8_t* left, const uint8_t* right, int w, int h, 
 
 // ---------------------------------------------------------------- direct pose
 constexpr int kMaxMapPoints = 16384;
+// Device scratch of the direct pose (carved from one buffer of
+// direct_scratch_bytes() by direct_scratch_at).
 struct DirectScratch {
-    double* tile_part = nullptr;  // [28 x 4096] k-major
-    int* tile_good = nullptr;     // [4096]
+    double* part = nullptr;       // [kLevels][256 tiles][28] tile partial sums
+    int* good = nullptr;          // [kLevels][256]
+    double* state = nullptr;      // [kLevels + 1][8] T21 per level (+ result)
+    double* cont_part = nullptr;  // [256 workgroups][256][28] continuation scratch
+    int* cont_good = nullptr;     // [256 workgroups][256]
 };
 size_t direct_scratch_bytes();
-// SE3 state on the device: 7 doubles (qx, qy, qz, qw, tx, ty, tz).
-// One DirectPoseEstimationSingleLayer call (faithful: one GN step).
-// stats (device, may be null): [nGood, cost, H(36), b(6), update(6)].
-// seed_from_last: start from SE3(R, t) of pose_last12 instead of se3_state.
-// pose_out (may be null): receives R, t of the result, also stored at
+DirectScratch direct_scratch_at(void* base);
+// DirectPoseEstimationMultiLayer (src/viso.cpp:760-766): levels 3..0, each a
+// faithful DirectPoseEstimationSingleLayer (:661-758), starting from
+// T21 = SE3(R, t) of pose_seed12 (src/viso.cpp:114); the patch reference is
+// `last` at pose_last12.  Five launches: the tiles of level l run in a launch
+// whose prologue solves level l+1 from its tile partials; a final one-
+// workgroup launch solves level 0.
+// stats (device, may be null): per level [nGood, cost, H(36), b(6), update(6)].
+// pose_out (device, may be null) receives R, t of the result, also stored at
 // log[12*log_index] when log is non-null.
-void launch_direct_level(const FrameDev& last, const FrameDev& cur, const PyrGeom& g,
-                         const double K[4], const double* points, int n,
-                         const double* pose_last12, double* se3_state, int level,
-                         DirectScratch& s, double* stats, hipStream_t stream,
-                         bool seed_from_last = false, double* pose_out = nullptr,
-                         double* log = nullptr, int log_index = -1);
+void launch_direct_pose(const FrameDev& last, const FrameDev& cur, const PyrGeom& g,
+                        const double K[4], const double* points, int n,
+                        const double* pose_last12, const double* pose_seed12,
+                        const DirectScratch& s, double* stats, double* pose_out, double* log,
+                        int log_index, hipStream_t stream);
 // dst (12 doubles, device) <- src (host values, passed by value)
 void launch_set_pose(double* dst, const double src[12], hipStream_t stream);
-// se3_state <- SE3(R, t) of a 12-double pose (Sophus::SE3d(R, t)).
-void launch_se3_from_pose(const double* pose12, double* se3_state, hipStream_t stream);
-// pose12 <- rotationMatrix(), translation() of se3_state (optionally also
-// stored at log[12*log_index]).
-void launch_se3_to_pose(const double* se3_state, double* pose12, double* log, int log_index,
-                        hipStream_t stream);
 
 }  // namespace viso

@@ -178,6 +178,11 @@ __global__ __launch_bounds__(256) void lk_align_kernel(LkAlignArgs a) {
     __shared__ uint8_t s_win[4][kWinW * kWinH];
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= a.n) return;
+    // frame of the batch (blockIdx.y): its pyramid, pose and output rows
+    const LkFrame& fr = a.frames[blockIdx.y];
+    const FrameDev cur = fr.cur;
+    const double* cur_pose = fr.pose;
+    const size_t o = (size_t)blockIdx.y * a.out_stride;
     const int lane = threadIdx.x & 63;
     uint8_t* my_win = s_win[threadIdx.x >> 6];
     const int px = (lane >> 3) - 4, py = (lane & 7) - 4;
@@ -188,7 +193,7 @@ __global__ __launch_bounds__(256) void lk_align_kernel(LkAlignArgs a) {
     uint8_t succ_out = 0;
     double ub[2] = {0.0, 0.0}, ua[2] = {0.0, 0.0};
     double uc, vc;
-    project_px(a.cur_pose, K, P, 1.0, uc, vc);
+    project_px(cur_pose, K, P, 1.0, uc, vc);
     if (inside_px(uc, vc, w0, h0)) {  // current_frame->IsInside(Pw, 0)
         double best_angle = 180.0;
         double bu = 0, bv = 0;
@@ -228,8 +233,8 @@ __global__ __launch_bounds__(256) void lk_align_kernel(LkAlignArgs a) {
                 const int w = a.g.w[level], h = a.g.h[level];
                 const double rx = bu * s + px, ry = bv * s + py;
                 const double cx = cu * s + px, cy = cv * s + py;
-                const Window win = load_window(my_win, a.cur.l[level], w, h, cu * s, cv * s);
-                LkResult r = lk_level<100, false>(refp.l[level], w, h, a.cur.l[level], w, h, rx,
+                const Window win = load_window(my_win, cur.l[level], w, h, cu * s, cv * s);
+                LkResult r = lk_level<100, false>(refp.l[level], w, h, cur.l[level], w, h, rx,
                                                   ry, cx, cy, bu * s, bv * s, 0.0, 0.0, a.thresh,
                                                   win);
                 succ = r.succ;
@@ -242,12 +247,12 @@ __global__ __launch_bounds__(256) void lk_align_kernel(LkAlignArgs a) {
         }
     }
     if (lane == 0) {
-        a.pair_kf[i] = kf;
-        a.success[i] = succ_out;
-        a.uv_before[2 * i] = ub[0];
-        a.uv_before[2 * i + 1] = ub[1];
-        a.uv_after[2 * i] = ua[0];
-        a.uv_after[2 * i + 1] = ua[1];
+        a.pair_kf[o + i] = kf;
+        a.success[o + i] = succ_out;
+        a.uv_before[2 * (o + i)] = ub[0];
+        a.uv_before[2 * (o + i) + 1] = ub[1];
+        a.uv_after[2 * (o + i)] = ua[0];
+        a.uv_after[2 * (o + i) + 1] = ua[1];
     }
 }
 
@@ -298,8 +303,8 @@ void launch_klt(const FrameDev& ref, const FrameDev& cur, const PyrGeom& g, cons
 }
 
 void launch_lk_align(const LkAlignArgs& a, hipStream_t stream) {
-    if (a.n <= 0) return;
-    lk_align_kernel<<<(a.n + 3) / 4, 256, 0, stream>>>(a);
+    if (a.n <= 0 || a.n_frames <= 0) return;
+    lk_align_kernel<<<dim3((a.n + 3) / 4, a.n_frames), 256, 0, stream>>>(a);
 }
 
 }  // namespace viso
