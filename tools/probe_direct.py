@@ -56,12 +56,21 @@ def main():
     for k, name in enumerate(["F", "L(0)", "L(1)", "L(2)", "L(3)"]):
         c = p[16 + k]
         print(f"{name:6s} {c:6d}  {us(p[k], c):12.2f}  {us(p[8 + k], c):11.2f}")
+    print("prologue phases (us from entry): B1  S-combined  solved  prologue-done")
+    for k, name in enumerate(["F", "L(0)", "L(1)", "L(2)", "L(3)"]):
+        c = p[16 + k]
+        ph = [us(p[32 + 6 * k + j], c) for j in range(3)]
+        print(f"{name:6s} {ph[0]:8.2f} {ph[1]:8.2f} {ph[2]:8.2f} {us(p[k], c):8.2f}")
+    c = p[16 + 2]
+    print("L(1) solve_wave0 (us from entry): LU %.2f  inverse %.2f  update %.2f  exp %.2f" %
+          tuple(us(p[90 + k], c) for k in range(4)))
     stamps = [x for x in p[64:84] if x]
     t0 = min(stamps)
     print("last frame timeline (us from the first launch entry):")
     for k, name in [(4, "L(3)"), (3, "L(2)"), (2, "L(1)"), (1, "L(0)"), (0, "F")]:
         a, b = (p[64 + 4 * k] - t0) * 0.01, (p[65 + 4 * k] - t0) * 0.01
-        print(f"  {name:5s} entry {a:7.2f}  block0 exit {b:7.2f}")
+        last = (p[100 + k] - t0) * 0.01
+        print(f"  {name:5s} entry {a:7.2f}  block0 exit {b:7.2f}  last block exit {last:7.2f}")
 
 if __name__ == "__main__":
     main()

@@ -51,7 +51,12 @@ __device__ unsigned long long g_probe[128];
     do {                                                                                \
         if (threadIdx.x == 0 && blockIdx.x == 0) g_probe[(i)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
+#define PROBE_MAX(i)                                                                    \
+    do {                                                                                \
+        if (threadIdx.x == 0) atomicMax(&g_probe[(i)], __builtin_amdgcn_s_memrealtime()); \
+    } while (0)
 #else
+#define PROBE_MAX(i)
 #define PROBE_T0()
 #define PROBE(i)
 #define PROBE_ABS(i)
@@ -114,15 +119,20 @@ __device__ inline void d_pixel_d_xi(const Intrinsics& K, const double* pose, con
 }
 
 // The part of one map point that does not depend on T21: the point, its
-// projection into the last frame (src/viso.cpp:697) and the `last` sample.
+// projection into the last frame (src/viso.cpp:697) and the `last` patch
+// sample.  sample_px is split in two so the tap loads can be issued early and
+// combined after a barrier: ref_issue loads the four tap bytes, ref_finish
+// forms the bilinear value with sample_px's exact expression.
 struct RefSample {
     double P[3];
     double ur, vr;
+    double xx, yy;
     double lval;
+    int t0, t1, t2, t3;
     bool ok;
 };
 
-__device__ inline void ref_sample(const DirectArgs& a, int lv, int i, RefSample& r) {
+__device__ inline void ref_issue(const DirectArgs& a, int lv, int i, RefSample& r) {
     const int lane = threadIdx.x & 63;
     const int px = (lane >> 3) - 4, py = (lane & 7) - 4;
     const double scale = kScale[lv];
@@ -133,13 +143,98 @@ __device__ inline void ref_sample(const DirectArgs& a, int lv, int i, RefSample&
     project_px(a.pose_last, a.K, r.P, scale, r.ur, r.vr);
     const double hp = 4.0;
     r.ok = inside_px(r.ur - hp, r.vr - hp, w, h) && inside_px(r.ur + hp, r.vr + hp, w, h);
-    r.lval = r.ok ? sample_px(a.last.l[lv], w, h, r.ur + px, r.vr + py) : 0.0;
+    const double x = r.ur + px, y = r.vr + py;
+    const uint8_t* img = a.last.l[lv];
+    const long long n = (long long)w * (long long)h;
+    const long long base = r.ok ? (long long)(int)y * (long long)w + (long long)(int)x : -(1LL << 40);
+    r.t0 = (base >= 0 && base < n) ? img[base] : 0;
+    r.t1 = (base + 1 >= 0 && base + 1 < n) ? img[base + 1] : 0;
+    r.t2 = (base + w >= 0 && base + w < n) ? img[base + w] : 0;
+    r.t3 = (base + w + 1 >= 0 && base + w + 1 < n) ? img[base + w + 1] : 0;
+    r.xx = x - floor(x);
+    r.yy = y - floor(y);
+}
+
+__device__ inline void ref_finish(RefSample& r) {
+    const double d0 = (double)r.t0, d1 = (double)r.t1, d2 = (double)r.t2, d3 = (double)r.t3;
+    const double xx = r.xx, yy = r.yy;
+    r.lval = r.ok ? double((1 - xx) * (1 - yy) * d0 + xx * (1 - yy) * d1 + (1 - xx) * yy * d2 +
+                           xx * yy * d3)
+                  : 0.0;
+}
+
+__device__ inline void ref_sample(const DirectArgs& a, int lv, int i, RefSample& r) {
+    ref_issue(a, lv, i, r);
+    ref_finish(r);
+}
+
+// Per-wave LDS window (16 x 16 bytes) of the current image around the
+// point's projection under a predicted T21 (the previous level's starting
+// pose), loaded while the prologue solves.  A sample whose four taps lie in
+// the window (itself inside the image, so no tap wraps a row or leaves the
+// buffer) reads the same bytes from LDS; any other takes sample_px's path.
+constexpr int kCW = 16;
+
+struct CurWin {
+    int x0, y0;
+    bool on;
+    int b0, b1, b2, b3;  // this lane's 4 bytes: row lane/4, columns 4*(lane%4)..+3
+};
+
+__device__ inline void win_issue(const uint8_t* __restrict__ img, int w, int h, double u, double v,
+                                 CurWin& c) {
+    c.on = w >= kCW && h >= kCW && u > -1e6 && u < 1e6 && v > -1e6 && v < 1e6;
+    c.x0 = 0;
+    c.y0 = 0;
+    c.b0 = c.b1 = c.b2 = c.b3 = 0;
+    if (!c.on) return;
+    int x0 = (int)floor(u) - kCW / 2 + 1;
+    int y0 = (int)floor(v) - kCW / 2 + 1;
+    x0 = min(max(x0, 0), w - kCW);
+    y0 = min(max(y0, 0), h - kCW);
+    c.x0 = x0;
+    c.y0 = y0;
+    const int lane = threadIdx.x & 63;
+    const uint8_t* p = img + (size_t)(y0 + (lane >> 2)) * w + x0 + 4 * (lane & 3);
+    c.b0 = p[0];
+    c.b1 = p[1];
+    c.b2 = p[2];
+    c.b3 = p[3];
+}
+
+__device__ inline void win_store(uint8_t* lds, const CurWin& c) {
+    const int lane = threadIdx.x & 63;
+    uint8_t* q = lds + (lane >> 2) * kCW + 4 * (lane & 3);
+    q[0] = (uint8_t)c.b0;
+    q[1] = (uint8_t)c.b1;
+    q[2] = (uint8_t)c.b2;
+    q[3] = (uint8_t)c.b3;
+}
+
+// sample_px with the taps served from the window when all four lie in it
+__device__ inline double sample_cw(const uint8_t* __restrict__ img, int w, int h, double x,
+                                   double y, const uint8_t* win, const CurWin& c) {
+    const bool finite = (x > -1e9 && x < 1e9 && y > -1e9 && y < 1e9);
+    if (finite && c.on) {
+        const int ix = (int)x, iy = (int)y;
+        if (ix >= c.x0 && ix + 1 < c.x0 + kCW && iy >= c.y0 && iy + 1 < c.y0 + kCW) {
+            const uint8_t* q = win + (iy - c.y0) * kCW + (ix - c.x0);
+            const double d0 = (double)q[0], d1 = (double)q[1];
+            const double d2 = (double)q[kCW], d3 = (double)q[kCW + 1];
+            const double xx = x - floor(x);
+            const double yy = y - floor(y);
+            return double((1 - xx) * (1 - yy) * d0 + xx * (1 - yy) * d1 + (1 - xx) * yy * d2 +
+                          xx * yy * d3);
+        }
+    }
+    return sample_px(img, w, h, x, y);
 }
 
 // The 28 sums of one map point by reduce-scatter: returns good; lane l < 32
 // with *idx >= 0 holds sum *idx in *out.
 __device__ inline bool direct_point_rs(const DirectArgs& a, int lv, const double* cur_pose,
-                                       const RefSample& r, double* out, int* idx) {
+                                       const RefSample& r, const uint8_t* win, const CurWin& cw,
+                                       double* out, int* idx) {
     const int lane = threadIdx.x & 63;
     const int px = (lane >> 3) - 4, py = (lane & 7) - 4;
     const double scale = kScale[lv];
@@ -152,9 +247,11 @@ __device__ inline bool direct_point_rs(const DirectArgs& a, int lv, const double
     double Jp[12];
     d_pixel_d_xi(a.K, cur_pose, r.P, scale, Jp);
     const uint8_t* C = a.cur.l[lv];
-    const double error = r.lval - sample_px(C, w, h, uc + px, vc + py);
-    double g0, g1;
-    gradient_px(C, w, h, uc + px, vc + py, g0, g1);
+    const double x = uc + px, y = vc + py;
+    const double error = r.lval - sample_cw(C, w, h, x, y, win, cw);
+    // GetGradient (include/keyframe.h:57-64)
+    const double g0 = 0.5 * (sample_cw(C, w, h, x + 1, y, win, cw) - sample_cw(C, w, h, x - 1, y, win, cw));
+    const double g1 = 0.5 * (sample_cw(C, w, h, x, y + 1, win, cw) - sample_cw(C, w, h, x, y - 1, win, cw));
     double J[6];
 #pragma unroll
     for (int k = 0; k < 6; ++k) J[k] = -g0 * Jp[k] + -g1 * Jp[6 + k];
@@ -175,12 +272,15 @@ __device__ inline bool direct_point_rs(const DirectArgs& a, int lv, const double
 // every thread of the workgroup.  `pre` (may be null) is the prefetched
 // RefSample of this wave's first point of the tile (valid when has_pre).
 __device__ void direct_tile(const DirectArgs& a, int lv, const double* cur_pose, int b,
-                            const RefSample& pre, bool has_pre, double* part, int* good,
-                            double* s_pts, int* s_good) {
+                            const RefSample& pre, bool has_pre, const uint8_t* win,
+                            const CurWin& cw, double* part, int* good, double* s_pts,
+                            int* s_good, bool zeroed = false) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int T = a.tile;
-    if (threadIdx.x == 0) *s_good = 0;
-    __syncthreads();
+    if (!zeroed) {
+        if (threadIdx.x == 0) *s_good = 0;
+        __syncthreads();
+    }
     int good_cnt = 0;
     for (int local = wave; local < T; local += kWaves) {
         const int i = b * T + local;
@@ -188,12 +288,14 @@ __device__ void direct_tile(const DirectArgs& a, int lv, const double* cur_pose,
         int idx = -1;
         bool ok = false;
         if (i < a.n) {
-            RefSample r;
-            if (has_pre && local == wave)
-                r = pre;
-            else
+            if (has_pre && local == wave) {
+                ok = direct_point_rs(a, lv, cur_pose, pre, win, cw, &f, &idx);
+            } else {
+                RefSample r;
                 ref_sample(a, lv, i, r);
-            ok = direct_point_rs(a, lv, cur_pose, r, &f, &idx);
+                CurWin none{};
+                ok = direct_point_rs(a, lv, cur_pose, r, nullptr, none, &f, &idx);
+            }
         }
         if (!ok) {
             if (lane < kSums) s_pts[local * kSums + lane] = 0.0;
@@ -273,7 +375,17 @@ __device__ inline double shfl_f64(double v, int src) { return __shfl(v, src, 64)
 
 // One GN step of one level on wave 0 (all 64 lanes): L.S -> update, the new
 // L.state and the loop decision L.cont (src/viso.cpp:731-753).
-__device__ void solve_wave0(SolveLds& L, int iter, double* stats) {
+__device__ void solve_wave0(SolveLds& L, int iter, double* stats, int probe_base = -1,
+                            unsigned long long probe_t0 = 0) {
+#ifdef VISO_PROBE
+#define SPROBE(k)                                                                       \
+    do {                                                                                \
+        if (probe_base >= 0 && (threadIdx.x & 63) == 0 && blockIdx.x == 0)             \
+            g_probe[probe_base + (k)] += __builtin_amdgcn_s_memrealtime() - probe_t0;   \
+    } while (0)
+#else
+#define SPROBE(k)
+#endif
     const int lane = threadIdx.x & 63;
     const int row = lane / 6, col = lane - 6 * (lane / 6);
     const bool in = lane < 36;
@@ -310,6 +422,7 @@ __device__ void solve_wave0(SolveLds& L, int iter, double* stats) {
         const double ukj = shfl_f64(v, 6 * k + col);
         if (in && row > k && col > k) v = v - lik * ukj;
     }
+    SPROBE(0);
     // ---- inverse: lane (row, col) holds X[row][col], X = P * I then
     // forward (unit L) and backward (U) substitution per column
     int pos = col;
@@ -333,6 +446,7 @@ __device__ void solve_wave0(SolveLds& L, int iter, double* stats) {
         const double uij = shfl_f64(v, (6 * row + j) & 63);
         if (in && row < j) x = x - uij * xj;
     }
+    SPROBE(1);
     // ---- update = H^-1 * b (row-wise, ascending columns)
     double update[6];
 #pragma unroll
@@ -342,6 +456,7 @@ __device__ void solve_wave0(SolveLds& L, int iter, double* stats) {
         for (int c = 1; c < 6; ++c) s = s + readlane_f64(x, 6 * r + c) * L.S[21 + c];
         update[r] = s;
     }
+    SPROBE(2);
     // ---- SE3::exp(update) (Sophus), sin/cos of theta/2 and theta in lanes 0/1
     SE3d E;
     {
@@ -389,6 +504,7 @@ __device__ void solve_wave0(SolveLds& L, int iter, double* stats) {
         }
         mat3_vec(V, update, E.t);
     }
+    SPROBE(3);
     SE3d T21;
 #pragma unroll
     for (int k = 0; k < 4; ++k) T21.q[k] = L.state[k];
@@ -444,39 +560,63 @@ __device__ void continue_tiles(const DirectArgs& a, int lv,
     double pose[12];
     for (int k = 0; k < 12; ++k) pose[k] = s_pose[k];
     RefSample none{};
+    CurWin off{};
     for (int b = 0; b < a.n_tiles; ++b)
-        direct_tile(a, lv, pose, b, none, false, part, good, s_pts, s_good);
+        direct_tile(a, lv, pose, b, none, false, nullptr, off, part, good, s_pts, s_good);
     __threadfence_block();
     __syncthreads();
 }
 
-// The GN loop of level lv on its tile partials (thread t < 256 already holds
-// tile t's in v / gg); L.state holds the T21 the tiles were evaluated at and
-// is left holding the level's result.
-__device__ void solve_level(const DirectArgs& a, int lv, SolveLds& L, double* v, int gg,
-                            double* stats, double* s_pose, double* s_pts, int* s_good) {
+// Barrier for LDS hand-offs only: waits for this wave's LDS operations, not
+// for its global loads, so loads issued before it stay in flight (a
+// __syncthreads() also drains vmcnt).
+__device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// GN iterations 1.. of level lv (the faithful continuation, rare): every
+// workgroup re-evaluates all tiles itself at the new T21 and solves again.
+__device__ void solve_continue(const DirectArgs& a, int lv, SolveLds& L, double* stats,
+                               double* s_pose, double* s_pts, int* s_good) {
     const int t = threadIdx.x, wave = t >> 6;
-    if (t == 0) {
-        for (int k = 0; k < 7; ++k) L.best[k] = L.state[k];
-        L.cost = 0.0;
-        L.last_cost = 0.0;
-    }
-    __syncthreads();
-    for (int iter = 0; iter < 100; ++iter) {
-        if (iter > 0) {
-            continue_tiles(a, lv, L.state, s_pose, s_pts, s_good);
-            if (t < 256)
-                load_partials(a.s.cont_part + (size_t)blockIdx.x * kMaxTiles * kSums,
-                              a.s.cont_good + (size_t)blockIdx.x * kMaxTiles, a.n_tiles, v, gg);
-        }
+    for (int iter = 1; iter < 100 && L.cont; ++iter) {
+        continue_tiles(a, lv, L.state, s_pose, s_pts, s_good);
+        double v[kSums];
+        int gg = 0;
+        if (t < 256)
+            load_partials(a.s.cont_part + (size_t)blockIdx.x * kMaxTiles * kSums,
+                          a.s.cont_good + (size_t)blockIdx.x * kMaxTiles, a.n_tiles, v, gg);
         reduce_partials(v, gg, L);
         if (wave == 0) solve_wave0(L, iter, stats);
         __syncthreads();
-        if (!L.cont) break;
     }
 }
 
+// Issue the T21-independent loads of map point i: the `last` patch taps and
+// the current-image window around its projection under the predicted T21
+// (the pose `prev` was evaluated at, or the seed).
+__device__ inline void prefetch_point(const DirectArgs& a, int lv, int i, bool solve, int prev,
+                                      RefSample& r, CurWin& cw) {
+    ref_issue(a, lv, i, r);
+    double pred[12];
+    if (!solve) {
+        for (int k = 0; k < 12; ++k) pred[k] = a.pose_seed[k];
+    } else {
+        double sp[7];
+        for (int k = 0; k < 7; ++k) sp[k] = a.s.state[prev * kStateStride + k];
+        state_to_pose(sp, pred);
+    }
+    double up, vp;
+    project_px(pred, a.K, r.P, kScale[lv], up, vp);
+    win_issue(a.cur.l[lv], a.g.w[lv], a.g.h[lv], up, vp, cw);
+}
+
 // L(level) and F (level = -1).
+//   Wave 0 is the solver: it reduces its quarter of the tile partials of
+//   `prev`, waits on an LDS arrival count for waves 1-3 (the other quarters)
+//   and thread 256 (the T21 `prev` was evaluated at), then solves.  No block
+//   barrier sits in front of the solve, so the other waves' prefetches (their
+//   map point, `last` patch taps and current-image window; wave 4 also
+//   prefetches wave 0's point) stay off its path.  B2 (block barrier) hands
+//   the new pose to every wave; then the tiles.
 __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
     PROBE_T0();
     PROBE_ABS(64 + 4 * (a.level + 1));
@@ -484,64 +624,152 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
     __shared__ double s_pose[12];
     __shared__ double s_pts[kMaxTile * kSums];
     __shared__ int s_good;
+    __shared__ int s_arrive;
+    __shared__ uint8_t s_win[kWaves][kCW * kCW];
+    __shared__ double s_lval0[64];  // wave 0's point, prefetched by wave 4
+    __shared__ int s_ok0, s_cw0[3];
     const int lv = a.level;
     const int prev = lv + 1;  // level solved in the prologue (kLevels: seeded)
-    const int t = threadIdx.x, wave = t >> 6;
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const bool tiles = lv >= 0 && (int)blockIdx.x < a.n_tiles;
+    const bool solve = prev < kLevels;
+    if (t == 0) {
+        s_arrive = 0;
+        s_good = 0;
+    }
+    lds_barrier();  // nothing is in flight yet
 
-    // ---- independent of T21: partials of `prev`, this wave's point
+    // ---- partials of `prev` (waves 0-3) and the starting T21 (thread 256)
     double v[kSums];
     int gg = 0;
-    if (prev < kLevels && t < 256)
+    if (solve && t < 256)
         load_partials(a.s.part + (size_t)prev * kMaxTiles * kSums, a.s.good + prev * kMaxTiles,
                       a.n_tiles, v, gg);
+    if (t == 256) {
+        double st[7];
+        if (!solve) {
+            // Sophus::SE3d(R, t): R -> quaternion
+            quat_from_matrix(a.pose_seed, st);
+            st[4] = a.pose_seed[9];
+            st[5] = a.pose_seed[10];
+            st[6] = a.pose_seed[11];
+        } else {
+            for (int k = 0; k < 7; ++k) st[k] = a.s.state[prev * kStateStride + k];
+        }
+        for (int k = 0; k < 7; ++k) {
+            L.state[k] = st[k];
+            L.best[k] = st[k];
+        }
+        L.cost = 0.0;
+        L.last_cost = 0.0;
+        L.cont = 0;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        atomicAdd(&s_arrive, 1);
+    }
+    if (solve && t < 256) {
+        int idx;
+        const double f = reduce_scatter_28(v, &idx);
+        if (lane < 32 && idx >= 0) L.red[wave][idx] = f;
+        const int g = wave_sum_int(gg);
+        if (lane == 0) L.g[wave] = g;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) atomicAdd(&s_arrive, 1);
+    }
+    PROBE(32 + 6 * (lv + 1));
+
+    // ---- prefetches (every wave but the solver)
     RefSample pre;
+    CurWin cw{};
     const int i0 = (int)blockIdx.x * a.tile + wave;
     const bool has_pre = tiles && wave < a.tile && i0 < a.n;
-    if (has_pre) ref_sample(a, lv, i0, pre);
-    // ---- T21 the prologue starts from
-    if (t == 0) {
-        if (prev == kLevels) {
-            // Sophus::SE3d(R, t): R -> quaternion
-            double q[4];
-            quat_from_matrix(a.pose_seed, q);
-            for (int k = 0; k < 4; ++k) L.state[k] = q[k];
-            L.state[4] = a.pose_seed[9];
-            L.state[5] = a.pose_seed[10];
-            L.state[6] = a.pose_seed[11];
-        } else {
-            for (int k = 0; k < 7; ++k) L.state[k] = a.s.state[prev * kStateStride + k];
+    const bool solver = solve && wave == 0;
+    if (has_pre && !solver) {
+        prefetch_point(a, lv, i0, solve, prev, pre, cw);
+        ref_finish(pre);
+        if (cw.on) win_store(s_win[wave], cw);
+    }
+    if (solve && wave == 4 && tiles && a.tile > 0 && (int)blockIdx.x * a.tile < a.n) {
+        RefSample r0;
+        CurWin c0{};
+        prefetch_point(a, lv, (int)blockIdx.x * a.tile, solve, prev, r0, c0);
+        ref_finish(r0);
+        s_lval0[lane] = r0.lval;
+        if (c0.on) win_store(s_win[0], c0);
+        if (lane == 0) {
+            s_ok0 = r0.ok ? 1 : 0;
+            s_cw0[0] = c0.x0;
+            s_cw0[1] = c0.y0;
+            s_cw0[2] = c0.on ? 1 : 0;
         }
     }
-    __syncthreads();
-    if (prev < kLevels) {
-        double* st = (a.stats && blockIdx.x == 0) ? a.stats + (size_t)kStats * prev : nullptr;
-        solve_level(a, prev, L, v, gg, st, s_pose, s_pts, &s_good);
+
+    // ---- the solve (wave 0)
+    if (solver) {
+        if (has_pre) {
+            // wave 0's own map point (the rest of its prefetch is wave 4's)
+            pre.P[0] = a.points[3 * i0];
+            pre.P[1] = a.points[3 * i0 + 1];
+            pre.P[2] = a.points[3 * i0 + 2];
+        }
+        while (__hip_atomic_load(&s_arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 5)
+            __builtin_amdgcn_s_sleep(1);
+        // canonical tree, last level: (w0 + w1) + (w2 + w3)
+        if (lane < kSums) L.S[lane] = (L.red[0][lane] + L.red[1][lane]) + (L.red[2][lane] + L.red[3][lane]);
+        if (lane == 0) L.ngood = (L.g[0] + L.g[1]) + (L.g[2] + L.g[3]);
+        PROBE(32 + 6 * (lv + 1) + 1);
+        double* stp = (a.stats && blockIdx.x == 0) ? a.stats + (size_t)kStats * prev : nullptr;
+#ifdef VISO_PROBE
+        solve_wave0(L, 0, stp, lv == 1 ? 90 : -1, probe_t0);
+#else
+        solve_wave0(L, 0, stp);
+#endif
+        PROBE(32 + 6 * (lv + 1) + 2);
+    }
+    if (!solve && wave == 0 && lane == 0) {
+        // seeded level: no solve, T21 is the seed (thread 256 wrote it)
+        while (__hip_atomic_load(&s_arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 1)
+            __builtin_amdgcn_s_sleep(1);
+    }
+    if (wave == 0 && lane == 0) state_to_pose(L.state, s_pose);
+    __syncthreads();  // B2
+    if (solver && has_pre) {
+        pre.ok = s_ok0 != 0;
+        pre.lval = s_lval0[lane];
+        cw.x0 = s_cw0[0];
+        cw.y0 = s_cw0[1];
+        cw.on = s_cw0[2] != 0;
+    }
+    if (solve && L.cont) {
+        // the continuation needs every thread; it leaves s_good dirty
+        double* stp = (a.stats && blockIdx.x == 0) ? a.stats + (size_t)kStats * prev : nullptr;
+        solve_continue(a, prev, L, stp, s_pose, s_pts, &s_good);
+        if (t == 0) {
+            state_to_pose(L.state, s_pose);
+            s_good = 0;
+        }
+        __syncthreads();
     }
     PROBE(lv + 1);
     const int out = lv >= 0 ? lv : kLevels;
     if (blockIdx.x == 0 && t == 0) {
         for (int k = 0; k < 7; ++k) a.s.state[out * kStateStride + k] = L.state[k];
         if (lv < 0 && a.pose_out) {
-            double p[12];
-            state_to_pose(L.state, p);
-            for (int k = 0; k < 12; ++k) a.pose_out[k] = p[k];
+            for (int k = 0; k < 12; ++k) a.pose_out[k] = s_pose[k];
             if (a.log && a.log_index >= 0)
-                for (int k = 0; k < 12; ++k) a.log[12 * (size_t)a.log_index + k] = p[k];
+                for (int k = 0; k < 12; ++k) a.log[12 * (size_t)a.log_index + k] = s_pose[k];
         }
     }
     if (tiles) {
-        if (t == 0) state_to_pose(L.state, s_pose);
-        __syncthreads();
         double pose[12];
 #pragma unroll
         for (int k = 0; k < 12; ++k) pose[k] = s_pose[k];
-        direct_tile(a, lv, pose, blockIdx.x, pre, has_pre,
+        direct_tile(a, lv, pose, blockIdx.x, pre, has_pre, s_win[wave], cw,
                     a.s.part + (size_t)lv * kMaxTiles * kSums, a.s.good + lv * kMaxTiles, s_pts,
-                    &s_good);
+                    &s_good, true);
     }
     PROBE(8 + lv + 1);
     PROBE_ABS(65 + 4 * (a.level + 1));
+    PROBE_MAX(100 + lv + 1);
 #ifdef VISO_PROBE
     if (threadIdx.x == 0 && blockIdx.x == 0) g_probe[16 + lv + 1] += 1;
 #endif
