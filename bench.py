@@ -139,12 +139,13 @@ def main():
     algo_bytes_img = dims[0][0] * dims[0][1] + sum(w * h for w, h in dims[1:])
     roofline = None
     if "pyramid" in timing:
-        # one timed region = one pyr_fused_kernel launch building levels 1..3
-        # of every image of one ingest chunk (left + right; <= 128 images)
+        # one timed region = the image pass of one ingest chunk (left + right,
+        # <= 128 images): three pyr_down_stream_kernel launches (L0->L1,
+        # L1->L2, L2->L3) back to back on the context stream
         imgs_per_launch = 2 * args.steps / timing["pyramid"]["launches"]
         bytes_per_launch = algo_bytes_img * imgs_per_launch
         achieved = bytes_per_launch / (timing["pyramid"]["avg_ms"] * 1e-3) / 1e9
-        roofline = {"kernel": "pyr_fused_kernel (batched image pass, L0 read + L1..L3 write)", "bound": "hbm",
+        roofline = {"kernel": "pyr_down_stream_kernel x3 (batched image pass; algorithmic bytes = L0 read + L1..L3 write)", "bound": "hbm",
                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                     "algorithmic_bytes_per_launch": int(bytes_per_launch),

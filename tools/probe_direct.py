@@ -44,12 +44,19 @@ def main():
             v.process_device(d_left.data_ptr() + f * W * H, None, k, W * H)
             f += k
 
+    lib.viso_debug_probe_lk.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lkbuf = (ctypes.c_ulonglong * 16)()
     run(0, warm)
     v.synchronize()
     lib.viso_debug_probe(buf, 128, 1)
+    lib.viso_debug_probe_lk(lkbuf, 1)
     run(warm, steps)
     v.synchronize()
     assert lib.viso_debug_probe(buf, 128, 0) == 0
+    lib.viso_debug_probe_lk(lkbuf, 0)
+    q = list(lkbuf)
+    print("LK alignment: mean GN iterations per (pair, level):",
+          ", ".join(f"L{l} {q[l] / max(q[4 + l], 1):.2f} ({q[4 + l]} calls)" for l in range(4)))
     p = list(buf)
     us = lambda x, c: 10.0 * x / max(c, 1) / 1e3  # 100 MHz ticks -> us
     print("launch  count  prologue-done  block0-done   (us from entry, block 0)")

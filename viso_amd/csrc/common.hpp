@@ -116,20 +116,46 @@ __device__ inline double readlane_f64(double v, int lane) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// gfx950 v_permlane16_swap / v_permlane32_swap on both halves of a double:
+// with both operands = v, lane l receives v[l ^ 16] (v[l ^ 32]) in one of the
+// two results and its own row's value in the other.
+__device__ inline void permlane16_swap_f64(double a, double b, double& ra, double& rb) {
+    const long long x = __double_as_longlong(a), y = __double_as_longlong(b);
+    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)(x & 0xffffffffLL),
+                                                     (unsigned)(y & 0xffffffffLL), false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(x >> 32), (unsigned)(y >> 32), false,
+                                                     false);
+    ra = __longlong_as_double(((long long)hi[0] << 32) | lo[0]);
+    rb = __longlong_as_double(((long long)hi[1] << 32) | lo[1]);
+}
+
+__device__ inline void permlane32_swap_f64(double a, double b, double& ra, double& rb) {
+    const long long x = __double_as_longlong(a), y = __double_as_longlong(b);
+    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)(x & 0xffffffffLL),
+                                                     (unsigned)(y & 0xffffffffLL), false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(x >> 32), (unsigned)(y >> 32), false,
+                                                     false);
+    ra = __longlong_as_double(((long long)hi[0] << 32) | lo[0]);
+    rb = __longlong_as_double(((long long)hi[1] << 32) | lo[1]);
+}
+
 // The same canonical tree as wave_tree_sum, built from DPP row operations:
 // xor-1 and xor-2 by quad_perm; then, because every lane of an aligned 4-
 // (8-) group already holds the same partial, row_half_mirror (row_mirror)
 // pairs each group with its sibling exactly like xor-4 (xor-8); the last two
-// levels read the four row sums with v_readlane: (r0 + r1) + (r2 + r3).
-// Result is wave-uniform.  Requires EXEC = all 64 lanes.
+// levels pair rows with v_permlane16_swap (row r with r ^ 1) and the wave
+// halves with v_permlane32_swap: (r0 + r1) + (r2 + r3).  Every lane ends
+// with the sum.  Requires EXEC = all 64 lanes.
 __device__ inline double wave_tree_sum_dpp(double v) {
     v = v + dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]  (xor 1)
     v = v + dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]  (xor 2)
     v = v + dpp_f64<0x141>(v);  // row_half_mirror      (xor 4 on uniform quads)
     v = v + dpp_f64<0x140>(v);  // row_mirror           (xor 8 on uniform octets)
-    const double r0 = readlane_f64(v, 0), r1 = readlane_f64(v, 16);
-    const double r2 = readlane_f64(v, 32), r3 = readlane_f64(v, 48);
-    return (r0 + r1) + (r2 + r3);
+    double a, b;
+    permlane16_swap_f64(v, v, a, b);  // rows (0,1) and (2,3): a + b = r_even + r_odd
+    v = a + b;
+    permlane32_swap_f64(v, v, a, b);  // halves: (r0 + r1) + (r2 + r3)
+    return a + b;
 }
 
 // 28 canonical wave trees at once by reduce-scatter: at butterfly level s
@@ -137,7 +163,7 @@ __device__ inline double wave_tree_sum_dpp(double v) {
 // values and adds the partner's copy of that half, so each value's partial
 // sums follow exactly the ascending-xor tree of wave_tree_sum.  Partners:
 // xor 1/2 by DPP quad_perm; xor 4/8 by DPP row_shl/row_shr + select; xor 16
-// by ds_swizzle; xor 32 by a lane shuffle.  On return, lane l (and l^32)
+// and xor 32 by v_permlane16_swap / v_permlane32_swap.  On return, lane l (and l^32)
 // holds value index 14*b0 + 7*b1 + 4*b2 + 2*b3 + b4 (b = bits of l) when
 // 4*b2 + 2*b3 + b4 < 7; the other 4 lane classes hold garbage.
 __device__ inline double dsel(bool c, double a, double b) { return c ? a : b; }
@@ -188,10 +214,13 @@ __device__ inline double reduce_scatter_28(const double* v, int* value_index) {
         const double recv = dsel(b3, dpp_f64<0x118>(send), dpp_f64<0x108>(send));  // row_shr:8 / row_shl:8
         e[k] = keep + recv;
     }
-    const double send = dsel(b4, e[0], e[1]);
-    const double keep = dsel(b4, e[1], e[0]);
-    double f = keep + swizzle_xor16_f64(send);
-    f = f + __shfl_xor(f, 32, 64);
+    // xor 16: row pairs (0,1), (2,3); even rows keep e[0], odd rows e[1]
+    double ra, rb;
+    permlane16_swap_f64(e[0], e[1], ra, rb);
+    double f = ra + rb;
+    // xor 32: the two wave halves
+    permlane32_swap_f64(f, f, ra, rb);
+    f = ra + rb;
     *value_index = (b0 ? 14 : 0) + (b1 ? 7 : 0) + (b2 ? 4 : 0) + (b3 ? 2 : 0) + (b4 ? 1 : 0);
     const int local = (b2 ? 4 : 0) + (b3 ? 2 : 0) + (b4 ? 1 : 0);
     if (local >= 7) *value_index = -1;

@@ -2,18 +2,18 @@
 // and FAST-9/16 + NMS (cv::FAST restated).  Integer arithmetic, bit-exact
 // against the oracle (oracle/oracle_image.cpp).
 //
-// Pyramid: one launch per level, batched over every image of a chunk
-// (grid.z = image).  A 256-thread workgroup produces a 64x16 output tile: it
-// stages the (2*16+3) x (2*64+3) source window in LDS with BORDER_REFLECT_101
-// resolved at load time, runs the horizontal 5-tap pass into an int LDS
-// buffer, then the vertical pass.  HBM-bound: algorithmic bytes per image =
-// level-0 read + levels 1..3 written.
+// Pyramid (product path): pyr_down_stream_kernel, one launch per level,
+// batched over every image of a chunk; register-streaming bands (see below).
+// HBM-bound: algorithmic bytes per image = level-0 read + levels 1..3 written
+// (DESIGN.md §4).  pyr_fused3_kernel (one launch for all levels, LDS tiles)
+// is kept for A/B timing (launch_pyramid_frames_fused).
 //
 // FAST: one workgroup per image row y.  It scores rows y-1, y, y+1 from a
 // 9-row LDS window, applies the strict 3x3 NMS to row y and appends the
 // surviving corners in ascending x with a ballot/popcount prefix (row-major
 // order is then restored across rows by fast_compact, an exclusive prefix
 // over per-row counts).
+#include <algorithm>
 #include <vector>
 
 #include "kernels.hpp"
@@ -22,72 +22,20 @@ namespace viso {
 
 namespace {
 
-constexpr int kPyrTileW = 64;
-constexpr int kPyrTileH = 16;
-constexpr int kPyrInW = 2 * kPyrTileW + 3;  // 131
-constexpr int kPyrInH = 2 * kPyrTileH + 3;  // 35
-
 __device__ inline int reflect101(int p, int len) {
     if (len == 1) return 0;
     while (p < 0 || p >= len) p = (p < 0) ? -p : 2 * len - p - 2;
     return p;
 }
 
-struct PyrPtrs {
-    const uint8_t* src[kPyrBatch];
-    uint8_t* dst[kPyrBatch];
-};
-
-__global__ __launch_bounds__(256) void pyr_down_kernel(PyrPtrs ptrs, int sw, int sh, int dw,
-                                                       int dh) {
-    __shared__ uint8_t s_in[kPyrInH][kPyrInW + 1];
-    __shared__ int s_h[kPyrInH][kPyrTileW + 1];
-    const uint8_t* __restrict__ src = ptrs.src[blockIdx.z];
-    uint8_t* __restrict__ dst = ptrs.dst[blockIdx.z];
-    const int ox0 = blockIdx.x * kPyrTileW;
-    const int oy0 = blockIdx.y * kPyrTileH;
-    const int tid = threadIdx.x;
-    const int gx0 = 2 * ox0 - 2, gy0 = 2 * oy0 - 2;
-    // stage the source window (coalesced byte loads along x)
-    for (int idx = tid; idx < kPyrInH * kPyrInW; idx += 256) {
-        int r = idx / kPyrInW, c = idx - r * kPyrInW;
-        int gy = reflect101(gy0 + r, sh);
-        int gx = reflect101(gx0 + c, sw);
-        s_in[r][c] = src[(size_t)gy * sw + gx];
-    }
-    __syncthreads();
-    // horizontal 5-tap at even centres
-    for (int idx = tid; idx < kPyrInH * kPyrTileW; idx += 256) {
-        int r = idx / kPyrTileW, c = idx - r * kPyrTileW;
-        const uint8_t* p = &s_in[r][2 * c];
-        s_h[r][c] = (int)p[0] + 4 * (int)p[1] + 6 * (int)p[2] + 4 * (int)p[3] + (int)p[4];
-    }
-    __syncthreads();
-    // vertical 5-tap + FixPtCast<uchar,8>
-    const int c = tid & 63;
-    for (int r = tid >> 6; r < kPyrTileH; r += 4) {
-        int ox = ox0 + c, oy = oy0 + r;
-        if (ox < dw && oy < dh) {
-            int s = s_h[2 * r][c] + 4 * s_h[2 * r + 1][c] + 6 * s_h[2 * r + 2][c] +
-                    4 * s_h[2 * r + 3][c] + s_h[2 * r + 4][c];
-            dst[(size_t)oy * dw + ox] = (uint8_t)((s + 128) >> 8);
-        }
-    }
-}
-
-// ---------------------------------------------------------------- fused pyramid
+// ---------------------------------------------------------------- fused pyramid (A/B)
 // One workgroup owns a level-3 tile of 16x8 and the matching level-2 (32x16)
-// and level-1 (64x32) tiles.  It stages the level-0 window that feeds them
-// (149 x 85, recursive 5-tap halos) in LDS with 16-byte loads, then runs
-// horizontal/vertical passes level by level entirely in LDS.  Every level's
-// border uses reflect-101 against that level's own (truncated) size, so
-// halo samples are read at reflected coordinates, which always fall inside
-// the window.  Integer math: identical to three separate pyrDown passes.
+// and level-1 (64x32) tiles, staging the level-0 window that feeds them
+// (149 x 85, recursive 5-tap halos) in LDS and filtering level by level.
 constexpr int kF3W = 16, kF3H = 8;
 constexpr int kF2W = 2 * kF3W + 3, kF2H = 2 * kF3H + 3;  // 35 x 19
 constexpr int kF1W = 2 * kF2W + 3, kF1H = 2 * kF2H + 3;  // 73 x 41
 constexpr int kF0W = 2 * kF1W + 3, kF0H = 2 * kF1H + 3;  // 149 x 85
-constexpr int kF0P = 160;                                // LDS pitch of the level-0 window
 
 struct PyrFusedArgs {
     const uint8_t* l0[kPyrBatch];
@@ -96,132 +44,345 @@ struct PyrFusedArgs {
     unsigned long long off[4];
 };
 
-__global__ __launch_bounds__(256) void pyr_fused_kernel(PyrFusedArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t s0[kF0H][kF0P];
-    __shared__ short hs0[kF0H][kF1W];
-    __shared__ uint8_t s1[kF1H][kF1W + 3];
-    __shared__ short hs1[kF1H][kF2W];
-    __shared__ uint8_t s2[kF2H][kF2W + 1];
-    const uint8_t* __restrict__ src = a.l0[blockIdx.z];
-    uint8_t* __restrict__ base = a.slot[blockIdx.z];
-    const int tid = threadIdx.x;
-    const int X3 = blockIdx.x * kF3W, Y3 = blockIdx.y * kF3H;
-    const int ox2 = 2 * X3 - 2, oy2 = 2 * Y3 - 2;
+// Tile details:
+//  * every window (level 0 in LDS as loaded, levels 1 and 2 as computed) is
+//    made valid at its out-of-image positions by copying the reflect-101
+//    partner (per level, against that level's size) once per border tile, so
+//    the filter taps are plain LDS reads at fixed offsets (no per-tap
+//    reflection, no bounds tests);
+//  * level 0 rows are fetched as aligned 16-byte chunks straight into a raw
+//    LDS row (16 bytes of slack either side for the border fill) and read at
+//    a per-row byte offset;
+//  * the horizontal passes produce two adjacent outputs per thread from 7
+//    shared taps.
+// Integer sums are exact, so the result equals three separate pyrDown passes.
+constexpr int kR0P = 16 + 176 + 16;  // raw level-0 row: slack | chunks | slack
+
+// Barrier for LDS hand-offs only (global loads stay in flight across it).
+__device__ inline void lds_barrier_px() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+struct PyrTile {
+    const uint8_t* src;
+    uint8_t* base;
+    int X3, Y3, ox0, oy0, cl, ch;
+};
+
+__device__ inline PyrTile pyr_tile(const PyrFusedArgs& a, int t, int tx, int ty) {
+    PyrTile T;
+    const int per = tx * ty;
+    const int z = t / per, rem = t - z * per;
+    const int by = rem / tx, bx = rem - by * tx;
+    T.src = a.l0[z];
+    T.base = a.slot[z];
+    T.X3 = bx * kF3W;
+    T.Y3 = by * kF3H;
+    const int ox2 = 2 * T.X3 - 2, oy2 = 2 * T.Y3 - 2;
     const int ox1 = 2 * ox2 - 2, oy1 = 2 * oy2 - 2;
-    const int ox0 = 2 * ox1 - 2, oy0 = 2 * oy1 - 2;
+    T.ox0 = 2 * ox1 - 2;
+    T.oy0 = 2 * oy1 - 2;
+    T.cl = max(T.ox0, 0);
+    T.ch = min(T.ox0 + kF0W, a.w[0]);
+    return T;
+}
+
+// Level-0 window chunk j of this thread: row r = it / 11, 16-byte chunk k.
+// The chunk is addressed as src + off (an offset, not a rebuilt pointer, so
+// the load stays a global_load: a flat load would also count in lgkmcnt and
+// be drained by the LDS-only barriers).
+__device__ inline bool pyr_chunk(const PyrFusedArgs& a, const PyrTile& T, int j, int& r, int& k,
+                                 long long& off) {
+    const int it = (int)threadIdx.x + 256 * j;
+    if (it >= kF0H * 11) return false;
+    r = it / 11;
+    k = it - r * 11;
+    const int ys = reflect101(T.oy0 + r, a.h[0]);
+    const long long row = (long long)ys * a.w[0];
+    const long long mis = (long long)(((uintptr_t)T.src + (uintptr_t)(row + T.cl)) & 15);
+    off = row + T.cl - mis + 16 * (long long)k;
+    return off < row + T.ch;
+}
+
+__device__ inline void pyr_issue(const PyrFusedArgs& a, const PyrTile& T, uint4 (&v)[4]) {
+    const long long n = (long long)a.w[0] * a.h[0];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        int r, k;
+        long long off;
+        v[j] = make_uint4(0, 0, 0, 0);
+        if (!pyr_chunk(a, T, j, r, k, off)) continue;
+        if (off >= 0 && off + 16 <= n) {
+            v[j] = *reinterpret_cast<const uint4*>(T.src + off);
+        } else {  // the image's first / last bytes: no read outside the buffer
+            uint32_t wv[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int b = 0; b < 16; ++b)
+                if (off + b >= 0 && off + b < n) wv[b >> 2] |= (uint32_t)T.src[off + b] << (8 * (b & 3));
+            v[j] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+        }
+    }
+}
+
+// Persistent form of the v2 tile: each workgroup walks tiles t, t + grid,
+// ...; the next tile's level-0 chunks are loaded into registers while the
+// current tile is filtered (the passes hand off through LDS-only barriers,
+// so those loads stay in flight).
+__global__ __launch_bounds__(256) void pyr_fused3_kernel(PyrFusedArgs a, int tx, int ty, int total) {
+    __shared__ __attribute__((aligned(16))) uint8_t s0[kF0H][kR0P];
+    __shared__ int s_base[kF0H];
+    __shared__ short hs0[kF0H][kF1W + 1];
+    __shared__ uint8_t s1[kF1H][kF1W + 3];
+    __shared__ short hs1[kF1H][kF2W + 1];
+    __shared__ uint8_t s2[kF2H][kF2W + 1];
+    const int tid = threadIdx.x;
     const int w0 = a.w[0], h0 = a.h[0], w1 = a.w[1], h1 = a.h[1];
     const int w2 = a.w[2], h2 = a.h[2], w3 = a.w[3], h3 = a.h[3];
-    // ---- stage the level-0 window (in-range part), 16-byte aligned chunks
-    {
-        const int c_lo = max(ox0, 0), c_hi = min(ox0 + kF0W, w0);
-        const uintptr_t img_lo = (uintptr_t)src, img_hi = img_lo + (uintptr_t)w0 * h0;
-        const int nchunk = (c_hi > c_lo) ? ((c_hi - c_lo) + 15 + 15) / 16 : 0;
-        for (int it = tid; it < kF0H * nchunk; it += 256) {
-            const int r = it / nchunk, k = it - r * nchunk;
-            const int y = oy0 + r;
-            if (y < 0 || y >= h0) continue;
-            const uintptr_t row = img_lo + (uintptr_t)y * w0;
-            const uintptr_t a0 = ((row + c_lo) & ~(uintptr_t)15) + 16 * (uintptr_t)k;
-            const uintptr_t lo = row + c_lo, hi = row + c_hi;
-            if (a0 >= hi) continue;
-            if (a0 >= img_lo && a0 + 16 <= img_hi) {
-                const uint4 v = *reinterpret_cast<const uint4*>(a0);
-                const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+    int t = blockIdx.x;
+    if (t >= total) return;
+    uint4 v[4];
+    PyrTile T = pyr_tile(a, t, tx, ty);
+    pyr_issue(a, T, v);
+    for (; t < total; t += gridDim.x) {
+        const int X3 = T.X3, Y3 = T.Y3;
+        const int ox2 = 2 * X3 - 2, oy2 = 2 * Y3 - 2;
+        const int ox1 = 2 * ox2 - 2, oy1 = 2 * oy2 - 2;
+        const int ox0 = T.ox0, oy0 = T.oy0;
+        uint8_t* __restrict__ base = T.base;
+        if (tid < kF0H) {
+            const int ys = reflect101(oy0 + tid, h0);
+            const uintptr_t row = (uintptr_t)T.src + (uintptr_t)ys * w0;
+            s_base[tid] = 16 + (int)((row + ox0) - ((row + T.cl) & ~(uintptr_t)15));
+        }
 #pragma unroll
-                for (int b = 0; b < 16; ++b) {
-                    const uintptr_t ad = a0 + b;
-                    if (ad >= lo && ad < hi) s0[r][(int)(ad - row) - ox0] = (uint8_t)(wv[b >> 2] >> (8 * (b & 3)));
-                }
-            } else {
-                for (int b = 0; b < 16; ++b) {
-                    const uintptr_t ad = a0 + b;
-                    if (ad >= lo && ad < hi) s0[r][(int)(ad - row) - ox0] = *reinterpret_cast<const uint8_t*>(ad);
-                }
+        for (int j = 0; j < 4; ++j) {
+            int r, k;
+            long long off;
+            if (pyr_chunk(a, T, j, r, k, off)) *reinterpret_cast<uint4*>(&s0[r][16 + 16 * k]) = v[j];
+        }
+        lds_barrier_px();
+        const bool xborder = ox0 < 0 || ox0 + kF0W > w0;
+        // prefetch the next tile
+        const int tn = t + (int)gridDim.x;
+        if (tn < total) {
+            T = pyr_tile(a, tn, tx, ty);
+            pyr_issue(a, T, v);
+        }
+        if (xborder) {  // out-of-image columns <- reflect-101 partners (same row)
+            for (int it = tid; it < kF0H * kF0W; it += 256) {
+                const int r = it / kF0W, c = it - r * kF0W;
+                const int x = ox0 + c;
+                if (x >= 0 && x < w0) continue;
+                const int b = s_base[r];
+                s0[r][b + c] = s0[r][b + reflect101(x, w0) - ox0];
+            }
+            lds_barrier_px();
+        }
+        // ---- level 1, horizontal: hs0[r][c] for in-image x1 = ox1 + c, two at a time
+        const int c1lo = max(0, -ox1), c1hi = min(kF1W, w1 - ox1);
+#pragma unroll 4
+        for (int it = tid; it < kF0H * 37; it += 256) {
+            const int r = it / 37, c = 2 * (it - r * 37);
+            if (c >= c1hi || c + 1 < c1lo) continue;
+            const uint8_t* p = &s0[r][s_base[r] + 2 * c];
+            const int t0 = p[0], t1 = p[1], t2 = p[2], t3 = p[3], t4 = p[4], t5 = p[5], t6 = p[6];
+            if (c >= c1lo) hs0[r][c] = (short)(t0 + 4 * t1 + 6 * t2 + 4 * t3 + t4);
+            if (c + 1 < c1hi) hs0[r][c + 1] = (short)(t2 + 4 * t3 + 6 * t4 + 4 * t5 + t6);
+        }
+        lds_barrier_px();
+        // ---- level 1, vertical (+ store of the tile's own 64 x 32 core)
+        uint8_t* d1 = base + a.off[1];
+        const int r1lo = max(0, -oy1), r1hi = min(kF1H, h1 - oy1);
+#pragma unroll 4
+        for (int it = tid; it < kF1H * kF1W; it += 256) {
+            const int r = it / kF1W, c = it - r * kF1W;
+            if (r < r1lo || r >= r1hi || c < c1lo || c >= c1hi) continue;
+            const int s = hs0[2 * r][c] + 4 * hs0[2 * r + 1][c] + 6 * hs0[2 * r + 2][c] +
+                          4 * hs0[2 * r + 3][c] + hs0[2 * r + 4][c];
+            const uint8_t o = (uint8_t)((s + 128) >> 8);
+            s1[r][c] = o;
+            const int x1 = ox1 + c, y1 = oy1 + r;
+            if (x1 >= 4 * X3 && x1 < 4 * X3 + 4 * kF3W && y1 >= 4 * Y3 && y1 < 4 * Y3 + 4 * kF3H)
+                d1[(size_t)y1 * w1 + x1] = o;
+        }
+        lds_barrier_px();
+        const bool b1 = c1lo > 0 || c1hi < kF1W || r1lo > 0 || r1hi < kF1H;
+        if (b1) {
+            for (int it = tid; it < kF1H * kF1W; it += 256) {  // columns, in-image rows
+                const int r = it / kF1W, c = it - r * kF1W;
+                if (r < r1lo || r >= r1hi || (c >= c1lo && c < c1hi)) continue;
+                s1[r][c] = s1[r][reflect101(ox1 + c, w1) - ox1];
+            }
+            lds_barrier_px();
+            for (int it = tid; it < kF1H * kF1W; it += 256) {  // whole rows
+                const int r = it / kF1W, c = it - r * kF1W;
+                if (r >= r1lo && r < r1hi) continue;
+                s1[r][c] = s1[reflect101(oy1 + r, h1) - oy1][c];
+            }
+            lds_barrier_px();
+        }
+        // ---- level 2, horizontal
+        const int c2lo = max(0, -ox2), c2hi = min(kF2W, w2 - ox2);
+#pragma unroll 4
+        for (int it = tid; it < kF1H * 18; it += 256) {
+            const int r = it / 18, c = 2 * (it - r * 18);
+            if (c >= c2hi || c + 1 < c2lo) continue;
+            const uint8_t* p = &s1[r][2 * c];
+            const int t0 = p[0], t1 = p[1], t2 = p[2], t3 = p[3], t4 = p[4];
+            if (c >= c2lo) hs1[r][c] = (short)(t0 + 4 * t1 + 6 * t2 + 4 * t3 + t4);
+            if (c + 1 < c2hi) {
+                const int t5 = p[5], t6 = p[6];
+                hs1[r][c + 1] = (short)(t2 + 4 * t3 + 6 * t4 + 4 * t5 + t6);
             }
         }
-    }
-    __syncthreads();
-    // ---- level 1: horizontal pass on every staged row
-    for (int it = tid; it < kF0H * kF1W; it += 256) {
-        const int r = it / kF1W, c = it - r * kF1W;
-        const int y = oy0 + r, x1 = ox1 + c;
-        if (y < 0 || y >= h0 || x1 < 0 || x1 >= w1) continue;
-        int s = 0;
-#pragma unroll
-        for (int j = 0; j < 5; ++j) {
-            const int wgt = j == 2 ? 6 : ((j & 1) ? 4 : 1);
-            s += wgt * (int)s0[r][reflect101(2 * x1 - 2 + j, w0) - ox0];
+        lds_barrier_px();
+        // ---- level 2, vertical (+ 32 x 16 core)
+        uint8_t* d2 = base + a.off[2];
+        const int r2lo = max(0, -oy2), r2hi = min(kF2H, h2 - oy2);
+#pragma unroll 4
+        for (int it = tid; it < kF2H * kF2W; it += 256) {
+            const int r = it / kF2W, c = it - r * kF2W;
+            if (r < r2lo || r >= r2hi || c < c2lo || c >= c2hi) continue;
+            const int s = hs1[2 * r][c] + 4 * hs1[2 * r + 1][c] + 6 * hs1[2 * r + 2][c] +
+                          4 * hs1[2 * r + 3][c] + hs1[2 * r + 4][c];
+            const uint8_t o = (uint8_t)((s + 128) >> 8);
+            s2[r][c] = o;
+            const int x2 = ox2 + c, y2 = oy2 + r;
+            if (x2 >= 2 * X3 && x2 < 2 * X3 + 2 * kF3W && y2 >= 2 * Y3 && y2 < 2 * Y3 + 2 * kF3H)
+                d2[(size_t)y2 * w2 + x2] = o;
         }
-        hs0[r][c] = (short)s;
-    }
-    __syncthreads();
-    uint8_t* d1 = base + a.off[1];
-    for (int it = tid; it < kF1H * kF1W; it += 256) {
-        const int r = it / kF1W, c = it - r * kF1W;
-        const int y1 = oy1 + r, x1 = ox1 + c;
-        if (y1 < 0 || y1 >= h1 || x1 < 0 || x1 >= w1) continue;
-        int s = 0;
-#pragma unroll
-        for (int i = 0; i < 5; ++i) {
-            const int wgt = i == 2 ? 6 : ((i & 1) ? 4 : 1);
-            s += wgt * (int)hs0[reflect101(2 * y1 - 2 + i, h0) - oy0][c];
-        }
-        const uint8_t v = (uint8_t)((s + 128) >> 8);
-        s1[r][c] = v;
-        if (x1 >= 4 * X3 && x1 < 4 * X3 + 4 * kF3W && y1 >= 4 * Y3 && y1 < 4 * Y3 + 4 * kF3H)
-            d1[(size_t)y1 * w1 + x1] = v;
-    }
-    __syncthreads();
-    // ---- level 2
-    for (int it = tid; it < kF1H * kF2W; it += 256) {
-        const int r = it / kF2W, c = it - r * kF2W;
-        const int y1 = oy1 + r, x2 = ox2 + c;
-        if (y1 < 0 || y1 >= h1 || x2 < 0 || x2 >= w2) continue;
-        int s = 0;
-#pragma unroll
-        for (int j = 0; j < 5; ++j) {
-            const int wgt = j == 2 ? 6 : ((j & 1) ? 4 : 1);
-            s += wgt * (int)s1[r][reflect101(2 * x2 - 2 + j, w1) - ox1];
-        }
-        hs1[r][c] = (short)s;
-    }
-    __syncthreads();
-    uint8_t* d2 = base + a.off[2];
-    for (int it = tid; it < kF2H * kF2W; it += 256) {
-        const int r = it / kF2W, c = it - r * kF2W;
-        const int y2 = oy2 + r, x2 = ox2 + c;
-        if (y2 < 0 || y2 >= h2 || x2 < 0 || x2 >= w2) continue;
-        int s = 0;
-#pragma unroll
-        for (int i = 0; i < 5; ++i) {
-            const int wgt = i == 2 ? 6 : ((i & 1) ? 4 : 1);
-            s += wgt * (int)hs1[reflect101(2 * y2 - 2 + i, h1) - oy1][c];
-        }
-        const uint8_t v = (uint8_t)((s + 128) >> 8);
-        s2[r][c] = v;
-        if (x2 >= 2 * X3 && x2 < 2 * X3 + 2 * kF3W && y2 >= 2 * Y3 && y2 < 2 * Y3 + 2 * kF3H)
-            d2[(size_t)y2 * w2 + x2] = v;
-    }
-    __syncthreads();
-    // ---- level 3 (128 outputs, 25 taps each; integer sums are exact)
-    uint8_t* d3 = base + a.off[3];
-    if (tid < kF3W * kF3H) {
-        const int x3 = X3 + (tid & (kF3W - 1)), y3 = Y3 + tid / kF3W;
-        if (x3 < w3 && y3 < h3) {
-            int s = 0;
-#pragma unroll
-            for (int i = 0; i < 5; ++i) {
-                const int wi = i == 2 ? 6 : ((i & 1) ? 4 : 1);
-                const int rr = reflect101(2 * y3 - 2 + i, h2) - oy2;
-                int hsum = 0;
-#pragma unroll
-                for (int j = 0; j < 5; ++j) {
-                    const int wj = j == 2 ? 6 : ((j & 1) ? 4 : 1);
-                    hsum += wj * (int)s2[rr][reflect101(2 * x3 - 2 + j, w2) - ox2];
-                }
-                s += wi * hsum;
+        lds_barrier_px();
+        const bool b2 = c2lo > 0 || c2hi < kF2W || r2lo > 0 || r2hi < kF2H;
+        if (b2) {
+            for (int it = tid; it < kF2H * kF2W; it += 256) {
+                const int r = it / kF2W, c = it - r * kF2W;
+                if (r < r2lo || r >= r2hi || (c >= c2lo && c < c2hi)) continue;
+                s2[r][c] = s2[r][reflect101(ox2 + c, w2) - ox2];
             }
-            d3[(size_t)y3 * w3 + x3] = (uint8_t)((s + 128) >> 8);
+            lds_barrier_px();
+            for (int it = tid; it < kF2H * kF2W; it += 256) {
+                const int r = it / kF2W, c = it - r * kF2W;
+                if (r >= r2lo && r < r2hi) continue;
+                s2[r][c] = s2[reflect101(oy2 + r, h2) - oy2][c];
+            }
+            lds_barrier_px();
+        }
+        // ---- level 3 (16 x 8 outputs, 25 taps each)
+        uint8_t* d3 = base + a.off[3];
+        if (tid < kF3W * kF3H) {
+            const int cx = tid & (kF3W - 1), cy = tid / kF3W;
+            const int x3 = X3 + cx, y3 = Y3 + cy;
+            if (x3 < w3 && y3 < h3) {
+                int s = 0;
+    #pragma unroll
+                for (int i = 0; i < 5; ++i) {
+                    const int wi = i == 2 ? 6 : ((i & 1) ? 4 : 1);
+                    const uint8_t* p = &s2[2 * cy + i][2 * cx];
+                    s += wi * ((int)p[0] + 4 * (int)p[1] + 6 * (int)p[2] + 4 * (int)p[3] + (int)p[4]);
+                }
+                d3[(size_t)y3 * w3 + x3] = (uint8_t)((s + 128) >> 8);
+            }
+        }
+        lds_barrier_px();  // the next tile overwrites the windows
+    }
+}
+
+// ---------------------------------------------------------------- streaming pyrDown
+// One launch per level (L0->L1, L1->L2, L2->L3), batched over images.  A wave
+// owns a strip of 248 destination columns (4 per lane on lanes 0..61) and a
+// band of BH destination rows.  At entry it issues the loads of all 2*BH+3
+// source rows of its band (one 8-byte load per lane and row: 512 contiguous
+// bytes per wave, enough for the strip's 2*248+3 source columns at any
+// alignment), so the band costs one memory round trip; then it walks down the
+// band keeping the horizontal 5-tap sums of the last five source rows in
+// registers.  Each source row is staged through a 512-byte LDS row so every
+// lane can read its 11 taps at offsets with reflect-101 resolved once per
+// wave.  Integer sums are exact: the result is cv::pyrDown's.
+constexpr int kPsW = 248;   // destination columns per wave
+constexpr int kPsRow = 512; // staged source row
+
+struct PyrLevelArgs {
+    const uint8_t* src[kPyrBatch];
+    uint8_t* dst[kPyrBatch];
+    int sw, sh, dw, dh;
+    int bands, units;
+};
+
+// 8 source bytes at offset off, never reading outside [0, n).
+__device__ inline uint2 ps_load(const uint8_t* __restrict__ img, long long off, long long n) {
+    if (off >= 0 && off + 8 <= n) return *reinterpret_cast<const uint2*>(img + off);
+    uint32_t w[2] = {0, 0};
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+        if (off + b >= 0 && off + b < n) w[b >> 2] |= (uint32_t)img[off + b] << (8 * (b & 3));
+    return make_uint2(w[0], w[1]);
+}
+
+template <int BH>
+__global__ __launch_bounds__(256) void pyr_down_stream_kernel(PyrLevelArgs a) {
+    constexpr int NR = 2 * BH + 3;  // source rows of a band
+    __shared__ __attribute__((aligned(16))) uint8_t s_row[4][kPsRow];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int unit = blockIdx.x * 4 + wave;
+    if (unit >= a.units) return;  // waves are independent: no block barrier below
+    const uint8_t* __restrict__ src = a.src[blockIdx.y];
+    uint8_t* __restrict__ dst = a.dst[blockIdx.y];
+    const int sw = a.sw, sh = a.sh, dw = a.dw, dh = a.dh;
+    // consecutive units = consecutive bands of one strip (shared halo rows)
+    const int strip = unit / a.bands, band = unit - strip * a.bands;
+    const int X = strip * kPsW, Y = band * BH;
+    const int rows = min(BH, dh - Y);
+    const long long n = (long long)sw * sh;
+    const int cs = max(2 * X - 2, 0);  // first in-image source column of the strip
+    // ---- all source rows of the band: one 8-byte load per lane and row
+    uint2 v[NR];
+    int mis[NR];
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+        const long long off = (long long)reflect101(2 * Y - 2 + i, sh) * sw + cs;
+        mis[i] = (int)(((uintptr_t)src + (uintptr_t)off) & 7);
+        v[i] = ps_load(src, off - mis[i] + 8 * lane, n);
+    }
+    // per-lane tap offsets (relative to column cs) of source columns
+    // 2X + 8*lane - 2 + k, k < 11, reflect-101 against sw; lanes past the
+    // level's edge read clamped junk that is never stored
+    int P[11];
+#pragma unroll
+    for (int k = 0; k < 11; ++k)
+        P[k] = min(max(reflect101(2 * X + 8 * lane - 2 + k, sw) - cs, 0), kPsRow - 8);
+    uint8_t* row_lds = s_row[wave];
+    auto hsum = [&](uint2 r, int m, int (&h)[4]) {
+        *reinterpret_cast<uint2*>(row_lds + 8 * lane) = r;
+        __builtin_amdgcn_wave_barrier();
+        int t[11];
+#pragma unroll
+        for (int k = 0; k < 11; ++k) t[k] = row_lds[P[k] + m];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            h[q] = t[2 * q] + t[2 * q + 4] + 4 * (t[2 * q + 1] + t[2 * q + 3]) + 6 * t[2 * q + 2];
+        __builtin_amdgcn_wave_barrier();
+    };
+    int H[5][4];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) hsum(v[i], mis[i], H[i]);
+#pragma unroll
+    for (int j = 0; j < BH; ++j) {
+        if (j < rows) {
+            const int y = Y + j;
+            uint8_t* out = dst + (size_t)y * dw + X + 4 * lane;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int s = H[0][q] + H[4][q] + 4 * (H[1][q] + H[3][q]) + 6 * H[2][q];
+                if (lane < kPsW / 4 && X + 4 * lane + q < dw) out[q] = (uint8_t)((s + 128) >> 8);
+            }
+            if (j + 1 < rows) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    H[0][q] = H[2][q];
+                    H[1][q] = H[3][q];
+                    H[2][q] = H[4][q];
+                }
+                hsum(v[5 + 2 * j], mis[5 + 2 * j], H[3]);
+                hsum(v[6 + 2 * j], mis[6 + 2 * j], H[4]);
+            }
         }
     }
 }
@@ -392,6 +553,35 @@ __global__ __launch_bounds__(256) void fast_compact_kernel(const int* __restrict
 
 void launch_pyramid_frames(const PyrGeom& g, const uint8_t* const* l0, uint8_t* const* slot,
                            int n, hipStream_t stream) {
+    for (int b0 = 0; b0 < n; b0 += kPyrBatch) {
+        const int nb = (n - b0) < kPyrBatch ? (n - b0) : kPyrBatch;
+        for (int l = 1; l < kLevels; ++l) {
+            PyrLevelArgs a;
+            for (int i = 0; i < nb; ++i) {
+                a.src[i] = l == 1 ? l0[b0 + i] : slot[b0 + i] + g.off[l - 1];
+                a.dst[i] = slot[b0 + i] + g.off[l];
+            }
+            a.sw = g.w[l - 1];
+            a.sh = g.h[l - 1];
+            a.dw = g.w[l];
+            a.dh = g.h[l];
+            const int bh = l == 1 ? 8 : (l == 2 ? 4 : 2);
+            a.bands = (a.dh + bh - 1) / bh;
+            a.units = a.bands * ((a.dw + kPsW - 1) / kPsW);
+            const dim3 grid((a.units + 3) / 4, nb);
+            if (l == 1)
+                pyr_down_stream_kernel<8><<<grid, 256, 0, stream>>>(a);
+            else if (l == 2)
+                pyr_down_stream_kernel<4><<<grid, 256, 0, stream>>>(a);
+            else
+                pyr_down_stream_kernel<2><<<grid, 256, 0, stream>>>(a);
+        }
+    }
+}
+
+// Fused single-launch form (pyr_fused3_kernel), kept for A/B timing.
+void launch_pyramid_frames_fused(const PyrGeom& g, const uint8_t* const* l0, uint8_t* const* slot,
+                                 int n, hipStream_t stream) {
     auto cdiv = [](int a, int b) { return (a + b - 1) / b; };
     const int tx = std::max(cdiv(g.w[3], kF3W), std::max(cdiv(g.w[2], 2 * kF3W), cdiv(g.w[1], 4 * kF3W)));
     const int ty = std::max(cdiv(g.h[3], kF3H), std::max(cdiv(g.h[2], 2 * kF3H), cdiv(g.h[1], 4 * kF3H)));
@@ -407,24 +597,8 @@ void launch_pyramid_frames(const PyrGeom& g, const uint8_t* const* l0, uint8_t* 
             a.l0[i] = l0[b0 + i];
             a.slot[i] = slot[b0 + i];
         }
-        pyr_fused_kernel<<<dim3(tx, ty, nb), 256, 0, stream>>>(a);
-    }
-}
-
-// Reference (unfused) form: one launch per level; kept for A/B timing.
-void launch_pyramid_frames_unfused(const PyrGeom& g, const uint8_t* const* l0,
-                                   uint8_t* const* slot, int n, hipStream_t stream) {
-    for (int b0 = 0; b0 < n; b0 += kPyrBatch) {
-        const int nb = (n - b0) < kPyrBatch ? (n - b0) : kPyrBatch;
-        for (int l = 1; l < kLevels; ++l) {
-            PyrPtrs p;
-            for (int i = 0; i < nb; ++i) {
-                p.src[i] = l == 1 ? l0[b0 + i] : slot[b0 + i] + g.off[l - 1];
-                p.dst[i] = slot[b0 + i] + g.off[l];
-            }
-            dim3 grid((g.w[l] + kPyrTileW - 1) / kPyrTileW, (g.h[l] + kPyrTileH - 1) / kPyrTileH, nb);
-            pyr_down_kernel<<<grid, 256, 0, stream>>>(p, g.w[l - 1], g.h[l - 1], g.w[l], g.h[l]);
-        }
+        const int total = tx * ty * nb;
+        pyr_fused3_kernel<<<std::min(total, 1024), 256, 0, stream>>>(a, tx, ty, total);
     }
 }
 

@@ -18,6 +18,11 @@
 #include "device_math.hpp"
 #include "kernels.hpp"
 
+#ifdef VISO_PROBE
+// [level] iterations summed, [4 + level] calls, [8 + level] window misses
+__device__ unsigned long long g_probe_lk[16];
+#endif
+
 namespace viso {
 
 namespace {
@@ -25,6 +30,7 @@ namespace {
 struct LkResult {
     double dx, dy;
     bool succ;
+    int iters;
 };
 
 // Per-wave LDS window of the current image around the patch's starting
@@ -102,7 +108,8 @@ __device__ inline LkResult lk_level(const uint8_t* __restrict__ img1, int w1, in
     const double i00 = H11 * invdet, i10 = -H10 * invdet, i01 = -H01 * invdet, i11 = H00 * invdet;
     double cost = 0, lastCost = 0;
     bool succ = true;
-    for (int iter = 0; iter < MAXIT; ++iter) {
+    int iter = 0;
+    for (; iter < MAXIT; ++iter) {
         bool out;
         if (KLT_BOUNDS) {  // src/viso.cpp:286
             out = bx + dx <= hp || bx + dx >= w1 - hp || by + dy <= hp || by + dy >= h1 - hp;
@@ -130,7 +137,7 @@ __device__ inline LkResult lk_level(const uint8_t* __restrict__ img1, int w1, in
         lastCost = cost;
         succ = !(lastCost > thresh);
     }
-    return {dx, dy, succ};
+    return {dx, dy, succ, iter};
 }
 
 __global__ __launch_bounds__(256) void klt_kernel(FrameDev ref, FrameDev cur, PyrDev g,
@@ -238,6 +245,12 @@ __global__ __launch_bounds__(256) void lk_align_kernel(LkAlignArgs a) {
                                                   ry, cx, cy, bu * s, bv * s, 0.0, 0.0, a.thresh,
                                                   win);
                 succ = r.succ;
+#ifdef VISO_PROBE
+                if (lane == 0) {
+                    atomicAdd(&g_probe_lk[level], (unsigned long long)r.iters);
+                    atomicAdd(&g_probe_lk[4 + level], 1ull);
+                }
+#endif
                 cu = cu + r.dx / s;  // pair.uv_cur += V2d{dx/s, dy/s}
                 cv = cv + r.dy / s;
             }
@@ -308,3 +321,15 @@ void launch_lk_align(const LkAlignArgs& a, hipStream_t stream) {
 }
 
 }  // namespace viso
+
+#ifdef VISO_PROBE
+extern "C" int viso_debug_probe_lk(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_probe_lk), sizeof(unsigned long long) * 16) != hipSuccess)
+        return -2;
+    if (reset) {
+        static unsigned long long zero[16] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_probe_lk), zero, sizeof(zero)) != hipSuccess) return -2;
+    }
+    return 0;
+}
+#endif
