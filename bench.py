@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--width", type=int, default=1242)
     ap.add_argument("--height", type=int, default=375)
     ap.add_argument("--batch", type=int, default=50, help="frames per batched ingest call")
-    ap.add_argument("--cpu-frames", type=int, default=60,
+    ap.add_argument("--cpu-frames", type=int, default=200,
                     help="timed tracking frames of the CPU oracle sample (0 = skip)")
     ap.add_argument("--no-cpu", action="store_true")
     return ap.parse_args()
@@ -145,9 +145,21 @@ def main():
         imgs_per_launch = 2 * args.steps / timing["pyramid"]["launches"]
         bytes_per_launch = algo_bytes_img * imgs_per_launch
         achieved = bytes_per_launch / (timing["pyramid"]["avg_ms"] * 1e-3) / 1e9
-        roofline = {"kernel": "pyr_down_stream_kernel x3 (batched image pass; algorithmic bytes = L0 read + L1..L3 write)", "bound": "hbm",
+        # HBM traffic from the committed rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
+        # passes over this benchmark (tools/pmc_traffic.py; 100-image chunks),
+        # scaled to this run's images per launch
+        traffic = None
+        tfile = os.path.join(ROOT, "profiles", "r01_pyramid_traffic.json")
+        if os.path.exists(tfile):
+            with open(tfile) as fh:
+                t = json.load(fh)
+            traffic = int(t["traffic_bytes_per_launch"] / 100 * imgs_per_launch)
+        roofline = {"kernel": "pyr_down_stream_kernel x3 (batched image pass; algorithmic bytes = "
+                              "L0 read + L1..L3 write)", "bound": "hbm",
                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "traffic_source": "profiles/r01_pyramid_traffic.json (PMC, x2 FETCH correction)"
+                    if traffic else None,
                     "algorithmic_bytes_per_launch": int(bytes_per_launch),
                     "images_per_launch": imgs_per_launch}
     st = v.stats()
