@@ -78,7 +78,8 @@ def main():
     from viso_amd.synth import Sequence
 
     W, H = args.width, args.height
-    n_total = args.warmup + args.steps
+    n_break = args.batch  # one extra chunk after the timed region: per-kernel breakdown
+    n_total = args.warmup + args.steps + n_break
     seq = Sequence(W, H, seed=sequence_seed(rank))
     t0 = time.time()
     left = np.stack([seq.image(f, 0) for f in range(n_total)])
@@ -91,6 +92,10 @@ def main():
 
     v = viso_amd.Viso(*seq.K, width=W, height=H, device=local, enable_tracking=1,
                       batch_frames=args.batch, max_poses=max(1024, n_total + 16))
+    # inside the timed region only the per-chunk groups are bracketed by HIP
+    # events (the image pass for the roofline, the LK-alignment batch); the
+    # per-frame kernels are timed in a separate chunk afterwards
+    v.ctx.timing_select(["pyramid", "lkalign"])
 
     def run(f0, n):
         f = f0
@@ -131,10 +136,23 @@ def main():
 
     # ---------------------------------------------------------- kernel timing
     timing = {}
-    for k in ("pyramid", "fast", "klt", "ransac", "direct", "lkalign"):
+    for k in ("pyramid", "lkalign"):
         n_l, ms = v.ctx.timing(k)
         if n_l:
             timing[k] = {"launches": n_l, "avg_ms": ms / n_l, "total_ms": ms}
+    # per-kernel breakdown: one more chunk with every kernel group timed
+    v.ctx.timing_enable(False)
+    v.ctx.timing_select(None)
+    v.ctx.timing_enable(True)
+    run(args.warmup + args.steps, n_break)
+    v.synchronize()
+    breakdown = {}
+    for k in ("pyramid", "direct", "lkalign"):
+        n_l, ms = v.ctx.timing(k)
+        n0 = timing.get(k, {}).get("launches", 0)
+        ms0 = timing.get(k, {}).get("total_ms", 0.0)
+        if n_l - n0 > 0:
+            breakdown[k] = {"launches": n_l - n0, "avg_ms": round((ms - ms0) / (n_l - n0), 5)}
     dims, total_bytes = viso_amd.pyramid_dims(W, H)
     algo_bytes_img = dims[0][0] * dims[0][1] + sum(w * h for w, h in dims[1:])
     roofline = None
@@ -208,6 +226,7 @@ def main():
             "speedup_vs_cpu": round(value / world / cpu["value"], 1) if cpu else None,
             "kernels": {k: {"launches": t["launches"], "avg_ms": round(t["avg_ms"], 5)}
                         for k, t in timing.items()},
+            "kernels_breakdown_chunk": breakdown,
             "last_frame_stats": {"direct_nGood": st[9], "lk_pairs": st[6], "lk_success": st[7]},
         }
         print(json.dumps(out), flush=True)

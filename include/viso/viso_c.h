@@ -131,6 +131,9 @@ int viso_get_frame_stats(viso_ctx* ctx, double stats[16]);
 #define VISO_KERNEL_STEREO 7
 #define VISO_KERNEL_COUNT 8
 int viso_timing_enable(viso_ctx* ctx, int32_t enable);
+/* Restrict timing to the kernels whose bit (1 << VISO_KERNEL_*) is set
+ * (default: all).  Each timed region records two events on its stream. */
+int viso_timing_select(viso_ctx* ctx, uint32_t kernel_mask);
 int viso_timing_get(viso_ctx* ctx, int32_t kernel, int64_t* launches, double* total_ms);
 
 /* ------------------------------------------------------------------------

@@ -65,6 +65,7 @@ SIGNATURES = {
     "viso_get_alignment": [_vp, _vp, _vp, _vp, _vp, _sz, _vp],
     "viso_get_frame_stats": [_vp, _vp],
     "viso_timing_enable": [_vp, _i32],
+    "viso_timing_select": [_vp, ctypes.c_uint32],
     "viso_timing_get": [_vp, _i32, _vp, _vp],
     "viso_pyramid_dims": [_i32, _i32, _vp, _vp],
     "viso_pyramid": [_vp, _vp, _i32, _i32, _i32, _vp],

@@ -168,6 +168,11 @@ class Context:
     def timing_enable(self, on: bool = True):
         _lib.call("viso_timing_enable", self.h, 1 if on else 0)
 
+    def timing_select(self, kernels=None):
+        """Time only the named kernels (None: all)."""
+        mask = 0xFFFFFFFF if kernels is None else sum(1 << _lib.KERNEL_IDS[k] for k in kernels)
+        _lib.call("viso_timing_select", self.h, mask)
+
     def timing(self, kernel: str):
         launches = ctypes.c_int64(0)
         ms = ctypes.c_double(0.0)

@@ -133,6 +133,12 @@ int viso_timing_enable(viso_ctx* c, int32_t enable) {
     return VISO_OK;
 }
 
+int viso_timing_select(viso_ctx* c, uint32_t kernel_mask) {
+    if (!c) return VISO_ERR_ARG;
+    c->timing.mask = kernel_mask;
+    return VISO_OK;
+}
+
 int viso_timing_get(viso_ctx* c, int32_t kernel, int64_t* launches, double* total_ms) {
     if (!c || kernel < 0 || kernel >= VISO_KERNEL_COUNT) return VISO_ERR_ARG;
     int rc = c->timing.collect();

@@ -21,6 +21,8 @@ struct DevBuf {
 // HIP-event timing of selected kernels on the context stream.
 struct Timing {
     bool enabled = false;
+    uint32_t mask = 0xffffffffu;  // kernel ids timed when enabled
+    bool on(int kernel) const { return enabled && ((mask >> kernel) & 1u); }
     int64_t launches[VISO_KERNEL_COUNT] = {};
     double total_ms[VISO_KERNEL_COUNT] = {};
     struct Pending {
@@ -82,14 +84,14 @@ struct TimedRegion {
     hipStream_t s;
     hipEvent_t a = nullptr, b = nullptr;
     TimedRegion(Timing& t_, int k, hipStream_t s_) : t(t_), kernel(k), s(s_) {
-        if (t.enabled) {
+        if (t.on(kernel)) {
             a = t.get_event();
             b = t.get_event();
             (void)hipEventRecord(a, s);
         }
     }
     ~TimedRegion() {
-        if (t.enabled && a && b) {
+        if (a && b) {
             (void)hipEventRecord(b, s);
             t.pending.push_back({kernel, a, b});
         }
@@ -164,6 +166,9 @@ struct viso_ctx {
     std::vector<int> lk_pending;
     int lk_last_rows = 0;  // frames in the last launched batch
     viso::DevBuf lk_pair, lk_succ, lk_before, lk_after;  // kLkBatch x kMaxMapPoints
+    // per-map LK templates (keyframe choice + per-level template / H^-1),
+    // computed once when the map is created (launch_lk_template)
+    viso::DevBuf lk_tmpl, lk_tmpl_h, lk_tmpl_kf, lk_tmpl_uv;
     hipStream_t lk_stream = nullptr;
     hipEvent_t lk_ring[viso::kLkRing] = {};  // recorded after each lk_stream batch
     int64_t lk_seq = 0;                      // lk_stream batches launched
@@ -192,4 +197,6 @@ struct viso_ctx {
     int ingest_host(const uint8_t* grey, int32_t w, int32_t h, int32_t stride, int* slot_out);
     // launch LKAlignment of every pending tracking frame (on `s`)
     int flush_lk(hipStream_t s);
+    // LKAlignment arguments common to the template and alignment launches
+    viso::LkAlignArgs lk_args();
 };

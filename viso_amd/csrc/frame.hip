@@ -165,7 +165,8 @@ void viso_ctx::release() {
     DevBuf* bufs[] = {&scratch_a, &scratch_b, &scratch_c, &scratch_d, &slot_pool, &slot_pose,
                       &kp1, &kp2, &kp1b, &kp2b, &track_success, &n_track_dev, &fast_rows,
                       &geo_buf, &map_pts, &kf_poses, &direct_buf, &direct_stats,
-                      &lk_pair, &lk_succ, &lk_before, &lk_after, &pose_log};
+                      &lk_pair, &lk_succ, &lk_before, &lk_after, &lk_tmpl, &lk_tmpl_h,
+                      &lk_tmpl_kf, &lk_tmpl_uv, &pose_log};
     for (DevBuf* b : bufs) b->release();
     if (h_ctl) (void)hipHostFree(h_ctl);
     if (h_int) (void)hipHostFree(h_int);
@@ -243,18 +244,12 @@ int viso_ctx::ingest_host(const uint8_t* grey, int32_t w, int32_t h, int32_t str
 }
 
 // ------------------------------------------------------------------ LKAlignment batch
-int viso_ctx::flush_lk(hipStream_t ls) {
-    if (lk_pending.empty()) return VISO_OK;
+LkAlignArgs viso_ctx::lk_args() {
     const PyrGeom& g = geom;
     LkAlignArgs a{};
     a.n_kf = (int)kf_slots.size();
     for (int j = 0; j < a.n_kf; ++j) a.kf[j] = frame(kf_slots[(size_t)j]);
     a.kf_poses = (const double*)kf_poses.ptr;
-    a.n_frames = (int)lk_pending.size();
-    for (int f = 0; f < a.n_frames; ++f) {
-        a.frames[f].cur = frame(lk_pending[(size_t)f]);
-        a.frames[f].pose = pose_of(lk_pending[(size_t)f]);
-    }
     a.points = (const double*)map_pts.ptr;
     a.n = n_map;
     a.K[0] = p.fx;
@@ -266,6 +261,21 @@ int viso_ctx::flush_lk(hipStream_t ls) {
         a.g.w[l] = g.w[l];
         a.g.h[l] = g.h[l];
         a.g.off[l] = g.off[l];
+    }
+    a.tmpl = (double*)lk_tmpl.ptr;
+    a.tmpl_h = (double*)lk_tmpl_h.ptr;
+    a.tmpl_kf = (int32_t*)lk_tmpl_kf.ptr;
+    a.tmpl_uv = (double*)lk_tmpl_uv.ptr;
+    return a;
+}
+
+int viso_ctx::flush_lk(hipStream_t ls) {
+    if (lk_pending.empty()) return VISO_OK;
+    LkAlignArgs a = lk_args();
+    a.n_frames = (int)lk_pending.size();
+    for (int f = 0; f < a.n_frames; ++f) {
+        a.frames[f].cur = frame(lk_pending[(size_t)f]);
+        a.frames[f].pose = pose_of(lk_pending[(size_t)f]);
     }
     a.out_stride = kMaxMapPoints;
     a.pair_kf = (int32_t*)lk_pair.ptr;
@@ -371,6 +381,16 @@ int viso_ctx::on_new_frame(int cur) {
                     for (size_t j = 0; j < kf_slots.size(); ++j)
                         VISO_HIP_CHECK(hipMemcpyAsync((char*)kf_poses.ptr + 96 * j, pose_of(kf_slots[j]),
                                                       96, hipMemcpyDeviceToDevice, stream));
+                    // LK-alignment templates of the new map (constant while tracking)
+                    {
+                        const size_t m = (size_t)std::max(n_map, 1);
+                        int rc = lk_tmpl.ensure(m * kLevels * 192 * 8);
+                        if (!rc) rc = lk_tmpl_h.ensure(m * kLevels * 4 * 8);
+                        if (!rc) rc = lk_tmpl_kf.ensure(m * 4);
+                        if (!rc) rc = lk_tmpl_uv.ensure(m * 16);
+                        if (rc) return rc;
+                        launch_lk_template(lk_args(), stream);
+                    }
                     state = p.enable_tracking ? VISO_STATE_RUNNING : VISO_STATE_FINISHED;
                     stats[12] = 1;
                     counted = false;  // `break` skips ++frame_cnt (src/viso.cpp:98)

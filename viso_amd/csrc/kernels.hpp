@@ -66,8 +66,15 @@ struct LkAlignArgs {
     uint8_t* success;
     double* uv_before;  // 2 per point
     double* uv_after;
+    // per-map templates (lk_template_kernel); tmpl == nullptr: computed inline
+    double* tmpl = nullptr;    // [n][4 levels][3][64]
+    double* tmpl_h = nullptr;  // [n][4][4]
+    int32_t* tmpl_kf = nullptr;
+    double* tmpl_uv = nullptr;  // [n][2]
 };
 void launch_lk_align(const LkAlignArgs& a, hipStream_t stream);
+// Keyframe choice + per-level templates of every map point (once per map).
+void launch_lk_template(const LkAlignArgs& a, hipStream_t stream);
 
 // ---------------------------------------------------------------- stereo (north star)
 void launch_stereo_sad(const uint8_t* left, const uint8_t* right, int w, int h, const int* xs,

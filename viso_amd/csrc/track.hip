@@ -85,27 +85,46 @@ __device__ inline double sample_win(const uint8_t* __restrict__ img, int w, int 
     return sample_px(img, w, h, x, y);
 }
 
-// One level of the inverse-compositional LK used by both engines.
-//   ref_x/ref_y: template coordinate of THIS lane's pixel (already offset);
-//   cur_x/cur_y: current-image coordinate of this lane's pixel without d;
-//   bound_x/bound_y: coordinate whose +d is bounds-checked (per engine).
-template <int MAXIT, bool KLT_BOUNDS>
-__device__ inline LkResult lk_level(const uint8_t* __restrict__ img1, int w1, int h1,
-                                    const uint8_t* __restrict__ img2, int w2, int h2,
-                                    double ref_x, double ref_y, double cur_x, double cur_y,
-                                    double bx, double by, double dx, double dy, double thresh,
-                                    const Window& win) {
-    const double hp = 4.0;
+// The per-level template of the inverse-compositional LK: this lane's
+// template value I1 and Jacobian (J0, J1) = -grad at ref, and the 2x2 inverse
+// of H = sum J J^T (canonical wave trees).  It depends only on the reference
+// image and the template position, so LK alignment precomputes it once per
+// map (lk_template_kernel) instead of per frame.
+struct LkTemplate {
+    double I1, J0, J1;
+    double i00, i01, i10, i11;
+};
+
+__device__ inline LkTemplate lk_prepare(const uint8_t* __restrict__ img1, int w1, int h1,
+                                        double ref_x, double ref_y) {
+    LkTemplate t;
     double gx, gy;
     gradient_px(img1, w1, h1, ref_x, ref_y, gx, gy);
-    const double J0 = -gx, J1 = -gy;
-    const double I1 = sample_px(img1, w1, h1, ref_x, ref_y);
-    const double H00 = wave_tree_sum_dpp(J0 * J0);
-    const double H01 = wave_tree_sum_dpp(J0 * J1);
-    const double H11 = wave_tree_sum_dpp(J1 * J1);
+    t.J0 = -gx;
+    t.J1 = -gy;
+    t.I1 = sample_px(img1, w1, h1, ref_x, ref_y);
+    const double H00 = wave_tree_sum_dpp(t.J0 * t.J0);
+    const double H01 = wave_tree_sum_dpp(t.J0 * t.J1);
+    const double H11 = wave_tree_sum_dpp(t.J1 * t.J1);
     const double H10 = H01;  // J1*J0 == J0*J1 leaf by leaf
     const double invdet = 1.0 / (H00 * H11 - H10 * H01);
-    const double i00 = H11 * invdet, i10 = -H10 * invdet, i01 = -H01 * invdet, i11 = H00 * invdet;
+    t.i00 = H11 * invdet;
+    t.i10 = -H10 * invdet;
+    t.i01 = -H01 * invdet;
+    t.i11 = H00 * invdet;
+    return t;
+}
+
+// The GN iterations of one level.
+//   cur_x/cur_y: current-image coordinate of this lane's pixel without d;
+//   bx/by: coordinate whose +d is bounds-checked (per engine); w1/h1: the
+//   size the bounds test uses.
+template <int MAXIT, bool KLT_BOUNDS>
+__device__ inline LkResult lk_iterate(const LkTemplate& t, int w1, int h1,
+                                      const uint8_t* __restrict__ img2, int w2, int h2,
+                                      double cur_x, double cur_y, double bx, double by, double dx,
+                                      double dy, double thresh, const Window& win) {
+    const double hp = 4.0;
     double cost = 0, lastCost = 0;
     bool succ = true;
     int iter = 0;
@@ -121,12 +140,12 @@ __device__ inline LkResult lk_level(const uint8_t* __restrict__ img1, int w1, in
             succ = false;
             break;
         }
-        const double e = I1 - sample_win(img2, w2, h2, cur_x + dx, cur_y + dy, win);
-        const double B0 = wave_tree_sum_dpp(-J0 * e);
-        const double B1 = wave_tree_sum_dpp(-J1 * e);
+        const double e = t.I1 - sample_win(img2, w2, h2, cur_x + dx, cur_y + dy, win);
+        const double B0 = wave_tree_sum_dpp(-t.J0 * e);
+        const double B1 = wave_tree_sum_dpp(-t.J1 * e);
         cost = wave_tree_sum_dpp(e * e);
-        const double u0 = i00 * B0 + i01 * B1;
-        const double u1 = i10 * B0 + i11 * B1;
+        const double u0 = t.i00 * B0 + t.i01 * B1;
+        const double u1 = t.i10 * B0 + t.i11 * B1;
         if (isnan(u0)) {
             succ = false;
             break;
@@ -138,6 +157,19 @@ __device__ inline LkResult lk_level(const uint8_t* __restrict__ img1, int w1, in
         succ = !(lastCost > thresh);
     }
     return {dx, dy, succ, iter};
+}
+
+// One level of the inverse-compositional LK used by both engines.
+//   ref_x/ref_y: template coordinate of THIS lane's pixel (already offset).
+template <int MAXIT, bool KLT_BOUNDS>
+__device__ inline LkResult lk_level(const uint8_t* __restrict__ img1, int w1, int h1,
+                                    const uint8_t* __restrict__ img2, int w2, int h2,
+                                    double ref_x, double ref_y, double cur_x, double cur_y,
+                                    double bx, double by, double dx, double dy, double thresh,
+                                    const Window& win) {
+    const LkTemplate t = lk_prepare(img1, w1, h1, ref_x, ref_y);
+    return lk_iterate<MAXIT, KLT_BOUNDS>(t, w1, h1, img2, w2, h2, cur_x, cur_y, bx, by, dx, dy,
+                                         thresh, win);
 }
 
 __global__ __launch_bounds__(256) void klt_kernel(FrameDev ref, FrameDev cur, PyrDev g,
@@ -181,6 +213,85 @@ __global__ __launch_bounds__(256) void klt_kernel(FrameDev ref, FrameDev cur, Py
     }
 }
 
+// Keyframe choice of one map point (LKAlignment, src/viso.cpp:774-800):
+// the keyframe with the smallest viewing angle (Keyframe::ViewingAngle,
+// include/keyframe.h:93-98) among those the point projects into.  It does
+// not depend on the current frame.
+__device__ inline int lk_choose_kf(const LkAlignArgs& a, const double* P, double& bu, double& bv) {
+    const Intrinsics K{a.K[0], a.K[1], a.K[2], a.K[3]};
+    const int w0 = a.g.w[0], h0 = a.g.h[0];
+    double best_angle = 180.0;
+    int kf = -1;
+    bu = 0;
+    bv = 0;
+    const double kPi = 3.14159265358979323846;
+    for (int j = 0; j < a.n_kf; ++j) {
+        const double* kp = a.kf_poses + 12 * j;
+        double ur, vr;
+        project_px(kp, K, P, 1.0, ur, vr);
+        if (!inside_px(ur, vr, w0, h0)) continue;
+        double Pc[3];
+        mat3_vec(kp, P, Pc);
+        Pc[0] = Pc[0] + kp[9];
+        Pc[1] = Pc[1] + kp[10];
+        Pc[2] = Pc[2] + kp[11];
+        const double nrm = (Pc[0] * Pc[0] + Pc[1] * Pc[1]) + Pc[2] * Pc[2];
+        if (nrm > 0) {
+            const double sn = sqrt(nrm);
+            Pc[0] = Pc[0] / sn;
+            Pc[1] = Pc[1] / sn;
+            Pc[2] = Pc[2] / sn;
+        }
+        const double angle = fabs(acos(Pc[2]) / kPi * 180);
+        if (angle > 180.0 || angle > best_angle) continue;
+        best_angle = angle;
+        kf = j;
+        bu = ur;
+        bv = vr;
+    }
+    return kf;
+}
+
+// Per map point, once per map: the keyframe choice and the four levels'
+// templates (lk_prepare) of LK alignment.  tmpl layout: [point][level]
+// [I1 | J0 | J1][64 lanes]; tmpl_h: [point][level][i00, i01, i10, i11].
+__global__ __launch_bounds__(256) void lk_template_kernel(LkAlignArgs a) {
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= a.n) return;  // wave-uniform
+    const int lane = threadIdx.x & 63;
+    const int px = (lane >> 3) - 4, py = (lane & 7) - 4;
+    const double P[3] = {a.points[3 * i], a.points[3 * i + 1], a.points[3 * i + 2]};
+    double bu, bv;
+    const int kf = lk_choose_kf(a, P, bu, bv);
+    if (lane == 0) {
+        a.tmpl_kf[i] = kf;
+        a.tmpl_uv[2 * i] = bu;
+        a.tmpl_uv[2 * i + 1] = bv;
+    }
+    if (kf < 0) return;
+    const FrameDev refp = a.kf[kf];
+    for (int level = kLevels - 1; level >= 0; --level) {
+        const double s = kScale[level];
+        const int w = a.g.w[level], h = a.g.h[level];
+        const LkTemplate t = lk_prepare(refp.l[level], w, h, bu * s + px, bv * s + py);
+        double* d = a.tmpl + ((size_t)i * kLevels + level) * 192;
+        d[lane] = t.I1;
+        d[64 + lane] = t.J0;
+        d[128 + lane] = t.J1;
+        if (lane == 0) {
+            double* hh = a.tmpl_h + ((size_t)i * kLevels + level) * 4;
+            hh[0] = t.i00;
+            hh[1] = t.i01;
+            hh[2] = t.i10;
+            hh[3] = t.i11;
+        }
+    }
+}
+
+// LKAlignment over the frames of a batch (blockIdx.y = frame).  Blocks along
+// x are point groups; the grid's x extent is a multiple of 8, so a point
+// group stays on one XCD for every frame and its templates stay in that
+// XCD's L2.
 __global__ __launch_bounds__(256) void lk_align_kernel(LkAlignArgs a) {
     __shared__ uint8_t s_win[4][kWinW * kWinH];
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -202,32 +313,13 @@ __global__ __launch_bounds__(256) void lk_align_kernel(LkAlignArgs a) {
     double uc, vc;
     project_px(cur_pose, K, P, 1.0, uc, vc);
     if (inside_px(uc, vc, w0, h0)) {  // current_frame->IsInside(Pw, 0)
-        double best_angle = 180.0;
-        double bu = 0, bv = 0;
-        const double kPi = 3.14159265358979323846;
-        for (int j = 0; j < a.n_kf; ++j) {
-            const double* kp = a.kf_poses + 12 * j;
-            double ur, vr;
-            project_px(kp, K, P, 1.0, ur, vr);
-            if (!inside_px(ur, vr, w0, h0)) continue;
-            double Pc[3];
-            mat3_vec(kp, P, Pc);
-            Pc[0] = Pc[0] + kp[9];
-            Pc[1] = Pc[1] + kp[10];
-            Pc[2] = Pc[2] + kp[11];
-            const double nrm = (Pc[0] * Pc[0] + Pc[1] * Pc[1]) + Pc[2] * Pc[2];
-            if (nrm > 0) {
-                const double s = sqrt(nrm);
-                Pc[0] = Pc[0] / s;
-                Pc[1] = Pc[1] / s;
-                Pc[2] = Pc[2] / s;
-            }
-            const double angle = fabs(acos(Pc[2]) / kPi * 180);
-            if (angle > 180.0 || angle > best_angle) continue;
-            best_angle = angle;
-            kf = j;
-            bu = ur;
-            bv = vr;
+        double bu, bv;
+        if (a.tmpl) {
+            kf = a.tmpl_kf[i];
+            bu = a.tmpl_uv[2 * i];
+            bv = a.tmpl_uv[2 * i + 1];
+        } else {
+            kf = lk_choose_kf(a, P, bu, bv);
         }
         if (kf >= 0) {
             ub[0] = uc;
@@ -238,12 +330,24 @@ __global__ __launch_bounds__(256) void lk_align_kernel(LkAlignArgs a) {
             for (int level = kLevels - 1; level >= 0; --level) {
                 const double s = kScale[level];
                 const int w = a.g.w[level], h = a.g.h[level];
-                const double rx = bu * s + px, ry = bv * s + py;
                 const double cx = cu * s + px, cy = cv * s + py;
                 const Window win = load_window(my_win, cur.l[level], w, h, cu * s, cv * s);
-                LkResult r = lk_level<100, false>(refp.l[level], w, h, cur.l[level], w, h, rx,
-                                                  ry, cx, cy, bu * s, bv * s, 0.0, 0.0, a.thresh,
-                                                  win);
+                LkTemplate t;
+                if (a.tmpl) {
+                    const double* d = a.tmpl + ((size_t)i * kLevels + level) * 192;
+                    const double* hh = a.tmpl_h + ((size_t)i * kLevels + level) * 4;
+                    t.I1 = d[lane];
+                    t.J0 = d[64 + lane];
+                    t.J1 = d[128 + lane];
+                    t.i00 = hh[0];
+                    t.i01 = hh[1];
+                    t.i10 = hh[2];
+                    t.i11 = hh[3];
+                } else {
+                    t = lk_prepare(refp.l[level], w, h, bu * s + px, bv * s + py);
+                }
+                LkResult r = lk_iterate<100, false>(t, w, h, cur.l[level], w, h, cx, cy, bu * s,
+                                                    bv * s, 0.0, 0.0, a.thresh, win);
                 succ = r.succ;
 #ifdef VISO_PROBE
                 if (lane == 0) {
@@ -317,7 +421,13 @@ void launch_klt(const FrameDev& ref, const FrameDev& cur, const PyrGeom& g, cons
 
 void launch_lk_align(const LkAlignArgs& a, hipStream_t stream) {
     if (a.n <= 0 || a.n_frames <= 0) return;
-    lk_align_kernel<<<dim3((a.n + 3) / 4, a.n_frames), 256, 0, stream>>>(a);
+    const int gx = (((a.n + 3) / 4) + 7) / 8 * 8;  // multiple of 8: XCD-stable point groups
+    lk_align_kernel<<<dim3(gx, a.n_frames), 256, 0, stream>>>(a);
+}
+
+void launch_lk_template(const LkAlignArgs& a, hipStream_t stream) {
+    if (a.n <= 0) return;
+    lk_template_kernel<<<(a.n + 3) / 4, 256, 0, stream>>>(a);
 }
 
 }  // namespace viso
