@@ -172,6 +172,11 @@ struct viso_ctx {
     hipStream_t lk_stream = nullptr;
     hipEvent_t lk_ring[viso::kLkRing] = {};  // recorded after each lk_stream batch
     int64_t lk_seq = 0;                      // lk_stream batches launched
+    // The last tracking frame's final direct-pose solve (F) is deferred: it
+    // runs fused into the next tracking frame's L(3), or alone when the
+    // ingest call ends (resolve_direct).  Its frame and `last` slots are held.
+    bool dpend = false;
+    int dpend_cur = -1, dpend_last = -1, dpend_log = -1;
     viso::DevBuf pose_log;  // max_poses x 12
     int n_poses = 0;
 
@@ -197,6 +202,10 @@ struct viso_ctx {
     int ingest_host(const uint8_t* grey, int32_t w, int32_t h, int32_t stride, int* slot_out);
     // launch LKAlignment of every pending tracking frame (on `s`)
     int flush_lk(hipStream_t s);
+    // launch the pending final solve, if any
+    int resolve_direct();
+    // end of an ingest call: pending final solve, then the LK batch on `s`
+    int finish_call(hipStream_t s);
     // LKAlignment arguments common to the template and alignment launches
     viso::LkAlignArgs lk_args();
 };

@@ -74,14 +74,32 @@ constexpr int kMaxTile = kMaxMapPoints / kMaxTiles;  // 64 points
 constexpr int kStats = 50;
 constexpr int kStateStride = 8;
 
-struct DirectArgs {
+// The two frames of one DirectPoseEstimation call and the `last` pose the
+// patches are taken at (Keyframe::Project of last_frame, src/viso.cpp:697).
+struct FramePair {
     FrameDev last;
     FrameDev cur;
+    const double* pose_last;  // 12 doubles (may point into LDS)
+};
+
+// One level of a FramePair (the per-level image pointers resolved once, so no
+// local copy of a FrameDev array is ever indexed at run time).
+struct LevelPair {
+    const uint8_t* last;
+    const uint8_t* cur;
+    const double* pose_last;
+};
+
+__device__ inline LevelPair level_pair(const FramePair& fp, int lv) {
+    return LevelPair{fp.last.l[lv], fp.cur.l[lv], fp.pose_last};
+}
+
+struct DirectArgs {
+    FramePair fp;
     PyrDev g;
     Intrinsics K;
     const double* points;
     int n;
-    const double* pose_last;  // `last` frame pose: patch reference (12)
     const double* pose_seed;  // level 3 starts at SE3(R, t) of this pose (12)
     int level;                // tiles of this level; -1: final solve only
     int tile;                 // points per tile (power of two, >= kWaves)
@@ -91,6 +109,14 @@ struct DirectArgs {
     double* pose_out;  // result pose (12) or null
     double* log;
     int log_index;  // < 0: no log append
+    // L(3) fused with the previous frame's final solve (merged != 0): the
+    // prologue solves the previous frame's level 0, writes its pose (+ log),
+    // and seeds T21 from it (it is this frame's `last` pose)
+    int merged;
+    FramePair prev;  // the previous frame's pair (its rare continuation)
+    double* prev_pose_out;
+    double* prev_log;
+    int prev_log_index;
 };
 
 // dPixeldXi (src/viso.cpp:640-658)
@@ -132,7 +158,8 @@ struct RefSample {
     bool ok;
 };
 
-__device__ inline void ref_issue(const DirectArgs& a, int lv, int i, RefSample& r) {
+__device__ inline void ref_issue(const DirectArgs& a, const LevelPair& fp, int lv, int i,
+                                 RefSample& r) {
     const int lane = threadIdx.x & 63;
     const int px = (lane >> 3) - 4, py = (lane & 7) - 4;
     const double scale = kScale[lv];
@@ -140,11 +167,11 @@ __device__ inline void ref_issue(const DirectArgs& a, int lv, int i, RefSample& 
     r.P[0] = a.points[3 * i];
     r.P[1] = a.points[3 * i + 1];
     r.P[2] = a.points[3 * i + 2];
-    project_px(a.pose_last, a.K, r.P, scale, r.ur, r.vr);
+    project_px(fp.pose_last, a.K, r.P, scale, r.ur, r.vr);
     const double hp = 4.0;
     r.ok = inside_px(r.ur - hp, r.vr - hp, w, h) && inside_px(r.ur + hp, r.vr + hp, w, h);
     const double x = r.ur + px, y = r.vr + py;
-    const uint8_t* img = a.last.l[lv];
+    const uint8_t* img = fp.last;
     const long long n = (long long)w * (long long)h;
     const long long base = r.ok ? (long long)(int)y * (long long)w + (long long)(int)x : -(1LL << 40);
     r.t0 = (base >= 0 && base < n) ? img[base] : 0;
@@ -163,8 +190,9 @@ __device__ inline void ref_finish(RefSample& r) {
                   : 0.0;
 }
 
-__device__ inline void ref_sample(const DirectArgs& a, int lv, int i, RefSample& r) {
-    ref_issue(a, lv, i, r);
+__device__ inline void ref_sample(const DirectArgs& a, const LevelPair& fp, int lv, int i,
+                                  RefSample& r) {
+    ref_issue(a, fp, lv, i, r);
     ref_finish(r);
 }
 
@@ -232,7 +260,8 @@ __device__ inline double sample_cw(const uint8_t* __restrict__ img, int w, int h
 
 // The 28 sums of one map point by reduce-scatter: returns good; lane l < 32
 // with *idx >= 0 holds sum *idx in *out.
-__device__ inline bool direct_point_rs(const DirectArgs& a, int lv, const double* cur_pose,
+__device__ inline bool direct_point_rs(const DirectArgs& a, const LevelPair& fp, int lv,
+                                       const double* cur_pose,
                                        const RefSample& r, const uint8_t* win, const CurWin& cw,
                                        double* out, int* idx) {
     const int lane = threadIdx.x & 63;
@@ -246,7 +275,7 @@ __device__ inline bool direct_point_rs(const DirectArgs& a, int lv, const double
     if (!good) return false;
     double Jp[12];
     d_pixel_d_xi(a.K, cur_pose, r.P, scale, Jp);
-    const uint8_t* C = a.cur.l[lv];
+    const uint8_t* C = fp.cur;
     const double x = uc + px, y = vc + py;
     const double error = r.lval - sample_cw(C, w, h, x, y, win, cw);
     // GetGradient (include/keyframe.h:57-64)
@@ -271,7 +300,8 @@ __device__ inline bool direct_point_rs(const DirectArgs& a, int lv, const double
 // Tile b of level lv (a.tile points) -> part[b][28], good[b].  Called by
 // every thread of the workgroup.  `pre` (may be null) is the prefetched
 // RefSample of this wave's first point of the tile (valid when has_pre).
-__device__ void direct_tile(const DirectArgs& a, int lv, const double* cur_pose, int b,
+__device__ void direct_tile(const DirectArgs& a, const LevelPair& fp, int lv, const double* cur_pose,
+                            int b,
                             const RefSample& pre, bool has_pre, const uint8_t* win,
                             const CurWin& cw, double* part, int* good, double* s_pts,
                             int* s_good, bool zeroed = false) {
@@ -289,12 +319,12 @@ __device__ void direct_tile(const DirectArgs& a, int lv, const double* cur_pose,
         bool ok = false;
         if (i < a.n) {
             if (has_pre && local == wave) {
-                ok = direct_point_rs(a, lv, cur_pose, pre, win, cw, &f, &idx);
+                ok = direct_point_rs(a, fp, lv, cur_pose, pre, win, cw, &f, &idx);
             } else {
                 RefSample r;
-                ref_sample(a, lv, i, r);
+                ref_sample(a, fp, lv, i, r);
                 CurWin none{};
-                ok = direct_point_rs(a, lv, cur_pose, r, nullptr, none, &f, &idx);
+                ok = direct_point_rs(a, fp, lv, cur_pose, r, nullptr, none, &f, &idx);
             }
         }
         if (!ok) {
@@ -548,11 +578,9 @@ __device__ void solve_wave0(SolveLds& L, int iter, double* stats, int probe_base
 }
 
 // Continuation (faithful, rare): this workgroup re-evaluates every tile of
-// level lv at T21 = state into its own scratch.  Out of line: it keeps the
-// common path's register allocation small.
-__device__ void continue_tiles(const DirectArgs& a, int lv,
-                                                         const double* state, double* s_pose,
-                                                         double* s_pts, int* s_good) {
+// level lv of frame pair fp at T21 = state into its own scratch.
+__device__ void continue_tiles(const DirectArgs& a, const LevelPair& fp, int lv,
+                               const double* state, double* s_pose, double* s_pts, int* s_good) {
     double* part = a.s.cont_part + (size_t)blockIdx.x * kMaxTiles * kSums;
     int* good = a.s.cont_good + (size_t)blockIdx.x * kMaxTiles;
     if (threadIdx.x == 0) state_to_pose(state, s_pose);
@@ -562,7 +590,7 @@ __device__ void continue_tiles(const DirectArgs& a, int lv,
     RefSample none{};
     CurWin off{};
     for (int b = 0; b < a.n_tiles; ++b)
-        direct_tile(a, lv, pose, b, none, false, nullptr, off, part, good, s_pts, s_good);
+        direct_tile(a, fp, lv, pose, b, none, false, nullptr, off, part, good, s_pts, s_good);
     __threadfence_block();
     __syncthreads();
 }
@@ -574,11 +602,11 @@ __device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_b
 
 // GN iterations 1.. of level lv (the faithful continuation, rare): every
 // workgroup re-evaluates all tiles itself at the new T21 and solves again.
-__device__ void solve_continue(const DirectArgs& a, int lv, SolveLds& L, double* stats,
-                               double* s_pose, double* s_pts, int* s_good) {
+__device__ void solve_continue(const DirectArgs& a, const LevelPair& fp, int lv, SolveLds& L,
+                               double* stats, double* s_pose, double* s_pts, int* s_good) {
     const int t = threadIdx.x, wave = t >> 6;
     for (int iter = 1; iter < 100 && L.cont; ++iter) {
-        continue_tiles(a, lv, L.state, s_pose, s_pts, s_good);
+        continue_tiles(a, fp, lv, L.state, s_pose, s_pts, s_good);
         double v[kSums];
         int gg = 0;
         if (t < 256)
@@ -592,36 +620,66 @@ __device__ void solve_continue(const DirectArgs& a, int lv, SolveLds& L, double*
 
 // Issue the T21-independent loads of map point i: the `last` patch taps and
 // the current-image window around its projection under the predicted T21
-// (the pose `prev` was evaluated at, or the seed).
-__device__ inline void prefetch_point(const DirectArgs& a, int lv, int i, bool solve, int prev,
+// (the pose level sl was evaluated at, or the seed).  In a merged L(3) the
+// `last` pose is solved in the same launch, so its taps are issued again
+// after the solve; the early ones (projected with the stale pose, bounds-
+// checked) are discarded.
+__device__ inline void prefetch_point(const DirectArgs& a, int lv, int i, bool solve, int sl,
                                       RefSample& r, CurWin& cw) {
-    ref_issue(a, lv, i, r);
+    ref_issue(a, level_pair(a.fp, lv), lv, i, r);
     double pred[12];
     if (!solve) {
         for (int k = 0; k < 12; ++k) pred[k] = a.pose_seed[k];
     } else {
         double sp[7];
-        for (int k = 0; k < 7; ++k) sp[k] = a.s.state[prev * kStateStride + k];
+        for (int k = 0; k < 7; ++k) sp[k] = a.s.state[sl * kStateStride + k];
         state_to_pose(sp, pred);
     }
     double up, vp;
     project_px(pred, a.K, r.P, kScale[lv], up, vp);
-    win_issue(a.cur.l[lv], a.g.w[lv], a.g.h[lv], up, vp, cw);
+    win_issue(a.fp.cur.l[lv], a.g.w[lv], a.g.h[lv], up, vp, cw);
+}
+
+// After the solve of level sl: in a merged L(3), the solved T21 is the
+// previous frame's pose -> written out (block 0), kept in LDS as this
+// frame's `last` pose, and the seed SE3(R, t) of it becomes T21.  Then the
+// pose the tiles are evaluated at.  One thread.
+__device__ inline void after_solve(const DirectArgs& a, bool merged, SolveLds& L, double* s_last,
+                                   double* s_pose) {
+    if (merged) {
+        state_to_pose(L.state, s_last);
+        if (blockIdx.x == 0) {
+            for (int k = 0; k < 7; ++k) a.s.state[kLevels * kStateStride + k] = L.state[k];
+            if (a.prev_pose_out)
+                for (int k = 0; k < 12; ++k) a.prev_pose_out[k] = s_last[k];
+            if (a.prev_log && a.prev_log_index >= 0)
+                for (int k = 0; k < 12; ++k) a.prev_log[12 * (size_t)a.prev_log_index + k] = s_last[k];
+        }
+        // Sophus::SE3d(R, t) of last_frame (src/viso.cpp:114)
+        double q[4];
+        quat_from_matrix(s_last, q);
+        for (int k = 0; k < 4; ++k) L.state[k] = q[k];
+        L.state[4] = s_last[9];
+        L.state[5] = s_last[10];
+        L.state[6] = s_last[11];
+    }
+    state_to_pose(L.state, s_pose);
 }
 
 // L(level) and F (level = -1).
-//   Wave 0 is the solver: it reduces its quarter of the tile partials of
-//   `prev`, waits on an LDS arrival count for waves 1-3 (the other quarters)
-//   and thread 256 (the T21 `prev` was evaluated at), then solves.  No block
-//   barrier sits in front of the solve, so the other waves' prefetches (their
-//   map point, `last` patch taps and current-image window; wave 4 also
-//   prefetches wave 0's point) stay off its path.  B2 (block barrier) hands
-//   the new pose to every wave; then the tiles.
+//   Wave 0 is the solver: it reduces its quarter of the tile partials of the
+//   solved level, waits on an LDS arrival count for waves 1-3 (the other
+//   quarters) and thread 256 (the T21 that level was evaluated at), then
+//   solves.  No block barrier sits in front of the solve, so the other waves'
+//   prefetches (their map point, `last` patch taps and current-image window;
+//   wave 4 also prefetches wave 0's point) stay off its path.  B2 (block
+//   barrier) hands the new pose to every wave; then the tiles.
 __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
     PROBE_T0();
     PROBE_ABS(64 + 4 * (a.level + 1));
     __shared__ SolveLds L;
     __shared__ double s_pose[12];
+    __shared__ double s_last[12];  // merged L(3): this frame's `last` pose
     __shared__ double s_pts[kMaxTile * kSums];
     __shared__ int s_good;
     __shared__ int s_arrive;
@@ -629,21 +687,23 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
     __shared__ double s_lval0[64];  // wave 0's point, prefetched by wave 4
     __shared__ int s_ok0, s_cw0[3];
     const int lv = a.level;
-    const int prev = lv + 1;  // level solved in the prologue (kLevels: seeded)
+    const bool merged = a.merged && lv == kLevels - 1;
+    const int prev = lv + 1;
+    const bool solve = prev < kLevels || merged;
+    const int sl = merged ? 0 : prev;  // level solved in the prologue
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const bool tiles = lv >= 0 && (int)blockIdx.x < a.n_tiles;
-    const bool solve = prev < kLevels;
     if (t == 0) {
         s_arrive = 0;
         s_good = 0;
     }
     lds_barrier();  // nothing is in flight yet
 
-    // ---- partials of `prev` (waves 0-3) and the starting T21 (thread 256)
+    // ---- partials of level sl (waves 0-3) and the starting T21 (thread 256)
     double v[kSums];
     int gg = 0;
     if (solve && t < 256)
-        load_partials(a.s.part + (size_t)prev * kMaxTiles * kSums, a.s.good + prev * kMaxTiles,
+        load_partials(a.s.part + (size_t)sl * kMaxTiles * kSums, a.s.good + sl * kMaxTiles,
                       a.n_tiles, v, gg);
     if (t == 256) {
         double st[7];
@@ -654,7 +714,7 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
             st[5] = a.pose_seed[10];
             st[6] = a.pose_seed[11];
         } else {
-            for (int k = 0; k < 7; ++k) st[k] = a.s.state[prev * kStateStride + k];
+            for (int k = 0; k < 7; ++k) st[k] = a.s.state[sl * kStateStride + k];
         }
         for (int k = 0; k < 7; ++k) {
             L.state[k] = st[k];
@@ -678,22 +738,24 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
     PROBE(32 + 6 * (lv + 1));
 
     // ---- prefetches (every wave but the solver)
-    RefSample pre;
+    RefSample pre{};
     CurWin cw{};
     const int i0 = (int)blockIdx.x * a.tile + wave;
     const bool has_pre = tiles && wave < a.tile && i0 < a.n;
     const bool solver = solve && wave == 0;
     if (has_pre && !solver) {
-        prefetch_point(a, lv, i0, solve, prev, pre, cw);
-        ref_finish(pre);
+        prefetch_point(a, lv, i0, solve, sl, pre, cw);
+        if (!merged) ref_finish(pre);
         if (cw.on) win_store(s_win[wave], cw);
     }
     if (solve && wave == 4 && tiles && a.tile > 0 && (int)blockIdx.x * a.tile < a.n) {
-        RefSample r0;
+        RefSample r0{};
         CurWin c0{};
-        prefetch_point(a, lv, (int)blockIdx.x * a.tile, solve, prev, r0, c0);
-        ref_finish(r0);
-        s_lval0[lane] = r0.lval;
+        prefetch_point(a, lv, (int)blockIdx.x * a.tile, solve, sl, r0, c0);
+        if (!merged) {
+            ref_finish(r0);
+            s_lval0[lane] = r0.lval;
+        }
         if (c0.on) win_store(s_win[0], c0);
         if (lane == 0) {
             s_ok0 = r0.ok ? 1 : 0;
@@ -717,7 +779,7 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
         if (lane < kSums) L.S[lane] = (L.red[0][lane] + L.red[1][lane]) + (L.red[2][lane] + L.red[3][lane]);
         if (lane == 0) L.ngood = (L.g[0] + L.g[1]) + (L.g[2] + L.g[3]);
         PROBE(32 + 6 * (lv + 1) + 1);
-        double* stp = (a.stats && blockIdx.x == 0) ? a.stats + (size_t)kStats * prev : nullptr;
+        double* stp = (a.stats && blockIdx.x == 0) ? a.stats + (size_t)kStats * sl : nullptr;
 #ifdef VISO_PROBE
         solve_wave0(L, 0, stp, lv == 1 ? 90 : -1, probe_t0);
 #else
@@ -730,28 +792,31 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
         while (__hip_atomic_load(&s_arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 1)
             __builtin_amdgcn_s_sleep(1);
     }
-    if (wave == 0 && lane == 0) state_to_pose(L.state, s_pose);
+    if (wave == 0 && lane == 0 && !L.cont) after_solve(a, merged, L, s_last, s_pose);
     __syncthreads();  // B2
-    if (solver && has_pre) {
-        pre.ok = s_ok0 != 0;
-        pre.lval = s_lval0[lane];
-        cw.x0 = s_cw0[0];
-        cw.y0 = s_cw0[1];
-        cw.on = s_cw0[2] != 0;
-    }
     if (solve && L.cont) {
         // the continuation needs every thread; it leaves s_good dirty
-        double* stp = (a.stats && blockIdx.x == 0) ? a.stats + (size_t)kStats * prev : nullptr;
-        solve_continue(a, prev, L, stp, s_pose, s_pts, &s_good);
+        double* stp = (a.stats && blockIdx.x == 0) ? a.stats + (size_t)kStats * sl : nullptr;
+        const LevelPair cfp = merged ? level_pair(a.prev, sl) : level_pair(a.fp, sl);
+        solve_continue(a, cfp, sl, L, stp, s_pose, s_pts, &s_good);
         if (t == 0) {
-            state_to_pose(L.state, s_pose);
+            after_solve(a, merged, L, s_last, s_pose);
             s_good = 0;
         }
         __syncthreads();
     }
+    if (solver && has_pre && !merged) {
+        pre.ok = s_ok0 != 0;
+        pre.lval = s_lval0[lane];
+    }
+    if (solver && has_pre) {
+        cw.x0 = s_cw0[0];
+        cw.y0 = s_cw0[1];
+        cw.on = s_cw0[2] != 0;
+    }
     PROBE(lv + 1);
     const int out = lv >= 0 ? lv : kLevels;
-    if (blockIdx.x == 0 && t == 0) {
+    if (blockIdx.x == 0 && t == 0 && !merged) {
         for (int k = 0; k < 7; ++k) a.s.state[out * kStateStride + k] = L.state[k];
         if (lv < 0 && a.pose_out) {
             for (int k = 0; k < 12; ++k) a.pose_out[k] = s_pose[k];
@@ -759,11 +824,22 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
                 for (int k = 0; k < 12; ++k) a.log[12 * (size_t)a.log_index + k] = s_pose[k];
         }
     }
+    if (blockIdx.x == 0 && t == 0 && merged)
+        for (int k = 0; k < 7; ++k) a.s.state[lv * kStateStride + k] = L.state[k];
     if (tiles) {
+        LevelPair fp = level_pair(a.fp, lv);
+        if (merged) {
+            // `last` pose solved above: the patch taps are read now
+            fp.pose_last = s_last;
+            if (has_pre) {
+                ref_issue(a, fp, lv, i0, pre);
+                ref_finish(pre);
+            }
+        }
         double pose[12];
 #pragma unroll
         for (int k = 0; k < 12; ++k) pose[k] = s_pose[k];
-        direct_tile(a, lv, pose, blockIdx.x, pre, has_pre, s_win[wave], cw,
+        direct_tile(a, fp, lv, pose, blockIdx.x, pre, has_pre, s_win[wave], cw,
                     a.s.part + (size_t)lv * kMaxTiles * kSums, a.s.good + lv * kMaxTiles, s_pts,
                     &s_good, true);
     }
@@ -814,19 +890,18 @@ DirectScratch direct_scratch_at(void* base) {
     return s;
 }
 
-void launch_direct_pose(const FrameDev& last_pyr, const FrameDev& cur_pyr, const PyrGeom& g,
-                        const double K[4], const double* points, int n,
-                        const double* pose_last12, const double* pose_seed12,
-                        const DirectScratch& s, double* stats, double* pose_out, double* log,
-                        int log_index, hipStream_t stream) {
-    DirectArgs a;
-    a.last = last_pyr;
-    a.cur = cur_pyr;
+namespace {
+DirectArgs direct_args(const FrameDev& last_pyr, const FrameDev& cur_pyr, const PyrGeom& g,
+                       const double K[4], const double* points, int n, const double* pose_last12,
+                       const double* pose_seed12, const DirectScratch& s, double* stats) {
+    DirectArgs a{};
+    a.fp.last = last_pyr;
+    a.fp.cur = cur_pyr;
+    a.fp.pose_last = pose_last12;
     a.g = make_pyrdev(g);
     a.K = Intrinsics{K[0], K[1], K[2], K[3]};
     a.points = points;
     a.n = n;
-    a.pose_last = pose_last12;
     a.pose_seed = pose_seed12;
     int P = 1;
     while (P < n) P <<= 1;
@@ -834,16 +909,58 @@ void launch_direct_pose(const FrameDev& last_pyr, const FrameDev& cur_pyr, const
     a.n_tiles = (n + a.tile - 1) / a.tile;
     a.s = s;
     a.stats = stats;
-    a.pose_out = pose_out;
-    a.log = log;
-    a.log_index = log ? log_index : -1;
+    a.log_index = -1;
+    a.prev_log_index = -1;
+    return a;
+}
+}  // namespace
+
+void launch_direct_levels(const FrameDev& last_pyr, const FrameDev& cur_pyr, const PyrGeom& g,
+                          const double K[4], const double* points, int n,
+                          const double* pose_last12, const double* pose_seed12,
+                          const DirectScratch& s, double* stats, const DirectPrev* merge,
+                          hipStream_t stream) {
+    DirectArgs a = direct_args(last_pyr, cur_pyr, g, K, points, n, pose_last12, pose_seed12, s,
+                               stats);
+    if (merge) {
+        a.merged = 1;
+        a.prev.last = merge->last;
+        a.prev.cur = merge->cur;
+        a.prev.pose_last = merge->pose_last12;
+        a.prev_pose_out = merge->pose_out;
+        a.prev_log = merge->log;
+        a.prev_log_index = merge->log ? merge->log_index : -1;
+    }
     const int grid = a.n_tiles > 0 ? a.n_tiles : 1;
     for (int level = kLevels - 1; level >= 0; --level) {
         a.level = level;
         direct_level_kernel<<<grid, kThreads, 0, stream>>>(a);
+        a.merged = 0;
     }
+}
+
+void launch_direct_final(const FrameDev& last_pyr, const FrameDev& cur_pyr, const PyrGeom& g,
+                         const double K[4], const double* points, int n,
+                         const double* pose_last12, const DirectScratch& s, double* stats,
+                         double* pose_out, double* log, int log_index, hipStream_t stream) {
+    DirectArgs a = direct_args(last_pyr, cur_pyr, g, K, points, n, pose_last12, pose_last12, s,
+                               stats);
+    a.pose_out = pose_out;
+    a.log = log;
+    a.log_index = log ? log_index : -1;
     a.level = -1;
     direct_level_kernel<<<1, kThreads, 0, stream>>>(a);
+}
+
+void launch_direct_pose(const FrameDev& last_pyr, const FrameDev& cur_pyr, const PyrGeom& g,
+                        const double K[4], const double* points, int n,
+                        const double* pose_last12, const double* pose_seed12,
+                        const DirectScratch& s, double* stats, double* pose_out, double* log,
+                        int log_index, hipStream_t stream) {
+    launch_direct_levels(last_pyr, cur_pyr, g, K, points, n, pose_last12, pose_seed12, s, stats,
+                         nullptr, stream);
+    launch_direct_final(last_pyr, cur_pyr, g, K, points, n, pose_last12, s, stats, pose_out, log,
+                        log_index, stream);
 }
 
 }  // namespace viso

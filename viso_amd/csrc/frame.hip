@@ -309,6 +309,26 @@ int viso_ctx::flush_lk(hipStream_t ls) {
     return VISO_OK;
 }
 
+int viso_ctx::resolve_direct() {
+    if (!dpend) return VISO_OK;
+    const double K[4] = {p.fx, p.fy, p.cx, p.cy};
+    launch_direct_final(frame(dpend_last), frame(dpend_cur), geom, K, (const double*)map_pts.ptr,
+                        n_map, pose_of(dpend_last), direct, (double*)direct_stats.ptr,
+                        pose_of(dpend_cur), dpend_log >= 0 ? (double*)pose_log.ptr : nullptr,
+                        dpend_log, stream);
+    VISO_HIP_CHECK(hipGetLastError());
+    drop(dpend_cur);
+    drop(dpend_last);
+    dpend = false;
+    return VISO_OK;
+}
+
+int viso_ctx::finish_call(hipStream_t ls) {
+    int rc = resolve_direct();
+    if (rc) return rc;
+    return flush_lk(ls);
+}
+
 // ------------------------------------------------------------------ OnNewFrame
 int viso_ctx::on_new_frame(int cur) {
     const PyrGeom& g = geom;
@@ -424,21 +444,42 @@ int viso_ctx::on_new_frame(int cur) {
             // Sophus::SE3d X(last_frame->GetR(), last_frame->GetT()) (src/viso.cpp:114) is
             // seeded inside level 3; level 0 writes cur_frame->SetR/SetT(X) and
             // poses.push_back(X) (src/viso.cpp:117-118, 137)
+            // (the previous tracking frame's final solve, if pending, runs
+            // fused into this frame's level 3: its pose is this frame's
+            // last_frame pose)
             const bool log = n_poses < p.max_poses;
             {
                 TimedRegion t(timing, VISO_KERNEL_DIRECT, stream);
-                launch_direct_pose(frame(last_slot), frame(cur), g, K, (const double*)map_pts.ptr,
-                                   n_map, pose_of(last_slot), pose_of(last_slot), direct,
-                                   (double*)direct_stats.ptr, pose_of(cur),
-                                   log ? (double*)pose_log.ptr : nullptr, n_poses, stream);
+                DirectPrev m{};
+                if (dpend) {
+                    m.last = frame(dpend_last);
+                    m.cur = frame(dpend_cur);
+                    m.pose_last12 = pose_of(dpend_last);
+                    m.pose_out = pose_of(dpend_cur);
+                    m.log = dpend_log >= 0 ? (double*)pose_log.ptr : nullptr;
+                    m.log_index = dpend_log;
+                }
+                launch_direct_levels(frame(last_slot), frame(cur), g, K, (const double*)map_pts.ptr,
+                                     n_map, pose_of(last_slot), pose_of(last_slot), direct,
+                                     (double*)direct_stats.ptr, dpend ? &m : nullptr, stream);
             }
+            if (dpend) {
+                drop(dpend_cur);
+                drop(dpend_last);
+            }
+            dpend = true;
+            dpend_cur = cur;
+            dpend_last = last_slot;
+            hold(cur);
+            hold(last_slot);
+            dpend_log = log ? n_poses : -1;
             if (log) ++n_poses;
             // LKAlignment (src/viso.cpp:121, 768-843): queued for the batched
             // launch at the end of this ingest call
             hold(cur);
             lk_pending.push_back(cur);
             if ((int)lk_pending.size() == kLkBatch) {
-                int rc = flush_lk(stream);
+                int rc = finish_call(stream);
                 if (rc) return rc;
             }
             ran_tracking = true;
@@ -477,7 +518,7 @@ int viso_process_frame(viso_ctx* c, const uint8_t* grey, int32_t width, int32_t 
     VISO_HIP_CHECK(hipGetLastError());
     rc = c->on_new_frame(s);
     if (rc) return rc;
-    return c->flush_lk(c->lk_stream);
+    return c->finish_call(c->lk_stream);
 }
 
 int viso_process_stereo(viso_ctx* c, const uint8_t* left, const uint8_t* right,
@@ -506,7 +547,7 @@ int viso_process_stereo(viso_ctx* c, const uint8_t* left, const uint8_t* right,
     c->drop(sr);
     rc = c->on_new_frame(sl);
     if (rc) return rc;
-    return c->flush_lk(c->lk_stream);
+    return c->finish_call(c->lk_stream);
 }
 
 int viso_process_frames_device(viso_ctx* c, const uint8_t* d_left, const uint8_t* d_right,
@@ -548,8 +589,8 @@ int viso_process_frames_device(viso_ctx* c, const uint8_t* d_left, const uint8_t
             int rc = c->on_new_frame(sl[(size_t)i]);
             if (rc) return rc;
         }
-        // the chunk's LKAlignment batch, behind its direct-pose chain
-        int rc = c->flush_lk(c->stream);
+        // the last frame's final solve, then the chunk's LKAlignment batch
+        int rc = c->finish_call(c->stream);
         if (rc) return rc;
         // frames still referenced after the chunk get their own level 0
         int roles[3] = {c->ref_slot, c->last_slot, -1};

@@ -108,6 +108,27 @@ void launch_direct_pose(const FrameDev& last, const FrameDev& cur, const PyrGeom
                         const double* pose_last12, const double* pose_seed12,
                         const DirectScratch& s, double* stats, double* pose_out, double* log,
                         int log_index, hipStream_t stream);
+// The same call split for the frame pipeline: L(3..0) of this frame, then F
+// later.  With `merge`, L(3) also runs the previous frame's pending F (its
+// level-0 solve; the solved pose is this frame's `last` pose and seed, so
+// pose_last12 / pose_seed12 are read only by L(2..0), after L(3) wrote them
+// to merge->pose_out).
+struct DirectPrev {
+    FrameDev last, cur;         // the previous frame's pair (rare continuation)
+    const double* pose_last12;  // its `last` pose
+    double* pose_out;           // its pose (= this frame's pose_last12)
+    double* log;
+    int log_index;
+};
+void launch_direct_levels(const FrameDev& last, const FrameDev& cur, const PyrGeom& g,
+                          const double K[4], const double* points, int n,
+                          const double* pose_last12, const double* pose_seed12,
+                          const DirectScratch& s, double* stats, const DirectPrev* merge,
+                          hipStream_t stream);
+void launch_direct_final(const FrameDev& last, const FrameDev& cur, const PyrGeom& g,
+                         const double K[4], const double* points, int n,
+                         const double* pose_last12, const DirectScratch& s, double* stats,
+                         double* pose_out, double* log, int log_index, hipStream_t stream);
 // dst (12 doubles, device) <- src (host values, passed by value)
 void launch_set_pose(double* dst, const double src[12], hipStream_t stream);
 
