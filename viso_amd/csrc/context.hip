@@ -97,7 +97,7 @@ int viso_create(const viso_params* p, int device, viso_ctx** out) {
     c->p = *p;
     c->device = device;
     c->geom = make_geom(p->width, p->height);
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (c->create_streams() != VISO_OK) {
         delete c;
         return VISO_ERR_HIP;
     }

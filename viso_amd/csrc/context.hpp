@@ -1,6 +1,7 @@
 // viso_amd — context object behind the C ABI.
 #pragma once
 
+#include <deque>
 #include <vector>
 
 #include "../../include/viso/viso_c.h"
@@ -126,7 +127,7 @@ struct viso_ctx {
     viso::DevBuf slot_pool;   // n_slots x geom.slot bytes
     viso::DevBuf slot_pose;   // n_slots x 12 doubles (Keyframe R_, T_)
     std::vector<viso::SlotRec> slots;
-    std::vector<int> free_slots;
+    std::deque<int> free_slots;  // FIFO: the longest-free slot is reused first
     int ref_slot = -1, last_slot = -1;  // init_.ref_frame, last_frame
     std::vector<int> kf_slots;          // Map::keyframes_
 
@@ -186,6 +187,7 @@ struct viso_ctx {
     double stats[16] = {0};
     bool ran_tracking = false;
 
+    int create_streams();
     int init();
     void release();
     // frame pool

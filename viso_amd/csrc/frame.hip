@@ -51,13 +51,15 @@ const double kIdentityPose[12] = {1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0};
 int viso_ctx::init() {
     const PyrGeom& g = geom;
     const int cap = p.max_features;
+    // left + right of a chunk, roles; the free list is FIFO (the longest-free
+    // slot is reused first, so side-stream LK reads are long finished)
     n_slots = 2 * p.batch_frames + 8;
     int rc = slot_pool.ensure(g.slot * (size_t)n_slots);
     if (!rc) rc = slot_pose.ensure(sizeof(double) * 12 * (size_t)n_slots);
     if (rc) return rc;
     slots.assign((size_t)n_slots, SlotRec{});
     free_slots.clear();
-    for (int s = n_slots - 1; s >= 0; --s) free_slots.push_back(s);
+    for (int s = 0; s < n_slots; ++s) free_slots.push_back(s);
     // tracks
     const size_t kbytes = sizeof(float2) * (size_t)cap;
     if (!rc) rc = kp1.ensure(kbytes);
@@ -146,7 +148,6 @@ int viso_ctx::init() {
     if (!rc) rc = pose_log.ensure(96 * (size_t)std::max(p.max_poses, 1));
     if (rc) return rc;
     direct = direct_scratch_at(direct_buf.ptr);
-    VISO_HIP_CHECK(hipStreamCreateWithFlags(&lk_stream, hipStreamNonBlocking));
     for (int i = 0; i < kLkRing; ++i) VISO_HIP_CHECK(hipEventCreateWithFlags(&lk_ring[i], hipEventDisableTiming));
     VISO_HIP_CHECK(hipMemsetAsync(n_track_dev.ptr, 0, 256, stream));
     VISO_HIP_CHECK(hipStreamSynchronize(stream));
@@ -176,11 +177,18 @@ void viso_ctx::release() {
     h_dbl = nullptr;
 }
 
+// The context stream and the LK-alignment side stream (single-frame calls).
+int viso_ctx::create_streams() {
+    if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return VISO_ERR_HIP;
+    if (hipStreamCreateWithFlags(&lk_stream, hipStreamNonBlocking) != hipSuccess) return VISO_ERR_HIP;
+    return VISO_OK;
+}
+
 // ------------------------------------------------------------------ frame pool
 int viso_ctx::acquire_slot() {
     if (free_slots.empty()) return -1;
-    int s = free_slots.back();
-    free_slots.pop_back();
+    int s = free_slots.front();
+    free_slots.pop_front();
     // lk_stream may still read this slot's previous frame: order the reuse
     // behind that batch (a no-op wait in steady state; a later batch on the
     // same stream also implies completion)
@@ -590,6 +598,8 @@ int viso_process_frames_device(viso_ctx* c, const uint8_t* d_left, const uint8_t
             if (rc) return rc;
         }
         // the last frame's final solve, then the chunk's LKAlignment batch
+        // behind the chunk (the GPU is free then; beside the next chunk it
+        // would take the CU resources the latency-bound direct chain needs)
         int rc = c->finish_call(c->stream);
         if (rc) return rc;
         // frames still referenced after the chunk get their own level 0

@@ -353,6 +353,10 @@ __global__ __launch_bounds__(256) void lk_align_kernel(LkAlignArgs a) {
                 if (lane == 0) {
                     atomicAdd(&g_probe_lk[level], (unsigned long long)r.iters);
                     atomicAdd(&g_probe_lk[4 + level], 1ull);
+                    if (r.iters >= 10) atomicAdd(&g_probe_lk[8], 1ull);
+                    if (r.iters >= 50) atomicAdd(&g_probe_lk[9], 1ull);
+                    if (r.iters >= 99) atomicAdd(&g_probe_lk[10], 1ull);
+                    atomicMax(&g_probe_lk[11], (unsigned long long)r.iters);
                 }
 #endif
                 cu = cu + r.dx / s;  // pair.uv_cur += V2d{dx/s, dy/s}
