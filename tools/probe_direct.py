@@ -57,7 +57,11 @@ def main():
     q = list(lkbuf)
     print("LK alignment: mean GN iterations per (pair, level):",
           ", ".join(f"L{l} {q[l] / max(q[4 + l], 1):.2f} ({q[4 + l]} calls)" for l in range(4)))
-    print(f"  (pair, level) with >= 10 iterations: {q[8]}, >= 50: {q[9]}, >= 99: {q[10]}, max {q[11]}")
+    print(f"  (pair, level) with >= 10 iterations: {q[8]}")
+    calls = max(sum(q[4:8]), 1)
+    print(f"  per (pair, level): template+window {10.0 * q[12] / calls / 1e3:.2f} us, "
+          f"iterations {10.0 * q[13] / calls / 1e3:.2f} us; per pair (4 levels) "
+          f"{10.0 * q[14] / max(q[15], 1) / 1e3:.2f} us")
     p = list(buf)
     us = lambda x, c: 10.0 * x / max(c, 1) / 1e3  # 100 MHz ticks -> us
     print("launch  count  prologue-done  block0-done   (us from entry, block 0)")

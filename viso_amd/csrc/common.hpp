@@ -69,6 +69,21 @@ __host__ __device__ inline void mat3_vec(const double* R, const double* p, doubl
     o[2] = R[6] * p[0] + R[7] * p[1] + R[8] * p[2];
 }
 
+// Loads through explicit address spaces.  Image pointers often reach a
+// kernel through a run-time-indexed kernel-argument array (a frame of a
+// batch, a pyramid level), where the compiler can no longer prove they are
+// global and would emit flat loads (which also count in lgkmcnt and get
+// drained one by one); LDS windows passed as plain pointers likewise.
+__device__ inline uint8_t ld_global_u8(const uint8_t* p, long long i) {
+    return ((const __attribute__((address_space(1))) uint8_t*)p)[i];
+}
+__device__ inline uint8_t ld_lds_u8(const uint8_t* p, int i) {
+    return ((const __attribute__((address_space(3))) uint8_t*)p)[i];
+}
+__device__ inline void st_lds_u8(uint8_t* p, int i, uint8_t v) {
+    ((__attribute__((address_space(3))) uint8_t*)p)[i] = v;
+}
+
 // GetPixelValue (include/common.h:35-42): int() base, floor() weights,
 // taps outside the continuous level buffer read 0.
 __device__ inline double sample_px(const uint8_t* __restrict__ img, int w, int h, double x,
@@ -76,10 +91,10 @@ __device__ inline double sample_px(const uint8_t* __restrict__ img, int w, int h
     const long long n = (long long)w * (long long)h;
     const bool finite = (x > -1e9 && x < 1e9 && y > -1e9 && y < 1e9);
     long long base = finite ? (long long)(int)y * (long long)w + (long long)(int)x : -(1LL << 40);
-    double d0 = (base >= 0 && base < n) ? (double)img[base] : 0.0;
-    double d1 = (base + 1 >= 0 && base + 1 < n) ? (double)img[base + 1] : 0.0;
-    double d2 = (base + w >= 0 && base + w < n) ? (double)img[base + w] : 0.0;
-    double d3 = (base + w + 1 >= 0 && base + w + 1 < n) ? (double)img[base + w + 1] : 0.0;
+    double d0 = (base >= 0 && base < n) ? (double)ld_global_u8(img, base) : 0.0;
+    double d1 = (base + 1 >= 0 && base + 1 < n) ? (double)ld_global_u8(img, base + 1) : 0.0;
+    double d2 = (base + w >= 0 && base + w < n) ? (double)ld_global_u8(img, base + w) : 0.0;
+    double d3 = (base + w + 1 >= 0 && base + w + 1 < n) ? (double)ld_global_u8(img, base + w + 1) : 0.0;
     double xx = x - floor(x);
     double yy = y - floor(y);
     return double((1 - xx) * (1 - yy) * d0 + xx * (1 - yy) * d1 + (1 - xx) * yy * d2 +

@@ -174,10 +174,10 @@ __device__ inline void ref_issue(const DirectArgs& a, const LevelPair& fp, int l
     const uint8_t* img = fp.last;
     const long long n = (long long)w * (long long)h;
     const long long base = r.ok ? (long long)(int)y * (long long)w + (long long)(int)x : -(1LL << 40);
-    r.t0 = (base >= 0 && base < n) ? img[base] : 0;
-    r.t1 = (base + 1 >= 0 && base + 1 < n) ? img[base + 1] : 0;
-    r.t2 = (base + w >= 0 && base + w < n) ? img[base + w] : 0;
-    r.t3 = (base + w + 1 >= 0 && base + w + 1 < n) ? img[base + w + 1] : 0;
+    r.t0 = (base >= 0 && base < n) ? ld_global_u8(img, base) : 0;
+    r.t1 = (base + 1 >= 0 && base + 1 < n) ? ld_global_u8(img, base + 1) : 0;
+    r.t2 = (base + w >= 0 && base + w < n) ? ld_global_u8(img, base + w) : 0;
+    r.t3 = (base + w + 1 >= 0 && base + w + 1 < n) ? ld_global_u8(img, base + w + 1) : 0;
     r.xx = x - floor(x);
     r.yy = y - floor(y);
 }
@@ -223,20 +223,20 @@ __device__ inline void win_issue(const uint8_t* __restrict__ img, int w, int h, 
     c.x0 = x0;
     c.y0 = y0;
     const int lane = threadIdx.x & 63;
-    const uint8_t* p = img + (size_t)(y0 + (lane >> 2)) * w + x0 + 4 * (lane & 3);
-    c.b0 = p[0];
-    c.b1 = p[1];
-    c.b2 = p[2];
-    c.b3 = p[3];
+    const long long o = (long long)(y0 + (lane >> 2)) * w + x0 + 4 * (lane & 3);
+    c.b0 = ld_global_u8(img, o);
+    c.b1 = ld_global_u8(img, o + 1);
+    c.b2 = ld_global_u8(img, o + 2);
+    c.b3 = ld_global_u8(img, o + 3);
 }
 
 __device__ inline void win_store(uint8_t* lds, const CurWin& c) {
     const int lane = threadIdx.x & 63;
-    uint8_t* q = lds + (lane >> 2) * kCW + 4 * (lane & 3);
-    q[0] = (uint8_t)c.b0;
-    q[1] = (uint8_t)c.b1;
-    q[2] = (uint8_t)c.b2;
-    q[3] = (uint8_t)c.b3;
+    const int o = (lane >> 2) * kCW + 4 * (lane & 3);
+    st_lds_u8(lds, o, (uint8_t)c.b0);
+    st_lds_u8(lds, o + 1, (uint8_t)c.b1);
+    st_lds_u8(lds, o + 2, (uint8_t)c.b2);
+    st_lds_u8(lds, o + 3, (uint8_t)c.b3);
 }
 
 // sample_px with the taps served from the window when all four lie in it
@@ -246,9 +246,9 @@ __device__ inline double sample_cw(const uint8_t* __restrict__ img, int w, int h
     if (finite && c.on) {
         const int ix = (int)x, iy = (int)y;
         if (ix >= c.x0 && ix + 1 < c.x0 + kCW && iy >= c.y0 && iy + 1 < c.y0 + kCW) {
-            const uint8_t* q = win + (iy - c.y0) * kCW + (ix - c.x0);
-            const double d0 = (double)q[0], d1 = (double)q[1];
-            const double d2 = (double)q[kCW], d3 = (double)q[kCW + 1];
+            const int o = (iy - c.y0) * kCW + (ix - c.x0);
+            const double d0 = (double)ld_lds_u8(win, o), d1 = (double)ld_lds_u8(win, o + 1);
+            const double d2 = (double)ld_lds_u8(win, o + kCW), d3 = (double)ld_lds_u8(win, o + kCW + 1);
             const double xx = x - floor(x);
             const double yy = y - floor(y);
             return double((1 - xx) * (1 - yy) * d0 + xx * (1 - yy) * d1 + (1 - xx) * yy * d2 +

@@ -53,10 +53,18 @@ __device__ inline Window load_window(uint8_t* lds, const uint8_t* img, int w, in
     x0 = min(max(x0, 0), w - kWinW);
     y0 = min(max(y0, 0), h - kWinH);
     const int lane = threadIdx.x & 63;
-    for (int e = lane; e < kWinW * kWinH; e += 64) {
+    // all nine loads first, then the LDS stores: interleaved, each store
+    // (through a generic pointer) would wait for its load
+    constexpr int kPer = kWinW * kWinH / 64;  // 9
+    uint8_t v[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int e = lane + 64 * k;
         const int r = e / kWinW, c = e - r * kWinW;
-        lds[e] = img[(size_t)(y0 + r) * w + (x0 + c)];
+        v[k] = ld_global_u8(img, (long long)(y0 + r) * w + (x0 + c));
     }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) st_lds_u8(lds, lane + 64 * k, v[k]);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -73,9 +81,10 @@ __device__ inline double sample_win(const uint8_t* __restrict__ img, int w, int 
     if (finite && win.lds) {
         const int ix = (int)x, iy = (int)y;
         if (ix >= win.x0 && ix + 1 < win.x0 + kWinW && iy >= win.y0 && iy + 1 < win.y0 + kWinH) {
-            const uint8_t* p = win.lds + (iy - win.y0) * kWinW + (ix - win.x0);
-            const double d0 = (double)p[0], d1 = (double)p[1];
-            const double d2 = (double)p[kWinW], d3 = (double)p[kWinW + 1];
+            const int o = (iy - win.y0) * kWinW + (ix - win.x0);
+            const double d0 = (double)ld_lds_u8(win.lds, o), d1 = (double)ld_lds_u8(win.lds, o + 1);
+            const double d2 = (double)ld_lds_u8(win.lds, o + kWinW);
+            const double d3 = (double)ld_lds_u8(win.lds, o + kWinW + 1);
             const double xx = x - floor(x);
             const double yy = y - floor(y);
             return double((1 - xx) * (1 - yy) * d0 + xx * (1 - yy) * d1 + (1 - xx) * yy * d2 +
@@ -327,11 +336,18 @@ __global__ __launch_bounds__(256) void lk_align_kernel(LkAlignArgs a) {
             double cu = uc, cv = vc;
             const FrameDev refp = a.kf[kf];
             bool succ = false;
+#ifdef VISO_PROBE
+            unsigned long long pr_it[kLevels] = {0, 0, 0, 0}, pr_win = 0, pr_iter = 0, pr_long = 0;
+            const unsigned long long pr_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
             for (int level = kLevels - 1; level >= 0; --level) {
                 const double s = kScale[level];
                 const int w = a.g.w[level], h = a.g.h[level];
                 const double cx = cu * s + px, cy = cv * s + py;
-                const Window win = load_window(my_win, cur.l[level], w, h, cu * s, cv * s);
+#ifdef VISO_PROBE
+                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+#endif
+                // template loads first: in flight together with the window's
                 LkTemplate t;
                 if (a.tmpl) {
                     const double* d = a.tmpl + ((size_t)i * kLevels + level) * 192;
@@ -343,25 +359,37 @@ __global__ __launch_bounds__(256) void lk_align_kernel(LkAlignArgs a) {
                     t.i01 = hh[1];
                     t.i10 = hh[2];
                     t.i11 = hh[3];
-                } else {
-                    t = lk_prepare(refp.l[level], w, h, bu * s + px, bv * s + py);
                 }
+                const Window win = load_window(my_win, cur.l[level], w, h, cu * s, cv * s);
+                if (!a.tmpl) t = lk_prepare(refp.l[level], w, h, bu * s + px, bv * s + py);
+#ifdef VISO_PROBE
+                const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+#endif
                 LkResult r = lk_iterate<100, false>(t, w, h, cur.l[level], w, h, cx, cy, bu * s,
                                                     bv * s, 0.0, 0.0, a.thresh, win);
                 succ = r.succ;
 #ifdef VISO_PROBE
-                if (lane == 0) {
-                    atomicAdd(&g_probe_lk[level], (unsigned long long)r.iters);
-                    atomicAdd(&g_probe_lk[4 + level], 1ull);
-                    if (r.iters >= 10) atomicAdd(&g_probe_lk[8], 1ull);
-                    if (r.iters >= 50) atomicAdd(&g_probe_lk[9], 1ull);
-                    if (r.iters >= 99) atomicAdd(&g_probe_lk[10], 1ull);
-                    atomicMax(&g_probe_lk[11], (unsigned long long)r.iters);
-                }
+                pr_it[level] += (unsigned long long)r.iters;
+                pr_win += t1 - t0;
+                pr_iter += __builtin_amdgcn_s_memrealtime() - t1;
+                pr_long += r.iters >= 10 ? 1 : 0;
 #endif
                 cu = cu + r.dx / s;  // pair.uv_cur += V2d{dx/s, dy/s}
                 cv = cv + r.dy / s;
             }
+#ifdef VISO_PROBE
+            if (lane == 0) {
+                for (int l = 0; l < kLevels; ++l) {
+                    atomicAdd(&g_probe_lk[l], pr_it[l]);
+                    atomicAdd(&g_probe_lk[4 + l], 1ull);
+                }
+                atomicAdd(&g_probe_lk[8], pr_long);
+                atomicAdd(&g_probe_lk[12], pr_win);
+                atomicAdd(&g_probe_lk[13], pr_iter);
+                atomicAdd(&g_probe_lk[14], __builtin_amdgcn_s_memrealtime() - pr_t0);
+                atomicAdd(&g_probe_lk[15], 1ull);
+            }
+#endif
             succ_out = succ ? 1 : 0;
             ua[0] = cu;
             ua[1] = cv;
