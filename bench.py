@@ -171,7 +171,9 @@ def main():
         if os.path.exists(tfile):
             with open(tfile) as fh:
                 t = json.load(fh)
-            traffic = int(t["traffic_bytes_per_launch"] / 100 * imgs_per_launch)
+            if (t.get("width"), t.get("height")) == (W, H):  # profiled at this size only
+                traffic = int(t["traffic_bytes_per_launch"] / t.get("images_per_launch", 100)
+                              * imgs_per_launch)
         roofline = {"kernel": "pyr_down_stream_kernel x3 (batched image pass; algorithmic bytes = "
                               "L0 read + L1..L3 write)", "bound": "hbm",
                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -215,9 +217,12 @@ def main():
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": "configs[1]: one 1242x375 grey stereo sequence per GPU, "
-                                   "KITTI seq-00 intrinsics, synthetic KITTI-like frames "
-                                   "(KITTI absent offline), tracking enabled",
+            "config": {"workload": (f"configs[1]: one {W}x{H} grey stereo sequence per GPU, "
+                                    "KITTI seq-00 intrinsics" if (W, H) == (1242, 375) else
+                                    f"one {W}x{H} grey stereo sequence per GPU (configs[2] size "
+                                    "when 1920x1080), KITTI seq-00 intrinsics")
+                                   + ", synthetic KITTI-like frames (KITTI absent offline), "
+                                   "tracking enabled",
                        "width": W, "height": H, "map_points": n_map,
                        "ingest_batch": args.batch, "parallelism": f"independent sequences x{world}"},
             "roofline": roofline,

@@ -53,7 +53,9 @@ def main():
     scale = float(os.environ.get("FETCH_SCALE", "2"))
     fetch = scale * 1024 * sum(fc) / len(fc)
     write = 1024.0 * sum(wc) / len(wc)
-    res = {"fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
+    res = {"width": int(os.environ.get("WIDTH", "1242")), "height": int(os.environ.get("HEIGHT", "375")),
+           "images_per_launch": 100,
+           "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
            "traffic_bytes_per_launch": fetch + write, "chunks": len(fc),
            "fetch_scale": scale,
            "note": "FETCH_SIZE x fetch_scale + WRITE_SIZE (KB -> bytes) summed over the three "
