@@ -158,7 +158,7 @@ def main():
     roofline = None
     if "pyramid" in timing:
         # one timed region = the image pass of one ingest chunk (left + right,
-        # <= 128 images): three pyr_down_stream_kernel launches (L0->L1,
+        # <= 128 images): three pyr_down_sk_kernel launches (L0->L1,
         # L1->L2, L2->L3) back to back on the context stream
         imgs_per_launch = 2 * args.steps / timing["pyramid"]["launches"]
         bytes_per_launch = algo_bytes_img * imgs_per_launch
@@ -174,7 +174,7 @@ def main():
             if (t.get("width"), t.get("height")) == (W, H):  # profiled at this size only
                 traffic = int(t["traffic_bytes_per_launch"] / t.get("images_per_launch", 100)
                               * imgs_per_launch)
-        roofline = {"kernel": "pyr_down_stream_kernel x3 (batched image pass; algorithmic bytes = "
+        roofline = {"kernel": "pyr_down_sk_kernel x3 (batched image pass; algorithmic bytes = "
                               "L0 read + L1..L3 write)", "bound": "hbm",
                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

@@ -86,7 +86,12 @@ def test_fast_order_row_major():
 
 # ------------------------------------------------------------------ GPU parity
 @pytest.mark.gpu
-@pytest.mark.parametrize("h,w", [(375, 1242), (61, 97), (1080, 1920), (16, 16), (187, 621)])
+# sizes: the bench frame, odd/even widths, strip edges of the 248-column
+# waves (dst widths 248k +- 1), levels under 8 columns (scalar form) and
+# between 8 and 16 (packed form with both borders in one strip)
+@pytest.mark.parametrize("h,w", [(375, 1242), (61, 97), (1080, 1920), (16, 16), (187, 621),
+                                 (8, 8), (9, 17), (20, 15), (50, 497), (30, 993), (12, 994),
+                                 (9, 1001), (41, 2047), (33, 31), (18, 64)])
 def test_gpu_pyramid_bitexact(h, w):
     from viso_amd import default_context
     ctx = default_context()

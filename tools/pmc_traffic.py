@@ -6,11 +6,12 @@ Usage: tools/pmc_traffic.py FETCH_DIR WRITE_DIR [OUT_JSON]
 Each directory holds a run_counter_collection.csv of one `rocprofv3 --pmc`
 pass over `bench.py`.  MI355X_MICROARCH.md §HBM: FETCH_SIZE (KB) reports half
 the bytes of 16-byte-per-lane streaming reads on gfx950; other widths are
-uncalibrated.  pyr_down_stream_kernel reads 8 bytes per lane.  Its raw
-FETCH_SIZE for a 100-image chunk (39.9 MB for the level-0 pass) is below the
-46.6 MB of level 0 it must read at least once, while the doubled value (79.8
-MB) lies between that and the 87.6 MB of 128-byte lines its loads touch, so
-the same factor 2 is applied (FETCH_SCALE overrides).  WRITE_SIZE (KB) is
+uncalibrated.  The pyrDown kernels read 8 bytes per lane.  The raw
+FETCH_SIZE of the level-0 pass of a 100-image chunk is below the 46.6 MB of
+level 0 it must read at least once (round 1: 39.9 MB for the first streaming
+kernel), while the doubled value lies between that and the bytes of the
+128-byte lines its loads touch, so the same factor 2 is applied (FETCH_SCALE
+overrides; the per-launch raw values are printed for the check).  WRITE_SIZE (KB) is
 taken as is.  The per-chunk traffic of the image pass is the sum over its
 three launches, averaged over the full-size chunks.
 """
@@ -27,12 +28,26 @@ def per_dispatch(path, counter):
     vals = collections.defaultdict(float)
     grid = {}
     for r in csv.DictReader(open(os.path.join(path, "run_counter_collection.csv"))):
-        if "pyr_down_stream" not in r["Kernel_Name"] or r["Counter_Name"] != counter:
+        if "pyr_down_" not in r["Kernel_Name"] or r["Counter_Name"] != counter:
             continue
         d = int(r["Dispatch_Id"])
         vals[d] += float(r["Counter_Value"])
         grid[d] = (int(r["Grid_Size"]), r["Kernel_Name"])
     return vals, grid
+
+
+def big_groups(vals, grid):
+    """Dispatch-id triples (L1, L2, L3 of one chunk) of the full-size chunks."""
+    ids = sorted(vals)
+    groups = [ids[i:i + 3] for i in range(0, len(ids) - len(ids) % 3, 3)]
+    big = max(grid[g[0]][0] for g in groups)
+    return [g for g in groups if grid[g[0]][0] == big]
+
+
+def per_level(vals, grid):
+    """Mean raw counter value (KB) per launch of each level over the full-size chunks."""
+    gs = big_groups(vals, grid)
+    return [round(sum(vals[g[k]] for g in gs) / len(gs), 1) for k in range(3)]
 
 
 def main():
@@ -42,12 +57,7 @@ def main():
     w, wg = per_dispatch(wdir, "WRITE_SIZE")
 
     def chunks(vals, grid):
-        # group consecutive dispatches in threes (L1, L2, L3 of one chunk)
-        ids = sorted(vals)
-        groups = [ids[i:i + 3] for i in range(0, len(ids) - len(ids) % 3, 3)]
-        sums = [(sum(vals[d] for d in g), grid[g[0]][0]) for g in groups]
-        big = max(s[1] for s in sums)
-        return [s[0] for s in sums if s[1] == big]
+        return [sum(vals[d] for d in g) for g in big_groups(vals, grid)]
 
     fc, wc = chunks(f, fg), chunks(w, wg)
     scale = float(os.environ.get("FETCH_SCALE", "2"))
@@ -59,7 +69,8 @@ def main():
            "traffic_bytes_per_launch": fetch + write, "chunks": len(fc),
            "fetch_scale": scale,
            "note": "FETCH_SIZE x fetch_scale + WRITE_SIZE (KB -> bytes) summed over the three "
-                   "pyr_down_stream_kernel launches of one 100-image chunk (tools/pmc_traffic.py)"}
+                   "pyrDown launches of one 100-image chunk (tools/pmc_traffic.py)",
+           "raw_fetch_kb_per_level": per_level(f, fg), "raw_write_kb_per_level": per_level(w, wg)}
     print(json.dumps(res, indent=1))
     if out:
         json.dump(res, open(out, "w"), indent=1)

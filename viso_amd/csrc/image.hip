@@ -14,9 +14,17 @@
 // order is then restored across rows by fast_compact, an exclusive prefix
 // over per-row counts).
 #include <algorithm>
+#include <cstdlib>
+#include <type_traits>
 #include <vector>
 
 #include "kernels.hpp"
+
+#ifdef VISO_PROBE
+// wave timeline of the last level-1 pyrDown launch: start, end (s_memrealtime,
+// 100 MHz), HW_ID, XCC_ID per wave (dev instrumentation)
+__device__ unsigned long long g_pyr_tl[8192][5];
+#endif
 
 namespace viso {
 
@@ -304,6 +312,9 @@ struct PyrLevelArgs {
     uint8_t* dst[kPyrBatch];
     int sw, sh, dw, dh;
     int bands, units;
+#ifdef VISO_PROBE
+    int diag;  // dev: 1 = skip stores (timing only)
+#endif
 };
 
 // 8 source bytes at offset off, never reading outside [0, n).
@@ -385,6 +396,263 @@ __global__ __launch_bounds__(256) void pyr_down_stream_kernel(PyrLevelArgs a) {
             }
         }
     }
+}
+
+// Register-only pyrDown (pyr_down_sk_kernel below; same decomposition and
+// exact integer sums as pyr_down_stream_kernel) for source levels at least
+// 8 columns wide.  Lane l loads 8 source bytes per row (one unaligned 8-byte
+// load) and takes the next lane's first dword by DPP: its 11 taps are bytes
+// 0..10 of the 12-byte window (w0, w1, w2).  The horizontal 5-tap sums are
+// v_dot4_u32_u8 with weights (1, 4, 6, 4) plus the fifth tap, packed in pairs
+// into 16-bit halves, so the vertical sums of two destination columns run as
+// one packed op (max 65408 < 2^16).  Reflect-101 at the left/right image
+// edges is a per-lane byte permutation of the window, computed once per wave
+// (edge waves only).
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ inline u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+
+struct PkEdge {
+    uint32_t sel0, sel1, sel2;
+};
+
+// horizontal sums of one source row for the lane's 4 destination columns
+template <bool EDGE>
+__device__ inline void pk_hsum(uint2 r, const PkEdge& e, u16x2 (&h)[2]) {
+    uint32_t w0 = r.x, w1 = r.y;
+    // next lane's first dword; lane 63 (which covers the 4 columns left of
+    // the strip, see sk_band) wraps to lane 0
+    uint32_t w2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r.x, 0x134, 0xf, 0xf, false);
+    if (EDGE) {
+        const uint32_t e0 = __builtin_amdgcn_perm(w1, w0, e.sel0);
+        const uint32_t e1 = __builtin_amdgcn_perm(w1, w0, e.sel1);
+        w2 = __builtin_amdgcn_perm(w2, w1, e.sel2);
+        w0 = e0;
+        w1 = e1;
+    }
+    constexpr uint32_t K = 0x04060401u;  // taps 0..3 of [1 4 6 4 1]
+    const uint32_t a1 = __builtin_amdgcn_alignbyte(w1, w0, 2);  // t2..t5
+    const uint32_t a3 = __builtin_amdgcn_alignbyte(w2, w1, 2);  // t6..t9
+    const uint32_t h0 = __builtin_amdgcn_udot4(w1, 0x00000001u, __builtin_amdgcn_udot4(w0, K, 0, false), false);
+    const uint32_t h1 = __builtin_amdgcn_udot4(w1, 0x00010000u, __builtin_amdgcn_udot4(a1, K, 0, false), false);
+    const uint32_t h2 = __builtin_amdgcn_udot4(w2, 0x00000001u, __builtin_amdgcn_udot4(w1, K, 0, false), false);
+    const uint32_t h3 = __builtin_amdgcn_udot4(w2, 0x00010000u, __builtin_amdgcn_udot4(a3, K, 0, false), false);
+    h[0] = as_u16x2(__builtin_amdgcn_perm(h1, h0, 0x05040100u));
+    h[1] = as_u16x2(__builtin_amdgcn_perm(h3, h2, 0x05040100u));
+}
+
+// vertical 5-tap of two destination columns, rounded: (sum + 128) >> 8
+__device__ inline u16x2 pk_vsum(u16x2 h0, u16x2 h1, u16x2 h2, u16x2 h3, u16x2 h4) {
+    const u16x2 s = (u16x2)6 * h2 + (u16x2)128;
+    return ((h0 + h4) + ((u16x2)4 * (h1 + h3) + s)) >> (u16x2)8;
+}
+
+// One wave = one strip of 244 destination columns x a band of BH
+// destination rows, streamed: a ring of D source rows is kept in flight (one
+// 8-byte load per lane and row), each consumed row's slot is refilled with
+// the row D below, so HBM reads and the VALU work of the band overlap.
+// Wave-uniform work (row pointers, store alignment) is scalar and kept to a
+// few SALU ops per row: the scalar unit is shared by the CU's waves and was
+// this kernel's first bottleneck.  Bands whose source rows need no
+// reflect-101 and no load clamping (INTERIOR) walk running row pointers.
+constexpr int kSkRing = 8;
+constexpr int kSkW = 244;  // destination columns per wave (lanes 0..60; 61 = right context)
+// band heights per level: short bands keep ~7 waves per SIMD in flight
+// (measured: 24/12/6-row bands with a 16-row ring ran 30% slower)
+constexpr int kSkBH1 = 8, kSkBH2 = 4, kSkBH3 = 4;
+
+struct SkBand {
+    const uint8_t* src;
+    uint8_t* dst;
+    int sw, sh, dw, n;
+    int X, Y, rows, nr, c0, len;
+};
+
+template <int D, bool EDGE, bool INTERIOR>
+__device__ inline void sk_band(const SkBand& b, const PkEdge& e, int lane) {
+    // Lane l < 62 covers destination columns X + 4l .. X + 4l + 3 (lane 61:
+    // the next strip's first 4; lane 62 only feeds lane 61's taps), lane 63
+    // the 4 columns left of the strip (X > 0): so every aligned dword around
+    // the strip's row segment is
+    // computed whole by this wave, and neighbouring strips write the bytes
+    // they share with identical values.  Only the image's row ends (left of
+    // column 0, right of column dw - 1) need partial dwords.
+    const int loff = (lane == 63 && b.X > 0) ? -8 : 8 * lane;  // window start - c0
+    // ---- source rows: band row i (0 <= i < nr) is image row 2Y - 2 + i; rows
+    // past nr repeat row nr - 1 (one real load per call keeps the waitcnt
+    // counting exact; the repeats hit the cache)
+    const uint8_t* p_next = b.src + (ptrdiff_t)(2 * b.Y - 2) * b.sw + b.c0;  // INTERIOR
+    int issued = 0;
+    auto row_off = [&](int i) { return reflect101(2 * b.Y - 2 + min(i, b.nr - 1), b.sh) * b.sw + b.c0; };
+    auto unsafe_row = [&](int o0) { return o0 - 8 < 0 || o0 + 8 * 64 > b.n; };
+    auto issue = [&](int i) -> uint2 {
+        unsigned long long q;
+        if constexpr (INTERIOR) {
+            q = *reinterpret_cast<const __attribute__((address_space(1))) unsigned long long*>(
+                reinterpret_cast<uintptr_t>(p_next) + loff);
+            if (++issued < b.nr) p_next += b.sw;
+        } else {
+            const int o0 = row_off(i);
+            int oc = o0 + loff;
+            if (unsafe_row(o0)) oc = min(max(oc, 0), b.n - 8);
+            q = *reinterpret_cast<const __attribute__((address_space(1))) unsigned long long*>(
+                reinterpret_cast<uintptr_t>(b.src) + oc);
+        }
+        return make_uint2((uint32_t)q, (uint32_t)(q >> 32));
+    };
+    // clamped loads are shifted into place when consumed, not at issue, so
+    // no wait is forced on a load still in flight
+    auto fix = [&](uint2 r, int i) -> uint2 {
+        if constexpr (INTERIOR) {
+            return r;
+        } else {
+            const int o0 = row_off(i);
+            if (!unsafe_row(o0)) return r;
+            const int o = o0 + loff;
+            const int d = max(min(o - min(max(o, 0), b.n - 8), 7), -7);  // lanes past the image: junk
+            unsigned long long q = ((unsigned long long)r.y << 32) | r.x;
+            q = d >= 0 ? q >> (8 * d) : q << (-8 * d);  // bytes outside [0, n) read as 0
+            return make_uint2((uint32_t)q, (uint32_t)(q >> 32));
+        }
+    };
+    // ---- destination rows: lane k < 62 writes the k-th aligned dword from
+    // the row segment's start (bytes 4k - ma .. 4k - ma + 3 relative to
+    // column X), its low bytes taken from lane k-1 (lane 0: lane 63) by DPP
+    // wave_ror:1.  Writable bytes: [wlo, whi) relative to X.
+    uint8_t* row_out = b.dst + (ptrdiff_t)b.Y * b.dw + b.X;
+    const int wlo_x = b.X > 0 ? 1 : 0;                  // columns left of X exist
+    const int whi = b.X + kSkW < b.dw ? kSkW + 4 : b.len;  // columns right of the strip exist
+    auto store_row = [&](const u16x2 (&H)[5][2]) {
+        const u16x2 o0 = pk_vsum(H[0][0], H[1][0], H[2][0], H[3][0], H[4][0]);
+        const u16x2 o1 = pk_vsum(H[0][1], H[1][1], H[2][1], H[3][1], H[4][1]);
+        const uint32_t bb = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, o1),
+                                                  __builtin_bit_cast(uint32_t, o0), 0x06040200u);
+        const int ma = (int)((uintptr_t)row_out & 3);
+        const uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)bb, 0x13c, 0xf, 0xf, false);
+        const uint32_t word = ma ? __builtin_amdgcn_alignbyte(bb, prev, 4 - ma) : bb;
+        const int lo = 4 * lane - ma;
+        auto* out = reinterpret_cast<__attribute__((address_space(1))) uint8_t*>(
+            reinterpret_cast<uintptr_t>(row_out));
+        row_out += b.dw;
+        if constexpr (!EDGE) {
+            if (lane < 62) *reinterpret_cast<__attribute__((address_space(1))) uint32_t*>(out + lo) = word;
+        } else {
+            const int wlo = wlo_x ? -ma : 0;
+            if (lane < 62 && lo >= wlo && lo + 4 <= whi) {
+                *reinterpret_cast<__attribute__((address_space(1))) uint32_t*>(out + lo) = word;
+            } else if (lane < 62 && lo + 4 > wlo && lo < whi) {
+                // a partial dword at an image row end: 4 byte stores, the
+                // bytes outside [wlo, whi) redirected onto an own byte
+                const int q0 = max(wlo - lo, 0), q1 = min(whi - lo, 4) - 1;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int qq = min(max(q, q0), q1);
+                    out[lo + qq] = (uint8_t)(word >> (8 * qq));
+                }
+            }
+        }
+    };
+    uint2 ring[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) ring[i] = issue(i);
+    u16x2 H[5][2];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        pk_hsum<EDGE>(fix(ring[i], i), e, H[i]);
+        ring[i] = issue(D + i);
+    }
+    store_row(H);
+    // destination rows j0 .. j0 + D/2 - 1 (j0 = 1 + k D/2) consume source
+    // rows k D + 5 .. k D + D + 4, i.e. ring slots 5 .. D-1, 0 .. 4: static
+    // after unrolling
+    for (int j0 = 1; j0 < b.rows; j0 += D / 2) {
+#pragma unroll
+        for (int u = 0; u < D / 2; ++u) {
+            const int j = j0 + u;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                H[0][q] = H[2][q];
+                H[1][q] = H[3][q];
+                H[2][q] = H[4][q];
+            }
+            pk_hsum<EDGE>(fix(ring[(5 + 2 * u) % D], 2 * j + 3), e, H[3]);
+            ring[(5 + 2 * u) % D] = issue(2 * j + 3 + D);
+            pk_hsum<EDGE>(fix(ring[(6 + 2 * u) % D], 2 * j + 4), e, H[4]);
+            ring[(6 + 2 * u) % D] = issue(2 * j + 4 + D);
+            if (j < b.rows) store_row(H);
+        }
+    }
+}
+
+template <int BH, int D>
+__global__ __launch_bounds__(256) void pyr_down_sk_kernel(PyrLevelArgs a) {
+    const int lane = threadIdx.x & 63;
+    // everything that depends only on the wave's unit is wave-uniform: keep
+    // it in SGPRs (readfirstlane) so the VALU only does the per-lane work
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int unit = blockIdx.x * 4 + wave;
+    if (unit >= a.units) return;
+#ifdef VISO_PROBE
+    const unsigned long long pr_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    SkBand b;
+    b.src = a.src[blockIdx.y];
+    b.dst = a.dst[blockIdx.y];
+    b.sw = a.sw;
+    b.sh = a.sh;
+    b.dw = a.dw;
+    b.n = a.sw * a.sh;  // levels are < 2^31 bytes (kMaxWidth)
+    const int strip = unit / a.bands, band = unit - strip * a.bands;
+    b.X = strip * kSkW;
+    b.Y = band * BH;
+    b.rows = min(BH, a.dh - b.Y);
+    b.nr = 2 * b.rows + 3;  // source rows of the band
+    b.c0 = 2 * b.X - 2;     // source column of lane 0's window byte 0
+    b.len = min(kSkW, a.dw - b.X);  // destination bytes of the wave's row
+    // reflect-101 of the window bytes that fall outside [0, sw): byte k of
+    // lane l is column c = c0 + loff(l) + k; its value is column r(c), window byte
+    // k + r(c) - c.  Lanes whose outputs are never stored keep the identity.
+    const bool edge = b.X == 0 || b.c0 + 8 * (kSkW / 4) + 11 >= b.sw;
+    PkEdge e{0x03020100u, 0x07060504u, 0x07060504u};
+    if (edge) {
+#pragma unroll
+        for (int k = 0; k < 12; ++k) {
+            const int c = b.c0 + ((lane == 63 && b.X > 0) ? -8 : 8 * lane) + k;
+            const int rc = reflect101(c, b.sw);
+            const int base = k >= 8 ? 4 : 0;  // w2' selects from (w2:w1)
+            const int kk = k + rc - c - base;
+            if (c != rc && kk >= 0 && kk < 8) {
+                const int sh8 = 8 * (k & 3);
+                const uint32_t m = ~(0xffu << sh8), val = (uint32_t)kk << sh8;
+                if (k < 4) e.sel0 = (e.sel0 & m) | val;
+                else if (k < 8) e.sel1 = (e.sel1 & m) | val;
+                else e.sel2 = (e.sel2 & m) | val;
+            }
+        }
+    }
+    // interior: every band row is an image row and every load is in bounds
+    const int r0 = 2 * b.Y - 2, r1 = r0 + b.nr - 1;
+    const bool interior = r0 >= 0 && r1 < b.sh && r0 * b.sw + b.c0 >= 0 &&
+                          r1 * b.sw + b.c0 + 8 * 64 <= b.n;
+    if (interior) {
+        if (edge) sk_band<D, true, true>(b, e, lane);
+        else sk_band<D, false, true>(b, e, lane);
+    } else {
+        if (edge) sk_band<D, true, false>(b, e, lane);
+        else sk_band<D, false, false>(b, e, lane);
+    }
+#ifdef VISO_PROBE
+    if (lane == 0) {
+        const long long w = (long long)blockIdx.y * a.units + unit;
+        if (w < 8192 && a.diag >= 0) {
+            g_pyr_tl[w][0] = pr_t0;
+            g_pyr_tl[w][1] = __builtin_amdgcn_s_memrealtime();
+            g_pyr_tl[w][2] = __builtin_amdgcn_s_getreg(4 | (31 << 11));
+            g_pyr_tl[w][3] = __builtin_amdgcn_s_getreg(20 | (31 << 11));
+            g_pyr_tl[w][4] = pr_t0;
+        }
+    }
+#endif
 }
 
 // ---------------------------------------------------------------- FAST
@@ -567,14 +835,29 @@ void launch_pyramid_frames(const PyrGeom& g, const uint8_t* const* l0, uint8_t* 
             a.dh = g.h[l];
             const int bh = l == 1 ? 8 : (l == 2 ? 4 : 2);
             a.bands = (a.dh + bh - 1) / bh;
+#ifdef VISO_PROBE
+            a.diag = getenv("VISO_PYR_DIAG") ? atoi(getenv("VISO_PYR_DIAG")) : 0;
+#endif
             a.units = a.bands * ((a.dw + kPsW - 1) / kPsW);
             const dim3 grid((a.units + 3) / 4, nb);
-            if (l == 1)
+            if (a.sw >= 8) {  // register-only streaming form; the scalar form covers tiny levels
+                const int sbh = l == 1 ? kSkBH1 : (l == 2 ? kSkBH2 : kSkBH3);
+                a.bands = (a.dh + sbh - 1) / sbh;
+                a.units = a.bands * ((a.dw + kSkW - 1) / kSkW);
+                const dim3 sgrid((a.units + 3) / 4, nb);
+                if (l == 1)
+                    pyr_down_sk_kernel<kSkBH1, kSkRing><<<sgrid, 256, 0, stream>>>(a);
+                else if (l == 2)
+                    pyr_down_sk_kernel<kSkBH2, kSkRing><<<sgrid, 256, 0, stream>>>(a);
+                else
+                    pyr_down_sk_kernel<kSkBH3, kSkRing><<<sgrid, 256, 0, stream>>>(a);
+            } else if (l == 1) {
                 pyr_down_stream_kernel<8><<<grid, 256, 0, stream>>>(a);
-            else if (l == 2)
+            } else if (l == 2) {
                 pyr_down_stream_kernel<4><<<grid, 256, 0, stream>>>(a);
-            else
+            } else {
                 pyr_down_stream_kernel<2><<<grid, 256, 0, stream>>>(a);
+            }
         }
     }
 }
@@ -626,3 +909,11 @@ void launch_fast(const uint8_t* img, int w, int h, int thresh, FastScratch& s, f
 }
 
 }  // namespace viso
+
+#ifdef VISO_PROBE
+extern "C" int viso_debug_pyr_timeline(unsigned long long* out, int n) {
+    if (n > 8192) n = 8192;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pyr_tl), sizeof(unsigned long long) * 5 * n) ==
+                   hipSuccess ? 0 : -2;
+}
+#endif
