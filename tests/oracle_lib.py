@@ -55,6 +55,12 @@ SIG = {
     "oracle_viso_alignment": ([_vp, _vp, _vp, _vp, _vp, _i], _i),
     "oracle_viso_keyframe_poses": ([_vp, _vp, _i], _i),
     "oracle_stereo_match": ([_vp, _vp, _i, _i, _vp, _vp, _i, _i, _vp, _vp], None),
+    "oracle_svo_default_params": ([_vp, _i, _i, _d, _d, _d, _d, _d], None),
+    "oracle_svo_features": ([_vp, _i, _i, _vp, _i, _vp, _vp, _vp, _vp], _i),
+    "oracle_svo_responses": ([_vp, _i, _i, _vp, _vp], None),
+    "oracle_svo_match": ([_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _i], _i),
+    "oracle_svo_bucket": ([_vp, _i, _i, _i, _vp, _vp], _i),
+    "oracle_svo_estimate": ([_vp, _i, ctypes.c_int64, _vp, _vp, _vp], _i),
 }
 
 _lib = None
@@ -323,3 +329,146 @@ def fast(img: np.ndarray, thresh: int, cap: int = 1 << 20):
     n = lib.oracle_fast(ptr(img), w, h, thresh, ptr(xs), ptr(ys), ptr(sc), cap)
     n = min(n, cap)
     return xs[:n].copy(), ys[:n].copy(), sc[:n].copy()
+
+
+# ----------------------------------------------------------------- stereo VO (SVO) spec
+class SvoParams(ctypes.Structure):
+    """viso_svo_params (include/viso/viso_svo.h)."""
+    _fields_ = [
+        ("width", ctypes.c_int32), ("height", ctypes.c_int32),
+        ("fx", ctypes.c_double), ("fy", ctypes.c_double), ("cu", ctypes.c_double),
+        ("cv", ctypes.c_double), ("base", ctypes.c_double),
+        ("nms_n", ctypes.c_int32), ("nms_tau", ctypes.c_int32), ("margin", ctypes.c_int32),
+        ("disp_max", ctypes.c_int32), ("match_radius", ctypes.c_int32),
+        ("bucket_width", ctypes.c_int32), ("bucket_height", ctypes.c_int32),
+        ("bucket_max", ctypes.c_int32), ("ransac_iters", ctypes.c_int32),
+        ("gn_iters", ctypes.c_int32), ("inlier_threshold", ctypes.c_double),
+        ("gn_eps", ctypes.c_double), ("seed", ctypes.c_uint64),
+        ("max_features", ctypes.c_int32), ("reserved", ctypes.c_int32 * 7),
+    ]
+
+
+def svo_params(w, h, fx, fy, cu, cv, base, **kw) -> SvoParams:
+    p = SvoParams()
+    load().oracle_svo_default_params(ctypes.byref(p), w, h, fx, fy, cu, cv, base)
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+class SvoFeatures:
+    """Features of one image: u, v, cls (int32), desc (n x 32 u8)."""
+
+    def __init__(self, u, v, cls, desc):
+        self.u, self.v, self.cls, self.desc = u, v, cls, desc
+
+    def __len__(self):
+        return len(self.u)
+
+
+def svo_features(img: np.ndarray, p: SvoParams) -> SvoFeatures:
+    lib = load()
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    cap = p.max_features
+    u, v, c = (np.zeros(cap, np.int32) for _ in range(3))
+    d = np.zeros((cap, 32), np.uint8)
+    n = lib.oracle_svo_features(ptr(img), w, h, ctypes.byref(p), cap, ptr(u), ptr(v), ptr(c), ptr(d))
+    n = min(n, cap)
+    return SvoFeatures(u[:n].copy(), v[:n].copy(), c[:n].copy(), d[:n].copy())
+
+
+def svo_responses(img: np.ndarray):
+    lib = load()
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    b = np.zeros((h, w), np.int32)
+    c = np.zeros((h, w), np.int32)
+    lib.oracle_svo_responses(ptr(img), w, h, ptr(b), ptr(c))
+    return b, c
+
+
+def svo_match(f4, h: int, p: SvoParams) -> np.ndarray:
+    """Circular matches of (L1, R1, L2, R2) -> (n, 4) index quads {l1, r1, l2, r2}."""
+    lib = load()
+    arrs = [(np.ascontiguousarray(f.u), np.ascontiguousarray(f.v), np.ascontiguousarray(f.cls),
+             np.ascontiguousarray(f.desc)) for f in f4]
+    P4 = ctypes.c_void_p * 4
+    u4 = P4(*[a[0].ctypes.data for a in arrs])
+    v4 = P4(*[a[1].ctypes.data for a in arrs])
+    c4 = P4(*[a[2].ctypes.data for a in arrs])
+    d4 = P4(*[a[3].ctypes.data for a in arrs])
+    n4 = np.array([len(f) for f in f4], np.int32)
+    cap = max(1, len(f4[2]))
+    quad = np.zeros((cap, 4), np.int32)
+    n = lib.oracle_svo_match(u4, v4, c4, d4, ptr(n4), h, ctypes.byref(p), ptr(quad), cap)
+    return quad[:n].copy()
+
+
+def svo_uv8(f4, quad: np.ndarray) -> np.ndarray:
+    """Index quads -> {u_l1, v_l1, u_r1, v_r1, u_l2, v_l2, u_r2, v_r2} per match."""
+    out = np.zeros((len(quad), 8), np.int32)
+    for k in range(4):
+        out[:, 2 * k] = f4[k].u[quad[:, k]]
+        out[:, 2 * k + 1] = f4[k].v[quad[:, k]]
+    return out
+
+
+def svo_bucket(uv8: np.ndarray, w: int, h: int, p: SvoParams) -> np.ndarray:
+    lib = load()
+    uv8 = np.ascontiguousarray(uv8, np.int32)
+    keep = np.zeros(max(1, len(uv8)), np.uint8)
+    lib.oracle_svo_bucket(ptr(uv8), len(uv8), w, h, ctypes.byref(p), ptr(keep))
+    return keep[:len(uv8)].astype(bool)
+
+
+def svo_estimate(uv8: np.ndarray, frame: int, p: SvoParams):
+    """-> (motion12, inlier mask, n_inliers or -1)."""
+    lib = load()
+    uv8 = np.ascontiguousarray(uv8, np.int32)
+    motion = np.zeros(12, np.float64)
+    inl = np.zeros(max(1, len(uv8)), np.uint8)
+    n = lib.oracle_svo_estimate(ptr(uv8), len(uv8), frame, ctypes.byref(p), ptr(motion), ptr(inl))
+    return motion, inl[:len(uv8)].astype(bool), n
+
+
+class SvoSequence:
+    """The SVO spec end to end on the CPU: features -> circular matching ->
+    bucketing -> RANSAC + Gauss-Newton; poses accumulate T_wc = T_wc * Tr^-1."""
+
+    def __init__(self, p: SvoParams):
+        self.p = p
+        self.prev = None
+        self.frame = 0
+        self.pose = np.eye(4)
+        self.poses = [self.pose[:3].copy()]
+        self.motion = None
+        self.stats = None
+
+    def process(self, left, right) -> bool:
+        fl, fr = svo_features(left, self.p), svo_features(right, self.p)
+        ok = False
+        self.motion = np.array([1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0], np.float64)
+        n_match = n_bucket = n_inl = 0
+        if self.prev is not None:
+            f4 = [self.prev[0], self.prev[1], fl, fr]
+            quad = svo_match(f4, left.shape[0], self.p)
+            uv8 = svo_uv8(f4, quad)
+            keep = svo_bucket(uv8, left.shape[1], left.shape[0], self.p)
+            sel = uv8[keep]
+            n_match, n_bucket = len(uv8), len(sel)
+            motion, inl, n = svo_estimate(sel, self.frame, self.p)
+            self.matches, self.inliers = sel, inl
+            if n >= 6:
+                ok = True
+                n_inl = n
+                self.motion = motion
+                T = np.eye(4)
+                T[:3, :3] = motion[:9].reshape(3, 3)
+                T[:3, 3] = motion[9:]
+                self.pose = self.pose @ np.linalg.inv(T)
+            self.poses.append(np.concatenate([self.pose[:3, :3].ravel(), self.pose[:3, 3]]))
+        self.stats = [len(fl), len(fr), n_match, n_bucket, n_inl, int(ok)]
+        self.prev = (fl, fr)
+        self.frame += 1
+        return ok

@@ -1,0 +1,148 @@
+"""North-star stereo VO (SVO) stages: the CPU spec (oracle/oracle_svo.cpp) pinned
+by known answers and by the synthetic renderer's ground truth, then GPU parity
+(viso_amd/csrc/svo.hip) against it.  No reference counterpart: "parity
+unpinned vs reference" (SURVEY.md §8a)."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from tests import images, oracle_lib as ol
+
+
+def _params(w=1242, h=375, **kw):
+    return ol.svo_params(w, h, 718.856, 718.856, 607.19, 185.22, 0.54, **kw)
+
+
+def _T(p12):
+    M = np.eye(4)
+    M[:3, :3] = np.asarray(p12[:9]).reshape(3, 3)
+    M[:3, 3] = p12[9:]
+    return M
+
+
+# ------------------------------------------------------------------ CPU: spec known answers
+def test_responses_known_answers():
+    img = np.zeros((20, 20), np.uint8)
+    img[10, 10] = 200
+    b, c = ol.svo_responses(img)
+    assert b[10, 10] == 8 * 200             # centre weight
+    assert b[10, 11] == 200 and b[10, 12] == -200  # inner ring +1, outer ring -1
+    assert b[10, 13] == 0
+    assert c[10, 10] == 0                   # centre row/column weight 0
+    assert c[9, 9] == -200 and c[9, 11] == 200  # TL quadrant -1, TR +1 (relative to the pixel)
+    assert b[0, 0] == 0 and b[1, 10] == 0   # outside the 5x5 domain
+    # checkerboard corner: TL/BR dark, TR/BL bright -> positive corner response
+    chk = np.zeros((20, 20), np.uint8)
+    chk[:10, 10:] = 100
+    chk[10:, :10] = 100
+    _, c = ol.svo_responses(chk)
+    assert c[10, 10] == 8 * 100
+    assert c[10, 10] == c.max()
+
+
+def test_features_nms_and_order():
+    p = _params(64, 48, nms_tau=100, nms_n=2, margin=8)
+    img = np.full((48, 64), 50, np.uint8)
+    img[20, 30] = 250               # blob max
+    img[30, 12] = 0                 # blob min (dark dot on grey)
+    img[30, 40] = 250
+    img[30, 41] = 250               # a plateau pair: equal responses suppress each other
+    f = ol.svo_features(img, p)
+    pts = list(zip(f.v.tolist(), f.u.tolist(), f.cls.tolist()))
+    assert (20, 30, 0) in pts
+    assert (30, 12, 1) in pts
+    assert (30, 40, 0) not in pts and (30, 41, 0) not in pts
+    assert pts == sorted(pts)       # row-major, then u, then class
+    # descriptor of the blob: du at (x-5, y-1) is 0 gradient -> 128
+    i = pts.index((20, 30, 0))
+    assert f.desc[i, 0] == 128
+    # du at (x-1, y-1): right column holds the 250 pixel at weight 1:
+    # d = (250 - 50) -> (200 >> 3) + 128 = 153
+    assert f.desc[i, 6] == 153
+
+
+def test_bucketing_keeps_lowest_indices():
+    p = _params(200, 100, bucket_width=50, bucket_height=50, bucket_max=2)
+    uv8 = np.zeros((6, 8), np.int32)
+    uv8[:, 4] = [10, 20, 30, 60, 15, 70]   # u_l2
+    uv8[:, 5] = [10, 10, 10, 10, 60, 10]   # v_l2
+    keep = ol.svo_bucket(uv8, 200, 100, p)
+    assert keep.tolist() == [True, True, False, True, True, True]
+
+
+def _synthetic_matches(motion, n=300, seed=0, noise=0.0):
+    """Points in front of camera t-1 -> integer observations of both pairs."""
+    rng = np.random.default_rng(seed)
+    fx, fy, cu, cv, b = 718.856, 718.856, 607.19, 185.22, 0.54
+    R, t = motion[:9].reshape(3, 3), motion[9:]
+    out = []
+    while len(out) < n:
+        Z = rng.uniform(5, 40)
+        u1, v1 = rng.uniform(20, 1220), rng.uniform(20, 355)
+        d1 = np.round(fx * b / Z)
+        if d1 < 1:
+            continue
+        u1, v1 = np.round(u1), np.round(v1)
+        Zq = fx * b / d1
+        P = np.array([(u1 - cu) * Zq / fx, (v1 - cv) * Zq / fy, Zq])
+        Q = R @ P + t
+        if Q[2] <= 1:
+            continue
+        uL = fx * Q[0] / Q[2] + cu + rng.normal(0, noise)
+        vL = fy * Q[1] / Q[2] + cv + rng.normal(0, noise)
+        uR = fx * (Q[0] - b) / Q[2] + cu + rng.normal(0, noise)
+        out.append([u1, v1, u1 - d1, v1, np.round(uL), np.round(vL), np.round(uR), np.round(vL)])
+    return np.array(out, np.int32)
+
+
+def test_estimate_recovers_known_motion():
+    p = _params()
+    a = 0.02
+    Rz = np.array([[np.cos(a), -np.sin(a), 0], [np.sin(a), np.cos(a), 0], [0, 0, 1]])
+    motion = np.concatenate([Rz.ravel(), [0.1, -0.05, 0.8]])
+    uv8 = _synthetic_matches(motion, n=400)
+    # 20 % gross outliers
+    rng = np.random.default_rng(1)
+    bad = rng.choice(len(uv8), 80, replace=False)
+    uv8[bad, 4] += rng.integers(20, 60, len(bad))
+    m, inl, n = ol.svo_estimate(uv8, 0, p)
+    assert n >= 250
+    assert not inl[bad].any()
+    assert np.abs(m[:9] - motion[:9]).max() < 2e-3
+    assert np.abs(m[9:] - motion[9:]).max() < 0.05
+
+
+def test_estimate_too_few_matches_fails():
+    p = _params()
+    uv8 = _synthetic_matches(np.array([1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0.5]), n=5)
+    m, inl, n = ol.svo_estimate(uv8, 0, p)
+    assert n == -1 and not inl.any()
+    assert np.array_equal(m, [1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0])
+
+
+@pytest.fixture(scope="module")
+def synth_frames():
+    from viso_amd.synth import Sequence
+    seq = Sequence(1242, 375, seed=0)
+    return seq, [seq.frame(f) for f in range(4)]
+
+
+def test_sequence_tracks_ground_truth(synth_frames):
+    seq, frames = synth_frames
+    p = ol.svo_params(1242, 375, *seq.K, seq.p.baseline)
+    S = ol.SvoSequence(p)
+    for f, (l, r) in enumerate(frames):
+        ok = S.process(l, r)
+        if f == 0:
+            continue
+        assert ok
+        nl, nr, nm, nb, ni, _ = S.stats
+        assert 1500 < nl < 4000 and 1500 < nr < 4000
+        assert nb <= nm and ni > 0.6 * nb
+        gt = _T(seq.pose(f, 0)) @ np.linalg.inv(_T(seq.pose(f - 1, 0)))
+        est = _T(S.motion)
+        assert np.abs(gt[:3, :3] - est[:3, :3]).max() < 1e-3
+        assert np.abs(gt[:3, 3] - est[:3, 3]).max() < 0.01
+    # circular consistency of the last pair's matches: every l2 appears once
+    assert len(np.unique(S.matches[:, 4] * 4096 + S.matches[:, 5])) == len(S.matches)
