@@ -347,9 +347,10 @@ int estimate(const int32_t* uv8, int M, int64_t frame, const viso_svo_params& p,
         double R[9], t[3] = {0, 0, 0};
         std::memcpy(R, kI3, sizeof(R));
         if (sample3(seed, h, M, idx)) {
-            std::fill(sel.begin(), sel.end(), 0);
-            for (int j = 0; j < 3; ++j) sel[(size_t)idx[j]] = 1;
-            if (gauss_newton(obs, sel, p, R, t))
+            // the three samples, in draw order, as a 3-leaf tree: (s0 + s1) + (s2 + 0)
+            const std::vector<Obs> obs3 = {obs[(size_t)idx[0]], obs[(size_t)idx[1]], obs[(size_t)idx[2]]};
+            const std::vector<uint8_t> sel3 = {1, 1, 1};
+            if (gauss_newton(obs3, sel3, p, R, t))
                 for (int i = 0; i < M; ++i) cnt += is_inlier(R, t, obs[(size_t)i], p) ? 1 : 0;
         }
         if (cnt > best_cnt) {
@@ -373,9 +374,13 @@ int estimate(const int32_t* uv8, int M, int64_t frame, const viso_svo_params& p,
         inlier[i] = is_inlier(R, t, obs[(size_t)i], p) ? 1 : 0;
         n_inl += inlier[i];
     }
+    if (n_inl < 6) {
+        for (int i = 0; i < M; ++i) inlier[i] = 0;
+        return -1;  // motion stays the identity
+    }
     for (int i = 0; i < 9; ++i) motion[i] = R[i];
     for (int i = 0; i < 3; ++i) motion[9 + i] = t[i];
-    return n_inl >= 6 ? n_inl : -1;
+    return n_inl;
 }
 
 }  // namespace

@@ -441,7 +441,7 @@ class SvoSequence:
         self.prev = None
         self.frame = 0
         self.pose = np.eye(4)
-        self.poses = [self.pose[:3].copy()]
+        self.poses = [np.concatenate([self.pose[:3, :3].ravel(), self.pose[:3, 3]])]
         self.motion = None
         self.stats = None
 

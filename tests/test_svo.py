@@ -146,3 +146,114 @@ def test_sequence_tracks_ground_truth(synth_frames):
         assert np.abs(gt[:3, 3] - est[:3, 3]).max() < 0.01
     # circular consistency of the last pair's matches: every l2 appears once
     assert len(np.unique(S.matches[:, 4] * 4096 + S.matches[:, 5])) == len(S.matches)
+
+
+def test_params_layout_and_defaults_match_spec():
+    """The library's viso_svo_params / defaults are the spec's (host-only call)."""
+    from viso_amd import svo
+    assert ctypes_sizeof(svo.SvoParams) == ctypes_sizeof(ol.SvoParams)
+    assert [f[0] for f in svo.SvoParams._fields_] == [f[0] for f in ol.SvoParams._fields_]
+    a = svo.default_params(1242, 375, 718.856, 718.856, 607.19, 185.22, 0.54)
+    b = _params()
+    for name, _ in ol.SvoParams._fields_:
+        if name != "reserved":
+            assert getattr(a, name) == getattr(b, name), name
+
+
+def ctypes_sizeof(t):
+    import ctypes
+    return ctypes.sizeof(t)
+
+
+# ------------------------------------------------------------------ GPU parity
+@pytest.fixture(scope="module")
+def gpu_vo():
+    from viso_amd import svo
+    p = svo.default_params(1242, 375, 718.856, 718.856, 607.19, 185.22, 0.54)
+    return svo.VisualOdometryStereo(p)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,h,w,tau,n", [
+    ("synth", 375, 1242, 700, 5), ("mixed", 375, 1242, 700, 5), ("noise", 120, 160, 300, 2),
+    ("blocks", 96, 128, 100, 1), ("synth1080", 1080, 1920, 700, 5), ("smooth", 64, 64, 50, 3)])
+def test_gpu_features_bitexact(kind, h, w, tau, n):
+    from viso_amd import svo
+    if kind.startswith("synth"):
+        from viso_amd.synth import Sequence
+        img = Sequence(w, h, seed=3).image(2, 1)
+    else:
+        img = getattr(images, kind)(h, w, seed=7)
+    p = svo.default_params(w, h, 718.856, 718.856, w / 2, h / 2, 0.54, nms_tau=tau, nms_n=n)
+    vo = svo.VisualOdometryStereo(p)
+    got = vo.features(img)
+    exp = ol.svo_features(img, ol.svo_params(w, h, 718.856, 718.856, w / 2, h / 2, 0.54,
+                                             nms_tau=tau, nms_n=n))
+    assert len(got) == len(exp) > 0
+    for a in ("u", "v", "cls", "desc"):
+        assert np.array_equal(getattr(got, a), getattr(exp, a)), a
+
+
+@pytest.mark.gpu
+def test_gpu_match_bitexact(gpu_vo, synth_frames):
+    seq, frames = synth_frames
+    p = _params()
+    f4 = [ol.svo_features(frames[0][0], p), ol.svo_features(frames[0][1], p),
+          ol.svo_features(frames[1][0], p), ol.svo_features(frames[1][1], p)]
+    exp = ol.svo_match(f4, 375, p)
+    got = gpu_vo.match(f4)
+    assert len(exp) > 500
+    assert np.array_equal(got, exp)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("frame", [1, 2, 3])
+def test_gpu_estimate_bitexact(gpu_vo, synth_frames, frame):
+    seq, frames = synth_frames
+    p = _params()
+    f4 = [ol.svo_features(frames[frame - 1][0], p), ol.svo_features(frames[frame - 1][1], p),
+          ol.svo_features(frames[frame][0], p), ol.svo_features(frames[frame][1], p)]
+    uv8 = ol.svo_uv8(f4, ol.svo_match(f4, 375, p))
+    sel = uv8[ol.svo_bucket(uv8, 1242, 375, p)]
+    m_exp, inl_exp, n_exp = ol.svo_estimate(sel, frame, p)
+    m_got, inl_got, n_got = gpu_vo.estimate(sel, frame)
+    assert n_got == n_exp > 0
+    assert np.array_equal(inl_got, inl_exp)
+    assert np.array_equal(m_got, m_exp)  # fp64, same expression order: bit-exact
+
+
+@pytest.mark.gpu
+def test_gpu_estimate_outliers_and_failure(gpu_vo):
+    p = _params()
+    motion = np.array([1, 0, 0, 0, 1, 0, 0, 0, 1, 0.05, 0, 0.7])
+    uv8 = _synthetic_matches(motion, n=300, seed=4)
+    uv8[::5, 5] += 30
+    for frame in (0, 7):
+        m_exp, inl_exp, n_exp = ol.svo_estimate(uv8, frame, p)
+        m_got, inl_got, n_got = gpu_vo.estimate(uv8, frame)
+        assert n_got == n_exp and np.array_equal(inl_got, inl_exp) and np.array_equal(m_got, m_exp)
+    few = uv8[:5]
+    m_got, inl_got, n_got = gpu_vo.estimate(few, 0)
+    assert n_got == -1 and np.array_equal(m_got, [1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0])
+
+
+@pytest.mark.gpu
+def test_gpu_sequence_matches_oracle(synth_frames):
+    from viso_amd import svo
+    seq, frames = synth_frames
+    p = svo.default_params(1242, 375, *seq.K, seq.p.baseline)
+    vo = svo.VisualOdometryStereo(p)
+    S = ol.SvoSequence(ol.svo_params(1242, 375, *seq.K, seq.p.baseline))
+    for f, (l, r) in enumerate(frames):
+        ok = vo.process(l, r)
+        ok_exp = S.process(l, r)
+        assert ok == ok_exp == (f > 0)
+        assert vo.stats().tolist() == S.stats
+        if f > 0:
+            assert np.array_equal(vo.getMotion()[:3].ravel()[[0, 1, 2, 4, 5, 6, 8, 9, 10]],
+                                  S.motion[:9])
+            uv8, inl = vo.getMatches()
+            assert np.array_equal(uv8, S.matches) and np.array_equal(inl, S.inliers)
+    P = vo.poses
+    assert len(P) == len(S.poses)
+    assert np.allclose(P, np.array(S.poses), rtol=0, atol=1e-9)

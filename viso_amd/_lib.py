@@ -77,6 +77,20 @@ SIGNATURES = {
     "viso_pose_2d2d": [_vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp],
     "viso_stereo_match": [_vp, _vp, _vp, _i32, _i32, _vp, _vp, _i32, _i32, _vp, _vp],
     "viso_version": [],
+    # north-star stereo VO (include/viso/viso_svo.h)
+    "viso_svo_default_params": [_vp, _i32, _i32, _d, _d, _d, _d, _d],
+    "viso_svo_create": [_vp, ctypes.c_int, _vp],
+    "viso_svo_destroy": [_vp],
+    "viso_svo_process": [_vp, _vp, _vp, _vp, _vp],
+    "viso_svo_process_device": [_vp, _vp, _vp, _i32, ctypes.c_int64, _i32],
+    "viso_svo_synchronize": [_vp],
+    "viso_svo_get_motion": [_vp, _vp],
+    "viso_svo_get_stats": [_vp, _vp],
+    "viso_svo_get_poses": [_vp, _vp, _sz, _vp],
+    "viso_svo_get_matches": [_vp, _vp, _vp, _sz, _vp],
+    "viso_svo_features": [_vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _i32, _vp],
+    "viso_svo_match": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
+    "viso_svo_estimate": [_vp, _vp, _i32, ctypes.c_int64, _vp, _vp, _vp],
 }
 _RESTYPES = {"viso_version": ctypes.c_char_p}
 

@@ -1,0 +1,1202 @@
+// viso_amd — north-star stereo visual odometry (SVO) on gfx950.
+//
+// Spec: include/viso/viso_svo.h + DESIGN.md §10; CPU restatement (the parity
+// checker): oracle/oracle_svo.cpp.  No reference counterpart.
+//
+// Per stereo pair (all on one HIP stream, no host round trip):
+//   svo_detect_kernel    image tile -> LDS, 5x5 blob / checkerboard responses,
+//                        strict (2n+1)^2 NMS of the four classes, per-(row,
+//                        tile) candidate lists in (x, class) order
+//   svo_scan_kernel      row-major prefix over the lists -> feature indices
+//   svo_describe_kernel  16 lanes per feature: Sobel du/dv at the 16 sample
+//                        offsets -> 32-byte descriptor, SoA feature arrays
+//   svo_circle_kernel    wave per current-left feature: four best-SAD
+//                        searches (v_sad_u8, wave argmin on (sad, index))
+//                        left_t -> right_t -> right_t-1 -> left_t-1 -> left_t
+//   svo_select_kernel    one workgroup: compaction in left order, bucketing
+//                        (rank within bucket), 3-D points of the matches
+//   svo_ransac_kernel    wave per hypothesis: 3-point Gauss-Newton (lane per
+//                        match), inlier count by ballot over all matches
+//   svo_refine_kernel    one workgroup: best hypothesis, Gauss-Newton over
+//                        its inliers (28 canonical tree sums per iteration),
+//                        inlier flags, motion, pose accumulation
+// Integer stages are exact; the pose math is fp64 with +,-,*,/ only in the
+// oracle's expression order (-ffp-contract=off), so results are bit-identical.
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/viso/viso_svo.h"
+#include "common.hpp"
+
+namespace viso {
+namespace {
+
+constexpr int kTW = 128;        // detect tile: output columns
+constexpr int kTH = 16;         // detect tile: output rows
+constexpr int kMaxNms = 8;      // nms_n bound (LDS sizing)
+constexpr int kListCap = 256;   // candidates per (row, tile): 4 classes x 64 (nms_n >= 1)
+constexpr int kDesc = VISO_SVO_DESC_BYTES;
+
+__constant__ int c_p16[16][2] = {{-5, -1}, {-5, 1}, {-3, -3}, {-3, 3}, {-1, -5}, {-1, 5},
+                                 {-1, -1}, {-1, 1}, {1, -1},  {1, 1},  {1, -5},  {1, 5},
+                                 {3, -3},  {3, 3},  {5, -1},  {5, 1}};
+
+struct SvoDev {  // kernel view of the parameters
+    int w, h, nms_n, tau, margin, disp_max, radius, bw, bh, bmax, iters, gn_iters, cap;
+    double fx, fy, cu, cv, base, th2, eps;
+    uint64_t seed;
+};
+
+// one feature set (an image's features), SoA in device memory
+struct FeatDev {
+    int* u;
+    int* v;
+    int* c;
+    uint8_t* d;    // [cap][32]
+    int* row0;     // [h + 1]: first feature index of each row; row0[h] = n
+    int* n;        // [1]
+    int* cnt;      // [h][tiles] candidate counts
+    int* list;     // [h][tiles][kListCap] packed x | cls << 16
+    int* off;      // [h][tiles] feature index of the first candidate
+};
+
+// ---------------------------------------------------------------- detect
+__global__ __launch_bounds__(256) void svo_detect_kernel(const uint8_t* const* imgs, SvoDev p,
+                                                         FeatDev f0, FeatDev f1, int tiles) {
+    constexpr int RW = kTW + 2 * kMaxNms, RH = kTH + 2 * kMaxNms;   // response region
+    constexpr int IW = RW + 4, IH = RH + 4;                         // image region
+    __shared__ uint8_t s_img[IH][IW];
+    __shared__ short s_b[RH][RW];
+    __shared__ short s_c[RH][RW];
+    const uint8_t* __restrict__ img = imgs[blockIdx.z];
+    const FeatDev F = blockIdx.z == 0 ? f0 : f1;  // by value: no kernarg address taken
+    const int w = p.w, h = p.h, R = p.nms_n;
+    const int x0 = blockIdx.x * kTW, y0 = blockIdx.y * kTH;
+    const int tid = threadIdx.x;
+    // image region [x0 - R - 2, ...) x [y0 - R - 2, ...)
+    const int ix0 = x0 - R - 2, iy0 = y0 - R - 2;
+    const int iw = kTW + 2 * R + 4, ih = kTH + 2 * R + 4;
+    for (int i = tid; i < iw * ih; i += 256) {
+        const int yy = i / iw, xx = i - yy * iw;
+        const int gx = ix0 + xx, gy = iy0 + yy;
+        s_img[yy][xx] = (gx >= 0 && gx < w && gy >= 0 && gy < h) ? img[(size_t)gy * w + gx] : 0;
+    }
+    __syncthreads();
+    // responses over [x0 - R, x0 + kTW + R) x [y0 - R, y0 + kTH + R)
+    const int rw = kTW + 2 * R, rh = kTH + 2 * R;
+    for (int i = tid; i < rw * rh; i += 256) {
+        const int yy = i / rw, xx = i - yy * rw;
+        int b = 0, c = 0;
+#pragma unroll
+        for (int dy = -2; dy <= 2; ++dy)
+#pragma unroll
+            for (int dx = -2; dx <= 2; ++dx) {
+                const int a = s_img[yy + 2 + dy][xx + 2 + dx];
+                const int r = max(abs(dx), abs(dy));
+                b += r == 2 ? -a : (r == 1 ? a : 8 * a);
+                if (dx != 0 && dy != 0) c += ((dx < 0) == (dy < 0)) ? -a : a;
+            }
+        s_b[yy][xx] = (short)b;
+        s_c[yy][xx] = (short)c;
+    }
+    __syncthreads();
+    // NMS + ordered emission: wave k handles rows k, k+4, ...; lane l the
+    // columns 2l, 2l+1 of the tile
+    const int lane = tid & 63, wave = tid >> 6;
+    for (int ry = wave; ry < kTH; ry += 4) {
+        const int y = y0 + ry;
+        if (y >= h) break;
+        int flags = 0;  // bit 4*q + k: column 2l+q, class k
+        if (y >= p.margin && y < h - p.margin) {
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int x = x0 + 2 * lane + q;
+                if (x < p.margin || x >= w - p.margin || 2 * lane + q >= kTW) continue;
+                const int lx = 2 * lane + q + R, ly = ry + R;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    auto M = [&](int yy, int xx) { return k < 2 ? (int)s_b[yy][xx] : (int)s_c[yy][xx]; };
+                    const int sg = (k & 1) ? -1 : 1;
+                    const int r = sg * M(ly, lx);
+                    if (r <= p.tau) continue;
+                    bool mx = true;
+                    for (int dy = -R; dy <= R && mx; ++dy) {
+                        const int qy = y + dy;
+                        if (qy < 2 || qy >= h - 2) continue;
+                        for (int dx = -R; dx <= R; ++dx) {
+                            const int qx = x + dx;
+                            if ((dx == 0 && dy == 0) || qx < 2 || qx >= w - 2) continue;
+                            if (sg * M(ly + dy, lx + dx) >= r) {
+                                mx = false;
+                                break;
+                            }
+                        }
+                    }
+                    if (mx) flags |= 1 << (4 * q + k);
+                }
+            }
+        }
+        // ordered append: (x, class) ascending = lane order, then bit order
+        const int cnt = __popc(flags);
+        int incl = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += t;
+        }
+        const int total = __shfl(incl, 63, 64);
+        int pos = incl - cnt;
+        int* list = F.list + ((size_t)y * tiles + blockIdx.x) * kListCap;
+        for (int b = 0; b < 8; ++b)
+            if (flags & (1 << b)) {
+                if (pos < kListCap) list[pos] = (x0 + 2 * lane + (b >> 2)) | ((b & 3) << 16);
+                ++pos;
+            }
+        if (lane == 0) F.cnt[(size_t)y * tiles + blockIdx.x] = min(total, kListCap);
+    }
+}
+
+// row-major exclusive prefix over the (row, tile) candidate counts
+__global__ __launch_bounds__(1024) void svo_scan_kernel(SvoDev p, FeatDev f0, FeatDev f1, int tiles) {
+    const FeatDev F = blockIdx.x == 0 ? f0 : f1;
+    __shared__ int s_part[1024];
+    const int n = p.h * tiles;
+    const int tid = threadIdx.x;
+    const int per = (n + 1023) / 1024;
+    const int b = tid * per, e = min(b + per, n);
+    int s = 0;
+    for (int i = b; i < e; ++i) s += F.cnt[i];
+    s_part[tid] = s;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const int t = tid >= o ? s_part[tid - o] : 0;
+        __syncthreads();
+        s_part[tid] += t;
+        __syncthreads();
+    }
+    int acc = s_part[tid] - s;
+    for (int i = b; i < e; ++i) {
+        F.off[i] = acc;
+        if (i % tiles == 0) F.row0[i / tiles] = min(acc, p.cap);
+        acc += F.cnt[i];
+    }
+    if (tid == 1023) {
+        F.row0[p.h] = min(s_part[1023], p.cap);
+        *F.n = min(s_part[1023], p.cap);
+    }
+}
+
+__device__ inline int sobel_q(const uint8_t* I, int w, int x, int y, bool du) {
+    auto px = [&](int dx, int dy) { return (int)I[(size_t)(y + dy) * w + x + dx]; };
+    const int d = du ? (px(1, -1) + 2 * px(1, 0) + px(1, 1)) - (px(-1, -1) + 2 * px(-1, 0) + px(-1, 1))
+                     : (px(-1, 1) + 2 * px(0, 1) + px(1, 1)) - (px(-1, -1) + 2 * px(0, -1) + px(1, -1));
+    return (d >> 3) + 128;
+}
+
+// 16 lanes per feature (lane j: sample offset j): descriptor + SoA arrays
+__global__ __launch_bounds__(256) void svo_describe_kernel(const uint8_t* const* imgs, SvoDev p,
+                                                           FeatDev f0, FeatDev f1, int tiles) {
+    const uint8_t* __restrict__ img = imgs[blockIdx.z];
+    const FeatDev F = blockIdx.z == 0 ? f0 : f1;
+    const int y0 = blockIdx.y * kTH;
+    const int j = threadIdx.x & 15, slot = threadIdx.x >> 4;  // 16 features per pass
+    for (int ry = 0; ry < kTH; ++ry) {
+        const int y = y0 + ry;
+        if (y >= p.h) break;
+        const size_t rt = (size_t)y * tiles + blockIdx.x;
+        const int cnt = F.cnt[rt], base = F.off[rt];
+        for (int i = slot; i < cnt; i += 16) {
+            const int o = base + i;
+            if (o >= p.cap) break;
+            const int e = F.list[rt * kListCap + i];
+            const int x = e & 0xffff, k = e >> 16;
+            const int sx = x + c_p16[j][0], sy = y + c_p16[j][1];
+            F.d[(size_t)o * kDesc + j] = (uint8_t)sobel_q(img, p.w, sx, sy, true);
+            F.d[(size_t)o * kDesc + 16 + j] = (uint8_t)sobel_q(img, p.w, sx, sy, false);
+            if (j == 0) {
+                F.u[o] = x;
+                F.v[o] = y;
+                F.c[o] = k;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- matching
+__device__ inline int sad32(const uint4 a0, const uint4 a1, const uint4 b0, const uint4 b1) {
+    unsigned s = 0;
+    s = __builtin_amdgcn_sad_u8(a0.x, b0.x, s);
+    s = __builtin_amdgcn_sad_u8(a0.y, b0.y, s);
+    s = __builtin_amdgcn_sad_u8(a0.z, b0.z, s);
+    s = __builtin_amdgcn_sad_u8(a0.w, b0.w, s);
+    s = __builtin_amdgcn_sad_u8(a1.x, b1.x, s);
+    s = __builtin_amdgcn_sad_u8(a1.y, b1.y, s);
+    s = __builtin_amdgcn_sad_u8(a1.z, b1.z, s);
+    s = __builtin_amdgcn_sad_u8(a1.w, b1.w, s);
+    return (int)s;
+}
+
+__device__ inline unsigned wave_min_u32(unsigned v) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) v = min(v, (unsigned)__shfl_xor((int)v, o, 64));
+    return v;
+}
+
+// best candidate in `S` for the query (u, v, class, desc): rows [v - dv, v + dv]
+// (a contiguous index range), u - du_hi <= u' <= u - du_lo; min SAD, ties ->
+// lowest index.  Wave-uniform arguments; returns -1 if none.
+__device__ int best_match(const FeatDev& S, int h, int u, int v, int c, uint4 q0, uint4 q1, int du_lo,
+                          int du_hi, int dv) {
+    const int lane = threadIdx.x & 63;
+    const int b = S.row0[max(v - dv, 0)], e = S.row0[min(v + dv, h - 1) + 1];
+    unsigned best = 0xffffffffu;
+    for (int j = b + lane; j < e; j += 64) {
+        if (S.c[j] != c) continue;
+        const int dd = u - S.u[j];
+        if (dd < du_lo || dd > du_hi) continue;
+        const uint4* dj = reinterpret_cast<const uint4*>(S.d + (size_t)j * kDesc);
+        const int s = sad32(q0, q1, dj[0], dj[1]);
+        best = min(best, ((unsigned)s << 15) | (unsigned)j);
+    }
+    best = wave_min_u32(best);
+    return best == 0xffffffffu ? -1 : (int)(best & 0x7fffu);
+}
+
+// wave per current-left feature; out[i2] = {l1, r1, r2} or l1 = -1
+__global__ __launch_bounds__(256) void svo_circle_kernel(SvoDev p, FeatDev L1, FeatDev R1, FeatDev L2,
+                                                         FeatDev R2, int4* __restrict__ out) {
+    const int n2 = *L2.n;
+    const int D = p.disp_max, Rr = p.radius, h = p.h;
+    auto desc = [](const FeatDev& S, int i, uint4& a, uint4& b) {
+        const uint4* d = reinterpret_cast<const uint4*>(S.d + (size_t)i * kDesc);
+        a = d[0];
+        b = d[1];
+    };
+    for (int i2 = blockIdx.x * 4 + (threadIdx.x >> 6); i2 < n2; i2 += gridDim.x * 4) {
+        const int c = L2.c[i2];
+        uint4 a, b;
+        int4 res = make_int4(-1, -1, -1, 0);
+        desc(L2, i2, a, b);
+        const int r2 = best_match(R2, h, L2.u[i2], L2.v[i2], c, a, b, 0, D, 1);
+        if (r2 >= 0) {
+            desc(R2, r2, a, b);
+            const int r1 = best_match(R1, h, R2.u[r2], R2.v[r2], c, a, b, -Rr, Rr, Rr);
+            if (r1 >= 0) {
+                desc(R1, r1, a, b);
+                const int l1 = best_match(L1, h, R1.u[r1], R1.v[r1], c, a, b, -D, 0, 1);
+                if (l1 >= 0) {
+                    desc(L1, l1, a, b);
+                    const int i2b = best_match(L2, h, L1.u[l1], L1.v[l1], c, a, b, -Rr, Rr, Rr);
+                    if (i2b == i2 && L1.u[l1] - R1.u[r1] >= 1 && L2.u[i2] - R2.u[r2] >= 1)
+                        res = make_int4(l1, r1, r2, 0);
+                }
+            }
+        }
+        if ((threadIdx.x & 63) == 0) out[i2] = res;
+    }
+}
+
+// ---------------------------------------------------------------- pose math
+// (oracle_svo.cpp: make_obs, transform, residual_rows, match_sums, solve6,
+// apply_update, is_inlier — same expressions, same order)
+struct Obs {
+    double X, Y, Z, uL, vL, uR, vR;
+};
+
+__device__ inline Obs make_obs(const int* m, const SvoDev& p) {
+    Obs o;
+    const double d = (double)(m[0] - m[2]);
+    o.Z = (p.fx * p.base) / d;
+    o.X = (((double)m[0] - p.cu) * o.Z) / p.fx;
+    o.Y = (((double)m[1] - p.cv) * o.Z) / p.fy;
+    o.uL = (double)m[4];
+    o.vL = (double)m[5];
+    o.uR = (double)m[6];
+    o.vR = (double)m[7];
+    return o;
+}
+
+__device__ inline void transform(const double* R, const double* t, const Obs& o, double* P) {
+    P[0] = ((R[0] * o.X + R[1] * o.Y) + R[2] * o.Z) + t[0];
+    P[1] = ((R[3] * o.X + R[4] * o.Y) + R[5] * o.Z) + t[1];
+    P[2] = ((R[6] * o.X + R[7] * o.Y) + R[8] * o.Z) + t[2];
+}
+
+__device__ inline void residual_rows(const double* P, const Obs& o, const SvoDev& p, double* e,
+                                     double (*J)[6]) {
+    const double iz = 1.0 / P[2];
+    const double iz2 = iz * iz;
+    const double xr = P[0] - p.base;
+    const double pu = ((p.fx * P[0]) * iz) + p.cu;
+    const double pv = ((p.fy * P[1]) * iz) + p.cv;
+    const double pr = ((p.fx * xr) * iz) + p.cu;
+    e[0] = o.uL - pu;
+    e[1] = o.vL - pv;
+    e[2] = o.uR - pr;
+    e[3] = o.vR - pv;
+    const double g[4][3] = {{p.fx * iz, 0.0, -(p.fx * P[0]) * iz2},
+                            {0.0, p.fy * iz, -(p.fy * P[1]) * iz2},
+                            {p.fx * iz, 0.0, -(p.fx * xr) * iz2},
+                            {0.0, p.fy * iz, -(p.fy * P[1]) * iz2}};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const double gx = g[r][0], gy = g[r][1], gz = g[r][2];
+        J[r][0] = gz * P[1] - gy * P[2];
+        J[r][1] = gx * P[2] - gz * P[0];
+        J[r][2] = gy * P[0] - gx * P[1];
+        J[r][3] = gx;
+        J[r][4] = gy;
+        J[r][5] = gz;
+    }
+}
+
+__device__ inline void match_sums(const double* e, const double (*J)[6], double* s) {
+    int k = 0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+        for (int b = a; b < 6; ++b, ++k)
+            s[k] = ((J[0][a] * J[0][b] + J[1][a] * J[1][b]) + J[2][a] * J[2][b]) + J[3][a] * J[3][b];
+#pragma unroll
+    for (int a = 0; a < 6; ++a, ++k) s[k] = ((J[0][a] * e[0] + J[1][a] * e[1]) + J[2][a] * e[2]) + J[3][a] * e[3];
+    s[27] = ((e[0] * e[0] + e[1] * e[1]) + e[2] * e[2]) + e[3] * e[3];
+}
+
+// the 28 sums of match o under (R, t); zeros if !sel
+__device__ inline void match_leaf(const double* R, const double* t, const Obs& o, const SvoDev& p,
+                                  bool sel, double* s) {
+    if (!sel) {
+#pragma unroll
+        for (int k = 0; k < 28; ++k) s[k] = 0.0;
+        return;
+    }
+    double P[3], e[4], J[4][6];
+    transform(R, t, o, P);
+    residual_rows(P, o, p, e, J);
+    match_sums(e, J, s);
+}
+
+__device__ inline bool solve6(const double* S, double* x) {
+    double A[6][6], g[6];
+    int k = 0;
+    for (int a = 0; a < 6; ++a)
+        for (int b = a; b < 6; ++b, ++k) A[a][b] = A[b][a] = S[k];
+    for (int a = 0; a < 6; ++a) g[a] = S[21 + a];
+    for (int c = 0; c < 6; ++c) {
+        int piv = c;
+        double best = fabs(A[c][c]);
+        for (int i = c + 1; i < 6; ++i)
+            if (fabs(A[i][c]) > best) {
+                best = fabs(A[i][c]);
+                piv = i;
+            }
+        if (!(best >= 1e-12)) return false;
+        if (piv != c) {
+            for (int j = 0; j < 6; ++j) {
+                const double t = A[c][j];
+                A[c][j] = A[piv][j];
+                A[piv][j] = t;
+            }
+            const double t = g[c];
+            g[c] = g[piv];
+            g[piv] = t;
+        }
+        for (int i = c + 1; i < 6; ++i) {
+            const double f = A[i][c] / A[c][c];
+            for (int j = c; j < 6; ++j) A[i][j] = A[i][j] - f * A[c][j];
+            g[i] = g[i] - f * g[c];
+        }
+    }
+    for (int i = 5; i >= 0; --i) {
+        double s = g[i];
+        for (int j = i + 1; j < 6; ++j) s = s - A[i][j] * x[j];
+        x[i] = s / A[i][i];
+    }
+    return true;
+}
+
+__device__ inline void mat3_mul_s(const double* A, const double* B, double* C) {
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            C[3 * i + j] = (A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j]) + A[3 * i + 2] * B[6 + j];
+}
+
+__device__ inline void apply_update(const double* x, double* R, double* t) {
+    const double w2 = (x[0] * x[0] + x[1] * x[1]) + x[2] * x[2];
+    const double c = 1.0 / (1.0 + 0.25 * w2);
+    const double W[9] = {0.0, -x[2], x[1], x[2], 0.0, -x[0], -x[1], x[0], 0.0};
+    double W2[9], Q[9], Rn[9], tn[3];
+    mat3_mul_s(W, W, W2);
+    for (int i = 0; i < 9; ++i) Q[i] = ((i % 4 == 0) ? 1.0 : 0.0) + c * (W[i] + 0.5 * W2[i]);
+    mat3_mul_s(Q, R, Rn);
+    for (int i = 0; i < 3; ++i) tn[i] = ((Q[3 * i] * t[0] + Q[3 * i + 1] * t[1]) + Q[3 * i + 2] * t[2]) + x[3 + i];
+    for (int i = 0; i < 9; ++i) R[i] = Rn[i];
+    for (int i = 0; i < 3; ++i) t[i] = tn[i];
+}
+
+__device__ inline bool is_inlier(const double* R, const double* t, const Obs& o, const SvoDev& p) {
+    double P[3], e[4], J[4][6];
+    transform(R, t, o, P);
+    if (!(P[2] > 0.0)) return false;
+    residual_rows(P, o, p, e, J);
+    const double d2 = ((e[0] * e[0] + e[1] * e[1]) + e[2] * e[2]) + e[3] * e[3];
+    return d2 < p.th2;
+}
+
+__device__ inline double shfl_xor_f64(double v, int m) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __shfl_xor((int)(b & 0xffffffffLL), m, 64);
+    const int hi = __shfl_xor((int)(b >> 32), m, 64);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// canonical pairwise tree of lanes [0, 2^levels) (ascending xor butterfly)
+__device__ inline double lane_tree(double v, int levels) {
+    for (int s = 0; s < levels; ++s) v = v + shfl_xor_f64(v, 1 << s);
+    return v;
+}
+
+// ---------------------------------------------------------------- selection
+// One workgroup: (1) compact circular matches in left order, (2) bucketing
+// rank (matches before it in its bucket), (3) compact the kept matches ->
+// uv8 + points; stats[2] = circular matches, stats[3] = bucketed.
+constexpr int kMaxBuckets = 4096;
+
+__global__ __launch_bounds__(256) void svo_select_kernel(SvoDev p, FeatDev L1, FeatDev R1, FeatDev L2,
+                                                         FeatDev R2, const int4* __restrict__ circ,
+                                                         int* __restrict__ all_idx,
+                                                         int* __restrict__ uv8, int* __restrict__ n_sel,
+                                                         int* __restrict__ stats) {
+    __shared__ int s_cnt[kMaxBuckets];
+    __shared__ int s_scan[256];
+    __shared__ int s_bkt[256];
+    __shared__ int s_base;
+    const int tid = threadIdx.x;
+    const int n2 = *L2.n;
+    const int nbx = (p.w + p.bw - 1) / p.bw, nby = (p.h + p.bh - 1) / p.bh;
+    for (int i = tid; i < nbx * nby; i += 256) s_cnt[i] = 0;
+    if (tid == 0) s_base = 0;
+    __syncthreads();
+    // (1) compaction of circ[i2].x >= 0 in i2 order
+    for (int c0 = 0; c0 < n2; c0 += 256) {
+        const int i2 = c0 + tid;
+        const int f = (i2 < n2 && circ[i2].x >= 0) ? 1 : 0;
+        s_scan[tid] = f;
+        __syncthreads();
+        for (int o = 1; o < 256; o <<= 1) {
+            const int t = tid >= o ? s_scan[tid - o] : 0;
+            __syncthreads();
+            s_scan[tid] += t;
+            __syncthreads();
+        }
+        if (f) all_idx[s_base + s_scan[tid] - 1] = i2;
+        __syncthreads();
+        if (tid == 255) s_base += s_scan[255];
+        __syncthreads();
+    }
+    const int m_all = s_base;
+    __syncthreads();
+    if (tid == 0) s_base = 0;
+    __syncthreads();
+    // (2)+(3) bucketing in match order
+    for (int c0 = 0; c0 < m_all; c0 += 256) {
+        const int m = c0 + tid;
+        int b = -1;
+        if (m < m_all) {
+            const int i2 = all_idx[m];
+            b = (L2.v[i2] / p.bh) * nbx + L2.u[i2] / p.bw;
+        }
+        s_bkt[tid] = b;
+        __syncthreads();
+        int before = 0;
+        if (b >= 0)
+            for (int t = 0; t < tid; ++t) before += s_bkt[t] == b ? 1 : 0;
+        const int keep = (b >= 0 && s_cnt[b] + before < p.bmax) ? 1 : 0;
+        __syncthreads();
+        if (b >= 0) atomicAdd(&s_cnt[b], 1);
+        s_scan[tid] = keep;
+        __syncthreads();
+        for (int o = 1; o < 256; o <<= 1) {
+            const int t = tid >= o ? s_scan[tid - o] : 0;
+            __syncthreads();
+            s_scan[tid] += t;
+            __syncthreads();
+        }
+        if (keep) {
+            const int o = s_base + s_scan[tid] - 1;
+            const int i2 = all_idx[m];
+            const int4 q = circ[i2];
+            int* r = uv8 + 8 * (size_t)o;
+            r[0] = L1.u[q.x];
+            r[1] = L1.v[q.x];
+            r[2] = R1.u[q.y];
+            r[3] = R1.v[q.y];
+            r[4] = L2.u[i2];
+            r[5] = L2.v[i2];
+            r[6] = R2.u[q.z];
+            r[7] = R2.v[q.z];
+        }
+        __syncthreads();
+        if (tid == 255) s_base += s_scan[255];
+        __syncthreads();
+    }
+    if (tid == 0) {
+        *n_sel = s_base;
+        stats[2] = m_all;
+        stats[3] = s_base;
+    }
+}
+
+// ---------------------------------------------------------------- RANSAC
+__device__ inline bool sample3(uint64_t seed, int h, int M, int* idx) {
+    int got = 0;
+    for (int k = 0; k < 16 && got < 3; ++k) {
+        const int r = (int)(mix64(seed + (uint64_t)h * 16u + (uint64_t)k) % (uint64_t)M);
+        bool dup = false;
+        for (int j = 0; j < got; ++j) dup = dup || idx[j] == r;
+        if (!dup) idx[got++] = r;
+    }
+    return got == 3;
+}
+
+// wave per hypothesis: counts[h], models[h] = R(9) t(3)
+__global__ __launch_bounds__(256) void svo_ransac_kernel(SvoDev p, const int* __restrict__ uv8,
+                                                         const int* __restrict__ n_sel, uint64_t seed,
+                                                         int* __restrict__ counts, double* __restrict__ models) {
+    __shared__ double s_st[4][12];
+    __shared__ int s_ok[4];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int hyp = blockIdx.x * 4 + wave;
+    const int M = *n_sel;
+    if (hyp >= p.iters) return;
+    double* st = s_st[wave];
+    if (M < 6) {
+        if (lane == 0) counts[hyp] = 0;
+        return;
+    }
+    int idx[3];
+    const bool okS = sample3(seed, hyp, M, idx);
+    if (lane < 12) st[lane] = (lane % 4 == 0 && lane < 9) ? 1.0 : 0.0;
+    if (lane == 0) s_ok[wave] = okS ? 1 : 0;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    // lanes 0..2: the sampled matches; lanes 3: a zero leaf (tree over 4)
+    Obs o{};
+    if (lane < 3 && okS) o = make_obs(uv8 + 8 * (size_t)idx[lane], p);
+    for (int it = 0; it < p.gn_iters && s_ok[wave]; ++it) {
+        double R[9], t[3];
+        for (int i = 0; i < 9; ++i) R[i] = st[i];
+        for (int i = 0; i < 3; ++i) t[i] = st[9 + i];
+        double s[28];
+        match_leaf(R, t, o, p, lane < 3, s);
+        double S[28];
+#pragma unroll
+        for (int k = 0; k < 28; ++k) S[k] = lane_tree(s[k], 2);
+        int conv = 0;
+        if (lane == 0) {
+            double x[6];
+            if (!solve6(S, x)) {
+                s_ok[wave] = 0;
+            } else {
+                apply_update(x, R, t);
+                for (int i = 0; i < 9; ++i) st[i] = R[i];
+                for (int i = 0; i < 3; ++i) st[9 + i] = t[i];
+                double mx = 0.0;
+                for (int k = 0; k < 6; ++k) mx = fmax(mx, fabs(x[k]));
+                conv = mx < p.eps ? 1 : 0;
+            }
+        }
+        conv = __shfl(conv, 0, 64);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (conv) break;
+    }
+    double R[9], t[3];
+    for (int i = 0; i < 9; ++i) R[i] = st[i];
+    for (int i = 0; i < 3; ++i) t[i] = st[9 + i];
+    int cnt = 0;
+    if (s_ok[wave]) {
+        for (int m0 = 0; m0 < M; m0 += 64) {
+            const int m = m0 + lane;
+            bool in = false;
+            if (m < M) in = is_inlier(R, t, make_obs(uv8 + 8 * (size_t)m, p), p);
+            cnt += __popcll(__ballot(in));
+        }
+    } else {
+        for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0) ? 1.0 : 0.0;
+        for (int i = 0; i < 3; ++i) t[i] = 0.0;
+    }
+    if (lane == 0) counts[hyp] = cnt;
+    if (lane < 12) models[(size_t)hyp * 12 + lane] = lane < 9 ? R[lane] : t[lane - 9];
+}
+
+// ---------------------------------------------------------------- refine
+// One workgroup: best hypothesis (max count, lowest index), Gauss-Newton over
+// its inliers (sums: canonical tree over all M leaves, unselected = 0), final
+// inlier flags, motion, pose update T_wc <- T_wc * Tr^-1, stats.
+constexpr int kMaxChunks = 128;  // 64-leaf chunks: M <= 8192 (bucket count x bucket_max)
+
+__global__ __launch_bounds__(256) void svo_refine_kernel(SvoDev p, const int* __restrict__ uv8,
+                                                         const int* __restrict__ n_sel,
+                                                         const int* __restrict__ counts,
+                                                         const double* __restrict__ models,
+                                                         uint8_t* __restrict__ sel, uint8_t* __restrict__ inl,
+                                                         double* __restrict__ motion, double* __restrict__ pose,
+                                                         double* __restrict__ pose_log, int* __restrict__ stats) {
+    __shared__ double s_chunk[kMaxChunks][28];
+    __shared__ double s_st[12];
+    __shared__ int s_best, s_ok, s_conv, s_cnt;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int M = *n_sel;
+    if (tid == 0) {
+        int bh = -1, bc = -1;
+        for (int h = 0; h < p.iters; ++h)
+            if (counts[h] > bc) {
+                bc = counts[h];
+                bh = h;
+            }
+        s_best = (M >= 6 && bc >= 6) ? bh : -1;
+        s_ok = s_best >= 0 ? 1 : 0;
+        s_cnt = 0;
+    }
+    __syncthreads();
+    const int best = s_best;
+    if (tid < 12) s_st[tid] = best >= 0 ? models[(size_t)best * 12 + tid] : ((tid % 4 == 0 && tid < 9) ? 1.0 : 0.0);
+    __syncthreads();
+    if (best >= 0) {
+        double R[9], t[3];
+        for (int i = 0; i < 9; ++i) R[i] = s_st[i];
+        for (int i = 0; i < 3; ++i) t[i] = s_st[9 + i];
+        for (int m = tid; m < M; m += 256) sel[m] = is_inlier(R, t, make_obs(uv8 + 8 * (size_t)m, p), p) ? 1 : 0;
+        __syncthreads();
+        int P2 = 1;
+        while (P2 < M) P2 <<= 1;
+        const int nch = (P2 + 63) / 64;               // chunks of 64 leaves (P2 >= 64) or 1
+        const int lv_in = P2 >= 64 ? 6 : __builtin_ctz(P2);
+        int lv_out = 0;
+        while ((1 << lv_out) < nch) ++lv_out;
+        for (int it = 0; it < p.gn_iters; ++it) {
+            for (int i = 0; i < 9; ++i) R[i] = s_st[i];
+            for (int i = 0; i < 3; ++i) t[i] = s_st[9 + i];
+            for (int ch = wave; ch < nch; ch += 4) {
+                const int m = ch * 64 + lane;
+                double s[28];
+                if (m < M) match_leaf(R, t, make_obs(uv8 + 8 * (size_t)m, p), p, sel[m] != 0, s);
+                else
+                    for (int k = 0; k < 28; ++k) s[k] = 0.0;
+                if (lv_in == 6) {
+                    int vi;
+                    const double r = reduce_scatter_28(s, &vi);
+                    if (vi >= 0 && lane < 32) s_chunk[ch][vi] = r;
+                } else {
+                    for (int k = 0; k < 28; ++k) {
+                        const double r = lane_tree(s[k], lv_in);
+                        if (lane == 0) s_chunk[ch][k] = r;
+                    }
+                }
+            }
+            __syncthreads();
+            if (wave == 0) {
+                // pairwise tree over the chunk sums (padded to 2^lv_out with zeros)
+                double S[28];
+                for (int k = 0; k < 28; ++k) {
+                    if (lv_out <= 6) {
+                        S[k] = lane_tree(lane < nch ? s_chunk[lane][k] : 0.0, lv_out);
+                    } else {
+                        // more than 64 chunks: each lane first sums its aligned block of
+                        // `per` chunks (pairwise), then the 64 block sums
+                        const int per = (1 << lv_out) / 64;
+                        double a[2];
+                        for (int q = 0; q < per; ++q) a[q] = s_chunk[lane * per + q][k];
+                        S[k] = lane_tree(per == 2 ? a[0] + a[1] : a[0], 6);
+                    }
+                }
+                if (lane == 0) {
+                    double x[6];
+                    if (!solve6(S, x)) {
+                        s_ok = 0;
+                        s_conv = 1;
+                    } else {
+                        apply_update(x, R, t);
+                        for (int i = 0; i < 9; ++i) s_st[i] = R[i];
+                        for (int i = 0; i < 3; ++i) s_st[9 + i] = t[i];
+                        double mx = 0.0;
+                        for (int k = 0; k < 6; ++k) mx = fmax(mx, fabs(x[k]));
+                        s_conv = mx < p.eps ? 1 : 0;
+                    }
+                }
+            }
+            __syncthreads();
+            if (s_conv) break;
+            __syncthreads();
+        }
+        if (!s_ok && tid < 12) s_st[tid] = models[(size_t)best * 12 + tid];  // keep the hypothesis
+        __syncthreads();
+        for (int i = 0; i < 9; ++i) R[i] = s_st[i];
+        for (int i = 0; i < 3; ++i) t[i] = s_st[9 + i];
+        int c = 0;
+        for (int m = tid; m < M; m += 256) {
+            const bool in = is_inlier(R, t, make_obs(uv8 + 8 * (size_t)m, p), p);
+            inl[m] = in ? 1 : 0;
+            c += in ? 1 : 0;
+        }
+        atomicAdd(&s_cnt, c);
+        __syncthreads();
+    } else {
+        for (int m = tid; m < M; m += 256) inl[m] = 0;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const bool ok = best >= 0 && s_cnt >= 6;
+        double T[12];
+        for (int i = 0; i < 12; ++i) T[i] = ok ? s_st[i] : ((i % 4 == 0 && i < 9) ? 1.0 : 0.0);
+        for (int i = 0; i < 12; ++i) motion[i] = T[i];
+        stats[4] = ok ? s_cnt : 0;
+        stats[5] = ok ? 1 : 0;
+        if (ok) {
+            // T_wc <- T_wc * Tr^-1,  Tr^-1 = [R^T, -R^T t]
+            double Ri[9], ti[3];
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) Ri[3 * i + j] = T[3 * j + i];
+            for (int i = 0; i < 3; ++i) ti[i] = -((Ri[3 * i] * T[9] + Ri[3 * i + 1] * T[10]) + Ri[3 * i + 2] * T[11]);
+            double Rn[9], tn[3];
+            mat3_mul_s(pose, Ri, Rn);
+            for (int i = 0; i < 3; ++i) tn[i] = ((pose[3 * i] * ti[0] + pose[3 * i + 1] * ti[1]) + pose[3 * i + 2] * ti[2]) + pose[9 + i];
+            for (int i = 0; i < 9; ++i) pose[i] = Rn[i];
+            for (int i = 0; i < 3; ++i) pose[9 + i] = tn[i];
+        }
+        for (int i = 0; i < 12; ++i) pose_log[i] = pose[i];
+    }
+}
+
+__global__ void svo_stats_kernel(FeatDev a, FeatDev b, int* stats, double* pose, double* pose_log,
+                                 int first) {
+    stats[0] = *a.n;
+    stats[1] = *b.n;
+    if (first) {
+        for (int i = 2; i < 6; ++i) stats[i] = 0;
+        for (int i = 0; i < 12; ++i) {
+            pose[i] = (i % 4 == 0 && i < 9) ? 1.0 : 0.0;
+            pose_log[i] = pose[i];
+        }
+    }
+}
+
+}  // namespace
+}  // namespace viso
+
+// ====================================================================== context
+using namespace viso;
+
+struct viso_svo {
+    viso_svo_params p{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int tiles = 0;
+    size_t frame = 0;       // pairs processed
+    int have_prev = 0;
+    // feature sets: 4 slots (ping-pong pairs)
+    FeatDev set[4]{};
+    int cur = 0;            // slot pair of the current frame: sets 2*cur, 2*cur + 1
+    std::vector<void*> allocs;
+    uint8_t* img = nullptr;       // host-path upload buffer (left, right)
+    int4* circ = nullptr;
+    int* all_idx = nullptr;
+    int* uv8 = nullptr;
+    int* n_sel = nullptr;
+    int* counts = nullptr;
+    double* models = nullptr;
+    uint8_t* sel = nullptr;
+    uint8_t* inl = nullptr;
+    double* motion = nullptr;
+    double* pose = nullptr;
+    double* pose_log = nullptr;   // [max_poses][12]
+    int* stats = nullptr;
+    size_t max_poses = 0;
+    size_t n_poses = 0;
+    const uint8_t** imgs = nullptr;  // device array of 2 image pointers
+
+    SvoDev dev() const {
+        SvoDev d;
+        d.w = p.width;
+        d.h = p.height;
+        d.nms_n = p.nms_n;
+        d.tau = p.nms_tau;
+        d.margin = p.margin;
+        d.disp_max = p.disp_max;
+        d.radius = p.match_radius;
+        d.bw = p.bucket_width;
+        d.bh = p.bucket_height;
+        d.bmax = p.bucket_max;
+        d.iters = p.ransac_iters;
+        d.gn_iters = p.gn_iters;
+        d.cap = p.max_features;
+        d.fx = p.fx;
+        d.fy = p.fy;
+        d.cu = p.cu;
+        d.cv = p.cv;
+        d.base = p.base;
+        d.th2 = p.inlier_threshold * p.inlier_threshold;
+        d.eps = p.gn_eps;
+        d.seed = p.seed;
+        return d;
+    }
+    template <class T>
+    int alloc(T*& ptr, size_t n) {
+        void* q = nullptr;
+        VISO_HIP_CHECK(hipMalloc(&q, std::max<size_t>(n * sizeof(T), 256)));
+        VISO_HIP_CHECK(hipMemset(q, 0, std::max<size_t>(n * sizeof(T), 256)));
+        allocs.push_back(q);
+        ptr = (T*)q;
+        return VISO_OK;
+    }
+    int init() {
+        const int w = p.width, h = p.height, cap = p.max_features;
+        tiles = (w + kTW - 1) / kTW;
+        for (int k = 0; k < 4; ++k) {
+            FeatDev& f = set[k];
+            if (alloc(f.u, cap) || alloc(f.v, cap) || alloc(f.c, cap) || alloc(f.d, (size_t)cap * kDesc) ||
+                alloc(f.row0, (size_t)h + 1) || alloc(f.n, 1) || alloc(f.cnt, (size_t)h * tiles) ||
+                alloc(f.list, (size_t)h * tiles * kListCap) || alloc(f.off, (size_t)h * tiles))
+                return VISO_ERR_HIP;
+        }
+        max_poses = 65536;
+        if (alloc(img, 2 * (size_t)w * h) || alloc(circ, cap) || alloc(all_idx, cap) ||
+            alloc(uv8, (size_t)cap * 8) || alloc(n_sel, 1) || alloc(counts, std::max(1, p.ransac_iters)) ||
+            alloc(models, (size_t)std::max(1, p.ransac_iters) * 12) || alloc(sel, cap) || alloc(inl, cap) ||
+            alloc(motion, 12) || alloc(pose, 12) || alloc(pose_log, max_poses * 12) || alloc(stats, 8) ||
+            alloc(imgs, 2 * kMaxPairBatch))
+            return VISO_ERR_HIP;
+        return VISO_OK;
+    }
+    static constexpr int kMaxPairBatch = 256;
+    void release() {
+        for (void* q : allocs) (void)hipFree(q);
+        allocs.clear();
+        if (stream) (void)hipStreamDestroy(stream);
+        stream = nullptr;
+    }
+
+    // features of the pair at device pointers (l, r) into the current slots
+    int detect(const uint8_t* const* pair_ptrs_dev) {
+        const SvoDev d = dev();
+        FeatDev& A = set[2 * cur];
+        FeatDev& B = set[2 * cur + 1];
+        const dim3 g(tiles, (p.height + kTH - 1) / kTH, 2);
+        svo_detect_kernel<<<g, 256, 0, stream>>>(pair_ptrs_dev, d, A, B, tiles);
+        svo_scan_kernel<<<2, 1024, 0, stream>>>(d, A, B, tiles);
+        svo_describe_kernel<<<g, 256, 0, stream>>>(pair_ptrs_dev, d, A, B, tiles);
+        VISO_HIP_CHECK(hipGetLastError());
+        return VISO_OK;
+    }
+    int match_and_estimate() {
+        const SvoDev d = dev();
+        FeatDev &L1 = set[2 * (cur ^ 1)], &R1 = set[2 * (cur ^ 1) + 1], &L2 = set[2 * cur],
+                &R2 = set[2 * cur + 1];
+        svo_circle_kernel<<<1024, 256, 0, stream>>>(d, L1, R1, L2, R2, circ);
+        svo_select_kernel<<<1, 256, 0, stream>>>(d, L1, R1, L2, R2, circ, all_idx, uv8, n_sel, stats);
+        const uint64_t seed = mix64(p.seed ^ (uint64_t)frame);
+        svo_ransac_kernel<<<(p.ransac_iters + 3) / 4, 256, 0, stream>>>(d, uv8, n_sel, seed, counts, models);
+        svo_refine_kernel<<<1, 256, 0, stream>>>(d, uv8, n_sel, counts, models, sel, inl, motion, pose,
+                                                 pose_log + 12 * std::min(n_poses, max_poses - 1), stats);
+        VISO_HIP_CHECK(hipGetLastError());
+        return VISO_OK;
+    }
+    // one pair at device pointers
+    int step(const uint8_t* const* pair_ptrs_dev) {
+        int rc = detect(pair_ptrs_dev);
+        if (rc) return rc;
+        FeatDev &A = set[2 * cur], &B = set[2 * cur + 1];
+        svo_stats_kernel<<<1, 1, 0, stream>>>(A, B, stats, pose, pose_log + 12 * std::min(n_poses, max_poses - 1),
+                                              have_prev ? 0 : 1);
+        if (have_prev) {
+            rc = match_and_estimate();
+            if (rc) return rc;
+        }
+        have_prev = 1;
+        ++frame;
+        ++n_poses;
+        cur ^= 1;
+        return VISO_OK;
+    }
+};
+
+namespace {
+int svo_check(const viso_svo_params* p) {
+    if (!p || p->width < 32 || p->height < 32 || p->width > 32767 || p->nms_n < 1 ||
+        p->nms_n > kMaxNms || p->margin < 8 || p->max_features < 1 || p->max_features > 32768 ||
+        p->bucket_width < 1 || p->bucket_height < 1 || p->ransac_iters < 1 || p->gn_iters < 1 ||
+        p->disp_max < 0 || p->match_radius < 0 || !(p->base > 0) || !(p->fx > 0) || !(p->fy > 0))
+        return VISO_ERR_ARG;
+    const int nbx = (p->width + p->bucket_width - 1) / p->bucket_width;
+    const int nby = (p->height + p->bucket_height - 1) / p->bucket_height;
+    if ((long long)nbx * nby > kMaxBuckets) return VISO_ERR_ARG;
+    if ((long long)nbx * nby * p->bucket_max > 64LL * kMaxChunks) return VISO_ERR_ARG;  // M bound
+    return VISO_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int viso_svo_default_params(viso_svo_params* p, int32_t width, int32_t height, double fx, double fy,
+                            double cu, double cv, double base) {
+    if (!p) return VISO_ERR_ARG;
+    std::memset(p, 0, sizeof(*p));
+    p->width = width;
+    p->height = height;
+    p->fx = fx;
+    p->fy = fy;
+    p->cu = cu;
+    p->cv = cv;
+    p->base = base;
+    p->nms_n = 5;
+    p->nms_tau = 700;
+    p->margin = 8;
+    p->disp_max = 255;
+    p->match_radius = 96;
+    p->bucket_width = 50;
+    p->bucket_height = 50;
+    p->bucket_max = 4;
+    p->ransac_iters = 200;
+    p->gn_iters = 20;
+    p->inlier_threshold = 2.0;
+    p->gn_eps = 1e-6;
+    p->seed = 0x5EED5EEDull;
+    p->max_features = 16384;
+    return VISO_OK;
+}
+
+int viso_svo_create(const viso_svo_params* p, int device, viso_svo** out) {
+    if (!out) return VISO_ERR_ARG;
+    *out = nullptr;
+    if (svo_check(p)) return VISO_ERR_ARG;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return VISO_ERR_NODEVICE;
+    VISO_HIP_CHECK(hipSetDevice(device));
+    viso_svo* s = new (std::nothrow) viso_svo();
+    if (!s) return VISO_ERR_ARG;
+    s->p = *p;
+    s->device = device;
+    if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess || s->init() != VISO_OK) {
+        s->release();
+        delete s;
+        return VISO_ERR_HIP;
+    }
+    *out = s;
+    return VISO_OK;
+}
+
+int viso_svo_destroy(viso_svo* s) {
+    if (!s) return VISO_ERR_ARG;
+    (void)hipSetDevice(s->device);
+    (void)hipStreamSynchronize(s->stream);
+    s->release();
+    delete s;
+    return VISO_OK;
+}
+
+int viso_svo_synchronize(viso_svo* s) {
+    if (!s) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipSetDevice(s->device));
+    VISO_HIP_CHECK(hipStreamSynchronize(s->stream));
+    return VISO_OK;
+}
+
+int viso_svo_process(viso_svo* s, const uint8_t* left, const uint8_t* right, const int32_t dims[3],
+                     int32_t* ok) {
+    if (!s || !left || !right || !dims) return VISO_ERR_ARG;
+    const int w = dims[0], h = dims[1], stride = dims[2];
+    if (w != s->p.width || h != s->p.height || stride < w) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipSetDevice(s->device));
+    uint8_t* dl = s->img;
+    uint8_t* dr = s->img + (size_t)w * h;
+    VISO_HIP_CHECK(hipMemcpy2DAsync(dl, w, left, stride, w, h, hipMemcpyHostToDevice, s->stream));
+    VISO_HIP_CHECK(hipMemcpy2DAsync(dr, w, right, stride, w, h, hipMemcpyHostToDevice, s->stream));
+    const uint8_t* ptrs[2] = {dl, dr};
+    VISO_HIP_CHECK(hipMemcpyAsync(s->imgs, ptrs, sizeof(ptrs), hipMemcpyHostToDevice, s->stream));
+    int rc = s->step(s->imgs);
+    if (rc) return rc;
+    VISO_HIP_CHECK(hipStreamSynchronize(s->stream));
+    if (ok) {
+        int st[8];
+        VISO_HIP_CHECK(hipMemcpy(st, s->stats, sizeof(st), hipMemcpyDeviceToHost));
+        *ok = st[5];
+    }
+    return VISO_OK;
+}
+
+int viso_svo_process_device(viso_svo* s, const uint8_t* left, const uint8_t* right, int32_t n,
+                            int64_t pair_stride, int32_t stride) {
+    if (!s || !left || !right || n < 0 || stride != s->p.width) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipSetDevice(s->device));
+    for (int i0 = 0; i0 < n; i0 += viso_svo::kMaxPairBatch) {
+        const int nb = std::min(n - i0, viso_svo::kMaxPairBatch);
+        std::vector<const uint8_t*> ptrs((size_t)2 * nb);
+        for (int i = 0; i < nb; ++i) {
+            ptrs[(size_t)2 * i] = left + (i0 + i) * pair_stride;
+            ptrs[(size_t)2 * i + 1] = right + (i0 + i) * pair_stride;
+        }
+        VISO_HIP_CHECK(hipMemcpyAsync(s->imgs, ptrs.data(), ptrs.size() * sizeof(void*),
+                                      hipMemcpyHostToDevice, s->stream));
+        for (int i = 0; i < nb; ++i) {
+            const int rc = s->step(s->imgs + 2 * i);
+            if (rc) return rc;
+        }
+        // the pointer table is reused by the next batch
+        VISO_HIP_CHECK(hipStreamSynchronize(s->stream));
+    }
+    return VISO_OK;
+}
+
+int viso_svo_get_motion(viso_svo* s, double* motion12) {
+    if (!s || !motion12) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipSetDevice(s->device));
+    VISO_HIP_CHECK(hipStreamSynchronize(s->stream));
+    if (s->frame < 2) {
+        for (int i = 0; i < 12; ++i) motion12[i] = (i % 4 == 0 && i < 9) ? 1.0 : 0.0;
+        return VISO_OK;
+    }
+    VISO_HIP_CHECK(hipMemcpy(motion12, s->motion, 12 * sizeof(double), hipMemcpyDeviceToHost));
+    return VISO_OK;
+}
+
+int viso_svo_get_stats(viso_svo* s, int32_t* stats6) {
+    if (!s || !stats6) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipSetDevice(s->device));
+    VISO_HIP_CHECK(hipStreamSynchronize(s->stream));
+    VISO_HIP_CHECK(hipMemcpy(stats6, s->stats, 6 * sizeof(int32_t), hipMemcpyDeviceToHost));
+    return VISO_OK;
+}
+
+int viso_svo_get_poses(viso_svo* s, double* poses12, size_t cap, size_t* n) {
+    if (!s || !n) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipSetDevice(s->device));
+    VISO_HIP_CHECK(hipStreamSynchronize(s->stream));
+    const size_t m = std::min(s->n_poses, s->max_poses);
+    *n = m;
+    if (poses12 && cap)
+        VISO_HIP_CHECK(hipMemcpy(poses12, s->pose_log, std::min(m, cap) * 12 * sizeof(double),
+                                 hipMemcpyDeviceToHost));
+    return VISO_OK;
+}
+
+int viso_svo_get_matches(viso_svo* s, int32_t* uv8, uint8_t* inlier, size_t cap, size_t* n) {
+    if (!s || !n) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipSetDevice(s->device));
+    VISO_HIP_CHECK(hipStreamSynchronize(s->stream));
+    int m = 0;
+    if (s->frame >= 2) VISO_HIP_CHECK(hipMemcpy(&m, s->n_sel, sizeof(int), hipMemcpyDeviceToHost));
+    *n = (size_t)m;
+    const size_t k = std::min((size_t)m, cap);
+    if (uv8 && k) VISO_HIP_CHECK(hipMemcpy(uv8, s->uv8, k * 8 * sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (inlier && k) VISO_HIP_CHECK(hipMemcpy(inlier, s->inl, k, hipMemcpyDeviceToHost));
+    return VISO_OK;
+}
+
+int viso_svo_features(viso_svo* s, const uint8_t* img, int32_t width, int32_t height, int32_t* u,
+                      int32_t* v, int32_t* cls, uint8_t* desc, int32_t cap, int32_t* n) {
+    if (!s || !img || !n || width != s->p.width || height != s->p.height) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipSetDevice(s->device));
+    const size_t bytes = (size_t)width * height;
+    VISO_HIP_CHECK(hipMemcpyAsync(s->img, img, bytes, hipMemcpyHostToDevice, s->stream));
+    VISO_HIP_CHECK(hipMemcpyAsync(s->img + bytes, img, bytes, hipMemcpyHostToDevice, s->stream));
+    const uint8_t* ptrs[2] = {s->img, s->img + bytes};
+    VISO_HIP_CHECK(hipMemcpyAsync(s->imgs, ptrs, sizeof(ptrs), hipMemcpyHostToDevice, s->stream));
+    int rc = s->detect(s->imgs);
+    if (rc) return rc;
+    VISO_HIP_CHECK(hipStreamSynchronize(s->stream));
+    const FeatDev& F = s->set[2 * s->cur];
+    int m = 0;
+    VISO_HIP_CHECK(hipMemcpy(&m, F.n, sizeof(int), hipMemcpyDeviceToHost));
+    *n = m;
+    const int k = std::min(m, cap);
+    if (k > 0) {
+        if (u) VISO_HIP_CHECK(hipMemcpy(u, F.u, k * sizeof(int), hipMemcpyDeviceToHost));
+        if (v) VISO_HIP_CHECK(hipMemcpy(v, F.v, k * sizeof(int), hipMemcpyDeviceToHost));
+        if (cls) VISO_HIP_CHECK(hipMemcpy(cls, F.c, k * sizeof(int), hipMemcpyDeviceToHost));
+        if (desc) VISO_HIP_CHECK(hipMemcpy(desc, F.d, (size_t)k * kDesc, hipMemcpyDeviceToHost));
+    }
+    return VISO_OK;
+}
+
+int viso_svo_match(viso_svo* s, const int32_t* const* u4, const int32_t* const* v4,
+                   const int32_t* const* cls4, const uint8_t* const* desc4, const int32_t n4[4],
+                   int32_t* quad, int32_t cap, int32_t* n) {
+    if (!s || !u4 || !v4 || !cls4 || !desc4 || !n4 || !n) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipSetDevice(s->device));
+    const int h = s->p.height;
+    // load the four sets into slots: prev = (cur^1), current = cur
+    const int slot[4] = {2 * (s->cur ^ 1), 2 * (s->cur ^ 1) + 1, 2 * s->cur, 2 * s->cur + 1};
+    for (int k = 0; k < 4; ++k) {
+        const int m = n4[k];
+        if (m < 0 || m > s->p.max_features) return VISO_ERR_ARG;
+        for (int i = 1; i < m; ++i)
+            if (v4[k][i] < v4[k][i - 1]) return VISO_ERR_ARG;  // row-major order required
+        FeatDev& F = s->set[slot[k]];
+        std::vector<int> row0((size_t)h + 1, m);
+        for (int i = m - 1; i >= 0; --i) {
+            if (v4[k][i] < 0 || v4[k][i] >= h) return VISO_ERR_ARG;
+            row0[(size_t)v4[k][i]] = i;
+        }
+        for (int y = h - 1; y >= 0; --y) row0[(size_t)y] = std::min(row0[(size_t)y], row0[(size_t)y + 1]);
+        if (m > 0) {
+            VISO_HIP_CHECK(hipMemcpy(F.u, u4[k], m * sizeof(int), hipMemcpyHostToDevice));
+            VISO_HIP_CHECK(hipMemcpy(F.v, v4[k], m * sizeof(int), hipMemcpyHostToDevice));
+            VISO_HIP_CHECK(hipMemcpy(F.c, cls4[k], m * sizeof(int), hipMemcpyHostToDevice));
+            VISO_HIP_CHECK(hipMemcpy(F.d, desc4[k], (size_t)m * kDesc, hipMemcpyHostToDevice));
+        }
+        VISO_HIP_CHECK(hipMemcpy(F.row0, row0.data(), row0.size() * sizeof(int), hipMemcpyHostToDevice));
+        VISO_HIP_CHECK(hipMemcpy(F.n, &m, sizeof(int), hipMemcpyHostToDevice));
+    }
+    const SvoDev d = s->dev();
+    FeatDev &L1 = s->set[slot[0]], &R1 = s->set[slot[1]], &L2 = s->set[slot[2]], &R2 = s->set[slot[3]];
+    svo_circle_kernel<<<1024, 256, 0, s->stream>>>(d, L1, R1, L2, R2, s->circ);
+    VISO_HIP_CHECK(hipGetLastError());
+    VISO_HIP_CHECK(hipStreamSynchronize(s->stream));
+    std::vector<int4> res((size_t)std::max(1, n4[2]));
+    if (n4[2] > 0)
+        VISO_HIP_CHECK(hipMemcpy(res.data(), s->circ, (size_t)n4[2] * sizeof(int4), hipMemcpyDeviceToHost));
+    int m = 0;
+    for (int i2 = 0; i2 < n4[2]; ++i2)
+        if (res[(size_t)i2].x >= 0) {
+            if (m < cap && quad) {
+                quad[4 * m + 0] = res[(size_t)i2].x;
+                quad[4 * m + 1] = res[(size_t)i2].y;
+                quad[4 * m + 2] = i2;
+                quad[4 * m + 3] = res[(size_t)i2].z;
+            }
+            ++m;
+        }
+    *n = m;
+    return VISO_OK;
+}
+
+int viso_svo_estimate(viso_svo* s, const int32_t* uv8, int32_t n, int64_t frame, double* motion12,
+                      uint8_t* inlier, int32_t* n_inliers) {
+    if (!s || (!uv8 && n > 0) || n < 0 || n > s->p.max_features || !motion12) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipSetDevice(s->device));
+    if (n > 0) VISO_HIP_CHECK(hipMemcpy(s->uv8, uv8, (size_t)n * 8 * sizeof(int), hipMemcpyHostToDevice));
+    VISO_HIP_CHECK(hipMemcpy(s->n_sel, &n, sizeof(int), hipMemcpyHostToDevice));
+    const SvoDev d = s->dev();
+    // scratch pose so the sequence state is untouched
+    double* pose_tmp = s->pose_log + 12 * (s->max_poses - 1);
+    const double I12[12] = {1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0};
+    VISO_HIP_CHECK(hipMemcpy(pose_tmp, I12, sizeof(I12), hipMemcpyHostToDevice));
+    const uint64_t seed = mix64(s->p.seed ^ (uint64_t)frame);
+    svo_ransac_kernel<<<(s->p.ransac_iters + 3) / 4, 256, 0, s->stream>>>(d, s->uv8, s->n_sel, seed, s->counts,
+                                                                         s->models);
+    svo_refine_kernel<<<1, 256, 0, s->stream>>>(d, s->uv8, s->n_sel, s->counts, s->models, s->sel, s->inl,
+                                                s->motion, pose_tmp, pose_tmp, s->stats);
+    VISO_HIP_CHECK(hipGetLastError());
+    VISO_HIP_CHECK(hipStreamSynchronize(s->stream));
+    VISO_HIP_CHECK(hipMemcpy(motion12, s->motion, 12 * sizeof(double), hipMemcpyDeviceToHost));
+    if (inlier && n > 0) VISO_HIP_CHECK(hipMemcpy(inlier, s->inl, n, hipMemcpyDeviceToHost));
+    int st[8];
+    VISO_HIP_CHECK(hipMemcpy(st, s->stats, sizeof(st), hipMemcpyDeviceToHost));
+    if (n_inliers) *n_inliers = st[5] ? st[4] : -1;
+    return VISO_OK;
+}
+
+}  // extern "C"
