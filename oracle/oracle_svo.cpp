@@ -218,36 +218,37 @@ void match_sums(const double e[4], const double J[4][6], double* s28) {
     s28[27] = ((e[0] * e[0] + e[1] * e[1]) + e[2] * e[2]) + e[3] * e[3];
 }
 
-// Gaussian elimination with partial pivoting (first largest |a|) on A x = g.
+// A x = g by LDL^T (A = J^T J is symmetric positive definite unless the
+// samples are degenerate): no pivoting, one division per column; fails if a
+// pivot D_j is not > 1e-12.  Every sum runs in ascending k.
 bool solve6(const double* S, double* x) {
-    double A[6][6], g[6];
+    double A[6][6], g[6], L[6][6] = {}, D[6], inv[6];
     int k = 0;
     for (int a = 0; a < 6; ++a)
         for (int b = a; b < 6; ++b, ++k) A[a][b] = A[b][a] = S[k];
     for (int a = 0; a < 6; ++a) g[a] = S[21 + a];
-    for (int c = 0; c < 6; ++c) {
-        int piv = c;
-        double best = std::fabs(A[c][c]);
-        for (int i = c + 1; i < 6; ++i)
-            if (std::fabs(A[i][c]) > best) {
-                best = std::fabs(A[i][c]);
-                piv = i;
-            }
-        if (!(best >= 1e-12)) return false;
-        if (piv != c) {
-            for (int j = 0; j < 6; ++j) std::swap(A[c][j], A[piv][j]);
-            std::swap(g[c], g[piv]);
-        }
-        for (int i = c + 1; i < 6; ++i) {
-            const double f = A[i][c] / A[c][c];
-            for (int j = c; j < 6; ++j) A[i][j] = A[i][j] - f * A[c][j];
-            g[i] = g[i] - f * g[c];
+    for (int j = 0; j < 6; ++j) {
+        double d = A[j][j];
+        for (int q = 0; q < j; ++q) d = d - (L[j][q] * L[j][q]) * D[q];
+        if (!(d > 1e-12)) return false;
+        D[j] = d;
+        inv[j] = 1.0 / d;
+        for (int i = j + 1; i < 6; ++i) {
+            double s = A[i][j];
+            for (int q = 0; q < j; ++q) s = s - (L[i][q] * L[j][q]) * D[q];
+            L[i][j] = s * inv[j];
         }
     }
-    for (int i = 5; i >= 0; --i) {
+    double z[6];
+    for (int i = 0; i < 6; ++i) {
         double s = g[i];
-        for (int j = i + 1; j < 6; ++j) s = s - A[i][j] * x[j];
-        x[i] = s / A[i][i];
+        for (int q = 0; q < i; ++q) s = s - L[i][q] * z[q];
+        z[i] = s;
+    }
+    for (int i = 5; i >= 0; --i) {
+        double s = z[i] * inv[i];
+        for (int q = i + 1; q < 6; ++q) s = s - L[q][i] * x[q];
+        x[i] = s;
     }
     return true;
 }

@@ -63,6 +63,23 @@ struct FeatDev {
 };
 
 // ---------------------------------------------------------------- detect
+// Strict NMS by separable maxima: for class map V (sign-adjusted response,
+// -inf outside the response domain) the largest neighbour of p is
+// max( max_{dy != 0} HI(y + dy, x), HE(y, x) ) with HI / HE the row maxima
+// over [x - n, x + n] including / excluding x itself: fixed cost per pixel,
+// no divergent early-exit loops.
+constexpr int kNegInf = -32768;
+
+template <bool BORDER>
+__device__ inline int class_val(const short (*M)[kTW + 2 * kMaxNms], int sg, int yy, int xx, int gy0,
+                                int gx0, int w, int h) {
+    if (BORDER) {
+        const int gy = gy0 + yy, gx = gx0 + xx;
+        if (gy < 2 || gy >= h - 2 || gx < 2 || gx >= w - 2) return kNegInf;
+    }
+    return sg * (int)M[yy][xx];
+}
+
 __global__ __launch_bounds__(256) void svo_detect_kernel(const uint8_t* const* imgs, SvoDev p,
                                                          FeatDev f0, FeatDev f1, int tiles) {
     constexpr int RW = kTW + 2 * kMaxNms, RH = kTH + 2 * kMaxNms;   // response region
@@ -70,6 +87,8 @@ __global__ __launch_bounds__(256) void svo_detect_kernel(const uint8_t* const* i
     __shared__ uint8_t s_img[IH][IW];
     __shared__ short s_b[RH][RW];
     __shared__ short s_c[RH][RW];
+    __shared__ short s_hi[RH][kTW];
+    __shared__ short s_he[RH][kTW];
     const uint8_t* __restrict__ img = imgs[blockIdx.z];
     const FeatDev F = blockIdx.z == 0 ? f0 : f1;  // by value: no kernarg address taken
     const int w = p.w, h = p.h, R = p.nms_n;
@@ -101,45 +120,58 @@ __global__ __launch_bounds__(256) void svo_detect_kernel(const uint8_t* const* i
         s_b[yy][xx] = (short)b;
         s_c[yy][xx] = (short)c;
     }
-    __syncthreads();
-    // NMS + ordered emission: wave k handles rows k, k+4, ...; lane l the
-    // columns 2l, 2l+1 of the tile
+    // tiles whose response region leaves the domain [2, w-3] x [2, h-3] mask it
+    const bool border = x0 - R < 2 || x0 + kTW + R > w - 2 || y0 - R < 2 || y0 + kTH + R > h - 2;
+    const int gy0 = y0 - R, gx0 = x0 - R;
     const int lane = tid & 63, wave = tid >> 6;
-    for (int ry = wave; ry < kTH; ry += 4) {
-        const int y = y0 + ry;
-        if (y >= h) break;
-        int flags = 0;  // bit 4*q + k: column 2l+q, class k
-        if (y >= p.margin && y < h - p.margin) {
+    int flags = 0;  // bit 8*s + 4*q + k: row slot s (row wave + 4s), column 2*lane + q, class k
 #pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const int x = x0 + 2 * lane + q;
-                if (x < p.margin || x >= w - p.margin || 2 * lane + q >= kTW) continue;
-                const int lx = 2 * lane + q + R, ly = ry + R;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    auto M = [&](int yy, int xx) { return k < 2 ? (int)s_b[yy][xx] : (int)s_c[yy][xx]; };
-                    const int sg = (k & 1) ? -1 : 1;
-                    const int r = sg * M(ly, lx);
-                    if (r <= p.tau) continue;
-                    bool mx = true;
-                    for (int dy = -R; dy <= R && mx; ++dy) {
-                        const int qy = y + dy;
-                        if (qy < 2 || qy >= h - 2) continue;
-                        for (int dx = -R; dx <= R; ++dx) {
-                            const int qx = x + dx;
-                            if ((dx == 0 && dy == 0) || qx < 2 || qx >= w - 2) continue;
-                            if (sg * M(ly + dy, lx + dx) >= r) {
-                                mx = false;
-                                break;
-                            }
-                        }
-                    }
-                    if (mx) flags |= 1 << (4 * q + k);
-                }
+    for (int k = 0; k < 4; ++k) {
+        const short(*M)[RW] = k < 2 ? s_b : s_c;
+        const int sg = (k & 1) ? -1 : 1;
+        __syncthreads();  // responses ready / previous class done with s_hi, s_he
+        // row maxima of the class map at the tile's output columns
+        for (int i = tid; i < rh * kTW; i += 256) {
+            const int yy = i / kTW, xo = i - yy * kTW, lx = xo + R;
+            int mx = kNegInf;
+            if (border) {
+                for (int d = 1; d <= R; ++d)
+                    mx = max(mx, max(class_val<true>(M, sg, yy, lx - d, gy0, gx0, w, h),
+                                     class_val<true>(M, sg, yy, lx + d, gy0, gx0, w, h)));
+                s_he[yy][xo] = (short)mx;
+                s_hi[yy][xo] = (short)max(mx, class_val<true>(M, sg, yy, lx, gy0, gx0, w, h));
+            } else {
+                for (int d = 1; d <= R; ++d)
+                    mx = max(mx, max(sg * (int)M[yy][lx - d], sg * (int)M[yy][lx + d]));
+                s_he[yy][xo] = (short)mx;
+                s_hi[yy][xo] = (short)max(mx, sg * (int)M[yy][lx]);
             }
         }
-        // ordered append: (x, class) ascending = lane order, then bit order
-        const int cnt = __popc(flags);
+        __syncthreads();
+#pragma unroll
+        for (int sl = 0; sl < kTH / 4; ++sl) {
+            const int ry = wave + 4 * sl, y = y0 + ry;
+            if (y < p.margin || y >= h - p.margin) continue;
+            const int yy = ry + R;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int xo = 2 * lane + q, x = x0 + xo;
+                if (x < p.margin || x >= w - p.margin) continue;
+                const int r = sg * (int)M[yy][xo + R];
+                if (r <= p.tau) continue;
+                int nb = s_he[yy][xo];
+                for (int d = 1; d <= R; ++d) nb = max(nb, max((int)s_hi[yy - d][xo], (int)s_hi[yy + d][xo]));
+                if (r > nb) flags |= 1 << (8 * sl + 4 * q + k);
+            }
+        }
+    }
+    // ordered emission: per row, (x, class) ascending = lane order, then bit order
+#pragma unroll
+    for (int sl = 0; sl < kTH / 4; ++sl) {
+        const int y = y0 + wave + 4 * sl;
+        if (y >= h) break;
+        const int fl = (flags >> (8 * sl)) & 0xff;
+        const int cnt = __popc(fl);
         int incl = cnt;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -150,7 +182,7 @@ __global__ __launch_bounds__(256) void svo_detect_kernel(const uint8_t* const* i
         int pos = incl - cnt;
         int* list = F.list + ((size_t)y * tiles + blockIdx.x) * kListCap;
         for (int b = 0; b < 8; ++b)
-            if (flags & (1 << b)) {
+            if (fl & (1 << b)) {
                 if (pos < kListCap) list[pos] = (x0 + 2 * lane + (b >> 2)) | ((b & 3) << 16);
                 ++pos;
             }
@@ -378,41 +410,51 @@ __device__ inline void match_leaf(const double* R, const double* t, const Obs& o
     match_sums(e, J, s);
 }
 
+// A x = g by LDL^T, no pivoting (oracle_svo.cpp solve6: same operations,
+// same order); fully unrolled, register-resident.
 __device__ inline bool solve6(const double* S, double* x) {
-    double A[6][6], g[6];
-    int k = 0;
-    for (int a = 0; a < 6; ++a)
-        for (int b = a; b < 6; ++b, ++k) A[a][b] = A[b][a] = S[k];
+    double A[6][6], g[6], L[6][6], D[6], inv[6];
+    {
+        int k = 0;
+#pragma unroll
+        for (int a = 0; a < 6; ++a)
+#pragma unroll
+            for (int b = a; b < 6; ++b, ++k) A[a][b] = A[b][a] = S[k];
+    }
+#pragma unroll
     for (int a = 0; a < 6; ++a) g[a] = S[21 + a];
-    for (int c = 0; c < 6; ++c) {
-        int piv = c;
-        double best = fabs(A[c][c]);
-        for (int i = c + 1; i < 6; ++i)
-            if (fabs(A[i][c]) > best) {
-                best = fabs(A[i][c]);
-                piv = i;
-            }
-        if (!(best >= 1e-12)) return false;
-        if (piv != c) {
-            for (int j = 0; j < 6; ++j) {
-                const double t = A[c][j];
-                A[c][j] = A[piv][j];
-                A[piv][j] = t;
-            }
-            const double t = g[c];
-            g[c] = g[piv];
-            g[piv] = t;
-        }
-        for (int i = c + 1; i < 6; ++i) {
-            const double f = A[i][c] / A[c][c];
-            for (int j = c; j < 6; ++j) A[i][j] = A[i][j] - f * A[c][j];
-            g[i] = g[i] - f * g[c];
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        double d = A[j][j];
+#pragma unroll
+        for (int q = 0; q < j; ++q) d = d - (L[j][q] * L[j][q]) * D[q];
+        ok = ok && d > 1e-12;
+        D[j] = d;
+        inv[j] = 1.0 / d;
+#pragma unroll
+        for (int i = j + 1; i < 6; ++i) {
+            double s = A[i][j];
+#pragma unroll
+            for (int q = 0; q < j; ++q) s = s - (L[i][q] * L[j][q]) * D[q];
+            L[i][j] = s * inv[j];
         }
     }
-    for (int i = 5; i >= 0; --i) {
+    if (!ok) return false;
+    double z[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
         double s = g[i];
-        for (int j = i + 1; j < 6; ++j) s = s - A[i][j] * x[j];
-        x[i] = s / A[i][i];
+#pragma unroll
+        for (int q = 0; q < i; ++q) s = s - L[i][q] * z[q];
+        z[i] = s;
+    }
+#pragma unroll
+    for (int i = 5; i >= 0; --i) {
+        double s = z[i] * inv[i];
+#pragma unroll
+        for (int q = i + 1; q < 6; ++q) s = s - L[q][i] * x[q];
+        x[i] = s;
     }
     return true;
 }
@@ -452,9 +494,23 @@ __device__ inline double shfl_xor_f64(double v, int m) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-// canonical pairwise tree of lanes [0, 2^levels) (ascending xor butterfly)
+// canonical pairwise tree over aligned groups of 2^levels lanes (every lane
+// of a group ends with the group's sum): the levels of wave_tree_sum_dpp
 __device__ inline double lane_tree(double v, int levels) {
-    for (int s = 0; s < levels; ++s) v = v + shfl_xor_f64(v, 1 << s);
+    if (levels >= 1) v = v + dpp_f64<0xB1>(v);   // xor 1
+    if (levels >= 2) v = v + dpp_f64<0x4E>(v);   // xor 2
+    if (levels >= 3) v = v + dpp_f64<0x141>(v);  // xor 4 (uniform quads)
+    if (levels >= 4) v = v + dpp_f64<0x140>(v);  // xor 8 (uniform octets)
+    if (levels >= 5) {
+        double a, b;
+        permlane16_swap_f64(v, v, a, b);
+        v = a + b;
+    }
+    if (levels >= 6) {
+        double a, b;
+        permlane32_swap_f64(v, v, a, b);
+        v = a + b;
+    }
     return v;
 }
 
@@ -638,7 +694,7 @@ __global__ __launch_bounds__(256) void svo_ransac_kernel(SvoDev p, const int* __
 // inlier flags, motion, pose update T_wc <- T_wc * Tr^-1, stats.
 constexpr int kMaxChunks = 128;  // 64-leaf chunks: M <= 8192 (bucket count x bucket_max)
 
-__global__ __launch_bounds__(256) void svo_refine_kernel(SvoDev p, const int* __restrict__ uv8,
+__global__ __launch_bounds__(1024) void svo_refine_kernel(SvoDev p, const int* __restrict__ uv8,
                                                          const int* __restrict__ n_sel,
                                                          const int* __restrict__ counts,
                                                          const double* __restrict__ models,
@@ -669,7 +725,7 @@ __global__ __launch_bounds__(256) void svo_refine_kernel(SvoDev p, const int* __
         double R[9], t[3];
         for (int i = 0; i < 9; ++i) R[i] = s_st[i];
         for (int i = 0; i < 3; ++i) t[i] = s_st[9 + i];
-        for (int m = tid; m < M; m += 256) sel[m] = is_inlier(R, t, make_obs(uv8 + 8 * (size_t)m, p), p) ? 1 : 0;
+        for (int m = tid; m < M; m += 1024) sel[m] = is_inlier(R, t, make_obs(uv8 + 8 * (size_t)m, p), p) ? 1 : 0;
         __syncthreads();
         int P2 = 1;
         while (P2 < M) P2 <<= 1;
@@ -680,7 +736,7 @@ __global__ __launch_bounds__(256) void svo_refine_kernel(SvoDev p, const int* __
         for (int it = 0; it < p.gn_iters; ++it) {
             for (int i = 0; i < 9; ++i) R[i] = s_st[i];
             for (int i = 0; i < 3; ++i) t[i] = s_st[9 + i];
-            for (int ch = wave; ch < nch; ch += 4) {
+            for (int ch = wave; ch < nch; ch += 16) {
                 const int m = ch * 64 + lane;
                 double s[28];
                 if (m < M) match_leaf(R, t, make_obs(uv8 + 8 * (size_t)m, p), p, sel[m] != 0, s);
@@ -737,7 +793,7 @@ __global__ __launch_bounds__(256) void svo_refine_kernel(SvoDev p, const int* __
         for (int i = 0; i < 9; ++i) R[i] = s_st[i];
         for (int i = 0; i < 3; ++i) t[i] = s_st[9 + i];
         int c = 0;
-        for (int m = tid; m < M; m += 256) {
+        for (int m = tid; m < M; m += 1024) {
             const bool in = is_inlier(R, t, make_obs(uv8 + 8 * (size_t)m, p), p);
             inl[m] = in ? 1 : 0;
             c += in ? 1 : 0;
@@ -745,7 +801,7 @@ __global__ __launch_bounds__(256) void svo_refine_kernel(SvoDev p, const int* __
         atomicAdd(&s_cnt, c);
         __syncthreads();
     } else {
-        for (int m = tid; m < M; m += 256) inl[m] = 0;
+        for (int m = tid; m < M; m += 1024) inl[m] = 0;
     }
     __syncthreads();
     if (tid == 0) {
@@ -899,7 +955,7 @@ struct viso_svo {
         svo_select_kernel<<<1, 256, 0, stream>>>(d, L1, R1, L2, R2, circ, all_idx, uv8, n_sel, stats);
         const uint64_t seed = mix64(p.seed ^ (uint64_t)frame);
         svo_ransac_kernel<<<(p.ransac_iters + 3) / 4, 256, 0, stream>>>(d, uv8, n_sel, seed, counts, models);
-        svo_refine_kernel<<<1, 256, 0, stream>>>(d, uv8, n_sel, counts, models, sel, inl, motion, pose,
+        svo_refine_kernel<<<1, 1024, 0, stream>>>(d, uv8, n_sel, counts, models, sel, inl, motion, pose,
                                                  pose_log + 12 * std::min(n_poses, max_poses - 1), stats);
         VISO_HIP_CHECK(hipGetLastError());
         return VISO_OK;
@@ -1187,7 +1243,7 @@ int viso_svo_estimate(viso_svo* s, const int32_t* uv8, int32_t n, int64_t frame,
     const uint64_t seed = mix64(s->p.seed ^ (uint64_t)frame);
     svo_ransac_kernel<<<(s->p.ransac_iters + 3) / 4, 256, 0, s->stream>>>(d, s->uv8, s->n_sel, seed, s->counts,
                                                                          s->models);
-    svo_refine_kernel<<<1, 256, 0, s->stream>>>(d, s->uv8, s->n_sel, s->counts, s->models, s->sel, s->inl,
+    svo_refine_kernel<<<1, 1024, 0, s->stream>>>(d, s->uv8, s->n_sel, s->counts, s->models, s->sel, s->inl,
                                                 s->motion, pose_tmp, pose_tmp, s->stats);
     VISO_HIP_CHECK(hipGetLastError());
     VISO_HIP_CHECK(hipStreamSynchronize(s->stream));
