@@ -84,6 +84,7 @@ SIGNATURES = {
     "viso_svo_process": [_vp, _vp, _vp, _vp, _vp],
     "viso_svo_process_device": [_vp, _vp, _vp, _i32, ctypes.c_int64, _i32],
     "viso_svo_synchronize": [_vp],
+    "viso_svo_timing": [_vp, _i32, _vp, _vp],
     "viso_svo_get_motion": [_vp, _vp],
     "viso_svo_get_stats": [_vp, _vp],
     "viso_svo_get_poses": [_vp, _vp, _sz, _vp],

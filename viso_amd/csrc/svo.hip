@@ -13,8 +13,9 @@
 //   svo_circle_kernel    wave per current-left feature: four best-SAD
 //                        searches (v_sad_u8, wave argmin on (sad, index))
 //                        left_t -> right_t -> right_t-1 -> left_t-1 -> left_t
-//   svo_select_kernel    one workgroup: compaction in left order, bucketing
-//                        (rank within bucket), 3-D points of the matches
+//   svo_bucket_kernel    wave per bucket: first bucket_max matches of the
+//                        bucket in left order (ballot ranks)
+//   svo_select_kernel    one workgroup: compaction of the kept matches
 //   svo_ransac_kernel    wave per hypothesis: 3-point Gauss-Newton (lane per
 //                        match), inlier count by ballot over all matches
 //   svo_refine_kernel    one workgroup: best hypothesis, Gauss-Newton over
@@ -80,8 +81,15 @@ __device__ inline int class_val(const short (*M)[kTW + 2 * kMaxNms], int sg, int
     return sg * (int)M[yy][xx];
 }
 
+// image z of a batch = pair z / 2 (left, right); its feature set lives in the
+// ring slot of that pair
+__device__ inline FeatDev set_of(const FeatDev* sets, int ring, int pair0, int z) {
+    return sets[2 * ((pair0 + z / 2) % ring) + (z & 1)];
+}
+
 __global__ __launch_bounds__(256) void svo_detect_kernel(const uint8_t* const* imgs, SvoDev p,
-                                                         FeatDev f0, FeatDev f1, int tiles) {
+                                                         const FeatDev* __restrict__ sets, int ring,
+                                                         int pair0, int tiles, int list_cap) {
     constexpr int RW = kTW + 2 * kMaxNms, RH = kTH + 2 * kMaxNms;   // response region
     constexpr int IW = RW + 4, IH = RH + 4;                         // image region
     __shared__ uint8_t s_img[IH][IW];
@@ -90,7 +98,7 @@ __global__ __launch_bounds__(256) void svo_detect_kernel(const uint8_t* const* i
     __shared__ short s_hi[RH][kTW];
     __shared__ short s_he[RH][kTW];
     const uint8_t* __restrict__ img = imgs[blockIdx.z];
-    const FeatDev F = blockIdx.z == 0 ? f0 : f1;  // by value: no kernarg address taken
+    const FeatDev F = set_of(sets, ring, pair0, blockIdx.z);
     const int w = p.w, h = p.h, R = p.nms_n;
     const int x0 = blockIdx.x * kTW, y0 = blockIdx.y * kTH;
     const int tid = threadIdx.x;
@@ -180,19 +188,20 @@ __global__ __launch_bounds__(256) void svo_detect_kernel(const uint8_t* const* i
         }
         const int total = __shfl(incl, 63, 64);
         int pos = incl - cnt;
-        int* list = F.list + ((size_t)y * tiles + blockIdx.x) * kListCap;
+        int* list = F.list + ((size_t)y * tiles + blockIdx.x) * list_cap;
         for (int b = 0; b < 8; ++b)
             if (fl & (1 << b)) {
-                if (pos < kListCap) list[pos] = (x0 + 2 * lane + (b >> 2)) | ((b & 3) << 16);
+                if (pos < list_cap) list[pos] = (x0 + 2 * lane + (b >> 2)) | ((b & 3) << 16);
                 ++pos;
             }
-        if (lane == 0) F.cnt[(size_t)y * tiles + blockIdx.x] = min(total, kListCap);
+        if (lane == 0) F.cnt[(size_t)y * tiles + blockIdx.x] = min(total, list_cap);
     }
 }
 
 // row-major exclusive prefix over the (row, tile) candidate counts
-__global__ __launch_bounds__(1024) void svo_scan_kernel(SvoDev p, FeatDev f0, FeatDev f1, int tiles) {
-    const FeatDev F = blockIdx.x == 0 ? f0 : f1;
+__global__ __launch_bounds__(1024) void svo_scan_kernel(SvoDev p, const FeatDev* __restrict__ sets, int ring,
+                                                        int pair0, int tiles) {
+    const FeatDev F = set_of(sets, ring, pair0, blockIdx.x);
     __shared__ int s_part[1024];
     const int n = p.h * tiles;
     const int tid = threadIdx.x;
@@ -229,9 +238,10 @@ __device__ inline int sobel_q(const uint8_t* I, int w, int x, int y, bool du) {
 
 // 16 lanes per feature (lane j: sample offset j): descriptor + SoA arrays
 __global__ __launch_bounds__(256) void svo_describe_kernel(const uint8_t* const* imgs, SvoDev p,
-                                                           FeatDev f0, FeatDev f1, int tiles) {
+                                                           const FeatDev* __restrict__ sets, int ring,
+                                                           int pair0, int tiles, int list_cap) {
     const uint8_t* __restrict__ img = imgs[blockIdx.z];
-    const FeatDev F = blockIdx.z == 0 ? f0 : f1;
+    const FeatDev F = set_of(sets, ring, pair0, blockIdx.z);
     const int y0 = blockIdx.y * kTH;
     const int j = threadIdx.x & 15, slot = threadIdx.x >> 4;  // 16 features per pass
     for (int ry = 0; ry < kTH; ++ry) {
@@ -242,7 +252,7 @@ __global__ __launch_bounds__(256) void svo_describe_kernel(const uint8_t* const*
         for (int i = slot; i < cnt; i += 16) {
             const int o = base + i;
             if (o >= p.cap) break;
-            const int e = F.list[rt * kListCap + i];
+            const int e = F.list[rt * list_cap + i];
             const int x = e & 0xffff, k = e >> 16;
             const int sx = x + c_p16[j][0], sy = y + c_p16[j][1];
             F.d[(size_t)o * kDesc + j] = (uint8_t)sobel_q(img, p.w, sx, sy, true);
@@ -296,9 +306,11 @@ __device__ int best_match(const FeatDev& S, int h, int u, int v, int c, uint4 q0
     return best == 0xffffffffu ? -1 : (int)(best & 0x7fffu);
 }
 
-// wave per current-left feature; out[i2] = {l1, r1, r2} or l1 = -1
+// wave per current-left feature; rec[i2] = {l1, r1, r2, -} and
+// rec8[i2] = {u_l1, v_l1, u_r1, v_r1, u_l2, v_l2, u_r2, v_r2}, or rec[i2].x = -1
 __global__ __launch_bounds__(256) void svo_circle_kernel(SvoDev p, FeatDev L1, FeatDev R1, FeatDev L2,
-                                                         FeatDev R2, int4* __restrict__ out) {
+                                                         FeatDev R2, int4* __restrict__ out,
+                                                         int4* __restrict__ rec8, uint8_t* __restrict__ keep) {
     const int n2 = *L2.n;
     const int D = p.disp_max, Rr = p.radius, h = p.h;
     auto desc = [](const FeatDev& S, int i, uint4& a, uint4& b) {
@@ -326,7 +338,16 @@ __global__ __launch_bounds__(256) void svo_circle_kernel(SvoDev p, FeatDev L1, F
                 }
             }
         }
-        if ((threadIdx.x & 63) == 0) out[i2] = res;
+        const int lane = threadIdx.x & 63;
+        if (lane == 0) out[i2] = res;
+        if (lane == 2) keep[i2] = 0;
+        if (lane == 1) {
+            const bool m = res.x >= 0;
+            rec8[2 * (size_t)i2] = m ? make_int4(L1.u[res.x], L1.v[res.x], R1.u[res.y], R1.v[res.y])
+                                     : make_int4(-1, 0, 0, 0);
+            rec8[2 * (size_t)i2 + 1] = m ? make_int4(L2.u[i2], L2.v[i2], R2.u[res.z], R2.v[res.z])
+                                         : make_int4(0, 0, 0, 0);
+        }
     }
 }
 
@@ -515,93 +536,96 @@ __device__ inline double lane_tree(double v, int levels) {
 }
 
 // ---------------------------------------------------------------- selection
-// One workgroup: (1) compact circular matches in left order, (2) bucketing
-// rank (matches before it in its bucket), (3) compact the kept matches ->
-// uv8 + points; stats[2] = circular matches, stats[3] = bucketed.
+// ---- selection: bucketing (wave per bucket) and compaction
+// exclusive block prefix (1024 threads): wave scans by shuffles + wave totals
+__device__ inline int block_excl_scan(int v, int* s_w, int& total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    int base = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int t = s_w[k];
+        base += k < wave ? t : 0;
+        tot += t;
+    }
+    __syncthreads();
+    total = tot;
+    return base + incl - v;
+}
+
 constexpr int kMaxBuckets = 4096;
 
-__global__ __launch_bounds__(256) void svo_select_kernel(SvoDev p, FeatDev L1, FeatDev R1, FeatDev L2,
-                                                         FeatDev R2, const int4* __restrict__ circ,
-                                                         int* __restrict__ all_idx,
-                                                         int* __restrict__ uv8, int* __restrict__ n_sel,
-                                                         int* __restrict__ stats) {
-    __shared__ int s_cnt[kMaxBuckets];
-    __shared__ int s_scan[256];
-    __shared__ int s_bkt[256];
-    __shared__ int s_base;
+// Bucketing: wave per bucket.  The bucket's candidates are the current-left
+// features of its band of rows (a contiguous index range, features being
+// row-major); lanes test 64 at a time (circular match present, column in the
+// bucket), a ballot ranks them in index order, the first bucket_max are kept.
+__global__ __launch_bounds__(256) void svo_bucket_kernel(SvoDev p, const FeatDev L2,
+                                                         const int4* __restrict__ rec8,
+                                                         uint8_t* __restrict__ keep) {
+    const int lane = threadIdx.x & 63;
+    const int nbx = (p.w + p.bw - 1) / p.bw, nby = (p.h + p.bh - 1) / p.bh;
+    const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= nbx * nby) return;
+    const int br = b / nbx, bc = b - br * nbx;
+    const int i0 = L2.row0[br * p.bh], i1 = L2.row0[min((br + 1) * p.bh, p.h)];
+    int kept = 0;
+    for (int j0 = i0; j0 < i1 && kept < p.bmax; j0 += 64) {
+        const int j = j0 + lane;
+        bool mem = false;
+        if (j < i1) {
+            const int4 a = rec8[2 * (size_t)j];
+            mem = a.x >= 0 && L2.u[j] / p.bw == bc;
+        }
+        const unsigned long long bal = __ballot(mem);
+        const int rank = kept + __popcll(bal & ((1ull << lane) - 1ull));
+        if (mem && rank < p.bmax) keep[j] = 1;
+        kept += __popcll(bal);
+    }
+}
+
+// Compaction of the kept matches in left order -> uv8; stats[2] = circular
+// matches, stats[3] = bucketed.
+__global__ __launch_bounds__(1024) void svo_select_kernel(SvoDev p, const FeatDev L2,
+                                                          const int4* __restrict__ rec8,
+                                                          const uint8_t* __restrict__ keep,
+                                                          int* __restrict__ uv8, int* __restrict__ n_sel,
+                                                          int* __restrict__ stats) {
+    __shared__ int s_w[16];
     const int tid = threadIdx.x;
     const int n2 = *L2.n;
-    const int nbx = (p.w + p.bw - 1) / p.bw, nby = (p.h + p.bh - 1) / p.bh;
-    for (int i = tid; i < nbx * nby; i += 256) s_cnt[i] = 0;
-    if (tid == 0) s_base = 0;
-    __syncthreads();
-    // (1) compaction of circ[i2].x >= 0 in i2 order
-    for (int c0 = 0; c0 < n2; c0 += 256) {
+    int base = 0, m_all = 0;
+    for (int c0 = 0; c0 < n2; c0 += 1024) {
         const int i2 = c0 + tid;
-        const int f = (i2 < n2 && circ[i2].x >= 0) ? 1 : 0;
-        s_scan[tid] = f;
-        __syncthreads();
-        for (int o = 1; o < 256; o <<= 1) {
-            const int t = tid >= o ? s_scan[tid - o] : 0;
-            __syncthreads();
-            s_scan[tid] += t;
-            __syncthreads();
+        int4 a = make_int4(-1, 0, 0, 0), bq = make_int4(0, 0, 0, 0);
+        int k = 0;
+        if (i2 < n2) {
+            a = rec8[2 * (size_t)i2];
+            bq = rec8[2 * (size_t)i2 + 1];
+            k = keep[i2];
         }
-        if (f) all_idx[s_base + s_scan[tid] - 1] = i2;
-        __syncthreads();
-        if (tid == 255) s_base += s_scan[255];
-        __syncthreads();
-    }
-    const int m_all = s_base;
-    __syncthreads();
-    if (tid == 0) s_base = 0;
-    __syncthreads();
-    // (2)+(3) bucketing in match order
-    for (int c0 = 0; c0 < m_all; c0 += 256) {
-        const int m = c0 + tid;
-        int b = -1;
-        if (m < m_all) {
-            const int i2 = all_idx[m];
-            b = (L2.v[i2] / p.bh) * nbx + L2.u[i2] / p.bw;
+        const int f = a.x >= 0 ? 1 : 0;
+        int tot, totf;
+        block_excl_scan(f, s_w, totf);
+        const int o = block_excl_scan(k, s_w, tot);
+        if (k) {
+            int4* r = reinterpret_cast<int4*>(uv8 + 8 * (size_t)(base + o));
+            r[0] = a;
+            r[1] = bq;
         }
-        s_bkt[tid] = b;
-        __syncthreads();
-        int before = 0;
-        if (b >= 0)
-            for (int t = 0; t < tid; ++t) before += s_bkt[t] == b ? 1 : 0;
-        const int keep = (b >= 0 && s_cnt[b] + before < p.bmax) ? 1 : 0;
-        __syncthreads();
-        if (b >= 0) atomicAdd(&s_cnt[b], 1);
-        s_scan[tid] = keep;
-        __syncthreads();
-        for (int o = 1; o < 256; o <<= 1) {
-            const int t = tid >= o ? s_scan[tid - o] : 0;
-            __syncthreads();
-            s_scan[tid] += t;
-            __syncthreads();
-        }
-        if (keep) {
-            const int o = s_base + s_scan[tid] - 1;
-            const int i2 = all_idx[m];
-            const int4 q = circ[i2];
-            int* r = uv8 + 8 * (size_t)o;
-            r[0] = L1.u[q.x];
-            r[1] = L1.v[q.x];
-            r[2] = R1.u[q.y];
-            r[3] = R1.v[q.y];
-            r[4] = L2.u[i2];
-            r[5] = L2.v[i2];
-            r[6] = R2.u[q.z];
-            r[7] = R2.v[q.z];
-        }
-        __syncthreads();
-        if (tid == 255) s_base += s_scan[255];
-        __syncthreads();
+        base += tot;
+        m_all += totf;
     }
     if (tid == 0) {
-        *n_sel = s_base;
+        *n_sel = base;
         stats[2] = m_all;
-        stats[3] = s_base;
+        stats[3] = base;
     }
 }
 
@@ -706,16 +730,24 @@ __global__ __launch_bounds__(1024) void svo_refine_kernel(SvoDev p, const int* _
     __shared__ int s_best, s_ok, s_conv, s_cnt;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int M = *n_sel;
-    if (tid == 0) {
-        int bh = -1, bc = -1;
-        for (int h = 0; h < p.iters; ++h)
-            if (counts[h] > bc) {
-                bc = counts[h];
-                bh = h;
-            }
-        s_best = (M >= 6 && bc >= 6) ? bh : -1;
-        s_ok = s_best >= 0 ? 1 : 0;
-        s_cnt = 0;
+    if (wave == 0) {
+        // argmax (max count, lowest hypothesis) as a wave min of
+        // (-count, h) packed into 64 bits
+        unsigned long long key = ~0ull;
+        for (int h = lane; h < p.iters; h += 64)
+            key = min(key, ((unsigned long long)(0x7fffffff - counts[h]) << 32) | (unsigned)h);
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned long long t = ((unsigned long long)(unsigned)__shfl_xor((int)(key >> 32), o, 64) << 32) |
+                                         (unsigned)__shfl_xor((int)(key & 0xffffffffu), o, 64);
+            key = min(key, t);
+        }
+        if (lane == 0) {
+            const int bc = 0x7fffffff - (int)(key >> 32), bh = (int)(key & 0xffffffffu);
+            s_best = (M >= 6 && bc >= 6) ? bh : -1;
+            s_ok = s_best >= 0 ? 1 : 0;
+            s_cnt = 0;
+        }
     }
     __syncthreads();
     const int best = s_best;
@@ -847,19 +879,21 @@ __global__ void svo_stats_kernel(FeatDev a, FeatDev b, int* stats, double* pose,
 using namespace viso;
 
 struct viso_svo {
+    static constexpr int kMaxPairBatch = 64;   // pairs whose features are extracted in one launch
+    static constexpr int kRing = kMaxPairBatch + 1;  // feature-set ring (pairs): a batch + the previous pair
     viso_svo_params p{};
     int device = 0;
     hipStream_t stream = nullptr;
     int tiles = 0;
-    size_t frame = 0;       // pairs processed
-    int have_prev = 0;
-    // feature sets: 4 slots (ping-pong pairs)
-    FeatDev set[4]{};
-    int cur = 0;            // slot pair of the current frame: sets 2*cur, 2*cur + 1
+    int list_cap = 0;
+    size_t frame = 0;       // pairs processed; pair k uses ring slot k % kRing
+    std::vector<FeatDev> sets;        // 2 * kRing (left, right of each slot)
+    FeatDev* d_sets = nullptr;
     std::vector<void*> allocs;
-    uint8_t* img = nullptr;       // host-path upload buffer (left, right)
+    uint8_t* img = nullptr;           // host-path upload buffer (left, right)
     int4* circ = nullptr;
-    int* all_idx = nullptr;
+    int4* rec8 = nullptr;
+    uint8_t* keep = nullptr;
     int* uv8 = nullptr;
     int* n_sel = nullptr;
     int* counts = nullptr;
@@ -868,11 +902,14 @@ struct viso_svo {
     uint8_t* inl = nullptr;
     double* motion = nullptr;
     double* pose = nullptr;
-    double* pose_log = nullptr;   // [max_poses][12]
+    double* pose_log = nullptr;       // [max_poses][12]
     int* stats = nullptr;
     size_t max_poses = 0;
-    size_t n_poses = 0;
-    const uint8_t** imgs = nullptr;  // device array of 2 image pointers
+    const uint8_t** imgs = nullptr;   // device table of 2 * kMaxPairBatch image pointers
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    double detect_ms = 0.0;           // timing of the last batched feature pass (if timed)
+    int detect_pairs = 0;
+    bool timed = false;
 
     SvoDev dev() const {
         SvoDev d;
@@ -911,70 +948,80 @@ struct viso_svo {
     int init() {
         const int w = p.width, h = p.height, cap = p.max_features;
         tiles = (w + kTW - 1) / kTW;
-        for (int k = 0; k < 4; ++k) {
-            FeatDev& f = set[k];
+        // strict NMS of radius n: same-class maxima of a row are > n apart
+        list_cap = std::min(kListCap, 4 * ((kTW + p.nms_n) / (p.nms_n + 1)));
+        sets.assign(2 * kRing, FeatDev{});
+        for (FeatDev& f : sets)
             if (alloc(f.u, cap) || alloc(f.v, cap) || alloc(f.c, cap) || alloc(f.d, (size_t)cap * kDesc) ||
                 alloc(f.row0, (size_t)h + 1) || alloc(f.n, 1) || alloc(f.cnt, (size_t)h * tiles) ||
-                alloc(f.list, (size_t)h * tiles * kListCap) || alloc(f.off, (size_t)h * tiles))
+                alloc(f.list, (size_t)h * tiles * list_cap) || alloc(f.off, (size_t)h * tiles))
                 return VISO_ERR_HIP;
-        }
         max_poses = 65536;
-        if (alloc(img, 2 * (size_t)w * h) || alloc(circ, cap) || alloc(all_idx, cap) ||
-            alloc(uv8, (size_t)cap * 8) || alloc(n_sel, 1) || alloc(counts, std::max(1, p.ransac_iters)) ||
+        if (alloc(d_sets, sets.size()) || alloc(img, 2 * (size_t)w * h) || alloc(circ, cap) ||
+            alloc(rec8, 2 * (size_t)cap) || alloc(keep, cap) || alloc(uv8, (size_t)cap * 8) || alloc(n_sel, 1) ||
+            alloc(counts, std::max(1, p.ransac_iters)) ||
             alloc(models, (size_t)std::max(1, p.ransac_iters) * 12) || alloc(sel, cap) || alloc(inl, cap) ||
             alloc(motion, 12) || alloc(pose, 12) || alloc(pose_log, max_poses * 12) || alloc(stats, 8) ||
             alloc(imgs, 2 * kMaxPairBatch))
             return VISO_ERR_HIP;
+        VISO_HIP_CHECK(hipMemcpy(d_sets, sets.data(), sets.size() * sizeof(FeatDev), hipMemcpyHostToDevice));
+        VISO_HIP_CHECK(hipEventCreate(&ev[0]));
+        VISO_HIP_CHECK(hipEventCreate(&ev[1]));
         return VISO_OK;
     }
-    static constexpr int kMaxPairBatch = 256;
     void release() {
         for (void* q : allocs) (void)hipFree(q);
         allocs.clear();
+        for (hipEvent_t& e : ev)
+            if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
         stream = nullptr;
     }
+    FeatDev& set_at(size_t pair, int side) { return sets[2 * (pair % kRing) + side]; }
 
-    // features of the pair at device pointers (l, r) into the current slots
-    int detect(const uint8_t* const* pair_ptrs_dev) {
+    // features of pairs frame .. frame + nb - 1 (image pointers in imgs[0 .. 2 nb))
+    int detect(int nb) {
         const SvoDev d = dev();
-        FeatDev& A = set[2 * cur];
-        FeatDev& B = set[2 * cur + 1];
-        const dim3 g(tiles, (p.height + kTH - 1) / kTH, 2);
-        svo_detect_kernel<<<g, 256, 0, stream>>>(pair_ptrs_dev, d, A, B, tiles);
-        svo_scan_kernel<<<2, 1024, 0, stream>>>(d, A, B, tiles);
-        svo_describe_kernel<<<g, 256, 0, stream>>>(pair_ptrs_dev, d, A, B, tiles);
+        const int pair0 = (int)(frame % kRing);
+        const dim3 g(tiles, (p.height + kTH - 1) / kTH, 2 * nb);
+        if (timed) VISO_HIP_CHECK(hipEventRecord(ev[0], stream));
+        svo_detect_kernel<<<g, 256, 0, stream>>>(imgs, d, d_sets, kRing, pair0, tiles, list_cap);
+        svo_scan_kernel<<<2 * nb, 1024, 0, stream>>>(d, d_sets, kRing, pair0, tiles);
+        svo_describe_kernel<<<g, 256, 0, stream>>>(imgs, d, d_sets, kRing, pair0, tiles, list_cap);
+        if (timed) VISO_HIP_CHECK(hipEventRecord(ev[1], stream));
         VISO_HIP_CHECK(hipGetLastError());
         return VISO_OK;
     }
+    // matching + motion of pair `frame` against pair `frame - 1`
     int match_and_estimate() {
         const SvoDev d = dev();
-        FeatDev &L1 = set[2 * (cur ^ 1)], &R1 = set[2 * (cur ^ 1) + 1], &L2 = set[2 * cur],
-                &R2 = set[2 * cur + 1];
-        svo_circle_kernel<<<1024, 256, 0, stream>>>(d, L1, R1, L2, R2, circ);
-        svo_select_kernel<<<1, 256, 0, stream>>>(d, L1, R1, L2, R2, circ, all_idx, uv8, n_sel, stats);
+        const FeatDev L1 = set_at(frame - 1, 0), R1 = set_at(frame - 1, 1), L2 = set_at(frame, 0),
+                      R2 = set_at(frame, 1);
+        svo_circle_kernel<<<1024, 256, 0, stream>>>(d, L1, R1, L2, R2, circ, rec8, keep);
+        const int nbk = ((p.width + p.bucket_width - 1) / p.bucket_width) *
+                        ((p.height + p.bucket_height - 1) / p.bucket_height);
+        svo_bucket_kernel<<<(nbk + 3) / 4, 256, 0, stream>>>(d, L2, rec8, keep);
+        svo_select_kernel<<<1, 1024, 0, stream>>>(d, L2, rec8, keep, uv8, n_sel, stats);
         const uint64_t seed = mix64(p.seed ^ (uint64_t)frame);
         svo_ransac_kernel<<<(p.ransac_iters + 3) / 4, 256, 0, stream>>>(d, uv8, n_sel, seed, counts, models);
         svo_refine_kernel<<<1, 1024, 0, stream>>>(d, uv8, n_sel, counts, models, sel, inl, motion, pose,
-                                                 pose_log + 12 * std::min(n_poses, max_poses - 1), stats);
+                                                  pose_log + 12 * std::min(frame, max_poses - 1), stats);
         VISO_HIP_CHECK(hipGetLastError());
         return VISO_OK;
     }
-    // one pair at device pointers
-    int step(const uint8_t* const* pair_ptrs_dev) {
-        int rc = detect(pair_ptrs_dev);
-        if (rc) return rc;
-        FeatDev &A = set[2 * cur], &B = set[2 * cur + 1];
-        svo_stats_kernel<<<1, 1, 0, stream>>>(A, B, stats, pose, pose_log + 12 * std::min(n_poses, max_poses - 1),
-                                              have_prev ? 0 : 1);
-        if (have_prev) {
-            rc = match_and_estimate();
-            if (rc) return rc;
+    // the per-pair chain of the pairs whose features were just extracted
+    int steps(int nb) {
+        for (int i = 0; i < nb; ++i) {
+            const FeatDev A = set_at(frame, 0), B = set_at(frame, 1);
+            svo_stats_kernel<<<1, 1, 0, stream>>>(A, B, stats, pose,
+                                                  pose_log + 12 * std::min(frame, max_poses - 1),
+                                                  frame == 0 ? 1 : 0);
+            if (frame > 0) {
+                const int rc = match_and_estimate();
+                if (rc) return rc;
+            }
+            ++frame;
         }
-        have_prev = 1;
-        ++frame;
-        ++n_poses;
-        cur ^= 1;
         return VISO_OK;
     }
 };
@@ -1072,7 +1119,8 @@ int viso_svo_process(viso_svo* s, const uint8_t* left, const uint8_t* right, con
     VISO_HIP_CHECK(hipMemcpy2DAsync(dr, w, right, stride, w, h, hipMemcpyHostToDevice, s->stream));
     const uint8_t* ptrs[2] = {dl, dr};
     VISO_HIP_CHECK(hipMemcpyAsync(s->imgs, ptrs, sizeof(ptrs), hipMemcpyHostToDevice, s->stream));
-    int rc = s->step(s->imgs);
+    int rc = s->detect(1);
+    if (!rc) rc = s->steps(1);
     if (rc) return rc;
     VISO_HIP_CHECK(hipStreamSynchronize(s->stream));
     if (ok) {
@@ -1096,13 +1144,28 @@ int viso_svo_process_device(viso_svo* s, const uint8_t* left, const uint8_t* rig
         }
         VISO_HIP_CHECK(hipMemcpyAsync(s->imgs, ptrs.data(), ptrs.size() * sizeof(void*),
                                       hipMemcpyHostToDevice, s->stream));
-        for (int i = 0; i < nb; ++i) {
-            const int rc = s->step(s->imgs + 2 * i);
-            if (rc) return rc;
+        // one batched feature pass over the nb pairs, then their per-pair chains
+        int rc = s->detect(nb);
+        if (!rc) rc = s->steps(nb);
+        if (rc) return rc;
+        if (s->timed) {
+            VISO_HIP_CHECK(hipEventSynchronize(s->ev[1]));
+            float ms = 0.f;
+            VISO_HIP_CHECK(hipEventElapsedTime(&ms, s->ev[0], s->ev[1]));
+            s->detect_ms = ms;
+            s->detect_pairs = nb;
         }
         // the pointer table is reused by the next batch
         VISO_HIP_CHECK(hipStreamSynchronize(s->stream));
     }
+    return VISO_OK;
+}
+
+int viso_svo_timing(viso_svo* s, int32_t enable, double* last_feature_pass_ms, int32_t* pairs) {
+    if (!s) return VISO_ERR_ARG;
+    s->timed = enable != 0;
+    if (last_feature_pass_ms) *last_feature_pass_ms = s->detect_ms;
+    if (pairs) *pairs = s->detect_pairs;
     return VISO_OK;
 }
 
@@ -1130,7 +1193,7 @@ int viso_svo_get_poses(viso_svo* s, double* poses12, size_t cap, size_t* n) {
     if (!s || !n) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(s->device));
     VISO_HIP_CHECK(hipStreamSynchronize(s->stream));
-    const size_t m = std::min(s->n_poses, s->max_poses);
+    const size_t m = std::min(s->frame, s->max_poses);
     *n = m;
     if (poses12 && cap)
         VISO_HIP_CHECK(hipMemcpy(poses12, s->pose_log, std::min(m, cap) * 12 * sizeof(double),
@@ -1160,10 +1223,10 @@ int viso_svo_features(viso_svo* s, const uint8_t* img, int32_t width, int32_t he
     VISO_HIP_CHECK(hipMemcpyAsync(s->img + bytes, img, bytes, hipMemcpyHostToDevice, s->stream));
     const uint8_t* ptrs[2] = {s->img, s->img + bytes};
     VISO_HIP_CHECK(hipMemcpyAsync(s->imgs, ptrs, sizeof(ptrs), hipMemcpyHostToDevice, s->stream));
-    int rc = s->detect(s->imgs);
+    int rc = s->detect(1);  // into the slot of pair `frame` (not advanced)
     if (rc) return rc;
     VISO_HIP_CHECK(hipStreamSynchronize(s->stream));
-    const FeatDev& F = s->set[2 * s->cur];
+    const FeatDev F = s->set_at(s->frame, 0);
     int m = 0;
     VISO_HIP_CHECK(hipMemcpy(&m, F.n, sizeof(int), hipMemcpyDeviceToHost));
     *n = m;
@@ -1183,14 +1246,16 @@ int viso_svo_match(viso_svo* s, const int32_t* const* u4, const int32_t* const* 
     if (!s || !u4 || !v4 || !cls4 || !desc4 || !n4 || !n) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(s->device));
     const int h = s->p.height;
-    // load the four sets into slots: prev = (cur^1), current = cur
-    const int slot[4] = {2 * (s->cur ^ 1), 2 * (s->cur ^ 1) + 1, 2 * s->cur, 2 * s->cur + 1};
+    // the four sets go to the slots of pairs frame + 1 (previous) and
+    // frame + 2 (current): pair `frame`'s slot (the sequence's last pair) is kept
+    const size_t pa = s->frame + 1, pb = s->frame + 2;
+    FeatDev* F4[4] = {&s->set_at(pa, 0), &s->set_at(pa, 1), &s->set_at(pb, 0), &s->set_at(pb, 1)};
     for (int k = 0; k < 4; ++k) {
         const int m = n4[k];
         if (m < 0 || m > s->p.max_features) return VISO_ERR_ARG;
         for (int i = 1; i < m; ++i)
             if (v4[k][i] < v4[k][i - 1]) return VISO_ERR_ARG;  // row-major order required
-        FeatDev& F = s->set[slot[k]];
+        FeatDev& F = *F4[k];
         std::vector<int> row0((size_t)h + 1, m);
         for (int i = m - 1; i >= 0; --i) {
             if (v4[k][i] < 0 || v4[k][i] >= h) return VISO_ERR_ARG;
@@ -1207,8 +1272,8 @@ int viso_svo_match(viso_svo* s, const int32_t* const* u4, const int32_t* const* 
         VISO_HIP_CHECK(hipMemcpy(F.n, &m, sizeof(int), hipMemcpyHostToDevice));
     }
     const SvoDev d = s->dev();
-    FeatDev &L1 = s->set[slot[0]], &R1 = s->set[slot[1]], &L2 = s->set[slot[2]], &R2 = s->set[slot[3]];
-    svo_circle_kernel<<<1024, 256, 0, s->stream>>>(d, L1, R1, L2, R2, s->circ);
+    svo_circle_kernel<<<1024, 256, 0, s->stream>>>(d, *F4[0], *F4[1], *F4[2], *F4[3], s->circ, s->rec8,
+                                                   s->keep);
     VISO_HIP_CHECK(hipGetLastError());
     VISO_HIP_CHECK(hipStreamSynchronize(s->stream));
     std::vector<int4> res((size_t)std::max(1, n4[2]));

@@ -96,6 +96,13 @@ class VisualOdometryStereo:
     def synchronize(self):
         _lib.call("viso_svo_synchronize", self.h)
 
+    def timing(self, enable: bool = True):
+        """HIP-event timing of the batched feature pass -> (last batch ms, pairs)."""
+        ms = ctypes.c_double(0.0)
+        n = ctypes.c_int32(0)
+        _lib.call("viso_svo_timing", self.h, int(enable), ctypes.byref(ms), ctypes.byref(n))
+        return ms.value, n.value
+
     def getMotion(self) -> np.ndarray:  # noqa: N802 (north-star name)
         m = np.zeros(12, np.float64)
         _lib.call("viso_svo_get_motion", self.h, _p(m))
