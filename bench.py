@@ -22,7 +22,10 @@ Prints ONE JSON line on rank 0 (the driver's contract), including:
                  HIP-event timed inside this run;
   cpu_baseline — the CPU oracle (single thread) on a bounded sample of the
                  same sequence, timed on this host;
-  parity       — GPU vs oracle pose rel-Frobenius on the sampled frames.
+  parity       — GPU vs oracle pose rel-Frobenius on the sampled frames;
+  stereo_vo    — the north-star stereo VO (no reference counterpart) on the
+                 same resident pairs: pairs/s, its batched feature pass, its
+                 CPU spec on a bounded sample and pose parity.
 """
 from __future__ import annotations
 
@@ -56,7 +59,58 @@ def parse():
     ap.add_argument("--cpu-frames", type=int, default=200,
                     help="timed tracking frames of the CPU oracle sample (0 = skip)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-svo", action="store_true", help="skip the stereo-VO side measurement")
+    ap.add_argument("--svo-cpu-pairs", type=int, default=12,
+                    help="pairs of the stereo-VO CPU spec timed for its baseline (0 = skip)")
     return ap.parse_args()
+
+
+def measure_svo(args, seq, left, right, d_left, d_right, W, H, log):
+    """Stereo VO (viso_svo_process_device) over the timed pairs: pairs/s, the
+    batched feature pass vs HBM peak, and the CPU spec on a bounded sample."""
+    import torch
+
+    from viso_amd import svo
+
+    n = args.warmup + args.steps
+    p = svo.default_params(W, H, *seq.K, seq.p.baseline)
+    vo = svo.VisualOdometryStereo(p)
+    vo.process_device(d_left.data_ptr(), d_right.data_ptr(), min(8, n), W * H)  # warm-up
+    vo.synchronize()
+    vo = svo.VisualOdometryStereo(p)
+    vo.timing(True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    vo.process_device(d_left.data_ptr(), d_right.data_ptr(), n, W * H)
+    vo.synchronize()
+    dt = time.perf_counter() - t0
+    ms, pairs = vo.timing(False)
+    feat_bytes = 2.0 * W * H * pairs  # the batch's left + right images, read once
+    out = {"pairs": n, "pairs_per_s": round(n / dt, 1), "us_per_pair": round(1e6 * dt / n, 2),
+           "feature_pass": {"pairs_per_launch": pairs, "ms": round(ms, 4),
+                            "achieved_GBps": round(feat_bytes / (ms * 1e-3) / 1e9, 1) if ms else None,
+                            "peak_GBps": HBM_PEAK_GBS,
+                            "frac": round(feat_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if ms else None,
+                            "bound": "VALU (filters + NMS per pixel), not HBM"},
+           "last_pair_stats": vo.stats().tolist()}
+    log(f"[svo] {out['pairs_per_s']} pairs/s")
+    if not args.no_cpu and args.svo_cpu_pairs > 0:
+        from tests import oracle_lib
+        m = min(args.svo_cpu_pairs, n)
+        S = oracle_lib.SvoSequence(oracle_lib.svo_params(W, H, *seq.K, seq.p.baseline))
+        t0 = time.perf_counter()
+        for f in range(m):
+            S.process(left[f], right[f])
+        cpu_s = time.perf_counter() - t0
+        gp = vo.poses[:m]
+        op = np.array(S.poses[:m])
+        out["cpu_baseline"] = {"value": round(m / cpu_s, 3), "unit": "pairs/s", "cores": 1, "kind": "port",
+                               "sample": f"oracle/oracle_svo.cpp spec, single thread, pairs 0-{m - 1} of "
+                                         "the same synthetic sequence"}
+        out["speedup_vs_cpu"] = round(out["pairs_per_s"] / out["cpu_baseline"]["value"], 1)
+        out["parity_vs_oracle"] = {"pairs": int(m),
+                                   "pose_max_abs_diff": float(np.abs(gp - op).max()) if len(gp) == len(op) else None}
+    return out
 
 
 def main():
@@ -186,6 +240,15 @@ def main():
     n_map = len(v.GetPoints())
     value = world * args.steps / elapsed
 
+    # ---------------------------------------------------------- north-star stereo VO
+    # The stereo path the north star names (blob/corner NMS features, SAD
+    # circular matching, RANSAC + Gauss-Newton; include/viso/viso_svo.h) has
+    # no reference counterpart; it is measured beside the headline metric on
+    # the same resident pairs (rank 0).
+    stereo_vo = None
+    if rank == 0 and not args.no_svo:
+        stereo_vo = measure_svo(args, seq, left, right, d_left, d_right, W, H, log)
+
     # ---------------------------------------------------------- CPU baseline + parity
     cpu = None
     parity = None
@@ -232,6 +295,7 @@ def main():
             "kernels": {k: {"launches": t["launches"], "avg_ms": round(t["avg_ms"], 5)}
                         for k, t in timing.items()},
             "kernels_breakdown_chunk": breakdown,
+            "stereo_vo": stereo_vo,
             "last_frame_stats": {"direct_nGood": st[9], "lk_pairs": st[6], "lk_success": st[7]},
         }
         print(json.dumps(out), flush=True)

@@ -257,3 +257,28 @@ def test_gpu_sequence_matches_oracle(synth_frames):
     P = vo.poses
     assert len(P) == len(S.poses)
     assert np.allclose(P, np.array(S.poses), rtol=0, atol=1e-9)
+
+
+@pytest.mark.gpu
+def test_gpu_batched_device_path_matches_sequential(synth_frames):
+    """viso_svo_process_device (one feature pass + side-by-side motions for a
+    batch) gives the per-pair results of process() and of the spec."""
+    import torch
+
+    from viso_amd import svo
+    seq, frames = synth_frames
+    p = svo.default_params(1242, 375, *seq.K, seq.p.baseline)
+    L = torch.from_numpy(np.stack([f[0] for f in frames])).cuda()
+    R = torch.from_numpy(np.stack([f[1] for f in frames])).cuda()
+    vb = svo.VisualOdometryStereo(p)
+    vb.process_device(L.data_ptr(), R.data_ptr(), len(frames), 1242 * 375)
+    vs = svo.VisualOdometryStereo(p)
+    S = ol.SvoSequence(ol.svo_params(1242, 375, *seq.K, seq.p.baseline))
+    for l, r in frames:
+        vs.process(l, r)
+        S.process(l, r)
+    assert np.array_equal(vb.poses, vs.poses)
+    assert vb.stats().tolist() == vs.stats().tolist() == S.stats
+    assert np.array_equal(vb.getMotion(), vs.getMotion())
+    ub, ib = vb.getMatches()
+    assert np.array_equal(ub, S.matches) and np.array_equal(ib, S.inliers)

@@ -63,6 +63,30 @@ struct FeatDev {
     int* off;      // [h][tiles] feature index of the first candidate
 };
 
+// per-batch estimation buffers: pair b of a batch (sequence frame frame0 + b)
+// owns slot b of every array
+struct PairArgs {
+    const FeatDev* sets;
+    int ring;
+    long long frame0;
+    int cap, mcap;       // features per image, bucketed matches per pair
+    int4* circ;          // [P][cap]      {l1, r1, r2, -}
+    int4* rec8;          // [P][2 cap]    {u_l1, v_l1, u_r1, v_r1}, {u_l2, v_l2, u_r2, v_r2}
+    uint8_t* keep;       // [P][cap]
+    int* uv8;            // [P][mcap * 8]
+    int* n_sel;          // [P]
+    int* counts;         // [P][iters]
+    double* models;      // [P][iters * 12]
+    uint8_t* sel;        // [P][mcap]
+    uint8_t* inl;        // [P][mcap]
+    double* motion;      // [P][12]
+    int* stats;          // [P][8]
+};
+
+__device__ inline FeatDev set_frame(const PairArgs& a, long long frame, int side) {
+    return a.sets[2 * (int)(frame % a.ring) + side];
+}
+
 // ---------------------------------------------------------------- detect
 // Strict NMS by separable maxima: for class map V (sign-adjusted response,
 // -inf outside the response domain) the largest neighbour of p is
@@ -306,11 +330,17 @@ __device__ int best_match(const FeatDev& S, int h, int u, int v, int c, uint4 q0
     return best == 0xffffffffu ? -1 : (int)(best & 0x7fffu);
 }
 
-// wave per current-left feature; rec[i2] = {l1, r1, r2, -} and
-// rec8[i2] = {u_l1, v_l1, u_r1, v_r1, u_l2, v_l2, u_r2, v_r2}, or rec[i2].x = -1
-__global__ __launch_bounds__(256) void svo_circle_kernel(SvoDev p, FeatDev L1, FeatDev R1, FeatDev L2,
-                                                         FeatDev R2, int4* __restrict__ out,
-                                                         int4* __restrict__ rec8, uint8_t* __restrict__ keep) {
+// wave per current-left feature of pair b0 + blockIdx.y; circ[i2] = {l1,
+// r1, r2, -} and rec8[i2] = {u_l1, v_l1, u_r1, v_r1, u_l2, v_l2, u_r2, v_r2},
+// or circ[i2].x = rec8[i2].x = -1
+__global__ __launch_bounds__(256) void svo_circle_kernel(SvoDev p, PairArgs pa, int b0) {
+    const int pb = b0 + blockIdx.y;
+    const long long fr = pa.frame0 + pb;
+    const FeatDev L1 = set_frame(pa, fr - 1, 0), R1 = set_frame(pa, fr - 1, 1), L2 = set_frame(pa, fr, 0),
+                  R2 = set_frame(pa, fr, 1);
+    int4* __restrict__ out = pa.circ + (size_t)pb * pa.cap;
+    int4* __restrict__ rec8 = pa.rec8 + (size_t)pb * 2 * pa.cap;
+    uint8_t* __restrict__ keep = pa.keep + (size_t)pb * pa.cap;
     const int n2 = *L2.n;
     const int D = p.disp_max, Rr = p.radius, h = p.h;
     auto desc = [](const FeatDev& S, int i, uint4& a, uint4& b) {
@@ -566,9 +596,11 @@ constexpr int kMaxBuckets = 4096;
 // features of its band of rows (a contiguous index range, features being
 // row-major); lanes test 64 at a time (circular match present, column in the
 // bucket), a ballot ranks them in index order, the first bucket_max are kept.
-__global__ __launch_bounds__(256) void svo_bucket_kernel(SvoDev p, const FeatDev L2,
-                                                         const int4* __restrict__ rec8,
-                                                         uint8_t* __restrict__ keep) {
+__global__ __launch_bounds__(256) void svo_bucket_kernel(SvoDev p, PairArgs pa, int b0) {
+    const int pb = b0 + blockIdx.y;
+    const FeatDev L2 = set_frame(pa, pa.frame0 + pb, 0);
+    const int4* __restrict__ rec8 = pa.rec8 + (size_t)pb * 2 * pa.cap;
+    uint8_t* __restrict__ keep = pa.keep + (size_t)pb * pa.cap;
     const int lane = threadIdx.x & 63;
     const int nbx = (p.w + p.bw - 1) / p.bw, nby = (p.h + p.bh - 1) / p.bh;
     const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -592,11 +624,14 @@ __global__ __launch_bounds__(256) void svo_bucket_kernel(SvoDev p, const FeatDev
 
 // Compaction of the kept matches in left order -> uv8; stats[2] = circular
 // matches, stats[3] = bucketed.
-__global__ __launch_bounds__(1024) void svo_select_kernel(SvoDev p, const FeatDev L2,
-                                                          const int4* __restrict__ rec8,
-                                                          const uint8_t* __restrict__ keep,
-                                                          int* __restrict__ uv8, int* __restrict__ n_sel,
-                                                          int* __restrict__ stats) {
+__global__ __launch_bounds__(1024) void svo_select_kernel(SvoDev p, PairArgs pa, int b0) {
+    const int pb = b0 + blockIdx.x;
+    const FeatDev L2 = set_frame(pa, pa.frame0 + pb, 0);
+    const int4* __restrict__ rec8 = pa.rec8 + (size_t)pb * 2 * pa.cap;
+    const uint8_t* __restrict__ keep = pa.keep + (size_t)pb * pa.cap;
+    int* __restrict__ uv8 = pa.uv8 + (size_t)pb * pa.mcap * 8;
+    int* __restrict__ n_sel = pa.n_sel + pb;
+    int* __restrict__ stats = pa.stats + (size_t)pb * 8;
     __shared__ int s_w[16];
     const int tid = threadIdx.x;
     const int n2 = *L2.n;
@@ -642,9 +677,13 @@ __device__ inline bool sample3(uint64_t seed, int h, int M, int* idx) {
 }
 
 // wave per hypothesis: counts[h], models[h] = R(9) t(3)
-__global__ __launch_bounds__(256) void svo_ransac_kernel(SvoDev p, const int* __restrict__ uv8,
-                                                         const int* __restrict__ n_sel, uint64_t seed,
-                                                         int* __restrict__ counts, double* __restrict__ models) {
+__global__ __launch_bounds__(256) void svo_ransac_kernel(SvoDev p, PairArgs pa, int b0) {
+    const int pb = b0 + blockIdx.y;
+    const uint64_t seed = mix64(p.seed ^ (uint64_t)(pa.frame0 + pb));
+    const int* __restrict__ uv8 = pa.uv8 + (size_t)pb * pa.mcap * 8;
+    const int* __restrict__ n_sel = pa.n_sel + pb;
+    int* __restrict__ counts = pa.counts + (size_t)pb * p.iters;
+    double* __restrict__ models = pa.models + (size_t)pb * p.iters * 12;
     __shared__ double s_st[4][12];
     __shared__ int s_ok[4];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -718,13 +757,16 @@ __global__ __launch_bounds__(256) void svo_ransac_kernel(SvoDev p, const int* __
 // inlier flags, motion, pose update T_wc <- T_wc * Tr^-1, stats.
 constexpr int kMaxChunks = 128;  // 64-leaf chunks: M <= 8192 (bucket count x bucket_max)
 
-__global__ __launch_bounds__(1024) void svo_refine_kernel(SvoDev p, const int* __restrict__ uv8,
-                                                         const int* __restrict__ n_sel,
-                                                         const int* __restrict__ counts,
-                                                         const double* __restrict__ models,
-                                                         uint8_t* __restrict__ sel, uint8_t* __restrict__ inl,
-                                                         double* __restrict__ motion, double* __restrict__ pose,
-                                                         double* __restrict__ pose_log, int* __restrict__ stats) {
+__global__ __launch_bounds__(1024) void svo_refine_kernel(SvoDev p, PairArgs pa, int b0) {
+    const int pb = b0 + blockIdx.x;
+    const int* __restrict__ uv8 = pa.uv8 + (size_t)pb * pa.mcap * 8;
+    const int* __restrict__ n_sel = pa.n_sel + pb;
+    const int* __restrict__ counts = pa.counts + (size_t)pb * p.iters;
+    const double* __restrict__ models = pa.models + (size_t)pb * p.iters * 12;
+    uint8_t* __restrict__ sel = pa.sel + (size_t)pb * pa.mcap;
+    uint8_t* __restrict__ inl = pa.inl + (size_t)pb * pa.mcap;
+    double* __restrict__ motion = pa.motion + (size_t)pb * 12;
+    int* __restrict__ stats = pa.stats + (size_t)pb * 8;
     __shared__ double s_chunk[kMaxChunks][28];
     __shared__ double s_st[12];
     __shared__ int s_best, s_ok, s_conv, s_cnt;
@@ -843,32 +885,34 @@ __global__ __launch_bounds__(1024) void svo_refine_kernel(SvoDev p, const int* _
         for (int i = 0; i < 12; ++i) motion[i] = T[i];
         stats[4] = ok ? s_cnt : 0;
         stats[5] = ok ? 1 : 0;
-        if (ok) {
-            // T_wc <- T_wc * Tr^-1,  Tr^-1 = [R^T, -R^T t]
-            double Ri[9], ti[3];
+    }
+}
+
+// Sequential tail of a batch (one thread): feature counts, and the camera
+// poses T_wc <- T_wc * Tr^-1 (Tr^-1 = [R^T, -R^T t]) in pair order.
+__global__ void svo_pose_kernel(PairArgs pa, int nb, double* __restrict__ pose,
+                                double* __restrict__ pose_log, long long max_poses) {
+    for (int b = 0; b < nb; ++b) {
+        const long long fr = pa.frame0 + b;
+        int* st = pa.stats + (size_t)b * 8;
+        st[0] = *set_frame(pa, fr, 0).n;
+        st[1] = *set_frame(pa, fr, 1).n;
+        if (fr == 0) {
+            for (int i = 2; i < 8; ++i) st[i] = 0;
+            for (int i = 0; i < 12; ++i) pose[i] = (i % 4 == 0 && i < 9) ? 1.0 : 0.0;
+        } else if (st[5]) {
+            const double* T = pa.motion + (size_t)b * 12;
+            double Ri[9], ti[3], Rn[9], tn[3];
             for (int i = 0; i < 3; ++i)
                 for (int j = 0; j < 3; ++j) Ri[3 * i + j] = T[3 * j + i];
             for (int i = 0; i < 3; ++i) ti[i] = -((Ri[3 * i] * T[9] + Ri[3 * i + 1] * T[10]) + Ri[3 * i + 2] * T[11]);
-            double Rn[9], tn[3];
             mat3_mul_s(pose, Ri, Rn);
             for (int i = 0; i < 3; ++i) tn[i] = ((pose[3 * i] * ti[0] + pose[3 * i + 1] * ti[1]) + pose[3 * i + 2] * ti[2]) + pose[9 + i];
             for (int i = 0; i < 9; ++i) pose[i] = Rn[i];
             for (int i = 0; i < 3; ++i) pose[9 + i] = tn[i];
         }
-        for (int i = 0; i < 12; ++i) pose_log[i] = pose[i];
-    }
-}
-
-__global__ void svo_stats_kernel(FeatDev a, FeatDev b, int* stats, double* pose, double* pose_log,
-                                 int first) {
-    stats[0] = *a.n;
-    stats[1] = *b.n;
-    if (first) {
-        for (int i = 2; i < 6; ++i) stats[i] = 0;
-        for (int i = 0; i < 12; ++i) {
-            pose[i] = (i % 4 == 0 && i < 9) ? 1.0 : 0.0;
-            pose_log[i] = pose[i];
-        }
+        double* out = pose_log + 12 * (fr < max_poses ? fr : max_poses - 1);
+        for (int i = 0; i < 12; ++i) out[i] = pose[i];
     }
 }
 
@@ -879,7 +923,7 @@ __global__ void svo_stats_kernel(FeatDev a, FeatDev b, int* stats, double* pose,
 using namespace viso;
 
 struct viso_svo {
-    static constexpr int kMaxPairBatch = 64;   // pairs whose features are extracted in one launch
+    static constexpr int kMaxPairBatch = 64;   // pairs per batch (feature pass + estimation)
     static constexpr int kRing = kMaxPairBatch + 1;  // feature-set ring (pairs): a batch + the previous pair
     viso_svo_params p{};
     int device = 0;
@@ -887,23 +931,14 @@ struct viso_svo {
     int tiles = 0;
     int list_cap = 0;
     size_t frame = 0;       // pairs processed; pair k uses ring slot k % kRing
+    int last_b = -1;        // batch slot of the last processed pair
     std::vector<FeatDev> sets;        // 2 * kRing (left, right of each slot)
     FeatDev* d_sets = nullptr;
+    PairArgs pa{};                    // per-pair estimation buffers of a batch
     std::vector<void*> allocs;
     uint8_t* img = nullptr;           // host-path upload buffer (left, right)
-    int4* circ = nullptr;
-    int4* rec8 = nullptr;
-    uint8_t* keep = nullptr;
-    int* uv8 = nullptr;
-    int* n_sel = nullptr;
-    int* counts = nullptr;
-    double* models = nullptr;
-    uint8_t* sel = nullptr;
-    uint8_t* inl = nullptr;
-    double* motion = nullptr;
     double* pose = nullptr;
     double* pose_log = nullptr;       // [max_poses][12]
-    int* stats = nullptr;
     size_t max_poses = 0;
     const uint8_t** imgs = nullptr;   // device table of 2 * kMaxPairBatch image pointers
     hipEvent_t ev[2] = {nullptr, nullptr};
@@ -956,14 +991,20 @@ struct viso_svo {
                 alloc(f.row0, (size_t)h + 1) || alloc(f.n, 1) || alloc(f.cnt, (size_t)h * tiles) ||
                 alloc(f.list, (size_t)h * tiles * list_cap) || alloc(f.off, (size_t)h * tiles))
                 return VISO_ERR_HIP;
+        const int nbk = ((w + p.bucket_width - 1) / p.bucket_width) * ((h + p.bucket_height - 1) / p.bucket_height);
+        const int P = kMaxPairBatch, it = std::max(1, p.ransac_iters);
+        pa.ring = kRing;
+        pa.cap = cap;
+        pa.mcap = std::min(cap, nbk * p.bucket_max);
         max_poses = 65536;
-        if (alloc(d_sets, sets.size()) || alloc(img, 2 * (size_t)w * h) || alloc(circ, cap) ||
-            alloc(rec8, 2 * (size_t)cap) || alloc(keep, cap) || alloc(uv8, (size_t)cap * 8) || alloc(n_sel, 1) ||
-            alloc(counts, std::max(1, p.ransac_iters)) ||
-            alloc(models, (size_t)std::max(1, p.ransac_iters) * 12) || alloc(sel, cap) || alloc(inl, cap) ||
-            alloc(motion, 12) || alloc(pose, 12) || alloc(pose_log, max_poses * 12) || alloc(stats, 8) ||
-            alloc(imgs, 2 * kMaxPairBatch))
+        if (alloc(d_sets, sets.size()) || alloc(img, 2 * (size_t)w * h) ||
+            alloc(pa.circ, (size_t)P * cap) || alloc(pa.rec8, (size_t)P * 2 * cap) || alloc(pa.keep, (size_t)P * cap) ||
+            alloc(pa.uv8, (size_t)P * pa.mcap * 8) || alloc(pa.n_sel, P) || alloc(pa.counts, (size_t)P * it) ||
+            alloc(pa.models, (size_t)P * it * 12) || alloc(pa.sel, (size_t)P * pa.mcap) ||
+            alloc(pa.inl, (size_t)P * pa.mcap) || alloc(pa.motion, (size_t)P * 12) || alloc(pa.stats, (size_t)P * 8) ||
+            alloc(pose, 12) || alloc(pose_log, max_poses * 12) || alloc(imgs, 2 * kMaxPairBatch))
             return VISO_ERR_HIP;
+        pa.sets = d_sets;
         VISO_HIP_CHECK(hipMemcpy(d_sets, sets.data(), sets.size() * sizeof(FeatDev), hipMemcpyHostToDevice));
         VISO_HIP_CHECK(hipEventCreate(&ev[0]));
         VISO_HIP_CHECK(hipEventCreate(&ev[1]));
@@ -992,36 +1033,35 @@ struct viso_svo {
         VISO_HIP_CHECK(hipGetLastError());
         return VISO_OK;
     }
-    // matching + motion of pair `frame` against pair `frame - 1`
-    int match_and_estimate() {
+    // motion estimation of batch slots [b0, b0 + np) (pairs frame0 + b): every
+    // pair needs only its own and the previous pair's features, so the pairs
+    // of a batch run side by side in each launch
+    int estimate(long long frame0, int b0, int np) {
+        if (np <= 0) return VISO_OK;
         const SvoDev d = dev();
-        const FeatDev L1 = set_at(frame - 1, 0), R1 = set_at(frame - 1, 1), L2 = set_at(frame, 0),
-                      R2 = set_at(frame, 1);
-        svo_circle_kernel<<<1024, 256, 0, stream>>>(d, L1, R1, L2, R2, circ, rec8, keep);
+        pa.frame0 = frame0;
         const int nbk = ((p.width + p.bucket_width - 1) / p.bucket_width) *
                         ((p.height + p.bucket_height - 1) / p.bucket_height);
-        svo_bucket_kernel<<<(nbk + 3) / 4, 256, 0, stream>>>(d, L2, rec8, keep);
-        svo_select_kernel<<<1, 1024, 0, stream>>>(d, L2, rec8, keep, uv8, n_sel, stats);
-        const uint64_t seed = mix64(p.seed ^ (uint64_t)frame);
-        svo_ransac_kernel<<<(p.ransac_iters + 3) / 4, 256, 0, stream>>>(d, uv8, n_sel, seed, counts, models);
-        svo_refine_kernel<<<1, 1024, 0, stream>>>(d, uv8, n_sel, counts, models, sel, inl, motion, pose,
-                                                  pose_log + 12 * std::min(frame, max_poses - 1), stats);
+        svo_circle_kernel<<<dim3(std::max(32, 2048 / np), np), 256, 0, stream>>>(d, pa, b0);
+        svo_bucket_kernel<<<dim3((nbk + 3) / 4, np), 256, 0, stream>>>(d, pa, b0);
+        svo_select_kernel<<<np, 1024, 0, stream>>>(d, pa, b0);
+        svo_ransac_kernel<<<dim3((p.ransac_iters + 3) / 4, np), 256, 0, stream>>>(d, pa, b0);
+        svo_refine_kernel<<<np, 1024, 0, stream>>>(d, pa, b0);
         VISO_HIP_CHECK(hipGetLastError());
         return VISO_OK;
     }
-    // the per-pair chain of the pairs whose features were just extracted
-    int steps(int nb) {
-        for (int i = 0; i < nb; ++i) {
-            const FeatDev A = set_at(frame, 0), B = set_at(frame, 1);
-            svo_stats_kernel<<<1, 1, 0, stream>>>(A, B, stats, pose,
-                                                  pose_log + 12 * std::min(frame, max_poses - 1),
-                                                  frame == 0 ? 1 : 0);
-            if (frame > 0) {
-                const int rc = match_and_estimate();
-                if (rc) return rc;
-            }
-            ++frame;
-        }
+    // a batch of nb pairs whose image pointers are in imgs: features, motions, poses
+    int batch(int nb) {
+        int rc = detect(nb);
+        if (rc) return rc;
+        const int b0 = frame == 0 ? 1 : 0;
+        rc = estimate((long long)frame, b0, nb - b0);
+        if (rc) return rc;
+        pa.frame0 = (long long)frame;
+        svo_pose_kernel<<<1, 1, 0, stream>>>(pa, nb, pose, pose_log, (long long)max_poses);
+        VISO_HIP_CHECK(hipGetLastError());
+        frame += nb;
+        last_b = nb - 1;
         return VISO_OK;
     }
 };
@@ -1119,13 +1159,12 @@ int viso_svo_process(viso_svo* s, const uint8_t* left, const uint8_t* right, con
     VISO_HIP_CHECK(hipMemcpy2DAsync(dr, w, right, stride, w, h, hipMemcpyHostToDevice, s->stream));
     const uint8_t* ptrs[2] = {dl, dr};
     VISO_HIP_CHECK(hipMemcpyAsync(s->imgs, ptrs, sizeof(ptrs), hipMemcpyHostToDevice, s->stream));
-    int rc = s->detect(1);
-    if (!rc) rc = s->steps(1);
+    int rc = s->batch(1);
     if (rc) return rc;
     VISO_HIP_CHECK(hipStreamSynchronize(s->stream));
     if (ok) {
         int st[8];
-        VISO_HIP_CHECK(hipMemcpy(st, s->stats, sizeof(st), hipMemcpyDeviceToHost));
+        VISO_HIP_CHECK(hipMemcpy(st, s->pa.stats + 8 * s->last_b, sizeof(st), hipMemcpyDeviceToHost));
         *ok = st[5];
     }
     return VISO_OK;
@@ -1144,9 +1183,8 @@ int viso_svo_process_device(viso_svo* s, const uint8_t* left, const uint8_t* rig
         }
         VISO_HIP_CHECK(hipMemcpyAsync(s->imgs, ptrs.data(), ptrs.size() * sizeof(void*),
                                       hipMemcpyHostToDevice, s->stream));
-        // one batched feature pass over the nb pairs, then their per-pair chains
-        int rc = s->detect(nb);
-        if (!rc) rc = s->steps(nb);
+        // one batched feature pass over the nb pairs, then their motions side by side
+        const int rc = s->batch(nb);
         if (rc) return rc;
         if (s->timed) {
             VISO_HIP_CHECK(hipEventSynchronize(s->ev[1]));
@@ -1177,7 +1215,7 @@ int viso_svo_get_motion(viso_svo* s, double* motion12) {
         for (int i = 0; i < 12; ++i) motion12[i] = (i % 4 == 0 && i < 9) ? 1.0 : 0.0;
         return VISO_OK;
     }
-    VISO_HIP_CHECK(hipMemcpy(motion12, s->motion, 12 * sizeof(double), hipMemcpyDeviceToHost));
+    VISO_HIP_CHECK(hipMemcpy(motion12, s->pa.motion + 12 * s->last_b, 12 * sizeof(double), hipMemcpyDeviceToHost));
     return VISO_OK;
 }
 
@@ -1185,7 +1223,11 @@ int viso_svo_get_stats(viso_svo* s, int32_t* stats6) {
     if (!s || !stats6) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(s->device));
     VISO_HIP_CHECK(hipStreamSynchronize(s->stream));
-    VISO_HIP_CHECK(hipMemcpy(stats6, s->stats, 6 * sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (s->last_b < 0) {
+        for (int i = 0; i < 6; ++i) stats6[i] = 0;
+        return VISO_OK;
+    }
+    VISO_HIP_CHECK(hipMemcpy(stats6, s->pa.stats + 8 * s->last_b, 6 * sizeof(int32_t), hipMemcpyDeviceToHost));
     return VISO_OK;
 }
 
@@ -1206,11 +1248,15 @@ int viso_svo_get_matches(viso_svo* s, int32_t* uv8, uint8_t* inlier, size_t cap,
     VISO_HIP_CHECK(hipSetDevice(s->device));
     VISO_HIP_CHECK(hipStreamSynchronize(s->stream));
     int m = 0;
-    if (s->frame >= 2) VISO_HIP_CHECK(hipMemcpy(&m, s->n_sel, sizeof(int), hipMemcpyDeviceToHost));
+    const int b = s->last_b;
+    if (s->frame >= 2) VISO_HIP_CHECK(hipMemcpy(&m, s->pa.n_sel + b, sizeof(int), hipMemcpyDeviceToHost));
     *n = (size_t)m;
     const size_t k = std::min((size_t)m, cap);
-    if (uv8 && k) VISO_HIP_CHECK(hipMemcpy(uv8, s->uv8, k * 8 * sizeof(int32_t), hipMemcpyDeviceToHost));
-    if (inlier && k) VISO_HIP_CHECK(hipMemcpy(inlier, s->inl, k, hipMemcpyDeviceToHost));
+    if (uv8 && k)
+        VISO_HIP_CHECK(hipMemcpy(uv8, s->pa.uv8 + (size_t)b * s->pa.mcap * 8, k * 8 * sizeof(int32_t),
+                                 hipMemcpyDeviceToHost));
+    if (inlier && k)
+        VISO_HIP_CHECK(hipMemcpy(inlier, s->pa.inl + (size_t)b * s->pa.mcap, k, hipMemcpyDeviceToHost));
     return VISO_OK;
 }
 
@@ -1248,8 +1294,8 @@ int viso_svo_match(viso_svo* s, const int32_t* const* u4, const int32_t* const* 
     const int h = s->p.height;
     // the four sets go to the slots of pairs frame + 1 (previous) and
     // frame + 2 (current): pair `frame`'s slot (the sequence's last pair) is kept
-    const size_t pa = s->frame + 1, pb = s->frame + 2;
-    FeatDev* F4[4] = {&s->set_at(pa, 0), &s->set_at(pa, 1), &s->set_at(pb, 0), &s->set_at(pb, 1)};
+    const size_t p1 = s->frame + 1, p2 = s->frame + 2;
+    FeatDev* F4[4] = {&s->set_at(p1, 0), &s->set_at(p1, 1), &s->set_at(p2, 0), &s->set_at(p2, 1)};
     for (int k = 0; k < 4; ++k) {
         const int m = n4[k];
         if (m < 0 || m > s->p.max_features) return VISO_ERR_ARG;
@@ -1272,13 +1318,14 @@ int viso_svo_match(viso_svo* s, const int32_t* const* u4, const int32_t* const* 
         VISO_HIP_CHECK(hipMemcpy(F.n, &m, sizeof(int), hipMemcpyHostToDevice));
     }
     const SvoDev d = s->dev();
-    svo_circle_kernel<<<1024, 256, 0, s->stream>>>(d, *F4[0], *F4[1], *F4[2], *F4[3], s->circ, s->rec8,
-                                                   s->keep);
+    PairArgs pa = s->pa;
+    pa.frame0 = (long long)p2;  // slot 0 = pair p2 (previous: p1)
+    svo_circle_kernel<<<dim3(1024, 1), 256, 0, s->stream>>>(d, pa, 0);
     VISO_HIP_CHECK(hipGetLastError());
     VISO_HIP_CHECK(hipStreamSynchronize(s->stream));
     std::vector<int4> res((size_t)std::max(1, n4[2]));
     if (n4[2] > 0)
-        VISO_HIP_CHECK(hipMemcpy(res.data(), s->circ, (size_t)n4[2] * sizeof(int4), hipMemcpyDeviceToHost));
+        VISO_HIP_CHECK(hipMemcpy(res.data(), s->pa.circ, (size_t)n4[2] * sizeof(int4), hipMemcpyDeviceToHost));
     int m = 0;
     for (int i2 = 0; i2 < n4[2]; ++i2)
         if (res[(size_t)i2].x >= 0) {
@@ -1298,24 +1345,20 @@ int viso_svo_estimate(viso_svo* s, const int32_t* uv8, int32_t n, int64_t frame,
                       uint8_t* inlier, int32_t* n_inliers) {
     if (!s || (!uv8 && n > 0) || n < 0 || n > s->p.max_features || !motion12) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(s->device));
-    if (n > 0) VISO_HIP_CHECK(hipMemcpy(s->uv8, uv8, (size_t)n * 8 * sizeof(int), hipMemcpyHostToDevice));
-    VISO_HIP_CHECK(hipMemcpy(s->n_sel, &n, sizeof(int), hipMemcpyHostToDevice));
+    if (n > s->pa.mcap) return VISO_ERR_CAPACITY;
+    if (n > 0) VISO_HIP_CHECK(hipMemcpy(s->pa.uv8, uv8, (size_t)n * 8 * sizeof(int), hipMemcpyHostToDevice));
+    VISO_HIP_CHECK(hipMemcpy(s->pa.n_sel, &n, sizeof(int), hipMemcpyHostToDevice));
     const SvoDev d = s->dev();
-    // scratch pose so the sequence state is untouched
-    double* pose_tmp = s->pose_log + 12 * (s->max_poses - 1);
-    const double I12[12] = {1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0};
-    VISO_HIP_CHECK(hipMemcpy(pose_tmp, I12, sizeof(I12), hipMemcpyHostToDevice));
-    const uint64_t seed = mix64(s->p.seed ^ (uint64_t)frame);
-    svo_ransac_kernel<<<(s->p.ransac_iters + 3) / 4, 256, 0, s->stream>>>(d, s->uv8, s->n_sel, seed, s->counts,
-                                                                         s->models);
-    svo_refine_kernel<<<1, 1024, 0, s->stream>>>(d, s->uv8, s->n_sel, s->counts, s->models, s->sel, s->inl,
-                                                s->motion, pose_tmp, pose_tmp, s->stats);
+    PairArgs pa = s->pa;
+    pa.frame0 = frame;  // slot 0: the sampler stream of `frame`
+    svo_ransac_kernel<<<dim3((s->p.ransac_iters + 3) / 4, 1), 256, 0, s->stream>>>(d, pa, 0);
+    svo_refine_kernel<<<1, 1024, 0, s->stream>>>(d, pa, 0);
     VISO_HIP_CHECK(hipGetLastError());
     VISO_HIP_CHECK(hipStreamSynchronize(s->stream));
-    VISO_HIP_CHECK(hipMemcpy(motion12, s->motion, 12 * sizeof(double), hipMemcpyDeviceToHost));
-    if (inlier && n > 0) VISO_HIP_CHECK(hipMemcpy(inlier, s->inl, n, hipMemcpyDeviceToHost));
+    VISO_HIP_CHECK(hipMemcpy(motion12, s->pa.motion, 12 * sizeof(double), hipMemcpyDeviceToHost));
+    if (inlier && n > 0) VISO_HIP_CHECK(hipMemcpy(inlier, s->pa.inl, n, hipMemcpyDeviceToHost));
     int st[8];
-    VISO_HIP_CHECK(hipMemcpy(st, s->stats, sizeof(st), hipMemcpyDeviceToHost));
+    VISO_HIP_CHECK(hipMemcpy(st, s->pa.stats, sizeof(st), hipMemcpyDeviceToHost));
     if (n_inliers) *n_inliers = st[5] ? st[4] : -1;
     return VISO_OK;
 }
