@@ -76,9 +76,10 @@ int viso_svo_process_device(viso_svo* s, const uint8_t* left, const uint8_t* rig
                             int64_t pair_stride, int32_t stride);
 int viso_svo_synchronize(viso_svo* s);
 /* HIP-event timing of the batched feature pass (detect + scan + describe of
- * all pairs of a viso_svo_process_device batch): enable, and read the last
- * batch's time and pair count. */
-int viso_svo_timing(viso_svo* s, int32_t enable, double* last_feature_pass_ms, int32_t* pairs);
+ * the pairs of each batch): returns the time summed over the batches since
+ * the previous call and their pair count (waits for the stream if any batch
+ * was timed), then enables (enable != 0) or disables timing. */
+int viso_svo_timing(viso_svo* s, int32_t enable, double* feature_pass_ms, int32_t* pairs);
 
 /* Last motion Tr (camera t-1 -> camera t: P_t = R P_{t-1} + t), 12 doubles
  * (R row-major, t).  getMotion(). */

@@ -176,7 +176,9 @@ def gpu_vo():
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind,h,w,tau,n", [
     ("synth", 375, 1242, 700, 5), ("mixed", 375, 1242, 700, 5), ("noise", 120, 160, 300, 2),
-    ("blocks", 96, 128, 100, 1), ("synth1080", 1080, 1920, 700, 5), ("smooth", 64, 64, 50, 3)])
+    ("blocks", 96, 128, 100, 1), ("synth1080", 1080, 1920, 700, 5), ("smooth", 64, 64, 50, 3),
+    # margin 8 < n + 2: responses outside the domain enter the NMS (as -inf)
+    ("noise", 150, 300, 200, 7), ("mixed", 200, 700, 300, 8)])
 def test_gpu_features_bitexact(kind, h, w, tau, n):
     from viso_amd import svo
     if kind.startswith("synth"):

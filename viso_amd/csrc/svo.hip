@@ -4,12 +4,14 @@
 // checker): oracle/oracle_svo.cpp.  No reference counterpart.
 //
 // Per stereo pair (all on one HIP stream, no host round trip):
-//   svo_detect_kernel    image tile -> LDS, 5x5 blob / checkerboard responses,
-//                        strict (2n+1)^2 NMS of the four classes, per-(row,
-//                        tile) candidate lists in (x, class) order
-//   svo_scan_kernel      row-major prefix over the lists -> feature indices
+//   svo_detect_kernel    thread per column of a 256-column tile: image rows
+//                        staged in LDS, 5x5 blob / checkerboard responses
+//                        from a register row window, strict (2n+1)^2 NMS of
+//                        the four classes as packed 16-bit max/min, per-(row,
+//                        tile, wave) candidate lists in (x, class) order
+//   svo_scan_kernel      row-major prefix over the lists -> u, v, class
 //   svo_describe_kernel  16 lanes per feature: Sobel du/dv at the 16 sample
-//                        offsets -> 32-byte descriptor, SoA feature arrays
+//                        offsets -> 32-byte descriptor
 //   svo_circle_kernel    wave per current-left feature: four best-SAD
 //                        searches (v_sad_u8, wave argmin on (sad, index))
 //                        left_t -> right_t -> right_t-1 -> left_t-1 -> left_t
@@ -34,10 +36,7 @@
 namespace viso {
 namespace {
 
-constexpr int kTW = 128;        // detect tile: output columns
-constexpr int kTH = 16;         // detect tile: output rows
-constexpr int kMaxNms = 8;      // nms_n bound (LDS sizing)
-constexpr int kListCap = 256;   // candidates per (row, tile): 4 classes x 64 (nms_n >= 1)
+constexpr int kMaxNms = 8;      // nms_n bound (detect kernel instances)
 constexpr int kDesc = VISO_SVO_DESC_BYTES;
 
 __constant__ int c_p16[16][2] = {{-5, -1}, {-5, 1}, {-3, -3}, {-3, 3}, {-1, -5}, {-1, 5},
@@ -45,7 +44,7 @@ __constant__ int c_p16[16][2] = {{-5, -1}, {-5, 1}, {-3, -3}, {-3, 3}, {-1, -5},
                                  {3, -3},  {3, 3},  {5, -1},  {5, 1}};
 
 struct SvoDev {  // kernel view of the parameters
-    int w, h, nms_n, tau, margin, disp_max, radius, bw, bh, bmax, iters, gn_iters, cap;
+    int w, h, nms_n, tau, margin, disp_max, radius, bw, bh, bmax, iters, gn_iters, cap, nband, ow;
     double fx, fy, cu, cv, base, th2, eps;
     uint64_t seed;
 };
@@ -57,10 +56,23 @@ struct FeatDev {
     int* c;
     uint8_t* d;    // [cap][32]
     int* row0;     // [h + 1]: first feature index of each row; row0[h] = n
+    // column-band index (bands of kBand columns): the features of band b in
+    // row-major order; brow0[b * (h + 1) + y] = first position of row y
+    int* bidx;     // [cap] feature index
+    int* buc;      // [cap] u | class << 16 of that feature
+    int* brow0;    // [nband][h + 1]
+    int* bcnt;     // [nband][h] per (band, row) counts (scratch)
     int* n;        // [1]
-    int* cnt;      // [h][tiles] candidate counts
-    int* list;     // [h][tiles][kListCap] packed x | cls << 16
-    int* off;      // [h][tiles] feature index of the first candidate
+    int* cnt;      // [h][tiles][4] candidate counts per (row, tile, wave) segment
+    int* list;     // [h][tiles][4][seg_cap] packed x | cls << 16
+};
+
+// the images of a batch: image z = pair z / 2, side z & 1 (left, right)
+struct ImgSrc {
+    const uint8_t* left;
+    const uint8_t* right;
+    long long pair_stride;  // bytes between consecutive pairs
+    __device__ const uint8_t* at(int z) const { return ((z & 1) ? right : left) + (long long)(z >> 1) * pair_stride; }
 };
 
 // per-batch estimation buffers: pair b of a batch (sequence frame frame0 + b)
@@ -88,21 +100,31 @@ __device__ inline FeatDev set_frame(const PairArgs& a, long long frame, int side
 }
 
 // ---------------------------------------------------------------- detect
-// Strict NMS by separable maxima: for class map V (sign-adjusted response,
-// -inf outside the response domain) the largest neighbour of p is
-// max( max_{dy != 0} HI(y + dy, x), HE(y, x) ) with HI / HE the row maxima
-// over [x - n, x + n] including / excluding x itself: fixed cost per pixel,
-// no divergent early-exit loops.
-constexpr int kNegInf = -32768;
+// Thread per response column, workgroup = 256 columns x kDTH output rows of
+// one image (grid.z = images of the batch).  The tile's image rows are staged
+// in LDS once (coalesced dword loads); each thread then walks its column down
+// the rows: horizontal tap sums of a new image row from two LDS dwords (dot4),
+// the 5x5 blob / checkerboard responses from a 5-row register window
+//   B = 7 I + 2 S3x3 - S5x5,   C = g(y-2) + g(y-1) - g(y+1) - g(y+2),
+//   g = (I(x+1) + I(x+2)) - (I(x-2) + I(x-1)),
+// packed as (B, C) 16-bit pairs, so the four classes' strict NMS runs as
+// packed max (B max, C max) and packed min (B min, C min) ops: horizontal
+// neighbour extrema over +-R columns through one LDS row buffer per response
+// row, vertical ones from a (2R+1)-row register window.  Features of an
+// output row are emitted per (row, tile, wave) segment in (x, class) order by
+// ballot ranks.  Responses outside the domain [2, w-3] x [2, h-3] only matter
+// when margin < R + 2 (DOM): then they enter the NMS as -inf / +inf.
+constexpr int kDW = 256;                  // response columns per workgroup
+constexpr int kDTH = 64;                  // output rows per tile
+constexpr int kImgDw = (kDW + 4) / 4;     // LDS dwords per staged image row (260 bytes)
 
-template <bool BORDER>
-__device__ inline int class_val(const short (*M)[kTW + 2 * kMaxNms], int sg, int yy, int xx, int gy0,
-                                int gx0, int w, int h) {
-    if (BORDER) {
-        const int gy = gy0 + yy, gx = gx0 + xx;
-        if (gy < 2 || gy >= h - 2 || gx < 2 || gx >= w - 2) return kNegInf;
-    }
-    return sg * (int)M[yy][xx];
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ inline s16x2 pk_max(s16x2 a, s16x2 b) { return __builtin_elementwise_max(a, b); }
+__device__ inline s16x2 pk_min(s16x2 a, s16x2 b) { return __builtin_elementwise_min(a, b); }
+__device__ inline uint32_t pk_bits(s16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ inline s16x2 pk_of(uint32_t v) { return __builtin_bit_cast(s16x2, v); }
+__device__ inline int mbcnt64(unsigned long long b) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
 }
 
 // image z of a batch = pair z / 2 (left, right); its feature set lives in the
@@ -111,145 +133,238 @@ __device__ inline FeatDev set_of(const FeatDev* sets, int ring, int pair0, int z
     return sets[2 * ((pair0 + z / 2) % ring) + (z & 1)];
 }
 
-__global__ __launch_bounds__(256) void svo_detect_kernel(const uint8_t* const* imgs, SvoDev p,
+template <int R, bool DOM>
+__global__ __launch_bounds__(256) void svo_detect_kernel(ImgSrc src, SvoDev p,
                                                          const FeatDev* __restrict__ sets, int ring,
-                                                         int pair0, int tiles, int list_cap) {
-    constexpr int RW = kTW + 2 * kMaxNms, RH = kTH + 2 * kMaxNms;   // response region
-    constexpr int IW = RW + 4, IH = RH + 4;                         // image region
-    __shared__ uint8_t s_img[IH][IW];
-    __shared__ short s_b[RH][RW];
-    __shared__ short s_c[RH][RW];
-    __shared__ short s_hi[RH][kTW];
-    __shared__ short s_he[RH][kTW];
-    const uint8_t* __restrict__ img = imgs[blockIdx.z];
+                                                         int pair0, int seg_cap) {
+    constexpr int OW = kDW - 2 * R;   // output columns per tile
+    constexpr int RR = kDTH + 2 * R;  // response rows
+    constexpr int IR = RR + 4;        // image rows
+    constexpr int NV = 2 * R + 1;
+    __shared__ uint32_t s_img[IR * kImgDw];
+    __shared__ uint32_t s_rx[2][kDW + 2 * R];                 // P (max view)
+    __shared__ uint32_t s_rn[DOM ? 2 : 1][DOM ? kDW + 2 * R : 1];  // P (min view, DOM only)
+    const uint8_t* __restrict__ img = src.at(blockIdx.z);
     const FeatDev F = set_of(sets, ring, pair0, blockIdx.z);
-    const int w = p.w, h = p.h, R = p.nms_n;
-    const int x0 = blockIdx.x * kTW, y0 = blockIdx.y * kTH;
-    const int tid = threadIdx.x;
-    // image region [x0 - R - 2, ...) x [y0 - R - 2, ...)
-    const int ix0 = x0 - R - 2, iy0 = y0 - R - 2;
-    const int iw = kTW + 2 * R + 4, ih = kTH + 2 * R + 4;
-    for (int i = tid; i < iw * ih; i += 256) {
-        const int yy = i / iw, xx = i - yy * iw;
-        const int gx = ix0 + xx, gy = iy0 + yy;
-        s_img[yy][xx] = (gx >= 0 && gx < w && gy >= 0 && gy < h) ? img[(size_t)gy * w + gx] : 0;
+    const int w = p.w, h = p.h;
+    const int x0 = blockIdx.x * OW, y0 = blockIdx.y * kDTH;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // ---- stage image rows y0-R-2 .. y0+kDTH+R+1, columns x0-R-2 .. x0-R+257:
+    // every load is issued unconditionally (clamped into the image buffer) before
+    // the first LDS store, then shifted into place / zeroed where it was clamped
+    {
+        constexpr int NI = IR * kImgDw, NL = (NI + kDW - 1) / kDW;
+        const long long n = (long long)w * h;
+        const int gx0 = x0 - R - 2, gy0 = y0 - R - 2;
+        uint32_t v[NL];
+#pragma unroll
+        for (int q = 0; q < NL; ++q) {
+            const int i = tid + q * kDW;
+            const int r = i / kImgDw, k = i - r * kImgDw;
+            const long long o = (long long)(gy0 + r) * w + gx0 + 4 * k;
+            const long long oc = min(max(o, 0LL), n - 4);
+            v[q] = *reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(
+                reinterpret_cast<uintptr_t>(img) + oc);
+        }
+#pragma unroll
+        for (int q = 0; q < NL; ++q) {
+            const int i = tid + q * kDW;
+            if (q == NL - 1 && i >= NI) break;
+            const int r = i / kImgDw, k = i - r * kImgDw;
+            const int gy = gy0 + r;
+            const long long o = (long long)gy * w + gx0 + 4 * k;
+            const long long d = o - min(max(o, 0LL), n - 4);
+            uint32_t x = v[q];
+            if (gy < 0 || gy >= h || d <= -4 || d >= 4) x = 0;
+            else if (d < 0) x <<= (uint32_t)(-8 * d);
+            else if (d > 0) x >>= (uint32_t)(8 * d);
+            s_img[i] = x;
+        }
     }
     __syncthreads();
-    // responses over [x0 - R, x0 + kTW + R) x [y0 - R, y0 + kTH + R)
-    const int rw = kTW + 2 * R, rh = kTH + 2 * R;
-    for (int i = tid; i < rw * rh; i += 256) {
-        const int yy = i / rw, xx = i - yy * rw;
-        int b = 0, c = 0;
+    const int x = x0 - R + tid;  // this thread's response column
+    const bool xin = tid >= R && tid < kDW - R && x >= p.margin && x < w - p.margin;
+    const int tau = p.tau;
+    const int sh = 8 * (tid & 3);
+    const uint32_t* srow = s_img + (tid >> 2);
+    const int tiles = gridDim.x;
+    int H5[5], H3[5], G[5], Cc[5];
+    s16x2 VX[NV], VN[NV], DP[R + 1], DX[R + 1], DN[R + 1];
+    for (int i = 0; i < IR; ++i) {
+        // taps a0..a4 = image columns x-2 .. x+2 of image row i
+        const uint32_t lo = srow[i * kImgDw], hi = srow[i * kImgDw + 1];
+        const uint32_t win = __builtin_amdgcn_alignbyte(hi, lo, tid & 3);  // a0..a3
+        const int a4 = (int)((hi >> sh) & 0xffu);
 #pragma unroll
-        for (int dy = -2; dy <= 2; ++dy)
-#pragma unroll
-            for (int dx = -2; dx <= 2; ++dx) {
-                const int a = s_img[yy + 2 + dy][xx + 2 + dx];
-                const int r = max(abs(dx), abs(dy));
-                b += r == 2 ? -a : (r == 1 ? a : 8 * a);
-                if (dx != 0 && dy != 0) c += ((dx < 0) == (dy < 0)) ? -a : a;
-            }
-        s_b[yy][xx] = (short)b;
-        s_c[yy][xx] = (short)c;
-    }
-    // tiles whose response region leaves the domain [2, w-3] x [2, h-3] mask it
-    const bool border = x0 - R < 2 || x0 + kTW + R > w - 2 || y0 - R < 2 || y0 + kTH + R > h - 2;
-    const int gy0 = y0 - R, gx0 = x0 - R;
-    const int lane = tid & 63, wave = tid >> 6;
-    int flags = 0;  // bit 8*s + 4*q + k: row slot s (row wave + 4s), column 2*lane + q, class k
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const short(*M)[RW] = k < 2 ? s_b : s_c;
-        const int sg = (k & 1) ? -1 : 1;
-        __syncthreads();  // responses ready / previous class done with s_hi, s_he
-        // row maxima of the class map at the tile's output columns
-        for (int i = tid; i < rh * kTW; i += 256) {
-            const int yy = i / kTW, xo = i - yy * kTW, lx = xo + R;
-            int mx = kNegInf;
-            if (border) {
-                for (int d = 1; d <= R; ++d)
-                    mx = max(mx, max(class_val<true>(M, sg, yy, lx - d, gy0, gx0, w, h),
-                                     class_val<true>(M, sg, yy, lx + d, gy0, gx0, w, h)));
-                s_he[yy][xo] = (short)mx;
-                s_hi[yy][xo] = (short)max(mx, class_val<true>(M, sg, yy, lx, gy0, gx0, w, h));
-            } else {
-                for (int d = 1; d <= R; ++d)
-                    mx = max(mx, max(sg * (int)M[yy][lx - d], sg * (int)M[yy][lx + d]));
-                s_he[yy][xo] = (short)mx;
-                s_hi[yy][xo] = (short)max(mx, sg * (int)M[yy][lx]);
+        for (int k = 0; k < 4; ++k) {
+            H5[k] = H5[k + 1];
+            H3[k] = H3[k + 1];
+            G[k] = G[k + 1];
+            Cc[k] = Cc[k + 1];
+        }
+        H5[4] = (int)__builtin_amdgcn_udot4(win, 0x01010101u, 0u, false) + a4;
+        H3[4] = (int)__builtin_amdgcn_udot4(win, 0x01010100u, 0u, false);
+        G[4] = ((int)(win >> 24) + a4) - (int)__builtin_amdgcn_udot4(win, 0x00000101u, 0u, false);
+        Cc[4] = (int)((win >> 16) & 0xffu);
+        if (i < 4) continue;
+        const int j = i - 4;  // response row: y = y0 - R + j
+        const int B = (7 * Cc[2] + 2 * ((H3[1] + H3[2]) + H3[3])) - ((((H5[0] + H5[1]) + H5[2]) + H5[3]) + H5[4]);
+        const int C = (G[0] + G[1]) - (G[3] + G[4]);
+        const s16x2 P = {(short)B, (short)C};
+        s16x2 PX = P, PN = P;
+        if (DOM) {
+            const int y = y0 - R + j;
+            if (x < 2 || x >= w - 2 || y < 2 || y >= h - 2) {
+                PX = s16x2{-32768, -32768};
+                PN = s16x2{32767, 32767};
             }
         }
+        uint32_t* bx = s_rx[j & 1];
+        bx[tid + R] = pk_bits(PX);
+        if (DOM) s_rn[j & 1][tid + R] = pk_bits(PN);
         __syncthreads();
+        s16x2 EX = s16x2{-32768, -32768}, EN = s16x2{32767, 32767};
 #pragma unroll
-        for (int sl = 0; sl < kTH / 4; ++sl) {
-            const int ry = wave + 4 * sl, y = y0 + ry;
-            if (y < p.margin || y >= h - p.margin) continue;
-            const int yy = ry + R;
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const int xo = 2 * lane + q, x = x0 + xo;
-                if (x < p.margin || x >= w - p.margin) continue;
-                const int r = sg * (int)M[yy][xo + R];
-                if (r <= p.tau) continue;
-                int nb = s_he[yy][xo];
-                for (int d = 1; d <= R; ++d) nb = max(nb, max((int)s_hi[yy - d][xo], (int)s_hi[yy + d][xo]));
-                if (r > nb) flags |= 1 << (8 * sl + 4 * q + k);
+        for (int d = 1; d <= R; ++d) {
+            const s16x2 l = pk_of(bx[tid + R - d]), r = pk_of(bx[tid + R + d]);
+            EX = pk_max(EX, pk_max(l, r));
+            if (DOM) {
+                const uint32_t* bn = s_rn[j & 1];
+                EN = pk_min(EN, pk_min(pk_of(bn[tid + R - d]), pk_of(bn[tid + R + d])));
+            } else {
+                EN = pk_min(EN, pk_min(l, r));
             }
         }
-    }
-    // ordered emission: per row, (x, class) ascending = lane order, then bit order
 #pragma unroll
-    for (int sl = 0; sl < kTH / 4; ++sl) {
-        const int y = y0 + wave + 4 * sl;
-        if (y >= h) break;
-        const int fl = (flags >> (8 * sl)) & 0xff;
-        const int cnt = __popc(fl);
-        int incl = cnt;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int t = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += t;
+        for (int k = 0; k < NV - 1; ++k) {
+            VX[k] = VX[k + 1];
+            VN[k] = VN[k + 1];
         }
-        const int total = __shfl(incl, 63, 64);
-        int pos = incl - cnt;
-        int* list = F.list + ((size_t)y * tiles + blockIdx.x) * list_cap;
-        for (int b = 0; b < 8; ++b)
-            if (fl & (1 << b)) {
-                if (pos < list_cap) list[pos] = (x0 + 2 * lane + (b >> 2)) | ((b & 3) << 16);
-                ++pos;
+        VX[NV - 1] = pk_max(EX, PX);
+        VN[NV - 1] = pk_min(EN, PN);
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            DP[k] = DP[k + 1];
+            DX[k] = DX[k + 1];
+            DN[k] = DN[k + 1];
+        }
+        DP[R] = P;
+        DX[R] = EX;
+        DN[R] = EN;
+        if (j < 2 * R) continue;
+        const int yc = y0 + j - 2 * R;  // centre (output) row
+        if (yc >= h) break;             // uniform: no later row of the tile is in the image
+        s16x2 NX = DX[0], NN = DN[0];
+#pragma unroll
+        for (int k = 0; k < NV; ++k)
+            if (k != R) {
+                NX = pk_max(NX, VX[k]);
+                NN = pk_min(NN, VN[k]);
             }
-        if (lane == 0) F.cnt[(size_t)y * tiles + blockIdx.x] = min(total, list_cap);
+        int flags = 0;
+        if (xin && yc >= p.margin && yc < h - p.margin) {
+            const int b = DP[0].x, c = DP[0].y;
+            flags = (b > tau && b > NX.x ? 1 : 0) | (-b > tau && b < NN.x ? 2 : 0) |
+                    (c > tau && c > NX.y ? 4 : 0) | (-c > tau && c < NN.y ? 8 : 0);
+        }
+        const unsigned long long q0 = __ballot(flags & 1), q1 = __ballot(flags & 2),
+                                 q2 = __ballot(flags & 4), q3 = __ballot(flags & 8);
+        const size_t seg = ((size_t)yc * tiles + blockIdx.x) * 4 + wave;
+        const int total = __popcll(q0) + __popcll(q1) + __popcll(q2) + __popcll(q3);
+        if (total) {
+            int pos = (mbcnt64(q0) + mbcnt64(q1)) + (mbcnt64(q2) + mbcnt64(q3));
+            int* list = F.list + seg * seg_cap;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (flags & (1 << k)) {
+                    if (pos < seg_cap) list[pos] = x | (k << 16);
+                    ++pos;
+                }
+        }
+        if (lane == 0) F.cnt[seg] = min(total, seg_cap);
     }
 }
 
-// row-major exclusive prefix over the (row, tile) candidate counts
+// exclusive block prefix (1024 threads): wave scans by shuffles + wave totals
+__device__ inline int block_excl_scan(int v, int* s_w, int& total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    int base = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int t = s_w[k];
+        base += k < wave ? t : 0;
+        tot += t;
+    }
+    __syncthreads();
+    total = tot;
+    return base + incl - v;
+}
+
+// Per image (1024 threads): row-major exclusive prefix over the segment
+// counts -> row index row0 and the features' u, v, class in that order; then
+// the band-major prefix over the same segments (band = segment column,
+// features past the capacity dropped) -> the column-band index.
 __global__ __launch_bounds__(1024) void svo_scan_kernel(SvoDev p, const FeatDev* __restrict__ sets, int ring,
-                                                        int pair0, int tiles) {
+                                                        int pair0, int segs, int seg_cap) {
     const FeatDev F = set_of(sets, ring, pair0, blockIdx.x);
-    __shared__ int s_part[1024];
-    const int n = p.h * tiles;
+    __shared__ int s_w[16];
+    const int h = p.h, n = h * segs;
     const int tid = threadIdx.x;
     const int per = (n + 1023) / 1024;
-    const int b = tid * per, e = min(b + per, n);
+    const int b = min(tid * per, n), e = min(b + per, n);
+    int* off = F.bcnt;  // [h][segs] row-major offset of each segment
     int s = 0;
     for (int i = b; i < e; ++i) s += F.cnt[i];
-    s_part[tid] = s;
-    __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {
-        const int t = tid >= o ? s_part[tid - o] : 0;
-        __syncthreads();
-        s_part[tid] += t;
-        __syncthreads();
-    }
-    int acc = s_part[tid] - s;
+    int total;
+    int acc = block_excl_scan(s, s_w, total);
     for (int i = b; i < e; ++i) {
-        F.off[i] = acc;
-        if (i % tiles == 0) F.row0[i / tiles] = min(acc, p.cap);
-        acc += F.cnt[i];
+        const int y = i / segs;
+        if (i == y * segs) F.row0[y] = min(acc, p.cap);
+        off[i] = acc;
+        const int c = F.cnt[i];
+        const int* list = F.list + (size_t)i * seg_cap;
+        for (int k = 0; k < c; ++k) {
+            const int o = acc + k;
+            if (o >= p.cap) break;
+            const int q = list[k];
+            F.u[o] = q & 0xffff;
+            F.v[o] = y;
+            F.c[o] = q >> 16;
+        }
+        acc += c;
     }
-    if (tid == 1023) {
-        F.row0[p.h] = min(s_part[1023], p.cap);
-        *F.n = min(s_part[1023], p.cap);
+    if (tid == 0) {
+        F.row0[h] = min(total, p.cap);
+        *F.n = min(total, p.cap);
+    }
+    __syncthreads();
+    // band-major: transposed index t = band * h + y
+    auto kept = [&](int i) { return min(max(p.cap - off[i], 0), F.cnt[i]); };
+    s = 0;
+    for (int t = b; t < e; ++t) {
+        const int bd = t / h, y = t - bd * h;
+        s += kept(y * segs + bd);
+    }
+    acc = block_excl_scan(s, s_w, total);
+    for (int t = b; t < e; ++t) {
+        const int bd = t / h, y = t - bd * h, i = y * segs + bd;
+        const int c = kept(i), o0 = off[i];
+        F.brow0[bd * (h + 1) + y] = acc;
+        const int* list = F.list + (size_t)i * seg_cap;
+        for (int k = 0; k < c; ++k) {
+            F.bidx[acc + k] = o0 + k;
+            F.buc[acc + k] = list[k];
+        }
+        acc += c;
+        if (y == h - 1) F.brow0[bd * (h + 1) + h] = acc;
     }
 }
 
@@ -260,32 +375,69 @@ __device__ inline int sobel_q(const uint8_t* I, int w, int x, int y, bool du) {
     return (d >> 3) + 128;
 }
 
-// 16 lanes per feature (lane j: sample offset j): descriptor + SoA arrays
-__global__ __launch_bounds__(256) void svo_describe_kernel(const uint8_t* const* imgs, SvoDev p,
+// 16 lanes per feature (lane j: sample offset j): the 32-byte descriptor;
+// grid (blocks per image, images), grid-stride over the image's features
+__global__ __launch_bounds__(256) void svo_describe_kernel(ImgSrc src, SvoDev p,
                                                            const FeatDev* __restrict__ sets, int ring,
-                                                           int pair0, int tiles, int list_cap) {
-    const uint8_t* __restrict__ img = imgs[blockIdx.z];
-    const FeatDev F = set_of(sets, ring, pair0, blockIdx.z);
-    const int y0 = blockIdx.y * kTH;
-    const int j = threadIdx.x & 15, slot = threadIdx.x >> 4;  // 16 features per pass
-    for (int ry = 0; ry < kTH; ++ry) {
-        const int y = y0 + ry;
-        if (y >= p.h) break;
-        const size_t rt = (size_t)y * tiles + blockIdx.x;
-        const int cnt = F.cnt[rt], base = F.off[rt];
-        for (int i = slot; i < cnt; i += 16) {
-            const int o = base + i;
-            if (o >= p.cap) break;
-            const int e = F.list[rt * list_cap + i];
-            const int x = e & 0xffff, k = e >> 16;
-            const int sx = x + c_p16[j][0], sy = y + c_p16[j][1];
-            F.d[(size_t)o * kDesc + j] = (uint8_t)sobel_q(img, p.w, sx, sy, true);
-            F.d[(size_t)o * kDesc + 16 + j] = (uint8_t)sobel_q(img, p.w, sx, sy, false);
-            if (j == 0) {
-                F.u[o] = x;
-                F.v[o] = y;
-                F.c[o] = k;
-            }
+                                                           int pair0) {
+    const uint8_t* __restrict__ img = src.at(blockIdx.y);
+    const FeatDev F = set_of(sets, ring, pair0, blockIdx.y);
+    const int n = *F.n;
+    const int j = threadIdx.x & 15;
+    for (int o = blockIdx.x * 16 + (threadIdx.x >> 4); o < n; o += gridDim.x * 16) {
+        const int sx = F.u[o] + c_p16[j][0], sy = F.v[o] + c_p16[j][1];
+        F.d[(size_t)o * kDesc + j] = (uint8_t)sobel_q(img, p.w, sx, sy, true);
+        F.d[(size_t)o * kDesc + 16 + j] = (uint8_t)sobel_q(img, p.w, sx, sy, false);
+    }
+}
+
+// Column-band index of a feature set (one workgroup of 1024 threads per
+// set): per (band, row) counts by a thread per row, a band-major exclusive
+// scan, then each row's features placed in index order.  The matching
+// searches then visit only the bands their column window overlaps.
+// Bands are the detect kernel's (tile, wave) column segments (wave w of tile
+// t: columns t*ow + 64w - n .. +63, clipped to the tile), so the feature pass
+// emits the band-major order directly (svo_scan_kernel); this kernel builds
+// the same index for feature sets uploaded by viso_svo_match.
+__device__ inline int band_of(int u, const SvoDev& p) {
+    const int t = u / p.ow;
+    return min(max(4 * t + ((u - t * p.ow + p.nms_n) >> 6), 0), p.nband - 1);
+}
+
+__global__ __launch_bounds__(1024) void svo_index_kernel(SvoDev p, const FeatDev* __restrict__ sets, int ring,
+                                                         int pair0) {
+    const FeatDev F = set_of(sets, ring, pair0, blockIdx.x);
+    __shared__ int s_w[16];
+    const int h = p.h, nb = p.nband, tid = threadIdx.x;
+    for (int y = tid; y < h; y += 1024) {
+        for (int b = 0; b < nb; ++b) F.bcnt[b * h + y] = 0;
+        const int e = F.row0[y + 1];
+        for (int i = F.row0[y]; i < e; ++i) ++F.bcnt[band_of(F.u[i], p) * h + y];
+    }
+    __syncthreads();
+    const int n = nb * h;
+    const int per = (n + 1023) / 1024;
+    const int b0 = min(tid * per, n), e0 = min(b0 + per, n);
+    int sum = 0;
+    for (int i = b0; i < e0; ++i) sum += F.bcnt[i];
+    int total;
+    int acc = block_excl_scan(sum, s_w, total);
+    for (int i = b0; i < e0; ++i) {
+        const int b = i / h, y = i - b * h;
+        F.brow0[b * (h + 1) + y] = acc;
+        acc += F.bcnt[i];
+        if (y == h - 1) F.brow0[b * (h + 1) + h] = acc;
+    }
+    __syncthreads();
+    for (int y = tid; y < h; y += 1024) {
+        const int r0 = F.row0[y], e = F.row0[y + 1];
+        for (int i = r0; i < e; ++i) {
+            const int u = F.u[i], b = band_of(u, p);
+            int rank = 0;
+            for (int k = r0; k < i; ++k) rank += band_of(F.u[k], p) == b ? 1 : 0;
+            const int pos = F.brow0[b * (h + 1) + y] + rank;
+            F.bidx[pos] = i;
+            F.buc[pos] = (u & 0xffff) | (F.c[i] << 16);
         }
     }
 }
@@ -310,21 +462,57 @@ __device__ inline unsigned wave_min_u32(unsigned v) {
     return v;
 }
 
-// best candidate in `S` for the query (u, v, class, desc): rows [v - dv, v + dv]
-// (a contiguous index range), u - du_hi <= u' <= u - du_lo; min SAD, ties ->
-// lowest index.  Wave-uniform arguments; returns -1 if none.
-__device__ int best_match(const FeatDev& S, int h, int u, int v, int c, uint4 q0, uint4 q1, int du_lo,
-                          int du_hi, int dv) {
-    const int lane = threadIdx.x & 63;
-    const int b = S.row0[max(v - dv, 0)], e = S.row0[min(v + dv, h - 1) + 1];
+// best candidate in `S` for the query (u, v, class, desc): rows [v - dv, v + dv],
+// u - du_hi <= u' <= u - du_lo; min SAD, ties -> lowest index.  The column
+// window's bands give one contiguous position range each (lanes 0..nq-1 load
+// the bounds, a wave scan concatenates them); lanes take 128 candidates per
+// step (two independent load chains in flight).  Wave-uniform arguments;
+// returns -1 if none.
+__device__ int best_match(const FeatDev& S, const SvoDev& p, int u, int v, int c, uint4 q0, uint4 q1,
+                          int du_lo, int du_hi, int dv) {
+    const int lane = threadIdx.x & 63, h = p.h;
+    const int va = max(v - dv, 0), vb = min(v + dv, h - 1);
+    const int ua = u - du_hi, ub = u - du_lo;
+    if (ub < 0) return -1;
+    const int ba = band_of(max(ua, 0), p), bq = band_of(ub, p);
+    const int nq = min(bq - ba + 1, 64);  // (a window over > 64 bands: disp_max > ~3900)
+    int s = 0, len = 0;
+    if (lane < nq) {
+        const int* r = S.brow0 + (size_t)(ba + lane) * (h + 1);
+        s = r[va];
+        len = r[vb + 1] - s;
+    }
+    int incl = len;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+    }
+    const int total = __shfl(incl, 63, 64);
+    const int excl = incl - len;
     unsigned best = 0xffffffffu;
-    for (int j = b + lane; j < e; j += 64) {
-        if (S.c[j] != c) continue;
-        const int dd = u - S.u[j];
-        if (dd < du_lo || dd > du_hi) continue;
-        const uint4* dj = reinterpret_cast<const uint4*>(S.d + (size_t)j * kDesc);
-        const int s = sad32(q0, q1, dj[0], dj[1]);
-        best = min(best, ((unsigned)s << 15) | (unsigned)j);
+    for (int k0 = 0; k0 < total; k0 += 128) {
+        const int ka = k0 + lane, kb = ka + 64;
+        int pa = 0, pb = 0;
+        for (int l = 0; l < nq; ++l) {
+            const int el = __builtin_amdgcn_readlane(excl, l), sl = __builtin_amdgcn_readlane(s, l);
+            if (ka >= el) pa = sl + (ka - el);
+            if (kb >= el) pb = sl + (kb - el);
+        }
+        const bool va_ = ka < total, vb_ = kb < total;
+        const int ea = va_ ? S.buc[pa] : -1, eb = vb_ ? S.buc[pb] : -1;
+        const int ja = va_ ? S.bidx[pa] : 0, jb = vb_ ? S.bidx[pb] : 0;
+        const int da = u - (ea & 0xffff), db = u - (eb & 0xffff);
+        const bool ma = va_ && (ea >> 16) == c && da >= du_lo && da <= du_hi;
+        const bool mb = vb_ && (eb >> 16) == c && db >= du_lo && db <= du_hi;
+        if (ma) {
+            const uint4* dj = reinterpret_cast<const uint4*>(S.d + (size_t)ja * kDesc);
+            best = min(best, ((unsigned)sad32(q0, q1, dj[0], dj[1]) << 15) | (unsigned)ja);
+        }
+        if (mb) {
+            const uint4* dj = reinterpret_cast<const uint4*>(S.d + (size_t)jb * kDesc);
+            best = min(best, ((unsigned)sad32(q0, q1, dj[0], dj[1]) << 15) | (unsigned)jb);
+        }
     }
     best = wave_min_u32(best);
     return best == 0xffffffffu ? -1 : (int)(best & 0x7fffu);
@@ -353,16 +541,16 @@ __global__ __launch_bounds__(256) void svo_circle_kernel(SvoDev p, PairArgs pa, 
         uint4 a, b;
         int4 res = make_int4(-1, -1, -1, 0);
         desc(L2, i2, a, b);
-        const int r2 = best_match(R2, h, L2.u[i2], L2.v[i2], c, a, b, 0, D, 1);
+        const int r2 = best_match(R2, p, L2.u[i2], L2.v[i2], c, a, b, 0, D, 1);
         if (r2 >= 0) {
             desc(R2, r2, a, b);
-            const int r1 = best_match(R1, h, R2.u[r2], R2.v[r2], c, a, b, -Rr, Rr, Rr);
+            const int r1 = best_match(R1, p, R2.u[r2], R2.v[r2], c, a, b, -Rr, Rr, Rr);
             if (r1 >= 0) {
                 desc(R1, r1, a, b);
-                const int l1 = best_match(L1, h, R1.u[r1], R1.v[r1], c, a, b, -D, 0, 1);
+                const int l1 = best_match(L1, p, R1.u[r1], R1.v[r1], c, a, b, -D, 0, 1);
                 if (l1 >= 0) {
                     desc(L1, l1, a, b);
-                    const int i2b = best_match(L2, h, L1.u[l1], L1.v[l1], c, a, b, -Rr, Rr, Rr);
+                    const int i2b = best_match(L2, p, L1.u[l1], L1.v[l1], c, a, b, -Rr, Rr, Rr);
                     if (i2b == i2 && L1.u[l1] - R1.u[r1] >= 1 && L2.u[i2] - R2.u[r2] >= 1)
                         res = make_int4(l1, r1, r2, 0);
                 }
@@ -567,29 +755,6 @@ __device__ inline double lane_tree(double v, int levels) {
 
 // ---------------------------------------------------------------- selection
 // ---- selection: bucketing (wave per bucket) and compaction
-// exclusive block prefix (1024 threads): wave scans by shuffles + wave totals
-__device__ inline int block_excl_scan(int v, int* s_w, int& total) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    int incl = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int t = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += t;
-    }
-    if (lane == 63) s_w[wave] = incl;
-    __syncthreads();
-    int base = 0, tot = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const int t = s_w[k];
-        base += k < wave ? t : 0;
-        tot += t;
-    }
-    __syncthreads();
-    total = tot;
-    return base + incl - v;
-}
-
 constexpr int kMaxBuckets = 4096;
 
 // Bucketing: wave per bucket.  The bucket's candidates are the current-left
@@ -888,31 +1053,83 @@ __global__ __launch_bounds__(1024) void svo_refine_kernel(SvoDev p, PairArgs pa,
     }
 }
 
-// Sequential tail of a batch (one thread): feature counts, and the camera
-// poses T_wc <- T_wc * Tr^-1 (Tr^-1 = [R^T, -R^T t]) in pair order.
-__global__ void svo_pose_kernel(PairArgs pa, int nb, double* __restrict__ pose,
-                                double* __restrict__ pose_log, long long max_poses) {
-    for (int b = 0; b < nb; ++b) {
+// Tail of a batch (one wave): feature counts, each pair's Tr^-1 = [R^T,
+// -R^T t] lane-parallel, then the camera poses T_wc <- T_wc * Tr^-1 composed
+// in pair order by lane 0 and written back lane-parallel.
+__global__ __launch_bounds__(64) void svo_pose_kernel(PairArgs pa, int nb, double* __restrict__ pose,
+                                                      double* __restrict__ pose_log, long long max_poses) {
+    __shared__ double s_inv[64][12];
+    __shared__ double s_pose[64][12];
+    __shared__ int s_ok[64];
+    const int b = threadIdx.x;
+    if (b < nb) {
         const long long fr = pa.frame0 + b;
         int* st = pa.stats + (size_t)b * 8;
         st[0] = *set_frame(pa, fr, 0).n;
         st[1] = *set_frame(pa, fr, 1).n;
+        int ok = 0;
         if (fr == 0) {
             for (int i = 2; i < 8; ++i) st[i] = 0;
-            for (int i = 0; i < 12; ++i) pose[i] = (i % 4 == 0 && i < 9) ? 1.0 : 0.0;
+            ok = -1;  // pose := identity
         } else if (st[5]) {
             const double* T = pa.motion + (size_t)b * 12;
-            double Ri[9], ti[3], Rn[9], tn[3];
+            double Ri[9];
             for (int i = 0; i < 3; ++i)
                 for (int j = 0; j < 3; ++j) Ri[3 * i + j] = T[3 * j + i];
-            for (int i = 0; i < 3; ++i) ti[i] = -((Ri[3 * i] * T[9] + Ri[3 * i + 1] * T[10]) + Ri[3 * i + 2] * T[11]);
-            mat3_mul_s(pose, Ri, Rn);
-            for (int i = 0; i < 3; ++i) tn[i] = ((pose[3 * i] * ti[0] + pose[3 * i + 1] * ti[1]) + pose[3 * i + 2] * ti[2]) + pose[9 + i];
-            for (int i = 0; i < 9; ++i) pose[i] = Rn[i];
-            for (int i = 0; i < 3; ++i) pose[9 + i] = tn[i];
+            for (int i = 0; i < 9; ++i) s_inv[b][i] = Ri[i];
+            for (int i = 0; i < 3; ++i)
+                s_inv[b][9 + i] = -((Ri[3 * i] * T[9] + Ri[3 * i + 1] * T[10]) + Ri[3 * i + 2] * T[11]);
+            ok = 1;
         }
-        double* out = pose_log + 12 * (fr < max_poses ? fr : max_poses - 1);
-        for (int i = 0; i < 12; ++i) out[i] = pose[i];
+        s_ok[b] = ok;
+    }
+    __syncthreads();
+    if (b == 0) {
+        double P[12];
+        for (int i = 0; i < 12; ++i) P[i] = pose[i];
+        for (int k = 0; k < nb; ++k) {
+            if (s_ok[k] < 0) {
+                for (int i = 0; i < 12; ++i) P[i] = (i % 4 == 0 && i < 9) ? 1.0 : 0.0;
+            } else if (s_ok[k] > 0) {
+                const double* Ri = s_inv[k];
+                const double* ti = s_inv[k] + 9;
+                double Rn[9], tn[3];
+                mat3_mul_s(P, Ri, Rn);
+                for (int i = 0; i < 3; ++i) tn[i] = ((P[3 * i] * ti[0] + P[3 * i + 1] * ti[1]) + P[3 * i + 2] * ti[2]) + P[9 + i];
+                for (int i = 0; i < 9; ++i) P[i] = Rn[i];
+                for (int i = 0; i < 3; ++i) P[9 + i] = tn[i];
+            }
+            for (int i = 0; i < 12; ++i) s_pose[k][i] = P[i];
+        }
+        for (int i = 0; i < 12; ++i) pose[i] = P[i];
+    }
+    __syncthreads();
+    for (int q = b; q < nb * 12; q += 64) {
+        const int k = q / 12, i = q - k * 12;
+        const long long fr = pa.frame0 + k;
+        if (fr < max_poses) pose_log[12 * fr + i] = s_pose[k][i];
+        else if (k == nb - 1) pose_log[12 * (max_poses - 1) + i] = s_pose[k][i];
+    }
+}
+
+template <int R>
+void launch_detect_r(bool dom, dim3 g, hipStream_t st, const ImgSrc& imgs, const SvoDev& d,
+                     const FeatDev* sets, int ring, int pair0, int seg_cap) {
+    if (dom) svo_detect_kernel<R, true><<<g, kDW, 0, st>>>(imgs, d, sets, ring, pair0, seg_cap);
+    else svo_detect_kernel<R, false><<<g, kDW, 0, st>>>(imgs, d, sets, ring, pair0, seg_cap);
+}
+
+void launch_detect(int R, bool dom, dim3 g, hipStream_t st, const ImgSrc& imgs, const SvoDev& d,
+                   const FeatDev* sets, int ring, int pair0, int seg_cap) {
+    switch (R) {
+        case 1: launch_detect_r<1>(dom, g, st, imgs, d, sets, ring, pair0, seg_cap); break;
+        case 2: launch_detect_r<2>(dom, g, st, imgs, d, sets, ring, pair0, seg_cap); break;
+        case 3: launch_detect_r<3>(dom, g, st, imgs, d, sets, ring, pair0, seg_cap); break;
+        case 4: launch_detect_r<4>(dom, g, st, imgs, d, sets, ring, pair0, seg_cap); break;
+        case 5: launch_detect_r<5>(dom, g, st, imgs, d, sets, ring, pair0, seg_cap); break;
+        case 6: launch_detect_r<6>(dom, g, st, imgs, d, sets, ring, pair0, seg_cap); break;
+        case 7: launch_detect_r<7>(dom, g, st, imgs, d, sets, ring, pair0, seg_cap); break;
+        default: launch_detect_r<8>(dom, g, st, imgs, d, sets, ring, pair0, seg_cap); break;
     }
 }
 
@@ -928,8 +1145,8 @@ struct viso_svo {
     viso_svo_params p{};
     int device = 0;
     hipStream_t stream = nullptr;
-    int tiles = 0;
-    int list_cap = 0;
+    int tiles = 0;          // detect tiles per row (256 - 2 nms_n output columns each)
+    int seg_cap = 0;        // candidates per (row, tile, wave) segment
     size_t frame = 0;       // pairs processed; pair k uses ring slot k % kRing
     int last_b = -1;        // batch slot of the last processed pair
     std::vector<FeatDev> sets;        // 2 * kRing (left, right of each slot)
@@ -940,10 +1157,11 @@ struct viso_svo {
     double* pose = nullptr;
     double* pose_log = nullptr;       // [max_poses][12]
     size_t max_poses = 0;
-    const uint8_t** imgs = nullptr;   // device table of 2 * kMaxPairBatch image pointers
-    hipEvent_t ev[2] = {nullptr, nullptr};
-    double detect_ms = 0.0;           // timing of the last batched feature pass (if timed)
-    int detect_pairs = 0;
+    // HIP-event timing of the batched feature passes while enabled: an event
+    // pair per batch, read (and summed) only when timing is queried
+    std::vector<hipEvent_t> tev;
+    int tev_n = 0;
+    int timed_pairs = 0;
     bool timed = false;
 
     SvoDev dev() const {
@@ -961,6 +1179,8 @@ struct viso_svo {
         d.iters = p.ransac_iters;
         d.gn_iters = p.gn_iters;
         d.cap = p.max_features;
+        d.ow = kDW - 2 * p.nms_n;
+        d.nband = 4 * ((p.width + d.ow - 1) / d.ow);
         d.fx = p.fx;
         d.fy = p.fy;
         d.cu = p.cu;
@@ -982,14 +1202,16 @@ struct viso_svo {
     }
     int init() {
         const int w = p.width, h = p.height, cap = p.max_features;
-        tiles = (w + kTW - 1) / kTW;
-        // strict NMS of radius n: same-class maxima of a row are > n apart
-        list_cap = std::min(kListCap, 4 * ((kTW + p.nms_n) / (p.nms_n + 1)));
+        tiles = (w + kDW - 2 * p.nms_n - 1) / (kDW - 2 * p.nms_n);
+        // strict NMS of radius n: same-class maxima of a row are > n apart, so
+        // a wave's 64 columns hold at most ceil(64 / (n + 1)) per class
+        seg_cap = 4 * ((64 + p.nms_n) / (p.nms_n + 1));
         sets.assign(2 * kRing, FeatDev{});
         for (FeatDev& f : sets)
             if (alloc(f.u, cap) || alloc(f.v, cap) || alloc(f.c, cap) || alloc(f.d, (size_t)cap * kDesc) ||
-                alloc(f.row0, (size_t)h + 1) || alloc(f.n, 1) || alloc(f.cnt, (size_t)h * tiles) ||
-                alloc(f.list, (size_t)h * tiles * list_cap) || alloc(f.off, (size_t)h * tiles))
+                alloc(f.row0, (size_t)h + 1) || alloc(f.n, 1) || alloc(f.cnt, (size_t)h * tiles * 4) ||
+                alloc(f.list, (size_t)h * tiles * 4 * seg_cap) || alloc(f.bidx, cap) || alloc(f.buc, cap) ||
+                alloc(f.brow0, (size_t)nband() * (h + 1)) || alloc(f.bcnt, (size_t)nband() * h))
                 return VISO_ERR_HIP;
         const int nbk = ((w + p.bucket_width - 1) / p.bucket_width) * ((h + p.bucket_height - 1) / p.bucket_height);
         const int P = kMaxPairBatch, it = std::max(1, p.ransac_iters);
@@ -1002,34 +1224,47 @@ struct viso_svo {
             alloc(pa.uv8, (size_t)P * pa.mcap * 8) || alloc(pa.n_sel, P) || alloc(pa.counts, (size_t)P * it) ||
             alloc(pa.models, (size_t)P * it * 12) || alloc(pa.sel, (size_t)P * pa.mcap) ||
             alloc(pa.inl, (size_t)P * pa.mcap) || alloc(pa.motion, (size_t)P * 12) || alloc(pa.stats, (size_t)P * 8) ||
-            alloc(pose, 12) || alloc(pose_log, max_poses * 12) || alloc(imgs, 2 * kMaxPairBatch))
+            alloc(pose, 12) || alloc(pose_log, max_poses * 12))
             return VISO_ERR_HIP;
         pa.sets = d_sets;
         VISO_HIP_CHECK(hipMemcpy(d_sets, sets.data(), sets.size() * sizeof(FeatDev), hipMemcpyHostToDevice));
-        VISO_HIP_CHECK(hipEventCreate(&ev[0]));
-        VISO_HIP_CHECK(hipEventCreate(&ev[1]));
         return VISO_OK;
     }
     void release() {
         for (void* q : allocs) (void)hipFree(q);
         allocs.clear();
-        for (hipEvent_t& e : ev)
+        for (hipEvent_t& e : tev)
             if (e) (void)hipEventDestroy(e);
+        tev.clear();
         if (stream) (void)hipStreamDestroy(stream);
         stream = nullptr;
     }
     FeatDev& set_at(size_t pair, int side) { return sets[2 * (pair % kRing) + side]; }
+    int nband() const { return 4 * tiles; }
 
-    // features of pairs frame .. frame + nb - 1 (image pointers in imgs[0 .. 2 nb))
-    int detect(int nb) {
+    // features of pairs frame .. frame + nb - 1
+    int detect(const ImgSrc& imgs, int nb) {
         const SvoDev d = dev();
         const int pair0 = (int)(frame % kRing);
-        const dim3 g(tiles, (p.height + kTH - 1) / kTH, 2 * nb);
-        if (timed) VISO_HIP_CHECK(hipEventRecord(ev[0], stream));
-        svo_detect_kernel<<<g, 256, 0, stream>>>(imgs, d, d_sets, kRing, pair0, tiles, list_cap);
-        svo_scan_kernel<<<2 * nb, 1024, 0, stream>>>(d, d_sets, kRing, pair0, tiles);
-        svo_describe_kernel<<<g, 256, 0, stream>>>(imgs, d, d_sets, kRing, pair0, tiles, list_cap);
-        if (timed) VISO_HIP_CHECK(hipEventRecord(ev[1], stream));
+        const dim3 g(tiles, (p.height + kDTH - 1) / kDTH, 2 * nb);
+        if (timed) {
+            while ((int)tev.size() < 2 * (tev_n + 1)) {
+                hipEvent_t e;
+                VISO_HIP_CHECK(hipEventCreate(&e));
+                tev.push_back(e);
+            }
+            VISO_HIP_CHECK(hipEventRecord(tev[2 * tev_n], stream));
+        }
+        // responses outside [2, w-3] x [2, h-3] reach the NMS only if margin < n + 2
+        const bool dom = p.margin < p.nms_n + 2;
+        launch_detect(p.nms_n, dom, g, stream, imgs, d, d_sets, kRing, pair0, seg_cap);
+        svo_scan_kernel<<<2 * nb, 1024, 0, stream>>>(d, d_sets, kRing, pair0, 4 * tiles, seg_cap);
+        svo_describe_kernel<<<dim3(16, 2 * nb), 256, 0, stream>>>(imgs, d, d_sets, kRing, pair0);
+        if (timed) {
+            VISO_HIP_CHECK(hipEventRecord(tev[2 * tev_n + 1], stream));
+            ++tev_n;
+            timed_pairs += nb;
+        }
         VISO_HIP_CHECK(hipGetLastError());
         return VISO_OK;
     }
@@ -1050,15 +1285,15 @@ struct viso_svo {
         VISO_HIP_CHECK(hipGetLastError());
         return VISO_OK;
     }
-    // a batch of nb pairs whose image pointers are in imgs: features, motions, poses
-    int batch(int nb) {
-        int rc = detect(nb);
+    // a batch of nb pairs: features, motions, poses
+    int batch(const ImgSrc& imgs, int nb) {
+        int rc = detect(imgs, nb);
         if (rc) return rc;
         const int b0 = frame == 0 ? 1 : 0;
         rc = estimate((long long)frame, b0, nb - b0);
         if (rc) return rc;
         pa.frame0 = (long long)frame;
-        svo_pose_kernel<<<1, 1, 0, stream>>>(pa, nb, pose, pose_log, (long long)max_poses);
+        svo_pose_kernel<<<1, 64, 0, stream>>>(pa, nb, pose, pose_log, (long long)max_poses);
         VISO_HIP_CHECK(hipGetLastError());
         frame += nb;
         last_b = nb - 1;
@@ -1157,9 +1392,7 @@ int viso_svo_process(viso_svo* s, const uint8_t* left, const uint8_t* right, con
     uint8_t* dr = s->img + (size_t)w * h;
     VISO_HIP_CHECK(hipMemcpy2DAsync(dl, w, left, stride, w, h, hipMemcpyHostToDevice, s->stream));
     VISO_HIP_CHECK(hipMemcpy2DAsync(dr, w, right, stride, w, h, hipMemcpyHostToDevice, s->stream));
-    const uint8_t* ptrs[2] = {dl, dr};
-    VISO_HIP_CHECK(hipMemcpyAsync(s->imgs, ptrs, sizeof(ptrs), hipMemcpyHostToDevice, s->stream));
-    int rc = s->batch(1);
+    int rc = s->batch(ImgSrc{dl, dr, 0}, 1);
     if (rc) return rc;
     VISO_HIP_CHECK(hipStreamSynchronize(s->stream));
     if (ok) {
@@ -1174,36 +1407,34 @@ int viso_svo_process_device(viso_svo* s, const uint8_t* left, const uint8_t* rig
                             int64_t pair_stride, int32_t stride) {
     if (!s || !left || !right || n < 0 || stride != s->p.width) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(s->device));
+    // batches of up to kMaxPairBatch pairs, queued back to back on the stream
+    // (image addresses are computed in the kernels: no per-batch host data)
     for (int i0 = 0; i0 < n; i0 += viso_svo::kMaxPairBatch) {
         const int nb = std::min(n - i0, viso_svo::kMaxPairBatch);
-        std::vector<const uint8_t*> ptrs((size_t)2 * nb);
-        for (int i = 0; i < nb; ++i) {
-            ptrs[(size_t)2 * i] = left + (i0 + i) * pair_stride;
-            ptrs[(size_t)2 * i + 1] = right + (i0 + i) * pair_stride;
-        }
-        VISO_HIP_CHECK(hipMemcpyAsync(s->imgs, ptrs.data(), ptrs.size() * sizeof(void*),
-                                      hipMemcpyHostToDevice, s->stream));
-        // one batched feature pass over the nb pairs, then their motions side by side
-        const int rc = s->batch(nb);
+        const int rc = s->batch(ImgSrc{left + (long long)i0 * pair_stride, right + (long long)i0 * pair_stride,
+                                       (long long)pair_stride}, nb);
         if (rc) return rc;
-        if (s->timed) {
-            VISO_HIP_CHECK(hipEventSynchronize(s->ev[1]));
-            float ms = 0.f;
-            VISO_HIP_CHECK(hipEventElapsedTime(&ms, s->ev[0], s->ev[1]));
-            s->detect_ms = ms;
-            s->detect_pairs = nb;
-        }
-        // the pointer table is reused by the next batch
-        VISO_HIP_CHECK(hipStreamSynchronize(s->stream));
     }
     return VISO_OK;
 }
 
-int viso_svo_timing(viso_svo* s, int32_t enable, double* last_feature_pass_ms, int32_t* pairs) {
+int viso_svo_timing(viso_svo* s, int32_t enable, double* feature_pass_ms, int32_t* pairs) {
     if (!s) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipSetDevice(s->device));
+    double ms = 0.0;
+    if (s->tev_n > 0) {
+        VISO_HIP_CHECK(hipStreamSynchronize(s->stream));
+        for (int k = 0; k < s->tev_n; ++k) {
+            float m = 0.f;
+            VISO_HIP_CHECK(hipEventElapsedTime(&m, s->tev[2 * k], s->tev[2 * k + 1]));
+            ms += m;
+        }
+    }
+    if (feature_pass_ms) *feature_pass_ms = ms;
+    if (pairs) *pairs = s->timed_pairs;
+    s->tev_n = 0;
+    s->timed_pairs = 0;
     s->timed = enable != 0;
-    if (last_feature_pass_ms) *last_feature_pass_ms = s->detect_ms;
-    if (pairs) *pairs = s->detect_pairs;
     return VISO_OK;
 }
 
@@ -1266,10 +1497,7 @@ int viso_svo_features(viso_svo* s, const uint8_t* img, int32_t width, int32_t he
     VISO_HIP_CHECK(hipSetDevice(s->device));
     const size_t bytes = (size_t)width * height;
     VISO_HIP_CHECK(hipMemcpyAsync(s->img, img, bytes, hipMemcpyHostToDevice, s->stream));
-    VISO_HIP_CHECK(hipMemcpyAsync(s->img + bytes, img, bytes, hipMemcpyHostToDevice, s->stream));
-    const uint8_t* ptrs[2] = {s->img, s->img + bytes};
-    VISO_HIP_CHECK(hipMemcpyAsync(s->imgs, ptrs, sizeof(ptrs), hipMemcpyHostToDevice, s->stream));
-    int rc = s->detect(1);  // into the slot of pair `frame` (not advanced)
+    int rc = s->detect(ImgSrc{s->img, s->img, 0}, 1);  // into the slot of pair `frame` (not advanced)
     if (rc) return rc;
     VISO_HIP_CHECK(hipStreamSynchronize(s->stream));
     const FeatDev F = s->set_at(s->frame, 0);
@@ -1304,7 +1532,7 @@ int viso_svo_match(viso_svo* s, const int32_t* const* u4, const int32_t* const* 
         FeatDev& F = *F4[k];
         std::vector<int> row0((size_t)h + 1, m);
         for (int i = m - 1; i >= 0; --i) {
-            if (v4[k][i] < 0 || v4[k][i] >= h) return VISO_ERR_ARG;
+            if (v4[k][i] < 0 || v4[k][i] >= h || u4[k][i] < 0 || u4[k][i] >= s->p.width) return VISO_ERR_ARG;
             row0[(size_t)v4[k][i]] = i;
         }
         for (int y = h - 1; y >= 0; --y) row0[(size_t)y] = std::min(row0[(size_t)y], row0[(size_t)y + 1]);
@@ -1318,6 +1546,7 @@ int viso_svo_match(viso_svo* s, const int32_t* const* u4, const int32_t* const* 
         VISO_HIP_CHECK(hipMemcpy(F.n, &m, sizeof(int), hipMemcpyHostToDevice));
     }
     const SvoDev d = s->dev();
+    svo_index_kernel<<<4, 1024, 0, s->stream>>>(d, s->d_sets, viso_svo::kRing, (int)(p1 % viso_svo::kRing));
     PairArgs pa = s->pa;
     pa.frame0 = (long long)p2;  // slot 0 = pair p2 (previous: p1)
     svo_circle_kernel<<<dim3(1024, 1), 256, 0, s->stream>>>(d, pa, 0);

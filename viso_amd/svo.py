@@ -97,7 +97,8 @@ class VisualOdometryStereo:
         _lib.call("viso_svo_synchronize", self.h)
 
     def timing(self, enable: bool = True):
-        """HIP-event timing of the batched feature pass -> (last batch ms, pairs)."""
+        """HIP-event timing of the batched feature pass -> (ms, pairs) summed
+        over the batches since the previous call; then enable / disable."""
         ms = ctypes.c_double(0.0)
         n = ctypes.c_int32(0)
         _lib.call("viso_svo_timing", self.h, int(enable), ctypes.byref(ms), ctypes.byref(n))
