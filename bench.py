@@ -62,6 +62,8 @@ def parse():
     ap.add_argument("--no-svo", action="store_true", help="skip the stereo-VO side measurement")
     ap.add_argument("--svo-cpu-pairs", type=int, default=12,
                     help="pairs of the stereo-VO CPU spec timed for its baseline (0 = skip)")
+    ap.add_argument("--rig-steps", type=int, default=64,
+                    help="timesteps of the 4-camera rig measurement (configs[4]; 0 = skip)")
     return ap.parse_args()
 
 
@@ -113,6 +115,54 @@ def measure_svo(args, seq, left, right, d_left, d_right, W, H, log):
         out["speedup_vs_cpu"] = round(out["pairs_per_s"] / out["cpu_baseline"]["value"], 1)
         out["parity_vs_oracle"] = {"pairs": int(m),
                                    "pose_max_abs_diff": float(np.abs(gp - op).max()) if len(gp) == len(op) else None}
+    return out
+
+
+def measure_rig(args, W, H, log):
+    """BASELINE.json configs[4]: a rig of 4 stereo cameras per timestep, one
+    shared RANSAC + Gauss-Newton rig motion; timesteps/s with the frames
+    resident in HBM, and the CPU spec on a bounded sample."""
+    import torch
+
+    from viso_amd import svo
+    from viso_amd.synth import RigSequence
+
+    nc, n = 4, args.rig_steps
+    seq = RigSequence(W, H, seed=2000, n_cams=nc)
+    frames = [seq.frame(f) for f in range(n)]
+    L = [torch.from_numpy(np.stack([fr[0][c] for fr in frames])).cuda() for c in range(nc)]
+    R = [torch.from_numpy(np.stack([fr[1][c] for fr in frames])).cuda() for c in range(nc)]
+    E = seq.extrinsics()
+    p = svo.default_params(W, H, *seq.K, seq.p.baseline)
+    lp, rp = [t.data_ptr() for t in L], [t.data_ptr() for t in R]
+    vo = svo.VisualOdometryStereoRig(p, E)
+    vo.process_device(lp, rp, min(8, n), W * H)  # warm-up
+    vo.synchronize()
+    vo = svo.VisualOdometryStereoRig(p, E)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    vo.process_device(lp, rp, n, W * H)
+    vo.synchronize()
+    dt = time.perf_counter() - t0
+    out = {"workload": f"configs[4]: {nc} synthetic {W}x{H} stereo cameras per timestep (rig), "
+                       "shared RANSAC + Gauss-Newton rig motion", "timesteps": n,
+           "timesteps_per_s": round(n / dt, 1), "camera_pairs_per_s": round(nc * n / dt, 1),
+           "last_step_stats": vo.stats().tolist()}
+    log(f"[rig] {out['timesteps_per_s']} timesteps/s")
+    if not args.no_cpu and args.svo_cpu_pairs > 0:
+        from tests import oracle_lib
+        m = min(max(2, args.svo_cpu_pairs // nc), n)
+        S = oracle_lib.SvoRigSequence(oracle_lib.svo_params(W, H, *seq.K, seq.p.baseline), E)
+        t0 = time.perf_counter()
+        for f in range(m):
+            S.process(*frames[f])
+        cpu_s = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(m / cpu_s, 3), "unit": "timesteps/s", "cores": 1, "kind": "port",
+                               "sample": f"tests/oracle_lib.SvoRigSequence (oracle/oracle_svo.cpp), single "
+                                         f"thread, timesteps 0-{m - 1}"}
+        gp = vo.poses[:m]
+        out["parity_vs_oracle"] = {"timesteps": int(m),
+                                   "pose_max_abs_diff": float(np.abs(gp - np.array(S.poses[:m])).max())}
     return out
 
 
@@ -251,6 +301,8 @@ def main():
     stereo_vo = None
     if rank == 0 and not args.no_svo:
         stereo_vo = measure_svo(args, seq, left, right, d_left, d_right, W, H, log)
+        if args.rig_steps > 0:
+            stereo_vo["rig"] = measure_rig(args, W, H, log)
 
     # ---------------------------------------------------------- CPU baseline + parity
     cpu = None

@@ -31,6 +31,7 @@ extern "C" {
 #define VISO_SVO_CORNER_MAX 2
 #define VISO_SVO_CORNER_MIN 3
 #define VISO_SVO_DESC_BYTES 32
+#define VISO_SVO_MAX_CAMS 8      /* stereo cameras of a rig */
 
 typedef struct viso_svo_params {
     int32_t width, height;       /* rectified grey pair size (continuous rows) */
@@ -94,6 +95,28 @@ int viso_svo_get_poses(viso_svo* s, double* poses12, size_t cap, size_t* n);
  * per match {u_l1, v_l1, u_r1, v_r1, u_l2, v_l2, u_r2, v_r2} and its
  * inlier flag. */
 int viso_svo_get_matches(viso_svo* s, int32_t* uv8, uint8_t* inlier, size_t cap, size_t* n);
+
+/* ---- multi-camera rig (BASELINE.json configs[4]) -----------------------
+ * n_cams rigidly mounted stereo cameras with identical parameters p;
+ * extrinsics (n_cams x 12 doubles, R row-major + t) map the rig frame to
+ * camera c's left camera: P_c = R P_rig + t.  Per timestep every camera's
+ * pair runs the stereo path (features, circular matching, bucketing); one
+ * RANSAC + Gauss-Newton estimates the rig motion from the matches of all
+ * cameras (camera order, then left order), residuals taken through each
+ * match's extrinsic.  get_motion / get_poses then report the rig's motion and
+ * poses, get_stats sums over the cameras.  viso_svo_create is this with
+ * n_cams = 1 (no extrinsic); the stage entry points below need n_cams = 1. */
+int viso_svo_rig_create(const viso_svo_params* p, int32_t n_cams, const double* extrinsics, int device,
+                        viso_svo** out);
+/* one timestep: lefts[c], rights[c] = host images of camera c */
+int viso_svo_rig_process(viso_svo* s, const uint8_t* const* lefts, const uint8_t* const* rights,
+                         const int32_t dims[3], int32_t* ok);
+/* n timesteps already in HBM: camera c's pairs at lefts[c] / rights[c]
+ * (device pointers), consecutive timesteps pair_stride bytes apart */
+int viso_svo_rig_process_device(viso_svo* s, const uint8_t* const* lefts, const uint8_t* const* rights,
+                                int32_t n, int64_t pair_stride, int32_t stride);
+/* camera of each match returned by viso_svo_get_matches */
+int viso_svo_get_match_cams(viso_svo* s, uint8_t* cams, size_t cap, size_t* n);
 
 /* ---- stage entry points (parity tests) ---------------------------------
  * Features of one image: row-major (v, then u, then class); n <= cap. */

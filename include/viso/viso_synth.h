@@ -37,6 +37,15 @@ int viso_synth_pose(const viso_synth_params* p, int frame, int cam, double* Rt12
 /* Render one grey frame (width x height, continuous rows). */
 int viso_synth_render(const viso_synth_params* p, int frame, int cam, uint8_t* out, int threads);
 
+/* Multi-camera rig (BASELINE.json configs[4]): n_cams stereo cameras fixed on
+ * the trajectory of viso_synth_pose(frame, 0) (the rig frame), camera c yawed
+ * by (c - (n-1)/2) * 20 deg and offset (c - (n-1)/2) * 0.35 m along the rig x
+ * axis.  Extrinsic E_c: rig -> camera c (left), 12 doubles (R row-major, t). */
+int viso_synth_rig_extrinsic(int cam, int n_cams, double* E12);
+int viso_synth_rig_pose(const viso_synth_params* p, int frame, int n_cams, int cam, int side, double* Rt12);
+int viso_synth_rig_render(const viso_synth_params* p, int frame, int n_cams, int cam, int side, uint8_t* out,
+                          int threads);
+
 #ifdef __cplusplus
 }
 #endif

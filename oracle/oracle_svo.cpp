@@ -158,6 +158,8 @@ int best_match(const FeatSet& dst, int h, int u, int v, int c, const uint8_t* d,
 struct Obs {
     double X, Y, Z;         // point in camera t-1
     double uL, vL, uR, vR;  // observations in the current pair
+    const double* E;        // rig: extrinsic of the match's camera (rig -> camera), else null
+    double Xr[3];           // rig: the point in the rig frame t-1, E^-1 (X, Y, Z)
 };
 
 Obs make_obs(const int32_t* m, const viso_svo_params& p) {
@@ -170,6 +172,20 @@ Obs make_obs(const int32_t* m, const viso_svo_params& p) {
     o.vL = (double)m[5];
     o.uR = (double)m[6];
     o.vR = (double)m[7];
+    o.E = nullptr;
+    o.Xr[0] = o.Xr[1] = o.Xr[2] = 0.0;
+    return o;
+}
+
+// Multi-camera rig (BASELINE.json configs[4]): camera c sees the rig frame
+// through its extrinsic E_c = (Re, te), P_c = Re P_rig + te (12 doubles, Re
+// row-major).  The motion (R, t) is the rig's; a match of camera c predicts
+// Q = R Xr + t (rig frame t), P = Re Q + te (camera c, t).
+Obs make_obs_rig(const int32_t* m, const double* E, const viso_svo_params& p) {
+    Obs o = make_obs(m, p);
+    o.E = E;
+    const double d0 = o.X - E[9], d1 = o.Y - E[10], d2 = o.Z - E[11];
+    for (int k = 0; k < 3; ++k) o.Xr[k] = ((E[k] * d0 + E[3 + k] * d1) + E[6 + k] * d2);
     return o;
 }
 
@@ -204,6 +220,62 @@ void residual_rows(const double* P, const Obs& o, const viso_svo_params& p, doub
         J[r][3] = gx;
         J[r][4] = gy;
         J[r][5] = gz;
+    }
+}
+
+// rig form of transform + residual_rows: Q = R Xr + t, P = Re Q + te; the
+// residual gradients g (w.r.t. P) are taken to the rig frame, g' = Re^T g,
+// and J = [Q x g', g'] (left perturbation of the rig motion)
+void rig_point(const double* R, const double* t, const Obs& o, double* Q, double* P) {
+    Q[0] = ((R[0] * o.Xr[0] + R[1] * o.Xr[1]) + R[2] * o.Xr[2]) + t[0];
+    Q[1] = ((R[3] * o.Xr[0] + R[4] * o.Xr[1]) + R[5] * o.Xr[2]) + t[1];
+    Q[2] = ((R[6] * o.Xr[0] + R[7] * o.Xr[1]) + R[8] * o.Xr[2]) + t[2];
+    const double* E = o.E;
+    P[0] = ((E[0] * Q[0] + E[1] * Q[1]) + E[2] * Q[2]) + E[9];
+    P[1] = ((E[3] * Q[0] + E[4] * Q[1]) + E[5] * Q[2]) + E[10];
+    P[2] = ((E[6] * Q[0] + E[7] * Q[1]) + E[8] * Q[2]) + E[11];
+}
+
+void residual_rows_rig(const double* P, const double* Q, const Obs& o, const viso_svo_params& p, double e[4],
+                       double J[4][6]) {
+    const double iz = 1.0 / P[2];
+    const double iz2 = iz * iz;
+    const double xr = P[0] - p.base;
+    const double pu = ((p.fx * P[0]) * iz) + p.cu;
+    const double pv = ((p.fy * P[1]) * iz) + p.cv;
+    const double pr = ((p.fx * xr) * iz) + p.cu;
+    e[0] = o.uL - pu;
+    e[1] = o.vL - pv;
+    e[2] = o.uR - pr;
+    e[3] = o.vR - pv;
+    const double g[4][3] = {{p.fx * iz, 0.0, -(p.fx * P[0]) * iz2},
+                            {0.0, p.fy * iz, -(p.fy * P[1]) * iz2},
+                            {p.fx * iz, 0.0, -(p.fx * xr) * iz2},
+                            {0.0, p.fy * iz, -(p.fy * P[1]) * iz2}};
+    const double* E = o.E;
+    for (int r = 0; r < 4; ++r) {
+        const double gx = (E[0] * g[r][0] + E[3] * g[r][1]) + E[6] * g[r][2];
+        const double gy = (E[1] * g[r][0] + E[4] * g[r][1]) + E[7] * g[r][2];
+        const double gz = (E[2] * g[r][0] + E[5] * g[r][1]) + E[8] * g[r][2];
+        J[r][0] = gz * Q[1] - gy * Q[2];
+        J[r][1] = gx * Q[2] - gz * Q[0];
+        J[r][2] = gy * Q[0] - gx * Q[1];
+        J[r][3] = gx;
+        J[r][4] = gy;
+        J[r][5] = gz;
+    }
+}
+
+// residuals + Jacobian of one match under (R, t), mono or rig; P = camera point
+void match_rows(const double* R, const double* t, const Obs& o, const viso_svo_params& p, double* P, double e[4],
+                double J[4][6]) {
+    if (o.E) {
+        double Q[3];
+        rig_point(R, t, o, Q, P);
+        residual_rows_rig(P, Q, o, p, e, J);
+    } else {
+        transform(R, t, o, P);
+        residual_rows(P, o, p, e, J);
     }
 }
 
@@ -290,8 +362,7 @@ bool gauss_newton(const std::vector<Obs>& obs, const std::vector<uint8_t>& sel,
                 continue;
             }
             double P[3], e[4], J[4][6];
-            transform(R, t, obs[(size_t)i], P);
-            residual_rows(P, obs[(size_t)i], p, e, J);
+            match_rows(R, t, obs[(size_t)i], p, P, e, J);
             match_sums(e, J, s);
         }
         double S[28], x[6];
@@ -310,9 +381,16 @@ bool gauss_newton(const std::vector<Obs>& obs, const std::vector<uint8_t>& sel,
 
 bool is_inlier(const double* R, const double* t, const Obs& o, const viso_svo_params& p) {
     double P[3], e[4], J[4][6];
-    transform(R, t, o, P);
-    if (!(P[2] > 0.0)) return false;
-    residual_rows(P, o, p, e, J);
+    if (o.E) {
+        double Q[3];
+        rig_point(R, t, o, Q, P);
+        if (!(P[2] > 0.0)) return false;
+        residual_rows_rig(P, Q, o, p, e, J);
+    } else {
+        transform(R, t, o, P);
+        if (!(P[2] > 0.0)) return false;
+        residual_rows(P, o, p, e, J);
+    }
     const double d2 = ((e[0] * e[0] + e[1] * e[1]) + e[2] * e[2]) + e[3] * e[3];
     return d2 < p.inlier_threshold * p.inlier_threshold;
 }
@@ -331,13 +409,16 @@ bool sample3(uint64_t seed, int h, int M, int* idx) {
     return got == 3;
 }
 
+// cams / extr: the rig form (match i seen by camera cams[i], extrinsics
+// extr[12 c ..]); null for one stereo camera
 int estimate(const int32_t* uv8, int M, int64_t frame, const viso_svo_params& p, double* motion,
-             uint8_t* inlier) {
+             uint8_t* inlier, const int32_t* cams = nullptr, const double* extr = nullptr) {
     for (int i = 0; i < 12; ++i) motion[i] = (i < 9) ? kI3[i] : 0.0;
     for (int i = 0; i < M; ++i) inlier[i] = 0;
     if (M < 6) return -1;
     std::vector<Obs> obs((size_t)M);
-    for (int i = 0; i < M; ++i) obs[(size_t)i] = make_obs(uv8 + 8 * i, p);
+    for (int i = 0; i < M; ++i)
+        obs[(size_t)i] = cams ? make_obs_rig(uv8 + 8 * i, extr + 12 * cams[i], p) : make_obs(uv8 + 8 * i, p);
     const uint64_t seed = mix64(p.seed ^ (uint64_t)frame);
     int best_h = -1, best_cnt = -1;
     double bR[9], bt[3];
@@ -474,6 +555,12 @@ int oracle_svo_bucket(const int32_t* uv8, int n, int w, int h, const viso_svo_pa
 int oracle_svo_estimate(const int32_t* uv8, int n, int64_t frame, const viso_svo_params* p,
                         double* motion12, uint8_t* inlier) {
     return estimate(uv8, n, frame, *p, motion12, inlier);
+}
+
+// Rig motion from the matches of all cameras (camera of match i: cams[i]).
+int oracle_svo_rig_estimate(const int32_t* uv8, const int32_t* cams, int n, int64_t frame,
+                            const viso_svo_params* p, const double* extr, double* motion12, uint8_t* inlier) {
+    return estimate(uv8, n, frame, *p, motion12, inlier, cams, extr);
 }
 
 }  // extern "C"

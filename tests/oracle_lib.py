@@ -61,6 +61,7 @@ SIG = {
     "oracle_svo_match": ([_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _i], _i),
     "oracle_svo_bucket": ([_vp, _i, _i, _i, _vp, _vp], _i),
     "oracle_svo_estimate": ([_vp, _i, ctypes.c_int64, _vp, _vp, _vp], _i),
+    "oracle_svo_rig_estimate": ([_vp, _vp, _i, ctypes.c_int64, _vp, _vp, _vp, _vp], _i),
 }
 
 _lib = None
@@ -470,5 +471,72 @@ class SvoSequence:
             self.poses.append(np.concatenate([self.pose[:3, :3].ravel(), self.pose[:3, 3]]))
         self.stats = [len(fl), len(fr), n_match, n_bucket, n_inl, int(ok)]
         self.prev = (fl, fr)
+        self.frame += 1
+        return ok
+
+
+def svo_rig_estimate(uv8: np.ndarray, cams: np.ndarray, frame: int, p: SvoParams, extr: np.ndarray):
+    """Rig motion from the matches of all cameras -> (motion12, inlier mask, n or -1)."""
+    lib = load()
+    uv8 = np.ascontiguousarray(uv8, np.int32)
+    cams = np.ascontiguousarray(cams, np.int32)
+    extr = np.ascontiguousarray(extr, np.float64)
+    motion = np.zeros(12, np.float64)
+    inl = np.zeros(max(1, len(uv8)), np.uint8)
+    n = lib.oracle_svo_rig_estimate(ptr(uv8), ptr(cams), len(uv8), frame, ctypes.byref(p), ptr(extr),
+                                    ptr(motion), ptr(inl))
+    return motion, inl[:len(uv8)].astype(bool), n
+
+
+class SvoRigSequence:
+    """Multi-camera rig (BASELINE.json configs[4]) on the CPU: per camera the
+    SVO features, circular matching and bucketing; one RANSAC + Gauss-Newton
+    over the matches of all cameras (camera order, then left order) for the
+    rig motion; rig poses accumulate T_wr = T_wr * Tr^-1."""
+
+    def __init__(self, p: SvoParams, extr: np.ndarray):
+        self.p = p
+        self.extr = np.ascontiguousarray(extr, np.float64)
+        self.n_cams = len(extr)
+        self.prev = None
+        self.frame = 0
+        self.pose = np.eye(4)
+        self.poses = [np.concatenate([self.pose[:3, :3].ravel(), self.pose[:3, 3]])]
+        self.motion = None
+        self.stats = None
+
+    def process(self, lefts, rights) -> bool:
+        feats = [(svo_features(l, self.p), svo_features(r, self.p)) for l, r in zip(lefts, rights)]
+        ok = False
+        self.motion = np.array([1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0], np.float64)
+        n_match = n_bucket = n_inl = 0
+        if self.prev is not None:
+            sels, cams = [], []
+            h, w = lefts[0].shape
+            for c in range(self.n_cams):
+                f4 = [self.prev[c][0], self.prev[c][1], feats[c][0], feats[c][1]]
+                quad = svo_match(f4, h, self.p)
+                uv8 = svo_uv8(f4, quad)
+                keep = svo_bucket(uv8, w, h, self.p)
+                n_match += len(uv8)
+                sels.append(uv8[keep])
+                cams.append(np.full(int(keep.sum()), c, np.int32))
+            sel = np.concatenate(sels).reshape(-1, 8)
+            cam = np.concatenate(cams)
+            n_bucket = len(sel)
+            motion, inl, n = svo_rig_estimate(sel, cam, self.frame, self.p, self.extr)
+            self.matches, self.cams, self.inliers = sel, cam, inl
+            if n >= 6:
+                ok = True
+                n_inl = n
+                self.motion = motion
+                T = np.eye(4)
+                T[:3, :3] = motion[:9].reshape(3, 3)
+                T[:3, 3] = motion[9:]
+                self.pose = self.pose @ np.linalg.inv(T)
+            self.poses.append(np.concatenate([self.pose[:3, :3].ravel(), self.pose[:3, 3]]))
+        self.stats = [sum(len(f[0]) for f in feats), sum(len(f[1]) for f in feats), n_match, n_bucket,
+                      n_inl, int(ok)]
+        self.prev = feats
         self.frame += 1
         return ok

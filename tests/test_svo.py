@@ -284,3 +284,101 @@ def test_gpu_batched_device_path_matches_sequential(synth_frames):
     assert np.array_equal(vb.getMotion(), vs.getMotion())
     ub, ib = vb.getMatches()
     assert np.array_equal(ub, S.matches) and np.array_equal(ib, S.inliers)
+
+
+@pytest.mark.gpu
+def test_gpu_config3_1080p_2048_hypotheses():
+    """BASELINE.json configs[2]: synthetic 1920x1080 stereo, ~8k features per
+    image, 2048 RANSAC hypotheses — per-pair stats, matches, inlier masks and
+    motions identical to the spec, batched device path == per-pair path."""
+    import torch
+
+    from viso_amd import svo
+    from viso_amd.synth import Sequence
+    W, H, n = 1920, 1080, 4
+    seq = Sequence(W, H, seed=1000)
+    frames = [seq.frame(f) for f in range(n)]
+    kw = dict(ransac_iters=2048)
+    p = svo.default_params(W, H, *seq.K, seq.p.baseline, **kw)
+    vo = svo.VisualOdometryStereo(p)
+    S = ol.SvoSequence(ol.svo_params(W, H, *seq.K, seq.p.baseline, **kw))
+    for f, (l, r) in enumerate(frames):
+        assert vo.process(l, r) == S.process(l, r)
+        st = vo.stats().tolist()
+        assert st == S.stats
+        assert min(st[0], st[1]) > 4000
+        if f > 0:
+            assert st[5] == 1
+            uv8, inl = vo.getMatches()
+            assert np.array_equal(uv8, S.matches) and np.array_equal(inl, S.inliers)
+    assert np.allclose(vo.poses, np.array(S.poses), rtol=0, atol=1e-9)
+    L = torch.from_numpy(np.stack([f[0] for f in frames])).cuda()
+    R = torch.from_numpy(np.stack([f[1] for f in frames])).cuda()
+    vb = svo.VisualOdometryStereo(p)
+    vb.process_device(L.data_ptr(), R.data_ptr(), n, W * H)
+    assert np.array_equal(vb.poses, vo.poses)
+
+
+# ------------------------------------------------------------------ multi-camera rig (configs[4])
+@pytest.fixture(scope="module")
+def rig_frames():
+    from viso_amd.synth import RigSequence
+    seq = RigSequence(1242, 375, seed=2000, n_cams=4)
+    return seq, [seq.frame(f) for f in range(4)]
+
+
+def test_rig_spec_recovers_ground_truth(rig_frames):
+    seq, frames = rig_frames
+    S = ol.SvoRigSequence(ol.svo_params(1242, 375, *seq.K, seq.p.baseline), seq.extrinsics())
+    for f, (L, R) in enumerate(frames):
+        assert S.process(L, R) == (f > 0)
+        if f > 0:
+            gt = _T(seq.rig_pose(f)) @ np.linalg.inv(_T(seq.rig_pose(f - 1)))
+            M = _T(S.motion)
+            assert np.abs(M[:3, :3] - gt[:3, :3]).max() < 1e-3
+            assert np.abs(M[:3, 3] - gt[:3, 3]).max() < 5e-3
+            assert S.stats[4] > 0.6 * S.stats[3]
+
+
+def test_rig_identity_extrinsic_is_the_stereo_spec(synth_frames):
+    """One camera with the identity extrinsic: the rig estimator performs the
+    single-camera arithmetic exactly (multiplications by 1 and additions of 0)."""
+    seq, frames = synth_frames
+    p = ol.svo_params(1242, 375, *seq.K, seq.p.baseline)
+    E = np.array([[1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0]], np.float64)
+    A, B = ol.SvoSequence(p), ol.SvoRigSequence(p, E)
+    for l, r in frames[:3]:
+        assert A.process(l, r) == B.process([l], [r])
+        assert A.stats == B.stats
+        assert np.array_equal(A.motion, B.motion)
+
+
+@pytest.mark.gpu
+def test_gpu_rig_matches_oracle(rig_frames):
+    """configs[4]: 4 stereo cameras per timestep, one shared RANSAC + GN —
+    per-timestep stats, matches, cameras, inlier masks and motion identical to
+    the spec; batched device path == per-timestep path."""
+    import torch
+
+    from viso_amd import svo
+    seq, frames = rig_frames
+    E = seq.extrinsics()
+    p = svo.default_params(1242, 375, *seq.K, seq.p.baseline)
+    vo = svo.VisualOdometryStereoRig(p, E)
+    S = ol.SvoRigSequence(ol.svo_params(1242, 375, *seq.K, seq.p.baseline), E)
+    for f, (L, R) in enumerate(frames):
+        assert vo.process(L, R) == S.process(L, R) == (f > 0)
+        assert vo.stats().tolist() == S.stats
+        if f > 0:
+            uv8, inl = vo.getMatches()
+            assert np.array_equal(uv8, S.matches) and np.array_equal(inl, S.inliers)
+            assert np.array_equal(vo.getMatchCams(), S.cams)
+            assert np.array_equal(vo.getMotion()[:3].ravel(), _T(S.motion)[:3].ravel())
+    assert np.allclose(vo.poses, np.array(S.poses), rtol=0, atol=1e-9)
+    n = len(frames)
+    Ls = [torch.from_numpy(np.stack([fr[0][c] for fr in frames])).cuda() for c in range(4)]
+    Rs = [torch.from_numpy(np.stack([fr[1][c] for fr in frames])).cuda() for c in range(4)]
+    vb = svo.VisualOdometryStereoRig(p, E)
+    vb.process_device([t.data_ptr() for t in Ls], [t.data_ptr() for t in Rs], n, 1242 * 375)
+    assert np.array_equal(vb.poses, vo.poses)
+    assert vb.stats().tolist() == vo.stats().tolist()

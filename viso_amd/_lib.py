@@ -92,6 +92,10 @@ SIGNATURES = {
     "viso_svo_features": [_vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _i32, _vp],
     "viso_svo_match": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
     "viso_svo_estimate": [_vp, _vp, _i32, ctypes.c_int64, _vp, _vp, _vp],
+    "viso_svo_rig_create": [_vp, _i32, _vp, ctypes.c_int, _vp],
+    "viso_svo_rig_process": [_vp, _vp, _vp, _vp, _vp],
+    "viso_svo_rig_process_device": [_vp, _vp, _vp, _i32, ctypes.c_int64, _i32],
+    "viso_svo_get_match_cams": [_vp, _vp, _sz, _vp],
 }
 _RESTYPES = {"viso_version": ctypes.c_char_p}
 

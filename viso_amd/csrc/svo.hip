@@ -44,7 +44,7 @@ __constant__ int c_p16[16][2] = {{-5, -1}, {-5, 1}, {-3, -3}, {-3, 3}, {-1, -5},
                                  {3, -3},  {3, 3},  {5, -1},  {5, 1}};
 
 struct SvoDev {  // kernel view of the parameters
-    int w, h, nms_n, tau, margin, disp_max, radius, bw, bh, bmax, iters, gn_iters, cap, nband, ow;
+    int w, h, nms_n, tau, margin, disp_max, radius, bw, bh, bmax, iters, gn_iters, cap, nband, ow, ncam;
     double fx, fy, cu, cv, base, th2, eps;
     uint64_t seed;
 };
@@ -67,12 +67,18 @@ struct FeatDev {
     int* list;     // [h][tiles][4][seg_cap] packed x | cls << 16
 };
 
-// the images of a batch: image z = pair z / 2, side z & 1 (left, right)
+constexpr int kMaxCams = VISO_SVO_MAX_CAMS;
+
+// the images of a batch of timesteps, nc cameras each: image z = timestep
+// z / (2 nc), camera (z / 2) % nc, side z & 1 (left, right)
 struct ImgSrc {
-    const uint8_t* left;
-    const uint8_t* right;
-    long long pair_stride;  // bytes between consecutive pairs
-    __device__ const uint8_t* at(int z) const { return ((z & 1) ? right : left) + (long long)(z >> 1) * pair_stride; }
+    const uint8_t* left[kMaxCams];
+    const uint8_t* right[kMaxCams];
+    long long pair_stride;  // bytes between consecutive timesteps
+    __device__ const uint8_t* at(int z, int nc) const {
+        const int cam = (z >> 1) % nc;
+        return ((z & 1) ? right[cam] : left[cam]) + (long long)(z / (2 * nc)) * pair_stride;
+    }
 };
 
 // per-batch estimation buffers: pair b of a batch (sequence frame frame0 + b)
@@ -81,11 +87,14 @@ struct PairArgs {
     const FeatDev* sets;
     int ring;
     long long frame0;
-    int cap, mcap;       // features per image, bucketed matches per pair
+    int ncam;            // cameras per timestep (1: one stereo camera; > 1: rig)
+    int cap, mcap;       // features per image, bucketed matches per timestep (all cameras)
     int4* circ;          // [P][cap]      {l1, r1, r2, -}
     int4* rec8;          // [P][2 cap]    {u_l1, v_l1, u_r1, v_r1}, {u_l2, v_l2, u_r2, v_r2}
     uint8_t* keep;       // [P][cap]
     int* uv8;            // [P][mcap * 8]
+    uint8_t* mcam;       // [P][mcap] camera of each selected match
+    const double* extr;  // [ncam][12] rig -> camera extrinsics (rig only)
     int* n_sel;          // [P]
     int* counts;         // [P][iters]
     double* models;      // [P][iters * 12]
@@ -95,8 +104,8 @@ struct PairArgs {
     int* stats;          // [P][8]
 };
 
-__device__ inline FeatDev set_frame(const PairArgs& a, long long frame, int side) {
-    return a.sets[2 * (int)(frame % a.ring) + side];
+__device__ inline FeatDev set_frame(const PairArgs& a, long long frame, int cam, int side) {
+    return a.sets[2 * ((int)(frame % a.ring) * a.ncam + cam) + side];
 }
 
 // ---------------------------------------------------------------- detect
@@ -129,8 +138,8 @@ __device__ inline int mbcnt64(unsigned long long b) {
 
 // image z of a batch = pair z / 2 (left, right); its feature set lives in the
 // ring slot of that pair
-__device__ inline FeatDev set_of(const FeatDev* sets, int ring, int pair0, int z) {
-    return sets[2 * ((pair0 + z / 2) % ring) + (z & 1)];
+__device__ inline FeatDev set_of(const FeatDev* sets, int ring, int nc, int pair0, int z) {
+    return sets[2 * (((pair0 + z / (2 * nc)) % ring) * nc + (z >> 1) % nc) + (z & 1)];
 }
 
 template <int R, bool DOM>
@@ -144,8 +153,8 @@ __global__ __launch_bounds__(256) void svo_detect_kernel(ImgSrc src, SvoDev p,
     __shared__ uint32_t s_img[IR * kImgDw];
     __shared__ uint32_t s_rx[2][kDW + 2 * R];                 // P (max view)
     __shared__ uint32_t s_rn[DOM ? 2 : 1][DOM ? kDW + 2 * R : 1];  // P (min view, DOM only)
-    const uint8_t* __restrict__ img = src.at(blockIdx.z);
-    const FeatDev F = set_of(sets, ring, pair0, blockIdx.z);
+    const uint8_t* __restrict__ img = src.at(blockIdx.z, p.ncam);
+    const FeatDev F = set_of(sets, ring, p.ncam, pair0, blockIdx.z);
     const int w = p.w, h = p.h;
     const int x0 = blockIdx.x * OW, y0 = blockIdx.y * kDTH;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -314,7 +323,7 @@ __device__ inline int block_excl_scan(int v, int* s_w, int& total) {
 // features past the capacity dropped) -> the column-band index.
 __global__ __launch_bounds__(1024) void svo_scan_kernel(SvoDev p, const FeatDev* __restrict__ sets, int ring,
                                                         int pair0, int segs, int seg_cap) {
-    const FeatDev F = set_of(sets, ring, pair0, blockIdx.x);
+    const FeatDev F = set_of(sets, ring, p.ncam, pair0, blockIdx.x);
     __shared__ int s_w[16];
     const int h = p.h, n = h * segs;
     const int tid = threadIdx.x;
@@ -380,8 +389,8 @@ __device__ inline int sobel_q(const uint8_t* I, int w, int x, int y, bool du) {
 __global__ __launch_bounds__(256) void svo_describe_kernel(ImgSrc src, SvoDev p,
                                                            const FeatDev* __restrict__ sets, int ring,
                                                            int pair0) {
-    const uint8_t* __restrict__ img = src.at(blockIdx.y);
-    const FeatDev F = set_of(sets, ring, pair0, blockIdx.y);
+    const uint8_t* __restrict__ img = src.at(blockIdx.y, p.ncam);
+    const FeatDev F = set_of(sets, ring, p.ncam, pair0, blockIdx.y);
     const int n = *F.n;
     const int j = threadIdx.x & 15;
     for (int o = blockIdx.x * 16 + (threadIdx.x >> 4); o < n; o += gridDim.x * 16) {
@@ -406,7 +415,7 @@ __device__ inline int band_of(int u, const SvoDev& p) {
 
 __global__ __launch_bounds__(1024) void svo_index_kernel(SvoDev p, const FeatDev* __restrict__ sets, int ring,
                                                          int pair0) {
-    const FeatDev F = set_of(sets, ring, pair0, blockIdx.x);
+    const FeatDev F = set_of(sets, ring, p.ncam, pair0, blockIdx.x);
     __shared__ int s_w[16];
     const int h = p.h, nb = p.nband, tid = threadIdx.x;
     for (int y = tid; y < h; y += 1024) {
@@ -518,17 +527,18 @@ __device__ int best_match(const FeatDev& S, const SvoDev& p, int u, int v, int c
     return best == 0xffffffffu ? -1 : (int)(best & 0x7fffu);
 }
 
-// wave per current-left feature of pair b0 + blockIdx.y; circ[i2] = {l1,
-// r1, r2, -} and rec8[i2] = {u_l1, v_l1, u_r1, v_r1, u_l2, v_l2, u_r2, v_r2},
-// or circ[i2].x = rec8[i2].x = -1
+// wave per current-left feature of (timestep, camera) slot q = b0 * ncam +
+// blockIdx.y; circ[i2] = {l1, r1, r2, -} and rec8[i2] = {u_l1, v_l1, u_r1,
+// v_r1, u_l2, v_l2, u_r2, v_r2}, or circ[i2].x = rec8[i2].x = -1
 __global__ __launch_bounds__(256) void svo_circle_kernel(SvoDev p, PairArgs pa, int b0) {
-    const int pb = b0 + blockIdx.y;
+    const int q = b0 * pa.ncam + blockIdx.y;
+    const int pb = q / pa.ncam, cam = q - pb * pa.ncam;
     const long long fr = pa.frame0 + pb;
-    const FeatDev L1 = set_frame(pa, fr - 1, 0), R1 = set_frame(pa, fr - 1, 1), L2 = set_frame(pa, fr, 0),
-                  R2 = set_frame(pa, fr, 1);
-    int4* __restrict__ out = pa.circ + (size_t)pb * pa.cap;
-    int4* __restrict__ rec8 = pa.rec8 + (size_t)pb * 2 * pa.cap;
-    uint8_t* __restrict__ keep = pa.keep + (size_t)pb * pa.cap;
+    const FeatDev L1 = set_frame(pa, fr - 1, cam, 0), R1 = set_frame(pa, fr - 1, cam, 1),
+                  L2 = set_frame(pa, fr, cam, 0), R2 = set_frame(pa, fr, cam, 1);
+    int4* __restrict__ out = pa.circ + (size_t)q * pa.cap;
+    int4* __restrict__ rec8 = pa.rec8 + (size_t)q * 2 * pa.cap;
+    uint8_t* __restrict__ keep = pa.keep + (size_t)q * pa.cap;
     const int n2 = *L2.n;
     const int D = p.disp_max, Rr = p.radius, h = p.h;
     auto desc = [](const FeatDev& S, int i, uint4& a, uint4& b) {
@@ -574,6 +584,8 @@ __global__ __launch_bounds__(256) void svo_circle_kernel(SvoDev p, PairArgs pa, 
 // apply_update, is_inlier — same expressions, same order)
 struct Obs {
     double X, Y, Z, uL, vL, uR, vR;
+    const double* E;  // rig: extrinsic of the match's camera (rig -> camera), else null
+    double Xr[3];     // rig: the point in the rig frame t-1
 };
 
 __device__ inline Obs make_obs(const int* m, const SvoDev& p) {
@@ -586,7 +598,33 @@ __device__ inline Obs make_obs(const int* m, const SvoDev& p) {
     o.vL = (double)m[5];
     o.uR = (double)m[6];
     o.vR = (double)m[7];
+    o.E = nullptr;
     return o;
+}
+
+// match m of a timestep's selection; rig (ncam > 1): with its camera's
+// extrinsic E and the rig-frame point Xr = Re^T (X - te) (oracle make_obs_rig)
+__device__ inline Obs obs_at(const int* uv8, const uint8_t* mcam, int m, const PairArgs& pa, const SvoDev& p) {
+    Obs o = make_obs(uv8 + 8 * (size_t)m, p);
+    if (pa.ncam > 1) {
+        const double* E = pa.extr + 12 * (int)mcam[m];
+        o.E = E;
+        const double d0 = o.X - E[9], d1 = o.Y - E[10], d2 = o.Z - E[11];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) o.Xr[k] = ((E[k] * d0 + E[3 + k] * d1) + E[6 + k] * d2);
+    }
+    return o;
+}
+
+// rig: Q = R Xr + t (rig frame t), P = Re Q + te (camera frame t)
+__device__ inline void rig_point(const double* R, const double* t, const Obs& o, double* Q, double* P) {
+    Q[0] = ((R[0] * o.Xr[0] + R[1] * o.Xr[1]) + R[2] * o.Xr[2]) + t[0];
+    Q[1] = ((R[3] * o.Xr[0] + R[4] * o.Xr[1]) + R[5] * o.Xr[2]) + t[1];
+    Q[2] = ((R[6] * o.Xr[0] + R[7] * o.Xr[1]) + R[8] * o.Xr[2]) + t[2];
+    const double* E = o.E;
+    P[0] = ((E[0] * Q[0] + E[1] * Q[1]) + E[2] * Q[2]) + E[9];
+    P[1] = ((E[3] * Q[0] + E[4] * Q[1]) + E[5] * Q[2]) + E[10];
+    P[2] = ((E[6] * Q[0] + E[7] * Q[1]) + E[8] * Q[2]) + E[11];
 }
 
 __device__ inline void transform(const double* R, const double* t, const Obs& o, double* P) {
@@ -623,6 +661,38 @@ __device__ inline void residual_rows(const double* P, const Obs& o, const SvoDev
     }
 }
 
+// rig: residuals from P; gradients taken to the rig frame (g' = Re^T g), J = [Q x g', g']
+__device__ inline void residual_rows_rig(const double* P, const double* Q, const Obs& o, const SvoDev& p,
+                                         double* e, double (*J)[6]) {
+    const double iz = 1.0 / P[2];
+    const double iz2 = iz * iz;
+    const double xr = P[0] - p.base;
+    const double pu = ((p.fx * P[0]) * iz) + p.cu;
+    const double pv = ((p.fy * P[1]) * iz) + p.cv;
+    const double pr = ((p.fx * xr) * iz) + p.cu;
+    e[0] = o.uL - pu;
+    e[1] = o.vL - pv;
+    e[2] = o.uR - pr;
+    e[3] = o.vR - pv;
+    const double g[4][3] = {{p.fx * iz, 0.0, -(p.fx * P[0]) * iz2},
+                            {0.0, p.fy * iz, -(p.fy * P[1]) * iz2},
+                            {p.fx * iz, 0.0, -(p.fx * xr) * iz2},
+                            {0.0, p.fy * iz, -(p.fy * P[1]) * iz2}};
+    const double* E = o.E;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const double gx = (E[0] * g[r][0] + E[3] * g[r][1]) + E[6] * g[r][2];
+        const double gy = (E[1] * g[r][0] + E[4] * g[r][1]) + E[7] * g[r][2];
+        const double gz = (E[2] * g[r][0] + E[5] * g[r][1]) + E[8] * g[r][2];
+        J[r][0] = gz * Q[1] - gy * Q[2];
+        J[r][1] = gx * Q[2] - gz * Q[0];
+        J[r][2] = gy * Q[0] - gx * Q[1];
+        J[r][3] = gx;
+        J[r][4] = gy;
+        J[r][5] = gz;
+    }
+}
+
 __device__ inline void match_sums(const double* e, const double (*J)[6], double* s) {
     int k = 0;
 #pragma unroll
@@ -644,8 +714,14 @@ __device__ inline void match_leaf(const double* R, const double* t, const Obs& o
         return;
     }
     double P[3], e[4], J[4][6];
-    transform(R, t, o, P);
-    residual_rows(P, o, p, e, J);
+    if (o.E) {
+        double Q[3];
+        rig_point(R, t, o, Q, P);
+        residual_rows_rig(P, Q, o, p, e, J);
+    } else {
+        transform(R, t, o, P);
+        residual_rows(P, o, p, e, J);
+    }
     match_sums(e, J, s);
 }
 
@@ -719,9 +795,16 @@ __device__ inline void apply_update(const double* x, double* R, double* t) {
 
 __device__ inline bool is_inlier(const double* R, const double* t, const Obs& o, const SvoDev& p) {
     double P[3], e[4], J[4][6];
-    transform(R, t, o, P);
-    if (!(P[2] > 0.0)) return false;
-    residual_rows(P, o, p, e, J);
+    if (o.E) {
+        double Q[3];
+        rig_point(R, t, o, Q, P);
+        if (!(P[2] > 0.0)) return false;
+        residual_rows_rig(P, Q, o, p, e, J);
+    } else {
+        transform(R, t, o, P);
+        if (!(P[2] > 0.0)) return false;
+        residual_rows(P, o, p, e, J);
+    }
     const double d2 = ((e[0] * e[0] + e[1] * e[1]) + e[2] * e[2]) + e[3] * e[3];
     return d2 < p.th2;
 }
@@ -762,10 +845,11 @@ constexpr int kMaxBuckets = 4096;
 // row-major); lanes test 64 at a time (circular match present, column in the
 // bucket), a ballot ranks them in index order, the first bucket_max are kept.
 __global__ __launch_bounds__(256) void svo_bucket_kernel(SvoDev p, PairArgs pa, int b0) {
-    const int pb = b0 + blockIdx.y;
-    const FeatDev L2 = set_frame(pa, pa.frame0 + pb, 0);
-    const int4* __restrict__ rec8 = pa.rec8 + (size_t)pb * 2 * pa.cap;
-    uint8_t* __restrict__ keep = pa.keep + (size_t)pb * pa.cap;
+    const int q = b0 * pa.ncam + blockIdx.y;  // (timestep, camera) slot
+    const int pb = q / pa.ncam, cam = q - pb * pa.ncam;
+    const FeatDev L2 = set_frame(pa, pa.frame0 + pb, cam, 0);
+    const int4* __restrict__ rec8 = pa.rec8 + (size_t)q * 2 * pa.cap;
+    uint8_t* __restrict__ keep = pa.keep + (size_t)q * pa.cap;
     const int lane = threadIdx.x & 63;
     const int nbx = (p.w + p.bw - 1) / p.bw, nby = (p.h + p.bh - 1) / p.bh;
     const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -787,40 +871,46 @@ __global__ __launch_bounds__(256) void svo_bucket_kernel(SvoDev p, PairArgs pa, 
     }
 }
 
-// Compaction of the kept matches in left order -> uv8; stats[2] = circular
-// matches, stats[3] = bucketed.
+// Compaction of the kept matches of timestep b0 + blockIdx.x, camera by
+// camera, each in left order -> uv8 (+ the camera of each match in mcam);
+// stats[2] = circular matches, stats[3] = bucketed (all cameras).
 __global__ __launch_bounds__(1024) void svo_select_kernel(SvoDev p, PairArgs pa, int b0) {
     const int pb = b0 + blockIdx.x;
-    const FeatDev L2 = set_frame(pa, pa.frame0 + pb, 0);
-    const int4* __restrict__ rec8 = pa.rec8 + (size_t)pb * 2 * pa.cap;
-    const uint8_t* __restrict__ keep = pa.keep + (size_t)pb * pa.cap;
     int* __restrict__ uv8 = pa.uv8 + (size_t)pb * pa.mcap * 8;
+    uint8_t* __restrict__ mcam = pa.mcam + (size_t)pb * pa.mcap;
     int* __restrict__ n_sel = pa.n_sel + pb;
     int* __restrict__ stats = pa.stats + (size_t)pb * 8;
     __shared__ int s_w[16];
     const int tid = threadIdx.x;
-    const int n2 = *L2.n;
     int base = 0, m_all = 0;
-    for (int c0 = 0; c0 < n2; c0 += 1024) {
-        const int i2 = c0 + tid;
-        int4 a = make_int4(-1, 0, 0, 0), bq = make_int4(0, 0, 0, 0);
-        int k = 0;
-        if (i2 < n2) {
-            a = rec8[2 * (size_t)i2];
-            bq = rec8[2 * (size_t)i2 + 1];
-            k = keep[i2];
+    for (int cam = 0; cam < pa.ncam; ++cam) {
+        const size_t q = (size_t)pb * pa.ncam + cam;
+        const FeatDev L2 = set_frame(pa, pa.frame0 + pb, cam, 0);
+        const int4* __restrict__ rec8 = pa.rec8 + q * 2 * pa.cap;
+        const uint8_t* __restrict__ keep = pa.keep + q * pa.cap;
+        const int n2 = *L2.n;
+        for (int c0 = 0; c0 < n2; c0 += 1024) {
+            const int i2 = c0 + tid;
+            int4 a = make_int4(-1, 0, 0, 0), bq = make_int4(0, 0, 0, 0);
+            int k = 0;
+            if (i2 < n2) {
+                a = rec8[2 * (size_t)i2];
+                bq = rec8[2 * (size_t)i2 + 1];
+                k = keep[i2];
+            }
+            const int f = a.x >= 0 ? 1 : 0;
+            int tot, totf;
+            block_excl_scan(f, s_w, totf);
+            const int o = block_excl_scan(k, s_w, tot);
+            if (k) {
+                int4* r = reinterpret_cast<int4*>(uv8 + 8 * (size_t)(base + o));
+                r[0] = a;
+                r[1] = bq;
+                mcam[base + o] = (uint8_t)cam;
+            }
+            base += tot;
+            m_all += totf;
         }
-        const int f = a.x >= 0 ? 1 : 0;
-        int tot, totf;
-        block_excl_scan(f, s_w, totf);
-        const int o = block_excl_scan(k, s_w, tot);
-        if (k) {
-            int4* r = reinterpret_cast<int4*>(uv8 + 8 * (size_t)(base + o));
-            r[0] = a;
-            r[1] = bq;
-        }
-        base += tot;
-        m_all += totf;
     }
     if (tid == 0) {
         *n_sel = base;
@@ -846,6 +936,7 @@ __global__ __launch_bounds__(256) void svo_ransac_kernel(SvoDev p, PairArgs pa, 
     const int pb = b0 + blockIdx.y;
     const uint64_t seed = mix64(p.seed ^ (uint64_t)(pa.frame0 + pb));
     const int* __restrict__ uv8 = pa.uv8 + (size_t)pb * pa.mcap * 8;
+    const uint8_t* __restrict__ mcam = pa.mcam + (size_t)pb * pa.mcap;
     const int* __restrict__ n_sel = pa.n_sel + pb;
     int* __restrict__ counts = pa.counts + (size_t)pb * p.iters;
     double* __restrict__ models = pa.models + (size_t)pb * p.iters * 12;
@@ -868,7 +959,8 @@ __global__ __launch_bounds__(256) void svo_ransac_kernel(SvoDev p, PairArgs pa, 
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     // lanes 0..2: the sampled matches; lanes 3: a zero leaf (tree over 4)
     Obs o{};
-    if (lane < 3 && okS) o = make_obs(uv8 + 8 * (size_t)idx[lane], p);
+    o.E = nullptr;
+    if (lane < 3 && okS) o = obs_at(uv8, mcam, idx[lane], pa, p);
     for (int it = 0; it < p.gn_iters && s_ok[wave]; ++it) {
         double R[9], t[3];
         for (int i = 0; i < 9; ++i) R[i] = st[i];
@@ -905,7 +997,7 @@ __global__ __launch_bounds__(256) void svo_ransac_kernel(SvoDev p, PairArgs pa, 
         for (int m0 = 0; m0 < M; m0 += 64) {
             const int m = m0 + lane;
             bool in = false;
-            if (m < M) in = is_inlier(R, t, make_obs(uv8 + 8 * (size_t)m, p), p);
+            if (m < M) in = is_inlier(R, t, obs_at(uv8, mcam, m, pa, p), p);
             cnt += __popcll(__ballot(in));
         }
     } else {
@@ -925,6 +1017,7 @@ constexpr int kMaxChunks = 128;  // 64-leaf chunks: M <= 8192 (bucket count x bu
 __global__ __launch_bounds__(1024) void svo_refine_kernel(SvoDev p, PairArgs pa, int b0) {
     const int pb = b0 + blockIdx.x;
     const int* __restrict__ uv8 = pa.uv8 + (size_t)pb * pa.mcap * 8;
+    const uint8_t* __restrict__ mcam = pa.mcam + (size_t)pb * pa.mcap;
     const int* __restrict__ n_sel = pa.n_sel + pb;
     const int* __restrict__ counts = pa.counts + (size_t)pb * p.iters;
     const double* __restrict__ models = pa.models + (size_t)pb * p.iters * 12;
@@ -964,7 +1057,7 @@ __global__ __launch_bounds__(1024) void svo_refine_kernel(SvoDev p, PairArgs pa,
         double R[9], t[3];
         for (int i = 0; i < 9; ++i) R[i] = s_st[i];
         for (int i = 0; i < 3; ++i) t[i] = s_st[9 + i];
-        for (int m = tid; m < M; m += 1024) sel[m] = is_inlier(R, t, make_obs(uv8 + 8 * (size_t)m, p), p) ? 1 : 0;
+        for (int m = tid; m < M; m += 1024) sel[m] = is_inlier(R, t, obs_at(uv8, mcam, m, pa, p), p) ? 1 : 0;
         __syncthreads();
         int P2 = 1;
         while (P2 < M) P2 <<= 1;
@@ -978,7 +1071,7 @@ __global__ __launch_bounds__(1024) void svo_refine_kernel(SvoDev p, PairArgs pa,
             for (int ch = wave; ch < nch; ch += 16) {
                 const int m = ch * 64 + lane;
                 double s[28];
-                if (m < M) match_leaf(R, t, make_obs(uv8 + 8 * (size_t)m, p), p, sel[m] != 0, s);
+                if (m < M) match_leaf(R, t, obs_at(uv8, mcam, m, pa, p), p, sel[m] != 0, s);
                 else
                     for (int k = 0; k < 28; ++k) s[k] = 0.0;
                 if (lv_in == 6) {
@@ -1033,7 +1126,7 @@ __global__ __launch_bounds__(1024) void svo_refine_kernel(SvoDev p, PairArgs pa,
         for (int i = 0; i < 3; ++i) t[i] = s_st[9 + i];
         int c = 0;
         for (int m = tid; m < M; m += 1024) {
-            const bool in = is_inlier(R, t, make_obs(uv8 + 8 * (size_t)m, p), p);
+            const bool in = is_inlier(R, t, obs_at(uv8, mcam, m, pa, p), p);
             inl[m] = in ? 1 : 0;
             c += in ? 1 : 0;
         }
@@ -1065,8 +1158,13 @@ __global__ __launch_bounds__(64) void svo_pose_kernel(PairArgs pa, int nb, doubl
     if (b < nb) {
         const long long fr = pa.frame0 + b;
         int* st = pa.stats + (size_t)b * 8;
-        st[0] = *set_frame(pa, fr, 0).n;
-        st[1] = *set_frame(pa, fr, 1).n;
+        int nl = 0, nr = 0;
+        for (int cam = 0; cam < pa.ncam; ++cam) {
+            nl += *set_frame(pa, fr, cam, 0).n;
+            nr += *set_frame(pa, fr, cam, 1).n;
+        }
+        st[0] = nl;
+        st[1] = nr;
         int ok = 0;
         if (fr == 0) {
             for (int i = 2; i < 8; ++i) st[i] = 0;
@@ -1140,20 +1238,23 @@ void launch_detect(int R, bool dom, dim3 g, hipStream_t st, const ImgSrc& imgs, 
 using namespace viso;
 
 struct viso_svo {
-    static constexpr int kMaxPairBatch = 64;   // pairs per batch (feature pass + estimation)
-    static constexpr int kRing = kMaxPairBatch + 1;  // feature-set ring (pairs): a batch + the previous pair
+    static constexpr int kMaxPairBatch = 64;   // camera pairs per batch (feature pass + estimation)
     viso_svo_params p{};
+    int ncam = 1;           // stereo cameras per timestep (> 1: rig, BASELINE.json configs[4])
+    int tb = kMaxPairBatch; // timesteps per batch: kMaxPairBatch / ncam
+    int ring = kMaxPairBatch + 1;  // feature-set ring (timesteps): a batch + the previous timestep
+    std::vector<double> extr;      // [ncam][12] rig -> camera (rig only)
     int device = 0;
     hipStream_t stream = nullptr;
     int tiles = 0;          // detect tiles per row (256 - 2 nms_n output columns each)
     int seg_cap = 0;        // candidates per (row, tile, wave) segment
-    size_t frame = 0;       // pairs processed; pair k uses ring slot k % kRing
-    int last_b = -1;        // batch slot of the last processed pair
-    std::vector<FeatDev> sets;        // 2 * kRing (left, right of each slot)
+    size_t frame = 0;       // timesteps processed; timestep k uses ring slot k % ring
+    int last_b = -1;        // batch slot of the last processed timestep
+    std::vector<FeatDev> sets;        // [ring][ncam][left, right]
     FeatDev* d_sets = nullptr;
     PairArgs pa{};                    // per-pair estimation buffers of a batch
     std::vector<void*> allocs;
-    uint8_t* img = nullptr;           // host-path upload buffer (left, right)
+    uint8_t* img = nullptr;           // host-path upload buffer (ncam x (left, right))
     double* pose = nullptr;
     double* pose_log = nullptr;       // [max_poses][12]
     size_t max_poses = 0;
@@ -1179,6 +1280,7 @@ struct viso_svo {
         d.iters = p.ransac_iters;
         d.gn_iters = p.gn_iters;
         d.cap = p.max_features;
+        d.ncam = ncam;
         d.ow = kDW - 2 * p.nms_n;
         d.nband = 4 * ((p.width + d.ow - 1) / d.ow);
         d.fx = p.fx;
@@ -1206,7 +1308,9 @@ struct viso_svo {
         // strict NMS of radius n: same-class maxima of a row are > n apart, so
         // a wave's 64 columns hold at most ceil(64 / (n + 1)) per class
         seg_cap = 4 * ((64 + p.nms_n) / (p.nms_n + 1));
-        sets.assign(2 * kRing, FeatDev{});
+        tb = kMaxPairBatch / ncam;
+        ring = tb + 1;
+        sets.assign((size_t)2 * ring * ncam, FeatDev{});
         for (FeatDev& f : sets)
             if (alloc(f.u, cap) || alloc(f.v, cap) || alloc(f.c, cap) || alloc(f.d, (size_t)cap * kDesc) ||
                 alloc(f.row0, (size_t)h + 1) || alloc(f.n, 1) || alloc(f.cnt, (size_t)h * tiles * 4) ||
@@ -1215,11 +1319,14 @@ struct viso_svo {
                 return VISO_ERR_HIP;
         const int nbk = ((w + p.bucket_width - 1) / p.bucket_width) * ((h + p.bucket_height - 1) / p.bucket_height);
         const int P = kMaxPairBatch, it = std::max(1, p.ransac_iters);
-        pa.ring = kRing;
+        pa.ring = ring;
+        pa.ncam = ncam;
         pa.cap = cap;
-        pa.mcap = std::min(cap, nbk * p.bucket_max);
+        pa.mcap = ncam * std::min(cap, nbk * p.bucket_max);  // per timestep, all cameras
         max_poses = 65536;
-        if (alloc(d_sets, sets.size()) || alloc(img, 2 * (size_t)w * h) ||
+        double* d_extr = nullptr;
+        if (alloc(d_sets, sets.size()) || alloc(img, 2 * (size_t)ncam * w * h) ||
+            alloc(pa.mcam, (size_t)P * pa.mcap) || alloc(d_extr, (size_t)12 * ncam) ||
             alloc(pa.circ, (size_t)P * cap) || alloc(pa.rec8, (size_t)P * 2 * cap) || alloc(pa.keep, (size_t)P * cap) ||
             alloc(pa.uv8, (size_t)P * pa.mcap * 8) || alloc(pa.n_sel, P) || alloc(pa.counts, (size_t)P * it) ||
             alloc(pa.models, (size_t)P * it * 12) || alloc(pa.sel, (size_t)P * pa.mcap) ||
@@ -1227,6 +1334,9 @@ struct viso_svo {
             alloc(pose, 12) || alloc(pose_log, max_poses * 12))
             return VISO_ERR_HIP;
         pa.sets = d_sets;
+        pa.extr = d_extr;
+        if (!extr.empty())
+            VISO_HIP_CHECK(hipMemcpy(d_extr, extr.data(), extr.size() * sizeof(double), hipMemcpyHostToDevice));
         VISO_HIP_CHECK(hipMemcpy(d_sets, sets.data(), sets.size() * sizeof(FeatDev), hipMemcpyHostToDevice));
         return VISO_OK;
     }
@@ -1239,14 +1349,15 @@ struct viso_svo {
         if (stream) (void)hipStreamDestroy(stream);
         stream = nullptr;
     }
-    FeatDev& set_at(size_t pair, int side) { return sets[2 * (pair % kRing) + side]; }
+    FeatDev& set_at(size_t pair, int side) { return sets[2 * ((pair % ring) * ncam) + side]; }  // camera 0
     int nband() const { return 4 * tiles; }
 
-    // features of pairs frame .. frame + nb - 1
+    // features of timesteps frame .. frame + nb - 1 (all cameras)
     int detect(const ImgSrc& imgs, int nb) {
         const SvoDev d = dev();
-        const int pair0 = (int)(frame % kRing);
-        const dim3 g(tiles, (p.height + kDTH - 1) / kDTH, 2 * nb);
+        const int pair0 = (int)(frame % ring);
+        const int ni = 2 * nb * ncam;  // images
+        const dim3 g(tiles, (p.height + kDTH - 1) / kDTH, ni);
         if (timed) {
             while ((int)tev.size() < 2 * (tev_n + 1)) {
                 hipEvent_t e;
@@ -1257,13 +1368,13 @@ struct viso_svo {
         }
         // responses outside [2, w-3] x [2, h-3] reach the NMS only if margin < n + 2
         const bool dom = p.margin < p.nms_n + 2;
-        launch_detect(p.nms_n, dom, g, stream, imgs, d, d_sets, kRing, pair0, seg_cap);
-        svo_scan_kernel<<<2 * nb, 1024, 0, stream>>>(d, d_sets, kRing, pair0, 4 * tiles, seg_cap);
-        svo_describe_kernel<<<dim3(16, 2 * nb), 256, 0, stream>>>(imgs, d, d_sets, kRing, pair0);
+        launch_detect(p.nms_n, dom, g, stream, imgs, d, d_sets, ring, pair0, seg_cap);
+        svo_scan_kernel<<<ni, 1024, 0, stream>>>(d, d_sets, ring, pair0, 4 * tiles, seg_cap);
+        svo_describe_kernel<<<dim3(16, ni), 256, 0, stream>>>(imgs, d, d_sets, ring, pair0);
         if (timed) {
             VISO_HIP_CHECK(hipEventRecord(tev[2 * tev_n + 1], stream));
             ++tev_n;
-            timed_pairs += nb;
+            timed_pairs += nb * ncam;
         }
         VISO_HIP_CHECK(hipGetLastError());
         return VISO_OK;
@@ -1277,15 +1388,16 @@ struct viso_svo {
         pa.frame0 = frame0;
         const int nbk = ((p.width + p.bucket_width - 1) / p.bucket_width) *
                         ((p.height + p.bucket_height - 1) / p.bucket_height);
-        svo_circle_kernel<<<dim3(std::max(32, 2048 / np), np), 256, 0, stream>>>(d, pa, b0);
-        svo_bucket_kernel<<<dim3((nbk + 3) / 4, np), 256, 0, stream>>>(d, pa, b0);
+        const int nq = np * ncam;  // (timestep, camera) slots
+        svo_circle_kernel<<<dim3(std::max(32, 2048 / nq), nq), 256, 0, stream>>>(d, pa, b0);
+        svo_bucket_kernel<<<dim3((nbk + 3) / 4, nq), 256, 0, stream>>>(d, pa, b0);
         svo_select_kernel<<<np, 1024, 0, stream>>>(d, pa, b0);
         svo_ransac_kernel<<<dim3((p.ransac_iters + 3) / 4, np), 256, 0, stream>>>(d, pa, b0);
         svo_refine_kernel<<<np, 1024, 0, stream>>>(d, pa, b0);
         VISO_HIP_CHECK(hipGetLastError());
         return VISO_OK;
     }
-    // a batch of nb pairs: features, motions, poses
+    // a batch of nb <= tb timesteps: features, motions, poses
     int batch(const ImgSrc& imgs, int nb) {
         int rc = detect(imgs, nb);
         if (rc) return rc;
@@ -1302,7 +1414,7 @@ struct viso_svo {
 };
 
 namespace {
-int svo_check(const viso_svo_params* p) {
+int svo_check(const viso_svo_params* p, int ncam) {
     if (!p || p->width < 32 || p->height < 32 || p->width > 32767 || p->nms_n < 1 ||
         p->nms_n > kMaxNms || p->margin < 8 || p->max_features < 1 || p->max_features > 32768 ||
         p->bucket_width < 1 || p->bucket_height < 1 || p->ransac_iters < 1 || p->gn_iters < 1 ||
@@ -1311,7 +1423,7 @@ int svo_check(const viso_svo_params* p) {
     const int nbx = (p->width + p->bucket_width - 1) / p->bucket_width;
     const int nby = (p->height + p->bucket_height - 1) / p->bucket_height;
     if ((long long)nbx * nby > kMaxBuckets) return VISO_ERR_ARG;
-    if ((long long)nbx * nby * p->bucket_max > 64LL * kMaxChunks) return VISO_ERR_ARG;  // M bound
+    if ((long long)ncam * nbx * nby * p->bucket_max > 64LL * kMaxChunks) return VISO_ERR_ARG;  // M bound
     return VISO_OK;
 }
 }  // namespace
@@ -1347,9 +1459,15 @@ int viso_svo_default_params(viso_svo_params* p, int32_t width, int32_t height, d
 }
 
 int viso_svo_create(const viso_svo_params* p, int device, viso_svo** out) {
+    return viso_svo_rig_create(p, 1, nullptr, device, out);
+}
+
+int viso_svo_rig_create(const viso_svo_params* p, int32_t n_cams, const double* extrinsics, int device,
+                        viso_svo** out) {
     if (!out) return VISO_ERR_ARG;
     *out = nullptr;
-    if (svo_check(p)) return VISO_ERR_ARG;
+    if (n_cams < 1 || n_cams > VISO_SVO_MAX_CAMS || (n_cams > 1 && !extrinsics) || svo_check(p, n_cams))
+        return VISO_ERR_ARG;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return VISO_ERR_NODEVICE;
     VISO_HIP_CHECK(hipSetDevice(device));
@@ -1357,6 +1475,8 @@ int viso_svo_create(const viso_svo_params* p, int device, viso_svo** out) {
     if (!s) return VISO_ERR_ARG;
     s->p = *p;
     s->device = device;
+    s->ncam = n_cams;
+    if (n_cams > 1) s->extr.assign(extrinsics, extrinsics + 12 * n_cams);
     if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess || s->init() != VISO_OK) {
         s->release();
         delete s;
@@ -1382,17 +1502,24 @@ int viso_svo_synchronize(viso_svo* s) {
     return VISO_OK;
 }
 
-int viso_svo_process(viso_svo* s, const uint8_t* left, const uint8_t* right, const int32_t dims[3],
-                     int32_t* ok) {
-    if (!s || !left || !right || !dims) return VISO_ERR_ARG;
+int viso_svo_rig_process(viso_svo* s, const uint8_t* const* lefts, const uint8_t* const* rights,
+                         const int32_t dims[3], int32_t* ok) {
+    if (!s || !lefts || !rights || !dims) return VISO_ERR_ARG;
     const int w = dims[0], h = dims[1], stride = dims[2];
     if (w != s->p.width || h != s->p.height || stride < w) return VISO_ERR_ARG;
+    for (int c = 0; c < s->ncam; ++c)
+        if (!lefts[c] || !rights[c]) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(s->device));
-    uint8_t* dl = s->img;
-    uint8_t* dr = s->img + (size_t)w * h;
-    VISO_HIP_CHECK(hipMemcpy2DAsync(dl, w, left, stride, w, h, hipMemcpyHostToDevice, s->stream));
-    VISO_HIP_CHECK(hipMemcpy2DAsync(dr, w, right, stride, w, h, hipMemcpyHostToDevice, s->stream));
-    int rc = s->batch(ImgSrc{dl, dr, 0}, 1);
+    ImgSrc src{};
+    for (int c = 0; c < s->ncam; ++c) {
+        uint8_t* dl = s->img + (size_t)(2 * c) * w * h;
+        uint8_t* dr = dl + (size_t)w * h;
+        VISO_HIP_CHECK(hipMemcpy2DAsync(dl, w, lefts[c], stride, w, h, hipMemcpyHostToDevice, s->stream));
+        VISO_HIP_CHECK(hipMemcpy2DAsync(dr, w, rights[c], stride, w, h, hipMemcpyHostToDevice, s->stream));
+        src.left[c] = dl;
+        src.right[c] = dr;
+    }
+    int rc = s->batch(src, 1);
     if (rc) return rc;
     VISO_HIP_CHECK(hipStreamSynchronize(s->stream));
     if (ok) {
@@ -1403,19 +1530,39 @@ int viso_svo_process(viso_svo* s, const uint8_t* left, const uint8_t* right, con
     return VISO_OK;
 }
 
-int viso_svo_process_device(viso_svo* s, const uint8_t* left, const uint8_t* right, int32_t n,
-                            int64_t pair_stride, int32_t stride) {
-    if (!s || !left || !right || n < 0 || stride != s->p.width) return VISO_ERR_ARG;
+int viso_svo_process(viso_svo* s, const uint8_t* left, const uint8_t* right, const int32_t dims[3],
+                     int32_t* ok) {
+    if (!s || s->ncam != 1) return VISO_ERR_ARG;
+    return viso_svo_rig_process(s, &left, &right, dims, ok);
+}
+
+int viso_svo_rig_process_device(viso_svo* s, const uint8_t* const* lefts, const uint8_t* const* rights, int32_t n,
+                                int64_t pair_stride, int32_t stride) {
+    if (!s || !lefts || !rights || n < 0 || stride != s->p.width) return VISO_ERR_ARG;
+    for (int c = 0; c < s->ncam; ++c)
+        if (!lefts[c] || !rights[c]) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(s->device));
-    // batches of up to kMaxPairBatch pairs, queued back to back on the stream
-    // (image addresses are computed in the kernels: no per-batch host data)
-    for (int i0 = 0; i0 < n; i0 += viso_svo::kMaxPairBatch) {
-        const int nb = std::min(n - i0, viso_svo::kMaxPairBatch);
-        const int rc = s->batch(ImgSrc{left + (long long)i0 * pair_stride, right + (long long)i0 * pair_stride,
-                                       (long long)pair_stride}, nb);
+    // batches of up to tb timesteps (kMaxPairBatch camera pairs), queued back
+    // to back on the stream (image addresses are computed in the kernels: no
+    // per-batch host data, no host synchronisation)
+    for (int i0 = 0; i0 < n; i0 += s->tb) {
+        const int nb = std::min(n - i0, s->tb);
+        ImgSrc src{};
+        for (int c = 0; c < s->ncam; ++c) {
+            src.left[c] = lefts[c] + (long long)i0 * pair_stride;
+            src.right[c] = rights[c] + (long long)i0 * pair_stride;
+        }
+        src.pair_stride = (long long)pair_stride;
+        const int rc = s->batch(src, nb);
         if (rc) return rc;
     }
     return VISO_OK;
+}
+
+int viso_svo_process_device(viso_svo* s, const uint8_t* left, const uint8_t* right, int32_t n,
+                            int64_t pair_stride, int32_t stride) {
+    if (!s || s->ncam != 1) return VISO_ERR_ARG;
+    return viso_svo_rig_process_device(s, &left, &right, n, pair_stride, stride);
 }
 
 int viso_svo_timing(viso_svo* s, int32_t enable, double* feature_pass_ms, int32_t* pairs) {
@@ -1491,13 +1638,29 @@ int viso_svo_get_matches(viso_svo* s, int32_t* uv8, uint8_t* inlier, size_t cap,
     return VISO_OK;
 }
 
+int viso_svo_get_match_cams(viso_svo* s, uint8_t* cams, size_t cap, size_t* n) {
+    if (!s || !n) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipSetDevice(s->device));
+    VISO_HIP_CHECK(hipStreamSynchronize(s->stream));
+    int m = 0;
+    const int b = s->last_b;
+    if (s->frame >= 2) VISO_HIP_CHECK(hipMemcpy(&m, s->pa.n_sel + b, sizeof(int), hipMemcpyDeviceToHost));
+    *n = (size_t)m;
+    const size_t k = std::min((size_t)m, cap);
+    if (cams && k)
+        VISO_HIP_CHECK(hipMemcpy(cams, s->pa.mcam + (size_t)b * s->pa.mcap, k, hipMemcpyDeviceToHost));
+    return VISO_OK;
+}
+
 int viso_svo_features(viso_svo* s, const uint8_t* img, int32_t width, int32_t height, int32_t* u,
                       int32_t* v, int32_t* cls, uint8_t* desc, int32_t cap, int32_t* n) {
-    if (!s || !img || !n || width != s->p.width || height != s->p.height) return VISO_ERR_ARG;
+    if (!s || !img || !n || width != s->p.width || height != s->p.height || s->ncam != 1) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(s->device));
     const size_t bytes = (size_t)width * height;
     VISO_HIP_CHECK(hipMemcpyAsync(s->img, img, bytes, hipMemcpyHostToDevice, s->stream));
-    int rc = s->detect(ImgSrc{s->img, s->img, 0}, 1);  // into the slot of pair `frame` (not advanced)
+    ImgSrc src{};
+    src.left[0] = src.right[0] = s->img;
+    int rc = s->detect(src, 1);  // into the slot of pair `frame` (not advanced)
     if (rc) return rc;
     VISO_HIP_CHECK(hipStreamSynchronize(s->stream));
     const FeatDev F = s->set_at(s->frame, 0);
@@ -1517,7 +1680,7 @@ int viso_svo_features(viso_svo* s, const uint8_t* img, int32_t width, int32_t he
 int viso_svo_match(viso_svo* s, const int32_t* const* u4, const int32_t* const* v4,
                    const int32_t* const* cls4, const uint8_t* const* desc4, const int32_t n4[4],
                    int32_t* quad, int32_t cap, int32_t* n) {
-    if (!s || !u4 || !v4 || !cls4 || !desc4 || !n4 || !n) return VISO_ERR_ARG;
+    if (!s || !u4 || !v4 || !cls4 || !desc4 || !n4 || !n || s->ncam != 1) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(s->device));
     const int h = s->p.height;
     // the four sets go to the slots of pairs frame + 1 (previous) and
@@ -1546,7 +1709,7 @@ int viso_svo_match(viso_svo* s, const int32_t* const* u4, const int32_t* const* 
         VISO_HIP_CHECK(hipMemcpy(F.n, &m, sizeof(int), hipMemcpyHostToDevice));
     }
     const SvoDev d = s->dev();
-    svo_index_kernel<<<4, 1024, 0, s->stream>>>(d, s->d_sets, viso_svo::kRing, (int)(p1 % viso_svo::kRing));
+    svo_index_kernel<<<4, 1024, 0, s->stream>>>(d, s->d_sets, s->ring, (int)(p1 % s->ring));
     PairArgs pa = s->pa;
     pa.frame0 = (long long)p2;  // slot 0 = pair p2 (previous: p1)
     svo_circle_kernel<<<dim3(1024, 1), 256, 0, s->stream>>>(d, pa, 0);
@@ -1572,7 +1735,7 @@ int viso_svo_match(viso_svo* s, const int32_t* const* u4, const int32_t* const* 
 
 int viso_svo_estimate(viso_svo* s, const int32_t* uv8, int32_t n, int64_t frame, double* motion12,
                       uint8_t* inlier, int32_t* n_inliers) {
-    if (!s || (!uv8 && n > 0) || n < 0 || n > s->p.max_features || !motion12) return VISO_ERR_ARG;
+    if (!s || (!uv8 && n > 0) || n < 0 || n > s->p.max_features || !motion12 || s->ncam != 1) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(s->device));
     if (n > s->pa.mcap) return VISO_ERR_CAPACITY;
     if (n > 0) VISO_HIP_CHECK(hipMemcpy(s->pa.uv8, uv8, (size_t)n * 8 * sizeof(int), hipMemcpyHostToDevice));

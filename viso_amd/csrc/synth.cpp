@@ -99,6 +99,8 @@ void viso_synth_default(viso_synth_params* p, int width, int height) {
     p->noise = 2;
 }
 
+void rig_extrinsic(int cam, int n_cams, double* E12);
+
 int viso_synth_pose(const viso_synth_params* p, int frame, int cam, double* Rt12) {
     const double two_pi = 6.28318530717958647692;
     double f = (double)frame;
@@ -119,10 +121,43 @@ int viso_synth_pose(const viso_synth_params* p, int frame, int cam, double* Rt12
     return 0;
 }
 
-static void render_rows(const viso_synth_params* p, int frame, int cam, uint8_t* out, int y0,
-                        int y1) {
-    double Rt[12];
-    viso_synth_pose(p, frame, cam, Rt);
+// Rig of n_cams stereo cameras (BASELINE.json configs[4]): camera c is yawed by
+// (c - (n-1)/2) * 20 deg and sits (c - (n-1)/2) * 0.35 m along the rig x axis;
+// E_c maps rig -> camera c (left): P_c = Re P_rig + te.  The rig frame is the
+// trajectory camera of viso_synth_pose(frame, 0).
+void rig_extrinsic(int cam, int n_cams, double* E12) {
+    const double k = (double)cam - 0.5 * (double)(n_cams - 1);
+    const double a = k * 20.0 * 3.14159265358979323846 / 180.0;
+    const double c = std::cos(a), sn = std::sin(a);
+    const double Re[9] = {c, 0.0, -sn, 0.0, 1.0, 0.0, sn, 0.0, c};  // camera <- rig, yaw about y
+    const double pos[3] = {0.35 * k, 0.0, 0.0};
+    std::memcpy(E12, Re, sizeof(Re));
+    for (int i = 0; i < 3; ++i) E12[9 + i] = -((Re[3 * i] * pos[0] + Re[3 * i + 1] * pos[1]) + Re[3 * i + 2] * pos[2]);
+}
+
+int viso_synth_rig_extrinsic(int cam, int n_cams, double* E12) {
+    if (!E12 || n_cams < 1 || cam < 0 || cam >= n_cams) return -1;
+    rig_extrinsic(cam, n_cams, E12);
+    return 0;
+}
+
+// camera (cam, side) of the rig at `frame`: Tcw = E_c * Trig_w (+ baseline for the right image)
+int viso_synth_rig_pose(const viso_synth_params* p, int frame, int n_cams, int cam, int side, double* Rt12) {
+    if (!p || !Rt12 || n_cams < 1 || cam < 0 || cam >= n_cams) return -1;
+    double T[12], E[12];
+    viso_synth_pose(p, frame, 0, T);
+    rig_extrinsic(cam, n_cams, E);
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j)
+            Rt12[3 * i + j] = (E[3 * i] * T[j] + E[3 * i + 1] * T[3 + j]) + E[3 * i + 2] * T[6 + j];
+        Rt12[9 + i] = ((E[3 * i] * T[9] + E[3 * i + 1] * T[10]) + E[3 * i + 2] * T[11]) + E[9 + i];
+    }
+    if (side == 1) Rt12[9] -= p->baseline;
+    return 0;
+}
+
+static void render_rows(const viso_synth_params* p, const double* Rt, int frame, int cam, uint8_t* out,
+                        int y0, int y1) {
     const double* R = Rt;
     // camera centre C = -R^T t
     double C[3];
@@ -178,10 +213,10 @@ static void render_rows(const viso_synth_params* p, int frame, int cam, uint8_t*
     }
 }
 
-int viso_synth_render(const viso_synth_params* p, int frame, int cam, uint8_t* out, int threads) {
-    if (!p || !out || p->width <= 0 || p->height <= 0) return -1;
+static int render(const viso_synth_params* p, const double* Rt, int frame, int noise_cam, uint8_t* out,
+                  int threads) {
     if (threads <= 1) {
-        render_rows(p, frame, cam, out, 0, p->height);
+        render_rows(p, Rt, frame, noise_cam, out, 0, p->height);
         return 0;
     }
     std::vector<std::thread> ts;
@@ -189,10 +224,26 @@ int viso_synth_render(const viso_synth_params* p, int frame, int cam, uint8_t* o
     for (int i = 0; i < threads; ++i) {
         int y0 = i * rows, y1 = std::min(p->height, y0 + rows);
         if (y0 >= y1) break;
-        ts.emplace_back(render_rows, p, frame, cam, out, y0, y1);
+        ts.emplace_back(render_rows, p, Rt, frame, noise_cam, out, y0, y1);
     }
     for (auto& t : ts) t.join();
     return 0;
+}
+
+int viso_synth_render(const viso_synth_params* p, int frame, int cam, uint8_t* out, int threads) {
+    if (!p || !out || p->width <= 0 || p->height <= 0) return -1;
+    double Rt[12];
+    viso_synth_pose(p, frame, cam, Rt);
+    return render(p, Rt, frame, cam, out, threads);
+}
+
+int viso_synth_rig_render(const viso_synth_params* p, int frame, int n_cams, int cam, int side, uint8_t* out,
+                          int threads) {
+    if (!p || !out || p->width <= 0 || p->height <= 0) return -1;
+    double Rt[12];
+    if (viso_synth_rig_pose(p, frame, n_cams, cam, side, Rt)) return -1;
+    // pixel noise keyed by (camera, side) as well (cam field: 2 bits side+cam)
+    return render(p, Rt, frame, 2 * cam + side, out, threads);
 }
 
 }  // extern "C"

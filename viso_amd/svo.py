@@ -183,6 +183,47 @@ class VisualOdometryStereo:
         return m, inl[:len(uv8)].astype(bool), n.value
 
 
+class VisualOdometryStereoRig(VisualOdometryStereo):
+    """Multi-camera rig (BASELINE.json configs[4]): ``n_cams`` stereo cameras
+    with shared parameters and rig -> camera extrinsics (n_cams x 12); one
+    shared RANSAC + Gauss-Newton estimate of the rig motion per timestep."""
+
+    def __init__(self, params: SvoParams, extrinsics: np.ndarray, device: int = 0):
+        self.params = params
+        self.extrinsics = np.ascontiguousarray(extrinsics, np.float64).reshape(-1, 12)
+        self.n_cams = len(self.extrinsics)
+        h = ctypes.c_void_p()
+        _lib.call("viso_svo_rig_create", ctypes.byref(params), self.n_cams, _p(self.extrinsics), device,
+                  ctypes.byref(h))
+        self.h = h
+
+    def process(self, lefts, rights) -> bool:
+        """One timestep: lists of n_cams left / right images."""
+        ls = [np.ascontiguousarray(x, np.uint8) for x in lefts]
+        rs = [np.ascontiguousarray(x, np.uint8) for x in rights]
+        h, w = ls[0].shape
+        P = ctypes.c_void_p * self.n_cams
+        dims = (ctypes.c_int32 * 3)(w, h, w)
+        ok = ctypes.c_int32(0)
+        _lib.call("viso_svo_rig_process", self.h, P(*[_p(x) for x in ls]), P(*[_p(x) for x in rs]), dims,
+                  ctypes.byref(ok))
+        return bool(ok.value)
+
+    def process_device(self, left_ptrs, right_ptrs, n: int, pair_stride: int):
+        """n timesteps in HBM: camera c's pairs at left_ptrs[c] / right_ptrs[c]."""
+        P = ctypes.c_void_p * self.n_cams
+        _lib.call("viso_svo_rig_process_device", self.h, P(*left_ptrs), P(*right_ptrs), n, pair_stride,
+                  self.params.width)
+
+    def getMatchCams(self) -> np.ndarray:  # noqa: N802
+        """Camera of each match of getMatches()."""
+        n = ctypes.c_size_t(0)
+        _lib.call("viso_svo_get_match_cams", self.h, None, 0, ctypes.byref(n))
+        out = np.zeros(max(1, n.value), np.uint8)
+        _lib.call("viso_svo_get_match_cams", self.h, _p(out), n.value, ctypes.byref(n))
+        return out[:n.value]
+
+
 class Matcher:
     """Matcher facade: pushBack(left, right) twice, matchFeatures(), getMatches()."""
 

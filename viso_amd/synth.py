@@ -36,6 +36,11 @@ def _fns():
     lib.viso_synth_pose.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     lib.viso_synth_render.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                       ctypes.c_void_p, ctypes.c_int]
+    lib.viso_synth_rig_extrinsic.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    lib.viso_synth_rig_pose.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_int, ctypes.c_void_p]
+    lib.viso_synth_rig_render.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
     return lib
 
 
@@ -71,3 +76,34 @@ class Sequence:
         out = np.zeros(12, np.float64)
         _fns().viso_synth_pose(ctypes.byref(self.p), frame, cam, out.ctypes.data)
         return out
+
+
+class RigSequence(Sequence):
+    """The same scene seen by a rig of ``n_cams`` stereo cameras (BASELINE.json
+    configs[4]); ``frame(i)`` -> (lefts, rights), one image per camera."""
+
+    def __init__(self, width: int = 1242, height: int = 375, seed: int = 0, n_cams: int = 4, **kw):
+        super().__init__(width, height, seed, **kw)
+        self.n_cams = n_cams
+
+    def extrinsics(self) -> np.ndarray:
+        """(n_cams, 12): rig -> camera c (left), R row-major + t."""
+        out = np.zeros((self.n_cams, 12), np.float64)
+        for c in range(self.n_cams):
+            _fns().viso_synth_rig_extrinsic(c, self.n_cams, out[c].ctypes.data)
+        return out
+
+    def cam_image(self, frame: int, cam: int, side: int) -> np.ndarray:
+        out = np.empty((self.height, self.width), np.uint8)
+        rc = _fns().viso_synth_rig_render(ctypes.byref(self.p), frame, self.n_cams, cam, side,
+                                          out.ctypes.data, self.threads)
+        if rc != 0:
+            raise RuntimeError("viso_synth_rig_render failed")
+        return out
+
+    def frame(self, i: int):
+        return ([self.cam_image(i, c, 0) for c in range(self.n_cams)],
+                [self.cam_image(i, c, 1) for c in range(self.n_cams)])
+
+    def rig_pose(self, frame: int) -> np.ndarray:
+        return self.pose(frame, 0)
