@@ -18,8 +18,9 @@
 //   svo_bucket_kernel    wave per bucket: first bucket_max matches of the
 //                        bucket in left order (ballot ranks)
 //   svo_select_kernel    one workgroup: compaction of the kept matches
-//   svo_ransac_kernel    wave per hypothesis: 3-point Gauss-Newton (lane per
-//                        match), inlier count by ballot over all matches
+//   svo_obs_kernel       the selected matches' 3-D points / observations
+//   svo_hyp_kernel       thread per RANSAC hypothesis: 3-point Gauss-Newton
+//   svo_count_kernel     hypotheses x matches inlier counts (ballot/popc)
 //   svo_refine_kernel    one workgroup: best hypothesis, Gauss-Newton over
 //                        its inliers (28 canonical tree sums per iteration),
 //                        inlier flags, motion, pose accumulation
@@ -56,14 +57,18 @@ struct FeatDev {
     int* c;
     uint8_t* d;    // [cap][32]
     int* row0;     // [h + 1]: first feature index of each row; row0[h] = n
-    // column-band index (bands of kBand columns): the features of band b in
-    // row-major order; brow0[b * (h + 1) + y] = first position of row y
+    // class-band index: the features of class k in column band b, rows in
+    // ascending order; list kb = k * nband + b, brow0[kb * (h + 1) + y] = first
+    // position of row y
     int* bidx;     // [cap] feature index
-    int* buc;      // [cap] u | class << 16 of that feature
-    int* brow0;    // [nband][h + 1]
-    int* bcnt;     // [nband][h] per (band, row) counts (scratch)
+    int* buc;      // [cap] u | v << 15 | class << 30 of that feature
+    uint8_t* bd;   // [cap][32] its descriptor
+    int* bpos;     // [cap] position of feature i in the index
+    int* brow0;    // [4 nband][h + 1]
+    int* bcnt;     // [4 nband][h] scratch
     int* n;        // [1]
-    int* cnt;      // [h][tiles][4] candidate counts per (row, tile, wave) segment
+    int* cnt;      // [h][tiles][4] per (row, tile, wave) segment: candidate counts of the
+                   // four classes, 8 bits each
     int* list;     // [h][tiles][4][seg_cap] packed x | cls << 16
 };
 
@@ -94,6 +99,8 @@ struct PairArgs {
     uint8_t* keep;       // [P][cap]
     int* uv8;            // [P][mcap * 8]
     uint8_t* mcam;       // [P][mcap] camera of each selected match
+    double* obs;         // [P][mcap][kObs] each selected match's Obs (svo_obs_kernel)
+    uint8_t* hok;        // [P][iters] hypothesis solved (svo_hyp_kernel)
     const double* extr;  // [ncam][12] rig -> camera extrinsics (rig only)
     int* n_sel;          // [P]
     int* counts;         // [P][iters]
@@ -290,7 +297,9 @@ __global__ __launch_bounds__(256) void svo_detect_kernel(ImgSrc src, SvoDev p,
                     ++pos;
                 }
         }
-        if (lane == 0) F.cnt[seg] = min(total, seg_cap);
+        // per-class counts (strict NMS: <= ceil(64 / (n + 1)) <= 32 per class)
+        if (lane == 0)
+            F.cnt[seg] = __popcll(q0) | (__popcll(q1) << 8) | (__popcll(q2) << 16) | (__popcll(q3) << 24);
     }
 }
 
@@ -317,63 +326,94 @@ __device__ inline int block_excl_scan(int v, int* s_w, int& total) {
     return base + incl - v;
 }
 
-// Per image (1024 threads): row-major exclusive prefix over the segment
-// counts -> row index row0 and the features' u, v, class in that order; then
-// the band-major prefix over the same segments (band = segment column,
-// features past the capacity dropped) -> the column-band index.
+__device__ inline int bytesum(int c) { return (c & 0xff) + ((c >> 8) & 0xff) + ((c >> 16) & 0xff) + ((c >> 24) & 0xff); }
+__device__ inline int pack_uvc(int u, int v, int c) { return u | (v << 15) | (c << 30); }
+
+// Per image, five workgroups of 1024 threads (blockIdx.y):
+//   4     row-major exclusive prefix over the segment counts -> row index row0
+//         and the features' u, v, class in that order;
+//   k < 4 the class-k lists of the class-band index: the same row-major prefix
+//         (the features' indices, capacity truncation), the base of class k
+//         (kept features of the classes below), then the band-major prefix of
+//         the class-k counts over (band, row) and the scatter.
 __global__ __launch_bounds__(1024) void svo_scan_kernel(SvoDev p, const FeatDev* __restrict__ sets, int ring,
                                                         int pair0, int segs, int seg_cap) {
     const FeatDev F = set_of(sets, ring, p.ncam, pair0, blockIdx.x);
     __shared__ int s_w[16];
     const int h = p.h, n = h * segs;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, k = blockIdx.y;
     const int per = (n + 1023) / 1024;
     const int b = min(tid * per, n), e = min(b + per, n);
-    int* off = F.bcnt;  // [h][segs] row-major offset of each segment
     int s = 0;
-    for (int i = b; i < e; ++i) s += F.cnt[i];
+    for (int i = b; i < e; ++i) s += bytesum(F.cnt[i]);
     int total;
     int acc = block_excl_scan(s, s_w, total);
-    for (int i = b; i < e; ++i) {
-        const int y = i / segs;
-        if (i == y * segs) F.row0[y] = min(acc, p.cap);
-        off[i] = acc;
-        const int c = F.cnt[i];
-        const int* list = F.list + (size_t)i * seg_cap;
-        for (int k = 0; k < c; ++k) {
-            const int o = acc + k;
-            if (o >= p.cap) break;
-            const int q = list[k];
-            F.u[o] = q & 0xffff;
-            F.v[o] = y;
-            F.c[o] = q >> 16;
+    if (k == 4) {
+        for (int i = b; i < e; ++i) {
+            const int y = i / segs;
+            if (i == y * segs) F.row0[y] = min(acc, p.cap);
+            const int c = bytesum(F.cnt[i]);
+            const int* list = F.list + (size_t)i * seg_cap;
+            for (int q = 0; q < c; ++q) {
+                const int o = acc + q;
+                if (o >= p.cap) break;
+                const int ent = list[q];
+                F.u[o] = ent & 0xffff;
+                F.v[o] = y;
+                F.c[o] = ent >> 16;
+            }
+            acc += c;
         }
-        acc += c;
+        if (tid == 0) {
+            F.row0[h] = min(total, p.cap);
+            *F.n = min(total, p.cap);
+        }
+        return;
     }
-    if (tid == 0) {
-        F.row0[h] = min(total, p.cap);
-        *F.n = min(total, p.cap);
+    // class-k entries of segment i among its first min(count, cap - off) entries
+    auto kept = [&](int i, int kk, int c4, int o0) {
+        const int c = bytesum(c4), lim = min(c, max(p.cap - o0, 0));
+        if (lim == c) return (c4 >> (8 * kk)) & 0xff;
+        const int* list = F.list + (size_t)i * seg_cap;
+        int r = 0;
+        for (int q = 0; q < lim; ++q) r += (list[q] >> 16) == kk ? 1 : 0;
+        return r;
+    };
+    int* off = F.bcnt + (size_t)k * n;  // [h][segs] row-major offset of each segment (scratch of class k)
+    int below = 0;                      // kept features of classes < k in this thread's segments
+    for (int i = b; i < e; ++i) {
+        const int c4 = F.cnt[i];
+        off[i] = acc;
+        for (int kk = 0; kk < k; ++kk) below += kept(i, kk, c4, acc);
+        acc += bytesum(c4);
     }
+    int base;
+    block_excl_scan(below, s_w, base);
     __syncthreads();
-    // band-major: transposed index t = band * h + y
-    auto kept = [&](int i) { return min(max(p.cap - off[i], 0), F.cnt[i]); };
+    // band-major over t = band * h + y; segment i = y * segs + band
     s = 0;
     for (int t = b; t < e; ++t) {
-        const int bd = t / h, y = t - bd * h;
-        s += kept(y * segs + bd);
-    }
-    acc = block_excl_scan(s, s_w, total);
-    for (int t = b; t < e; ++t) {
         const int bd = t / h, y = t - bd * h, i = y * segs + bd;
-        const int c = kept(i), o0 = off[i];
-        F.brow0[bd * (h + 1) + y] = acc;
-        const int* list = F.list + (size_t)i * seg_cap;
-        for (int k = 0; k < c; ++k) {
-            F.bidx[acc + k] = o0 + k;
-            F.buc[acc + k] = list[k];
+        s += kept(i, k, F.cnt[i], off[i]);
+    }
+    acc = base + block_excl_scan(s, s_w, total);
+    for (int t = b; t < e; ++t) {
+        const int bd = t / h, y = t - bd * h, i = y * segs + bd, kb = k * segs + bd;
+        const int c4 = F.cnt[i], o0 = off[i];
+        const int lim = min(bytesum(c4), max(p.cap - o0, 0));
+        F.brow0[kb * (h + 1) + y] = acc;
+        if ((c4 >> (8 * k)) & 0xff) {
+            const int* list = F.list + (size_t)i * seg_cap;
+            for (int q = 0; q < lim; ++q) {
+                const int ent = list[q];
+                if ((ent >> 16) != k) continue;
+                F.bidx[acc] = o0 + q;
+                F.buc[acc] = pack_uvc(ent & 0xffff, y, k);
+                F.bpos[o0 + q] = acc;
+                ++acc;
+            }
         }
-        acc += c;
-        if (y == h - 1) F.brow0[bd * (h + 1) + h] = acc;
+        if (y == h - 1) F.brow0[kb * (h + 1) + h] = acc;
     }
 }
 
@@ -395,8 +435,12 @@ __global__ __launch_bounds__(256) void svo_describe_kernel(ImgSrc src, SvoDev p,
     const int j = threadIdx.x & 15;
     for (int o = blockIdx.x * 16 + (threadIdx.x >> 4); o < n; o += gridDim.x * 16) {
         const int sx = F.u[o] + c_p16[j][0], sy = F.v[o] + c_p16[j][1];
-        F.d[(size_t)o * kDesc + j] = (uint8_t)sobel_q(img, p.w, sx, sy, true);
-        F.d[(size_t)o * kDesc + 16 + j] = (uint8_t)sobel_q(img, p.w, sx, sy, false);
+        const uint8_t du = (uint8_t)sobel_q(img, p.w, sx, sy, true), dv = (uint8_t)sobel_q(img, p.w, sx, sy, false);
+        const size_t bp = (size_t)F.bpos[o] * kDesc;
+        F.d[(size_t)o * kDesc + j] = du;
+        F.d[(size_t)o * kDesc + 16 + j] = dv;
+        F.bd[bp + j] = du;
+        F.bd[bp + 16 + j] = dv;
     }
 }
 
@@ -417,14 +461,15 @@ __global__ __launch_bounds__(1024) void svo_index_kernel(SvoDev p, const FeatDev
                                                          int pair0) {
     const FeatDev F = set_of(sets, ring, p.ncam, pair0, blockIdx.x);
     __shared__ int s_w[16];
-    const int h = p.h, nb = p.nband, tid = threadIdx.x;
+    const int h = p.h, nk = 4 * p.nband, tid = threadIdx.x;
+    auto kb_of = [&](int i) { return F.c[i] * p.nband + band_of(F.u[i], p); };
     for (int y = tid; y < h; y += 1024) {
-        for (int b = 0; b < nb; ++b) F.bcnt[b * h + y] = 0;
+        for (int kb = 0; kb < nk; ++kb) F.bcnt[kb * h + y] = 0;
         const int e = F.row0[y + 1];
-        for (int i = F.row0[y]; i < e; ++i) ++F.bcnt[band_of(F.u[i], p) * h + y];
+        for (int i = F.row0[y]; i < e; ++i) ++F.bcnt[kb_of(i) * h + y];
     }
     __syncthreads();
-    const int n = nb * h;
+    const int n = nk * h;
     const int per = (n + 1023) / 1024;
     const int b0 = min(tid * per, n), e0 = min(b0 + per, n);
     int sum = 0;
@@ -432,21 +477,23 @@ __global__ __launch_bounds__(1024) void svo_index_kernel(SvoDev p, const FeatDev
     int total;
     int acc = block_excl_scan(sum, s_w, total);
     for (int i = b0; i < e0; ++i) {
-        const int b = i / h, y = i - b * h;
-        F.brow0[b * (h + 1) + y] = acc;
+        const int kb = i / h, y = i - kb * h;
+        F.brow0[kb * (h + 1) + y] = acc;
         acc += F.bcnt[i];
-        if (y == h - 1) F.brow0[b * (h + 1) + h] = acc;
+        if (y == h - 1) F.brow0[kb * (h + 1) + h] = acc;
     }
     __syncthreads();
     for (int y = tid; y < h; y += 1024) {
         const int r0 = F.row0[y], e = F.row0[y + 1];
         for (int i = r0; i < e; ++i) {
-            const int u = F.u[i], b = band_of(u, p);
+            const int kb = kb_of(i);
             int rank = 0;
-            for (int k = r0; k < i; ++k) rank += band_of(F.u[k], p) == b ? 1 : 0;
-            const int pos = F.brow0[b * (h + 1) + y] + rank;
+            for (int k = r0; k < i; ++k) rank += kb_of(k) == kb ? 1 : 0;
+            const int pos = F.brow0[kb * (h + 1) + y] + rank;
             F.bidx[pos] = i;
-            F.buc[pos] = (u & 0xffff) | (F.c[i] << 16);
+            F.buc[pos] = pack_uvc(F.u[i], y, F.c[i]);
+            F.bpos[i] = pos;
+            for (int q = 0; q < kDesc; ++q) F.bd[(size_t)pos * kDesc + q] = F.d[(size_t)i * kDesc + q];
         }
     }
 }
@@ -471,25 +518,37 @@ __device__ inline unsigned wave_min_u32(unsigned v) {
     return v;
 }
 
-// best candidate in `S` for the query (u, v, class, desc): rows [v - dv, v + dv],
-// u - du_hi <= u' <= u - du_lo; min SAD, ties -> lowest index.  The column
-// window's bands give one contiguous position range each (lanes 0..nq-1 load
-// the bounds, a wave scan concatenates them); lanes take 128 candidates per
-// step (two independent load chains in flight).  Wave-uniform arguments;
-// returns -1 if none.
-__device__ int best_match(const FeatDev& S, const SvoDev& p, int u, int v, int c, uint4 q0, uint4 q1,
-                          int du_lo, int du_hi, int dv) {
+// The best candidate of a search: feature index j (-1: none), its u, v and
+// descriptor (so the next search of the circle needs no extra loads).
+struct Cand {
+    int j, u, v;
+    uint4 d0, d1;
+};
+
+// best candidate in `S` for the query (u, v, class c, desc): rows [v - dv,
+// v + dv], u - du_hi <= u' <= u - du_lo; min SAD, ties -> lowest index.  The
+// class-c lists of the column bands the window overlaps give one contiguous
+// position range each (lanes 0..nq-1 load the bounds, a wave scan
+// concatenates them); every candidate's packed (u, v, class), index and
+// descriptor are loaded together, 128 candidates per step.  Wave-uniform
+// arguments and result.
+__device__ Cand best_match(const FeatDev& S, const SvoDev& p, int u, int v, int c, uint4 q0, uint4 q1,
+                           int du_lo, int du_hi, int dv) {
+    Cand r;
+    r.j = -1;
+    r.u = r.v = 0;
+    r.d0 = r.d1 = make_uint4(0, 0, 0, 0);
     const int lane = threadIdx.x & 63, h = p.h;
     const int va = max(v - dv, 0), vb = min(v + dv, h - 1);
     const int ua = u - du_hi, ub = u - du_lo;
-    if (ub < 0) return -1;
+    if (ub < 0) return r;
     const int ba = band_of(max(ua, 0), p), bq = band_of(ub, p);
     const int nq = min(bq - ba + 1, 64);  // (a window over > 64 bands: disp_max > ~3900)
     int s = 0, len = 0;
     if (lane < nq) {
-        const int* r = S.brow0 + (size_t)(ba + lane) * (h + 1);
-        s = r[va];
-        len = r[vb + 1] - s;
+        const int* rw = S.brow0 + (size_t)(c * p.nband + ba + lane) * (h + 1);
+        s = rw[va];
+        len = rw[vb + 1] - s;
     }
     int incl = len;
 #pragma unroll
@@ -500,36 +559,72 @@ __device__ int best_match(const FeatDev& S, const SvoDev& p, int u, int v, int c
     const int total = __shfl(incl, 63, 64);
     const int excl = incl - len;
     unsigned best = 0xffffffffu;
-    for (int k0 = 0; k0 < total; k0 += 128) {
-        const int ka = k0 + lane, kb = ka + 64;
-        int pa = 0, pb = 0;
+    int bu = 0, bv = 0;
+    uint4 bd0 = make_uint4(0, 0, 0, 0), bd1 = bd0;
+    // candidate slot k of the concatenated ranges -> its index position
+    auto pos_of = [&](int k) {
+        int ps = 0;
         for (int l = 0; l < nq; ++l) {
             const int el = __builtin_amdgcn_readlane(excl, l), sl = __builtin_amdgcn_readlane(s, l);
-            if (ka >= el) pa = sl + (ka - el);
-            if (kb >= el) pb = sl + (kb - el);
+            if (k >= el) ps = sl + (k - el);
         }
-        const bool va_ = ka < total, vb_ = kb < total;
-        const int ea = va_ ? S.buc[pa] : -1, eb = vb_ ? S.buc[pb] : -1;
-        const int ja = va_ ? S.bidx[pa] : 0, jb = vb_ ? S.bidx[pb] : 0;
-        const int da = u - (ea & 0xffff), db = u - (eb & 0xffff);
-        const bool ma = va_ && (ea >> 16) == c && da >= du_lo && da <= du_hi;
-        const bool mb = vb_ && (eb >> 16) == c && db >= du_lo && db <= du_hi;
-        if (ma) {
-            const uint4* dj = reinterpret_cast<const uint4*>(S.d + (size_t)ja * kDesc);
-            best = min(best, ((unsigned)sad32(q0, q1, dj[0], dj[1]) << 15) | (unsigned)ja);
+        return ps;
+    };
+    auto consider = [&](int e, int j, uint4 d0, uint4 d1) {
+        const int dd = u - (e & 0x7fff);
+        if (dd < du_lo || dd > du_hi) return;
+        const unsigned key = ((unsigned)sad32(q0, q1, d0, d1) << 15) | (unsigned)j;
+        if (key < best) {
+            best = key;
+            bu = e & 0x7fff;
+            bv = (e >> 15) & 0x7fff;
+            bd0 = d0;
+            bd1 = d1;
         }
-        if (mb) {
-            const uint4* dj = reinterpret_cast<const uint4*>(S.d + (size_t)jb * kDesc);
-            best = min(best, ((unsigned)sad32(q0, q1, dj[0], dj[1]) << 15) | (unsigned)jb);
+    };
+    for (int k0 = 0; k0 < total; k0 += 128) {
+        // two candidates per lane, all loads issued before the first use;
+        // lanes past the end load nothing
+        const int ka = k0 + lane, kb = ka + 64;
+        const bool two = k0 + 64 < total;  // wave-uniform
+        int ea = 0, eb = 0, ja = 0, jb = 0;
+        uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0, b0 = a0, b1 = a0;
+        if (ka < total) {
+            const int ps = pos_of(ka);
+            ea = S.buc[ps];
+            ja = S.bidx[ps];
+            const uint4* da = reinterpret_cast<const uint4*>(S.bd + (size_t)ps * kDesc);
+            a0 = da[0];
+            a1 = da[1];
         }
+        if (two && kb < total) {
+            const int ps = pos_of(kb);
+            eb = S.buc[ps];
+            jb = S.bidx[ps];
+            const uint4* db = reinterpret_cast<const uint4*>(S.bd + (size_t)ps * kDesc);
+            b0 = db[0];
+            b1 = db[1];
+        }
+        if (ka < total) consider(ea, ja, a0, a1);
+        if (two && kb < total) consider(eb, jb, b0, b1);
     }
-    best = wave_min_u32(best);
-    return best == 0xffffffffu ? -1 : (int)(best & 0x7fffu);
+    const unsigned wbest = wave_min_u32(best);
+    if (wbest == 0xffffffffu) return r;
+    const int owner = __builtin_ctzll(__ballot(best == wbest));
+    r.j = (int)(wbest & 0x7fffu);
+    r.u = __builtin_amdgcn_readlane(bu, owner);
+    r.v = __builtin_amdgcn_readlane(bv, owner);
+    r.d0 = make_uint4(__builtin_amdgcn_readlane(bd0.x, owner), __builtin_amdgcn_readlane(bd0.y, owner),
+                      __builtin_amdgcn_readlane(bd0.z, owner), __builtin_amdgcn_readlane(bd0.w, owner));
+    r.d1 = make_uint4(__builtin_amdgcn_readlane(bd1.x, owner), __builtin_amdgcn_readlane(bd1.y, owner),
+                      __builtin_amdgcn_readlane(bd1.z, owner), __builtin_amdgcn_readlane(bd1.w, owner));
+    return r;
 }
 
 // wave per current-left feature of (timestep, camera) slot q = b0 * ncam +
 // blockIdx.y; circ[i2] = {l1, r1, r2, -} and rec8[i2] = {u_l1, v_l1, u_r1,
-// v_r1, u_l2, v_l2, u_r2, v_r2}, or circ[i2].x = rec8[i2].x = -1
+// v_r1, u_l2, v_l2, u_r2, v_r2}, or circ[i2].x = rec8[i2].x = -1.  The four
+// searches chain through the winners' coordinates and descriptors.
 __global__ __launch_bounds__(256) void svo_circle_kernel(SvoDev p, PairArgs pa, int b0) {
     const int q = b0 * pa.ncam + blockIdx.y;
     const int pb = q / pa.ncam, cam = q - pb * pa.ncam;
@@ -540,41 +635,34 @@ __global__ __launch_bounds__(256) void svo_circle_kernel(SvoDev p, PairArgs pa, 
     int4* __restrict__ rec8 = pa.rec8 + (size_t)q * 2 * pa.cap;
     uint8_t* __restrict__ keep = pa.keep + (size_t)q * pa.cap;
     const int n2 = *L2.n;
-    const int D = p.disp_max, Rr = p.radius, h = p.h;
-    auto desc = [](const FeatDev& S, int i, uint4& a, uint4& b) {
-        const uint4* d = reinterpret_cast<const uint4*>(S.d + (size_t)i * kDesc);
-        a = d[0];
-        b = d[1];
-    };
+    const int D = p.disp_max, Rr = p.radius;
+    const int lane = threadIdx.x & 63;
     for (int i2 = blockIdx.x * 4 + (threadIdx.x >> 6); i2 < n2; i2 += gridDim.x * 4) {
-        const int c = L2.c[i2];
-        uint4 a, b;
+        const int c = L2.c[i2], u2 = L2.u[i2], v2 = L2.v[i2];
+        const uint4* dq = reinterpret_cast<const uint4*>(L2.d + (size_t)i2 * kDesc);
+        const uint4 a = dq[0], b = dq[1];
         int4 res = make_int4(-1, -1, -1, 0);
-        desc(L2, i2, a, b);
-        const int r2 = best_match(R2, p, L2.u[i2], L2.v[i2], c, a, b, 0, D, 1);
-        if (r2 >= 0) {
-            desc(R2, r2, a, b);
-            const int r1 = best_match(R1, p, R2.u[r2], R2.v[r2], c, a, b, -Rr, Rr, Rr);
-            if (r1 >= 0) {
-                desc(R1, r1, a, b);
-                const int l1 = best_match(L1, p, R1.u[r1], R1.v[r1], c, a, b, -D, 0, 1);
-                if (l1 >= 0) {
-                    desc(L1, l1, a, b);
-                    const int i2b = best_match(L2, p, L1.u[l1], L1.v[l1], c, a, b, -Rr, Rr, Rr);
-                    if (i2b == i2 && L1.u[l1] - R1.u[r1] >= 1 && L2.u[i2] - R2.u[r2] >= 1)
-                        res = make_int4(l1, r1, r2, 0);
+        int4 ra = make_int4(-1, 0, 0, 0), rb = make_int4(0, 0, 0, 0);
+        const Cand r2 = best_match(R2, p, u2, v2, c, a, b, 0, D, 1);  // left_t -> right_t
+        if (r2.j >= 0) {
+            const Cand r1 = best_match(R1, p, r2.u, r2.v, c, r2.d0, r2.d1, -Rr, Rr, Rr);  // -> right_t-1
+            if (r1.j >= 0) {
+                const Cand l1 = best_match(L1, p, r1.u, r1.v, c, r1.d0, r1.d1, -D, 0, 1);  // -> left_t-1
+                if (l1.j >= 0) {
+                    const Cand i2b = best_match(L2, p, l1.u, l1.v, c, l1.d0, l1.d1, -Rr, Rr, Rr);  // -> left_t
+                    if (i2b.j == i2 && l1.u - r1.u >= 1 && u2 - r2.u >= 1) {
+                        res = make_int4(l1.j, r1.j, r2.j, 0);
+                        ra = make_int4(l1.u, l1.v, r1.u, r1.v);
+                        rb = make_int4(u2, v2, r2.u, r2.v);
+                    }
                 }
             }
         }
-        const int lane = threadIdx.x & 63;
         if (lane == 0) out[i2] = res;
         if (lane == 2) keep[i2] = 0;
         if (lane == 1) {
-            const bool m = res.x >= 0;
-            rec8[2 * (size_t)i2] = m ? make_int4(L1.u[res.x], L1.v[res.x], R1.u[res.y], R1.v[res.y])
-                                     : make_int4(-1, 0, 0, 0);
-            rec8[2 * (size_t)i2 + 1] = m ? make_int4(L2.u[i2], L2.v[i2], R2.u[res.z], R2.v[res.z])
-                                         : make_int4(0, 0, 0, 0);
+            rec8[2 * (size_t)i2] = ra;
+            rec8[2 * (size_t)i2 + 1] = rb;
         }
     }
 }
@@ -606,6 +694,7 @@ __device__ inline Obs make_obs(const int* m, const SvoDev& p) {
 // extrinsic E and the rig-frame point Xr = Re^T (X - te) (oracle make_obs_rig)
 __device__ inline Obs obs_at(const int* uv8, const uint8_t* mcam, int m, const PairArgs& pa, const SvoDev& p) {
     Obs o = make_obs(uv8 + 8 * (size_t)m, p);
+    o.Xr[0] = o.Xr[1] = o.Xr[2] = 0.0;
     if (pa.ncam > 1) {
         const double* E = pa.extr + 12 * (int)mcam[m];
         o.E = E;
@@ -613,6 +702,34 @@ __device__ inline Obs obs_at(const int* uv8, const uint8_t* mcam, int m, const P
 #pragma unroll
         for (int k = 0; k < 3; ++k) o.Xr[k] = ((E[k] * d0 + E[3 + k] * d1) + E[6 + k] * d2);
     }
+    return o;
+}
+
+// Obs of the selected matches, computed once per timestep (svo_obs_kernel):
+// X, Y, Z, uL, vL, uR, vR, camera, Xr[3]
+constexpr int kObs = 12;
+
+__device__ inline void obs_store(double* O, const Obs& o, int cam) {
+    const double v[kObs] = {o.X, o.Y, o.Z, o.uL, o.vL, o.uR, o.vR, (double)cam, o.Xr[0], o.Xr[1], o.Xr[2], 0.0};
+#pragma unroll
+    for (int k = 0; k < kObs; ++k) O[k] = v[k];
+}
+
+__device__ inline Obs obs_load(const double* __restrict__ O, const PairArgs& pa) {
+    Obs o;
+    const double2* q = reinterpret_cast<const double2*>(O);
+    const double2 a = q[0], b = q[1], c = q[2], d = q[3], e = q[4];
+    o.X = a.x;
+    o.Y = a.y;
+    o.Z = b.x;
+    o.uL = b.y;
+    o.vL = c.x;
+    o.uR = c.y;
+    o.vR = d.x;
+    o.E = pa.ncam > 1 ? pa.extr + 12 * (int)d.y : nullptr;
+    o.Xr[0] = e.x;
+    o.Xr[1] = e.y;
+    o.Xr[2] = O[10];
     return o;
 }
 
@@ -793,18 +910,29 @@ __device__ inline void apply_update(const double* x, double* R, double* t) {
     for (int i = 0; i < 3; ++i) t[i] = tn[i];
 }
 
+// the residuals of residual_rows alone (same expressions)
+__device__ inline void residuals(const double* P, const Obs& o, const SvoDev& p, double* e) {
+    const double iz = 1.0 / P[2];
+    const double xr = P[0] - p.base;
+    const double pu = ((p.fx * P[0]) * iz) + p.cu;
+    const double pv = ((p.fy * P[1]) * iz) + p.cv;
+    const double pr = ((p.fx * xr) * iz) + p.cu;
+    e[0] = o.uL - pu;
+    e[1] = o.vL - pv;
+    e[2] = o.uR - pr;
+    e[3] = o.vR - pv;
+}
+
 __device__ inline bool is_inlier(const double* R, const double* t, const Obs& o, const SvoDev& p) {
-    double P[3], e[4], J[4][6];
+    double P[3], e[4];
     if (o.E) {
         double Q[3];
         rig_point(R, t, o, Q, P);
-        if (!(P[2] > 0.0)) return false;
-        residual_rows_rig(P, Q, o, p, e, J);
     } else {
         transform(R, t, o, P);
-        if (!(P[2] > 0.0)) return false;
-        residual_rows(P, o, p, e, J);
     }
+    if (!(P[2] > 0.0)) return false;
+    residuals(P, o, p, e);
     const double d2 = ((e[0] * e[0] + e[1] * e[1]) + e[2] * e[2]) + e[3] * e[3];
     return d2 < p.th2;
 }
@@ -931,81 +1059,96 @@ __device__ inline bool sample3(uint64_t seed, int h, int M, int* idx) {
     return got == 3;
 }
 
-// wave per hypothesis: counts[h], models[h] = R(9) t(3)
-__global__ __launch_bounds__(256) void svo_ransac_kernel(SvoDev p, PairArgs pa, int b0) {
+// Obs of every selected match of timestep b0 + blockIdx.y (thread per match)
+__global__ __launch_bounds__(256) void svo_obs_kernel(SvoDev p, PairArgs pa, int b0) {
     const int pb = b0 + blockIdx.y;
-    const uint64_t seed = mix64(p.seed ^ (uint64_t)(pa.frame0 + pb));
+    const int M = pa.n_sel[pb];
     const int* __restrict__ uv8 = pa.uv8 + (size_t)pb * pa.mcap * 8;
     const uint8_t* __restrict__ mcam = pa.mcam + (size_t)pb * pa.mcap;
-    const int* __restrict__ n_sel = pa.n_sel + pb;
-    int* __restrict__ counts = pa.counts + (size_t)pb * p.iters;
-    double* __restrict__ models = pa.models + (size_t)pb * p.iters * 12;
-    __shared__ double s_st[4][12];
-    __shared__ int s_ok[4];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int hyp = blockIdx.x * 4 + wave;
-    const int M = *n_sel;
+    double* __restrict__ O = pa.obs + (size_t)pb * pa.mcap * kObs;
+    for (int m = blockIdx.x * 256 + threadIdx.x; m < M; m += gridDim.x * 256)
+        obs_store(O + (size_t)m * kObs, obs_at(uv8, mcam, m, pa, p), pa.ncam > 1 ? (int)mcam[m] : 0);
+}
+
+// Thread per hypothesis: its 3-match sample, Gauss-Newton from the identity
+// (sums over the sample as the 3-leaf canonical tree (s0 + s1) + (s2 + 0)),
+// models[h] = R(9) t(3) (identity if the sample or a solve failed), hok[h].
+__global__ __launch_bounds__(64) void svo_hyp_kernel(SvoDev p, PairArgs pa, int b0) {
+    const int pb = b0 + blockIdx.y;
+    const int hyp = blockIdx.x * 64 + threadIdx.x;
     if (hyp >= p.iters) return;
-    double* st = s_st[wave];
-    if (M < 6) {
-        if (lane == 0) counts[hyp] = 0;
-        return;
-    }
+    const int M = pa.n_sel[pb];
+    const double* __restrict__ O = pa.obs + (size_t)pb * pa.mcap * kObs;
+    double* __restrict__ model = pa.models + ((size_t)pb * p.iters + hyp) * 12;
+    double R[9] = {1.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0}, t[3] = {0.0, 0.0, 0.0};
     int idx[3];
-    const bool okS = sample3(seed, hyp, M, idx);
-    if (lane < 12) st[lane] = (lane % 4 == 0 && lane < 9) ? 1.0 : 0.0;
-    if (lane == 0) s_ok[wave] = okS ? 1 : 0;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    // lanes 0..2: the sampled matches; lanes 3: a zero leaf (tree over 4)
-    Obs o{};
-    o.E = nullptr;
-    if (lane < 3 && okS) o = obs_at(uv8, mcam, idx[lane], pa, p);
-    for (int it = 0; it < p.gn_iters && s_ok[wave]; ++it) {
-        double R[9], t[3];
-        for (int i = 0; i < 9; ++i) R[i] = st[i];
-        for (int i = 0; i < 3; ++i) t[i] = st[9 + i];
-        double s[28];
-        match_leaf(R, t, o, p, lane < 3, s);
-        double S[28];
+    bool ok = M >= 6 && sample3(mix64(p.seed ^ (uint64_t)(pa.frame0 + pb)), hyp, M, idx);
+    if (ok) {
+        const Obs o0 = obs_load(O + (size_t)idx[0] * kObs, pa), o1 = obs_load(O + (size_t)idx[1] * kObs, pa),
+                  o2 = obs_load(O + (size_t)idx[2] * kObs, pa);
+        for (int it = 0; it < p.gn_iters; ++it) {
+            double S[28], l[28], x[6];
+            match_leaf(R, t, o0, p, true, S);
+            match_leaf(R, t, o1, p, true, l);
 #pragma unroll
-        for (int k = 0; k < 28; ++k) S[k] = lane_tree(s[k], 2);
-        int conv = 0;
-        if (lane == 0) {
-            double x[6];
+            for (int k = 0; k < 28; ++k) S[k] = S[k] + l[k];
+            match_leaf(R, t, o2, p, true, l);
+#pragma unroll
+            for (int k = 0; k < 28; ++k) S[k] = S[k] + (l[k] + 0.0);
             if (!solve6(S, x)) {
-                s_ok[wave] = 0;
-            } else {
-                apply_update(x, R, t);
-                for (int i = 0; i < 9; ++i) st[i] = R[i];
-                for (int i = 0; i < 3; ++i) st[9 + i] = t[i];
-                double mx = 0.0;
-                for (int k = 0; k < 6; ++k) mx = fmax(mx, fabs(x[k]));
-                conv = mx < p.eps ? 1 : 0;
+                ok = false;
+                break;
             }
+            apply_update(x, R, t);
+            double mx = 0.0;
+            for (int k = 0; k < 6; ++k) mx = fmax(mx, fabs(x[k]));
+            if (mx < p.eps) break;
         }
-        conv = __shfl(conv, 0, 64);
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if (conv) break;
     }
-    double R[9], t[3];
-    for (int i = 0; i < 9; ++i) R[i] = st[i];
-    for (int i = 0; i < 3; ++i) t[i] = st[9 + i];
-    int cnt = 0;
-    if (s_ok[wave]) {
-        for (int m0 = 0; m0 < M; m0 += 64) {
-            const int m = m0 + lane;
-            bool in = false;
-            if (m < M) in = is_inlier(R, t, obs_at(uv8, mcam, m, pa, p), p);
-            cnt += __popcll(__ballot(in));
+    for (int i = 0; i < 12; ++i) model[i] = ok ? (i < 9 ? R[i] : t[i - 9]) : ((i % 4 == 0 && i < 9) ? 1.0 : 0.0);
+    pa.hok[(size_t)pb * p.iters + hyp] = ok ? 1 : 0;
+}
+
+// Inlier counts: a workgroup scores kHypBlock hypotheses of one timestep
+// against all its matches (each match's Obs loaded once for all of them),
+// ballot + popcount per wave, wave totals summed in LDS.
+constexpr int kHypBlock = 8;
+
+__global__ __launch_bounds__(256) void svo_count_kernel(SvoDev p, PairArgs pa, int b0) {
+    const int pb = b0 + blockIdx.y;
+    const int h0 = blockIdx.x * kHypBlock;
+    const int M = pa.n_sel[pb];
+    const double* __restrict__ O = pa.obs + (size_t)pb * pa.mcap * kObs;
+    __shared__ double s_mod[kHypBlock][12];
+    __shared__ int s_ok[kHypBlock];
+    __shared__ int s_cnt[4][kHypBlock];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid < kHypBlock * 12) {
+        const int hh = tid / 12, i = tid - hh * 12;
+        s_mod[hh][i] = h0 + hh < p.iters ? pa.models[((size_t)pb * p.iters + h0 + hh) * 12 + i] : 0.0;
+    }
+    if (tid < kHypBlock) s_ok[tid] = h0 + tid < p.iters ? pa.hok[(size_t)pb * p.iters + h0 + tid] : 0;
+    __syncthreads();
+    int cnt[kHypBlock];
+#pragma unroll
+    for (int hh = 0; hh < kHypBlock; ++hh) cnt[hh] = 0;
+    for (int m0 = 0; m0 < M; m0 += 256) {
+        const int m = m0 + tid;
+        Obs o;
+        if (m < M) o = obs_load(O + (size_t)m * kObs, pa);
+#pragma unroll
+        for (int hh = 0; hh < kHypBlock; ++hh) {
+            if (!s_ok[hh]) continue;
+            const bool in = m < M && is_inlier(s_mod[hh], s_mod[hh] + 9, o, p);
+            cnt[hh] += __popcll(__ballot(in));
         }
-    } else {
-        for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0) ? 1.0 : 0.0;
-        for (int i = 0; i < 3; ++i) t[i] = 0.0;
     }
-    if (lane == 0) counts[hyp] = cnt;
-    if (lane < 12) models[(size_t)hyp * 12 + lane] = lane < 9 ? R[lane] : t[lane - 9];
+    if (lane == 0)
+#pragma unroll
+        for (int hh = 0; hh < kHypBlock; ++hh) s_cnt[wave][hh] = cnt[hh];
+    __syncthreads();
+    if (tid < kHypBlock && h0 + tid < p.iters)
+        pa.counts[(size_t)pb * p.iters + h0 + tid] = (s_cnt[0][tid] + s_cnt[1][tid]) + (s_cnt[2][tid] + s_cnt[3][tid]);
 }
 
 // ---------------------------------------------------------------- refine
@@ -1014,10 +1157,11 @@ __global__ __launch_bounds__(256) void svo_ransac_kernel(SvoDev p, PairArgs pa, 
 // inlier flags, motion, pose update T_wc <- T_wc * Tr^-1, stats.
 constexpr int kMaxChunks = 128;  // 64-leaf chunks: M <= 8192 (bucket count x bucket_max)
 
-__global__ __launch_bounds__(1024) void svo_refine_kernel(SvoDev p, PairArgs pa, int b0) {
+constexpr int kRefineThreads = 256;  // 4 waves: up to 256 VGPRs per lane (fp64 leaves + 28 sums)
+
+__global__ __launch_bounds__(kRefineThreads) void svo_refine_kernel(SvoDev p, PairArgs pa, int b0) {
     const int pb = b0 + blockIdx.x;
-    const int* __restrict__ uv8 = pa.uv8 + (size_t)pb * pa.mcap * 8;
-    const uint8_t* __restrict__ mcam = pa.mcam + (size_t)pb * pa.mcap;
+    const double* __restrict__ O = pa.obs + (size_t)pb * pa.mcap * kObs;
     const int* __restrict__ n_sel = pa.n_sel + pb;
     const int* __restrict__ counts = pa.counts + (size_t)pb * p.iters;
     const double* __restrict__ models = pa.models + (size_t)pb * p.iters * 12;
@@ -1057,7 +1201,8 @@ __global__ __launch_bounds__(1024) void svo_refine_kernel(SvoDev p, PairArgs pa,
         double R[9], t[3];
         for (int i = 0; i < 9; ++i) R[i] = s_st[i];
         for (int i = 0; i < 3; ++i) t[i] = s_st[9 + i];
-        for (int m = tid; m < M; m += 1024) sel[m] = is_inlier(R, t, obs_at(uv8, mcam, m, pa, p), p) ? 1 : 0;
+        for (int m = tid; m < M; m += kRefineThreads)
+            sel[m] = is_inlier(R, t, obs_load(O + (size_t)m * kObs, pa), p) ? 1 : 0;
         __syncthreads();
         int P2 = 1;
         while (P2 < M) P2 <<= 1;
@@ -1068,10 +1213,10 @@ __global__ __launch_bounds__(1024) void svo_refine_kernel(SvoDev p, PairArgs pa,
         for (int it = 0; it < p.gn_iters; ++it) {
             for (int i = 0; i < 9; ++i) R[i] = s_st[i];
             for (int i = 0; i < 3; ++i) t[i] = s_st[9 + i];
-            for (int ch = wave; ch < nch; ch += 16) {
+            for (int ch = wave; ch < nch; ch += kRefineThreads / 64) {
                 const int m = ch * 64 + lane;
                 double s[28];
-                if (m < M) match_leaf(R, t, obs_at(uv8, mcam, m, pa, p), p, sel[m] != 0, s);
+                if (m < M) match_leaf(R, t, obs_load(O + (size_t)m * kObs, pa), p, sel[m] != 0, s);
                 else
                     for (int k = 0; k < 28; ++k) s[k] = 0.0;
                 if (lv_in == 6) {
@@ -1079,6 +1224,7 @@ __global__ __launch_bounds__(1024) void svo_refine_kernel(SvoDev p, PairArgs pa,
                     const double r = reduce_scatter_28(s, &vi);
                     if (vi >= 0 && lane < 32) s_chunk[ch][vi] = r;
                 } else {
+#pragma unroll
                     for (int k = 0; k < 28; ++k) {
                         const double r = lane_tree(s[k], lv_in);
                         if (lane == 0) s_chunk[ch][k] = r;
@@ -1089,17 +1235,13 @@ __global__ __launch_bounds__(1024) void svo_refine_kernel(SvoDev p, PairArgs pa,
             if (wave == 0) {
                 // pairwise tree over the chunk sums (padded to 2^lv_out with zeros)
                 double S[28];
+#pragma unroll
                 for (int k = 0; k < 28; ++k) {
-                    if (lv_out <= 6) {
-                        S[k] = lane_tree(lane < nch ? s_chunk[lane][k] : 0.0, lv_out);
-                    } else {
-                        // more than 64 chunks: each lane first sums its aligned block of
-                        // `per` chunks (pairwise), then the 64 block sums
-                        const int per = (1 << lv_out) / 64;
-                        double a[2];
-                        for (int q = 0; q < per; ++q) a[q] = s_chunk[lane * per + q][k];
-                        S[k] = lane_tree(per == 2 ? a[0] + a[1] : a[0], 6);
-                    }
+                    // nch is a power of two; more than 64 chunks (128): each lane
+                    // first sums its aligned pair of chunks, then the 64 pair sums
+                    const double v = lv_out <= 6 ? (lane < nch ? s_chunk[lane][k] : 0.0)
+                                                 : s_chunk[2 * lane][k] + s_chunk[2 * lane + 1][k];
+                    S[k] = lane_tree(v, lv_out <= 6 ? lv_out : 6);
                 }
                 if (lane == 0) {
                     double x[6];
@@ -1125,15 +1267,15 @@ __global__ __launch_bounds__(1024) void svo_refine_kernel(SvoDev p, PairArgs pa,
         for (int i = 0; i < 9; ++i) R[i] = s_st[i];
         for (int i = 0; i < 3; ++i) t[i] = s_st[9 + i];
         int c = 0;
-        for (int m = tid; m < M; m += 1024) {
-            const bool in = is_inlier(R, t, obs_at(uv8, mcam, m, pa, p), p);
+        for (int m = tid; m < M; m += kRefineThreads) {
+            const bool in = is_inlier(R, t, obs_load(O + (size_t)m * kObs, pa), p);
             inl[m] = in ? 1 : 0;
             c += in ? 1 : 0;
         }
         atomicAdd(&s_cnt, c);
         __syncthreads();
     } else {
-        for (int m = tid; m < M; m += 1024) inl[m] = 0;
+        for (int m = tid; m < M; m += kRefineThreads) inl[m] = 0;
     }
     __syncthreads();
     if (tid == 0) {
@@ -1208,6 +1350,14 @@ __global__ __launch_bounds__(64) void svo_pose_kernel(PairArgs pa, int nb, doubl
         if (fr < max_poses) pose_log[12 * fr + i] = s_pose[k][i];
         else if (k == nb - 1) pose_log[12 * (max_poses - 1) + i] = s_pose[k][i];
     }
+}
+
+// RANSAC + refinement of timesteps b0 .. b0 + np - 1 (selection in pa)
+void launch_ransac(const SvoDev& d, const PairArgs& pa, int b0, int np, hipStream_t st) {
+    svo_obs_kernel<<<dim3((pa.mcap + 255) / 256, np), 256, 0, st>>>(d, pa, b0);
+    svo_hyp_kernel<<<dim3((d.iters + 63) / 64, np), 64, 0, st>>>(d, pa, b0);
+    svo_count_kernel<<<dim3((d.iters + kHypBlock - 1) / kHypBlock, np), 256, 0, st>>>(d, pa, b0);
+    svo_refine_kernel<<<np, kRefineThreads, 0, st>>>(d, pa, b0);
 }
 
 template <int R>
@@ -1315,7 +1465,8 @@ struct viso_svo {
             if (alloc(f.u, cap) || alloc(f.v, cap) || alloc(f.c, cap) || alloc(f.d, (size_t)cap * kDesc) ||
                 alloc(f.row0, (size_t)h + 1) || alloc(f.n, 1) || alloc(f.cnt, (size_t)h * tiles * 4) ||
                 alloc(f.list, (size_t)h * tiles * 4 * seg_cap) || alloc(f.bidx, cap) || alloc(f.buc, cap) ||
-                alloc(f.brow0, (size_t)nband() * (h + 1)) || alloc(f.bcnt, (size_t)nband() * h))
+                alloc(f.bd, (size_t)cap * kDesc) || alloc(f.bpos, cap) ||
+                alloc(f.brow0, (size_t)4 * nband() * (h + 1)) || alloc(f.bcnt, (size_t)4 * nband() * h))
                 return VISO_ERR_HIP;
         const int nbk = ((w + p.bucket_width - 1) / p.bucket_width) * ((h + p.bucket_height - 1) / p.bucket_height);
         const int P = kMaxPairBatch, it = std::max(1, p.ransac_iters);
@@ -1327,6 +1478,7 @@ struct viso_svo {
         double* d_extr = nullptr;
         if (alloc(d_sets, sets.size()) || alloc(img, 2 * (size_t)ncam * w * h) ||
             alloc(pa.mcam, (size_t)P * pa.mcap) || alloc(d_extr, (size_t)12 * ncam) ||
+            alloc(pa.obs, (size_t)P * pa.mcap * kObs) || alloc(pa.hok, (size_t)P * it) ||
             alloc(pa.circ, (size_t)P * cap) || alloc(pa.rec8, (size_t)P * 2 * cap) || alloc(pa.keep, (size_t)P * cap) ||
             alloc(pa.uv8, (size_t)P * pa.mcap * 8) || alloc(pa.n_sel, P) || alloc(pa.counts, (size_t)P * it) ||
             alloc(pa.models, (size_t)P * it * 12) || alloc(pa.sel, (size_t)P * pa.mcap) ||
@@ -1369,7 +1521,7 @@ struct viso_svo {
         // responses outside [2, w-3] x [2, h-3] reach the NMS only if margin < n + 2
         const bool dom = p.margin < p.nms_n + 2;
         launch_detect(p.nms_n, dom, g, stream, imgs, d, d_sets, ring, pair0, seg_cap);
-        svo_scan_kernel<<<ni, 1024, 0, stream>>>(d, d_sets, ring, pair0, 4 * tiles, seg_cap);
+        svo_scan_kernel<<<dim3(ni, 5), 1024, 0, stream>>>(d, d_sets, ring, pair0, 4 * tiles, seg_cap);
         svo_describe_kernel<<<dim3(16, ni), 256, 0, stream>>>(imgs, d, d_sets, ring, pair0);
         if (timed) {
             VISO_HIP_CHECK(hipEventRecord(tev[2 * tev_n + 1], stream));
@@ -1392,8 +1544,7 @@ struct viso_svo {
         svo_circle_kernel<<<dim3(std::max(32, 2048 / nq), nq), 256, 0, stream>>>(d, pa, b0);
         svo_bucket_kernel<<<dim3((nbk + 3) / 4, nq), 256, 0, stream>>>(d, pa, b0);
         svo_select_kernel<<<np, 1024, 0, stream>>>(d, pa, b0);
-        svo_ransac_kernel<<<dim3((p.ransac_iters + 3) / 4, np), 256, 0, stream>>>(d, pa, b0);
-        svo_refine_kernel<<<np, 1024, 0, stream>>>(d, pa, b0);
+        launch_ransac(d, pa, b0, np, stream);
         VISO_HIP_CHECK(hipGetLastError());
         return VISO_OK;
     }
@@ -1415,7 +1566,7 @@ struct viso_svo {
 
 namespace {
 int svo_check(const viso_svo_params* p, int ncam) {
-    if (!p || p->width < 32 || p->height < 32 || p->width > 32767 || p->nms_n < 1 ||
+    if (!p || p->width < 32 || p->height < 32 || p->width > 32767 || p->height > 32767 || p->nms_n < 1 ||
         p->nms_n > kMaxNms || p->margin < 8 || p->max_features < 1 || p->max_features > 32768 ||
         p->bucket_width < 1 || p->bucket_height < 1 || p->ransac_iters < 1 || p->gn_iters < 1 ||
         p->disp_max < 0 || p->match_radius < 0 || !(p->base > 0) || !(p->fx > 0) || !(p->fy > 0))
@@ -1743,8 +1894,7 @@ int viso_svo_estimate(viso_svo* s, const int32_t* uv8, int32_t n, int64_t frame,
     const SvoDev d = s->dev();
     PairArgs pa = s->pa;
     pa.frame0 = frame;  // slot 0: the sampler stream of `frame`
-    svo_ransac_kernel<<<dim3((s->p.ransac_iters + 3) / 4, 1), 256, 0, s->stream>>>(d, pa, 0);
-    svo_refine_kernel<<<1, 1024, 0, s->stream>>>(d, pa, 0);
+    launch_ransac(d, pa, 0, 1, s->stream);
     VISO_HIP_CHECK(hipGetLastError());
     VISO_HIP_CHECK(hipStreamSynchronize(s->stream));
     VISO_HIP_CHECK(hipMemcpy(motion12, s->pa.motion, 12 * sizeof(double), hipMemcpyDeviceToHost));
