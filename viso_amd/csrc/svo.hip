@@ -116,20 +116,23 @@ __device__ inline FeatDev set_frame(const PairArgs& a, long long frame, int cam,
 }
 
 // ---------------------------------------------------------------- detect
-// Thread per response column, workgroup = 256 columns x kDTH output rows of
-// one image (grid.z = images of the batch).  The tile's image rows are staged
-// in LDS once (coalesced dword loads); each thread then walks its column down
-// the rows: horizontal tap sums of a new image row from two LDS dwords (dot4),
-// the 5x5 blob / checkerboard responses from a 5-row register window
+// Thread per response column.  A workgroup stages the image rows of a tile
+// (4 x (64 - 2n) output columns x kDTH output rows, plus halos) in LDS once
+// (coalesced dword loads); each wave then owns a 64-column strip (its 64 - 2n
+// output columns and n halo columns either side) and walks it down the rows
+// on its own, with no workgroup barrier in the row loop: horizontal tap sums
+// of a new image row from two LDS dwords (dot4), the 5x5 blob / checkerboard
+// responses from a 5-row register window
 //   B = 7 I + 2 S3x3 - S5x5,   C = g(y-2) + g(y-1) - g(y+1) - g(y+2),
 //   g = (I(x+1) + I(x+2)) - (I(x-2) + I(x-1)),
 // packed as (B, C) 16-bit pairs, so the four classes' strict NMS runs as
 // packed max (B max, C max) and packed min (B min, C min) ops: horizontal
-// neighbour extrema over +-R columns through one LDS row buffer per response
-// row, vertical ones from a (2R+1)-row register window.  Features of an
-// output row are emitted per (row, tile, wave) segment in (x, class) order by
-// ballot ranks.  Responses outside the domain [2, w-3] x [2, h-3] only matter
-// when margin < R + 2 (DOM): then they enter the NMS as -inf / +inf.
+// neighbour extrema over +-n columns through the wave's LDS row buffer,
+// vertical ones from a (2n+1)-row register window.  Features of an output row
+// are emitted per (row, tile, wave) segment in (x, class) order by ballot
+// ranks, with per-class counts.  Responses outside the domain [2, w-3] x
+// [2, h-3] only matter when margin < n + 2 (DOM): then they enter the NMS as
+// -inf / +inf.
 constexpr int kDW = 256;                  // response columns per workgroup
 constexpr int kDTH = 64;                  // output rows per tile
 constexpr int kImgDw = (kDW + 4) / 4;     // LDS dwords per staged image row (260 bytes)
@@ -153,19 +156,21 @@ template <int R, bool DOM>
 __global__ __launch_bounds__(256) void svo_detect_kernel(ImgSrc src, SvoDev p,
                                                          const FeatDev* __restrict__ sets, int ring,
                                                          int pair0, int seg_cap) {
-    constexpr int OW = kDW - 2 * R;   // output columns per tile
+    constexpr int SW = 64 - 2 * R;    // output columns per wave strip
+    constexpr int OW = 4 * SW;        // output columns per tile
     constexpr int RR = kDTH + 2 * R;  // response rows
     constexpr int IR = RR + 4;        // image rows
     constexpr int NV = 2 * R + 1;
     __shared__ uint32_t s_img[IR * kImgDw];
-    __shared__ uint32_t s_rx[2][kDW + 2 * R];                 // P (max view)
-    __shared__ uint32_t s_rn[DOM ? 2 : 1][DOM ? kDW + 2 * R : 1];  // P (min view, DOM only)
+    __shared__ uint32_t s_rx[4][64 + 2 * R];                   // per wave: P (max view)
+    __shared__ uint32_t s_rn[DOM ? 4 : 1][DOM ? 64 + 2 * R : 1];  // P (min view, DOM only)
     const uint8_t* __restrict__ img = src.at(blockIdx.z, p.ncam);
     const FeatDev F = set_of(sets, ring, p.ncam, pair0, blockIdx.z);
     const int w = p.w, h = p.h;
     const int x0 = blockIdx.x * OW, y0 = blockIdx.y * kDTH;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    // ---- stage image rows y0-R-2 .. y0+kDTH+R+1, columns x0-R-2 .. x0-R+257:
+    // ---- stage image rows y0-R-2 .. y0+kDTH+R+1, columns x0-R-2 .. x0-R+257
+    // (the tile uses OW + 2R + 4 <= 260 of them):
     // every load is issued unconditionally (clamped into the image buffer) before
     // the first LDS store, then shifted into place / zeroed where it was clamped
     {
@@ -198,109 +203,125 @@ __global__ __launch_bounds__(256) void svo_detect_kernel(ImgSrc src, SvoDev p,
         }
     }
     __syncthreads();
-    const int x = x0 - R + tid;  // this thread's response column
-    const bool xin = tid >= R && tid < kDW - R && x >= p.margin && x < w - p.margin;
+    const int col = wave * SW + lane;  // this thread's response column, tile-relative (x0 - R + col)
+    const int x = x0 - R + col;
+    const bool xin = lane >= R && lane < 64 - R && x >= p.margin && x < w - p.margin;
     const int tau = p.tau;
-    const int sh = 8 * (tid & 3);
-    const uint32_t* srow = s_img + (tid >> 2);
+    const int sh = 8 * (col & 3);
+    const uint32_t* srow = s_img + (col >> 2);
+    uint32_t* bx = s_rx[wave];
     const int tiles = gridDim.x;
-    int H5[5], H3[5], G[5], Cc[5];
-    s16x2 VX[NV], VN[NV], DP[R + 1], DX[R + 1], DN[R + 1];
-    for (int i = 0; i < IR; ++i) {
-        // taps a0..a4 = image columns x-2 .. x+2 of image row i
-        const uint32_t lo = srow[i * kImgDw], hi = srow[i * kImgDw + 1];
-        const uint32_t win = __builtin_amdgcn_alignbyte(hi, lo, tid & 3);  // a0..a3
-        const int a4 = (int)((hi >> sh) & 0xffu);
+    // Row rings of length L (image row i lives in slot i % L): the row loop is
+    // unrolled L times, so every ring index is a compile-time constant and no
+    // register moves are needed.  Vertical strict-neighbour extrema through a
+    // sliding window of R rows built from power-of-two levels (M2, M4, M8):
+    //   U(c) = max HI(c-R .. c-1) = W(c-1),  D(c) = max HI(c+1 .. c+R) = W(c+R),
+    //   W(i) = max(M_K(i), M_K(i-R+K)), K = largest power of two <= R.
+    constexpr int L = R + 2 > 5 ? R + 2 : 5;
+    constexpr int K = R >= 8 ? 8 : (R >= 4 ? 4 : (R >= 2 ? 2 : 1));
+    int H5[L], H3[L], G[L], Cc[L];
+    s16x2 HX[L], HN[L], X2[L], N2[L], X4[L], N4[L], X8[L], N8[L], WX[L], WN[L], DP[L], DX[L], DN[L];
+    for (int i0 = 0; i0 < IR; i0 += L) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            H5[k] = H5[k + 1];
-            H3[k] = H3[k + 1];
-            G[k] = G[k + 1];
-            Cc[k] = Cc[k + 1];
-        }
-        H5[4] = (int)__builtin_amdgcn_udot4(win, 0x01010101u, 0u, false) + a4;
-        H3[4] = (int)__builtin_amdgcn_udot4(win, 0x01010100u, 0u, false);
-        G[4] = ((int)(win >> 24) + a4) - (int)__builtin_amdgcn_udot4(win, 0x00000101u, 0u, false);
-        Cc[4] = (int)((win >> 16) & 0xffu);
-        if (i < 4) continue;
-        const int j = i - 4;  // response row: y = y0 - R + j
-        const int B = (7 * Cc[2] + 2 * ((H3[1] + H3[2]) + H3[3])) - ((((H5[0] + H5[1]) + H5[2]) + H5[3]) + H5[4]);
-        const int C = (G[0] + G[1]) - (G[3] + G[4]);
-        const s16x2 P = {(short)B, (short)C};
-        s16x2 PX = P, PN = P;
-        if (DOM) {
-            const int y = y0 - R + j;
-            if (x < 2 || x >= w - 2 || y < 2 || y >= h - 2) {
-                PX = s16x2{-32768, -32768};
-                PN = s16x2{32767, 32767};
-            }
-        }
-        uint32_t* bx = s_rx[j & 1];
-        bx[tid + R] = pk_bits(PX);
-        if (DOM) s_rn[j & 1][tid + R] = pk_bits(PN);
-        __syncthreads();
-        s16x2 EX = s16x2{-32768, -32768}, EN = s16x2{32767, 32767};
-#pragma unroll
-        for (int d = 1; d <= R; ++d) {
-            const s16x2 l = pk_of(bx[tid + R - d]), r = pk_of(bx[tid + R + d]);
-            EX = pk_max(EX, pk_max(l, r));
+        for (int u = 0; u < L; ++u) {
+            const int i = i0 + u;
+            if (i >= IR) goto done;
+            auto S = [&](int k) { return (u - k + 4 * L) % L; };  // slot of row i - k
+            // taps a0..a4 = image columns x-2 .. x+2 of image row i
+            const uint32_t lo = srow[i * kImgDw], hi = srow[i * kImgDw + 1];
+            const uint32_t win = __builtin_amdgcn_alignbyte(hi, lo, col & 3);  // a0..a3
+            const int a4 = (int)((hi >> sh) & 0xffu);
+            H5[S(0)] = (int)__builtin_amdgcn_udot4(win, 0x01010101u, 0u, false) + a4;
+            H3[S(0)] = (int)__builtin_amdgcn_udot4(win, 0x01010100u, 0u, false);
+            G[S(0)] = ((int)(win >> 24) + a4) - (int)__builtin_amdgcn_udot4(win, 0x00000101u, 0u, false);
+            Cc[S(0)] = (int)((win >> 16) & 0xffu);
+            if (i < 4) continue;
+            const int j = i - 4;  // response row: y = y0 - R + j (centre image row i - 2)
+            const int B = (7 * Cc[S(2)] + 2 * ((H3[S(3)] + H3[S(2)]) + H3[S(1)])) -
+                          ((((H5[S(4)] + H5[S(3)]) + H5[S(2)]) + H5[S(1)]) + H5[S(0)]);
+            const int C = (G[S(4)] + G[S(3)]) - (G[S(1)] + G[S(0)]);
+            const s16x2 P = {(short)B, (short)C};
+            s16x2 PX = P, PN = P;
             if (DOM) {
-                const uint32_t* bn = s_rn[j & 1];
-                EN = pk_min(EN, pk_min(pk_of(bn[tid + R - d]), pk_of(bn[tid + R + d])));
-            } else {
-                EN = pk_min(EN, pk_min(l, r));
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < NV - 1; ++k) {
-            VX[k] = VX[k + 1];
-            VN[k] = VN[k + 1];
-        }
-        VX[NV - 1] = pk_max(EX, PX);
-        VN[NV - 1] = pk_min(EN, PN);
-#pragma unroll
-        for (int k = 0; k < R; ++k) {
-            DP[k] = DP[k + 1];
-            DX[k] = DX[k + 1];
-            DN[k] = DN[k + 1];
-        }
-        DP[R] = P;
-        DX[R] = EX;
-        DN[R] = EN;
-        if (j < 2 * R) continue;
-        const int yc = y0 + j - 2 * R;  // centre (output) row
-        if (yc >= h) break;             // uniform: no later row of the tile is in the image
-        s16x2 NX = DX[0], NN = DN[0];
-#pragma unroll
-        for (int k = 0; k < NV; ++k)
-            if (k != R) {
-                NX = pk_max(NX, VX[k]);
-                NN = pk_min(NN, VN[k]);
-            }
-        int flags = 0;
-        if (xin && yc >= p.margin && yc < h - p.margin) {
-            const int b = DP[0].x, c = DP[0].y;
-            flags = (b > tau && b > NX.x ? 1 : 0) | (-b > tau && b < NN.x ? 2 : 0) |
-                    (c > tau && c > NX.y ? 4 : 0) | (-c > tau && c < NN.y ? 8 : 0);
-        }
-        const unsigned long long q0 = __ballot(flags & 1), q1 = __ballot(flags & 2),
-                                 q2 = __ballot(flags & 4), q3 = __ballot(flags & 8);
-        const size_t seg = ((size_t)yc * tiles + blockIdx.x) * 4 + wave;
-        const int total = __popcll(q0) + __popcll(q1) + __popcll(q2) + __popcll(q3);
-        if (total) {
-            int pos = (mbcnt64(q0) + mbcnt64(q1)) + (mbcnt64(q2) + mbcnt64(q3));
-            int* list = F.list + seg * seg_cap;
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (flags & (1 << k)) {
-                    if (pos < seg_cap) list[pos] = x | (k << 16);
-                    ++pos;
+                const int y = y0 - R + j;
+                if (x < 2 || x >= w - 2 || y < 2 || y >= h - 2) {
+                    PX = s16x2{-32768, -32768};
+                    PN = s16x2{32767, 32767};
                 }
+            }
+            // the wave's row buffer: LDS ops of one wave complete in order, so the
+            // fences only keep the compiler from moving them across each other
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            bx[lane + R] = pk_bits(PX);
+            if (DOM) s_rn[wave][lane + R] = pk_bits(PN);
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            s16x2 EX = s16x2{-32768, -32768}, EN = s16x2{32767, 32767};
+#pragma unroll
+            for (int d = 1; d <= R; ++d) {
+                const s16x2 l = pk_of(bx[lane + R - d]), r = pk_of(bx[lane + R + d]);
+                EX = pk_max(EX, pk_max(l, r));
+                if (DOM) {
+                    const uint32_t* bn = s_rn[wave];
+                    EN = pk_min(EN, pk_min(pk_of(bn[lane + R - d]), pk_of(bn[lane + R + d])));
+                } else {
+                    EN = pk_min(EN, pk_min(l, r));
+                }
+            }
+            DP[S(0)] = P;
+            DX[S(0)] = EX;
+            DN[S(0)] = EN;
+            HX[S(0)] = pk_max(EX, PX);
+            HN[S(0)] = pk_min(EN, PN);
+            s16x2 MX = HX[S(0)], MN = HN[S(0)], MXo = HX[S(R - K)], MNo = HN[S(R - K)];
+            if (K >= 2) {
+                X2[S(0)] = pk_max(HX[S(0)], HX[S(1)]);
+                N2[S(0)] = pk_min(HN[S(0)], HN[S(1)]);
+                MX = X2[S(0)], MN = N2[S(0)], MXo = X2[S(R - K)], MNo = N2[S(R - K)];
+            }
+            if (K >= 4) {
+                X4[S(0)] = pk_max(X2[S(0)], X2[S(2)]);
+                N4[S(0)] = pk_min(N2[S(0)], N2[S(2)]);
+                MX = X4[S(0)], MN = N4[S(0)], MXo = X4[S(R - K)], MNo = N4[S(R - K)];
+            }
+            if (K >= 8) {
+                X8[S(0)] = pk_max(X4[S(0)], X4[S(4)]);
+                N8[S(0)] = pk_min(N4[S(0)], N4[S(4)]);
+                MX = X8[S(0)], MN = N8[S(0)], MXo = X8[S(R - K)], MNo = N8[S(R - K)];
+            }
+            WX[S(0)] = R == K ? MX : pk_max(MX, MXo);
+            WN[S(0)] = R == K ? MN : pk_min(MN, MNo);
+            if (j < 2 * R) continue;
+            const int yc = y0 + j - 2 * R;  // centre (output) row = response row j - R
+            if (yc >= h) goto done;         // uniform: no later row of the tile is in the image
+            const s16x2 NX = pk_max(pk_max(WX[S(R + 1)], WX[S(0)]), DX[S(R)]);
+            const s16x2 NN = pk_min(pk_min(WN[S(R + 1)], WN[S(0)]), DN[S(R)]);
+            int flags = 0;
+            if (xin && yc >= p.margin && yc < h - p.margin) {
+                const int b = DP[S(R)].x, c = DP[S(R)].y;
+                flags = (b > tau && b > NX.x ? 1 : 0) | (-b > tau && b < NN.x ? 2 : 0) |
+                        (c > tau && c > NX.y ? 4 : 0) | (-c > tau && c < NN.y ? 8 : 0);
+            }
+            const unsigned long long q0 = __ballot(flags & 1), q1 = __ballot(flags & 2),
+                                     q2 = __ballot(flags & 4), q3 = __ballot(flags & 8);
+            const size_t seg = ((size_t)yc * tiles + blockIdx.x) * 4 + wave;
+            if (q0 | q1 | q2 | q3) {
+                int pos = (mbcnt64(q0) + mbcnt64(q1)) + (mbcnt64(q2) + mbcnt64(q3));
+                int* list = F.list + seg * seg_cap;
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (flags & (1 << k)) {
+                        if (pos < seg_cap) list[pos] = x | (k << 16);
+                        ++pos;
+                    }
+            }
+            // per-class counts (strict NMS: <= ceil(64 / (n + 1)) <= 32 per class)
+            if (lane == 0)
+                F.cnt[seg] = __popcll(q0) | (__popcll(q1) << 8) | (__popcll(q2) << 16) | (__popcll(q3) << 24);
         }
-        // per-class counts (strict NMS: <= ceil(64 / (n + 1)) <= 32 per class)
-        if (lane == 0)
-            F.cnt[seg] = __popcll(q0) | (__popcll(q1) << 8) | (__popcll(q2) << 16) | (__popcll(q3) << 24);
     }
+done:;
 }
 
 // exclusive block prefix (1024 threads): wave scans by shuffles + wave totals
@@ -449,12 +470,12 @@ __global__ __launch_bounds__(256) void svo_describe_kernel(ImgSrc src, SvoDev p,
 // scan, then each row's features placed in index order.  The matching
 // searches then visit only the bands their column window overlaps.
 // Bands are the detect kernel's (tile, wave) column segments (wave w of tile
-// t: columns t*ow + 64w - n .. +63, clipped to the tile), so the feature pass
+// t: output columns t*ow + w*(64 - 2n) .. + 63 - 2n), so the feature pass
 // emits the band-major order directly (svo_scan_kernel); this kernel builds
 // the same index for feature sets uploaded by viso_svo_match.
 __device__ inline int band_of(int u, const SvoDev& p) {
     const int t = u / p.ow;
-    return min(max(4 * t + ((u - t * p.ow + p.nms_n) >> 6), 0), p.nband - 1);
+    return min(max(4 * t + (u - t * p.ow) / (64 - 2 * p.nms_n), 0), p.nband - 1);
 }
 
 __global__ __launch_bounds__(1024) void svo_index_kernel(SvoDev p, const FeatDev* __restrict__ sets, int ring,
@@ -512,10 +533,18 @@ __device__ inline int sad32(const uint4 a0, const uint4 a1, const uint4 b0, cons
     return (int)s;
 }
 
+// wave minimum by DPP butterflies (quad_perm xor 1 / xor 2, then half-row /
+// row mirrors on the already uniform groups) and the gfx950 permlane16/32
+// swaps: every lane ends with the minimum.  All 64 lanes must be active.
 __device__ inline unsigned wave_min_u32(unsigned v) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) v = min(v, (unsigned)__shfl_xor((int)v, o, 64));
-    return v;
+    v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));
+    v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));
+    v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false));
+    v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false));
+    const auto a = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    v = min((unsigned)a[0], (unsigned)a[1]);
+    const auto b = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return min((unsigned)b[0], (unsigned)b[1]);
 }
 
 // The best candidate of a search: feature index j (-1: none), its u, v and
@@ -530,8 +559,8 @@ struct Cand {
 // class-c lists of the column bands the window overlaps give one contiguous
 // position range each (lanes 0..nq-1 load the bounds, a wave scan
 // concatenates them); every candidate's packed (u, v, class), index and
-// descriptor are loaded together, 128 candidates per step.  Wave-uniform
-// arguments and result.
+// descriptor are loaded together, 128 candidates per step; the winner's data
+// is reloaded by scalar loads.  Wave-uniform arguments and result.
 __device__ Cand best_match(const FeatDev& S, const SvoDev& p, int u, int v, int c, uint4 q0, uint4 q1,
                            int du_lo, int du_hi, int dv) {
     Cand r;
@@ -559,8 +588,6 @@ __device__ Cand best_match(const FeatDev& S, const SvoDev& p, int u, int v, int 
     const int total = __shfl(incl, 63, 64);
     const int excl = incl - len;
     unsigned best = 0xffffffffu;
-    int bu = 0, bv = 0;
-    uint4 bd0 = make_uint4(0, 0, 0, 0), bd1 = bd0;
     // candidate slot k of the concatenated ranges -> its index position
     auto pos_of = [&](int k) {
         int ps = 0;
@@ -573,14 +600,7 @@ __device__ Cand best_match(const FeatDev& S, const SvoDev& p, int u, int v, int 
     auto consider = [&](int e, int j, uint4 d0, uint4 d1) {
         const int dd = u - (e & 0x7fff);
         if (dd < du_lo || dd > du_hi) return;
-        const unsigned key = ((unsigned)sad32(q0, q1, d0, d1) << 15) | (unsigned)j;
-        if (key < best) {
-            best = key;
-            bu = e & 0x7fff;
-            bv = (e >> 15) & 0x7fff;
-            bd0 = d0;
-            bd1 = d1;
-        }
+        best = min(best, ((unsigned)sad32(q0, q1, d0, d1) << 15) | (unsigned)j);
     };
     for (int k0 = 0; k0 < total; k0 += 128) {
         // two candidates per lane, all loads issued before the first use;
@@ -608,25 +628,41 @@ __device__ Cand best_match(const FeatDev& S, const SvoDev& p, int u, int v, int 
         if (ka < total) consider(ea, ja, a0, a1);
         if (two && kb < total) consider(eb, jb, b0, b1);
     }
-    const unsigned wbest = wave_min_u32(best);
+    const unsigned wbest = (unsigned)__builtin_amdgcn_readfirstlane((int)wave_min_u32(best));
     if (wbest == 0xffffffffu) return r;
-    const int owner = __builtin_ctzll(__ballot(best == wbest));
-    r.j = (int)(wbest & 0x7fffu);
-    r.u = __builtin_amdgcn_readlane(bu, owner);
-    r.v = __builtin_amdgcn_readlane(bv, owner);
-    r.d0 = make_uint4(__builtin_amdgcn_readlane(bd0.x, owner), __builtin_amdgcn_readlane(bd0.y, owner),
-                      __builtin_amdgcn_readlane(bd0.z, owner), __builtin_amdgcn_readlane(bd0.w, owner));
-    r.d1 = make_uint4(__builtin_amdgcn_readlane(bd1.x, owner), __builtin_amdgcn_readlane(bd1.y, owner),
-                      __builtin_amdgcn_readlane(bd1.z, owner), __builtin_amdgcn_readlane(bd1.w, owner));
+    // the winner's coordinates and descriptor: uniform (scalar) loads
+    const int j = (int)(wbest & 0x7fffu);
+    r.j = j;
+    r.u = S.u[j];
+    r.v = S.v[j];
+    const uint4* dj = reinterpret_cast<const uint4*>(S.d + (size_t)j * kDesc);
+    r.d0 = dj[0];
+    r.d1 = dj[1];
     return r;
 }
 
-// wave per current-left feature of (timestep, camera) slot q = b0 * ncam +
-// blockIdx.y; circ[i2] = {l1, r1, r2, -} and rec8[i2] = {u_l1, v_l1, u_r1,
-// v_r1, u_l2, v_l2, u_r2, v_r2}, or circ[i2].x = rec8[i2].x = -1.  The four
-// searches chain through the winners' coordinates and descriptors.
-__global__ __launch_bounds__(256) void svo_circle_kernel(SvoDev p, PairArgs pa, int b0) {
-    const int q = b0 * pa.ncam + blockIdx.y;
+// Workgroup -> (slot, chunk) so that consecutive (timestep, camera) slots
+// share an XCD: blocks b and b + 8 are dealt to the same XCD (MI355X guide,
+// workgroup dispatch), so block b serves slot (b % 8) * per + j, chunk c with
+// b / 8 = j * chunks + c.  A slot's four feature sets (and the next slot's
+// previous pair) then stay in one XCD's L2.  Returns false for padding blocks.
+__device__ inline bool xcd_slot(int nq, int chunks, int& slot, int& chunk) {
+    const int per = (nq + 7) >> 3;
+    const int b = blockIdx.x, s = b >> 3;
+    const int j = s / chunks;
+    chunk = s - j * chunks;
+    slot = (b & 7) * per + j;
+    return j < per && slot < nq;
+}
+
+// wave per current-left feature of (timestep, camera) slot q (b0 * ncam +
+// the block's slot); circ[i2] = {l1, r1, r2, -} and rec8[i2] = {u_l1, v_l1,
+// u_r1, v_r1, u_l2, v_l2, u_r2, v_r2}, or circ[i2].x = rec8[i2].x = -1.  The
+// four searches chain through the winners' coordinates and descriptors.
+__global__ __launch_bounds__(256) void svo_circle_kernel(SvoDev p, PairArgs pa, int b0, int nq, int chunks) {
+    int qr, chunk;
+    if (!xcd_slot(nq, chunks, qr, chunk)) return;
+    const int q = b0 * pa.ncam + qr;
     const int pb = q / pa.ncam, cam = q - pb * pa.ncam;
     const long long fr = pa.frame0 + pb;
     const FeatDev L1 = set_frame(pa, fr - 1, cam, 0), R1 = set_frame(pa, fr - 1, cam, 1),
@@ -637,7 +673,7 @@ __global__ __launch_bounds__(256) void svo_circle_kernel(SvoDev p, PairArgs pa, 
     const int n2 = *L2.n;
     const int D = p.disp_max, Rr = p.radius;
     const int lane = threadIdx.x & 63;
-    for (int i2 = blockIdx.x * 4 + (threadIdx.x >> 6); i2 < n2; i2 += gridDim.x * 4) {
+    for (int i2 = chunk * 4 + (threadIdx.x >> 6); i2 < n2; i2 += chunks * 4) {
         const int c = L2.c[i2], u2 = L2.u[i2], v2 = L2.v[i2];
         const uint4* dq = reinterpret_cast<const uint4*>(L2.d + (size_t)i2 * kDesc);
         const uint4 a = dq[0], b = dq[1];
@@ -1431,7 +1467,7 @@ struct viso_svo {
         d.gn_iters = p.gn_iters;
         d.cap = p.max_features;
         d.ncam = ncam;
-        d.ow = kDW - 2 * p.nms_n;
+        d.ow = 4 * (64 - 2 * p.nms_n);
         d.nband = 4 * ((p.width + d.ow - 1) / d.ow);
         d.fx = p.fx;
         d.fy = p.fy;
@@ -1454,7 +1490,7 @@ struct viso_svo {
     }
     int init() {
         const int w = p.width, h = p.height, cap = p.max_features;
-        tiles = (w + kDW - 2 * p.nms_n - 1) / (kDW - 2 * p.nms_n);
+        tiles = (w + 4 * (64 - 2 * p.nms_n) - 1) / (4 * (64 - 2 * p.nms_n));
         // strict NMS of radius n: same-class maxima of a row are > n apart, so
         // a wave's 64 columns hold at most ceil(64 / (n + 1)) per class
         seg_cap = 4 * ((64 + p.nms_n) / (p.nms_n + 1));
@@ -1541,7 +1577,8 @@ struct viso_svo {
         const int nbk = ((p.width + p.bucket_width - 1) / p.bucket_width) *
                         ((p.height + p.bucket_height - 1) / p.bucket_height);
         const int nq = np * ncam;  // (timestep, camera) slots
-        svo_circle_kernel<<<dim3(std::max(32, 2048 / nq), nq), 256, 0, stream>>>(d, pa, b0);
+        const int chunks = std::max(32, 2048 / nq);
+        svo_circle_kernel<<<8 * ((nq + 7) / 8) * chunks, 256, 0, stream>>>(d, pa, b0, nq, chunks);
         svo_bucket_kernel<<<dim3((nbk + 3) / 4, nq), 256, 0, stream>>>(d, pa, b0);
         svo_select_kernel<<<np, 1024, 0, stream>>>(d, pa, b0);
         launch_ransac(d, pa, b0, np, stream);
@@ -1863,7 +1900,7 @@ int viso_svo_match(viso_svo* s, const int32_t* const* u4, const int32_t* const* 
     svo_index_kernel<<<4, 1024, 0, s->stream>>>(d, s->d_sets, s->ring, (int)(p1 % s->ring));
     PairArgs pa = s->pa;
     pa.frame0 = (long long)p2;  // slot 0 = pair p2 (previous: p1)
-    svo_circle_kernel<<<dim3(1024, 1), 256, 0, s->stream>>>(d, pa, 0);
+    svo_circle_kernel<<<8 * 1024, 256, 0, s->stream>>>(d, pa, 0, 1, 1024);
     VISO_HIP_CHECK(hipGetLastError());
     VISO_HIP_CHECK(hipStreamSynchronize(s->stream));
     std::vector<int4> res((size_t)std::max(1, n4[2]));
