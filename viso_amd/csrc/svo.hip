@@ -45,7 +45,8 @@ __constant__ int c_p16[16][2] = {{-5, -1}, {-5, 1}, {-3, -3}, {-3, 3}, {-1, -5},
                                  {3, -3},  {3, 3},  {5, -1},  {5, 1}};
 
 struct SvoDev {  // kernel view of the parameters
-    int w, h, nms_n, tau, margin, disp_max, radius, bw, bh, bmax, iters, gn_iters, cap, nband, ow, ncam;
+    int w, h, nms_n, tau, margin, disp_max, radius, bw, bh, bmax, iters, gn_iters, cap, nband, ow, ncam, sw;
+    float inv_ow, inv_sw;  // 1 / ow, 1 / sw (division-free band_of)
     double fx, fy, cu, cv, base, th2, eps;
     uint64_t seed;
 };
@@ -473,9 +474,17 @@ __global__ __launch_bounds__(256) void svo_describe_kernel(ImgSrc src, SvoDev p,
 // t: output columns t*ow + w*(64 - 2n) .. + 63 - 2n), so the feature pass
 // emits the band-major order directly (svo_scan_kernel); this kernel builds
 // the same index for feature sets uploaded by viso_svo_match.
+// floor(a / b) for 0 <= a < 2^24 from a float reciprocal, corrected to exact
+__device__ inline int div_floor(int a, int b, float inv_b) {
+    int q = (int)((float)a * inv_b);
+    q -= q * b > a ? 1 : 0;
+    q += (q + 1) * b <= a ? 1 : 0;
+    return q;
+}
+
 __device__ inline int band_of(int u, const SvoDev& p) {
-    const int t = u / p.ow;
-    return min(max(4 * t + (u - t * p.ow) / (64 - 2 * p.nms_n), 0), p.nband - 1);
+    const int t = div_floor(u, p.ow, p.inv_ow);
+    return min(max(4 * t + div_floor(u - t * p.ow, p.sw, p.inv_sw), 0), p.nband - 1);
 }
 
 __global__ __launch_bounds__(1024) void svo_index_kernel(SvoDev p, const FeatDev* __restrict__ sets, int ring,
@@ -547,6 +556,8 @@ __device__ inline unsigned wave_min_u32(unsigned v) {
     return min((unsigned)b[0], (unsigned)b[1]);
 }
 
+constexpr int kMaxQB = 8;  // column bands a search window may span (svo_check)
+
 // The best candidate of a search: feature index j (-1: none), its u, v and
 // descriptor (so the next search of the circle needs no extra loads).
 struct Cand {
@@ -568,32 +579,38 @@ __device__ Cand best_match(const FeatDev& S, const SvoDev& p, int u, int v, int 
     r.u = r.v = 0;
     r.d0 = r.d1 = make_uint4(0, 0, 0, 0);
     const int lane = threadIdx.x & 63, h = p.h;
+    u = __builtin_amdgcn_readfirstlane(u);
+    v = __builtin_amdgcn_readfirstlane(v);
+    c = __builtin_amdgcn_readfirstlane(c);
     const int va = max(v - dv, 0), vb = min(v + dv, h - 1);
     const int ua = u - du_hi, ub = u - du_lo;
     if (ub < 0) return r;
     const int ba = band_of(max(ua, 0), p), bq = band_of(ub, p);
-    const int nq = min(bq - ba + 1, 64);  // (a window over > 64 bands: disp_max > ~3900)
+    const int nq = bq - ba + 1;  // <= kMaxQB: windows up to ~7 bands (disp_max 255 spans <= 6)
     int s = 0, len = 0;
-    if (lane < nq) {
+    if (lane < min(nq, kMaxQB)) {
         const int* rw = S.brow0 + (size_t)(c * p.nband + ba + lane) * (h + 1);
         s = rw[va];
         len = rw[vb + 1] - s;
     }
-    int incl = len;
+    // band l covers candidate slots [E[l], E[l + 1]) at positions k + O[l]
+    // (scalars; bands past nq have len = 0)
+    int E[kMaxQB], O[kMaxQB], total = 0;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int t = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += t;
+    for (int l = 0; l < kMaxQB; ++l) {
+        const int sl = __builtin_amdgcn_readlane(s, l), ll = __builtin_amdgcn_readlane(len, l);
+        E[l] = total;
+        O[l] = sl - total;
+        total += ll;
     }
-    const int total = __shfl(incl, 63, 64);
-    const int excl = incl - len;
     unsigned best = 0xffffffffu;
     // candidate slot k of the concatenated ranges -> its index position
     auto pos_of = [&](int k) {
-        int ps = 0;
-        for (int l = 0; l < nq; ++l) {
-            const int el = __builtin_amdgcn_readlane(excl, l), sl = __builtin_amdgcn_readlane(s, l);
-            if (k >= el) ps = sl + (k - el);
+        int ps = k + O[0];
+#pragma unroll
+        for (int l = 1; l < kMaxQB; ++l) {
+            if (l >= nq) break;
+            ps = k >= E[l] ? k + O[l] : ps;
         }
         return ps;
     };
@@ -1467,7 +1484,10 @@ struct viso_svo {
         d.gn_iters = p.gn_iters;
         d.cap = p.max_features;
         d.ncam = ncam;
-        d.ow = 4 * (64 - 2 * p.nms_n);
+        d.sw = 64 - 2 * p.nms_n;
+        d.ow = 4 * d.sw;
+        d.inv_ow = 1.0f / (float)d.ow;
+        d.inv_sw = 1.0f / (float)d.sw;
         d.nband = 4 * ((p.width + d.ow - 1) / d.ow);
         d.fx = p.fx;
         d.fy = p.fy;
@@ -1612,6 +1632,9 @@ int svo_check(const viso_svo_params* p, int ncam) {
     const int nby = (p->height + p->bucket_height - 1) / p->bucket_height;
     if ((long long)nbx * nby > kMaxBuckets) return VISO_ERR_ARG;
     if ((long long)ncam * nbx * nby * p->bucket_max > 64LL * kMaxChunks) return VISO_ERR_ARG;  // M bound
+    // a search window spans at most ceil(width / band width) + 1 <= kMaxQB column bands
+    const long long win = std::max((long long)p->disp_max + 1, 2LL * p->match_radius + 1);
+    if (win > (long long)(kMaxQB - 1) * (64 - 2 * p->nms_n)) return VISO_ERR_ARG;
     return VISO_OK;
 }
 }  // namespace
