@@ -91,7 +91,7 @@ def measure_svo(args, seq, left, right, d_left, d_right, W, H, log):
     gbs = feat_bytes / (ms * 1e-3) / 1e9 if ms else None
     out = {"pairs": n, "pairs_per_s": round(n / dt, 1), "us_per_pair": round(1e6 * dt / n, 2),
            "feature_pass": {"kernels": "svo_detect_kernel + svo_scan_kernel + svo_describe_kernel",
-                            "pairs": pairs, "batches": -(-pairs // 64), "ms": round(ms, 4),
+                            "pairs": pairs, "batches": -(-pairs // 128), "ms": round(ms, 4),
                             "us_per_pair": round(1e3 * ms / pairs, 3) if pairs else None,
                             "achieved_GBps": round(gbs, 1) if gbs else None,
                             "peak_GBps": HBM_PEAK_GBS,

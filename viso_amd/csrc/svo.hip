@@ -1344,11 +1344,13 @@ __global__ __launch_bounds__(kRefineThreads) void svo_refine_kernel(SvoDev p, Pa
 // Tail of a batch (one wave): feature counts, each pair's Tr^-1 = [R^T,
 // -R^T t] lane-parallel, then the camera poses T_wc <- T_wc * Tr^-1 composed
 // in pair order by lane 0 and written back lane-parallel.
-__global__ __launch_bounds__(64) void svo_pose_kernel(PairArgs pa, int nb, double* __restrict__ pose,
+constexpr int kPoseThreads = 128;  // >= timesteps per batch
+
+__global__ __launch_bounds__(kPoseThreads) void svo_pose_kernel(PairArgs pa, int nb, double* __restrict__ pose,
                                                       double* __restrict__ pose_log, long long max_poses) {
-    __shared__ double s_inv[64][12];
-    __shared__ double s_pose[64][12];
-    __shared__ int s_ok[64];
+    __shared__ double s_inv[kPoseThreads][12];
+    __shared__ double s_pose[kPoseThreads][12];
+    __shared__ int s_ok[kPoseThreads];
     const int b = threadIdx.x;
     if (b < nb) {
         const long long fr = pa.frame0 + b;
@@ -1397,7 +1399,7 @@ __global__ __launch_bounds__(64) void svo_pose_kernel(PairArgs pa, int nb, doubl
         for (int i = 0; i < 12; ++i) pose[i] = P[i];
     }
     __syncthreads();
-    for (int q = b; q < nb * 12; q += 64) {
+    for (int q = b; q < nb * 12; q += kPoseThreads) {
         const int k = q / 12, i = q - k * 12;
         const long long fr = pa.frame0 + k;
         if (fr < max_poses) pose_log[12 * fr + i] = s_pose[k][i];
@@ -1441,7 +1443,7 @@ void launch_detect(int R, bool dom, dim3 g, hipStream_t st, const ImgSrc& imgs, 
 using namespace viso;
 
 struct viso_svo {
-    static constexpr int kMaxPairBatch = 64;   // camera pairs per batch (feature pass + estimation)
+    static constexpr int kMaxPairBatch = 128;  // camera pairs per batch (feature pass + estimation)
     viso_svo_params p{};
     int ncam = 1;           // stereo cameras per timestep (> 1: rig, BASELINE.json configs[4])
     int tb = kMaxPairBatch; // timesteps per batch: kMaxPairBatch / ncam
@@ -1613,7 +1615,7 @@ struct viso_svo {
         rc = estimate((long long)frame, b0, nb - b0);
         if (rc) return rc;
         pa.frame0 = (long long)frame;
-        svo_pose_kernel<<<1, 64, 0, stream>>>(pa, nb, pose, pose_log, (long long)max_poses);
+        svo_pose_kernel<<<1, kPoseThreads, 0, stream>>>(pa, nb, pose, pose_log, (long long)max_poses);
         VISO_HIP_CHECK(hipGetLastError());
         frame += nb;
         last_b = nb - 1;
