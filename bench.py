@@ -62,6 +62,9 @@ def parse():
     ap.add_argument("--no-svo", action="store_true", help="skip the stereo-VO side measurement")
     ap.add_argument("--svo-cpu-pairs", type=int, default=12,
                     help="pairs of the stereo-VO CPU spec timed for its baseline (0 = skip)")
+    ap.add_argument("--kitti", default=os.environ.get("VISO_KITTI", ""),
+                    help="KITTI odometry data instead of the synthetic sequence: a sequence directory "
+                         "(image_0/, image_1/, calib.txt) or a root with sequences/NN (rank r reads NN = r)")
     ap.add_argument("--rig-steps", type=int, default=64,
                     help="timesteps of the 4-camera rig measurement (configs[4]; 0 = skip)")
     return ap.parse_args()
@@ -187,11 +190,27 @@ def main():
     W, H = args.width, args.height
     n_break = args.batch  # one extra chunk after the timed region: per-kernel breakdown
     n_total = args.warmup + args.steps + n_break
-    seq = Sequence(W, H, seed=sequence_seed(rank))
+    source = "synthetic"
+    if args.kitti:
+        # real KITTI-format grey pairs (PNG decoded by the library's own loader,
+        # include/viso/viso_io.h); the frame size is the sequence's own
+        from types import SimpleNamespace
+
+        from viso_amd.kitti import KittiSequence
+        root = args.kitti
+        if not os.path.isdir(os.path.join(root, "image_0")):
+            root = os.path.join(root, "sequences", f"{rank:02d}")
+        seq = KittiSequence(root)
+        seq.p = SimpleNamespace(baseline=seq.baseline)
+        W, H = seq.width, seq.height
+        n_total = min(n_total, len(seq))
+        source = f"KITTI {root}"
+    else:
+        seq = Sequence(W, H, seed=sequence_seed(rank))
     t0 = time.time()
     left = np.stack([seq.image(f, 0) for f in range(n_total)])
     right = np.stack([seq.image(f, 1) for f in range(n_total)])
-    log(f"[rank {rank}] rendered {n_total} stereo pairs in {time.time() - t0:.1f}s")
+    log(f"[rank {rank}] loaded {n_total} stereo pairs ({source}) in {time.time() - t0:.1f}s")
     d_left = torch.from_numpy(left).to(f"cuda:{local}")
     d_right = torch.from_numpy(right).to(f"cuda:{local}")
     torch.cuda.synchronize()
@@ -334,13 +353,15 @@ def main():
             "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic" if source == "synthetic" else "real (KITTI-format PNG pairs)",
             "config": {"workload": (f"configs[1]: one {W}x{H} grey stereo sequence per GPU, "
                                     "KITTI seq-00 intrinsics" if (W, H) == (1242, 375) else
                                     f"one {W}x{H} grey stereo sequence per GPU (configs[2] size "
                                     "when 1920x1080), KITTI seq-00 intrinsics")
-                                   + ", synthetic KITTI-like frames (KITTI absent offline), "
-                                   "tracking enabled",
+                                   + (", synthetic KITTI-like frames (KITTI absent offline), "
+                                      if source == "synthetic" else f", {source}, ")
+                                   + "tracking enabled",
                        "width": W, "height": H, "map_points": n_map,
                        "ingest_batch": args.batch, "parallelism": f"independent sequences x{world}"},
             "roofline": roofline,

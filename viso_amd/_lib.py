@@ -96,6 +96,11 @@ SIGNATURES = {
     "viso_svo_rig_process": [_vp, _vp, _vp, _vp, _vp],
     "viso_svo_rig_process_device": [_vp, _vp, _vp, _i32, ctypes.c_int64, _i32],
     "viso_svo_get_match_cams": [_vp, _vp, _sz, _vp],
+    # frame source (include/viso/viso_io.h)
+    "viso_png_info": [ctypes.c_char_p, _vp, _vp],
+    "viso_png_read_grey": [ctypes.c_char_p, _vp, _sz, _vp, _vp],
+    "viso_png_decode_grey": [_vp, _sz, _vp, _sz, _vp, _vp],
+    "viso_kitti_calib": [ctypes.c_char_p, _vp, _vp, _vp, _vp, _vp],
 }
 _RESTYPES = {"viso_version": ctypes.c_char_p}
 

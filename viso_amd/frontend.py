@@ -157,7 +157,6 @@ class FrameSequence:
         path = os.path.join(self.location_, f"{Keyframe.GetNextId() + 1}.png")
         if not os.path.exists(path):
             return False  # the reference silently skips a missing file
-        from PIL import Image
-        img = np.asarray(Image.open(path).convert("L"), dtype=np.uint8)
-        self.handler_.OnNewFrame(Keyframe(img))
+        from .kitti import read_png  # cv::imread(path, 0) restated (include/viso/viso_io.h)
+        self.handler_.OnNewFrame(Keyframe(read_png(path)))
         return True
