@@ -354,7 +354,7 @@ def main():
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic" if source == "synthetic" else "real (KITTI-format PNG pairs)",
+            "data": "synthetic" if source == "synthetic" else f"KITTI-format PNG pairs ({source})",
             "config": {"workload": (f"configs[1]: one {W}x{H} grey stereo sequence per GPU, "
                                     "KITTI seq-00 intrinsics" if (W, H) == (1242, 375) else
                                     f"one {W}x{H} grey stereo sequence per GPU (configs[2] size "
