@@ -173,6 +173,37 @@ __device__ inline double wave_tree_sum_dpp(double v) {
     return a + b;
 }
 
+__device__ inline double dsel(bool c, double a, double b) { return c ? a : b; }
+
+// The canonical wave trees of three values at once: reduce-scatter over the
+// xor-1 / xor-2 levels (lane class (b1, b0) = (0,0) / (0,1) / (1,0) keeps a /
+// b / c, (1,1) a zero), then true xor-4 / xor-8 partners (DPP row_shr /
+// row_shl by 4 / 8 + select) and the permlane16 / permlane32 swaps.  Every
+// partial sum is the one wave_tree_sum_dpp forms (f64 + is commutative), so
+// the results are bit-identical, at about half the instructions of three
+// separate trees.  Results read from lanes 0, 1, 2.  Requires EXEC = all lanes.
+__device__ inline void wave_tree_sum3(double a, double b, double c, double& ra, double& rb, double& rc) {
+    const int lane = threadIdx.x & 63;
+    const bool b0 = lane & 1, b1 = lane & 2, b2 = lane & 4, b3 = lane & 8;
+    const double p = (b0 ? b : a) + dpp_f64<0xB1>(b0 ? a : b);      // even: a pairs, odd: b pairs
+    const double q = (b0 ? 0.0 : c) + dpp_f64<0xB1>(b0 ? c : 0.0);  // even: c pairs, odd: 0
+    double v = (b1 ? q : p) + dpp_f64<0x4E>(b1 ? p : q);
+    // both DPP moves are evaluated by every lane (a conditional DPP would run
+    // under a partial EXEC and read inactive lanes), then selected
+    const double r4 = dpp_f64<0x114>(v), l4 = dpp_f64<0x104>(v);  // row_shr / row_shl by 4
+    v = v + dsel(b2, r4, l4);                                        // lane ^ 4
+    const double r8 = dpp_f64<0x118>(v), l8 = dpp_f64<0x108>(v);  // row_shr / row_shl by 8
+    v = v + dsel(b3, r8, l8);                                        // lane ^ 8
+    double x, y;
+    permlane16_swap_f64(v, v, x, y);
+    v = x + y;
+    permlane32_swap_f64(v, v, x, y);
+    v = x + y;
+    ra = readlane_f64(v, 0);
+    rb = readlane_f64(v, 1);
+    rc = readlane_f64(v, 2);
+}
+
 // 28 canonical wave trees at once by reduce-scatter: at butterfly level s
 // (partner lane ^ 2^s, ascending) every lane keeps half of its remaining
 // values and adds the partner's copy of that half, so each value's partial
@@ -181,7 +212,6 @@ __device__ inline double wave_tree_sum_dpp(double v) {
 // and xor 32 by v_permlane16_swap / v_permlane32_swap.  On return, lane l (and l^32)
 // holds value index 14*b0 + 7*b1 + 4*b2 + 2*b3 + b4 (b = bits of l) when
 // 4*b2 + 2*b3 + b4 < 7; the other 4 lane classes hold garbage.
-__device__ inline double dsel(bool c, double a, double b) { return c ? a : b; }
 
 template <int CTRL>
 __device__ inline double dpp_or0(double v) {

@@ -112,9 +112,8 @@ __device__ inline LkTemplate lk_prepare(const uint8_t* __restrict__ img1, int w1
     t.J0 = -gx;
     t.J1 = -gy;
     t.I1 = sample_px(img1, w1, h1, ref_x, ref_y);
-    const double H00 = wave_tree_sum_dpp(t.J0 * t.J0);
-    const double H01 = wave_tree_sum_dpp(t.J0 * t.J1);
-    const double H11 = wave_tree_sum_dpp(t.J1 * t.J1);
+    double H00, H01, H11;
+    wave_tree_sum3(t.J0 * t.J0, t.J0 * t.J1, t.J1 * t.J1, H00, H01, H11);
     const double H10 = H01;  // J1*J0 == J0*J1 leaf by leaf
     const double invdet = 1.0 / (H00 * H11 - H10 * H01);
     t.i00 = H11 * invdet;
@@ -150,9 +149,8 @@ __device__ inline LkResult lk_iterate(const LkTemplate& t, int w1, int h1,
             break;
         }
         const double e = t.I1 - sample_win(img2, w2, h2, cur_x + dx, cur_y + dy, win);
-        const double B0 = wave_tree_sum_dpp(-t.J0 * e);
-        const double B1 = wave_tree_sum_dpp(-t.J1 * e);
-        cost = wave_tree_sum_dpp(e * e);
+        double B0, B1;
+        wave_tree_sum3(-t.J0 * e, -t.J1 * e, e * e, B0, B1, cost);
         const double u0 = t.i00 * B0 + t.i01 * B1;
         const double u1 = t.i10 * B0 + t.i11 * B1;
         if (isnan(u0)) {
