@@ -13,7 +13,8 @@
  *   - RGB / RGBA / palette (8-bit): alpha dropped (png_set_strip_alpha),
  *     palette expanded, then libpng 1.6's png_set_rgb_to_gray(.., 0.299,
  *     0.587) without gamma tables: grey = r if r == g == b, else
- *     (9798 r + 19235 g + 3735 b) >> 15 (truncating);
+ *     (9797 r + 19234 g + 3737 b) >> 15 (truncating; libpng's fixed-point
+ *     weights 0.299 * 32768 and 0.587 * 32768 rounded down, blue the rest);
  *   - 16-bit colour is rejected (VISO_ERR_ARG).
  * Parity of the colour conversion against OpenCV itself is unpinned (neither
  * OpenCV nor libpng is in the image); grey PNGs (KITTI) are exact.

@@ -351,91 +351,143 @@ __device__ inline int block_excl_scan(int v, int* s_w, int& total) {
 __device__ inline int bytesum(int c) { return (c & 0xff) + ((c >> 8) & 0xff) + ((c >> 16) & 0xff) + ((c >> 24) & 0xff); }
 __device__ inline int pack_uvc(int u, int v, int c) { return u | (v << 15) | (c << 30); }
 
-// Per image, five workgroups of 1024 threads (blockIdx.y):
-//   4     row-major exclusive prefix over the segment counts -> row index row0
-//         and the features' u, v, class in that order;
-//   k < 4 the class-k lists of the class-band index: the same row-major prefix
-//         (the features' indices, capacity truncation), the base of class k
-//         (kept features of the classes below), then the band-major prefix of
-//         the class-k counts over (band, row) and the scatter.
+// Per image, one workgroup of 1024 threads, every phase parallel over rows,
+// (column, row-chunk) items or segments:
+//   1. row totals and each segment's offset within its row (thread per row);
+//   2. exclusive scan of the row totals -> row starts; segment offsets made
+//      absolute; row0 / n (capped at the feature capacity);
+//   3. class-band index: column kb = class k x band (segment column s), rows
+//      ascending; the kept (row-major index < cap) class-k counts summed per
+//      (column, chunk of CR rows), one exclusive scan over the items in
+//      (column, chunk) order = the index order, then brow0 row by row;
+//   4. thread per segment: the features' u, v, class at their row-major index
+//      and their index entries (rank among the segment's class-k entries).
+constexpr int kScanItems = 8192;
+
 __global__ __launch_bounds__(1024) void svo_scan_kernel(SvoDev p, const FeatDev* __restrict__ sets, int ring,
                                                         int pair0, int segs, int seg_cap) {
     const FeatDev F = set_of(sets, ring, p.ncam, pair0, blockIdx.x);
     __shared__ int s_w[16];
-    const int h = p.h, n = h * segs;
-    const int tid = threadIdx.x, k = blockIdx.y;
-    const int per = (n + 1023) / 1024;
-    const int b = min(tid * per, n), e = min(b + per, n);
-    int s = 0;
-    for (int i = b; i < e; ++i) s += bytesum(F.cnt[i]);
-    int total;
-    int acc = block_excl_scan(s, s_w, total);
-    if (k == 4) {
-        for (int i = b; i < e; ++i) {
-            const int y = i / segs;
-            if (i == y * segs) F.row0[y] = min(acc, p.cap);
-            const int c = bytesum(F.cnt[i]);
-            const int* list = F.list + (size_t)i * seg_cap;
-            for (int q = 0; q < c; ++q) {
-                const int o = acc + q;
-                if (o >= p.cap) break;
-                const int ent = list[q];
-                F.u[o] = ent & 0xffff;
-                F.v[o] = y;
-                F.c[o] = ent >> 16;
-            }
-            acc += c;
+    __shared__ int s_total;
+    __shared__ int s_item[kScanItems];
+    const int h = p.h, tid = threadIdx.x, cap = p.cap;
+    int* off = F.bcnt;                      // [h][segs] offset of each segment
+    int* rs = F.bcnt + (size_t)h * segs;    // [h] row starts (uncapped)
+    // ---- 1
+    for (int y = tid; y < h; y += 1024) {
+        const int* c = F.cnt + (size_t)y * segs;
+        int* o = off + (size_t)y * segs;
+        int acc = 0;
+#pragma unroll 8
+        for (int s = 0; s < segs; ++s) {
+            o[s] = acc;
+            acc += bytesum(c[s]);
+        }
+        rs[y] = acc;
+    }
+    __syncthreads();
+    // ---- 2
+    {
+        const int per = (h + 1023) / 1024, b = min(tid * per, h), e = min(b + per, h);
+        int sum = 0;
+        for (int y = b; y < e; ++y) sum += rs[y];
+        int total;
+        int acc = block_excl_scan(sum, s_w, total);
+        for (int y = b; y < e; ++y) {
+            const int t = rs[y];
+            rs[y] = acc;
+            F.row0[y] = min(acc, cap);
+            acc += t;
         }
         if (tid == 0) {
-            F.row0[h] = min(total, p.cap);
-            *F.n = min(total, p.cap);
+            F.row0[h] = min(total, cap);
+            *F.n = min(total, cap);
+            s_total = total;
         }
-        return;
     }
-    // class-k entries of segment i among its first min(count, cap - off) entries
-    auto kept = [&](int i, int kk, int c4, int o0) {
-        const int c = bytesum(c4), lim = min(c, max(p.cap - o0, 0));
-        if (lim == c) return (c4 >> (8 * kk)) & 0xff;
-        const int* list = F.list + (size_t)i * seg_cap;
+    __syncthreads();
+    for (int y = tid; y < h; y += 1024) {
+        int* o = off + (size_t)y * segs;
+        const int r = rs[y];
+#pragma unroll 8
+        for (int s = 0; s < segs; ++s) o[s] += r;
+    }
+    __syncthreads();
+    // ---- 3
+    const bool full = s_total <= cap;  // nothing truncated: every count is kept
+    auto kept = [&](int y, int s, int k) {
+        const size_t i = (size_t)y * segs + s;
+        const int c4 = F.cnt[i];
+        if (full) return (c4 >> (8 * k)) & 0xff;
+        const int c = bytesum(c4), lim = min(c, max(cap - off[i], 0));
+        if (lim == c) return (c4 >> (8 * k)) & 0xff;
+        const int* list = F.list + i * seg_cap;
         int r = 0;
-        for (int q = 0; q < lim; ++q) r += (list[q] >> 16) == kk ? 1 : 0;
+        for (int q = 0; q < lim; ++q) r += (list[q] >> 16) == k ? 1 : 0;
         return r;
     };
-    int* off = F.bcnt + (size_t)k * n;  // [h][segs] row-major offset of each segment (scratch of class k)
-    int below = 0;                      // kept features of classes < k in this thread's segments
-    for (int i = b; i < e; ++i) {
-        const int c4 = F.cnt[i];
-        off[i] = acc;
-        for (int kk = 0; kk < k; ++kk) below += kept(i, kk, c4, acc);
-        acc += bytesum(c4);
+    const int ncol = 4 * segs;
+    int cr = 32;
+    while ((long long)ncol * ((h + cr - 1) / cr) > kScanItems) cr *= 2;
+    const int nch = (h + cr - 1) / cr, items = ncol * nch;
+    for (int it = tid; it < items; it += 1024) {
+        const int col = it / nch, ch = it - col * nch, k = col / segs, s = col - k * segs;
+        const int y0 = ch * cr, y1 = min(y0 + cr, h);
+        int sum = 0;
+#pragma unroll 8
+        for (int y = y0; y < y1; ++y) sum += kept(y, s, k);
+        s_item[it] = sum;
     }
-    int base;
-    block_excl_scan(below, s_w, base);
     __syncthreads();
-    // band-major over t = band * h + y; segment i = y * segs + band
-    s = 0;
-    for (int t = b; t < e; ++t) {
-        const int bd = t / h, y = t - bd * h, i = y * segs + bd;
-        s += kept(i, k, F.cnt[i], off[i]);
+    {
+        const int per = (items + 1023) / 1024, b = min(tid * per, items), e = min(b + per, items);
+        int sum = 0;
+        for (int it = b; it < e; ++it) sum += s_item[it];
+        int total;
+        int acc = block_excl_scan(sum, s_w, total);
+        for (int it = b; it < e; ++it) {
+            const int t = s_item[it];
+            s_item[it] = acc;
+            acc += t;
+        }
     }
-    acc = base + block_excl_scan(s, s_w, total);
-    for (int t = b; t < e; ++t) {
-        const int bd = t / h, y = t - bd * h, i = y * segs + bd, kb = k * segs + bd;
-        const int c4 = F.cnt[i], o0 = off[i];
-        const int lim = min(bytesum(c4), max(p.cap - o0, 0));
-        F.brow0[kb * (h + 1) + y] = acc;
-        if ((c4 >> (8 * k)) & 0xff) {
-            const int* list = F.list + (size_t)i * seg_cap;
-            for (int q = 0; q < lim; ++q) {
-                const int ent = list[q];
-                if ((ent >> 16) != k) continue;
-                F.bidx[acc] = o0 + q;
-                F.buc[acc] = pack_uvc(ent & 0xffff, y, k);
-                F.bpos[o0 + q] = acc;
-                ++acc;
+    __syncthreads();
+    for (int it = tid; it < items; it += 1024) {
+        const int col = it / nch, ch = it - col * nch, k = col / segs, s = col - k * segs;
+        const int y0 = ch * cr, y1 = min(y0 + cr, h);
+        int* b0 = F.brow0 + (size_t)col * (h + 1);
+        int acc = s_item[it];
+#pragma unroll 8
+        for (int y = y0; y < y1; ++y) {
+            b0[y] = acc;
+            acc += kept(y, s, k);
+        }
+        if (y1 == h) b0[h] = acc;
+    }
+    __syncthreads();
+    // ---- 4
+    const int n = h * segs;
+    for (int i = tid; i < n; i += 1024) {
+        const int c4 = F.cnt[i];
+        if (!c4) continue;
+        const int y = i / segs, s = i - y * segs;
+        const int c = bytesum(c4), o0 = off[i], lim = min(c, max(cap - o0, 0));
+        const int* list = F.list + (size_t)i * seg_cap;
+        int rank[4] = {0, 0, 0, 0};
+        for (int q = 0; q < c; ++q) {
+            const int o = o0 + q;
+            if (o >= cap) break;
+            const int ent = list[q], k = ent >> 16, u = ent & 0xffff;
+            F.u[o] = u;
+            F.v[o] = y;
+            F.c[o] = k;
+            if (q < lim) {
+                const int pos = F.brow0[(size_t)(k * segs + s) * (h + 1) + y] + rank[k]++;
+                F.bidx[pos] = o;
+                F.buc[pos] = pack_uvc(u, y, k);
+                F.bpos[o] = pos;
             }
         }
-        if (y == h - 1) F.brow0[kb * (h + 1) + h] = acc;
     }
 }
 
@@ -1579,7 +1631,7 @@ struct viso_svo {
         // responses outside [2, w-3] x [2, h-3] reach the NMS only if margin < n + 2
         const bool dom = p.margin < p.nms_n + 2;
         launch_detect(p.nms_n, dom, g, stream, imgs, d, d_sets, ring, pair0, seg_cap);
-        svo_scan_kernel<<<dim3(ni, 5), 1024, 0, stream>>>(d, d_sets, ring, pair0, 4 * tiles, seg_cap);
+        svo_scan_kernel<<<ni, 1024, 0, stream>>>(d, d_sets, ring, pair0, 4 * tiles, seg_cap);
         svo_describe_kernel<<<dim3(16, ni), 256, 0, stream>>>(imgs, d, d_sets, ring, pair0);
         if (timed) {
             VISO_HIP_CHECK(hipEventRecord(tev[2 * tev_n + 1], stream));
