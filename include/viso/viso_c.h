@@ -190,6 +190,22 @@ int viso_stereo_match(viso_ctx* ctx, const uint8_t* left, const uint8_t* right, 
                       int32_t height, const int32_t* xs, const int32_t* ys, int32_t n,
                       int32_t max_disp, int32_t* disparity, int32_t* sad);
 
+/* Stereo initialisation (north star: metric depth from the right image
+ * replacing the 2D-2D init of Viso::PoseEstimation2d2d, src/viso.cpp:178-256
+ * and the map creation of src/viso.cpp:79-96; the repo's own spec, restated in
+ * oracle/oracle_stereo.cpp).  baseline > 0 enables it (metres; 0 disables):
+ * while initialising, a frame given with its right image (viso_process_stereo
+ * or viso_process_frames_device with d_right) runs FAST on the left image,
+ * the SAD disparity of every corner (as viso_stereo_match, d in
+ * 0..min(max_disp, x - 4)), keeps corners with min_disp <= d < that upper end,
+ * refines d by the parabola through SAD(d-1), SAD(d), SAD(d+1) and
+ * back-projects Z = fx * baseline / d.  More than 50 such points create the
+ * map at once (the frame is the only keyframe, at R = I, T = 0; points in its
+ * camera frame; metric scale; stats[3] = -2); otherwise the frame goes
+ * through the monocular initialisation.  VISO_ERR_ARG unless
+ * 1 <= min_disp < max_disp when enabled. */
+int viso_set_stereo(viso_ctx* ctx, double baseline, int32_t max_disp, int32_t min_disp);
+
 /* Library build/version string (e.g. "viso_amd 0.1 gfx950"). */
 const char* viso_version(void);
 

@@ -75,6 +75,9 @@ struct oracle_viso {
     std::vector<int32_t> al_kf;
     std::vector<uint8_t> al_succ;
     std::vector<double> al_before, al_after;
+    // stereo initialisation (viso_set_stereo)
+    double stereo_base = 0;
+    int max_disp = 0, min_disp = 1;
 };
 
 extern "C" {
@@ -117,7 +120,30 @@ oracle_viso* oracle_viso_create(const oracle_params* p) {
 
 void oracle_viso_destroy(oracle_viso* v) { delete v; }
 
-void oracle_viso_on_new_frame(oracle_viso* v, const uint8_t* img) {
+namespace {
+// map creation from one stereo pair (the stereo replacement of
+// src/viso.cpp:79-96): returns false when there are <= 50 points
+bool stereo_init(oracle_viso* v, const FramePtr& cur, const uint8_t* right) {
+    const int w = v->w, h = v->h;
+    std::vector<int32_t> xs((size_t)w * h / 4 + 16), ys(xs.size()), sc(xs.size());
+    const int n = oracle_fast(cur->pyr.data(), w, h, v->p.fast_thresh, xs.data(), ys.data(), sc.data(),
+                              (int)xs.size());
+    std::vector<double> pts((size_t)3 * n + 3);
+    const int m = oracle_stereo_points(cur->pyr.data(), right, w, h, xs.data(), ys.data(), n, v->max_disp,
+                                       v->min_disp, v->K4, v->stereo_base, pts.data());
+    v->stats[1] = n;
+    v->stats[2] = m;
+    if (m <= 50) return false;
+    v->keyframes.clear();
+    v->keyframes.push_back(cur);
+    v->points.assign(pts.begin(), pts.begin() + 3 * (size_t)m);
+    v->state = v->p.enable_tracking ? 1 : 2;
+    v->stats[3] = -2;  // stereo initialisation
+    v->stats[12] = 1;
+    return true;
+}
+
+void on_new(oracle_viso* v, const uint8_t* img, const uint8_t* right) {
     const int w = v->w, h = v->h;
     FramePtr cur = std::make_shared<Frame>();
     cur->pyr.resize(oracle_pyramid_bytes(w, h));
@@ -126,6 +152,7 @@ void oracle_viso_on_new_frame(oracle_viso* v, const uint8_t* img) {
     v->stats[12] = 0;
     switch (v->state) {
         case 0: {  // kInitialization
+            if (right && v->stereo_base > 0 && stereo_init(v, cur, right)) break;
             if (v->frame_cnt > 0 && v->frame_cnt <= v->p.reinitialize_after) {
                 int n = (int)v->kp1.size() / 2;
                 v->success.assign((size_t)n, 0);
@@ -258,6 +285,19 @@ void oracle_viso_on_new_frame(oracle_viso* v, const uint8_t* img) {
     v->stats[0] = v->state;
     v->stats[5] = v->frame_cnt;
     v->stats[11] = v->frames;
+}
+}  // namespace
+
+void oracle_viso_on_new_frame(oracle_viso* v, const uint8_t* img) { on_new(v, img, nullptr); }
+
+void oracle_viso_on_new_stereo(oracle_viso* v, const uint8_t* left, const uint8_t* right) {
+    on_new(v, left, right);
+}
+
+void oracle_viso_set_stereo(oracle_viso* v, double baseline, int max_disp, int min_disp) {
+    v->stereo_base = baseline;
+    v->max_disp = max_disp;
+    v->min_disp = min_disp;
 }
 
 int oracle_viso_state(const oracle_viso* v) { return v->state; }

@@ -123,6 +123,13 @@ int oracle_select_motion(const double* p1, const double* p2, int n, const double
 void oracle_stereo_match(const uint8_t* L, const uint8_t* R, int w, int h, const int32_t* xs,
                          const int32_t* ys, int n, int max_disp, int32_t* disp, int32_t* best_sad);
 
+// Stereo initialisation points (the repo's own spec, see oracle_stereo.cpp):
+// camera-frame points of the keypoints with a valid sub-pixel disparity, in
+// keypoint order; returns their count (pts: n x 3 capacity).
+int oracle_stereo_points(const uint8_t* L, const uint8_t* R, int w, int h, const int32_t* xs,
+                         const int32_t* ys, int n, int max_disp, int min_disp, const double K[4],
+                         double base, double* pts);
+
 // ---------------------------------------------------------------- full path
 struct oracle_params;
 // Viso::PoseEstimation2d2d (src/viso.cpp:178-256) + SelectMotion on n x 3
@@ -156,6 +163,13 @@ oracle_viso* oracle_viso_create(const oracle_params* p);
 void oracle_viso_destroy(oracle_viso* v);
 // FrameHandler::OnNewFrame equivalent (level-0 grey image, continuous rows).
 void oracle_viso_on_new_frame(oracle_viso* v, const uint8_t* img);
+// Stereo initialisation (viso_set_stereo): baseline > 0 enables it.
+void oracle_viso_set_stereo(oracle_viso* v, double baseline, int max_disp, int min_disp);
+// VisualOdometryStereo::process(left, right): while initialising with stereo
+// enabled, a frame whose left FAST corners give > 50 stereo points creates the
+// map from them (one keyframe, identity pose, metric scale); otherwise, and
+// in every other state, the left image goes through OnNewFrame.
+void oracle_viso_on_new_stereo(oracle_viso* v, const uint8_t* left, const uint8_t* right);
 int oracle_viso_state(const oracle_viso* v);
 int oracle_viso_num_poses(const oracle_viso* v);
 void oracle_viso_poses(const oracle_viso* v, double* out12);

@@ -45,6 +45,9 @@ SIG = {
     "oracle_viso_create": ([_vp], _vp),
     "oracle_viso_destroy": ([_vp], None),
     "oracle_viso_on_new_frame": ([_vp, _vp], None),
+    "oracle_viso_on_new_stereo": ([_vp, _vp, _vp], None),
+    "oracle_viso_set_stereo": ([_vp, _d, _i, _i], None),
+    "oracle_stereo_points": ([_vp, _vp, _i, _i, _vp, _vp, _i, _i, _i, _vp, _d, _vp], _i),
     "oracle_viso_state": ([_vp], _i),
     "oracle_viso_num_poses": ([_vp], _i),
     "oracle_viso_poses": ([_vp, _vp], None),
@@ -173,6 +176,21 @@ def pose_2d2d(p1, p2, K, w=1242, h=375, R0=None, T0=None, **kw):
             "candidates": cand[:int(st[2])], "stats": st}
 
 
+def stereo_points(left, right, xs, ys, max_disp, min_disp, K, base):
+    """Stereo-initialisation points (oracle_stereo_points): (m, 3)."""
+    left = np.ascontiguousarray(left, np.uint8)
+    right = np.ascontiguousarray(right, np.uint8)
+    h, w = left.shape
+    xs = np.ascontiguousarray(xs, np.int32)
+    ys = np.ascontiguousarray(ys, np.int32)
+    n = len(xs)
+    pts = np.zeros((n + 1, 3))
+    k = np.asarray(K, np.float64)
+    m = load().oracle_stereo_points(ptr(left), ptr(right), w, h, ptr(xs), ptr(ys), n, max_disp,
+                                    min_disp, ptr(k), float(base), ptr(pts))
+    return pts[:m]
+
+
 def stereo_match(left, right, xs, ys, max_disp):
     lib = load()
     left = np.ascontiguousarray(left, np.uint8)
@@ -273,6 +291,15 @@ class Viso:
         img = np.ascontiguousarray(img, np.uint8)
         assert img.shape == (self.h, self.w)
         self.lib.oracle_viso_on_new_frame(self.v, ptr(img))
+
+    def set_stereo(self, baseline, max_disp=128, min_disp=1):
+        self.lib.oracle_viso_set_stereo(self.v, float(baseline), int(max_disp), int(min_disp))
+
+    def on_new_stereo(self, left, right):
+        left = np.ascontiguousarray(left, np.uint8)
+        right = np.ascontiguousarray(right, np.uint8)
+        assert left.shape == right.shape == (self.h, self.w)
+        self.lib.oracle_viso_on_new_stereo(self.v, ptr(left), ptr(right))
 
     @property
     def state(self):

@@ -348,6 +348,15 @@ int viso_lk_align(viso_ctx* c, const uint8_t* kf_pyrs, const double* kf_poses, i
 
 }  // extern "C"
 
+extern "C" int viso_set_stereo(viso_ctx* c, double baseline, int32_t max_disp, int32_t min_disp) {
+    if (!c || !(baseline >= 0) || (baseline > 0 && (max_disp < 2 || min_disp < 1 || min_disp >= max_disp)))
+        return VISO_ERR_ARG;
+    c->stereo_base = baseline;
+    c->stereo_max_disp = max_disp;
+    c->stereo_min_disp = min_disp;
+    return VISO_OK;
+}
+
 extern "C" int viso_stereo_match(viso_ctx* c, const uint8_t* left, const uint8_t* right,
                                  int32_t width, int32_t height, const int32_t* xs,
                                  const int32_t* ys, int32_t n, int32_t max_disp,

@@ -181,6 +181,13 @@ struct viso_ctx {
     viso::DevBuf pose_log;  // max_poses x 12
     int n_poses = 0;
 
+    // ---------------- stereo initialisation (viso_set_stereo; the repo's own
+    // replacement of the 2D-2D init, no reference counterpart)
+    double stereo_base = 0.0;  // metres; > 0 enables it
+    int stereo_max_disp = 0, stereo_min_disp = 1;
+    int right_slot = -1;  // right image of the frame on_new_frame is processing
+    viso::DevBuf st_flag, st_pts;
+
     // ---------------- state (include/viso.h:44)
     int state = VISO_STATE_INITIALIZATION;
     int64_t frames = 0;
@@ -199,6 +206,11 @@ struct viso_ctx {
     uint8_t* slot_base(int slot) const;
     double* pose_of(int slot) const;
     int own_level0(int slot);
+    // map creation from the stereo pair (cur, right_slot); *made = 0 when
+    // there are too few stereo points (the mono path then runs)
+    int stereo_init(int cur, bool* made);
+    // per-map LK templates (after a map is created)
+    int build_lk_templates();
     // OnNewFrame on a frame whose pyramid is already built in `slot`
     int on_new_frame(int slot);
     int ingest_host(const uint8_t* grey, int32_t w, int32_t h, int32_t stride, int* slot_out);

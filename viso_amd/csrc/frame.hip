@@ -337,6 +337,67 @@ int viso_ctx::finish_call(hipStream_t ls) {
     return flush_lk(ls);
 }
 
+int viso_ctx::build_lk_templates() {
+    const size_t m = (size_t)std::max(n_map, 1);
+    int rc = lk_tmpl.ensure(m * kLevels * 192 * 8);
+    if (!rc) rc = lk_tmpl_h.ensure(m * kLevels * 4 * 8);
+    if (!rc) rc = lk_tmpl_kf.ensure(m * 4);
+    if (!rc) rc = lk_tmpl_uv.ensure(m * 16);
+    if (rc) return rc;
+    launch_lk_template(lk_args(), stream);
+    return VISO_OK;
+}
+
+// Stereo initialisation (the repo's own spec, oracle/oracle_stereo.cpp
+// oracle_stereo_points + oracle_viso.cpp stereo_init): FAST on the left
+// image, sub-pixel SAD disparity on the right one, metric camera points; with
+// more than 50 of them the map is created at once: the frame is the only
+// keyframe (R = I, T = 0), points in its camera frame, metric scale.
+int viso_ctx::stereo_init(int cur, bool* made) {
+    *made = false;
+    const PyrGeom& g = geom;
+    {
+        TimedRegion t(timing, VISO_KERNEL_FAST, stream);
+        launch_fast(frame(cur).l[0], g.w[0], g.h[0], p.fast_thresh, fast, (float2*)kp1.ptr, nullptr,
+                    p.max_features, (int*)n_track_dev.ptr, stream);
+    }
+    VISO_HIP_CHECK(hipGetLastError());
+    VISO_HIP_CHECK(hipMemcpyAsync(h_int, n_track_dev.ptr, sizeof(int), hipMemcpyDeviceToHost, stream));
+    VISO_HIP_CHECK(hipStreamSynchronize(stream));
+    const int n = std::min(h_int[0], p.max_features);
+    stats[1] = n;
+    int rc = st_flag.ensure((size_t)std::max(n, 1) * 4);
+    if (!rc) rc = st_pts.ensure((size_t)std::max(n, 1) * 24);
+    if (rc) return rc;
+    const StereoCam cam{p.fx, p.fy, p.cx, p.cy, stereo_base};
+    int* d_count = (int*)n_track_dev.ptr + 1;
+    {
+        TimedRegion t(timing, VISO_KERNEL_STEREO, stream);
+        launch_stereo_points(frame(cur).l[0], frame(right_slot).l[0], g.w[0], g.h[0], (const float2*)kp1.ptr,
+                             n, stereo_max_disp, stereo_min_disp, cam, (int*)st_flag.ptr, (double*)st_pts.ptr,
+                             (double*)map_pts.ptr, kMaxMapPoints, d_count, stream);
+    }
+    VISO_HIP_CHECK(hipGetLastError());
+    VISO_HIP_CHECK(hipMemcpyAsync(h_int + 2, d_count, sizeof(int), hipMemcpyDeviceToHost, stream));
+    VISO_HIP_CHECK(hipStreamSynchronize(stream));
+    const int m = h_int[2];
+    stats[2] = m;
+    if (m <= 50) return VISO_OK;
+    for (int s : kf_slots) drop(s);
+    kf_slots.clear();
+    kf_slots.push_back(cur);
+    hold(cur);
+    n_map = std::min(m, kMaxMapPoints);
+    VISO_HIP_CHECK(hipMemcpyAsync(kf_poses.ptr, pose_of(cur), 96, hipMemcpyDeviceToDevice, stream));
+    rc = build_lk_templates();
+    if (rc) return rc;
+    state = p.enable_tracking ? VISO_STATE_RUNNING : VISO_STATE_FINISHED;
+    stats[3] = -2;  // stereo initialisation
+    stats[12] = 1;
+    *made = true;
+    return VISO_OK;
+}
+
 // ------------------------------------------------------------------ OnNewFrame
 int viso_ctx::on_new_frame(int cur) {
     const PyrGeom& g = geom;
@@ -348,6 +409,12 @@ int viso_ctx::on_new_frame(int cur) {
     bool counted = true;  // ++init_.frame_cnt at the end of kInitialization
     switch (state) {
         case VISO_STATE_INITIALIZATION: {
+            if (stereo_base > 0 && right_slot >= 0) {
+                bool made = false;
+                const int rc = stereo_init(cur, &made);
+                if (rc) return rc;
+                if (made) break;  // no ++frame_cnt, as after the mono map creation
+            }
             if (frame_cnt > 0 && frame_cnt <= p.reinitialize_after) {
                 stats[3] = -1;
                 const int n = n_track;
@@ -411,13 +478,8 @@ int viso_ctx::on_new_frame(int cur) {
                                                       96, hipMemcpyDeviceToDevice, stream));
                     // LK-alignment templates of the new map (constant while tracking)
                     {
-                        const size_t m = (size_t)std::max(n_map, 1);
-                        int rc = lk_tmpl.ensure(m * kLevels * 192 * 8);
-                        if (!rc) rc = lk_tmpl_h.ensure(m * kLevels * 4 * 8);
-                        if (!rc) rc = lk_tmpl_kf.ensure(m * 4);
-                        if (!rc) rc = lk_tmpl_uv.ensure(m * 16);
+                        const int rc = build_lk_templates();
                         if (rc) return rc;
-                        launch_lk_template(lk_args(), stream);
                     }
                     state = p.enable_tracking ? VISO_STATE_RUNNING : VISO_STATE_FINISHED;
                     stats[12] = 1;
@@ -549,11 +611,13 @@ int viso_process_stereo(viso_ctx* c, const uint8_t* left, const uint8_t* right,
         launch_pyramid_frames(c->geom, l0s, slots, 2, c->stream);
     }
     VISO_HIP_CHECK(hipGetLastError());
-    // the right pyramid is the stereo stage's input (viso_stereo_match); the
+    // the right image feeds the stereo initialisation (viso_set_stereo); the
     // reference path runs on the left image only
     c->hold(sr);
-    c->drop(sr);
+    c->right_slot = sr;
     rc = c->on_new_frame(sl);
+    c->right_slot = -1;
+    c->drop(sr);
     if (rc) return rc;
     return c->finish_call(c->lk_stream);
 }
@@ -594,7 +658,9 @@ int viso_process_frames_device(viso_ctx* c, const uint8_t* d_left, const uint8_t
         }
         VISO_HIP_CHECK(hipGetLastError());
         for (int i = 0; i < nb; ++i) {
+            c->right_slot = sides == 2 ? sl[(size_t)(nb + i)] : -1;
             int rc = c->on_new_frame(sl[(size_t)i]);
+            c->right_slot = -1;
             if (rc) return rc;
         }
         // the last frame's final solve, then the chunk's LKAlignment batch

@@ -77,6 +77,14 @@ void launch_lk_align(const LkAlignArgs& a, hipStream_t stream);
 void launch_lk_template(const LkAlignArgs& a, hipStream_t stream);
 
 // ---------------------------------------------------------------- stereo (north star)
+// stereo initialisation (stereo.hip): per keypoint flag / camera point, then
+// the kept points compacted in keypoint order into out (<= cap), *count kept
+struct StereoCam {
+    double fx, fy, cx, cy, base;
+};
+void launch_stereo_points(const uint8_t* left, const uint8_t* right, int w, int h, const float2* kp,
+                          int n, int max_disp, int min_disp, const StereoCam& cam, int* flag,
+                          double* pts, double* out, int cap, int* count, hipStream_t stream);
 void launch_stereo_sad(const uint8_t* left, const uint8_t* right, int w, int h, const int* xs,
                        const int* ys, int n, int max_disp, int* disp, int* sad,
                        hipStream_t stream);

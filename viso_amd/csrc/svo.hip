@@ -1553,13 +1553,28 @@ struct viso_svo {
         d.seed = p.seed;
         return d;
     }
+    // device buffers are carved from one zeroed arena (256-byte aligned
+    // slices): alloc() records the slice, place() makes the one allocation
+    std::vector<std::pair<void**, size_t>> pending;
     template <class T>
     int alloc(T*& ptr, size_t n) {
-        void* q = nullptr;
-        VISO_HIP_CHECK(hipMalloc(&q, std::max<size_t>(n * sizeof(T), 256)));
-        VISO_HIP_CHECK(hipMemset(q, 0, std::max<size_t>(n * sizeof(T), 256)));
-        allocs.push_back(q);
-        ptr = (T*)q;
+        ptr = nullptr;
+        pending.emplace_back(reinterpret_cast<void**>(&ptr), (n * sizeof(T) + 255) & ~(size_t)255);
+        return VISO_OK;
+    }
+    int place() {
+        size_t total = 0;
+        for (const auto& q : pending) total += std::max<size_t>(q.second, 256);
+        void* base = nullptr;
+        VISO_HIP_CHECK(hipMalloc(&base, total));
+        allocs.push_back(base);
+        VISO_HIP_CHECK(hipMemset(base, 0, total));
+        size_t o = 0;
+        for (const auto& q : pending) {
+            *q.first = static_cast<char*>(base) + o;
+            o += std::max<size_t>(q.second, 256);
+        }
+        pending.clear();
         return VISO_OK;
     }
     int init() {
@@ -1595,6 +1610,7 @@ struct viso_svo {
             alloc(pa.inl, (size_t)P * pa.mcap) || alloc(pa.motion, (size_t)P * 12) || alloc(pa.stats, (size_t)P * 8) ||
             alloc(pose, 12) || alloc(pose_log, max_poses * 12))
             return VISO_ERR_HIP;
+        if (place()) return VISO_ERR_HIP;
         pa.sets = d_sets;
         pa.extr = d_extr;
         if (!extr.empty())

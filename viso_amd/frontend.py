@@ -95,6 +95,11 @@ class Viso(FrameHandler):
         dims = (ctypes.c_int32 * 3)(w, h, w)
         _lib.call("viso_process_stereo", self.ctx.h, left.ctypes.data, right.ctypes.data, dims)
 
+    def set_stereo(self, baseline: float, max_disp: int = 128, min_disp: int = 1) -> None:
+        """Stereo initialisation (viso_set_stereo): with baseline > 0 the first
+        frame given with its right image creates a metric map at once."""
+        _lib.call("viso_set_stereo", self.ctx.h, float(baseline), int(max_disp), int(min_disp))
+
     def process_device(self, d_left: int, d_right: int | None, n: int, frame_stride: int):
         """Batched ingest of n frames resident in HBM (device pointers)."""
         _lib.call("viso_process_frames_device", self.ctx.h, d_left, d_right, n, frame_stride)
