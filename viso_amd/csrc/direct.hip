@@ -422,68 +422,85 @@ __device__ void solve_wave0(SolveLds& L, int iter, double* stats, int probe_base
     // H (symmetric) from the 21 upper-triangle sums, one element per lane
     const int r0 = row < col ? row : col, c0 = row < col ? col : row;
     const double h = in ? L.S[r0 * 6 - (r0 * (r0 - 1)) / 2 + (c0 - r0)] : 0.0;
-    // ---- Eigen PartialPivLU (first maximal |pivot| wins)
-    double v = h;
+    // ---- Eigen PartialPivLU (first maximal |pivot| wins), replicated in the
+    // registers of every lane: no cross-lane traffic on the serial chain; the
+    // pivot row is wave-uniform, so a row swap is a scalar branch + moves.
+    double A[36];
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+            const int r1 = r < c ? r : c, c1 = r < c ? c : r;
+            A[6 * r + c] = L.S[r1 * 6 - (r1 * (r1 - 1)) / 2 + (c1 - r1)];
+        }
     int tr[6];
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
         int p = k;
-        double best = fabs(readlane_f64(v, 7 * k));
+        double best = fabs(A[7 * k]);
 #pragma unroll
         for (int i = k + 1; i < 6; ++i) {
-            const double s = fabs(readlane_f64(v, 6 * i + k));
+            const double s = fabs(A[6 * i + k]);
             if (s > best) {
                 best = s;
                 p = i;
             }
         }
+        p = __builtin_amdgcn_readfirstlane(p);
         tr[k] = p;
-        if (best != 0.0) {
-            if (p != k) {
-                const double vk = shfl_f64(v, 6 * k + col);
-                const double vp = shfl_f64(v, 6 * p + col);
-                if (row == k) v = vp;
-                else if (row == p) v = vk;
+        if (__builtin_amdgcn_readfirstlane(best != 0.0 ? 1 : 0)) {
+#pragma unroll
+            for (int i = k + 1; i < 6; ++i) {
+                if (p == i) {
+#pragma unroll
+                    for (int c = 0; c < 6; ++c) {
+                        const double tmp = A[6 * k + c];
+                        A[6 * k + c] = A[6 * i + c];
+                        A[6 * i + c] = tmp;
+                    }
+                }
             }
-            const double piv = readlane_f64(v, 7 * k);
-            if (in && row > k && col == k) v = v / piv;
+            const double piv = A[7 * k];
+#pragma unroll
+            for (int i = k + 1; i < 6; ++i) A[6 * i + k] = A[6 * i + k] / piv;
         }
-        const double lik = shfl_f64(v, (6 * row + k) & 63);
-        const double ukj = shfl_f64(v, 6 * k + col);
-        if (in && row > k && col > k) v = v - lik * ukj;
+#pragma unroll
+        for (int i = k + 1; i < 6; ++i)
+#pragma unroll
+            for (int c = k + 1; c < 6; ++c) A[6 * i + c] = A[6 * i + c] - A[6 * i + k] * A[6 * k + c];
     }
     SPROBE(0);
-    // ---- inverse: lane (row, col) holds X[row][col], X = P * I then
-    // forward (unit L) and backward (U) substitution per column
-    int pos = col;
+    // ---- inverse: lane c < 6 solves column c of X = P * I by forward (unit
+    // L) and backward (U) substitution
+    const int cc = lane < 6 ? lane : 0;
+    int pos = cc;
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
         if (pos == k) pos = tr[k];
         else if (pos == tr[k]) pos = k;
     }
-    double x = (row == pos) ? 1.0 : 0.0;
+    double x[6];
 #pragma unroll
-    for (int j = 0; j < 6; ++j) {
-        const double xj = shfl_f64(x, 6 * j + col);
-        const double lij = shfl_f64(v, (6 * row + j) & 63);
-        if (in && row > j) x = x - lij * xj;
-    }
+    for (int r = 0; r < 6; ++r) x[r] = (r == pos) ? 1.0 : 0.0;
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+#pragma unroll
+        for (int i = j + 1; i < 6; ++i) x[i] = x[i] - A[6 * i + j] * x[j];
 #pragma unroll
     for (int j = 5; j >= 0; --j) {
-        const double ujj = readlane_f64(v, 7 * j);
-        if (in && row == j) x = x / ujj;
-        const double xj = shfl_f64(x, 6 * j + col);
-        const double uij = shfl_f64(v, (6 * row + j) & 63);
-        if (in && row < j) x = x - uij * xj;
+        x[j] = x[j] / A[7 * j];
+#pragma unroll
+        for (int i = 0; i < j; ++i) x[i] = x[i] - A[6 * i + j] * x[j];
     }
     SPROBE(1);
-    // ---- update = H^-1 * b (row-wise, ascending columns)
+    // ---- update = H^-1 * b (row-wise, ascending columns); H^-1[r][c] is
+    // lane c's x[r]
     double update[6];
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
-        double s = readlane_f64(x, 6 * r) * L.S[21];
+        double s = readlane_f64(x[r], 0) * L.S[21];
 #pragma unroll
-        for (int c = 1; c < 6; ++c) s = s + readlane_f64(x, 6 * r + c) * L.S[21 + c];
+        for (int c = 1; c < 6; ++c) s = s + readlane_f64(x[r], c) * L.S[21 + c];
         update[r] = s;
     }
     SPROBE(2);
