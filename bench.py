@@ -349,6 +349,7 @@ def main():
                       "rmse_translation": float(np.sqrt(np.mean(np.sum((gP[:m, 9:] - oP[:m, 9:]) ** 2, 1))))}
 
     if rank == 0:
+        gn_ev, mp_ev = pmc_evidence(W, H, breakdown, stereo_vo)
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
@@ -371,6 +372,8 @@ def main():
             "kernels": {k: {"launches": t["launches"], "avg_ms": round(t["avg_ms"], 5)}
                         for k, t in timing.items()},
             "kernels_breakdown_chunk": breakdown,
+            "gn_reduction": gn_ev,
+            "matching_pass_hbm": mp_ev,
             "stereo_vo": stereo_vo,
             "last_frame_stats": {"direct_nGood": st[9], "lk_pairs": st[6], "lk_success": st[7]},
         }
@@ -378,6 +381,50 @@ def main():
     if distributed:
         dist.destroy_process_group()
     del _lib
+
+
+def pmc_evidence(W, H, breakdown, stereo_vo):
+    """The north star's two other rocprof figures, from the committed PMC passes
+    (tools/gpu_pmc.sh -> tools/pmc_kernels.py -> profiles/r01_gn_svo_pmc.json),
+    profiled at 1242x375 only: occupancy of the GN reduction (direct_level_kernel)
+    and HBM traffic of the matching pass (svo_circle_kernel).  Live durations
+    come from this run's HIP events where the bench has them."""
+    f = os.path.join(ROOT, "profiles", "r01_gn_svo_pmc.json")
+    if (W, H) != (1242, 375) or not os.path.exists(f):
+        return None, None
+    with open(f) as fh:
+        t = json.load(fh)
+    gn = None
+    d = t.get("gn", {}).get("direct_level_kernel")
+    if d:
+        # breakdown["direct"] = one frame's four level launches per "launch"
+        live_us = 1e3 * breakdown["direct"]["avg_ms"] / 4 if "direct" in breakdown else d["pmc_duration_us"]
+        flop = d.get("fp64_flop_per_dispatch")
+        gn = {"kernel": "direct_level_kernel (one pyramid level of the photometric GN: tiles + J^T J / J^T e "
+                        "reduction + the replicated 6x6 solve)",
+              "bound": "latency (serial reduce -> solve chain per level)",
+              "live_avg_us_per_launch": round(live_us, 2),
+              "waves_per_launch": d["waves"], "mean_resident_waves_per_cu": d["mean_resident_waves_per_cu"],
+              "max_waves_per_cu": d["max_waves_per_cu"],
+              "occupancy": round(d["mean_resident_waves_per_cu"] / d["max_waves_per_cu"], 4),
+              "valu_busy": d["valu_busy"], "vgpr": d["vgpr"], "lds_bytes": d["lds_bytes"],
+              "fp64_flop_per_launch": flop,
+              "fp64_tflops": round(flop / (live_us * 1e-6) / 1e12, 2) if flop else None,
+              "fp64_peak_tflops": d.get("fp64_peak_tflops"),
+              "source": "profiles/r01_gn_svo_pmc.json (SQ_WAVES, SQ_WAVE_CYCLES, SQ_ACTIVE_INST_VALU, "
+                        "SQ_INSTS_VALU_*_F64)"}
+    mp = None
+    c = t.get("svo", {}).get("svo_circle_kernel")
+    if c and c.get("traffic_bytes"):
+        us = c["pmc_duration_us"]
+        gbs = c["traffic_bytes"] / (us * 1e-6) / 1e9
+        mp = {"kernel": "svo_circle_kernel (circular SAD matching, one batch of 100 pairs)",
+              "traffic_bytes": c["traffic_bytes"], "pmc_duration_us": us,
+              "achieved_GBps": round(gbs, 1), "peak_GBps": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4),
+              "bound": "latency / VALU (four dependent best-SAD searches per feature over a cache-resident "
+                       "descriptor set), not HBM",
+              "source": "profiles/r01_gn_svo_pmc.json (FETCH_SIZE x2 + WRITE_SIZE)"}
+    return gn, mp
 
 
 if __name__ == "__main__":
