@@ -241,6 +241,9 @@ def main():
 
     # ---------------------------------------------------------- timed
     if distributed:
+        # warm the gather's collectives (all-reduce + all-gather at the timed
+        # region's shape) so no communicator / channel setup lands in the clock
+        gather_poses(np.zeros((args.steps, 12)), device=f"cuda:{local}")
         dist.barrier()
     torch.cuda.synchronize()
     v.synchronize()
