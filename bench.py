@@ -6,11 +6,14 @@ grey pairs, KITTI seq-00 intrinsics.  KITTI is not available offline, so the
 frames come from the repo's deterministic KITTI-like renderer (viso_amd.synth,
 seed = rank); they are rendered on the host and uploaded to HBM before the
 timed region.  A "step" is one stereo frame through
-viso_process_frames_device (batched pyramid build of left+right, then
+viso_process_frames_device (batched pyramid build of the left images, then
 Viso::OnNewFrame on the left image, src/viso.cpp:7-145, with tracking
-enabled so the direct-pose GN and LK alignment run every frame).  The W warmup
-frames include the 2D-2D initialisation; the K timed frames are tracking
-frames.
+enabled so the direct-pose GN and LK alignment run every frame).  Stereo
+initialisation (viso_set_stereo) creates the map from frame 0's pair; the
+warmup runs W frames and then, if needed, single frames until the state is
+kRunning (bounded; otherwise exit 3), so the K timed frames are tracking
+frames at any --warmup (init_frames_timed in the line counts any that are
+not).
 
 Multi-GPU (torchrun, one process per GPU): independent sequences, no
 data-path collective; after the timed frames the per-rank pose logs are
@@ -42,6 +45,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "stereo frames/sec at 1242x375 grey, 1/2/4/8 GPUs; pose RMSE vs reference"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+STEREO_MAX_DISP = 128
 
 
 def log(*a):
@@ -70,14 +74,14 @@ def parse():
     return ap.parse_args()
 
 
-def measure_svo(args, seq, left, right, d_left, d_right, W, H, log):
-    """Stereo VO (viso_svo_process_device) over the timed pairs: pairs/s, the
-    batched feature pass vs HBM peak, and the CPU spec on a bounded sample."""
+def measure_svo(args, seq, left, right, d_left, d_right, W, H, log, n):
+    """Stereo VO (viso_svo_process_device) over the first n resident pairs:
+    pairs/s, the batched feature pass vs HBM peak, and the CPU spec on a
+    bounded sample."""
     import torch
 
     from viso_amd import svo
 
-    n = args.warmup + args.steps
     p = svo.default_params(W, H, *seq.K, seq.p.baseline)
     vo = svo.VisualOdometryStereo(p)
     vo.process_device(d_left.data_ptr(), d_right.data_ptr(), min(8, n), W * H)  # warm-up
@@ -189,7 +193,12 @@ def main():
 
     W, H = args.width, args.height
     n_break = args.batch  # one extra chunk after the timed region: per-kernel breakdown
-    n_total = args.warmup + args.steps + n_break
+    # stereo initialisation (viso_set_stereo): frame 0's pair creates the map,
+    # so the warmup ends in kRunning and every timed frame is a tracking frame
+    # (a frame that fails to initialise extends the warmup, bounded below)
+    warm_cap = 64
+    steps = args.steps
+    n_total = max(args.warmup, 1) + warm_cap + steps + n_break
     source = "synthetic"
     if args.kitti:
         # real KITTI-format grey pairs (PNG decoded by the library's own loader,
@@ -203,7 +212,17 @@ def main():
         seq = KittiSequence(root)
         seq.p = SimpleNamespace(baseline=seq.baseline)
         W, H = seq.width, seq.height
-        n_total = min(n_total, len(seq))
+        if len(seq) < n_total:
+            # a short sequence: fewer warmup-extension / breakdown frames, then
+            # fewer timed steps; never index past the loaded frames
+            warm_cap = max(0, min(warm_cap, len(seq) - max(args.warmup, 1) - steps))
+            n_break = max(0, min(n_break, len(seq) - max(args.warmup, 1) - warm_cap - steps))
+            steps = min(steps, len(seq) - max(args.warmup, 1) - warm_cap - n_break)
+            if steps <= 0:
+                log(f"[rank {rank}] error: sequence {root} has {len(seq)} frames, too few for "
+                    f"--warmup {args.warmup}")
+                sys.exit(2)
+            n_total = max(args.warmup, 1) + warm_cap + steps + n_break
         source = f"KITTI {root}"
     else:
         seq = Sequence(W, H, seed=sequence_seed(rank))
@@ -218,6 +237,7 @@ def main():
 
     v = viso_amd.Viso(*seq.K, width=W, height=H, device=local, enable_tracking=1,
                       batch_frames=args.batch, max_poses=max(1024, n_total + 16))
+    v.set_stereo(seq.p.baseline, STEREO_MAX_DISP, 1)
     # inside the timed region only the per-chunk groups are bracketed by HIP
     # events (the image pass for the roofline, the LK-alignment batch); the
     # per-frame kernels are timed in a separate chunk afterwards
@@ -232,23 +252,30 @@ def main():
             f += m
 
     # ---------------------------------------------------------- warmup
-    run(0, args.warmup)
+    # W frames, then one frame at a time until the state is kRunning
+    warm = max(args.warmup, 1)
+    run(0, warm)
     v.synchronize()
-    n_pose_before = len(v.poses)
+    while v.state != 1 and warm < max(args.warmup, 1) + warm_cap:
+        run(warm, 1)
+        v.synchronize()
+        warm += 1
     if v.state != 1:
-        log(f"[rank {rank}] warning: not tracking after warmup (state {v.state})")
+        log(f"[rank {rank}] error: not tracking after {warm} warmup frames (state {v.state})")
+        sys.exit(3)
+    n_pose_before = len(v.poses)
     v.ctx.timing_enable(True)
 
     # ---------------------------------------------------------- timed
     if distributed:
         # warm the gather's collectives (all-reduce + all-gather at the timed
         # region's shape) so no communicator / channel setup lands in the clock
-        gather_poses(np.zeros((args.steps, 12)), device=f"cuda:{local}")
+        gather_poses(np.zeros((steps, 12)), device=f"cuda:{local}")
         dist.barrier()
     torch.cuda.synchronize()
     v.synchronize()
     t_start = time.perf_counter()
-    run(args.warmup, args.steps)
+    run(warm, steps)
     v.synchronize()
     poses = v.poses
     if distributed:
@@ -262,6 +289,10 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
+    # every tracking frame pushes one pose (src/viso.cpp:137); any other timed
+    # frame would be an initialisation frame
+    tracking_timed = len(poses) - n_pose_before
+    frames_by_state = {"initialization": steps - tracking_timed, "running": tracking_timed}
 
     # ---------------------------------------------------------- kernel timing
     timing = {}
@@ -273,7 +304,8 @@ def main():
     v.ctx.timing_enable(False)
     v.ctx.timing_select(None)
     v.ctx.timing_enable(True)
-    run(args.warmup + args.steps, n_break)
+    if n_break:
+        run(warm + steps, n_break)
     v.synchronize()
     breakdown = {}
     for k in ("pyramid", "direct", "lkalign"):
@@ -286,34 +318,23 @@ def main():
     algo_bytes_img = dims[0][0] * dims[0][1] + sum(w * h for w, h in dims[1:])
     roofline = None
     if "pyramid" in timing:
-        # one timed region = the image pass of one ingest chunk (left + right,
-        # <= 128 images): three pyr_down_sk_kernel launches (L0->L1,
-        # L1->L2, L2->L3) back to back on the context stream
-        imgs_per_launch = 2 * args.steps / timing["pyramid"]["launches"]
+        # one timed region = the image pass of one ingest chunk (the chunk's
+        # left images; no stage reads a right pyramid): the pyr_down launches
+        # back to back on the context stream
+        imgs_per_launch = steps / timing["pyramid"]["launches"]
         bytes_per_launch = algo_bytes_img * imgs_per_launch
         achieved = bytes_per_launch / (timing["pyramid"]["avg_ms"] * 1e-3) / 1e9
-        # HBM traffic from the committed rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
-        # passes over this benchmark (tools/pmc_traffic.py; 100-image chunks),
-        # scaled to this run's images per launch
-        traffic = None
-        tfile = os.path.join(ROOT, "profiles", "r01_pyramid_traffic.json")
-        if os.path.exists(tfile):
-            with open(tfile) as fh:
-                t = json.load(fh)
-            if (t.get("width"), t.get("height")) == (W, H):  # profiled at this size only
-                traffic = int(t["traffic_bytes_per_launch"] / t.get("images_per_launch", 100)
-                              * imgs_per_launch)
-        roofline = {"kernel": "pyr_down_sk_kernel x3 (batched image pass; algorithmic bytes = "
-                              "L0 read + L1..L3 write)", "bound": "hbm",
+        traffic, tsrc = pyramid_traffic(W, H, imgs_per_launch)
+        roofline = {"kernel": "pyr_down image pass of one ingest chunk (algorithmic bytes = "
+                              "L0 read + L1..L3 write per image)", "bound": "hbm",
                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "traffic_source": "profiles/r01_pyramid_traffic.json (PMC, x2 FETCH correction)"
-                    if traffic else None,
+                    "traffic_source": tsrc,
                     "algorithmic_bytes_per_launch": int(bytes_per_launch),
                     "images_per_launch": imgs_per_launch}
     st = v.stats()
     n_map = len(v.GetPoints())
-    value = world * args.steps / elapsed
+    value = world * steps / elapsed
 
     # ---------------------------------------------------------- north-star stereo VO
     # The stereo path the north star names (blob/corner NMS features, SAD
@@ -322,7 +343,7 @@ def main():
     # the same resident pairs (rank 0).
     stereo_vo = None
     if rank == 0 and not args.no_svo:
-        stereo_vo = measure_svo(args, seq, left, right, d_left, d_right, W, H, log)
+        stereo_vo = measure_svo(args, seq, left, right, d_left, d_right, W, H, log, warm + steps)
         if args.rig_steps > 0:
             stereo_vo["rig"] = measure_rig(args, W, H, log)
 
@@ -331,18 +352,28 @@ def main():
     parity = None
     if rank == 0 and not args.no_cpu and args.cpu_frames > 0:
         from tests import oracle_lib
+        host = host_info()
         ov = oracle_lib.Viso(seq.K, W, H, enable_tracking=1)
-        for f in range(args.warmup):
-            ov.on_new_frame(left[f])
-        n_cpu = min(args.cpu_frames, args.steps)
-        t0 = time.perf_counter()
-        for f in range(args.warmup, args.warmup + n_cpu):
-            ov.on_new_frame(left[f])
-        cpu_s = time.perf_counter() - t0
+        ov.set_stereo(seq.p.baseline, STEREO_MAX_DISP, 1)
+        for f in range(warm):
+            ov.on_new_stereo(left[f], right[f])
+        n_cpu = min(args.cpu_frames, steps)
+        # single thread pinned to one core (taskset -c <core> equivalent)
+        old_aff = os.sched_getaffinity(0)
+        core = min(old_aff)
+        os.sched_setaffinity(0, {core})
+        try:
+            t0 = time.perf_counter()
+            for f in range(warm, warm + n_cpu):
+                ov.on_new_stereo(left[f], right[f])
+            cpu_s = time.perf_counter() - t0
+        finally:
+            os.sched_setaffinity(0, old_aff)
         cpu = {"value": round(n_cpu / cpu_s, 3), "unit": "frames/s", "cores": 1, "kind": "port",
-               "sample": f"oracle/ C++ restatement, single thread, frames {args.warmup}-"
-                         f"{args.warmup + n_cpu - 1} (tracking) of the same synthetic sequence, "
-                         f"left image only (the reference is monocular)"}
+               "sample": f"oracle/ C++ restatement, single thread pinned to core {core}, frames "
+                         f"{warm}-{warm + n_cpu - 1} (all tracking: stereo-initialised at frame 0) of "
+                         f"the same {source} sequence",
+               "pinned_core": core, "nproc": host["nproc"], "cpu_model": host["cpu_model"]}
         oP = ov.poses()
         gP = poses
         m = min(len(oP), len(gP))
@@ -355,8 +386,8 @@ def main():
         gn_ev, mp_ev = pmc_evidence(W, H, breakdown, stereo_vo)
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True,
+            "steps": steps, "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / steps, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic" if source == "synthetic" else f"KITTI-format PNG pairs ({source})",
             "config": {"workload": (f"configs[1]: one {W}x{H} grey stereo sequence per GPU, "
@@ -365,7 +396,7 @@ def main():
                                     "when 1920x1080), KITTI seq-00 intrinsics")
                                    + (", synthetic KITTI-like frames (KITTI absent offline), "
                                       if source == "synthetic" else f", {source}, ")
-                                   + "tracking enabled",
+                                   + "stereo-initialised map, tracking enabled",
                        "width": W, "height": H, "map_points": n_map,
                        "ingest_batch": args.batch, "parallelism": f"independent sequences x{world}"},
             "roofline": roofline,
@@ -375,6 +406,9 @@ def main():
             "kernels": {k: {"launches": t["launches"], "avg_ms": round(t["avg_ms"], 5)}
                         for k, t in timing.items()},
             "kernels_breakdown_chunk": breakdown,
+            "warmup_frames_run": warm,
+            "init_frames_timed": frames_by_state["initialization"],
+            "timed_frames_by_state": frames_by_state,
             "gn_reduction": gn_ev,
             "matching_pass_hbm": mp_ev,
             "stereo_vo": stereo_vo,
@@ -384,6 +418,35 @@ def main():
     if distributed:
         dist.destroy_process_group()
     del _lib
+
+
+def host_info():
+    """nproc and the CPU model of this host (the cpu_baseline's machine)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "cpu_model": model}
+
+
+def pyramid_traffic(W, H, imgs_per_launch):
+    """HBM bytes per image-pass launch from the committed rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.py), only for an entry
+    profiled at exactly this frame size and chunk (no scaling)."""
+    f = os.path.join(ROOT, "profiles", "pyramid_traffic.json")
+    if not os.path.exists(f):
+        return None, None
+    with open(f) as fh:
+        t = json.load(fh)
+    for e in t.get("entries", []):
+        if (e["width"], e["height"]) == (W, H) and e["images_per_launch"] == imgs_per_launch:
+            return int(e["traffic_bytes_per_launch"]), f"profiles/pyramid_traffic.json ({e['source']})"
+    return None, None
 
 
 def pmc_evidence(W, H, breakdown, stereo_vo):

@@ -78,16 +78,21 @@ int viso_process_frame(viso_ctx* ctx, const uint8_t* grey, int32_t width, int32_
 
 /* North-star facade VisualOdometryStereo::process(left, right, dims):
  * dims = {width, height, stride}.  The left image drives the reference path;
- * the right image is ingested into the same frame slot (pyramid) and fed to
- * the stereo stage (viso_stereo_match).  (No reference counterpart: the
- * reference is monocular) */
+ * the right image (level 0 only, no pyramid) feeds the stereo initialisation
+ * and stereo keyframe insertion (viso_set_stereo).  (No reference
+ * counterpart: the reference is monocular) */
 int viso_process_stereo(viso_ctx* ctx, const uint8_t* left, const uint8_t* right,
                         const int32_t dims[3]);
 
 /* Batched ingest of n consecutive frames already resident in HBM (device
  * pointers, frame f at d_left + f * frame_stride, rows continuous).  Builds
- * all pyramids of the chunk in one batched launch, then runs OnNewFrame per
- * frame in order.  d_right may be NULL (mono). */
+ * all left pyramids of the chunk in one batched launch, then runs OnNewFrame
+ * per frame in order.  d_right may be NULL (mono).
+ * Buffer contract: the frames are read in place, asynchronously, on the
+ * context stream.  Their producer must have completed before the call (the
+ * caller synchronises its own stream), and the buffers must stay valid and
+ * unmodified until viso_synchronize(ctx) returns.  Frames the context retains
+ * (reference / last / keyframes) are copied into its own pool before that. */
 int viso_process_frames_device(viso_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right,
                                int32_t n, size_t frame_stride);
 

@@ -207,3 +207,35 @@ def test_gpu_stereo_init_device_ingest_matches_host():
     assert bat.state == ref.state == 1
     assert np.array_equal(bat.poses, ref.poses)
     assert np.array_equal(bat.GetPoints(), ref.GetPoints())
+
+
+@pytest.mark.gpu
+def test_gpu_failed_stereo_init_keeps_mono_tracks():
+    """A right image with no texture makes every stereo init fail, so each
+    frame falls back to the monocular initialisation.  The stereo attempt
+    must not disturb the mono state (init_.kp1 of the reference frame and the
+    track count): frame by frame the GPU matches the oracle's stats, tracks
+    and state through the KLT frames and the 2D-2D map creation."""
+    import viso_amd
+    seq = seqdata.sequence(0)
+    flat = np.full((H, W), 128, np.uint8)
+    ov = oracle_lib.Viso(seq.K, W, H, enable_tracking=1)
+    ov.set_stereo(seq.p.baseline, MAX_DISP, 1)
+    gv = viso_amd.Viso(*seq.K, width=W, height=H, enable_tracking=1)
+    gv.set_stereo(seq.p.baseline, MAX_DISP, 1)
+    states = []
+    for f in range(9):
+        ov.on_new_stereo(seqdata.image(f), flat)
+        gv.process(seqdata.image(f), flat)
+        gv.synchronize()
+        so, sg = ov.stats(), gv.stats()
+        assert gv.state == ov.state, f
+        assert [sg[k] for k in (1, 2, 3, 5)] == [so[k] for k in (1, 2, 3, 5)], (f, sg[:6], so[:6])
+        if ov.state == 0:
+            k1o, k2o, _ = ov.tracks()
+            k1g, k2g, _ = gv.tracks()
+            assert np.array_equal(k1g, k1o) and np.array_equal(k2g, k2o), f
+        states.append(ov.state)
+    assert 0 in states and states[-1] == 1  # fallback frames, then the mono map
+    assert np.array_equal(gv.GetPoints(), ov.points())
+    assert _rel(gv.poses, ov.poses()) < 1e-10

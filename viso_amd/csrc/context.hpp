@@ -185,7 +185,9 @@ struct viso_ctx {
     // replacement of the 2D-2D init, no reference counterpart)
     double stereo_base = 0.0;  // metres; > 0 enables it
     int stereo_max_disp = 0, stereo_min_disp = 1;
-    int right_slot = -1;  // right image of the frame on_new_frame is processing
+    // level 0 of the right image of the frame on_new_frame is processing
+    // (null: none); only the stereo initialisation reads it
+    const uint8_t* right_l0 = nullptr;
     viso::DevBuf st_flag, st_pts;
 
     // ---------------- state (include/viso.h:44)

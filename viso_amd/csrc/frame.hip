@@ -356,13 +356,18 @@ int viso_ctx::build_lk_templates() {
 int viso_ctx::stereo_init(int cur, bool* made) {
     *made = false;
     const PyrGeom& g = geom;
+    // FAST into scratch (kp1b, count slot 2): the monocular init state (kp1 =
+    // the reference frame's keypoints, n_track_dev[0]) must survive a stereo
+    // init that finds too few points, as the oracle's local xs/ys do
+    float2* corners = (float2*)kp1b.ptr;
+    int* d_nfast = (int*)n_track_dev.ptr + 2;
     {
         TimedRegion t(timing, VISO_KERNEL_FAST, stream);
-        launch_fast(frame(cur).l[0], g.w[0], g.h[0], p.fast_thresh, fast, (float2*)kp1.ptr, nullptr,
-                    p.max_features, (int*)n_track_dev.ptr, stream);
+        launch_fast(frame(cur).l[0], g.w[0], g.h[0], p.fast_thresh, fast, corners, nullptr,
+                    p.max_features, d_nfast, stream);
     }
     VISO_HIP_CHECK(hipGetLastError());
-    VISO_HIP_CHECK(hipMemcpyAsync(h_int, n_track_dev.ptr, sizeof(int), hipMemcpyDeviceToHost, stream));
+    VISO_HIP_CHECK(hipMemcpyAsync(h_int, d_nfast, sizeof(int), hipMemcpyDeviceToHost, stream));
     VISO_HIP_CHECK(hipStreamSynchronize(stream));
     const int n = std::min(h_int[0], p.max_features);
     stats[1] = n;
@@ -373,7 +378,7 @@ int viso_ctx::stereo_init(int cur, bool* made) {
     int* d_count = (int*)n_track_dev.ptr + 1;
     {
         TimedRegion t(timing, VISO_KERNEL_STEREO, stream);
-        launch_stereo_points(frame(cur).l[0], frame(right_slot).l[0], g.w[0], g.h[0], (const float2*)kp1.ptr,
+        launch_stereo_points(frame(cur).l[0], right_l0, g.w[0], g.h[0], corners,
                              n, stereo_max_disp, stereo_min_disp, cam, (int*)st_flag.ptr, (double*)st_pts.ptr,
                              (double*)map_pts.ptr, kMaxMapPoints, d_count, stream);
     }
@@ -401,7 +406,12 @@ int viso_ctx::stereo_init(int cur, bool* made) {
 // ------------------------------------------------------------------ OnNewFrame
 int viso_ctx::on_new_frame(int cur) {
     const PyrGeom& g = geom;
-    hold(cur);  // the "cur_frame" shared_ptr
+    hold(cur);  // the "cur_frame" shared_ptr, released on every return
+    struct CurRef {
+        viso_ctx* c;
+        int s;
+        ~CurRef() { c->drop(s); }
+    } cur_ref{this, cur};
     for (int k = 0; k < 16; ++k) stats[k] = 0;
     // Keyframe ctor: R = I, T = 0 (a tracking frame overwrites it below)
     if (state != VISO_STATE_RUNNING) launch_set_pose(pose_of(cur), kIdentityPose, stream);
@@ -409,7 +419,7 @@ int viso_ctx::on_new_frame(int cur) {
     bool counted = true;  // ++init_.frame_cnt at the end of kInitialization
     switch (state) {
         case VISO_STATE_INITIALIZATION: {
-            if (stereo_base > 0 && right_slot >= 0) {
+            if (stereo_base > 0 && right_l0) {
                 bool made = false;
                 const int rc = stereo_init(cur, &made);
                 if (rc) return rc;
@@ -560,7 +570,6 @@ int viso_ctx::on_new_frame(int cur) {
     }
     VISO_HIP_CHECK(hipGetLastError());
     set_role(last_slot, cur);  // last_frame = cur_frame (src/viso.cpp:144)
-    drop(cur);
     ++frames;
     stats[0] = state;
     stats[5] = frame_cnt;
@@ -604,19 +613,20 @@ int viso_process_stereo(viso_ctx* c, const uint8_t* left, const uint8_t* right,
         c->drop(sl);
         return rc;
     }
-    uint8_t* slots[2] = {c->slot_base(sl), c->slot_base(sr)};
-    const uint8_t* l0s[2] = {slots[0], slots[1]};
+    uint8_t* slot = c->slot_base(sl);
+    const uint8_t* l0 = slot;
     {
         TimedRegion t(c->timing, VISO_KERNEL_PYRAMID, c->stream);
-        launch_pyramid_frames(c->geom, l0s, slots, 2, c->stream);
+        launch_pyramid_frames(c->geom, &l0, &slot, 1, c->stream);
     }
     VISO_HIP_CHECK(hipGetLastError());
-    // the right image feeds the stereo initialisation (viso_set_stereo); the
-    // reference path runs on the left image only
+    // the right image feeds the stereo initialisation (viso_set_stereo), which
+    // reads its level 0 only: no pyramid is built for it; the reference path
+    // runs on the left image only
     c->hold(sr);
-    c->right_slot = sr;
+    c->right_l0 = c->slot_base(sr);
     rc = c->on_new_frame(sl);
-    c->right_slot = -1;
+    c->right_l0 = nullptr;
     c->drop(sr);
     if (rc) return rc;
     return c->finish_call(c->lk_stream);
@@ -630,21 +640,19 @@ int viso_process_frames_device(viso_ctx* c, const uint8_t* d_left, const uint8_t
     const int B = c->p.batch_frames;
     for (int f0 = 0; f0 < n; f0 += B) {
         const int nb = std::min(B, n - f0);
-        const int sides = d_right ? 2 : 1;
         std::vector<int> sl;
         std::vector<const uint8_t*> l0;
         std::vector<uint8_t*> dst;
-        for (int i = 0; i < nb * sides; ++i) {
+        // left images only: the right image is read at level 0, in place, by
+        // the stereo initialisation (no stage consumes a right pyramid)
+        for (int i = 0; i < nb; ++i) {
             const int s = c->acquire_slot();
             if (s < 0) {
-                for (int x : sl) {
-                    c->hold(x);
-                    c->drop(x);
-                }
+                for (int x : sl) c->drop(x);
                 return VISO_ERR_CAPACITY;
             }
-            const int f = f0 + (i % nb);
-            const uint8_t* src = (i < nb ? d_left : d_right) + frame_stride * (size_t)f;
+            const int f = f0 + i;
+            const uint8_t* src = d_left + frame_stride * (size_t)f;
             c->slots[(size_t)s].l0 = src;
             c->slots[(size_t)s].borrowed = true;
             c->hold(s);  // pending in this chunk
@@ -657,28 +665,35 @@ int viso_process_frames_device(viso_ctx* c, const uint8_t* d_left, const uint8_t
             launch_pyramid_frames(c->geom, l0.data(), dst.data(), (int)l0.size(), c->stream);
         }
         VISO_HIP_CHECK(hipGetLastError());
+        // end of the chunk, also on an error: launch what still reads the
+        // chunk's borrowed frames (the pending final solve, the LK batch),
+        // give retained frames their own level 0, release the chunk's holds
+        auto end_chunk = [&](int rc) -> int {
+            const int r1 = c->finish_call(c->stream);
+            if (!rc) rc = r1;
+            const int roles[2] = {c->ref_slot, c->last_slot};
+            for (int r : roles) {
+                const int r2 = c->own_level0(r);
+                if (!rc) rc = r2;
+            }
+            for (int s : c->kf_slots) {
+                const int r2 = c->own_level0(s);
+                if (!rc) rc = r2;
+            }
+            for (int s : sl) c->drop(s);
+            return rc;
+        };
         for (int i = 0; i < nb; ++i) {
-            c->right_slot = sides == 2 ? sl[(size_t)(nb + i)] : -1;
-            int rc = c->on_new_frame(sl[(size_t)i]);
-            c->right_slot = -1;
-            if (rc) return rc;
+            c->right_l0 = d_right ? d_right + frame_stride * (size_t)(f0 + i) : nullptr;
+            const int rc = c->on_new_frame(sl[(size_t)i]);
+            c->right_l0 = nullptr;
+            if (rc) return end_chunk(rc);
         }
         // the last frame's final solve, then the chunk's LKAlignment batch
         // behind the chunk (the GPU is free then; beside the next chunk it
         // would take the CU resources the latency-bound direct chain needs)
-        int rc = c->finish_call(c->stream);
+        const int rc = end_chunk(VISO_OK);
         if (rc) return rc;
-        // frames still referenced after the chunk get their own level 0
-        int roles[3] = {c->ref_slot, c->last_slot, -1};
-        for (int r : roles) {
-            rc = c->own_level0(r);
-            if (rc) return rc;
-        }
-        for (int s : c->kf_slots) {
-            rc = c->own_level0(s);
-            if (rc) return rc;
-        }
-        for (int s : sl) c->drop(s);
     }
     return VISO_OK;
 }
