@@ -54,6 +54,30 @@ inline double tree_sum(const double* v, int n) {
     return t[0];
 }
 
+// Summation order switch (oracle_set_sum_order, viso_oracle.h).  0: the
+// canonical pairwise tree the device reproduces bit for bit; 1: "literal",
+// the reference's own running sums in loop order (H += ..., b += ...,
+// cost += ... at src/viso.cpp:308-310, 727-729, 888-890; disparity and mean
+// depth at :199-201, :622-625).  Literal mode exists to measure the drift the
+// tree substitution causes (tests/test_literal_drift.py); the GPU is checked
+// against the tree mode.
+inline int& sum_literal() {
+    thread_local int mode = 0;  // per calling thread
+    return mode;
+}
+
+// Running sum in index order, starting from 0 (Eigen's Zero() then +=).
+inline double running_sum(const double* v, int n) {
+    double s = 0.0;
+    for (int i = 0; i < n; ++i) s = s + v[i];
+    return s;
+}
+
+// The sum of n per-item terms in the active order (tree or literal).
+inline double acc_sum(const double* v, int n) {
+    return sum_literal() ? running_sum(v, n) : tree_sum(v, n);
+}
+
 // GetPixelValue (include/common.h:35-42, include/keyframe.h:50-57).  Base
 // pointer uses int() truncation, weights use x - floor(x).  Taps outside the
 // continuous level buffer read 0 (reference: reads outside the cv::Mat).

@@ -563,7 +563,7 @@ int oracle_select_motion(const double* p1, const double* p2, int n, const double
     // depth normalisation (src/viso.cpp:622-637): tree sum of the inliers' z
     std::vector<double> leaf((size_t)n);
     for (int i = 0; i < n; ++i) leaf[(size_t)i] = best_in[(size_t)i] ? best_pts[(size_t)3 * i + 2] : 0.0;
-    double mean_depth = tree_sum(leaf.data(), n);
+    double mean_depth = acc_sum(leaf.data(), n);
     if (mean_depth != 0) {
         mean_depth /= best_nr;
         for (int i = 0; i < n; ++i)
@@ -599,7 +599,7 @@ int oracle_pose_2d2d(const double* p1, const double* p2, int n, const double K[4
         q2[(size_t)2 * i] = (double)(float)p2[3 * i];
         q2[(size_t)2 * i + 1] = (double)(float)p2[3 * i + 1];
     }
-    double disparity_squared = tree_sum(leaf.data(), n);
+    double disparity_squared = acc_sum(leaf.data(), n);
     if (disparity_squared != 0) {
         disparity_squared /= n;
         disparity_squared *= f * f;

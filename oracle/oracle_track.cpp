@@ -54,10 +54,10 @@ void klt_single_level(const uint8_t* img1, const uint8_t* img2, int cols, int ro
                     b1[p] = -J1 * error;
                     cc[p] = error * error;
                 }
-            const double H00 = tree_sum(hxx, 64), H01 = tree_sum(hxy, 64), H10 = tree_sum(hyx, 64),
-                         H11 = tree_sum(hyy, 64);
-            const double B0 = tree_sum(b0, 64), B1 = tree_sum(b1, 64);
-            cost = tree_sum(cc, 64);
+            const double H00 = acc_sum(hxx, 64), H01 = acc_sum(hxy, 64), H10 = acc_sum(hyx, 64),
+                         H11 = acc_sum(hyy, 64);
+            const double B0 = acc_sum(b0, 64), B1 = acc_sum(b1, 64);
+            cost = acc_sum(cc, 64);
             // Eigen 2x2 inverse (compute_inverse_size2_helper)
             const double invdet = 1.0 / (H00 * H11 - H10 * H01);
             const double i00 = H11 * invdet, i10 = -H10 * invdet, i01 = -H01 * invdet,
@@ -109,9 +109,12 @@ void d_pixel_d_xi(const double K[4], const double* R, const double* T, const dou
 // Per-map-point partial sums of one DirectPoseEstimationSingleLayer
 // iteration (28 = 21 upper-triangle H + 6 b + 1 cost, all tree sums over the
 // 64 patch pixels).  Returns false if the point is not "good" (:704-715).
+// With `running` (literal order) the pixel terms are instead added straight
+// into the level's running sums, x outer / y inner, as H += J J^T,
+// b += -error J, cost += error^2 do at src/viso.cpp:722-729.
 bool direct_point_partials(const PyrView& last, const PyrView& cur, const Pose& last_pose,
                            const Pose& cur_pose, const double K[4], const double* P, int level,
-                           double out[28]) {
+                           double out[28], double* running = nullptr) {
     const int w = last.w[level], h = last.h[level];
     double u_ref, v_ref, u_cur, v_cur;
     project(last_pose, K, P, level, u_ref, v_ref);
@@ -140,8 +143,11 @@ bool direct_point_partials(const PyrView& last, const PyrView& cur, const Pose& 
                 for (int b = a; b < 6; ++b) leaf[idx++][p] = J[a] * J[b];
             for (int k = 0; k < 6; ++k) leaf[21 + k][p] = -error * J[k];
             leaf[27][p] = error * error;
+            if (running)
+                for (int k = 0; k < 28; ++k) running[k] = running[k] + leaf[k][p];
         }
-    for (int k = 0; k < 28; ++k) out[k] = tree_sum(leaf[k], 64);
+    if (!running)
+        for (int k = 0; k < 28; ++k) out[k] = tree_sum(leaf[k], 64);
     return true;
 }
 
@@ -177,17 +183,29 @@ void direct_single_layer(const PyrView& last, const PyrView& cur, const double K
     for (int iter = 0; iter < 100; ++iter) {
         nGood = 0;
         Pose cur_pose = pose_from_se3(T21);
-        for (int i = 0; i < n; ++i) {
-            double* o = &part[(size_t)i * 28];
-            if (direct_point_partials(last, cur, last_pose, cur_pose, K, points + 3 * i, level, o))
-                ++nGood;
-            else
-                for (int k = 0; k < 28; ++k) o[k] = 0.0;
-        }
         double S[28];
-        for (int k = 0; k < 28; ++k) {
-            for (int i = 0; i < n; ++i) leaf[(size_t)i] = part[(size_t)i * 28 + k];
-            S[k] = tree_sum(leaf.data(), n);
+        if (sum_literal()) {
+            // M6d H = M6d::Zero(); V6d b = V6d::Zero(); running over points
+            // ascending, then the patch (src/viso.cpp:682-729); the cost's
+            // running sum continues across iterations (never reset, :673)
+            for (int k = 0; k < 28; ++k) S[k] = 0.0;
+            S[27] = cost;
+            for (int i = 0; i < n; ++i)
+                if (direct_point_partials(last, cur, last_pose, cur_pose, K, points + 3 * i, level,
+                                          nullptr, S))
+                    ++nGood;
+        } else {
+            for (int i = 0; i < n; ++i) {
+                double* o = &part[(size_t)i * 28];
+                if (direct_point_partials(last, cur, last_pose, cur_pose, K, points + 3 * i, level, o))
+                    ++nGood;
+                else
+                    for (int k = 0; k < 28; ++k) o[k] = 0.0;
+            }
+            for (int k = 0; k < 28; ++k) {
+                for (int i = 0; i < n; ++i) leaf[(size_t)i] = part[(size_t)i * 28 + k];
+                S[k] = tree_sum(leaf.data(), n);
+            }
         }
         double H[36], b[6];
         int idx = 0;
@@ -198,7 +216,7 @@ void direct_single_layer(const PyrView& last, const PyrView& cur, const double K
                 ++idx;
             }
         for (int k = 0; k < 6; ++k) b[k] = S[21 + k];
-        cost = cost + S[27];
+        cost = sum_literal() ? S[27] : cost + S[27];
         double inv[36], update[6];
         inverse6(H, inv);
         for (int r = 0; r < 6; ++r) {
@@ -265,10 +283,10 @@ void lk_pair_level(const PyrView& ref, const PyrView& cur, int level, const doub
                 b1[p] = -J1 * error;
                 cc[p] = error * error;
             }
-        const double H00 = tree_sum(hxx, 64), H01 = tree_sum(hxy, 64), H10 = tree_sum(hyx, 64),
-                     H11 = tree_sum(hyy, 64);
-        const double B0 = tree_sum(b0, 64), B1 = tree_sum(b1, 64);
-        cost = tree_sum(cc, 64);
+        const double H00 = acc_sum(hxx, 64), H01 = acc_sum(hxy, 64), H10 = acc_sum(hyx, 64),
+                     H11 = acc_sum(hyy, 64);
+        const double B0 = acc_sum(b0, 64), B1 = acc_sum(b1, 64);
+        cost = acc_sum(cc, 64);
         const double invdet = 1.0 / (H00 * H11 - H10 * H01);
         const double i00 = H11 * invdet, i10 = -H10 * invdet, i01 = -H01 * invdet, i11 = H00 * invdet;
         const double u0 = i00 * B0 + i01 * B1;
@@ -300,6 +318,9 @@ void direct_layer(const uint8_t* last_pyr, const uint8_t* cur_pyr, int w, int h,
 }  // namespace oracle
 
 extern "C" {
+
+void oracle_set_sum_order(int literal) { sum_literal() = literal ? 1 : 0; }
+int oracle_get_sum_order(void) { return sum_literal(); }
 
 void oracle_klt(const uint8_t* ref_pyr, const uint8_t* cur_pyr, int w, int h, const float* kp1,
                 float* kp2, uint8_t* success, int n, double photometric_thresh) {

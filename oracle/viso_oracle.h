@@ -32,6 +32,14 @@
 extern "C" {
 #endif
 
+// ---------------------------------------------------------------- summation order
+// 0 (default): canonical pairwise tree sums (the device's order, above).
+// 1: "literal" — the reference's running sums in its loop order (KLT, direct
+// pose, LK alignment, disparity, mean depth).  Per calling thread; used to
+// measure the drift of the tree substitution (tests/test_literal_drift.py).
+void oracle_set_sum_order(int literal);
+int oracle_get_sum_order(void);
+
 // ---------------------------------------------------------------- images
 // Level sizes: w_l = (int)(w_{l-1} * 0.5), h likewise (include/keyframe.h:42-43).
 void oracle_pyramid_dims(int w, int h, int32_t dims_out[8]);

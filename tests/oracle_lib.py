@@ -18,6 +18,8 @@ _i = ctypes.c_int
 _d = ctypes.c_double
 
 SIG = {
+    "oracle_set_sum_order": ([_i], None),
+    "oracle_get_sum_order": ([], _i),
     "oracle_pyramid_dims": ([_i, _i, _vp], None),
     "oracle_pyramid_bytes": ([_i, _i], ctypes.c_size_t),
     "oracle_pyr_down": ([_vp, _i, _i, _vp, _i, _i], None),
