@@ -150,3 +150,58 @@ def test_gpu_stereo_facade_uses_left():
         a.process(left, right)
         b.OnNewFrame(left)
     assert np.array_equal(a.poses, b.poses)
+
+
+# ------------------------------------------------------------------ configs[2] size
+W2, H2 = 1920, 1080
+# renderer texture scale giving ~8k FAST@50 corners on frame 0 (BASELINE.json
+# configs[2]: "~8k features/frame"; 8,215 on frame 0)
+BLOCK_1080 = 0.35
+
+
+@pytest.mark.gpu
+def test_gpu_1080p_reference_path_frame_by_frame():
+    """BASELINE.json configs[2] on the reference path: Viso::OnNewFrame at
+    1920x1080 with ~8k FAST corners, the monocular initialisation (KLT over
+    ~8k tracks, E-RANSAC 1000 + H-RANSAC 2000 hypotheses, SelectMotion over
+    five candidates, map of ~5.7k points), then tracking (direct pose + LK
+    alignment), GPU vs oracle frame by frame with the bars of
+    test_gpu_sequence_parity_frame_by_frame."""
+    import viso_amd
+    from viso_amd.synth import Sequence
+    seq = Sequence(W2, H2, seed=0, block_m=BLOCK_1080)
+    gv = viso_amd.Viso(*seq.K, width=W2, height=H2, enable_tracking=1)
+    ov = oracle_lib.Viso(seq.K, W2, H2, enable_tracking=1)
+    states = []
+    for f in range(10):
+        img = seq.image(f)
+        gv.OnNewFrame(img)
+        ov.on_new_frame(img)
+        assert gv.state == ov.state, f
+        gs, os_ = gv.stats(), ov.stats()
+        if f == 0:
+            assert os_[1] > 7500  # ~8k FAST corners
+        for k in (1, 2, 3, 4, 12):  # tracks, inliers, best motion, candidates, init
+            assert gs[k] == os_[k], (f, k, gs, os_)
+        if ov.state == 0:
+            gk1, gk2, gsu = gv.tracks()
+            ok1, ok2, osu = ov.tracks()
+            assert np.array_equal(gk1.view(np.uint32), ok1.view(np.uint32)), f
+            assert np.array_equal(gk2.view(np.uint32), ok2.view(np.uint32)), f
+            assert np.array_equal(gsu, osu), f
+        else:
+            assert gs[6] == os_[6] and gs[7] == os_[7], (f, gs, os_)  # LK pairs / successes
+            assert gs[9] == os_[9], (f, gs[9], os_[9])  # direct nGood
+        states.append(ov.state)
+    assert states.count(1) >= 4
+    gp, op = gv.GetPoints(), ov.points()
+    assert gp.shape == op.shape and len(op) > 5000
+    assert _rel(gp, op) < 1e-10
+    gP, oP = gv.poses, ov.poses()
+    assert gP.shape == oP.shape and len(oP) >= 4
+    for i in range(len(oP)):
+        assert _rel(gP[i], oP[i]) < 1e-10, (i, gP[i], oP[i])
+    pk, sc, ub, ua = gv.alignment()
+    opk, osc, oub, oua = ov.alignment()
+    assert np.array_equal(pk, opk) and np.array_equal(sc, osc)
+    assert np.max(np.abs(ua - oua)) < 1e-6

@@ -30,9 +30,14 @@ def main():
     seq = Sequence(W, H, seed=0)
     n = warm + steps
     left = np.stack([seq.image(f, 0) for f in range(n)])
+    right = np.stack([seq.image(f, 1) for f in range(n)])
     d_left = torch.from_numpy(left).cuda()
+    d_right = torch.from_numpy(right).cuda()
     v = viso_amd.Viso(*seq.K, width=W, height=H, enable_tracking=1, batch_frames=batch,
                       max_poses=4096)
+    stereo = os.environ.get("MONO", "0") != "1"
+    if stereo:  # the bench path: stereo-initialised map
+        v.set_stereo(seq.p.baseline, 128, 1)
     lib = _lib.load()
     lib.viso_debug_probe.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
     buf = (ctypes.c_ulonglong * 128)()
@@ -41,7 +46,8 @@ def main():
         f = f0
         while f < f0 + m:
             k = min(batch, f0 + m - f)
-            v.process_device(d_left.data_ptr() + f * W * H, None, k, W * H)
+            v.process_device(d_left.data_ptr() + f * W * H,
+                             d_right.data_ptr() + f * W * H if stereo else None, k, W * H)
             f += k
 
     lib.viso_debug_probe_lk.argtypes = [ctypes.c_void_p, ctypes.c_int]
@@ -52,6 +58,7 @@ def main():
     lib.viso_debug_probe_lk(lkbuf, 1)
     run(warm, steps)
     v.synchronize()
+    print(f"map points {len(v.GetPoints())}, state {v.state}")
     assert lib.viso_debug_probe(buf, 128, 0) == 0
     lib.viso_debug_probe_lk(lkbuf, 0)
     q = list(lkbuf)
