@@ -34,6 +34,7 @@
 // whose photometric cost is exactly 0) is executed faithfully by each
 // workgroup on its own, re-evaluating every tile into private scratch.
 #include "device_math.hpp"
+#include "direct_solve.hpp"
 #include "kernels.hpp"
 
 // Phase probes (build with VISO_VARIANT=probe; tools/probe_direct.py): block
@@ -346,6 +347,145 @@ __device__ void direct_tile(const DirectArgs& a, const LevelPair& fp, int lv, co
     __syncthreads();
 }
 
+// Prologue prefetch of a whole tile, in LDS: per point j of the tile its
+// world point, its projection into the last frame (ur, vr, the bounds test)
+// and the four `last` patch taps of every lane (sample_px's bytes, packed),
+// and the 16 x 16 current-image window around its projection under the
+// predicted T21.  Issued while wave 0 solves, so after the solve the tiles
+// read nothing but LDS (and the rare sample outside its window).
+struct PfLds {
+    uint32_t taps[kMaxTile][64];
+    uint8_t win[kMaxTile][kCW * kCW];
+    double P[kMaxTile][3];
+    double ur[kMaxTile], vr[kMaxTile];
+    int ok[kMaxTile];
+    int cw[kMaxTile][3];  // x0, y0, on
+};
+
+struct PfPoint {
+    RefSample r;
+    CurWin c;
+};
+
+__device__ inline void pf_issue(const DirectArgs& a, const LevelPair& fp, int lv, int i, const double* pred,
+                                bool ref, PfPoint& q) {
+    if (ref) {
+        ref_issue(a, fp, lv, i, q.r);
+    } else {
+        q.r.P[0] = a.points[3 * i];
+        q.r.P[1] = a.points[3 * i + 1];
+        q.r.P[2] = a.points[3 * i + 2];
+    }
+    double up, vp;
+    project_px(pred, a.K, q.r.P, kScale[lv], up, vp);
+    win_issue(fp.cur, a.g.w[lv], a.g.h[lv], up, vp, q.c);
+}
+
+__device__ inline void pf_store(int j, bool ref, const PfPoint& q, PfLds& pf) {
+    const int lane = threadIdx.x & 63;
+    if (ref)
+        pf.taps[j][lane] = (uint32_t)q.r.t0 | ((uint32_t)q.r.t1 << 8) | ((uint32_t)q.r.t2 << 16) |
+                           ((uint32_t)q.r.t3 << 24);
+    if (q.c.on) win_store(pf.win[j], q.c);
+    if (lane == 0) {
+        pf.P[j][0] = q.r.P[0];
+        pf.P[j][1] = q.r.P[1];
+        pf.P[j][2] = q.r.P[2];
+        pf.ur[j] = ref ? q.r.ur : 0.0;
+        pf.vr[j] = ref ? q.r.vr : 0.0;
+        pf.ok[j] = (ref && q.r.ok) ? 1 : 0;
+        pf.cw[j][0] = q.c.x0;
+        pf.cw[j][1] = q.c.y0;
+        pf.cw[j][2] = q.c.on ? 1 : 0;
+    }
+}
+
+// Points j = first, first + stride, ... of tile b, two at a time (the loads
+// of both in flight together).  `ref` = false when the `last` pose is solved
+// in this launch (merged L(3)): the taps are then read in the tile phase.
+__device__ void prefetch_tile(const DirectArgs& a, int lv, int b, const double* pred, bool ref, int first,
+                              int stride, PfLds& pf) {
+    const LevelPair fp = level_pair(a.fp, lv);
+    const int T = a.tile;
+    for (int j = first; j < T; j += 2 * stride) {
+        const int j2 = j + stride;
+        const int i0 = b * T + j, i1 = b * T + j2;
+        const bool v0 = i0 < a.n, v1 = j2 < T && i1 < a.n;
+        PfPoint q0{}, q1{};
+        if (v0) pf_issue(a, fp, lv, i0, pred, ref, q0);
+        if (v1) pf_issue(a, fp, lv, i1, pred, ref, q1);
+        if (v0) pf_store(j, ref, q0, pf);
+        if (v1) pf_store(j2, ref, q1, pf);
+    }
+}
+
+// The RefSample of prefetched point j: sample_px's expression on the
+// prefetched taps, with ref_issue's weights.
+__device__ inline void pf_ref(const PfLds& pf, int j, RefSample& r) {
+    const int lane = threadIdx.x & 63;
+    const int px = (lane >> 3) - 4, py = (lane & 7) - 4;
+    r.P[0] = pf.P[j][0];
+    r.P[1] = pf.P[j][1];
+    r.P[2] = pf.P[j][2];
+    r.ur = pf.ur[j];
+    r.vr = pf.vr[j];
+    r.ok = pf.ok[j] != 0;
+    const uint32_t t = pf.taps[j][lane];
+    r.t0 = (int)(t & 0xff);
+    r.t1 = (int)((t >> 8) & 0xff);
+    r.t2 = (int)((t >> 16) & 0xff);
+    r.t3 = (int)(t >> 24);
+    const double x = r.ur + px, y = r.vr + py;
+    r.xx = x - floor(x);
+    r.yy = y - floor(y);
+    ref_finish(r);
+}
+
+// Tile b of level lv from the prologue's prefetch (the tile phase of
+// direct_level_kernel; direct_tile's arithmetic and tree).
+__device__ void direct_tile_pf(const DirectArgs& a, const LevelPair& fp, int lv, const double* cur_pose, int b,
+                               const PfLds& pf, bool merged, double* part, int* good, double* s_pts,
+                               int* s_good) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int T = a.tile;
+    int good_cnt = 0;
+    for (int local = wave; local < T; local += kWaves) {
+        const int i = b * T + local;
+        double f = 0.0;
+        int idx = -1;
+        bool ok = false;
+        if (i < a.n) {
+            RefSample r;
+            if (merged) {
+                ref_issue(a, fp, lv, i, r);
+                ref_finish(r);
+            } else {
+                pf_ref(pf, local, r);
+            }
+            CurWin cw;
+            cw.x0 = pf.cw[local][0];
+            cw.y0 = pf.cw[local][1];
+            cw.on = pf.cw[local][2] != 0;
+            ok = direct_point_rs(a, fp, lv, cur_pose, r, pf.win[local], cw, &f, &idx);
+        }
+        if (!ok) {
+            if (lane < kSums) s_pts[local * kSums + lane] = 0.0;
+        } else if (lane < 32 && idx >= 0) {
+            s_pts[local * kSums + idx] = f;
+        }
+        good_cnt += ok ? 1 : 0;
+    }
+    if (lane == 0 && good_cnt) atomicAdd(s_good, good_cnt);
+    __syncthreads();
+    for (int k = wave; k < kSums; k += kWaves) {
+        const double v = lane < T ? s_pts[lane * kSums + k] : 0.0;
+        const double r = wave_tree_sum_dpp(v);
+        if (lane == 0) part[(size_t)b * kSums + k] = r;
+    }
+    if (threadIdx.x == 0) good[b] = *s_good;
+    __syncthreads();
+}
+
 __device__ inline void state_to_pose(const double* st, double* pose) {
     double q[4] = {st[0], st[1], st[2], st[3]};
     quat_to_matrix(q, pose);
@@ -355,15 +495,6 @@ __device__ inline void state_to_pose(const double* st, double* pose) {
 }
 
 // ---------------------------------------------------------------- solve
-struct SolveLds {
-    double red[4][kSums];
-    double S[kSums];
-    int g[4];
-    int ngood;
-    double state[kStateStride], best[kStateStride];
-    double cost, last_cost;
-    int cont;
-};
 
 // Thread t < 256 loads tile t's partials (zeros beyond n_tiles).
 __device__ inline void load_partials(const double* __restrict__ part, const int* __restrict__ good,
@@ -399,199 +530,6 @@ __device__ inline void reduce_partials(const double* v, int gg, SolveLds& L) {
     if (t < kSums) L.S[t] = (L.red[0][t] + L.red[1][t]) + (L.red[2][t] + L.red[3][t]);
     if (t == 0) L.ngood = (L.g[0] + L.g[1]) + (L.g[2] + L.g[3]);
     __syncthreads();
-}
-
-__device__ inline double shfl_f64(double v, int src) { return __shfl(v, src, 64); }
-
-// One GN step of one level on wave 0 (all 64 lanes): L.S -> update, the new
-// L.state and the loop decision L.cont (src/viso.cpp:731-753).
-__device__ void solve_wave0(SolveLds& L, int iter, double* stats, int probe_base = -1,
-                            unsigned long long probe_t0 = 0) {
-#ifdef VISO_PROBE
-#define SPROBE(k)                                                                       \
-    do {                                                                                \
-        if (probe_base >= 0 && (threadIdx.x & 63) == 0 && blockIdx.x == 0)             \
-            g_probe[probe_base + (k)] += __builtin_amdgcn_s_memrealtime() - probe_t0;   \
-    } while (0)
-#else
-#define SPROBE(k)
-#endif
-    const int lane = threadIdx.x & 63;
-    const int row = lane / 6, col = lane - 6 * (lane / 6);
-    const bool in = lane < 36;
-    // H (symmetric) from the 21 upper-triangle sums, one element per lane
-    const int r0 = row < col ? row : col, c0 = row < col ? col : row;
-    const double h = in ? L.S[r0 * 6 - (r0 * (r0 - 1)) / 2 + (c0 - r0)] : 0.0;
-    // ---- Eigen PartialPivLU (first maximal |pivot| wins), replicated in the
-    // registers of every lane: no cross-lane traffic on the serial chain; the
-    // pivot row is wave-uniform, so a row swap is a scalar branch + moves.
-    double A[36];
-#pragma unroll
-    for (int r = 0; r < 6; ++r)
-#pragma unroll
-        for (int c = 0; c < 6; ++c) {
-            const int r1 = r < c ? r : c, c1 = r < c ? c : r;
-            A[6 * r + c] = L.S[r1 * 6 - (r1 * (r1 - 1)) / 2 + (c1 - r1)];
-        }
-    int tr[6];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-        int p = k;
-        double best = fabs(A[7 * k]);
-#pragma unroll
-        for (int i = k + 1; i < 6; ++i) {
-            const double s = fabs(A[6 * i + k]);
-            if (s > best) {
-                best = s;
-                p = i;
-            }
-        }
-        p = __builtin_amdgcn_readfirstlane(p);
-        tr[k] = p;
-        if (__builtin_amdgcn_readfirstlane(best != 0.0 ? 1 : 0)) {
-#pragma unroll
-            for (int i = k + 1; i < 6; ++i) {
-                if (p == i) {
-#pragma unroll
-                    for (int c = 0; c < 6; ++c) {
-                        const double tmp = A[6 * k + c];
-                        A[6 * k + c] = A[6 * i + c];
-                        A[6 * i + c] = tmp;
-                    }
-                }
-            }
-            const double piv = A[7 * k];
-#pragma unroll
-            for (int i = k + 1; i < 6; ++i) A[6 * i + k] = A[6 * i + k] / piv;
-        }
-#pragma unroll
-        for (int i = k + 1; i < 6; ++i)
-#pragma unroll
-            for (int c = k + 1; c < 6; ++c) A[6 * i + c] = A[6 * i + c] - A[6 * i + k] * A[6 * k + c];
-    }
-    SPROBE(0);
-    // ---- inverse: lane c < 6 solves column c of X = P * I by forward (unit
-    // L) and backward (U) substitution
-    const int cc = lane < 6 ? lane : 0;
-    int pos = cc;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-        if (pos == k) pos = tr[k];
-        else if (pos == tr[k]) pos = k;
-    }
-    double x[6];
-#pragma unroll
-    for (int r = 0; r < 6; ++r) x[r] = (r == pos) ? 1.0 : 0.0;
-#pragma unroll
-    for (int j = 0; j < 6; ++j)
-#pragma unroll
-        for (int i = j + 1; i < 6; ++i) x[i] = x[i] - A[6 * i + j] * x[j];
-#pragma unroll
-    for (int j = 5; j >= 0; --j) {
-        x[j] = x[j] / A[7 * j];
-#pragma unroll
-        for (int i = 0; i < j; ++i) x[i] = x[i] - A[6 * i + j] * x[j];
-    }
-    SPROBE(1);
-    // ---- update = H^-1 * b (row-wise, ascending columns); H^-1[r][c] is
-    // lane c's x[r]
-    double update[6];
-#pragma unroll
-    for (int r = 0; r < 6; ++r) {
-        double s = readlane_f64(x[r], 0) * L.S[21];
-#pragma unroll
-        for (int c = 1; c < 6; ++c) s = s + readlane_f64(x[r], c) * L.S[21 + c];
-        update[r] = s;
-    }
-    SPROBE(2);
-    // ---- SE3::exp(update) (Sophus), sin/cos of theta/2 and theta in lanes 0/1
-    SE3d E;
-    {
-        const double eps = 1e-10;
-        const double* w = update + 3;
-        const double theta_sq = (w[0] * w[0] + w[1] * w[1]) + w[2] * w[2];
-        const double theta = sqrt(theta_sq);
-        const double half_theta = 0.5 * theta;
-        double sn, cs;
-        sincos((lane & 1) ? theta : half_theta, &sn, &cs);
-        const double s_half = readlane_f64(sn, 0), c_half = readlane_f64(cs, 0);
-        const double s_th = readlane_f64(sn, 1), c_th = readlane_f64(cs, 1);
-        double imag, real;
-        if (theta < eps) {
-            const double theta_po4 = theta_sq * theta_sq;
-            imag = 0.5 - (1.0 / 48.0) * theta_sq + (1.0 / 3840.0) * theta_po4;
-            real = 1.0 - 0.5 * theta_sq + (1.0 / 384.0) * theta_po4;
-        } else {
-            imag = s_half / theta;
-            real = c_half;
-        }
-        E.q[0] = imag * w[0];
-        E.q[1] = imag * w[1];
-        E.q[2] = imag * w[2];
-        E.q[3] = real;
-        double V[9];
-        if (theta < eps) {
-            quat_to_matrix(E.q, V);
-        } else {
-            const double O[9] = {0.0, -w[2], w[1], w[2], 0.0, -w[0], -w[1], w[0], 0.0};
-            double O2[9];
-#pragma unroll
-            for (int i = 0; i < 3; ++i)
-#pragma unroll
-                for (int j = 0; j < 3; ++j)
-                    O2[3 * i + j] = (O[3 * i + 0] * O[0 + j] + O[3 * i + 1] * O[3 + j]) + O[3 * i + 2] * O[6 + j];
-            const double th2 = theta * theta;
-            const double c1 = (1.0 - c_th) / th2;
-            const double c2 = (theta - s_th) / (th2 * theta);
-#pragma unroll
-            for (int i = 0; i < 9; ++i) {
-                const double id = (i % 4 == 0) ? 1.0 : 0.0;
-                V[i] = (id + c1 * O[i]) + c2 * O2[i];
-            }
-        }
-        mat3_vec(V, update, E.t);
-    }
-    SPROBE(3);
-    SE3d T21;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) T21.q[k] = L.state[k];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) T21.t[k] = L.state[4 + k];
-    T21 = se3_mul(E, T21);
-    const int ngood = L.ngood;
-    double cost = L.cost + L.S[27];
-    cost /= ngood;
-    const double lastCost = L.last_cost;
-    if (stats) {
-        if (in) stats[2 + lane] = h;
-        if (lane == 0) {
-            stats[0] = ngood;
-            stats[1] = cost;
-            for (int k = 0; k < 6; ++k) stats[38 + k] = L.S[21 + k];
-            for (int k = 0; k < 6; ++k) stats[44 + k] = update[k];
-        }
-    }
-    if (lane == 0) {
-        int cont = 1;
-        if (isnan(update[0])) {
-            for (int k = 0; k < 7; ++k) L.state[k] = L.best[k];
-            cont = 0;
-        } else {
-            for (int k = 0; k < 4; ++k) L.state[k] = T21.q[k];
-            for (int k = 0; k < 3; ++k) L.state[4 + k] = T21.t[k];
-            if (iter > 0 && cost > lastCost) {
-                for (int k = 0; k < 7; ++k) L.state[k] = L.best[k];
-                cont = 0;
-            } else if ((1 - cost / (double)lastCost) < 0.005) {
-                cont = 0;
-            } else {
-                for (int k = 0; k < 7; ++k) L.best[k] = L.state[k];
-                L.last_cost = cost;
-            }
-        }
-        L.cost = cost;
-        L.cont = cont;
-    }
 }
 
 // Continuation (faithful, rare): this workgroup re-evaluates every tile of
@@ -700,9 +638,7 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
     __shared__ double s_pts[kMaxTile * kSums];
     __shared__ int s_good;
     __shared__ int s_arrive;
-    __shared__ uint8_t s_win[kWaves][kCW * kCW];
-    __shared__ double s_lval0[64];  // wave 0's point, prefetched by wave 4
-    __shared__ int s_ok0, s_cw0[3];
+    __shared__ PfLds s_pf;
     const int lv = a.level;
     const bool merged = a.merged && lv == kLevels - 1;
     const int prev = lv + 1;
@@ -754,42 +690,30 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
     }
     PROBE(32 + 6 * (lv + 1));
 
-    // ---- prefetches (every wave but the solver)
-    RefSample pre{};
-    CurWin cw{};
-    const int i0 = (int)blockIdx.x * a.tile + wave;
-    const bool has_pre = tiles && wave < a.tile && i0 < a.n;
+    // ---- prefetch of the whole tile (every wave but the solver): the pose
+    // the windows are predicted at is the seed (unsolved L(3)) or the T21
+    // level sl was evaluated at
     const bool solver = solve && wave == 0;
-    if (has_pre && !solver) {
-        prefetch_point(a, lv, i0, solve, sl, pre, cw);
-        if (!merged) ref_finish(pre);
-        if (cw.on) win_store(s_win[wave], cw);
-    }
-    if (solve && wave == 4 && tiles && a.tile > 0 && (int)blockIdx.x * a.tile < a.n) {
-        RefSample r0{};
-        CurWin c0{};
-        prefetch_point(a, lv, (int)blockIdx.x * a.tile, solve, sl, r0, c0);
-        if (!merged) {
-            ref_finish(r0);
-            s_lval0[lane] = r0.lval;
+    // the solver's SIMD (waves 0 and 4) is left to the solver: wave 4 joins
+    // the prefetch only when there is no solve
+    const bool pf_wave = !solve || (wave != 0 && wave != 4);
+    if (tiles && pf_wave) {
+        double pred[12];
+        if (!solve) {
+            for (int k = 0; k < 12; ++k) pred[k] = a.pose_seed[k];
+        } else {
+            double sp[7];
+            for (int k = 0; k < 7; ++k) sp[k] = a.s.state[sl * kStateStride + k];
+            state_to_pose(sp, pred);
         }
-        if (c0.on) win_store(s_win[0], c0);
-        if (lane == 0) {
-            s_ok0 = r0.ok ? 1 : 0;
-            s_cw0[0] = c0.x0;
-            s_cw0[1] = c0.y0;
-            s_cw0[2] = c0.on ? 1 : 0;
-        }
+        const int first = solve ? wave - 1 - (wave > 4 ? 1 : 0) : wave;
+        const int stride = solve ? kWaves - 2 : kWaves;
+        prefetch_tile(a, lv, blockIdx.x, pred, !merged, first, stride, s_pf);
     }
 
     // ---- the solve (wave 0)
     if (solver) {
-        if (has_pre) {
-            // wave 0's own map point (the rest of its prefetch is wave 4's)
-            pre.P[0] = a.points[3 * i0];
-            pre.P[1] = a.points[3 * i0 + 1];
-            pre.P[2] = a.points[3 * i0 + 2];
-        }
+        __builtin_amdgcn_s_setprio(3);
         while (__hip_atomic_load(&s_arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 5)
             __builtin_amdgcn_s_sleep(1);
         // canonical tree, last level: (w0 + w1) + (w2 + w3)
@@ -798,11 +722,15 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
         PROBE(32 + 6 * (lv + 1) + 1);
         double* stp = (a.stats && blockIdx.x == 0) ? a.stats + (size_t)kStats * sl : nullptr;
 #ifdef VISO_PROBE
-        solve_wave0(L, 0, stp, lv == 1 ? 90 : -1, probe_t0);
+        unsigned long long stamps[4] = {probe_t0, probe_t0, probe_t0, probe_t0};
+        solve_wave0(L, 0, stp, lv == 1 ? stamps : nullptr);
+        if (lv == 1 && lane == 0 && blockIdx.x == 0)
+            for (int k = 0; k < 4; ++k) g_probe[90 + k] += stamps[k] - probe_t0;
 #else
         solve_wave0(L, 0, stp);
 #endif
         PROBE(32 + 6 * (lv + 1) + 2);
+        __builtin_amdgcn_s_setprio(0);
     }
     if (!solve && wave == 0 && lane == 0) {
         // seeded level: no solve, T21 is the seed (thread 256 wrote it)
@@ -822,15 +750,6 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
         }
         __syncthreads();
     }
-    if (solver && has_pre && !merged) {
-        pre.ok = s_ok0 != 0;
-        pre.lval = s_lval0[lane];
-    }
-    if (solver && has_pre) {
-        cw.x0 = s_cw0[0];
-        cw.y0 = s_cw0[1];
-        cw.on = s_cw0[2] != 0;
-    }
     PROBE(lv + 1);
     const int out = lv >= 0 ? lv : kLevels;
     if (blockIdx.x == 0 && t == 0 && !merged) {
@@ -845,20 +764,13 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
         for (int k = 0; k < 7; ++k) a.s.state[lv * kStateStride + k] = L.state[k];
     if (tiles) {
         LevelPair fp = level_pair(a.fp, lv);
-        if (merged) {
-            // `last` pose solved above: the patch taps are read now
-            fp.pose_last = s_last;
-            if (has_pre) {
-                ref_issue(a, fp, lv, i0, pre);
-                ref_finish(pre);
-            }
-        }
+        // merged: the `last` pose was solved above, its patch taps are read now
+        if (merged) fp.pose_last = s_last;
         double pose[12];
 #pragma unroll
         for (int k = 0; k < 12; ++k) pose[k] = s_pose[k];
-        direct_tile(a, fp, lv, pose, blockIdx.x, pre, has_pre, s_win[wave], cw,
-                    a.s.part + (size_t)lv * kMaxTiles * kSums, a.s.good + lv * kMaxTiles, s_pts,
-                    &s_good, true);
+        direct_tile_pf(a, fp, lv, pose, blockIdx.x, s_pf, merged, a.s.part + (size_t)lv * kMaxTiles * kSums,
+                       a.s.good + lv * kMaxTiles, s_pts, &s_good);
     }
     PROBE(8 + lv + 1);
     PROBE_ABS(65 + 4 * (a.level + 1));

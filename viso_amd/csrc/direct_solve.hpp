@@ -1,0 +1,217 @@
+// viso_amd — the serial 6x6 Gauss-Newton step of one direct-pose level on
+// one wave (DirectPoseEstimationSingleLayer, src/viso.cpp:731-753): H, b from
+// the 28 canonical sums -> Eigen PartialPivLU inverse -> update = H^-1 b ->
+// Sophus SE3::exp(update) * T21 -> the loop decision.  Shared by
+// direct_level_kernel (direct.hip) and the solve micro-benchmark
+// (tools/ubench/solve_bench.hip).
+#pragma once
+
+#include "common.hpp"
+#include "device_math.hpp"
+
+
+namespace viso {
+
+constexpr int kSolveSums = 28;
+constexpr int kSolveStateStride = 8;
+
+struct SolveLds {
+    double red[4][kSolveSums];
+    double S[kSolveSums];
+    int g[4];
+    int ngood;
+    double state[kSolveStateStride], best[kSolveStateStride];
+    double cost, last_cost;
+    int cont;
+};
+
+// One GN step of one level on wave 0 (all 64 lanes): L.S -> update, the new
+// L.state and the loop decision L.cont (src/viso.cpp:731-753).
+__device__ inline void solve_wave0(SolveLds& L, int iter, double* stats,
+                                   unsigned long long* stamps = nullptr) {
+    // phase stamps (probe builds): s_memrealtime after LU / inverse / update /
+    // exp, kept in registers (the caller records them)
+#define SPROBE(k)                                                   \
+    do {                                                            \
+        if (stamps) stamps[(k)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+    const int lane = threadIdx.x & 63;
+    const int row = lane / 6, col = lane - 6 * (lane / 6);
+    const bool in = lane < 36;
+    // H (symmetric) from the 21 upper-triangle sums, one element per lane
+    const int r0 = row < col ? row : col, c0 = row < col ? col : row;
+    const double h = in ? L.S[r0 * 6 - (r0 * (r0 - 1)) / 2 + (c0 - r0)] : 0.0;
+    // ---- Eigen PartialPivLU (first maximal |pivot| wins), replicated in the
+    // registers of every lane: no cross-lane traffic on the serial chain; the
+    // pivot row is wave-uniform, so a row swap is a scalar branch + moves.
+    double A[36];
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+            const int r1 = r < c ? r : c, c1 = r < c ? c : r;
+            A[6 * r + c] = L.S[r1 * 6 - (r1 * (r1 - 1)) / 2 + (c1 - r1)];
+        }
+    int tr[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        int p = k;
+        double best = fabs(A[7 * k]);
+#pragma unroll
+        for (int i = k + 1; i < 6; ++i) {
+            const double s = fabs(A[6 * i + k]);
+            if (s > best) {
+                best = s;
+                p = i;
+            }
+        }
+        p = __builtin_amdgcn_readfirstlane(p);
+        tr[k] = p;
+        if (__builtin_amdgcn_readfirstlane(best != 0.0 ? 1 : 0)) {
+#pragma unroll
+            for (int i = k + 1; i < 6; ++i) {
+                if (p == i) {
+#pragma unroll
+                    for (int c = 0; c < 6; ++c) {
+                        const double tmp = A[6 * k + c];
+                        A[6 * k + c] = A[6 * i + c];
+                        A[6 * i + c] = tmp;
+                    }
+                }
+            }
+            const double piv = A[7 * k];
+#pragma unroll
+            for (int i = k + 1; i < 6; ++i) A[6 * i + k] = A[6 * i + k] / piv;
+        }
+#pragma unroll
+        for (int i = k + 1; i < 6; ++i)
+#pragma unroll
+            for (int c = k + 1; c < 6; ++c) A[6 * i + c] = A[6 * i + c] - A[6 * i + k] * A[6 * k + c];
+    }
+    SPROBE(0);
+    // ---- inverse: lane c < 6 solves column c of X = P * I by forward (unit
+    // L) and backward (U) substitution
+    const int cc = lane < 6 ? lane : 0;
+    int pos = cc;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        if (pos == k) pos = tr[k];
+        else if (pos == tr[k]) pos = k;
+    }
+    double x[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) x[r] = (r == pos) ? 1.0 : 0.0;
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+#pragma unroll
+        for (int i = j + 1; i < 6; ++i) x[i] = x[i] - A[6 * i + j] * x[j];
+#pragma unroll
+    for (int j = 5; j >= 0; --j) {
+        x[j] = x[j] / A[7 * j];
+#pragma unroll
+        for (int i = 0; i < j; ++i) x[i] = x[i] - A[6 * i + j] * x[j];
+    }
+    SPROBE(1);
+    // ---- update = H^-1 * b (row-wise, ascending columns); H^-1[r][c] is
+    // lane c's x[r]
+    double update[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+        double s = readlane_f64(x[r], 0) * L.S[21];
+#pragma unroll
+        for (int c = 1; c < 6; ++c) s = s + readlane_f64(x[r], c) * L.S[21 + c];
+        update[r] = s;
+    }
+    SPROBE(2);
+    // ---- SE3::exp(update) (Sophus), sin/cos of theta/2 and theta in lanes 0/1
+    SE3d E;
+    {
+        const double eps = 1e-10;
+        const double* w = update + 3;
+        const double theta_sq = (w[0] * w[0] + w[1] * w[1]) + w[2] * w[2];
+        const double theta = sqrt(theta_sq);
+        const double half_theta = 0.5 * theta;
+        double sn, cs;
+        sincos((lane & 1) ? theta : half_theta, &sn, &cs);
+        const double s_half = readlane_f64(sn, 0), c_half = readlane_f64(cs, 0);
+        const double s_th = readlane_f64(sn, 1), c_th = readlane_f64(cs, 1);
+        double imag, real;
+        if (theta < eps) {
+            const double theta_po4 = theta_sq * theta_sq;
+            imag = 0.5 - (1.0 / 48.0) * theta_sq + (1.0 / 3840.0) * theta_po4;
+            real = 1.0 - 0.5 * theta_sq + (1.0 / 384.0) * theta_po4;
+        } else {
+            imag = s_half / theta;
+            real = c_half;
+        }
+        E.q[0] = imag * w[0];
+        E.q[1] = imag * w[1];
+        E.q[2] = imag * w[2];
+        E.q[3] = real;
+        double V[9];
+        if (theta < eps) {
+            quat_to_matrix(E.q, V);
+        } else {
+            const double O[9] = {0.0, -w[2], w[1], w[2], 0.0, -w[0], -w[1], w[0], 0.0};
+            double O2[9];
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j)
+                    O2[3 * i + j] = (O[3 * i + 0] * O[0 + j] + O[3 * i + 1] * O[3 + j]) + O[3 * i + 2] * O[6 + j];
+            const double th2 = theta * theta;
+            const double c1 = (1.0 - c_th) / th2;
+            const double c2 = (theta - s_th) / (th2 * theta);
+#pragma unroll
+            for (int i = 0; i < 9; ++i) {
+                const double id = (i % 4 == 0) ? 1.0 : 0.0;
+                V[i] = (id + c1 * O[i]) + c2 * O2[i];
+            }
+        }
+        mat3_vec(V, update, E.t);
+    }
+    SPROBE(3);
+    SE3d T21;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) T21.q[k] = L.state[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) T21.t[k] = L.state[4 + k];
+    T21 = se3_mul(E, T21);
+    const int ngood = L.ngood;
+    double cost = L.cost + L.S[27];
+    cost /= ngood;
+    const double lastCost = L.last_cost;
+    if (stats) {
+        if (in) stats[2 + lane] = h;
+        if (lane == 0) {
+            stats[0] = ngood;
+            stats[1] = cost;
+            for (int k = 0; k < 6; ++k) stats[38 + k] = L.S[21 + k];
+            for (int k = 0; k < 6; ++k) stats[44 + k] = update[k];
+        }
+    }
+    if (lane == 0) {
+        int cont = 1;
+        if (isnan(update[0])) {
+            for (int k = 0; k < 7; ++k) L.state[k] = L.best[k];
+            cont = 0;
+        } else {
+            for (int k = 0; k < 4; ++k) L.state[k] = T21.q[k];
+            for (int k = 0; k < 3; ++k) L.state[4 + k] = T21.t[k];
+            if (iter > 0 && cost > lastCost) {
+                for (int k = 0; k < 7; ++k) L.state[k] = L.best[k];
+                cont = 0;
+            } else if ((1 - cost / (double)lastCost) < 0.005) {
+                cont = 0;
+            } else {
+                for (int k = 0; k < 7; ++k) L.best[k] = L.state[k];
+                L.last_cost = cost;
+            }
+        }
+        L.cost = cost;
+        L.cont = cont;
+    }
+}
+
+
+}  // namespace viso
