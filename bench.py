@@ -69,6 +69,8 @@ def parse():
     ap.add_argument("--kitti", default=os.environ.get("VISO_KITTI", ""),
                     help="KITTI odometry data instead of the synthetic sequence: a sequence directory "
                          "(image_0/, image_1/, calib.txt) or a root with sequences/NN (rank r reads NN = r)")
+    ap.add_argument("--precision", choices=["faithful", "fast"], default="faithful",
+                    help="tracking-stage precision of the headline run (viso_params.precision)")
     ap.add_argument("--rig-steps", type=int, default=64,
                     help="timesteps of the 4-camera rig measurement (configs[4]; 0 = skip)")
     return ap.parse_args()
@@ -235,8 +237,9 @@ def main():
     torch.cuda.synchronize()
     frame_bytes = W * H
 
+    precision = viso_amd.PRECISION_FAST if args.precision == "fast" else viso_amd.PRECISION_FAITHFUL
     v = viso_amd.Viso(*seq.K, width=W, height=H, device=local, enable_tracking=1,
-                      batch_frames=args.batch, max_poses=max(1024, n_total + 16))
+                      batch_frames=args.batch, max_poses=max(1024, n_total + 16), precision=precision)
     v.set_stereo(seq.p.baseline, STEREO_MAX_DISP, 1)
     # inside the timed region only the per-chunk groups are bracketed by HIP
     # events (the image pass for the roofline, the LK-alignment batch); the

@@ -56,8 +56,21 @@ typedef struct viso_params {
     int32_t max_poses;                /* capacity of the pose log */
     int32_t batch_frames;             /* frames per viso_process_frames_device
                                          chunk (frame-slot pool size) */
-    int32_t reserved[7];
+    int32_t precision;                /* VISO_PRECISION_FAITHFUL (default) or
+                                         VISO_PRECISION_FAST (tracking stages) */
+    int32_t reserved[6];
 } viso_params;
+
+/* viso_params.precision.
+ * FAITHFUL: fp64 wherever the reference is fp64, results bit-identical to
+ *   the oracle (canonical tree sums, Eigen PartialPivLU inverse).
+ * FAST: tolerance mode for the tracking stages (direct pose, LK alignment):
+ *   fp32 per-pixel sampling / Jacobians / products with fp64 per-point and
+ *   per-map sums, an LDL^T solve of the 6x6 normal equations; validated
+ *   against the oracle at the north star's 1e-4 rel-Frobenius pose bar
+ *   (tests/test_fast_mode.py).  Initialisation stages are always faithful. */
+#define VISO_PRECISION_FAITHFUL 0
+#define VISO_PRECISION_FAST 1
 
 typedef struct viso_ctx viso_ctx;
 

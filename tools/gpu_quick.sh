@@ -19,3 +19,7 @@ timeout -k 10 200 python -u bench.py --no-cpu --no-svo --rig-steps 0 > $OUT/benc
 python -c "
 import json;d=json.loads(open('$OUT/bench.json').read().strip().splitlines()[-1])
 print('value',d['value'],'ms/step',d['ms_per_step'],'kernels',d['kernels'],'breakdown',d['kernels_breakdown_chunk'])"
+timeout -k 10 200 python -u bench.py --no-cpu --no-svo --rig-steps 0 --precision fast > $OUT/bench_fast.json 2> $OUT/bench_fast.err || { echo "bench fast failed"; tail -20 $OUT/bench_fast.err; exit 1; }
+python -c "
+import json;d=json.loads(open('$OUT/bench_fast.json').read().strip().splitlines()[-1])
+print('FAST value',d['value'],'ms/step',d['ms_per_step'],'kernels',d['kernels'],'breakdown',d['kernels_breakdown_chunk'])"

@@ -33,8 +33,9 @@ def main():
     right = np.stack([seq.image(f, 1) for f in range(n)])
     d_left = torch.from_numpy(left).cuda()
     d_right = torch.from_numpy(right).cuda()
+    prec = viso_amd.PRECISION_FAST if os.environ.get("PRECISION", "") == "fast" else viso_amd.PRECISION_FAITHFUL
     v = viso_amd.Viso(*seq.K, width=W, height=H, enable_tracking=1, batch_frames=batch,
-                      max_poses=4096)
+                      max_poses=4096, precision=prec)
     stereo = os.environ.get("MONO", "0") != "1"
     if stereo:  # the bench path: stereo-initialised map
         v.set_stereo(seq.p.baseline, 128, 1)

@@ -23,6 +23,7 @@ __device__ unsigned long long g_probe[128];
 #define REPS 200
 #endif
 
+template <bool LDLT>
 __global__ void bench(const double* S28, const double* st7, double* out, unsigned long long* ticks) {
     __shared__ SolveLds L;
     const int lane = threadIdx.x & 63;
@@ -41,9 +42,15 @@ __global__ void bench(const double* S28, const double* st7, double* out, unsigne
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 #ifdef VISO_PROBE
             unsigned long long stamps[4] = {t0, t0, t0, t0};
-            solve_wave0(L, 0, nullptr, stamps);
+            if (LDLT)
+                solve_wave0_ldlt(L, 0, nullptr, stamps);
+            else
+                solve_wave0(L, 0, nullptr, stamps);
 #else
-            solve_wave0(L, 0, nullptr);
+            if (LDLT)
+                solve_wave0_ldlt(L, 0, nullptr);
+            else
+                solve_wave0(L, 0, nullptr);
 #endif
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             acc += __builtin_amdgcn_s_memrealtime() - t0;
@@ -89,9 +96,14 @@ int main() {
     hipMalloc(&dt, sizeof(unsigned long long));
     hipMemcpy(dS, S, sizeof(S), hipMemcpyHostToDevice);
     hipMemcpy(dst, st, sizeof(st), hipMemcpyHostToDevice);
-    for (int threads : {64, 512}) {
+    for (int variant = 0; variant < 4; ++variant) {
+        const int threads = (variant & 1) ? 512 : 64;
+        const bool ldlt = variant >= 2;
         for (int rep = 0; rep < 2; ++rep) {
-            bench<<<1, threads>>>(dS, dst, dout, dt);
+            if (ldlt)
+                bench<true><<<1, threads>>>(dS, dst, dout, dt);
+            else
+                bench<false><<<1, threads>>>(dS, dst, dout, dt);
             hipDeviceSynchronize();
         }
         unsigned long long t;
@@ -116,8 +128,8 @@ int main() {
                    10.0 * pr[2] / (3.0 * REPS) / 1e3, 10.0 * pr[3] / (3.0 * REPS) / 1e3);
         }
 #endif
-        printf("threads %d: %.3f us per solve; result hash %016llx state %.17g %.17g %.17g\n", threads,
-               10.0 * (double)t / REPS / 1e3, bits, out[0], out[4], out[7]);
+        printf("%s threads %d: %.3f us per solve; result hash %016llx state %.17g %.17g %.17g\n",
+               ldlt ? "LDLT" : "LU", threads, 10.0 * (double)t / REPS / 1e3, bits, out[0], out[4], out[7]);
     }
     return 0;
 }

@@ -9,5 +9,9 @@ from . import _lib  # noqa: F401
 from .api import Context, default_context, default_params, pyramid_dims  # noqa: F401
 from .frontend import FrameHandler, FrameSequence, Keyframe, Viso  # noqa: F401
 
-__all__ = ["Context", "default_context", "default_params", "pyramid_dims", "Viso", "Keyframe",
+# viso_params.precision (include/viso/viso_c.h)
+PRECISION_FAITHFUL = 0
+PRECISION_FAST = 1
+
+__all__ = ["PRECISION_FAITHFUL", "PRECISION_FAST", "Context", "default_context", "default_params", "pyramid_dims", "Viso", "Keyframe",
            "FrameSequence", "FrameHandler"]

@@ -40,7 +40,7 @@ class viso_params(ctypes.Structure):
         ("ransac_h_iters", ctypes.c_int32), ("ransac_confidence", ctypes.c_double),
         ("ransac_seed", ctypes.c_uint64), ("max_features", ctypes.c_int32),
         ("max_poses", ctypes.c_int32), ("batch_frames", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 7),
+        ("precision", ctypes.c_int32), ("reserved", ctypes.c_int32 * 6),
     ]
 
 

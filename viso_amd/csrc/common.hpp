@@ -77,6 +77,14 @@ __host__ __device__ inline void mat3_vec(const double* R, const double* p, doubl
 __device__ inline uint8_t ld_global_u8(const uint8_t* p, long long i) {
     return ((const __attribute__((address_space(1))) uint8_t*)p)[i];
 }
+// Byte i of a buffer of n bytes, 0 outside it.  The load is unconditional
+// (index clamped, value selected): a conditional load compiles to a branch
+// with its own s_waitcnt, which serialises a lane's taps.
+__device__ inline int ld_u8_or0(const uint8_t* p, long long n, long long i) {
+    const bool in = i >= 0 && i < n;
+    const int v = ld_global_u8(p, in ? i : 0);
+    return in ? v : 0;
+}
 __device__ inline uint8_t ld_lds_u8(const uint8_t* p, int i) {
     return ((const __attribute__((address_space(3))) uint8_t*)p)[i];
 }
@@ -91,10 +99,10 @@ __device__ inline double sample_px(const uint8_t* __restrict__ img, int w, int h
     const long long n = (long long)w * (long long)h;
     const bool finite = (x > -1e9 && x < 1e9 && y > -1e9 && y < 1e9);
     long long base = finite ? (long long)(int)y * (long long)w + (long long)(int)x : -(1LL << 40);
-    double d0 = (base >= 0 && base < n) ? (double)ld_global_u8(img, base) : 0.0;
-    double d1 = (base + 1 >= 0 && base + 1 < n) ? (double)ld_global_u8(img, base + 1) : 0.0;
-    double d2 = (base + w >= 0 && base + w < n) ? (double)ld_global_u8(img, base + w) : 0.0;
-    double d3 = (base + w + 1 >= 0 && base + w + 1 < n) ? (double)ld_global_u8(img, base + w + 1) : 0.0;
+    double d0 = (double)ld_u8_or0(img, n, base);
+    double d1 = (double)ld_u8_or0(img, n, base + 1);
+    double d2 = (double)ld_u8_or0(img, n, base + w);
+    double d3 = (double)ld_u8_or0(img, n, base + w + 1);
     double xx = x - floor(x);
     double yy = y - floor(y);
     return double((1 - xx) * (1 - yy) * d0 + xx * (1 - yy) * d1 + (1 - xx) * yy * d2 +
@@ -270,6 +278,84 @@ __device__ inline double reduce_scatter_28(const double* v, int* value_index) {
     const int local = (b2 ? 4 : 0) + (b3 ? 2 : 0) + (b4 ? 1 : 0);
     if (local >= 7) *value_index = -1;
     return f;
+}
+
+// ---- fp32 forms (tolerance mode, VISO_PRECISION_FAST)
+template <int CTRL>
+__device__ inline float dpp_f32(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+__device__ inline void permlane16_swap_f32(float a, float b, float& ra, float& rb) {
+    const auto r = __builtin_amdgcn_permlane16_swap((unsigned)__float_as_int(a), (unsigned)__float_as_int(b),
+                                                    false, false);
+    ra = __int_as_float((int)r[0]);
+    rb = __int_as_float((int)r[1]);
+}
+
+__device__ inline void permlane32_swap_f32(float a, float b, float& ra, float& rb) {
+    const auto r = __builtin_amdgcn_permlane32_swap((unsigned)__float_as_int(a), (unsigned)__float_as_int(b),
+                                                    false, false);
+    ra = __int_as_float((int)r[0]);
+    rb = __int_as_float((int)r[1]);
+}
+
+// reduce_scatter_28 on fp32 values (same butterfly and lane -> index map).
+__device__ inline float reduce_scatter_28_f32(const float* v, int* value_index) {
+    const int lane = threadIdx.x & 63;
+    const bool b0 = lane & 1, b1 = lane & 2, b2 = lane & 4, b3 = lane & 8, b4 = lane & 16;
+    float a[14];
+#pragma unroll
+    for (int k = 0; k < 14; ++k) {
+        const float send = b0 ? v[k] : v[14 + k];
+        const float keep = b0 ? v[14 + k] : v[k];
+        a[k] = keep + dpp_f32<0xB1>(send);
+    }
+    float c[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+        const float send = b1 ? a[k] : a[7 + k];
+        const float keep = b1 ? a[7 + k] : a[k];
+        c[k] = keep + dpp_f32<0x4E>(send);
+    }
+    float d[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float hi = k < 3 ? c[4 + k] : 0.0f;
+        const float send = b2 ? c[k] : hi;
+        const float keep = b2 ? hi : c[k];
+        // both DPP moves evaluated by every lane, then selected (a DPP under a
+        // partial EXEC would read inactive lanes)
+        const float r4 = dpp_f32<0x114>(send), l4 = dpp_f32<0x104>(send);
+        const float recv = b2 ? r4 : l4;
+        d[k] = keep + recv;
+    }
+    float e[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const float send = b3 ? d[k] : d[2 + k];
+        const float keep = b3 ? d[2 + k] : d[k];
+        const float r8 = dpp_f32<0x118>(send), l8 = dpp_f32<0x108>(send);
+        const float recv = b3 ? r8 : l8;
+        e[k] = keep + recv;
+    }
+    float ra, rb;
+    permlane16_swap_f32(e[0], e[1], ra, rb);
+    float f = ra + rb;
+    permlane32_swap_f32(f, f, ra, rb);
+    f = ra + rb;
+    *value_index = (b0 ? 14 : 0) + (b1 ? 7 : 0) + (b2 ? 4 : 0) + (b3 ? 2 : 0) + (b4 ? 1 : 0);
+    const int local = (b2 ? 4 : 0) + (b3 ? 2 : 0) + (b4 ? 1 : 0);
+    if (local >= 7) *value_index = -1;
+    return f;
+}
+
+// fp32 bilinear with weights (xx, yy) of taps a (x, y), b (x + 1, y),
+// c (x, y + 1), d (x + 1, y + 1).
+__device__ inline float bilerp_f32(float a, float b, float c, float d, float xx, float yy) {
+    const float top = __builtin_fmaf(xx, b - a, a);
+    const float bot = __builtin_fmaf(xx, d - c, c);
+    return __builtin_fmaf(yy, bot - top, top);
 }
 
 __device__ inline int wave_sum_int(int v) {

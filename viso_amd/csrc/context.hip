@@ -70,6 +70,7 @@ int viso_default_params(viso_params* p, double fx, double fy, double cx, double 
     p->max_features = 32768;
     p->max_poses = 65536;
     p->batch_frames = 64;
+    p->precision = VISO_PRECISION_FAITHFUL;
     return VISO_OK;
 }
 
@@ -89,6 +90,7 @@ int viso_create(const viso_params* p, int device, viso_ctx** out) {
     *out = nullptr;
     if (p->width < 16 || p->height < 16 || p->width > kMaxWidth) return VISO_ERR_ARG;
     if (p->max_features <= 0 || p->batch_frames <= 0) return VISO_ERR_ARG;
+    if (p->precision != VISO_PRECISION_FAITHFUL && p->precision != VISO_PRECISION_FAST) return VISO_ERR_ARG;
     int rc = check_device_present();
     if (rc != VISO_OK) return rc;
     VISO_HIP_CHECK(hipSetDevice(device));
@@ -277,7 +279,7 @@ int viso_direct_pose(viso_ctx* c, const uint8_t* last_pyr, const uint8_t* cur_py
                            frame_from_base((const uint8_t*)(base + o_c), g), g, K,
                            (const double*)(base + o_p), n, (const double*)(base + o_pl),
                            (const double*)(base + o_pio), direct_scratch_at(base + o_ds), nullptr,
-                           (double*)(base + o_pio), nullptr, -1, c->stream);
+                           (double*)(base + o_pio), nullptr, -1, c->stream, c->p.precision);
     }
     VISO_HIP_CHECK(hipGetLastError());
     VISO_HIP_CHECK(hipMemcpyAsync(pose_io, base + o_pio, 96, hipMemcpyDeviceToHost, c->stream));

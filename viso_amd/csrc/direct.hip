@@ -103,8 +103,11 @@ struct DirectArgs {
     int n;
     const double* pose_seed;  // level 3 starts at SE3(R, t) of this pose (12)
     int level;                // tiles of this level; -1: final solve only
-    int tile;                 // points per tile (power of two, >= kWaves)
+    int tile;                 // points per tile (power of two, >= kWaves); split: the max
     int n_tiles;              // <= 256
+    int split;                // tolerance mode: workgroup b owns points
+                              // [b n / n_tiles, (b + 1) n / n_tiles) (all CUs busy;
+                              // no canonical tree to keep)
     DirectScratch s;
     double* stats;     // [kLevels][kStats] or null
     double* pose_out;  // result pose (12) or null
@@ -119,6 +122,18 @@ struct DirectArgs {
     double* prev_log;
     int prev_log_index;
 };
+
+// The map points of workgroup (tile) b: [*first, *first + *cnt).
+__device__ inline void tile_range(const DirectArgs& a, int b, int* first, int* cnt) {
+    if (a.split) {
+        const int f = (int)(((long long)b * a.n) / a.n_tiles);
+        *first = f;
+        *cnt = (int)(((long long)(b + 1) * a.n) / a.n_tiles) - f;
+    } else {
+        *first = b * a.tile;
+        *cnt = a.tile;  // points past n are skipped (+0.0 leaves)
+    }
+}
 
 // dPixeldXi (src/viso.cpp:640-658)
 __device__ inline void d_pixel_d_xi(const Intrinsics& K, const double* pose, const double* P,
@@ -175,10 +190,10 @@ __device__ inline void ref_issue(const DirectArgs& a, const LevelPair& fp, int l
     const uint8_t* img = fp.last;
     const long long n = (long long)w * (long long)h;
     const long long base = r.ok ? (long long)(int)y * (long long)w + (long long)(int)x : -(1LL << 40);
-    r.t0 = (base >= 0 && base < n) ? ld_global_u8(img, base) : 0;
-    r.t1 = (base + 1 >= 0 && base + 1 < n) ? ld_global_u8(img, base + 1) : 0;
-    r.t2 = (base + w >= 0 && base + w < n) ? ld_global_u8(img, base + w) : 0;
-    r.t3 = (base + w + 1 >= 0 && base + w + 1 < n) ? ld_global_u8(img, base + w + 1) : 0;
+    r.t0 = ld_u8_or0(img, n, base);
+    r.t1 = ld_u8_or0(img, n, base + 1);
+    r.t2 = ld_u8_or0(img, n, base + w);
+    r.t3 = ld_u8_or0(img, n, base + w + 1);
     r.xx = x - floor(x);
     r.yy = y - floor(y);
 }
@@ -202,12 +217,14 @@ __device__ inline void ref_sample(const DirectArgs& a, const LevelPair& fp, int 
 // pose), loaded while the prologue solves.  A sample whose four taps lie in
 // the window (itself inside the image, so no tap wraps a row or leaves the
 // buffer) reads the same bytes from LDS; any other takes sample_px's path.
-constexpr int kCW = 16;
+constexpr int kCW = 20;  // window side: +-4..5 px of prediction error still hit
+constexpr int kCWBytes = kCW * kCW;
+constexpr int kCWLoads = (kCWBytes + 63) / 64;  // bytes per lane
 
 struct CurWin {
     int x0, y0;
     bool on;
-    int b0, b1, b2, b3;  // this lane's 4 bytes: row lane/4, columns 4*(lane%4)..+3
+    uint8_t b[kCWLoads];  // this lane's bytes e = lane + 64 k of the row-major window
 };
 
 __device__ inline void win_issue(const uint8_t* __restrict__ img, int w, int h, double u, double v,
@@ -215,7 +232,6 @@ __device__ inline void win_issue(const uint8_t* __restrict__ img, int w, int h, 
     c.on = w >= kCW && h >= kCW && u > -1e6 && u < 1e6 && v > -1e6 && v < 1e6;
     c.x0 = 0;
     c.y0 = 0;
-    c.b0 = c.b1 = c.b2 = c.b3 = 0;
     if (!c.on) return;
     int x0 = (int)floor(u) - kCW / 2 + 1;
     int y0 = (int)floor(v) - kCW / 2 + 1;
@@ -224,20 +240,21 @@ __device__ inline void win_issue(const uint8_t* __restrict__ img, int w, int h, 
     c.x0 = x0;
     c.y0 = y0;
     const int lane = threadIdx.x & 63;
-    const long long o = (long long)(y0 + (lane >> 2)) * w + x0 + 4 * (lane & 3);
-    c.b0 = ld_global_u8(img, o);
-    c.b1 = ld_global_u8(img, o + 1);
-    c.b2 = ld_global_u8(img, o + 2);
-    c.b3 = ld_global_u8(img, o + 3);
+#pragma unroll
+    for (int k = 0; k < kCWLoads; ++k) {
+        const int e = lane + 64 * k;
+        const int r = e / kCW, col = e - r * kCW;
+        c.b[k] = ld_global_u8(img, (long long)(y0 + min(r, kCW - 1)) * w + x0 + col);
+    }
 }
 
 __device__ inline void win_store(uint8_t* lds, const CurWin& c) {
     const int lane = threadIdx.x & 63;
-    const int o = (lane >> 2) * kCW + 4 * (lane & 3);
-    st_lds_u8(lds, o, (uint8_t)c.b0);
-    st_lds_u8(lds, o + 1, (uint8_t)c.b1);
-    st_lds_u8(lds, o + 2, (uint8_t)c.b2);
-    st_lds_u8(lds, o + 3, (uint8_t)c.b3);
+#pragma unroll
+    for (int k = 0; k < kCWLoads; ++k) {
+        const int e = lane + 64 * k;
+        if (e < kCWBytes) st_lds_u8(lds, e, c.b[k]);
+    }
 }
 
 // sample_px with the taps served from the window when all four lie in it
@@ -298,6 +315,115 @@ __device__ inline bool direct_point_rs(const DirectArgs& a, const LevelPair& fp,
     return true;
 }
 
+// ---------------------------------------------------------------- tolerance mode
+// VISO_PRECISION_FAST: the point's projection and the good test stay fp64
+// (the faithful decisions); then fp32 arithmetic.  The sub-pixel fraction of
+// a projection is shared by all 64 patch pixels (their offsets are integers),
+// so every lane's five samples (value, x +- 1, y +- 1) come from one 12-tap
+// stencil (rows iy-1..iy+2, plus-shaped) with the same weights: from the
+// LDS window when it holds the stencil, else from the level buffer
+// (out-of-buffer taps 0).  dPixel/dXi, J, the 28 products and the reduce-
+// scatter in fp32; the per-point sums are widened to fp64 for the tile and
+// map trees.  Returns good; lane l < 32 with *idx >= 0 holds sum *idx.
+__device__ inline float tap_f32(const uint8_t* __restrict__ img, long long n, long long i) {
+    return (float)ld_u8_or0(img, n, i);
+}
+
+__device__ inline bool direct_point_fast(const DirectArgs& a, const LevelPair& fp, int lv, const double* cur_pose,
+                                         const double* P, float lval, const uint8_t* win, const CurWin& cw,
+                                         float* out, int* idx) {
+    const int lane = threadIdx.x & 63;
+    const int px = (lane >> 3) - 4, py = (lane & 7) - 4;
+    const double scale = kScale[lv];
+    const int w = a.g.w[lv], h = a.g.h[lv];
+    // project_px's arithmetic, keeping the camera-frame point for dPixel/dXi
+    double Pc[3];
+    mat3_vec(cur_pose, P, Pc);
+    Pc[0] = Pc[0] + cur_pose[9];
+    Pc[1] = Pc[1] + cur_pose[10];
+    Pc[2] = Pc[2] + cur_pose[11];
+    const double uc = scale * ((Pc[0] / Pc[2]) * a.K.fx + a.K.cx);
+    const double vc = scale * ((Pc[1] / Pc[2]) * a.K.fy + a.K.cy);
+    const double hp = 4.0;
+    if (!(inside_px(uc - hp, vc - hp, w, h) && inside_px(uc + hp, vc + hp, w, h))) return false;
+    const float x = (float)Pc[0], y = (float)Pc[1], z = (float)Pc[2];
+    const float fxs = (float)(a.K.fx * scale), fys = (float)(a.K.fy * scale);
+    const float iz = 1.0f / z, iz2 = iz * iz;
+    float Jp[12];
+    Jp[0] = fxs * iz;
+    Jp[1] = 0.0f;
+    Jp[2] = -fxs * x * iz2;
+    Jp[3] = -fxs * x * y * iz2;
+    Jp[4] = fxs + fxs * x * x * iz2;
+    Jp[5] = -fxs * y * iz;
+    Jp[6] = 0.0f;
+    Jp[7] = fys * iz;
+    Jp[8] = -fys * y * iz2;
+    Jp[9] = -fys - fys * y * y * iz2;
+    Jp[10] = fys * x * y * iz2;
+    Jp[11] = fys * x * iz;
+    const double fu = floor(uc), fv = floor(vc);
+    const float xx = (float)(uc - fu), yy = (float)(vc - fv);
+    const int ix = (int)fu + px, iy = (int)fv + py;
+    float t01, t02, t10, t11, t12, t13, t20, t21, t22, t23, t31, t32;
+    if (cw.on && ix - 1 >= cw.x0 && ix + 2 < cw.x0 + kCW && iy - 1 >= cw.y0 && iy + 2 < cw.y0 + kCW) {
+        const int o = (iy - cw.y0) * kCW + (ix - cw.x0);
+        t01 = (float)ld_lds_u8(win, o - kCW);
+        t02 = (float)ld_lds_u8(win, o - kCW + 1);
+        t10 = (float)ld_lds_u8(win, o - 1);
+        t11 = (float)ld_lds_u8(win, o);
+        t12 = (float)ld_lds_u8(win, o + 1);
+        t13 = (float)ld_lds_u8(win, o + 2);
+        t20 = (float)ld_lds_u8(win, o + kCW - 1);
+        t21 = (float)ld_lds_u8(win, o + kCW);
+        t22 = (float)ld_lds_u8(win, o + kCW + 1);
+        t23 = (float)ld_lds_u8(win, o + kCW + 2);
+        t31 = (float)ld_lds_u8(win, o + 2 * kCW);
+        t32 = (float)ld_lds_u8(win, o + 2 * kCW + 1);
+    } else {
+        const uint8_t* C = fp.cur;
+        const long long n = (long long)w * h, o = (long long)iy * w + ix;
+        t01 = tap_f32(C, n, o - w);
+        t02 = tap_f32(C, n, o - w + 1);
+        t10 = tap_f32(C, n, o - 1);
+        t11 = tap_f32(C, n, o);
+        t12 = tap_f32(C, n, o + 1);
+        t13 = tap_f32(C, n, o + 2);
+        t20 = tap_f32(C, n, o + w - 1);
+        t21 = tap_f32(C, n, o + w);
+        t22 = tap_f32(C, n, o + w + 1);
+        t23 = tap_f32(C, n, o + w + 2);
+        t31 = tap_f32(C, n, o + 2 * w);
+        t32 = tap_f32(C, n, o + 2 * w + 1);
+    }
+    const float i0 = bilerp_f32(t11, t12, t21, t22, xx, yy);
+    const float g0 = 0.5f * (bilerp_f32(t12, t13, t22, t23, xx, yy) - bilerp_f32(t10, t11, t20, t21, xx, yy));
+    const float g1 = 0.5f * (bilerp_f32(t21, t22, t31, t32, xx, yy) - bilerp_f32(t01, t02, t11, t12, xx, yy));
+    const float error = lval - i0;
+    float J[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) J[k] = -__builtin_fmaf(g0, Jp[k], g1 * Jp[6 + k]);
+    float leaf[kSums];
+    int e = 0;
+#pragma unroll
+    for (int rr = 0; rr < 6; ++rr)
+#pragma unroll
+        for (int c = rr; c < 6; ++c) leaf[e++] = J[rr] * J[c];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) leaf[21 + k] = -error * J[k];
+    leaf[27] = error * error;
+    *out = reduce_scatter_28_f32(leaf, idx);
+    return true;
+}
+
+// The `last` sample of this lane's pixel in tolerance mode: the four taps
+// (packed, sample_px's bytes) with the projection's shared fraction.
+__device__ inline float fast_lval(uint32_t t, double ur, double vr) {
+    const float xx = (float)(ur - floor(ur)), yy = (float)(vr - floor(vr));
+    return bilerp_f32((float)(t & 0xff), (float)((t >> 8) & 0xff), (float)((t >> 16) & 0xff), (float)(t >> 24),
+                      xx, yy);
+}
+
 // Tile b of level lv (a.tile points) -> part[b][28], good[b].  Called by
 // every thread of the workgroup.  `pre` (may be null) is the prefetched
 // RefSample of this wave's first point of the tile (valid when has_pre).
@@ -307,14 +433,15 @@ __device__ void direct_tile(const DirectArgs& a, const LevelPair& fp, int lv, co
                             const CurWin& cw, double* part, int* good, double* s_pts,
                             int* s_good, bool zeroed = false) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int T = a.tile;
+    int first, T;
+    tile_range(a, b, &first, &T);
     if (!zeroed) {
         if (threadIdx.x == 0) *s_good = 0;
         __syncthreads();
     }
     int good_cnt = 0;
     for (int local = wave; local < T; local += kWaves) {
-        const int i = b * T + local;
+        const int i = first + local;
         double f = 0.0;
         int idx = -1;
         bool ok = false;
@@ -355,7 +482,7 @@ __device__ void direct_tile(const DirectArgs& a, const LevelPair& fp, int lv, co
 // read nothing but LDS (and the rare sample outside its window).
 struct PfLds {
     uint32_t taps[kMaxTile][64];
-    uint8_t win[kMaxTile][kCW * kCW];
+    uint8_t win[kMaxTile][kCWBytes];
     double P[kMaxTile][3];
     double ur[kMaxTile], vr[kMaxTile];
     int ok[kMaxTile];
@@ -401,15 +528,18 @@ __device__ inline void pf_store(int j, bool ref, const PfPoint& q, PfLds& pf) {
 }
 
 // Points j = first, first + stride, ... of tile b, two at a time (the loads
-// of both in flight together).  `ref` = false when the `last` pose is solved
-// in this launch (merged L(3)): the taps are then read in the tile phase.
-__device__ void prefetch_tile(const DirectArgs& a, int lv, int b, const double* pred, bool ref, int first,
-                              int stride, PfLds& pf) {
-    const LevelPair fp = level_pair(a.fp, lv);
-    const int T = a.tile;
+// of both in flight together).  `pose_last` is the pose of the `last`
+// projection: the `last` frame's own, or in a merged L(3) (whose `last` pose
+// is solved in this launch) a prediction, checked per lane in the tile phase.
+__device__ void prefetch_tile(const DirectArgs& a, int lv, int b, const double* pred, const double* pose_last,
+                              bool ref, int first, int stride, PfLds& pf) {
+    LevelPair fp = level_pair(a.fp, lv);
+    fp.pose_last = pose_last;
+    int p0, T;
+    tile_range(a, b, &p0, &T);
     for (int j = first; j < T; j += 2 * stride) {
         const int j2 = j + stride;
-        const int i0 = b * T + j, i1 = b * T + j2;
+        const int i0 = p0 + j, i1 = p0 + j2;
         const bool v0 = i0 < a.n, v1 = j2 < T && i1 < a.n;
         PfPoint q0{}, q1{};
         if (v0) pf_issue(a, fp, lv, i0, pred, ref, q0);
@@ -441,32 +571,97 @@ __device__ inline void pf_ref(const PfLds& pf, int j, RefSample& r) {
     ref_finish(r);
 }
 
+// The `last` sample of prefetched point j in a merged L(3): the projection
+// under the solved `last` pose (ref_issue's arithmetic); the taps prefetched
+// under the predicted pose are used where a lane's base pixel is the same,
+// any other lane loads its four taps now (ref_issue's loads).
+__device__ inline void merged_ref(const DirectArgs& a, const LevelPair& fp, int lv, const PfLds& pf, int j,
+                                  RefSample& r) {
+    const int lane = threadIdx.x & 63;
+    const int px = (lane >> 3) - 4, py = (lane & 7) - 4;
+    const int w = a.g.w[lv], h = a.g.h[lv];
+    r.P[0] = pf.P[j][0];
+    r.P[1] = pf.P[j][1];
+    r.P[2] = pf.P[j][2];
+    project_px(fp.pose_last, a.K, r.P, kScale[lv], r.ur, r.vr);
+    const double hp = 4.0;
+    r.ok = inside_px(r.ur - hp, r.vr - hp, w, h) && inside_px(r.ur + hp, r.vr + hp, w, h);
+    const double x = r.ur + px, y = r.vr + py;
+    r.xx = x - floor(x);
+    r.yy = y - floor(y);
+    r.t0 = r.t1 = r.t2 = r.t3 = 0;
+    if (!r.ok) return;
+    const long long base = (long long)(int)y * (long long)w + (long long)(int)x;
+    const double xp = pf.ur[j] + px, yp = pf.vr[j] + py;
+    const long long bp = pf.ok[j] ? (long long)(int)yp * (long long)w + (long long)(int)xp : -(1LL << 40);
+    if (base == bp) {
+        const uint32_t t = pf.taps[j][lane];
+        r.t0 = (int)(t & 0xff);
+        r.t1 = (int)((t >> 8) & 0xff);
+        r.t2 = (int)((t >> 16) & 0xff);
+        r.t3 = (int)(t >> 24);
+    } else {
+        const uint8_t* img = fp.last;
+        const long long n = (long long)w * (long long)h;
+        r.t0 = ld_u8_or0(img, n, base);
+        r.t1 = ld_u8_or0(img, n, base + 1);
+        r.t2 = ld_u8_or0(img, n, base + w);
+        r.t3 = ld_u8_or0(img, n, base + w + 1);
+    }
+}
+
 // Tile b of level lv from the prologue's prefetch (the tile phase of
-// direct_level_kernel; direct_tile's arithmetic and tree).
+// direct_level_kernel; direct_tile's arithmetic and tree; FAST: the
+// tolerance-mode point sums).
+template <bool FAST>
 __device__ void direct_tile_pf(const DirectArgs& a, const LevelPair& fp, int lv, const double* cur_pose, int b,
                                const PfLds& pf, bool merged, double* part, int* good, double* s_pts,
                                int* s_good) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int T = a.tile;
+    int first, T;
+    tile_range(a, b, &first, &T);
     int good_cnt = 0;
     for (int local = wave; local < T; local += kWaves) {
-        const int i = b * T + local;
+        const int i = first + local;
         double f = 0.0;
         int idx = -1;
         bool ok = false;
         if (i < a.n) {
             RefSample r;
             if (merged) {
-                ref_issue(a, fp, lv, i, r);
-                ref_finish(r);
-            } else {
+                merged_ref(a, fp, lv, pf, local, r);
+                if (!FAST) ref_finish(r);
+            } else if (!FAST) {
                 pf_ref(pf, local, r);
+            } else {
+                r.P[0] = pf.P[local][0];
+                r.P[1] = pf.P[local][1];
+                r.P[2] = pf.P[local][2];
+                r.ur = pf.ur[local];
+                r.vr = pf.vr[local];
+                r.ok = pf.ok[local] != 0;
+                const uint32_t t = pf.taps[local][lane];
+                r.t0 = (int)(t & 0xff);
+                r.t1 = (int)((t >> 8) & 0xff);
+                r.t2 = (int)((t >> 16) & 0xff);
+                r.t3 = (int)(t >> 24);
             }
             CurWin cw;
             cw.x0 = pf.cw[local][0];
             cw.y0 = pf.cw[local][1];
             cw.on = pf.cw[local][2] != 0;
-            ok = direct_point_rs(a, fp, lv, cur_pose, r, pf.win[local], cw, &f, &idx);
+            if (FAST) {
+                float ff = 0.0f;
+                if (r.ok) {
+                    const uint32_t t = (uint32_t)r.t0 | ((uint32_t)r.t1 << 8) | ((uint32_t)r.t2 << 16) |
+                                       ((uint32_t)r.t3 << 24);
+                    ok = direct_point_fast(a, fp, lv, cur_pose, r.P, fast_lval(t, r.ur, r.vr), pf.win[local],
+                                           cw, &ff, &idx);
+                }
+                f = (double)ff;
+            } else {
+                ok = direct_point_rs(a, fp, lv, cur_pose, r, pf.win[local], cw, &f, &idx);
+            }
         }
         if (!ok) {
             if (lane < kSums) s_pts[local * kSums + lane] = 0.0;
@@ -557,6 +752,7 @@ __device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_b
 
 // GN iterations 1.. of level lv (the faithful continuation, rare): every
 // workgroup re-evaluates all tiles itself at the new T21 and solves again.
+template <bool FAST>
 __device__ void solve_continue(const DirectArgs& a, const LevelPair& fp, int lv, SolveLds& L,
                                double* stats, double* s_pose, double* s_pts, int* s_good) {
     const int t = threadIdx.x, wave = t >> 6;
@@ -568,7 +764,12 @@ __device__ void solve_continue(const DirectArgs& a, const LevelPair& fp, int lv,
             load_partials(a.s.cont_part + (size_t)blockIdx.x * kMaxTiles * kSums,
                           a.s.cont_good + (size_t)blockIdx.x * kMaxTiles, a.n_tiles, v, gg);
         reduce_partials(v, gg, L);
-        if (wave == 0) solve_wave0(L, iter, stats);
+        if (wave == 0) {
+            if (FAST)
+                solve_wave0_ldlt(L, iter, stats);
+            else
+                solve_wave0(L, iter, stats);
+        }
         __syncthreads();
     }
 }
@@ -629,6 +830,7 @@ __device__ inline void after_solve(const DirectArgs& a, bool merged, SolveLds& L
 //   prefetches (their map point, `last` patch taps and current-image window;
 //   wave 4 also prefetches wave 0's point) stay off its path.  B2 (block
 //   barrier) hands the new pose to every wave; then the tiles.
+template <bool FAST>
 __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
     PROBE_T0();
     PROBE_ABS(64 + 4 * (a.level + 1));
@@ -708,7 +910,9 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
         }
         const int first = solve ? wave - 1 - (wave > 4 ? 1 : 0) : wave;
         const int stride = solve ? kWaves - 2 : kWaves;
-        prefetch_tile(a, lv, blockIdx.x, pred, !merged, first, stride, s_pf);
+        // merged: the `last` pose is this launch's solve of the previous
+        // frame's level 0, predicted by the T21 that level was evaluated at
+        prefetch_tile(a, lv, blockIdx.x, pred, merged ? pred : a.fp.pose_last, true, first, stride, s_pf);
     }
 
     // ---- the solve (wave 0)
@@ -723,11 +927,17 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
         double* stp = (a.stats && blockIdx.x == 0) ? a.stats + (size_t)kStats * sl : nullptr;
 #ifdef VISO_PROBE
         unsigned long long stamps[4] = {probe_t0, probe_t0, probe_t0, probe_t0};
-        solve_wave0(L, 0, stp, lv == 1 ? stamps : nullptr);
+        if (FAST)
+            solve_wave0_ldlt(L, 0, stp, lv == 1 ? stamps : nullptr);
+        else
+            solve_wave0(L, 0, stp, lv == 1 ? stamps : nullptr);
         if (lv == 1 && lane == 0 && blockIdx.x == 0)
             for (int k = 0; k < 4; ++k) g_probe[90 + k] += stamps[k] - probe_t0;
 #else
-        solve_wave0(L, 0, stp);
+        if (FAST)
+            solve_wave0_ldlt(L, 0, stp);
+        else
+            solve_wave0(L, 0, stp);
 #endif
         PROBE(32 + 6 * (lv + 1) + 2);
         __builtin_amdgcn_s_setprio(0);
@@ -743,7 +953,7 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
         // the continuation needs every thread; it leaves s_good dirty
         double* stp = (a.stats && blockIdx.x == 0) ? a.stats + (size_t)kStats * sl : nullptr;
         const LevelPair cfp = merged ? level_pair(a.prev, sl) : level_pair(a.fp, sl);
-        solve_continue(a, cfp, sl, L, stp, s_pose, s_pts, &s_good);
+        solve_continue<FAST>(a, cfp, sl, L, stp, s_pose, s_pts, &s_good);
         if (t == 0) {
             after_solve(a, merged, L, s_last, s_pose);
             s_good = 0;
@@ -769,7 +979,7 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
         double pose[12];
 #pragma unroll
         for (int k = 0; k < 12; ++k) pose[k] = s_pose[k];
-        direct_tile_pf(a, fp, lv, pose, blockIdx.x, s_pf, merged, a.s.part + (size_t)lv * kMaxTiles * kSums,
+        direct_tile_pf<FAST>(a, fp, lv, pose, blockIdx.x, s_pf, merged, a.s.part + (size_t)lv * kMaxTiles * kSums,
                        a.s.good + lv * kMaxTiles, s_pts, &s_good);
     }
     PROBE(8 + lv + 1);
@@ -822,7 +1032,7 @@ DirectScratch direct_scratch_at(void* base) {
 namespace {
 DirectArgs direct_args(const FrameDev& last_pyr, const FrameDev& cur_pyr, const PyrGeom& g,
                        const double K[4], const double* points, int n, const double* pose_last12,
-                       const double* pose_seed12, const DirectScratch& s, double* stats) {
+                       const double* pose_seed12, const DirectScratch& s, double* stats, bool split) {
     DirectArgs a{};
     a.fp.last = last_pyr;
     a.fp.cur = cur_pyr;
@@ -836,6 +1046,11 @@ DirectArgs direct_args(const FrameDev& last_pyr, const FrameDev& cur_pyr, const 
     while (P < n) P <<= 1;
     a.tile = P / kMaxTiles > kWaves ? P / kMaxTiles : kWaves;
     a.n_tiles = (n + a.tile - 1) / a.tile;
+    if (split && n > 0) {
+        a.split = 1;
+        a.n_tiles = n < kMaxTiles ? n : kMaxTiles;
+        a.tile = (n + a.n_tiles - 1) / a.n_tiles;
+    }
     a.s = s;
     a.stats = stats;
     a.log_index = -1;
@@ -848,9 +1063,9 @@ void launch_direct_levels(const FrameDev& last_pyr, const FrameDev& cur_pyr, con
                           const double K[4], const double* points, int n,
                           const double* pose_last12, const double* pose_seed12,
                           const DirectScratch& s, double* stats, const DirectPrev* merge,
-                          hipStream_t stream) {
+                          hipStream_t stream, int precision) {
     DirectArgs a = direct_args(last_pyr, cur_pyr, g, K, points, n, pose_last12, pose_seed12, s,
-                               stats);
+                               stats, precision == VISO_PRECISION_FAST);
     if (merge) {
         a.merged = 1;
         a.prev.last = merge->last;
@@ -863,7 +1078,10 @@ void launch_direct_levels(const FrameDev& last_pyr, const FrameDev& cur_pyr, con
     const int grid = a.n_tiles > 0 ? a.n_tiles : 1;
     for (int level = kLevels - 1; level >= 0; --level) {
         a.level = level;
-        direct_level_kernel<<<grid, kThreads, 0, stream>>>(a);
+        if (precision == VISO_PRECISION_FAST)
+            direct_level_kernel<true><<<grid, kThreads, 0, stream>>>(a);
+        else
+            direct_level_kernel<false><<<grid, kThreads, 0, stream>>>(a);
         a.merged = 0;
     }
 }
@@ -871,25 +1089,28 @@ void launch_direct_levels(const FrameDev& last_pyr, const FrameDev& cur_pyr, con
 void launch_direct_final(const FrameDev& last_pyr, const FrameDev& cur_pyr, const PyrGeom& g,
                          const double K[4], const double* points, int n,
                          const double* pose_last12, const DirectScratch& s, double* stats,
-                         double* pose_out, double* log, int log_index, hipStream_t stream) {
+                         double* pose_out, double* log, int log_index, hipStream_t stream, int precision) {
     DirectArgs a = direct_args(last_pyr, cur_pyr, g, K, points, n, pose_last12, pose_last12, s,
-                               stats);
+                               stats, precision == VISO_PRECISION_FAST);
     a.pose_out = pose_out;
     a.log = log;
     a.log_index = log ? log_index : -1;
     a.level = -1;
-    direct_level_kernel<<<1, kThreads, 0, stream>>>(a);
+    if (precision == VISO_PRECISION_FAST)
+        direct_level_kernel<true><<<1, kThreads, 0, stream>>>(a);
+    else
+        direct_level_kernel<false><<<1, kThreads, 0, stream>>>(a);
 }
 
 void launch_direct_pose(const FrameDev& last_pyr, const FrameDev& cur_pyr, const PyrGeom& g,
                         const double K[4], const double* points, int n,
                         const double* pose_last12, const double* pose_seed12,
                         const DirectScratch& s, double* stats, double* pose_out, double* log,
-                        int log_index, hipStream_t stream) {
+                        int log_index, hipStream_t stream, int precision) {
     launch_direct_levels(last_pyr, cur_pyr, g, K, points, n, pose_last12, pose_seed12, s, stats,
-                         nullptr, stream);
+                         nullptr, stream, precision);
     launch_direct_final(last_pyr, cur_pyr, g, K, points, n, pose_last12, s, stats, pose_out, log,
-                        log_index, stream);
+                        log_index, stream, precision);
 }
 
 }  // namespace viso

@@ -25,16 +25,121 @@ struct SolveLds {
     int cont;
 };
 
-// One GN step of one level on wave 0 (all 64 lanes): L.S -> update, the new
-// L.state and the loop decision L.cont (src/viso.cpp:731-753).
-__device__ inline void solve_wave0(SolveLds& L, int iter, double* stats,
-                                   unsigned long long* stamps = nullptr) {
-    // phase stamps (probe builds): s_memrealtime after LU / inverse / update /
-    // exp, kept in registers (the caller records them)
+// phase stamps (probe builds): s_memrealtime after LU / inverse / update /
+// exp, kept in registers (the caller records them)
 #define SPROBE(k)                                                   \
     do {                                                            \
         if (stamps) stamps[(k)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
+
+// The rest of one GN step after `update` (src/viso.cpp:735-753): SE3::exp,
+// T21 = exp(update) * T21, cost /= nGood and the loop decision; stats of
+// block 0.  `h`: this lane's H element (lane < 36, row-major) for stats.
+__device__ inline void solve_finish(SolveLds& L, const double* update, double h, int iter, double* stats,
+                                    unsigned long long* stamps) {
+    const int lane = threadIdx.x & 63;
+    const bool in = lane < 36;
+    // the loop decision (src/viso.cpp:739-753) does not depend on the new
+    // T21: its operands are read and evaluated first, off the exp chain
+    const int ngood = L.ngood;
+    double cost = L.cost + L.S[27];
+    cost /= ngood;
+    const double lastCost = L.last_cost;
+    const bool nan_update = isnan(update[0]);
+    const bool cost_up = iter > 0 && cost > lastCost;
+    const bool converged = (1 - cost / (double)lastCost) < 0.005;
+    SE3d T21;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) T21.q[k] = L.state[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) T21.t[k] = L.state[4 + k];
+    // ---- SE3::exp(update) (Sophus), sin/cos of theta/2 and theta in lanes 0/1
+    SE3d E;
+    {
+        const double eps = 1e-10;
+        const double* w = update + 3;
+        const double theta_sq = (w[0] * w[0] + w[1] * w[1]) + w[2] * w[2];
+        const double theta = sqrt(theta_sq);
+        const double half_theta = 0.5 * theta;
+        double sn, cs;
+        sincos((lane & 1) ? theta : half_theta, &sn, &cs);
+        const double s_half = readlane_f64(sn, 0), c_half = readlane_f64(cs, 0);
+        const double s_th = readlane_f64(sn, 1), c_th = readlane_f64(cs, 1);
+        double imag, real;
+        if (theta < eps) {
+            const double theta_po4 = theta_sq * theta_sq;
+            imag = 0.5 - (1.0 / 48.0) * theta_sq + (1.0 / 3840.0) * theta_po4;
+            real = 1.0 - 0.5 * theta_sq + (1.0 / 384.0) * theta_po4;
+        } else {
+            imag = s_half / theta;
+            real = c_half;
+        }
+        E.q[0] = imag * w[0];
+        E.q[1] = imag * w[1];
+        E.q[2] = imag * w[2];
+        E.q[3] = real;
+        double V[9];
+        if (theta < eps) {
+            quat_to_matrix(E.q, V);
+        } else {
+            const double O[9] = {0.0, -w[2], w[1], w[2], 0.0, -w[0], -w[1], w[0], 0.0};
+            double O2[9];
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j)
+                    O2[3 * i + j] = (O[3 * i + 0] * O[0 + j] + O[3 * i + 1] * O[3 + j]) + O[3 * i + 2] * O[6 + j];
+            const double th2 = theta * theta;
+            const double c1 = (1.0 - c_th) / th2;
+            const double c2 = (theta - s_th) / (th2 * theta);
+#pragma unroll
+            for (int i = 0; i < 9; ++i) {
+                const double id = (i % 4 == 0) ? 1.0 : 0.0;
+                V[i] = (id + c1 * O[i]) + c2 * O2[i];
+            }
+        }
+        mat3_vec(V, update, E.t);
+    }
+    SPROBE(3);
+    T21 = se3_mul(E, T21);
+    if (stats) {
+        if (in) stats[2 + lane] = h;
+        if (lane == 0) {
+            stats[0] = ngood;
+            stats[1] = cost;
+            for (int k = 0; k < 6; ++k) stats[38 + k] = L.S[21 + k];
+            for (int k = 0; k < 6; ++k) stats[44 + k] = update[k];
+        }
+    }
+    if (lane == 0) {
+        int cont = 1;
+        if (nan_update) {
+            for (int k = 0; k < 7; ++k) L.state[k] = L.best[k];
+            cont = 0;
+        } else {
+            for (int k = 0; k < 4; ++k) L.state[k] = T21.q[k];
+            for (int k = 0; k < 3; ++k) L.state[4 + k] = T21.t[k];
+            if (cost_up) {
+                for (int k = 0; k < 7; ++k) L.state[k] = L.best[k];
+                cont = 0;
+            } else if (converged) {
+                cont = 0;
+            } else {
+                for (int k = 0; k < 7; ++k) L.best[k] = L.state[k];
+                L.last_cost = cost;
+            }
+        }
+        L.cost = cost;
+        L.cont = cont;
+    }
+}
+
+
+
+// One GN step of one level on wave 0 (all 64 lanes): L.S -> update, the new
+// L.state and the loop decision L.cont (src/viso.cpp:731-753).
+__device__ inline void solve_wave0(SolveLds& L, int iter, double* stats,
+                                   unsigned long long* stamps = nullptr) {
     const int lane = threadIdx.x & 63;
     const int row = lane / 6, col = lane - 6 * (lane / 6);
     const bool in = lane < 36;
@@ -123,95 +228,79 @@ __device__ inline void solve_wave0(SolveLds& L, int iter, double* stats,
         update[r] = s;
     }
     SPROBE(2);
-    // ---- SE3::exp(update) (Sophus), sin/cos of theta/2 and theta in lanes 0/1
-    SE3d E;
-    {
-        const double eps = 1e-10;
-        const double* w = update + 3;
-        const double theta_sq = (w[0] * w[0] + w[1] * w[1]) + w[2] * w[2];
-        const double theta = sqrt(theta_sq);
-        const double half_theta = 0.5 * theta;
-        double sn, cs;
-        sincos((lane & 1) ? theta : half_theta, &sn, &cs);
-        const double s_half = readlane_f64(sn, 0), c_half = readlane_f64(cs, 0);
-        const double s_th = readlane_f64(sn, 1), c_th = readlane_f64(cs, 1);
-        double imag, real;
-        if (theta < eps) {
-            const double theta_po4 = theta_sq * theta_sq;
-            imag = 0.5 - (1.0 / 48.0) * theta_sq + (1.0 / 3840.0) * theta_po4;
-            real = 1.0 - 0.5 * theta_sq + (1.0 / 384.0) * theta_po4;
-        } else {
-            imag = s_half / theta;
-            real = c_half;
-        }
-        E.q[0] = imag * w[0];
-        E.q[1] = imag * w[1];
-        E.q[2] = imag * w[2];
-        E.q[3] = real;
-        double V[9];
-        if (theta < eps) {
-            quat_to_matrix(E.q, V);
-        } else {
-            const double O[9] = {0.0, -w[2], w[1], w[2], 0.0, -w[0], -w[1], w[0], 0.0};
-            double O2[9];
-#pragma unroll
-            for (int i = 0; i < 3; ++i)
-#pragma unroll
-                for (int j = 0; j < 3; ++j)
-                    O2[3 * i + j] = (O[3 * i + 0] * O[0 + j] + O[3 * i + 1] * O[3 + j]) + O[3 * i + 2] * O[6 + j];
-            const double th2 = theta * theta;
-            const double c1 = (1.0 - c_th) / th2;
-            const double c2 = (theta - s_th) / (th2 * theta);
-#pragma unroll
-            for (int i = 0; i < 9; ++i) {
-                const double id = (i % 4 == 0) ? 1.0 : 0.0;
-                V[i] = (id + c1 * O[i]) + c2 * O2[i];
-            }
-        }
-        mat3_vec(V, update, E.t);
-    }
-    SPROBE(3);
-    SE3d T21;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) T21.q[k] = L.state[k];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) T21.t[k] = L.state[4 + k];
-    T21 = se3_mul(E, T21);
-    const int ngood = L.ngood;
-    double cost = L.cost + L.S[27];
-    cost /= ngood;
-    const double lastCost = L.last_cost;
-    if (stats) {
-        if (in) stats[2 + lane] = h;
-        if (lane == 0) {
-            stats[0] = ngood;
-            stats[1] = cost;
-            for (int k = 0; k < 6; ++k) stats[38 + k] = L.S[21 + k];
-            for (int k = 0; k < 6; ++k) stats[44 + k] = update[k];
-        }
-    }
-    if (lane == 0) {
-        int cont = 1;
-        if (isnan(update[0])) {
-            for (int k = 0; k < 7; ++k) L.state[k] = L.best[k];
-            cont = 0;
-        } else {
-            for (int k = 0; k < 4; ++k) L.state[k] = T21.q[k];
-            for (int k = 0; k < 3; ++k) L.state[4 + k] = T21.t[k];
-            if (iter > 0 && cost > lastCost) {
-                for (int k = 0; k < 7; ++k) L.state[k] = L.best[k];
-                cont = 0;
-            } else if ((1 - cost / (double)lastCost) < 0.005) {
-                cont = 0;
-            } else {
-                for (int k = 0; k < 7; ++k) L.best[k] = L.state[k];
-                L.last_cost = cost;
-            }
-        }
-        L.cost = cost;
-        L.cont = cont;
-    }
+    solve_finish(L, update, h, iter, stats, stamps);
 }
 
+
+// Tolerance mode (VISO_PRECISION_FAST): update = H^-1 b by an LDL^T
+// factorisation of the (symmetric positive semi-definite) H and two
+// triangular solves, replicated in every lane (no pivoting, no explicit
+// inverse: ~1/4 of the faithful PartialPivLU chain).  A non-positive or
+// non-finite pivot gives a NaN update, which reverts the level as the
+// reference's isnan(update[0]) test does.  Then solve_finish as faithful.
+__device__ inline void solve_wave0_ldlt(SolveLds& L, int iter, double* stats,
+                                        unsigned long long* stamps = nullptr) {
+    const int lane = threadIdx.x & 63;
+    const int row = lane / 6, col = lane - 6 * (lane / 6);
+    const bool in = lane < 36;
+    const int r0 = row < col ? row : col, c0 = row < col ? col : row;
+    const double h = in ? L.S[r0 * 6 - (r0 * (r0 - 1)) / 2 + (c0 - r0)] : 0.0;
+    double A[21];  // lower triangle, row-major: A[i(i+1)/2 + j], j <= i
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j) A[i * (i + 1) / 2 + j] = L.S[j * 6 - (j * (j - 1)) / 2 + (i - j)];
+    double b[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) b[k] = L.S[21 + k];
+    double Dinv[6];
+    bool bad = false;
+    // A = L D L^T in place: A[i][j] (j < i) <- L_ij, A[i][i] <- D_i
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        double d = A[k * (k + 1) / 2 + k];
+#pragma unroll
+        for (int j = 0; j < k; ++j) {
+            const double lkj = A[k * (k + 1) / 2 + j];
+            d = __builtin_fma(-lkj * lkj, A[j * (j + 1) / 2 + j], d);
+        }
+        bad = bad || !(d > 0.0) || !(d < 1e300);
+        const double di = 1.0 / d;
+        Dinv[k] = di;
+        A[k * (k + 1) / 2 + k] = d;
+#pragma unroll
+        for (int i = k + 1; i < 6; ++i) {
+            double s = A[i * (i + 1) / 2 + k];
+#pragma unroll
+            for (int j = 0; j < k; ++j)
+                s = __builtin_fma(-A[i * (i + 1) / 2 + j] * A[j * (j + 1) / 2 + j], A[k * (k + 1) / 2 + j], s);
+            A[i * (i + 1) / 2 + k] = s * di;
+        }
+    }
+    SPROBE(0);
+    // L y = b, z = D^-1 y, L^T x = z
+    double y[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        double s = b[i];
+#pragma unroll
+        for (int j = 0; j < i; ++j) s = __builtin_fma(-A[i * (i + 1) / 2 + j], y[j], s);
+        y[i] = s;
+    }
+    double update[6];
+#pragma unroll
+    for (int i = 5; i >= 0; --i) {
+        double s = y[i] * Dinv[i];
+#pragma unroll
+        for (int j = i + 1; j < 6; ++j) s = __builtin_fma(-A[j * (j + 1) / 2 + i], update[j], s);
+        update[i] = s;
+    }
+    if (bad)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) update[k] = __builtin_nan("");
+    SPROBE(1);
+    SPROBE(2);
+    solve_finish(L, update, h, iter, stats, stamps);
+}
 
 }  // namespace viso

@@ -323,7 +323,7 @@ int viso_ctx::resolve_direct() {
     launch_direct_final(frame(dpend_last), frame(dpend_cur), geom, K, (const double*)map_pts.ptr,
                         n_map, pose_of(dpend_last), direct, (double*)direct_stats.ptr,
                         pose_of(dpend_cur), dpend_log >= 0 ? (double*)pose_log.ptr : nullptr,
-                        dpend_log, stream);
+                        dpend_log, stream, p.precision);
     VISO_HIP_CHECK(hipGetLastError());
     drop(dpend_cur);
     drop(dpend_last);
@@ -541,7 +541,7 @@ int viso_ctx::on_new_frame(int cur) {
                 }
                 launch_direct_levels(frame(last_slot), frame(cur), g, K, (const double*)map_pts.ptr,
                                      n_map, pose_of(last_slot), pose_of(last_slot), direct,
-                                     (double*)direct_stats.ptr, dpend ? &m : nullptr, stream);
+                                     (double*)direct_stats.ptr, dpend ? &m : nullptr, stream, p.precision);
             }
             if (dpend) {
                 drop(dpend_cur);

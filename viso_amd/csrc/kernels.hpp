@@ -1,6 +1,7 @@
 // viso_amd — host-side launcher declarations (one translation unit per stage).
 #pragma once
 
+#include "../../include/viso/viso_c.h"
 #include "common.hpp"
 
 namespace viso {
@@ -115,7 +116,7 @@ void launch_direct_pose(const FrameDev& last, const FrameDev& cur, const PyrGeom
                         const double K[4], const double* points, int n,
                         const double* pose_last12, const double* pose_seed12,
                         const DirectScratch& s, double* stats, double* pose_out, double* log,
-                        int log_index, hipStream_t stream);
+                        int log_index, hipStream_t stream, int precision = VISO_PRECISION_FAITHFUL);
 // The same call split for the frame pipeline: L(3..0) of this frame, then F
 // later.  With `merge`, L(3) also runs the previous frame's pending F (its
 // level-0 solve; the solved pose is this frame's `last` pose and seed, so
@@ -132,11 +133,12 @@ void launch_direct_levels(const FrameDev& last, const FrameDev& cur, const PyrGe
                           const double K[4], const double* points, int n,
                           const double* pose_last12, const double* pose_seed12,
                           const DirectScratch& s, double* stats, const DirectPrev* merge,
-                          hipStream_t stream);
+                          hipStream_t stream, int precision = VISO_PRECISION_FAITHFUL);
 void launch_direct_final(const FrameDev& last, const FrameDev& cur, const PyrGeom& g,
                          const double K[4], const double* points, int n,
                          const double* pose_last12, const DirectScratch& s, double* stats,
-                         double* pose_out, double* log, int log_index, hipStream_t stream);
+                         double* pose_out, double* log, int log_index, hipStream_t stream,
+                         int precision = VISO_PRECISION_FAITHFUL);
 // dst (12 doubles, device) <- src (host values, passed by value)
 void launch_set_pose(double* dst, const double src[12], hipStream_t stream);
 
