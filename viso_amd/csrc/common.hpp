@@ -350,6 +350,27 @@ __device__ inline float reduce_scatter_28_f32(const float* v, int* value_index) 
     return f;
 }
 
+// wave_tree_sum3 on fp32 values (same butterfly; results of lanes 0, 1, 2).
+__device__ inline void wave_tree_sum3_f32(float a, float b, float c, float& ra, float& rb, float& rc) {
+    const int lane = threadIdx.x & 63;
+    const bool b0 = lane & 1, b1 = lane & 2, b2 = lane & 4, b3 = lane & 8;
+    const float p = (b0 ? b : a) + dpp_f32<0xB1>(b0 ? a : b);
+    const float q = (b0 ? 0.0f : c) + dpp_f32<0xB1>(b0 ? c : 0.0f);
+    float v = (b1 ? q : p) + dpp_f32<0x4E>(b1 ? p : q);
+    const float r4 = dpp_f32<0x114>(v), l4 = dpp_f32<0x104>(v);
+    v = v + (b2 ? r4 : l4);
+    const float r8 = dpp_f32<0x118>(v), l8 = dpp_f32<0x108>(v);
+    v = v + (b3 ? r8 : l8);
+    float x, y;
+    permlane16_swap_f32(v, v, x, y);
+    v = x + y;
+    permlane32_swap_f32(v, v, x, y);
+    v = x + y;
+    ra = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+    rb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 1));
+    rc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 2));
+}
+
 // fp32 bilinear with weights (xx, yy) of taps a (x, y), b (x + 1, y),
 // c (x, y + 1), d (x + 1, y + 1).
 __device__ inline float bilerp_f32(float a, float b, float c, float d, float xx, float yy) {

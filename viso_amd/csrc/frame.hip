@@ -274,6 +274,7 @@ LkAlignArgs viso_ctx::lk_args() {
     a.tmpl_h = (double*)lk_tmpl_h.ptr;
     a.tmpl_kf = (int32_t*)lk_tmpl_kf.ptr;
     a.tmpl_uv = (double*)lk_tmpl_uv.ptr;
+    a.fast = p.precision == VISO_PRECISION_FAST ? 1 : 0;
     return a;
 }
 

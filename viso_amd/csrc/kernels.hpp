@@ -72,6 +72,9 @@ struct LkAlignArgs {
     double* tmpl_h = nullptr;  // [n][4][4]
     int32_t* tmpl_kf = nullptr;
     double* tmpl_uv = nullptr;  // [n][2]
+    // tolerance mode (VISO_PRECISION_FAST): tmpl / tmpl_h hold floats, same
+    // layout; the iterations run in fp32 (lk_align_kernel<true>)
+    int fast = 0;
 };
 void launch_lk_align(const LkAlignArgs& a, hipStream_t stream);
 // Keyframe choice + per-level templates of every map point (once per map).

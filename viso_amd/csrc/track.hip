@@ -27,6 +27,12 @@ namespace viso {
 
 namespace {
 
+// f.l[level] without indexing a FrameDev at run time (a run-time index into
+// a by-value struct makes the compiler copy it per thread into LDS / scratch)
+__device__ inline const uint8_t* level_ptr(const FrameDev& f, int level) {
+    return level == 0 ? f.l[0] : level == 1 ? f.l[1] : level == 2 ? f.l[2] : f.l[3];
+}
+
 struct LkResult {
     double dx, dy;
     bool succ;
@@ -44,34 +50,55 @@ struct Window {
     int x0, y0;
 };
 
-__device__ inline Window load_window(uint8_t* lds, const uint8_t* img, int w, int h, double cx,
-                                     double cy) {
-    Window win{nullptr, 0, 0};
-    if (w < kWinW || h < kWinH || !(cx > -1e6 && cx < 1e6 && cy > -1e6 && cy < 1e6)) return win;
+// The window's bytes in flight (issued, not yet in LDS): lane l holds bytes
+// l + 64 k of the row-major window.
+constexpr int kWinPer = kWinW * kWinH / 64;  // 9
+struct WinRegs {
+    uint8_t v[kWinPer];
+    int x0, y0;
+    bool on;
+};
+
+__device__ inline WinRegs window_issue(const uint8_t* img, int w, int h, double cx, double cy) {
+    WinRegs r;
+    r.on = !(w < kWinW || h < kWinH || !(cx > -1e6 && cx < 1e6 && cy > -1e6 && cy < 1e6));
+    r.x0 = r.y0 = 0;
+    if (!r.on) return r;
     int x0 = (int)floor(cx) - kWinW / 2 + 1;
     int y0 = (int)floor(cy) - kWinH / 2 + 1;
     x0 = min(max(x0, 0), w - kWinW);
     y0 = min(max(y0, 0), h - kWinH);
     const int lane = threadIdx.x & 63;
-    // all nine loads first, then the LDS stores: interleaved, each store
-    // (through a generic pointer) would wait for its load
-    constexpr int kPer = kWinW * kWinH / 64;  // 9
-    uint8_t v[kPer];
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) {
+    for (int k = 0; k < kWinPer; ++k) {
         const int e = lane + 64 * k;
-        const int r = e / kWinW, c = e - r * kWinW;
-        v[k] = ld_global_u8(img, (long long)(y0 + r) * w + (x0 + c));
+        const int rr = e / kWinW, c = e - rr * kWinW;
+        r.v[k] = ld_global_u8(img, (long long)(y0 + rr) * w + (x0 + c));
     }
+    r.x0 = x0;
+    r.y0 = y0;
+    return r;
+}
+
+__device__ inline Window window_commit(uint8_t* lds, const WinRegs& r) {
+    Window win{nullptr, 0, 0};
+    if (!r.on) return win;
+    const int lane = threadIdx.x & 63;
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) st_lds_u8(lds, lane + 64 * k, v[k]);
+    for (int k = 0; k < kWinPer; ++k) st_lds_u8(lds, lane + 64 * k, r.v[k]);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     win.lds = lds;
-    win.x0 = x0;
-    win.y0 = y0;
+    win.x0 = r.x0;
+    win.y0 = r.y0;
     return win;
+}
+
+__device__ inline Window load_window(uint8_t* lds, const uint8_t* img, int w, int h, double cx,
+                                     double cy) {
+    // all nine loads first, then the LDS stores
+    return window_commit(lds, window_issue(img, w, h, cx, cy));
 }
 
 // sample_px with the tap fetch served from the window when possible
@@ -102,6 +129,12 @@ __device__ inline double sample_win(const uint8_t* __restrict__ img, int w, int 
 struct LkTemplate {
     double I1, J0, J1;
     double i00, i01, i10, i11;
+};
+
+// the same in fp32 (tolerance mode)
+struct LkTemplateF {
+    float I1, J0, J1;
+    float ih[4];
 };
 
 __device__ inline LkTemplate lk_prepare(const uint8_t* __restrict__ img1, int w1, int h1,
@@ -177,6 +210,63 @@ __device__ inline LkResult lk_level(const uint8_t* __restrict__ img1, int w1, in
     const LkTemplate t = lk_prepare(img1, w1, h1, ref_x, ref_y);
     return lk_iterate<MAXIT, KLT_BOUNDS>(t, w1, h1, img2, w2, h2, cur_x, cur_y, bx, by, dx, dy,
                                          thresh, win);
+}
+
+// Tolerance mode (VISO_PRECISION_FAST) GN iterations of one LKAlignment
+// level: the same control flow (bounds test on ref coords + d, NaN / cost-
+// increase stops, success = last accepted cost <= thresh) in fp32.  The
+// sub-pixel fraction of (patch origin + d) is shared by the 64 lanes (their
+// offsets are integers), so a sample is four window taps and three fmas.
+template <int MAXIT>
+__device__ inline LkResult lk_iterate_fast(float I1, float J0, float J1, const float* ih, int w1, int h1,
+                                           const uint8_t* __restrict__ img2, int w2, int h2, double ox,
+                                           double oy, int px, int py, double bx, double by, double thresh,
+                                           const Window& win) {
+    const double hp = 4.0;
+    double dx = 0.0, dy = 0.0;
+    float lastCost = 0.0f;
+    bool succ = true;
+    int iter = 0;
+    const long long n2 = (long long)w2 * h2;
+    for (; iter < MAXIT; ++iter) {
+        if (!inside_px(bx + dx - hp, by + dy - hp, w1, h1) || !inside_px(bx + dx + hp, by + dy + hp, w1, h1)) {
+            succ = false;
+            break;
+        }
+        const double X = ox + dx, Y = oy + dy;
+        const double fX = floor(X), fY = floor(Y);
+        const float xx = (float)(X - fX), yy = (float)(Y - fY);
+        const int ix = (int)fX + px, iy = (int)fY + py;
+        float t0, t1, t2, t3;
+        if (win.lds && ix >= win.x0 && ix + 1 < win.x0 + kWinW && iy >= win.y0 && iy + 1 < win.y0 + kWinH) {
+            const int o = (iy - win.y0) * kWinW + (ix - win.x0);
+            t0 = (float)ld_lds_u8(win.lds, o);
+            t1 = (float)ld_lds_u8(win.lds, o + 1);
+            t2 = (float)ld_lds_u8(win.lds, o + kWinW);
+            t3 = (float)ld_lds_u8(win.lds, o + kWinW + 1);
+        } else {
+            const long long o = (long long)iy * w2 + ix;
+            t0 = (float)ld_u8_or0(img2, n2, o);
+            t1 = (float)ld_u8_or0(img2, n2, o + 1);
+            t2 = (float)ld_u8_or0(img2, n2, o + w2);
+            t3 = (float)ld_u8_or0(img2, n2, o + w2 + 1);
+        }
+        const float e = I1 - bilerp_f32(t0, t1, t2, t3, xx, yy);
+        float B0, B1, cost;
+        wave_tree_sum3_f32(-J0 * e, -J1 * e, e * e, B0, B1, cost);
+        const float u0 = ih[0] * B0 + ih[1] * B1;
+        const float u1 = ih[2] * B0 + ih[3] * B1;
+        if (isnan(u0)) {
+            succ = false;
+            break;
+        }
+        if (iter > 0 && cost > lastCost) break;
+        dx += (double)u0;
+        dy += (double)u1;
+        lastCost = cost;
+        succ = !((double)lastCost > thresh);
+    }
+    return {dx, dy, succ, iter};
 }
 
 __global__ __launch_bounds__(256) void klt_kernel(FrameDev ref, FrameDev cur, PyrDev g,
@@ -281,6 +371,20 @@ __global__ __launch_bounds__(256) void lk_template_kernel(LkAlignArgs a) {
         const double s = kScale[level];
         const int w = a.g.w[level], h = a.g.h[level];
         const LkTemplate t = lk_prepare(refp.l[level], w, h, bu * s + px, bv * s + py);
+        if (a.fast) {
+            float* d = (float*)a.tmpl + ((size_t)i * kLevels + level) * 192;
+            d[lane] = (float)t.I1;
+            d[64 + lane] = (float)t.J0;
+            d[128 + lane] = (float)t.J1;
+            if (lane == 0) {
+                float* hh = (float*)a.tmpl_h + ((size_t)i * kLevels + level) * 4;
+                hh[0] = (float)t.i00;
+                hh[1] = (float)t.i01;
+                hh[2] = (float)t.i10;
+                hh[3] = (float)t.i11;
+            }
+            continue;
+        }
         double* d = a.tmpl + ((size_t)i * kLevels + level) * 192;
         d[lane] = t.I1;
         d[64 + lane] = t.J0;
@@ -299,17 +403,23 @@ __global__ __launch_bounds__(256) void lk_template_kernel(LkAlignArgs a) {
 // x are point groups; the grid's x extent is a multiple of 8, so a point
 // group stays on one XCD for every frame and its templates stay in that
 // XCD's L2.
-__global__ __launch_bounds__(256) void lk_align_kernel(LkAlignArgs a) {
-    __shared__ uint8_t s_win[4][kWinW * kWinH];
+template <bool FAST>
+__global__ __launch_bounds__(256, 4) void lk_align_kernel(LkAlignArgs a) {
+    __shared__ uint8_t s_win[4][2][kWinW * kWinH];
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= a.n) return;
     // frame of the batch (blockIdx.y): its pyramid, pose and output rows
-    const LkFrame& fr = a.frames[blockIdx.y];
+    // run-time indices into the kernel argument are read straight from the
+    // kernarg segment (`a` is the only argument, at offset 0): a run-time
+    // index into the by-value struct would copy it per thread to scratch
+    const LkAlignArgs* ka = (const LkAlignArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    const LkFrame& fr = ka->frames[blockIdx.y];
     const FrameDev cur = fr.cur;
     const double* cur_pose = fr.pose;
     const size_t o = (size_t)blockIdx.y * a.out_stride;
     const int lane = threadIdx.x & 63;
-    uint8_t* my_win = s_win[threadIdx.x >> 6];
+    uint8_t* my_win0 = s_win[threadIdx.x >> 6][0];
+    uint8_t* my_win1 = s_win[threadIdx.x >> 6][1];
     const int px = (lane >> 3) - 4, py = (lane & 7) - 4;
     const double P[3] = {a.points[3 * i], a.points[3 * i + 1], a.points[3 * i + 2]};
     const Intrinsics K{a.K[0], a.K[1], a.K[2], a.K[3]};
@@ -332,22 +442,23 @@ __global__ __launch_bounds__(256) void lk_align_kernel(LkAlignArgs a) {
             ub[0] = uc;
             ub[1] = vc;
             double cu = uc, cv = vc;
-            const FrameDev refp = a.kf[kf];
+            const FrameDev& refp = ka->kf[kf];
             bool succ = false;
 #ifdef VISO_PROBE
             unsigned long long pr_it[kLevels] = {0, 0, 0, 0}, pr_win = 0, pr_iter = 0, pr_long = 0;
             const unsigned long long pr_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
-            for (int level = kLevels - 1; level >= 0; --level) {
-                const double s = kScale[level];
-                const int w = a.g.w[level], h = a.g.h[level];
-                const double cx = cu * s + px, cy = cv * s + py;
-#ifdef VISO_PROBE
-                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-#endif
-                // template loads first: in flight together with the window's
-                LkTemplate t;
-                if (a.tmpl) {
+            // level l's window (around the position level l + 1 ended at) and
+            // template are loaded when level l + 1 is done
+            auto tmpl_load = [&](int level, LkTemplate& t, LkTemplateF& tf) {
+                if (FAST) {
+                    const float* d = (const float*)a.tmpl + ((size_t)i * kLevels + level) * 192;
+                    const float* hh = (const float*)a.tmpl_h + ((size_t)i * kLevels + level) * 4;
+                    tf.I1 = d[lane];
+                    tf.J0 = d[64 + lane];
+                    tf.J1 = d[128 + lane];
+                    for (int k = 0; k < 4; ++k) tf.ih[k] = hh[k];
+                } else if (a.tmpl) {
                     const double* d = a.tmpl + ((size_t)i * kLevels + level) * 192;
                     const double* hh = a.tmpl_h + ((size_t)i * kLevels + level) * 4;
                     t.I1 = d[lane];
@@ -358,13 +469,50 @@ __global__ __launch_bounds__(256) void lk_align_kernel(LkAlignArgs a) {
                     t.i10 = hh[2];
                     t.i11 = hh[3];
                 }
-                const Window win = load_window(my_win, cur.l[level], w, h, cu * s, cv * s);
-                if (!a.tmpl) t = lk_prepare(refp.l[level], w, h, bu * s + px, bv * s + py);
+            };
+            LkTemplate tn{};
+            LkTemplateF tfn{};
+            tmpl_load(kLevels - 1, tn, tfn);
+            Window win = load_window(my_win0, level_ptr(cur, kLevels - 1), a.g.w[kLevels - 1],
+                                     a.g.h[kLevels - 1], cu * kScale[kLevels - 1], cv * kScale[kLevels - 1]);
+            for (int level = kLevels - 1; level >= 0; --level) {
+                const double s = kScale[level];
+                const int w = a.g.w[level], h = a.g.h[level];
+                const double cx = cu * s + px, cy = cv * s + py;
+                LkTemplate t = tn;
+                const LkTemplateF tf = tfn;
+                const Window wcur = win;
+                // (issuing level l-1's loads before iterating level l was
+                // measured slower: the batch is issue-bound, and the extra
+                // live registers cost occupancy)
+                auto next = [&]() {
+                    if (level > 0) {
+                        const double s1 = kScale[level - 1];
+                        tmpl_load(level - 1, tn, tfn);
+                        win = load_window((level & 1) ? my_win0 : my_win1, level_ptr(cur, level - 1),
+                                          a.g.w[level - 1], a.g.h[level - 1], cu * s1, cv * s1);
+                    }
+                };
+#ifdef VISO_PROBE
+                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+#endif
+                if (FAST) {
+                    // tolerance mode: fp32 template (lk_template_kernel) and iterations
+                    const LkResult r = lk_iterate_fast<100>(tf.I1, tf.J0, tf.J1, tf.ih, w, h, level_ptr(cur, level),
+                                                            w, h, cu * s, cv * s, px, py, bu * s, bv * s, a.thresh,
+                                                            wcur);
+                    succ = r.succ;
+                    cu = cu + r.dx / s;
+                    cv = cv + r.dy / s;
+                    next();
+                    continue;
+                }
+                if (!a.tmpl) t = lk_prepare(level_ptr(refp, level), w, h, bu * s + px, bv * s + py);
 #ifdef VISO_PROBE
                 const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
 #endif
-                LkResult r = lk_iterate<100, false>(t, w, h, cur.l[level], w, h, cx, cy, bu * s,
-                                                    bv * s, 0.0, 0.0, a.thresh, win);
+                LkResult r = lk_iterate<100, false>(t, w, h, level_ptr(cur, level), w, h, cx, cy, bu * s,
+                                                    bv * s, 0.0, 0.0, a.thresh, wcur);
                 succ = r.succ;
 #ifdef VISO_PROBE
                 pr_it[level] += (unsigned long long)r.iters;
@@ -374,6 +522,7 @@ __global__ __launch_bounds__(256) void lk_align_kernel(LkAlignArgs a) {
 #endif
                 cu = cu + r.dx / s;  // pair.uv_cur += V2d{dx/s, dy/s}
                 cv = cv + r.dy / s;
+                next();
             }
 #ifdef VISO_PROBE
             if (lane == 0) {
@@ -452,7 +601,10 @@ void launch_klt(const FrameDev& ref, const FrameDev& cur, const PyrGeom& g, cons
 void launch_lk_align(const LkAlignArgs& a, hipStream_t stream) {
     if (a.n <= 0 || a.n_frames <= 0) return;
     const int gx = (((a.n + 3) / 4) + 7) / 8 * 8;  // multiple of 8: XCD-stable point groups
-    lk_align_kernel<<<dim3(gx, a.n_frames), 256, 0, stream>>>(a);
+    if (a.fast)
+        lk_align_kernel<true><<<dim3(gx, a.n_frames), 256, 0, stream>>>(a);
+    else
+        lk_align_kernel<false><<<dim3(gx, a.n_frames), 256, 0, stream>>>(a);
 }
 
 void launch_lk_template(const LkAlignArgs& a, hipStream_t stream) {
