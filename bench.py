@@ -71,6 +71,8 @@ def parse():
                          "(image_0/, image_1/, calib.txt) or a root with sequences/NN (rank r reads NN = r)")
     ap.add_argument("--precision", choices=["faithful", "fast"], default="faithful",
                     help="tracking-stage precision of the headline run (viso_params.precision)")
+    ap.add_argument("--no-other", action="store_true",
+                    help="skip the run at the other precision (other_precision in the line)")
     ap.add_argument("--rig-steps", type=int, default=64,
                     help="timesteps of the 4-camera rig measurement (configs[4]; 0 = skip)")
     return ap.parse_args()
@@ -125,6 +127,45 @@ def measure_svo(args, seq, left, right, d_left, d_right, W, H, log, n):
         out["parity_vs_oracle"] = {"pairs": int(m),
                                    "pose_max_abs_diff": float(np.abs(gp - op).max()) if len(gp) == len(op) else None}
     return out
+
+
+def measure_tolerance(args, seq, d_left, d_right, W, H, warm, steps, log):
+    """The other precision on the same resident pairs and frame range as the
+    headline (viso_params.precision; tolerance mode = fp32 per-pixel tracking
+    stages with fp64 sums, include/viso/viso_c.h): frames/s and its poses."""
+    import time as _t
+
+    import torch
+
+    import viso_amd
+    prec = viso_amd.PRECISION_FAITHFUL if args.precision == "fast" else viso_amd.PRECISION_FAST
+    v = viso_amd.Viso(*seq.K, width=W, height=H, enable_tracking=1, batch_frames=args.batch,
+                      max_poses=max(1024, warm + steps + 16), precision=prec)
+    v.set_stereo(seq.p.baseline, STEREO_MAX_DISP, 1)
+    fb = W * H
+
+    def run(f0, n):
+        f = f0
+        while f < f0 + n:
+            m = min(args.batch, f0 + n - f)
+            v.process_device(d_left.data_ptr() + f * fb, d_right.data_ptr() + f * fb, m, fb)
+            f += m
+
+    run(0, warm)
+    v.synchronize()
+    n0 = len(v.poses)
+    torch.cuda.synchronize()
+    t0 = _t.perf_counter()
+    run(warm, steps)
+    v.synchronize()
+    dt = _t.perf_counter() - t0
+    poses = v.poses
+    out = {"precision": "fast" if prec == viso_amd.PRECISION_FAST else "faithful",
+           "value": round(steps / dt, 2), "unit": "frames/s", "ms_per_step": round(1e3 * dt / steps, 4),
+           "tracking_frames_timed": len(poses) - n0,
+           "dtype": "f32 per-pixel, f64 sums and solve" if prec == viso_amd.PRECISION_FAST else "f64"}
+    log(f"[{out['precision']}] {out['value']} frames/s")
+    return out, poses
 
 
 def measure_rig(args, W, H, log):
@@ -344,6 +385,9 @@ def main():
     # circular matching, RANSAC + Gauss-Newton; include/viso/viso_svo.h) has
     # no reference counterpart; it is measured beside the headline metric on
     # the same resident pairs (rank 0).
+    other = other_poses = None
+    if rank == 0 and not args.no_other:
+        other, other_poses = measure_tolerance(args, seq, d_left, d_right, W, H, warm, steps, log)
     stereo_vo = None
     if rank == 0 and not args.no_svo:
         stereo_vo = measure_svo(args, seq, left, right, d_left, d_right, W, H, log, warm + steps)
@@ -382,6 +426,11 @@ def main():
         m = min(len(oP), len(gP))
         if m:
             diff = np.linalg.norm(gP[:m] - oP[:m], axis=1) / np.maximum(np.linalg.norm(oP[:m], axis=1), 1e-300)
+            if other_poses is not None and len(other_poses) >= m:
+                d2 = (np.linalg.norm(other_poses[:m] - oP[:m], axis=1) /
+                      np.maximum(np.linalg.norm(oP[:m], axis=1), 1e-300))
+                other["parity_vs_oracle"] = {"frames": int(m), "max_rel_frobenius": float(d2.max()),
+                                             "bar": 1e-4}
             parity = {"frames": int(m), "max_rel_frobenius": float(diff.max()),
                       "rmse_translation": float(np.sqrt(np.mean(np.sum((gP[:m, 9:] - oP[:m, 9:]) ** 2, 1))))}
 
@@ -391,7 +440,9 @@ def main():
             "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
             "steps": steps, "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / steps, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "scaling": "weak", "vs_baseline": None,
+            "dtype": "f64" if args.precision == "faithful" else "f32 per-pixel, f64 sums and solve",
+            "precision": args.precision,
             "data": "synthetic" if source == "synthetic" else f"KITTI-format PNG pairs ({source})",
             "config": {"workload": (f"configs[1]: one {W}x{H} grey stereo sequence per GPU, "
                                     "KITTI seq-00 intrinsics" if (W, H) == (1242, 375) else
@@ -414,6 +465,7 @@ def main():
             "timed_frames_by_state": frames_by_state,
             "gn_reduction": gn_ev,
             "matching_pass_hbm": mp_ev,
+            "other_precision": other,
             "stereo_vo": stereo_vo,
             "last_frame_stats": {"direct_nGood": st[9], "lk_pairs": st[6], "lk_success": st[7]},
         }

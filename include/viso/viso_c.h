@@ -224,6 +224,19 @@ int viso_stereo_match(viso_ctx* ctx, const uint8_t* left, const uint8_t* right, 
  * 1 <= min_disp < max_disp when enabled. */
 int viso_set_stereo(viso_ctx* ctx, double baseline, int32_t max_disp, int32_t min_disp);
 
+/* Stereo keyframe insertion (map maintenance the
+ * reference lacks: its map is frozen after src/viso.cpp:79-96; the repo's own
+ * spec, restated in oracle/oracle_viso.cpp).  With stereo enabled and
+ * interval > 0: after every interval-th tracking frame whose level-0 direct-
+ * pose nGood is below ngood_permille / 1000 of the map size, the frame's
+ * stereo points (as viso_set_stereo, in world coordinates R^T (Pc - T) with
+ * its pose) are appended to the map, the frame becomes a keyframe (LK
+ * alignment may pair points with it) and stats[14] = points added;
+ * stats[15] = keyframes.  At most 8 keyframes and 16384 map points.  Each
+ * check is one host synchronisation.  interval 0 (default) = off, the
+ * reference's frozen map. */
+int viso_set_keyframes(viso_ctx* ctx, int32_t interval, int32_t ngood_permille);
+
 /* Library build/version string (e.g. "viso_amd 0.1 gfx950"). */
 const char* viso_version(void);
 

@@ -78,6 +78,10 @@ struct oracle_viso {
     // stereo initialisation (viso_set_stereo)
     double stereo_base = 0;
     int max_disp = 0, min_disp = 1;
+    // stereo keyframe insertion (viso_set_keyframes; the repo's own map
+    // maintenance)
+    int kf_interval = 0, kf_permille = 0;
+    long long track_cnt = 0;
 };
 
 extern "C" {
@@ -275,6 +279,33 @@ void on_new(oracle_viso* v, const uint8_t* img, const uint8_t* right) {
             v->stats[6] = pairs;
             v->stats[7] = succ;
             v->poses.push_back(X);
+            // stereo keyframe insertion: every kf_interval-th tracking frame,
+            // when fewer than kf_permille / 1000 of the map points were good
+            // at level 0, this frame's stereo points join the map (world =
+            // R^T (Pc - T) with its pose) and the frame becomes a keyframe
+            ++v->track_cnt;
+            if (v->kf_interval > 0 && right && v->stereo_base > 0 && v->track_cnt % v->kf_interval == 0 &&
+                (int)v->keyframes.size() < 8 && (double)st[0] < v->kf_permille * (double)np / 1000.0) {
+                std::vector<int32_t> xs((size_t)w * h / 4 + 16), ys(xs.size()), sc(xs.size());
+                const int nf = oracle_fast(cur->pyr.data(), w, h, v->p.fast_thresh, xs.data(), ys.data(), sc.data(),
+                                           (int)xs.size());
+                std::vector<double> pts((size_t)3 * nf + 3);
+                int m = oracle_stereo_points(cur->pyr.data(), right, w, h, xs.data(), ys.data(), nf, v->max_disp,
+                                             v->min_disp, v->K4, v->stereo_base, pts.data());
+                const int cap = 16384 - np;  // kMaxMapPoints
+                if (m > cap) m = cap;
+                const double* R = cur->R;
+                const double* T = cur->T;
+                for (int i = 0; i < m; ++i) {
+                    const double d0 = pts[(size_t)3 * i] - T[0], d1 = pts[(size_t)3 * i + 1] - T[1],
+                                 d2 = pts[(size_t)3 * i + 2] - T[2];
+                    for (int k = 0; k < 3; ++k)
+                        v->points.push_back((R[k] * d0 + R[3 + k] * d1) + R[6 + k] * d2);
+                }
+                v->keyframes.push_back(cur);
+                v->stats[14] = m;
+            }
+            v->stats[15] = (double)v->keyframes.size();
             break;
         }
         default:
@@ -292,6 +323,11 @@ void oracle_viso_on_new_frame(oracle_viso* v, const uint8_t* img) { on_new(v, im
 
 void oracle_viso_on_new_stereo(oracle_viso* v, const uint8_t* left, const uint8_t* right) {
     on_new(v, left, right);
+}
+
+void oracle_viso_set_keyframes(oracle_viso* v, int interval, int ngood_permille) {
+    v->kf_interval = interval;
+    v->kf_permille = ngood_permille;
 }
 
 void oracle_viso_set_stereo(oracle_viso* v, double baseline, int max_disp, int min_disp) {

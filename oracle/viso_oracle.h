@@ -178,6 +178,13 @@ void oracle_viso_set_stereo(oracle_viso* v, double baseline, int max_disp, int m
 // map from them (one keyframe, identity pose, metric scale); otherwise, and
 // in every other state, the left image goes through OnNewFrame.
 void oracle_viso_on_new_stereo(oracle_viso* v, const uint8_t* left, const uint8_t* right);
+// Stereo keyframe insertion (viso_set_keyframes; the repo's own map
+// maintenance, no reference counterpart): with stereo enabled, after every
+// `interval`-th tracking frame whose level-0 nGood is below
+// ngood_permille / 1000 of the map size, the frame's stereo points (world =
+// R^T (Pc - T)) are appended to the map and the frame becomes a keyframe (at
+// most 8 keyframes, 16384 points).  interval 0 = off (default).
+void oracle_viso_set_keyframes(oracle_viso* v, int interval, int ngood_permille);
 int oracle_viso_state(const oracle_viso* v);
 int oracle_viso_num_poses(const oracle_viso* v);
 void oracle_viso_poses(const oracle_viso* v, double* out12);

@@ -49,6 +49,7 @@ SIG = {
     "oracle_viso_on_new_frame": ([_vp, _vp], None),
     "oracle_viso_on_new_stereo": ([_vp, _vp, _vp], None),
     "oracle_viso_set_stereo": ([_vp, _d, _i, _i], None),
+    "oracle_viso_set_keyframes": ([_vp, _i, _i], None),
     "oracle_stereo_points": ([_vp, _vp, _i, _i, _vp, _vp, _i, _i, _i, _vp, _d, _vp], _i),
     "oracle_viso_state": ([_vp], _i),
     "oracle_viso_num_poses": ([_vp], _i),
@@ -296,6 +297,9 @@ class Viso:
 
     def set_stereo(self, baseline, max_disp=128, min_disp=1):
         self.lib.oracle_viso_set_stereo(self.v, float(baseline), int(max_disp), int(min_disp))
+
+    def set_keyframes(self, interval, ngood_permille=500):
+        self.lib.oracle_viso_set_keyframes(self.v, int(interval), int(ngood_permille))
 
     def on_new_stereo(self, left, right):
         left = np.ascontiguousarray(left, np.uint8)

@@ -359,6 +359,13 @@ extern "C" int viso_set_stereo(viso_ctx* c, double baseline, int32_t max_disp, i
     return VISO_OK;
 }
 
+extern "C" int viso_set_keyframes(viso_ctx* c, int32_t interval, int32_t ngood_permille) {
+    if (!c || interval < 0 || ngood_permille < 0 || ngood_permille > 1000) return VISO_ERR_ARG;
+    c->kf_interval = interval;
+    c->kf_permille = ngood_permille;
+    return VISO_OK;
+}
+
 extern "C" int viso_stereo_match(viso_ctx* c, const uint8_t* left, const uint8_t* right,
                                  int32_t width, int32_t height, const int32_t* xs,
                                  const int32_t* ys, int32_t n, int32_t max_disp,

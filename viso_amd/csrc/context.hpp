@@ -189,6 +189,14 @@ struct viso_ctx {
     // (null: none); only the stereo initialisation reads it
     const uint8_t* right_l0 = nullptr;
     viso::DevBuf st_flag, st_pts;
+    // stereo keyframe insertion (viso_set_keyframes; the repo's own map
+    // maintenance): checked every kf_interval-th
+    // tracking frame (0 = off), inserting when level-0 nGood is below
+    // kf_permille / 1000 of the map
+    int kf_interval = 0, kf_permille = 0;
+    int64_t track_cnt = 0;
+    int stereo_points_into(int cur, double* out, int cap, int* kept);
+    int insert_keyframe(int cur);
 
     // ---------------- state (include/viso.h:44)
     int state = VISO_STATE_INITIALIZATION;

@@ -349,13 +349,11 @@ int viso_ctx::build_lk_templates() {
     return VISO_OK;
 }
 
-// Stereo initialisation (the repo's own spec, oracle/oracle_stereo.cpp
-// oracle_stereo_points + oracle_viso.cpp stereo_init): FAST on the left
-// image, sub-pixel SAD disparity on the right one, metric camera points; with
-// more than 50 of them the map is created at once: the frame is the only
-// keyframe (R = I, T = 0), points in its camera frame, metric scale.
-int viso_ctx::stereo_init(int cur, bool* made) {
-    *made = false;
+// FAST on the left image of `cur`, stereo points on it and right_l0, kept
+// points compacted into out (<= cap, camera frame); *kept = their count
+// (oracle_stereo.cpp oracle_stereo_points).  stats[1] = FAST corners.  Two
+// host syncs (the corner count, the point count).
+int viso_ctx::stereo_points_into(int cur, double* out, int cap, int* kept) {
     const PyrGeom& g = geom;
     // FAST into scratch (kp1b, count slot 2): the monocular init state (kp1 =
     // the reference frame's keypoints, n_track_dev[0]) must survive a stereo
@@ -379,14 +377,54 @@ int viso_ctx::stereo_init(int cur, bool* made) {
     int* d_count = (int*)n_track_dev.ptr + 1;
     {
         TimedRegion t(timing, VISO_KERNEL_STEREO, stream);
-        launch_stereo_points(frame(cur).l[0], right_l0, g.w[0], g.h[0], corners,
-                             n, stereo_max_disp, stereo_min_disp, cam, (int*)st_flag.ptr, (double*)st_pts.ptr,
-                             (double*)map_pts.ptr, kMaxMapPoints, d_count, stream);
+        launch_stereo_points(frame(cur).l[0], right_l0, g.w[0], g.h[0], corners, n, stereo_max_disp,
+                             stereo_min_disp, cam, (int*)st_flag.ptr, (double*)st_pts.ptr, out, cap, d_count,
+                             stream);
     }
     VISO_HIP_CHECK(hipGetLastError());
     VISO_HIP_CHECK(hipMemcpyAsync(h_int + 2, d_count, sizeof(int), hipMemcpyDeviceToHost, stream));
     VISO_HIP_CHECK(hipStreamSynchronize(stream));
-    const int m = h_int[2];
+    *kept = std::min(h_int[2], cap);
+    return VISO_OK;
+}
+
+// Stereo keyframe insertion (oracle_viso.cpp, the kRunning case): the frame's
+// pose is final (resolve_direct) and every earlier tracking frame's LK
+// alignment has been launched against the old map (flush_lk); then its
+// stereo points are appended in world coordinates, it becomes a keyframe
+// and the map's LK templates are rebuilt.
+int viso_ctx::insert_keyframe(int cur) {
+    const int cap = kMaxMapPoints - n_map;
+    int m = 0;
+    const double saved1 = stats[1];
+    int rc = stereo_points_into(cur, (double*)map_pts.ptr + 3 * (size_t)n_map, cap, &m);
+    stats[1] = saved1;
+    if (rc) return rc;
+    launch_points_to_world((double*)map_pts.ptr + 3 * (size_t)n_map, m, pose_of(cur), stream);
+    VISO_HIP_CHECK(hipGetLastError());
+    n_map += m;
+    rc = own_level0(cur);
+    if (rc) return rc;
+    kf_slots.push_back(cur);
+    hold(cur);
+    VISO_HIP_CHECK(hipMemcpyAsync((char*)kf_poses.ptr + 96 * (kf_slots.size() - 1), pose_of(cur), 96,
+                                  hipMemcpyDeviceToDevice, stream));
+    rc = build_lk_templates();
+    if (rc) return rc;
+    stats[14] = m;
+    return VISO_OK;
+}
+
+// Stereo initialisation (the repo's own spec, oracle/oracle_stereo.cpp
+// oracle_stereo_points + oracle_viso.cpp stereo_init): FAST on the left
+// image, sub-pixel SAD disparity on the right one, metric camera points; with
+// more than 50 of them the map is created at once: the frame is the only
+// keyframe (R = I, T = 0), points in its camera frame, metric scale.
+int viso_ctx::stereo_init(int cur, bool* made) {
+    *made = false;
+    int m = 0;
+    int rc = stereo_points_into(cur, (double*)map_pts.ptr, kMaxMapPoints, &m);
+    if (rc) return rc;
     stats[2] = m;
     if (m <= 50) return VISO_OK;
     for (int s : kf_slots) drop(s);
@@ -564,6 +602,23 @@ int viso_ctx::on_new_frame(int cur) {
                 if (rc) return rc;
             }
             ran_tracking = true;
+            // stereo keyframe insertion (oracle_viso.cpp): every
+            // kf_interval-th tracking frame, one host sync for its nGood
+            ++track_cnt;
+            stats[15] = (double)kf_slots.size();  // before a possible insertion, as the oracle
+            if (kf_interval > 0 && right_l0 && stereo_base > 0 && track_cnt % kf_interval == 0 &&
+                (int)kf_slots.size() < kMaxKeyframes) {
+                int rc = finish_call(stream);
+                if (rc) return rc;
+                VISO_HIP_CHECK(hipMemcpyAsync(h_dbl, direct_stats.ptr, sizeof(double), hipMemcpyDeviceToHost,
+                                              stream));
+                VISO_HIP_CHECK(hipStreamSynchronize(stream));
+                if (h_dbl[0] < kf_permille * (double)n_map / 1000.0) {
+                    rc = insert_keyframe(cur);
+                    if (rc) return rc;
+                    stats[15] = (double)kf_slots.size();
+                }
+            }
             break;
         }
         default:

@@ -89,6 +89,8 @@ struct StereoCam {
 void launch_stereo_points(const uint8_t* left, const uint8_t* right, int w, int h, const float2* kp,
                           int n, int max_disp, int min_disp, const StereoCam& cam, int* flag,
                           double* pts, double* out, int cap, int* count, hipStream_t stream);
+// pts (n x 3, device) <- R^T (pts - T) with the Tcw pose (12 doubles, device)
+void launch_points_to_world(double* pts, int n, const double* pose12, hipStream_t stream);
 void launch_stereo_sad(const uint8_t* left, const uint8_t* right, int w, int h, const int* xs,
                        const int* ys, int n, int max_disp, int* disp, int* sad,
                        hipStream_t stream);

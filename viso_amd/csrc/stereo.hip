@@ -183,7 +183,23 @@ __global__ __launch_bounds__(1024) void stereo_compact_kernel(const int* __restr
     if (tid == 0) *count = base;
 }
 
+// Stereo keyframe insertion: camera-frame points -> world, Pw = R^T (Pc - T)
+// with the keyframe's Tcw pose (oracle_viso.cpp restates the same order).
+__global__ __launch_bounds__(256) void points_to_world_kernel(double* __restrict__ pts, int n,
+                                                              const double* __restrict__ pose) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const double d0 = pts[3 * (size_t)i] - pose[9], d1 = pts[3 * (size_t)i + 1] - pose[10],
+                 d2 = pts[3 * (size_t)i + 2] - pose[11];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) pts[3 * (size_t)i + k] = (pose[k] * d0 + pose[3 + k] * d1) + pose[6 + k] * d2;
+}
+
 }  // namespace
+
+void launch_points_to_world(double* pts, int n, const double* pose12, hipStream_t stream) {
+    if (n > 0) points_to_world_kernel<<<(n + 255) / 256, 256, 0, stream>>>(pts, n, pose12);
+}
 
 void launch_stereo_points(const uint8_t* left, const uint8_t* right, int w, int h, const float2* kp,
                           int n, int max_disp, int min_disp, const StereoCam& cam, int* flag,

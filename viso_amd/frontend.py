@@ -100,6 +100,12 @@ class Viso(FrameHandler):
         frame given with its right image creates a metric map at once."""
         _lib.call("viso_set_stereo", self.ctx.h, float(baseline), int(max_disp), int(min_disp))
 
+    def set_keyframes(self, interval: int, ngood_permille: int = 500) -> None:
+        """Stereo keyframe insertion (viso_set_keyframes): every `interval`-th
+        tracking frame whose level-0 nGood is below ngood_permille / 1000 of
+        the map adds its stereo points and becomes a keyframe."""
+        _lib.call("viso_set_keyframes", self.ctx.h, int(interval), int(ngood_permille))
+
     def process_device(self, d_left: int, d_right: int | None, n: int, frame_stride: int):
         """Batched ingest of n frames resident in HBM (device pointers)."""
         _lib.call("viso_process_frames_device", self.ctx.h, d_left, d_right, n, frame_stride)
