@@ -166,6 +166,7 @@ struct viso_ctx {
     // use lk_stream so the host's next frame overlaps them.
     std::vector<int> lk_pending;
     int lk_last_rows = 0;  // frames in the last launched batch
+    int lk_last_pts = 0;   // map points of the last launched batch
     viso::DevBuf lk_pair, lk_succ, lk_before, lk_after;  // kLkBatch x kMaxMapPoints
     // per-map LK templates (keyframe choice + per-level template / H^-1),
     // computed once when the map is created (launch_lk_template)

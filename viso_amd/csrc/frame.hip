@@ -307,6 +307,7 @@ int viso_ctx::flush_lk(hipStream_t ls) {
     }
     VISO_HIP_CHECK(hipGetLastError());
     lk_last_rows = a.n_frames;
+    lk_last_pts = n_map;  // a later keyframe insertion grows n_map, not these rows
     if (side) {
         VISO_HIP_CHECK(hipEventRecord(lk_ring[lk_seq % kLkRing], ls));
         for (int s : lk_pending) slots[(size_t)s].lk_use = lk_seq;
@@ -808,7 +809,7 @@ int viso_get_alignment(viso_ctx* c, int32_t* pair_kf, uint8_t* success, double* 
     if (!c) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(c->device));
     VISO_HIP_CHECK(hipStreamSynchronize(c->lk_stream));
-    const size_t m = c->ran_tracking ? std::min(cap, (size_t)c->n_map) : 0;
+    const size_t m = c->ran_tracking ? std::min(cap, (size_t)c->lk_last_pts) : 0;
     const size_t o = (size_t)std::max(c->lk_last_rows - 1, 0) * kMaxMapPoints;
     if (m > 0) {
         if (pair_kf) VISO_HIP_CHECK(hipMemcpyAsync(pair_kf, (int32_t*)c->lk_pair.ptr + o, 4 * m, hipMemcpyDeviceToHost, c->stream));
@@ -817,7 +818,7 @@ int viso_get_alignment(viso_ctx* c, int32_t* pair_kf, uint8_t* success, double* 
         if (uv_after) VISO_HIP_CHECK(hipMemcpyAsync(uv_after, (double*)c->lk_after.ptr + 2 * o, 16 * m, hipMemcpyDeviceToHost, c->stream));
     }
     VISO_HIP_CHECK(hipStreamSynchronize(c->stream));
-    if (n) *n = c->ran_tracking ? (size_t)c->n_map : 0;
+    if (n) *n = c->ran_tracking ? (size_t)c->lk_last_pts : 0;
     return VISO_OK;
 }
 
@@ -828,7 +829,7 @@ int viso_get_frame_stats(viso_ctx* c, double out[16]) {
     if (c->state == VISO_STATE_RUNNING && c->stats[12] == 0 && c->ran_tracking) {
         // last frame was a tracking frame: level-0 direct stats + LK counts
         VISO_HIP_CHECK(hipStreamSynchronize(c->lk_stream));
-        const int m = c->n_map;
+        const int m = c->lk_last_pts;
         const size_t o = (size_t)std::max(c->lk_last_rows - 1, 0) * kMaxMapPoints;
         std::vector<int32_t> pk((size_t)m);
         std::vector<uint8_t> sc((size_t)m);
