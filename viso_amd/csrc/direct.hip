@@ -278,6 +278,44 @@ __device__ inline double sample_cw(const uint8_t* __restrict__ img, int w, int h
 
 // The 28 sums of one map point by reduce-scatter: returns good; lane l < 32
 // with *idx >= 0 holds sum *idx in *out.
+// The twelve quotients of one map point's projection (project_px) and
+// dPixel/dXi (d_pixel_d_xi), each with those functions' exact operations,
+// one per lane (lane k < 12) so that a single division sequence serves all
+// of them; every lane gets the results by readlane (wave-uniform values).
+//   0: x / z, 1: y / z (the projection)        -> Q[0], Q[1]
+//   2..11: J[0], J[2], J[3], J[4], J[5], J[7], J[8], J[9], J[10], J[11]
+__device__ inline void point_quotients(const Intrinsics& K, const double* pose, const double* P, double scale,
+                                       double* Q) {
+    const int lane = threadIdx.x & 63;
+    double Pc[3];
+    mat3_vec(pose, P, Pc);
+    const double x = Pc[0] + pose[9], y = Pc[1] + pose[10], z = Pc[2] + pose[11];
+    const double fx = K.fx * scale, fy = K.fy * scale;
+    const double zz = z * z, xy = x * y;
+    // numerator = c1 * c2 (c2 = 1.0 where the numerator is a single value:
+    // exact), denominator z or zz
+    double c1, c2 = 1.0, den = zz;
+    switch (lane < 12 ? lane : 0) {
+        case 0: c1 = x; den = z; break;
+        case 1: c1 = y; den = z; break;
+        case 2: c1 = fx; den = z; break;                 // J[0] = fx / z
+        case 3: c1 = -fx; c2 = x; break;                 // J[2] = -fx * x / zz
+        case 4: c1 = -fx; c2 = xy; break;                // J[3] = -fx * xy / zz
+        case 5: c1 = fx * x; c2 = x; break;              // J[4] = fx + fx * x * x / zz
+        case 6: c1 = -fx; c2 = y; den = z; break;        // J[5] = -fx * y / z
+        case 7: c1 = fy; den = z; break;                 // J[7] = fy / z
+        case 8: c1 = -fy; c2 = y; break;                 // J[8] = -fy * y / zz
+        case 9: c1 = fy * y; c2 = y; break;              // J[9] = -fy - fy * y * y / zz
+        case 10: c1 = fy; c2 = xy; break;                // J[10] = fy * xy / zz
+        default: c1 = fy; c2 = x; den = z; break;        // J[11] = fy * x / z
+    }
+    double q = (c1 * c2) / den;
+    if (lane == 5) q = fx + q;
+    if (lane == 9) q = -fy - q;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) Q[k] = readlane_f64(q, k);
+}
+
 __device__ inline bool direct_point_rs(const DirectArgs& a, const LevelPair& fp, int lv,
                                        const double* cur_pose,
                                        const RefSample& r, const uint8_t* win, const CurWin& cw,
@@ -286,13 +324,15 @@ __device__ inline bool direct_point_rs(const DirectArgs& a, const LevelPair& fp,
     const int px = (lane >> 3) - 4, py = (lane & 7) - 4;
     const double scale = kScale[lv];
     const int w = a.g.w[lv], h = a.g.h[lv];
-    double uc, vc;
-    project_px(cur_pose, a.K, r.P, scale, uc, vc);
+    // project_px and d_pixel_d_xi (bit-identical; divisions lane-parallel)
+    double Q[12];
+    point_quotients(a.K, cur_pose, r.P, scale, Q);
+    const double uc = scale * (Q[0] * a.K.fx + a.K.cx);
+    const double vc = scale * (Q[1] * a.K.fy + a.K.cy);
     const double hp = 4.0;
     const bool good = r.ok && inside_px(uc - hp, vc - hp, w, h) && inside_px(uc + hp, vc + hp, w, h);
     if (!good) return false;
-    double Jp[12];
-    d_pixel_d_xi(a.K, cur_pose, r.P, scale, Jp);
+    const double Jp[12] = {Q[2], 0.0, Q[3], Q[4], Q[5], Q[6], 0.0, Q[7], Q[8], Q[9], Q[10], Q[11]};
     const uint8_t* C = fp.cur;
     const double x = uc + px, y = vc + py;
     const double error = r.lval - sample_cw(C, w, h, x, y, win, cw);
