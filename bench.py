@@ -74,7 +74,7 @@ def parse():
     ap.add_argument("--no-other", action="store_true",
                     help="skip the run at the other precision (other_precision in the line)")
     ap.add_argument("--rig-steps", type=int, default=64,
-                    help="timesteps of the 4-camera rig measurement (configs[4]; 0 = skip)")
+                    help="timesteps of the 4-camera rig measurements (configs[4]: SVO rig and the reference-path photometric rig; 0 = skip)")
     return ap.parse_args()
 
 
@@ -213,6 +213,66 @@ def measure_rig(args, W, H, log):
         gp = vo.poses[:m]
         out["parity_vs_oracle"] = {"timesteps": int(m),
                                    "pose_max_abs_diff": float(np.abs(gp - np.array(S.poses[:m])).max())}
+    return out
+
+
+def measure_rig_direct(args, W, H, log):
+    """BASELINE.json configs[4] on the reference path:
+    4 stereo cameras per timestep, one photometric direct pose of the rig
+    (per-camera DirectPoseEstimationSingleLayer sums through the rig
+    extrinsics; include/viso/viso_rig.h).  Timesteps/s over the tracking
+    timesteps with the frames resident in HBM (the initialising timestep runs
+    before the clock), both precisions; the CPU spec (oracle/oracle_rig.cpp)
+    on a bounded sample."""
+    import torch
+
+    import viso_amd
+    from viso_amd.rig import VisoRig
+    from viso_amd.synth import RigSequence
+
+    nc, n = 4, max(args.rig_steps, 3)
+    seq = RigSequence(W, H, seed=2000, n_cams=nc)
+    frames = [seq.frame(f) for f in range(n)]
+    dl = torch.from_numpy(np.stack([im for ls, _ in frames for im in ls])).cuda()
+    dr = torch.from_numpy(np.stack([im for _, rs in frames for im in rs])).cuda()
+    E = seq.extrinsics()
+    fb = W * H
+    out = {"workload": f"configs[4] on the reference path: {nc} synthetic {W}x{H} stereo cameras per timestep, "
+                       "stereo-initialised metric map per camera, one photometric direct pose of the rig",
+           "timesteps": n - 1}
+    poses = {}
+    for name, prec in (("faithful", viso_amd.PRECISION_FAITHFUL), ("fast", viso_amd.PRECISION_FAST)):
+        g = VisoRig(*seq.K, W, H, E, precision=prec, max_poses=n + 8)
+        g.set_stereo(seq.p.baseline, STEREO_MAX_DISP, 1)
+        g.process_device(dl.data_ptr(), dr.data_ptr(), 1, fb)  # initialisation
+        g.synchronize()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        g.process_device(dl.data_ptr() + nc * fb, None, n - 1, fb)
+        g.synchronize()
+        dt = time.perf_counter() - t0
+        poses[name] = g.poses
+        out[name] = {"timesteps_per_s": round((n - 1) / dt, 1), "camera_frames_per_s": round(nc * (n - 1) / dt, 1),
+                     "map_points": [len(g.points(c)) for c in range(nc)],
+                     "dtype": "f64" if name == "faithful" else "f32 per-pixel (fp16 `last` patch in LDS), "
+                                                              "f64 sums, LDL^T solve"}
+        log(f"[rig direct {name}] {out[name]['timesteps_per_s']} timesteps/s")
+    if not args.no_cpu:
+        from tests import oracle_lib
+        m = min(3, n - 1)
+        r = oracle_lib.Rig(seq.K, W, H, E, seq.p.baseline, STEREO_MAX_DISP, 1)
+        r.process(*frames[0])
+        t0 = time.perf_counter()
+        for f in range(1, m + 1):
+            r.process(frames[f][0])
+        cpu_s = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(m / cpu_s, 3), "unit": "timesteps/s", "cores": 1, "kind": "port",
+                               "sample": f"oracle/oracle_rig.cpp spec, single thread, tracking timesteps 1-{m}"}
+        oP = r.poses[:m]
+        for name in poses:
+            gP = poses[name][:m]
+            rel = np.linalg.norm(gP - oP, axis=1) / np.maximum(np.linalg.norm(oP, axis=1), 1e-300)
+            out[name]["parity_vs_oracle"] = {"timesteps": int(m), "max_rel_frobenius": float(rel.max())}
     return out
 
 
@@ -393,6 +453,9 @@ def main():
         stereo_vo = measure_svo(args, seq, left, right, d_left, d_right, W, H, log, warm + steps)
         if args.rig_steps > 0:
             stereo_vo["rig"] = measure_rig(args, W, H, log)
+    rig_direct = None
+    if rank == 0 and args.rig_steps > 0 and (W, H) == (1242, 375):
+        rig_direct = measure_rig_direct(args, W, H, log)
 
     # ---------------------------------------------------------- CPU baseline + parity
     cpu = None
@@ -467,6 +530,7 @@ def main():
             "matching_pass_hbm": mp_ev,
             "other_precision": other,
             "stereo_vo": stereo_vo,
+            "rig_direct": rig_direct,
             "last_frame_stats": {"direct_nGood": st[9], "lk_pairs": st[6], "lk_success": st[7]},
         }
         print(json.dumps(out), flush=True)

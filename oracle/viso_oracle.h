@@ -202,6 +202,30 @@ int oracle_viso_keyframe_poses(const oracle_viso* v, double* out12, int cap);
 int oracle_viso_alignment(const oracle_viso* v, int32_t* pair_kf, uint8_t* success,
                           double* uv_before, double* uv_after, int cap);
 
+// ---------------------------------------------------------------- multi-camera rig
+// The repo's own spec for SURVEY.md §8(f) row 3 (oracle_rig.cpp header):
+// rig pose T (world -> rig), camera c at E_c T (extrinsics: n x 12 rig ->
+// camera, R row-major + t), per level one Gauss-Newton step whose H, b are
+// the cameras' DirectPoseEstimationSingleLayer sums through Ad(E_c).
+void oracle_rig_compose(const double E[12], const double T[12], double out[12]);
+void oracle_rig_adjoint(const double E[12], double Ad[36]);
+void oracle_rig_direct(int n_cams, const uint8_t* const* last_pyrs, const uint8_t* const* cur_pyrs, int w,
+                       int h, const double K[4], const double* const* points, const int* n_points,
+                       const double* extrinsics, const double* cam_last, double pose_io[12], double* stats);
+typedef struct oracle_rig oracle_rig;
+oracle_rig* oracle_rig_create(int n_cams, int w, int h, const double K[4], int fast_thresh, const double* extrinsics,
+                              double baseline, int max_disp, int min_disp);
+void oracle_rig_destroy(oracle_rig* r);
+// one timestep (rights: n images, or null while tracking)
+void oracle_rig_process(oracle_rig* r, const uint8_t* const* lefts, const uint8_t* const* rights);
+int oracle_rig_state(const oracle_rig* r);
+int oracle_rig_num_poses(const oracle_rig* r);
+void oracle_rig_poses(const oracle_rig* r, double* out12);
+int oracle_rig_num_points(const oracle_rig* r, int cam);
+void oracle_rig_points(const oracle_rig* r, int cam, double* out3);
+// [4 levels][50]: nGood, cost / nGood, H (36), b (6), update (6) of the last step
+void oracle_rig_level_stats(const oracle_rig* r, double* out200);
+
 #ifdef __cplusplus
 }
 #endif

@@ -45,6 +45,18 @@ SIG = {
     "oracle_recover_pose": ([_vp, _vp, _vp, _i, _vp, _vp, _vp], _i),
     "oracle_default_params": ([_vp, _d, _d, _d, _d, _i, _i], None),
     "oracle_viso_create": ([_vp], _vp),
+    "oracle_rig_compose": ([_vp, _vp, _vp], None),
+    "oracle_rig_adjoint": ([_vp, _vp], None),
+    "oracle_rig_direct": ([_i, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp], None),
+    "oracle_rig_create": ([_i, _i, _i, _vp, _i, _vp, ctypes.c_double, _i, _i], _vp),
+    "oracle_rig_destroy": ([_vp], None),
+    "oracle_rig_process": ([_vp, _vp, _vp], None),
+    "oracle_rig_state": ([_vp], _i),
+    "oracle_rig_num_poses": ([_vp], _i),
+    "oracle_rig_poses": ([_vp, _vp], None),
+    "oracle_rig_num_points": ([_vp, _i], _i),
+    "oracle_rig_points": ([_vp, _i, _vp], None),
+    "oracle_rig_level_stats": ([_vp, _vp], None),
     "oracle_viso_destroy": ([_vp], None),
     "oracle_viso_on_new_frame": ([_vp, _vp], None),
     "oracle_viso_on_new_stereo": ([_vp, _vp, _vp], None),
@@ -573,3 +585,83 @@ class SvoRigSequence:
         self.prev = feats
         self.frame += 1
         return ok
+
+
+# ----------------------------------------------------------------- multi-camera rig
+class Rig:
+    """oracle/oracle_rig.cpp: the multi-camera photometric rig spec."""
+
+    def __init__(self, K, w, h, extrinsics, baseline, max_disp=128, min_disp=1, fast_thresh=50):
+        self.E = np.ascontiguousarray(extrinsics, np.float64).reshape(-1, 12)
+        self.n = len(self.E)
+        k = np.asarray(K, np.float64)
+        self.h = load().oracle_rig_create(self.n, w, h, ptr(k), fast_thresh, ptr(self.E), float(baseline),
+                                          max_disp, min_disp)
+
+    def __del__(self):
+        try:
+            load().oracle_rig_destroy(self.h)
+        except Exception:
+            pass
+
+    def process(self, lefts, rights=None):
+        ls = [np.ascontiguousarray(x, np.uint8) for x in lefts]
+        P = ctypes.c_void_p * self.n
+        if rights is None:
+            load().oracle_rig_process(self.h, P(*[ptr(x) for x in ls]), None)
+        else:
+            rs = [np.ascontiguousarray(x, np.uint8) for x in rights]
+            load().oracle_rig_process(self.h, P(*[ptr(x) for x in ls]), P(*[ptr(x) for x in rs]))
+
+    @property
+    def state(self):
+        return load().oracle_rig_state(self.h)
+
+    @property
+    def poses(self):
+        n = load().oracle_rig_num_poses(self.h)
+        out = np.zeros((max(n, 1), 12))
+        load().oracle_rig_poses(self.h, ptr(out))
+        return out[:n]
+
+    def points(self, cam):
+        n = load().oracle_rig_num_points(self.h, cam)
+        out = np.zeros((max(n, 1), 3))
+        load().oracle_rig_points(self.h, cam, ptr(out))
+        return out[:n]
+
+    def level_stats(self):
+        out = np.zeros((4, 50))
+        load().oracle_rig_level_stats(self.h, ptr(out))
+        return out
+
+
+def rig_compose(E, T):
+    out = np.zeros(12)
+    load().oracle_rig_compose(ptr(np.ascontiguousarray(E, np.float64)), ptr(np.ascontiguousarray(T, np.float64)),
+                              ptr(out))
+    return out
+
+
+def rig_adjoint(E):
+    out = np.zeros(36)
+    load().oracle_rig_adjoint(ptr(np.ascontiguousarray(E, np.float64)), ptr(out))
+    return out.reshape(6, 6)
+
+
+def rig_direct(last_pyrs, cur_pyrs, w, h, K, points, E, cam_last, pose_seed):
+    """One rig direct pose (levels 3..0): returns (pose12, stats[4][50])."""
+    n = len(last_pyrs)
+    P = ctypes.c_void_p * n
+    lp = [np.ascontiguousarray(x, np.uint8) for x in last_pyrs]
+    cp = [np.ascontiguousarray(x, np.uint8) for x in cur_pyrs]
+    pts = [np.ascontiguousarray(x, np.float64).reshape(-1, 3) for x in points]
+    npts = np.array([len(x) for x in pts], np.int32)
+    k = np.asarray(K, np.float64)
+    E = np.ascontiguousarray(E, np.float64).reshape(-1, 12)
+    cl = np.ascontiguousarray(cam_last, np.float64).reshape(-1, 12)
+    pose = np.ascontiguousarray(pose_seed, np.float64).copy()
+    stats = np.zeros((4, 50))
+    load().oracle_rig_direct(n, P(*[ptr(x) for x in lp]), P(*[ptr(x) for x in cp]), w, h, ptr(k),
+                             P(*[ptr(x) for x in pts]), ptr(npts), ptr(E), ptr(cl), ptr(pose), ptr(stats))
+    return pose, stats

@@ -98,6 +98,17 @@ SIGNATURES = {
     "viso_svo_rig_process": [_vp, _vp, _vp, _vp, _vp],
     "viso_svo_rig_process_device": [_vp, _vp, _vp, _i32, ctypes.c_int64, _i32],
     "viso_svo_get_match_cams": [_vp, _vp, _sz, _vp],
+    # multi-camera photometric rig (include/viso/viso_rig.h)
+    "viso_rig_create": [_vp, _i32, _vp, ctypes.c_int, _vp],
+    "viso_rig_destroy": [_vp],
+    "viso_rig_set_stereo": [_vp, _d, _i32, _i32],
+    "viso_rig_process": [_vp, _vp, _vp, _vp],
+    "viso_rig_process_device": [_vp, _vp, _vp, _i32, _sz],
+    "viso_rig_synchronize": [_vp],
+    "viso_rig_get_state": [_vp, _vp],
+    "viso_rig_get_poses": [_vp, _vp, _sz, _vp],
+    "viso_rig_get_points": [_vp, _i32, _vp, _sz, _vp],
+    "viso_rig_get_level_stats": [_vp, _vp],
     # frame source (include/viso/viso_io.h)
     "viso_png_info": [ctypes.c_char_p, _vp, _vp],
     "viso_png_read_grey": [ctypes.c_char_p, _vp, _sz, _vp, _vp],

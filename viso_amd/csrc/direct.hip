@@ -33,6 +33,8 @@
 // reset, src/viso.cpp:673); the rare continuation (a level
 // whose photometric cost is exactly 0) is executed faithfully by each
 // workgroup on its own, re-evaluating every tile into private scratch.
+#include <algorithm>
+
 #include "device_math.hpp"
 #include "direct_solve.hpp"
 #include "kernels.hpp"
@@ -522,6 +524,9 @@ __device__ void direct_tile(const DirectArgs& a, const LevelPair& fp, int lv, co
 // read nothing but LDS (and the rare sample outside its window).
 struct PfLds {
     uint32_t taps[kMaxTile][64];
+    // tolerance-mode rig: the `last` patch sample of every lane as fp16
+    // (computed in the prefetch, off the tile phase's critical path)
+    _Float16 lv16[kMaxTile][64];
     uint8_t win[kMaxTile][kCWBytes];
     double P[kMaxTile][3];
     double ur[kMaxTile], vr[kMaxTile];
@@ -548,11 +553,15 @@ __device__ inline void pf_issue(const DirectArgs& a, const LevelPair& fp, int lv
     win_issue(fp.cur, a.g.w[lv], a.g.h[lv], up, vp, q.c);
 }
 
+__device__ inline float fast_lval(uint32_t t, double ur, double vr);
+
+template <bool LV16>
 __device__ inline void pf_store(int j, bool ref, const PfPoint& q, PfLds& pf) {
     const int lane = threadIdx.x & 63;
     if (ref)
         pf.taps[j][lane] = (uint32_t)q.r.t0 | ((uint32_t)q.r.t1 << 8) | ((uint32_t)q.r.t2 << 16) |
                            ((uint32_t)q.r.t3 << 24);
+    if (LV16) pf.lv16[j][lane] = (_Float16)(q.r.ok ? fast_lval(pf.taps[j][lane], q.r.ur, q.r.vr) : 0.0f);
     if (q.c.on) win_store(pf.win[j], q.c);
     if (lane == 0) {
         pf.P[j][0] = q.r.P[0];
@@ -571,6 +580,7 @@ __device__ inline void pf_store(int j, bool ref, const PfPoint& q, PfLds& pf) {
 // of both in flight together).  `pose_last` is the pose of the `last`
 // projection: the `last` frame's own, or in a merged L(3) (whose `last` pose
 // is solved in this launch) a prediction, checked per lane in the tile phase.
+template <bool LV16 = false>
 __device__ void prefetch_tile(const DirectArgs& a, int lv, int b, const double* pred, const double* pose_last,
                               bool ref, int first, int stride, PfLds& pf) {
     LevelPair fp = level_pair(a.fp, lv);
@@ -584,8 +594,8 @@ __device__ void prefetch_tile(const DirectArgs& a, int lv, int b, const double* 
         PfPoint q0{}, q1{};
         if (v0) pf_issue(a, fp, lv, i0, pred, ref, q0);
         if (v1) pf_issue(a, fp, lv, i1, pred, ref, q1);
-        if (v0) pf_store(j, ref, q0, pf);
-        if (v1) pf_store(j2, ref, q1, pf);
+        if (v0) pf_store<LV16>(j, ref, q0, pf);
+        if (v1) pf_store<LV16>(j2, ref, q1, pf);
     }
 }
 
@@ -653,7 +663,7 @@ __device__ inline void merged_ref(const DirectArgs& a, const LevelPair& fp, int 
 // Tile b of level lv from the prologue's prefetch (the tile phase of
 // direct_level_kernel; direct_tile's arithmetic and tree; FAST: the
 // tolerance-mode point sums).
-template <bool FAST>
+template <bool FAST, bool LV16 = false>
 __device__ void direct_tile_pf(const DirectArgs& a, const LevelPair& fp, int lv, const double* cur_pose, int b,
                                const PfLds& pf, bool merged, double* part, int* good, double* s_pts,
                                int* s_good) {
@@ -695,8 +705,8 @@ __device__ void direct_tile_pf(const DirectArgs& a, const LevelPair& fp, int lv,
                 if (r.ok) {
                     const uint32_t t = (uint32_t)r.t0 | ((uint32_t)r.t1 << 8) | ((uint32_t)r.t2 << 16) |
                                        ((uint32_t)r.t3 << 24);
-                    ok = direct_point_fast(a, fp, lv, cur_pose, r.P, fast_lval(t, r.ur, r.vr), pf.win[local],
-                                           cw, &ff, &idx);
+                    const float lval = (LV16 && !merged) ? (float)pf.lv16[local][lane] : fast_lval(t, r.ur, r.vr);
+                    ok = direct_point_fast(a, fp, lv, cur_pose, r.P, lval, pf.win[local], cw, &ff, &idx);
                 }
                 f = (double)ff;
             } else {
@@ -1030,6 +1040,256 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
 #endif
 }
 
+// ================================================================ rig
+// Multi-camera photometric rig (the repo's own spec,
+// oracle/oracle_rig.cpp): one Gauss-Newton step of the rig pose T (world ->
+// rig) per level.  Camera c sees the world at T_c = E_c T (E_c: rig ->
+// camera); its 28 sums are DirectPoseEstimationSingleLayer's
+// (src/viso.cpp:682-729) at T_c, reduced by the canonical tree over its own
+// points; a rig perturbation xi moves camera c by Ad(E_c) xi, so
+//   H = sum_c Ad_c^T H_c Ad_c,  b = sum_c Ad_c^T b_c,  cost = sum_c cost_c
+// (cameras ascending), then the direct pose's solve and T <- exp(update) T
+// (unchanged when the update is NaN).  Launches per frame: L(3..0) + F, the
+// tiles of all cameras in one grid (workgroup = one tile of one camera), the
+// prologue of L(l) solving level l+1 from every camera's tile partials.
+constexpr int kRigTiles = 64;  // tiles per camera (one wave reduces them)
+
+struct RigCamArgs {
+    DirectArgs d;       // the camera's pyramids (fp: last, cur; fp.pose_last =
+                        // its `last` pose E_c T_last), points, tiling, and
+                        // tile partials s.part / s.good ([kLevels][kRigTiles])
+    const double* Ad;   // 36, row-major Ad(E_c)
+    double E[12];       // rig -> camera (R row-major, t)
+};
+
+struct RigArgs {
+    RigCamArgs cam[kMaxRigCams];
+    int n_cams;
+    int tile_off[kMaxRigCams + 1];  // camera c owns workgroups [tile_off[c], tile_off[c + 1])
+    int level;                      // tiles of this level; -1: F
+    double* state;                  // [kLevels + 1][kStateStride]: T each level was evaluated at
+    const double* seed;             // L(3): the last rig pose (12)
+    double* stats;                  // [kLevels][kStats] or null
+    double* pose_out;               // F: rig pose (12)
+    double* log;
+    int log_index;
+    double* cam_last;               // F: n_cams x 12, E_c T (next frame's `last` poses)
+};
+
+// Tc = E T (R row-major + t): Rc = Re R, tc = Re t + te
+__device__ inline void rig_compose(const double* E, const double* T, double* out) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            out[3 * i + j] = (E[3 * i] * T[j] + E[3 * i + 1] * T[3 + j]) + E[3 * i + 2] * T[6 + j];
+        out[9 + i] = ((E[3 * i] * T[9] + E[3 * i + 1] * T[10]) + E[3 * i + 2] * T[11]) + E[9 + i];
+    }
+}
+
+__device__ inline int rig_camera(const RigArgs& ra, int b) {
+    int c = 0;
+    for (int k = 1; k < ra.n_cams; ++k)
+        if (b >= ra.tile_off[k]) c = k;
+    return c;
+}
+
+// Wave 0 (after every camera's S_c is in red[c]): the rig's 28 sums into
+// L.S and nGood into L.ngood.  Lane e < 21 (upper-triangle entry (i, j)),
+// 21 + i (b_i) or 27 (cost) folds the cameras in ascending order.
+__device__ inline void rig_combine(const RigArgs& ra, const double (*red)[kSums], const int* g, double* sM,
+                                   SolveLds& L) {
+    const int lane = threadIdx.x & 63;
+    // (i, j) of upper entry e, row-major over i <= j
+    int ei = 0, ej = 0;
+    {
+        int e = lane < 21 ? lane : 0, r = 0;
+        while (e >= 6 - r) {
+            e -= 6 - r;
+            ++r;
+        }
+        ei = r;
+        ej = r + e;
+    }
+    double acc = 0.0;
+    for (int c = 0; c < ra.n_cams; ++c) {
+        const double* S = red[c];
+        const double* Ad = ra.cam[c].Ad;
+        // M = H_c Ad (lane l < 36: M[l / 6][l % 6])
+        if (lane < 36) {
+            const int i = lane / 6, j = lane - 6 * (lane / 6);
+            double m = 0.0;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                const int a = i < k ? i : k, bb = i < k ? k : i;
+                const double h = S[a * 6 - (a * (a - 1)) / 2 + (bb - a)];
+                m = k == 0 ? h * Ad[j] : m + h * Ad[6 * k + j];
+            }
+            sM[lane] = m;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        double v = 0.0;
+        if (lane < 21) {
+            // Ad^T M: entry (ei, ej)
+#pragma unroll
+            for (int k = 0; k < 6; ++k) v = k == 0 ? Ad[ei] * sM[ej] : v + Ad[6 * k + ei] * sM[6 * k + ej];
+        } else if (lane < 27) {
+            const int i = lane - 21;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) v = k == 0 ? Ad[i] * S[21] : v + Ad[6 * k + i] * S[21 + k];
+        } else if (lane == 27) {
+            v = S[27];
+        }
+        acc = c == 0 ? v : acc + v;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    if (lane < kSums) L.S[lane] = acc;
+    if (lane == 0) {
+        int ng = 0;
+        for (int c = 0; c < ra.n_cams; ++c) ng += g[c];
+        L.ngood = ng;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+template <bool FAST>
+__global__ __launch_bounds__(kThreads) void rig_level_kernel(RigArgs ra) {
+    __shared__ SolveLds L;
+    __shared__ double s_red[kMaxRigCams][kSums];
+    __shared__ int s_g[kMaxRigCams];
+    __shared__ double s_M[36];
+    __shared__ double s_pose[12];
+    __shared__ double s_pts[kMaxTile * kSums];
+    __shared__ int s_good;
+    __shared__ int s_arrive;
+    __shared__ PfLds s_pf;
+    const int lv = ra.level;
+    const bool solve = lv < kLevels - 1;  // L(3) is seeded
+    const int sl = lv + 1;                // level solved in the prologue (F: 0)
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+    const int c = rig_camera(ra, blockIdx.x);
+    const int bt = (int)blockIdx.x - ra.tile_off[c];
+    const DirectArgs& a = ra.cam[c].d;
+    const bool tiles = lv >= 0 && bt < a.n_tiles;
+    if (t == 0) {
+        s_arrive = 0;
+        s_good = 0;
+    }
+    lds_barrier();
+    // ---- every camera's tile partials of level sl (wave w: camera w)
+    if (solve && wave < ra.n_cams) {
+        const DirectArgs& aw = ra.cam[wave].d;
+        double v[kSums];
+        int gg = 0;
+        if (lane < aw.n_tiles) {
+            const double2* src =
+                reinterpret_cast<const double2*>(aw.s.part + ((size_t)sl * kRigTiles + lane) * kSums);
+#pragma unroll
+            for (int k = 0; k < kSums / 2; ++k) {
+                const double2 d = src[k];
+                v[2 * k] = d.x;
+                v[2 * k + 1] = d.y;
+            }
+            gg = aw.s.good[sl * kRigTiles + lane];
+        } else {
+#pragma unroll
+            for (int k = 0; k < kSums; ++k) v[k] = 0.0;
+        }
+        int idx;
+        const double f = reduce_scatter_28(v, &idx);
+        if (lane < 32 && idx >= 0) s_red[wave][idx] = f;
+        const int g = wave_sum_int(gg);
+        if (lane == 0) s_g[wave] = g;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) atomicAdd(&s_arrive, 1);
+    }
+    // ---- the T this level starts from (thread 256)
+    if (t == 256) {
+        double st[7];
+        if (!solve) {
+            quat_from_matrix(ra.seed, st);
+            st[4] = ra.seed[9];
+            st[5] = ra.seed[10];
+            st[6] = ra.seed[11];
+        } else {
+            for (int k = 0; k < 7; ++k) st[k] = ra.state[sl * kStateStride + k];
+        }
+        for (int k = 0; k < 7; ++k) {
+            L.state[k] = st[k];
+            L.best[k] = st[k];
+        }
+        L.cost = 0.0;
+        L.last_cost = 0.0;
+        L.cont = 0;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        atomicAdd(&s_arrive, 1);
+    }
+    // ---- prefetch of this workgroup's tile at the predicted camera pose
+    const bool pf_wave = !solve || (wave != 0 && wave != 4);
+    if (tiles && pf_wave) {
+        double T[12], pred[12];
+        if (!solve) {
+            for (int k = 0; k < 12; ++k) T[k] = ra.seed[k];
+        } else {
+            double sp[7];
+            for (int k = 0; k < 7; ++k) sp[k] = ra.state[sl * kStateStride + k];
+            state_to_pose(sp, T);
+        }
+        rig_compose(ra.cam[c].E, T, pred);
+        const int first = solve ? wave - 1 - (wave > 4 ? 1 : 0) : wave;
+        const int stride = solve ? kWaves - 2 : kWaves;
+        prefetch_tile<FAST>(a, lv, bt, pred, a.fp.pose_last, true, first, stride, s_pf);
+    }
+    // ---- the solve (wave 0)
+    if (wave == 0) {
+        const int need = solve ? ra.n_cams + 1 : 1;
+        while (__hip_atomic_load(&s_arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
+            __builtin_amdgcn_s_sleep(1);
+        if (solve) {
+            __builtin_amdgcn_s_setprio(3);
+            rig_combine(ra, s_red, s_g, s_M, L);
+            double* stp = (ra.stats && blockIdx.x == 0) ? ra.stats + (size_t)kStats * sl : nullptr;
+            if (FAST)
+                solve_wave0_ldlt(L, 0, stp);
+            else
+                solve_wave0(L, 0, stp);
+            __builtin_amdgcn_s_setprio(0);
+        }
+        if (lane == 0) {
+            // one step per level: L.cont (the reference's cost == 0
+            // continuation) is not part of the rig spec
+            double T[12];
+            state_to_pose(L.state, T);
+            rig_compose(ra.cam[c].E, T, s_pose);
+            if (blockIdx.x == 0) {
+                const int out = lv >= 0 ? lv : kLevels;
+                for (int k = 0; k < 7; ++k) ra.state[out * kStateStride + k] = L.state[k];
+                if (lv < 0) {
+                    if (ra.pose_out)
+                        for (int k = 0; k < 12; ++k) ra.pose_out[k] = T[k];
+                    if (ra.log && ra.log_index >= 0)
+                        for (int k = 0; k < 12; ++k) ra.log[12 * (size_t)ra.log_index + k] = T[k];
+                    for (int cc = 0; cc < ra.n_cams; ++cc) {
+                        double Tc[12];
+                        rig_compose(ra.cam[cc].E, T, Tc);
+                        for (int k = 0; k < 12; ++k) ra.cam_last[12 * cc + k] = Tc[k];
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();  // B2
+    if (tiles) {
+        const LevelPair fp = level_pair(a.fp, lv);
+        double pose[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) pose[k] = s_pose[k];
+        direct_tile_pf<FAST, FAST>(a, fp, lv, pose, bt, s_pf, false, a.s.part + (size_t)lv * kRigTiles * kSums,
+                                   a.s.good + lv * kRigTiles, s_pts, &s_good);
+    }
+}
+static_assert(sizeof(RigArgs) <= 4096, "rig kernel arguments exceed 4 KB");
+
 struct Pose12v {
     double v[12];
 };
@@ -1140,6 +1400,77 @@ void launch_direct_final(const FrameDev& last_pyr, const FrameDev& cur_pyr, cons
         direct_level_kernel<true><<<1, kThreads, 0, stream>>>(a);
     else
         direct_level_kernel<false><<<1, kThreads, 0, stream>>>(a);
+}
+
+// Tiles of a rig camera with n points under a cap of max_tiles (<= 64):
+// faithful: the smallest power-of-two tile >= max(8, P / 64) that fits;
+// tolerance mode: min(n, max_tiles) even slices.
+static void rig_tiling(int n, int max_tiles, bool split, int* tile, int* n_tiles) {
+    int P = 1;
+    while (P < n) P <<= 1;
+    int T = P / kRigTiles > kWaves ? P / kRigTiles : kWaves;
+    while ((n + T - 1) / T > max_tiles && T < kMaxTile) T <<= 1;
+    *tile = T;
+    *n_tiles = (n + T - 1) / T;
+    if (split && n > 0) {
+        *n_tiles = n < max_tiles ? n : max_tiles;
+        *tile = (n + *n_tiles - 1) / *n_tiles;
+    }
+}
+
+size_t rig_scratch_bytes() { return (size_t)kLevels * kRigTiles * kSums * 8 + (size_t)kLevels * kRigTiles * 4; }
+
+int launch_rig_direct(const RigCamDev* cams, int n_cams, const PyrGeom& g, const double K[4], double* state,
+                      const double* seed12, double* stats, double* pose_out, double* log, int log_index,
+                      double* cam_last, hipStream_t stream, int precision) {
+    if (n_cams < 1 || n_cams > kMaxRigCams) return -1;
+    const bool fast = precision == VISO_PRECISION_FAST;
+    RigArgs ra{};
+    ra.n_cams = n_cams;
+    const int cap = std::min(kRigTiles, kMaxTiles / n_cams);
+    int off = 0;
+    for (int c = 0; c < n_cams; ++c) {
+        const RigCamDev& cd = cams[c];
+        DirectArgs& a = ra.cam[c].d;
+        a.fp.last = cd.last;
+        a.fp.cur = cd.cur;
+        a.fp.pose_last = cd.pose_last12;
+        a.g = make_pyrdev(g);
+        a.K = Intrinsics{K[0], K[1], K[2], K[3]};
+        a.points = cd.points;
+        a.n = cd.n;
+        rig_tiling(cd.n, cap, fast, &a.tile, &a.n_tiles);
+        a.split = fast && cd.n > 0 ? 1 : 0;
+        a.s.part = (double*)cd.scratch;
+        a.s.good = (int*)((char*)cd.scratch + (size_t)kLevels * kRigTiles * kSums * 8);
+        a.log_index = -1;
+        a.prev_log_index = -1;
+        ra.cam[c].Ad = cd.Ad;
+        for (int k = 0; k < 12; ++k) ra.cam[c].E[k] = cd.E[k];
+        ra.tile_off[c] = off;
+        off += a.n_tiles;
+    }
+    ra.tile_off[n_cams] = off;
+    ra.state = state;
+    ra.seed = seed12;
+    ra.stats = stats;
+    ra.log_index = -1;
+    const int grid = off > 0 ? off : 1;
+    for (int level = kLevels - 1; level >= -1; --level) {
+        ra.level = level;
+        if (level < 0) {
+            ra.pose_out = pose_out;
+            ra.log = log;
+            ra.log_index = log ? log_index : -1;
+            ra.cam_last = cam_last;
+        }
+        const int gl = level < 0 ? 1 : grid;
+        if (fast)
+            rig_level_kernel<true><<<gl, kThreads, 0, stream>>>(ra);
+        else
+            rig_level_kernel<false><<<gl, kThreads, 0, stream>>>(ra);
+    }
+    return 0;
 }
 
 void launch_direct_pose(const FrameDev& last_pyr, const FrameDev& cur_pyr, const PyrGeom& g,

@@ -144,6 +144,29 @@ void launch_direct_final(const FrameDev& last, const FrameDev& cur, const PyrGeo
                          const double* pose_last12, const DirectScratch& s, double* stats,
                          double* pose_out, double* log, int log_index, hipStream_t stream,
                          int precision = VISO_PRECISION_FAITHFUL);
+// ---------------------------------------------------------------- rig direct pose
+// Multi-camera photometric rig (the repo's own spec;
+// oracle/oracle_rig.cpp): levels 3..0 of one rig Gauss-Newton step each over
+// every camera's map points, camera c at E_c T, per-camera 28 sums combined
+// through Ad(E_c); then F writes the rig pose (+ log) and each camera's next
+// `last` pose E_c T.  5 launches.
+constexpr int kMaxRigCams = 4;
+struct RigCamDev {
+    FrameDev last, cur;          // the camera's pyramids
+    const double* points;        // its map points (world), n x 3
+    int n;
+    const double* pose_last12;   // its `last` pose (device, E_c T_last)
+    double E[12];                // rig -> camera
+    const double* Ad;            // device, 36
+    void* scratch;               // rig_scratch_bytes()
+};
+size_t rig_scratch_bytes();
+// state: [kLevels + 1][8] device; seed12: last rig pose (device); stats:
+// [kLevels][50] or null; cam_last: n_cams x 12 device.  Returns -1 on a bad
+// camera count.
+int launch_rig_direct(const RigCamDev* cams, int n_cams, const PyrGeom& g, const double K[4], double* state,
+                      const double* seed12, double* stats, double* pose_out, double* log, int log_index,
+                      double* cam_last, hipStream_t stream, int precision);
 // dst (12 doubles, device) <- src (host values, passed by value)
 void launch_set_pose(double* dst, const double src[12], hipStream_t stream);
 
