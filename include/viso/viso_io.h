@@ -10,12 +10,16 @@
  *   - 8-bit grey: the bytes as stored; 1/2/4-bit grey expanded to 0..255
  *     (libpng png_set_expand_gray_1_2_4_to_8); 16-bit grey: the high byte
  *     (png_set_strip_16);
- *   - RGB / RGBA / palette (8-bit): alpha dropped (png_set_strip_alpha),
+ *   - RGB / RGBA (8- or 16-bit; 16-bit samples to their high byte,
+ *     png_set_strip_16) / palette: alpha dropped (png_set_strip_alpha),
  *     palette expanded, then libpng 1.6's png_set_rgb_to_gray(.., 0.299,
  *     0.587) without gamma tables: grey = r if r == g == b, else
  *     (9797 r + 19234 g + 3737 b) >> 15 (truncating; libpng's fixed-point
  *     weights 0.299 * 32768 and 0.587 * 32768 rounded down, blue the rest);
- *   - 16-bit colour is rejected (VISO_ERR_ARG).
+ *   - ancillary chunks are not interpreted (gAMA / sRGB / iCCP: imread sets
+ *     no gamma transform; tRNS: expanded to alpha, then stripped); a CRC
+ *     error in an ancillary chunk skips the chunk (libpng's default), in a
+ *     critical chunk it fails the decode (VISO_ERR_ARG).
  * Parity of the colour conversion against OpenCV itself is unpinned (neither
  * OpenCV nor libpng is in the image); grey PNGs (KITTI) are exact.
  */

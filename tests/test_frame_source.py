@@ -114,6 +114,49 @@ def test_rejects_corrupt():
         kitti.decode_png(b"not a png at all")
 
 
+def _png_raw(ctype, depth, rows, w, h, extra=()):
+    """A minimal non-interlaced PNG (filter 0 on every line) with ancillary
+    chunks `extra` = [(type, data, crc_ok)] placed before IDAT."""
+    import struct
+    import zlib
+
+    def chunk(t, d, ok=True):
+        crc = zlib.crc32(t + d) & 0xFFFFFFFF
+        return struct.pack(">I", len(d)) + t + d + struct.pack(">I", crc if ok else crc ^ 0x5A5A5A5A)
+
+    ihdr = struct.pack(">IIBBBBB", w, h, depth, ctype, 0, 0, 0)
+    raw = b"".join(b"\x00" + r for r in rows)
+    body = b"".join(chunk(t, d, ok) for t, d, ok in extra)
+    return (b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", ihdr) + body + chunk(b"IDAT", zlib.compress(raw)) +
+            chunk(b"IEND", b""))
+
+
+def test_rgb16_ancillary_chunks_and_bad_ancillary_crc():
+    """16-bit RGB(A) -> the high byte of each sample (png_set_strip_16), then
+    the grey rule; gAMA / tRNS change nothing (imread sets no gamma
+    transform, transparency is stripped); an ancillary chunk with a bad CRC
+    is skipped (libpng's default), a critical one fails."""
+    import struct
+    from viso_amd._lib import VisoError
+    rng = np.random.default_rng(5)
+    h, w = 6, 11
+    rgb16 = rng.integers(0, 65536, (h, w, 3), dtype=np.uint16)
+    exp = _rgb_to_grey((rgb16 >> 8).astype(np.uint8))
+    rows = [rgb16[y].astype(">u2").tobytes() for y in range(h)]
+    extra = [(b"gAMA", struct.pack(">I", 45455), True), (b"tRNS", struct.pack(">HHH", 1, 2, 3), True),
+             (b"tEXt", b"Comment\x00corrupt", False)]
+    assert np.array_equal(kitti.decode_png(_png_raw(2, 16, rows, w, h, extra)), exp)
+    rgba16 = np.concatenate([rgb16, rng.integers(0, 65536, (h, w, 1), dtype=np.uint16)], axis=2)
+    rows = [rgba16[y].astype(">u2").tobytes() for y in range(h)]
+    assert np.array_equal(kitti.decode_png(_png_raw(6, 16, rows, w, h)), exp)
+    grey = rng.integers(0, 256, (h, w), dtype=np.uint8)
+    ok = _png_raw(0, 8, [grey[y].tobytes() for y in range(h)], w, h, [(b"tRNS", b"\x00\x07", True)])
+    assert np.array_equal(kitti.decode_png(ok), grey)
+    bad = _png_raw(0, 8, [grey[y].tobytes() for y in range(h)], w, h, [(b"PLTE", b"\x00\x00\x00", False)])
+    with pytest.raises(VisoError):
+        kitti.decode_png(bad)
+
+
 def _write_kitti(root, seq, n):
     os.makedirs(os.path.join(root, "image_0"))
     os.makedirs(os.path.join(root, "image_1"))

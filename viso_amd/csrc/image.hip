@@ -2,11 +2,11 @@
 // and FAST-9/16 + NMS (cv::FAST restated).  Integer arithmetic, bit-exact
 // against the oracle (oracle/oracle_image.cpp).
 //
-// Pyramid (product path): pyr_down_stream_kernel, one launch per level,
-// batched over every image of a chunk; register-streaming bands (see below).
-// HBM-bound: algorithmic bytes per image = level-0 read + levels 1..3 written
-// (DESIGN.md §4).  pyr_fused3_kernel (one launch for all levels, LDS tiles)
-// is kept for A/B timing (launch_pyramid_frames_fused).
+// Pyramid: one launch per level, batched over every image of a chunk:
+// pyr_down_sk_kernel (register-only streaming bands, below) for source levels
+// at least 8 columns wide, pyr_down_stream_kernel (LDS-staged rows) for the
+// tiny levels of small images.  HBM-bound: algorithmic bytes per image =
+// level-0 read + levels 1..3 written.
 //
 // FAST: one workgroup per image row y.  It scores rows y-1, y, y+1 from a
 // 9-row LDS window, applies the strict 3x3 NMS to row y and appends the
@@ -14,7 +14,6 @@
 // order is then restored across rows by fast_compact, an exclusive prefix
 // over per-row counts).
 #include <algorithm>
-#include <cstdlib>
 #include <type_traits>
 #include <vector>
 
@@ -36,263 +35,6 @@ __device__ inline int reflect101(int p, int len) {
     return p;
 }
 
-// ---------------------------------------------------------------- fused pyramid (A/B)
-// One workgroup owns a level-3 tile of 16x8 and the matching level-2 (32x16)
-// and level-1 (64x32) tiles, staging the level-0 window that feeds them
-// (149 x 85, recursive 5-tap halos) in LDS and filtering level by level.
-constexpr int kF3W = 16, kF3H = 8;
-constexpr int kF2W = 2 * kF3W + 3, kF2H = 2 * kF3H + 3;  // 35 x 19
-constexpr int kF1W = 2 * kF2W + 3, kF1H = 2 * kF2H + 3;  // 73 x 41
-constexpr int kF0W = 2 * kF1W + 3, kF0H = 2 * kF1H + 3;  // 149 x 85
-
-struct PyrFusedArgs {
-    const uint8_t* l0[kPyrBatch];
-    uint8_t* slot[kPyrBatch];
-    int w[4], h[4];
-    unsigned long long off[4];
-};
-
-// Tile details:
-//  * every window (level 0 in LDS as loaded, levels 1 and 2 as computed) is
-//    made valid at its out-of-image positions by copying the reflect-101
-//    partner (per level, against that level's size) once per border tile, so
-//    the filter taps are plain LDS reads at fixed offsets (no per-tap
-//    reflection, no bounds tests);
-//  * level 0 rows are fetched as aligned 16-byte chunks straight into a raw
-//    LDS row (16 bytes of slack either side for the border fill) and read at
-//    a per-row byte offset;
-//  * the horizontal passes produce two adjacent outputs per thread from 7
-//    shared taps.
-// Integer sums are exact, so the result equals three separate pyrDown passes.
-constexpr int kR0P = 16 + 176 + 16;  // raw level-0 row: slack | chunks | slack
-
-// Barrier for LDS hand-offs only (global loads stay in flight across it).
-__device__ inline void lds_barrier_px() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-struct PyrTile {
-    const uint8_t* src;
-    uint8_t* base;
-    int X3, Y3, ox0, oy0, cl, ch;
-};
-
-__device__ inline PyrTile pyr_tile(const PyrFusedArgs& a, int t, int tx, int ty) {
-    PyrTile T;
-    const int per = tx * ty;
-    const int z = t / per, rem = t - z * per;
-    const int by = rem / tx, bx = rem - by * tx;
-    T.src = a.l0[z];
-    T.base = a.slot[z];
-    T.X3 = bx * kF3W;
-    T.Y3 = by * kF3H;
-    const int ox2 = 2 * T.X3 - 2, oy2 = 2 * T.Y3 - 2;
-    const int ox1 = 2 * ox2 - 2, oy1 = 2 * oy2 - 2;
-    T.ox0 = 2 * ox1 - 2;
-    T.oy0 = 2 * oy1 - 2;
-    T.cl = max(T.ox0, 0);
-    T.ch = min(T.ox0 + kF0W, a.w[0]);
-    return T;
-}
-
-// Level-0 window chunk j of this thread: row r = it / 11, 16-byte chunk k.
-// The chunk is addressed as src + off (an offset, not a rebuilt pointer, so
-// the load stays a global_load: a flat load would also count in lgkmcnt and
-// be drained by the LDS-only barriers).
-__device__ inline bool pyr_chunk(const PyrFusedArgs& a, const PyrTile& T, int j, int& r, int& k,
-                                 long long& off) {
-    const int it = (int)threadIdx.x + 256 * j;
-    if (it >= kF0H * 11) return false;
-    r = it / 11;
-    k = it - r * 11;
-    const int ys = reflect101(T.oy0 + r, a.h[0]);
-    const long long row = (long long)ys * a.w[0];
-    const long long mis = (long long)(((uintptr_t)T.src + (uintptr_t)(row + T.cl)) & 15);
-    off = row + T.cl - mis + 16 * (long long)k;
-    return off < row + T.ch;
-}
-
-__device__ inline void pyr_issue(const PyrFusedArgs& a, const PyrTile& T, uint4 (&v)[4]) {
-    const long long n = (long long)a.w[0] * a.h[0];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        int r, k;
-        long long off;
-        v[j] = make_uint4(0, 0, 0, 0);
-        if (!pyr_chunk(a, T, j, r, k, off)) continue;
-        if (off >= 0 && off + 16 <= n) {
-            v[j] = *reinterpret_cast<const uint4*>(T.src + off);
-        } else {  // the image's first / last bytes: no read outside the buffer
-            uint32_t wv[4] = {0, 0, 0, 0};
-#pragma unroll
-            for (int b = 0; b < 16; ++b)
-                if (off + b >= 0 && off + b < n) wv[b >> 2] |= (uint32_t)T.src[off + b] << (8 * (b & 3));
-            v[j] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
-        }
-    }
-}
-
-// Persistent form of the v2 tile: each workgroup walks tiles t, t + grid,
-// ...; the next tile's level-0 chunks are loaded into registers while the
-// current tile is filtered (the passes hand off through LDS-only barriers,
-// so those loads stay in flight).
-__global__ __launch_bounds__(256) void pyr_fused3_kernel(PyrFusedArgs a, int tx, int ty, int total) {
-    __shared__ __attribute__((aligned(16))) uint8_t s0[kF0H][kR0P];
-    __shared__ int s_base[kF0H];
-    __shared__ short hs0[kF0H][kF1W + 1];
-    __shared__ uint8_t s1[kF1H][kF1W + 3];
-    __shared__ short hs1[kF1H][kF2W + 1];
-    __shared__ uint8_t s2[kF2H][kF2W + 1];
-    const int tid = threadIdx.x;
-    const int w0 = a.w[0], h0 = a.h[0], w1 = a.w[1], h1 = a.h[1];
-    const int w2 = a.w[2], h2 = a.h[2], w3 = a.w[3], h3 = a.h[3];
-    int t = blockIdx.x;
-    if (t >= total) return;
-    uint4 v[4];
-    PyrTile T = pyr_tile(a, t, tx, ty);
-    pyr_issue(a, T, v);
-    for (; t < total; t += gridDim.x) {
-        const int X3 = T.X3, Y3 = T.Y3;
-        const int ox2 = 2 * X3 - 2, oy2 = 2 * Y3 - 2;
-        const int ox1 = 2 * ox2 - 2, oy1 = 2 * oy2 - 2;
-        const int ox0 = T.ox0, oy0 = T.oy0;
-        uint8_t* __restrict__ base = T.base;
-        if (tid < kF0H) {
-            const int ys = reflect101(oy0 + tid, h0);
-            const uintptr_t row = (uintptr_t)T.src + (uintptr_t)ys * w0;
-            s_base[tid] = 16 + (int)((row + ox0) - ((row + T.cl) & ~(uintptr_t)15));
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            int r, k;
-            long long off;
-            if (pyr_chunk(a, T, j, r, k, off)) *reinterpret_cast<uint4*>(&s0[r][16 + 16 * k]) = v[j];
-        }
-        lds_barrier_px();
-        const bool xborder = ox0 < 0 || ox0 + kF0W > w0;
-        // prefetch the next tile
-        const int tn = t + (int)gridDim.x;
-        if (tn < total) {
-            T = pyr_tile(a, tn, tx, ty);
-            pyr_issue(a, T, v);
-        }
-        if (xborder) {  // out-of-image columns <- reflect-101 partners (same row)
-            for (int it = tid; it < kF0H * kF0W; it += 256) {
-                const int r = it / kF0W, c = it - r * kF0W;
-                const int x = ox0 + c;
-                if (x >= 0 && x < w0) continue;
-                const int b = s_base[r];
-                s0[r][b + c] = s0[r][b + reflect101(x, w0) - ox0];
-            }
-            lds_barrier_px();
-        }
-        // ---- level 1, horizontal: hs0[r][c] for in-image x1 = ox1 + c, two at a time
-        const int c1lo = max(0, -ox1), c1hi = min(kF1W, w1 - ox1);
-#pragma unroll 4
-        for (int it = tid; it < kF0H * 37; it += 256) {
-            const int r = it / 37, c = 2 * (it - r * 37);
-            if (c >= c1hi || c + 1 < c1lo) continue;
-            const uint8_t* p = &s0[r][s_base[r] + 2 * c];
-            const int t0 = p[0], t1 = p[1], t2 = p[2], t3 = p[3], t4 = p[4], t5 = p[5], t6 = p[6];
-            if (c >= c1lo) hs0[r][c] = (short)(t0 + 4 * t1 + 6 * t2 + 4 * t3 + t4);
-            if (c + 1 < c1hi) hs0[r][c + 1] = (short)(t2 + 4 * t3 + 6 * t4 + 4 * t5 + t6);
-        }
-        lds_barrier_px();
-        // ---- level 1, vertical (+ store of the tile's own 64 x 32 core)
-        uint8_t* d1 = base + a.off[1];
-        const int r1lo = max(0, -oy1), r1hi = min(kF1H, h1 - oy1);
-#pragma unroll 4
-        for (int it = tid; it < kF1H * kF1W; it += 256) {
-            const int r = it / kF1W, c = it - r * kF1W;
-            if (r < r1lo || r >= r1hi || c < c1lo || c >= c1hi) continue;
-            const int s = hs0[2 * r][c] + 4 * hs0[2 * r + 1][c] + 6 * hs0[2 * r + 2][c] +
-                          4 * hs0[2 * r + 3][c] + hs0[2 * r + 4][c];
-            const uint8_t o = (uint8_t)((s + 128) >> 8);
-            s1[r][c] = o;
-            const int x1 = ox1 + c, y1 = oy1 + r;
-            if (x1 >= 4 * X3 && x1 < 4 * X3 + 4 * kF3W && y1 >= 4 * Y3 && y1 < 4 * Y3 + 4 * kF3H)
-                d1[(size_t)y1 * w1 + x1] = o;
-        }
-        lds_barrier_px();
-        const bool b1 = c1lo > 0 || c1hi < kF1W || r1lo > 0 || r1hi < kF1H;
-        if (b1) {
-            for (int it = tid; it < kF1H * kF1W; it += 256) {  // columns, in-image rows
-                const int r = it / kF1W, c = it - r * kF1W;
-                if (r < r1lo || r >= r1hi || (c >= c1lo && c < c1hi)) continue;
-                s1[r][c] = s1[r][reflect101(ox1 + c, w1) - ox1];
-            }
-            lds_barrier_px();
-            for (int it = tid; it < kF1H * kF1W; it += 256) {  // whole rows
-                const int r = it / kF1W, c = it - r * kF1W;
-                if (r >= r1lo && r < r1hi) continue;
-                s1[r][c] = s1[reflect101(oy1 + r, h1) - oy1][c];
-            }
-            lds_barrier_px();
-        }
-        // ---- level 2, horizontal
-        const int c2lo = max(0, -ox2), c2hi = min(kF2W, w2 - ox2);
-#pragma unroll 4
-        for (int it = tid; it < kF1H * 18; it += 256) {
-            const int r = it / 18, c = 2 * (it - r * 18);
-            if (c >= c2hi || c + 1 < c2lo) continue;
-            const uint8_t* p = &s1[r][2 * c];
-            const int t0 = p[0], t1 = p[1], t2 = p[2], t3 = p[3], t4 = p[4];
-            if (c >= c2lo) hs1[r][c] = (short)(t0 + 4 * t1 + 6 * t2 + 4 * t3 + t4);
-            if (c + 1 < c2hi) {
-                const int t5 = p[5], t6 = p[6];
-                hs1[r][c + 1] = (short)(t2 + 4 * t3 + 6 * t4 + 4 * t5 + t6);
-            }
-        }
-        lds_barrier_px();
-        // ---- level 2, vertical (+ 32 x 16 core)
-        uint8_t* d2 = base + a.off[2];
-        const int r2lo = max(0, -oy2), r2hi = min(kF2H, h2 - oy2);
-#pragma unroll 4
-        for (int it = tid; it < kF2H * kF2W; it += 256) {
-            const int r = it / kF2W, c = it - r * kF2W;
-            if (r < r2lo || r >= r2hi || c < c2lo || c >= c2hi) continue;
-            const int s = hs1[2 * r][c] + 4 * hs1[2 * r + 1][c] + 6 * hs1[2 * r + 2][c] +
-                          4 * hs1[2 * r + 3][c] + hs1[2 * r + 4][c];
-            const uint8_t o = (uint8_t)((s + 128) >> 8);
-            s2[r][c] = o;
-            const int x2 = ox2 + c, y2 = oy2 + r;
-            if (x2 >= 2 * X3 && x2 < 2 * X3 + 2 * kF3W && y2 >= 2 * Y3 && y2 < 2 * Y3 + 2 * kF3H)
-                d2[(size_t)y2 * w2 + x2] = o;
-        }
-        lds_barrier_px();
-        const bool b2 = c2lo > 0 || c2hi < kF2W || r2lo > 0 || r2hi < kF2H;
-        if (b2) {
-            for (int it = tid; it < kF2H * kF2W; it += 256) {
-                const int r = it / kF2W, c = it - r * kF2W;
-                if (r < r2lo || r >= r2hi || (c >= c2lo && c < c2hi)) continue;
-                s2[r][c] = s2[r][reflect101(ox2 + c, w2) - ox2];
-            }
-            lds_barrier_px();
-            for (int it = tid; it < kF2H * kF2W; it += 256) {
-                const int r = it / kF2W, c = it - r * kF2W;
-                if (r >= r2lo && r < r2hi) continue;
-                s2[r][c] = s2[reflect101(oy2 + r, h2) - oy2][c];
-            }
-            lds_barrier_px();
-        }
-        // ---- level 3 (16 x 8 outputs, 25 taps each)
-        uint8_t* d3 = base + a.off[3];
-        if (tid < kF3W * kF3H) {
-            const int cx = tid & (kF3W - 1), cy = tid / kF3W;
-            const int x3 = X3 + cx, y3 = Y3 + cy;
-            if (x3 < w3 && y3 < h3) {
-                int s = 0;
-    #pragma unroll
-                for (int i = 0; i < 5; ++i) {
-                    const int wi = i == 2 ? 6 : ((i & 1) ? 4 : 1);
-                    const uint8_t* p = &s2[2 * cy + i][2 * cx];
-                    s += wi * ((int)p[0] + 4 * (int)p[1] + 6 * (int)p[2] + 4 * (int)p[3] + (int)p[4]);
-                }
-                d3[(size_t)y3 * w3 + x3] = (uint8_t)((s + 128) >> 8);
-            }
-        }
-        lds_barrier_px();  // the next tile overwrites the windows
-    }
-}
-
 // ---------------------------------------------------------------- streaming pyrDown
 // One launch per level (L0->L1, L1->L2, L2->L3), batched over images.  A wave
 // owns a strip of 248 destination columns (4 per lane on lanes 0..61) and a
@@ -312,9 +54,6 @@ struct PyrLevelArgs {
     uint8_t* dst[kPyrBatch];
     int sw, sh, dw, dh;
     int bands, units;
-#ifdef VISO_PROBE
-    int diag;  // dev: 1 = skip stores (timing only)
-#endif
 };
 
 // 8 source bytes at offset off, never reading outside [0, n).
@@ -644,7 +383,7 @@ __global__ __launch_bounds__(256) void pyr_down_sk_kernel(PyrLevelArgs a) {
 #ifdef VISO_PROBE
     if (lane == 0) {
         const long long w = (long long)blockIdx.y * a.units + unit;
-        if (w < 8192 && a.diag >= 0) {
+        if (w < 8192) {
             g_pyr_tl[w][0] = pr_t0;
             g_pyr_tl[w][1] = __builtin_amdgcn_s_memrealtime();
             g_pyr_tl[w][2] = __builtin_amdgcn_s_getreg(4 | (31 << 11));
@@ -835,9 +574,6 @@ void launch_pyramid_frames(const PyrGeom& g, const uint8_t* const* l0, uint8_t* 
             a.dh = g.h[l];
             const int bh = l == 1 ? 8 : (l == 2 ? 4 : 2);
             a.bands = (a.dh + bh - 1) / bh;
-#ifdef VISO_PROBE
-            a.diag = getenv("VISO_PYR_DIAG") ? atoi(getenv("VISO_PYR_DIAG")) : 0;
-#endif
             a.units = a.bands * ((a.dw + kPsW - 1) / kPsW);
             const dim3 grid((a.units + 3) / 4, nb);
             if (a.sw >= 8) {  // register-only streaming form; the scalar form covers tiny levels
@@ -859,29 +595,6 @@ void launch_pyramid_frames(const PyrGeom& g, const uint8_t* const* l0, uint8_t* 
                 pyr_down_stream_kernel<2><<<grid, 256, 0, stream>>>(a);
             }
         }
-    }
-}
-
-// Fused single-launch form (pyr_fused3_kernel), kept for A/B timing.
-void launch_pyramid_frames_fused(const PyrGeom& g, const uint8_t* const* l0, uint8_t* const* slot,
-                                 int n, hipStream_t stream) {
-    auto cdiv = [](int a, int b) { return (a + b - 1) / b; };
-    const int tx = std::max(cdiv(g.w[3], kF3W), std::max(cdiv(g.w[2], 2 * kF3W), cdiv(g.w[1], 4 * kF3W)));
-    const int ty = std::max(cdiv(g.h[3], kF3H), std::max(cdiv(g.h[2], 2 * kF3H), cdiv(g.h[1], 4 * kF3H)));
-    for (int b0 = 0; b0 < n; b0 += kPyrBatch) {
-        const int nb = (n - b0) < kPyrBatch ? (n - b0) : kPyrBatch;
-        PyrFusedArgs a;
-        for (int l = 0; l < kLevels; ++l) {
-            a.w[l] = g.w[l];
-            a.h[l] = g.h[l];
-            a.off[l] = g.off[l];
-        }
-        for (int i = 0; i < nb; ++i) {
-            a.l0[i] = l0[b0 + i];
-            a.slot[i] = slot[b0 + i];
-        }
-        const int total = tx * ty * nb;
-        pyr_fused3_kernel<<<std::min(total, 1024), 256, 0, stream>>>(a, tx, ty, total);
     }
 }
 

@@ -25,7 +25,13 @@ struct Png {
     std::vector<uint8_t> idat, plte;
 };
 
-// chunk walk: IHDR, PLTE, IDAT (concatenated), IEND; CRCs checked
+// chunk walk: IHDR, PLTE, IDAT (concatenated), IEND.  A CRC error in a
+// critical chunk (upper-case first letter) is fatal; an ancillary chunk with
+// a bad CRC is skipped, as libpng's default does (png_crc_finish: a benign
+// error for ancillary chunks).  Ancillary chunks are not interpreted: gAMA /
+// sRGB / iCCP (cv::imread sets no gamma transform) and tRNS (expanded to
+// alpha by OpenCV, then stripped for IMREAD_GRAYSCALE) do not change the
+// grey bytes.
 int parse(const uint8_t* d, size_t n, Png& png) {
     static const uint8_t sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
     if (!d || n < 8 || std::memcmp(d, sig, 8) != 0) return VISO_ERR_ARG;
@@ -36,7 +42,12 @@ int parse(const uint8_t* d, size_t n, Png& png) {
         if (len > n - o - 12) return VISO_ERR_ARG;
         const uint8_t* type = d + o + 4;
         const uint8_t* data = d + o + 8;
-        if (crc32(crc32(0L, Z_NULL, 0), type, len + 4) != be32(data + len)) return VISO_ERR_ARG;
+        const bool critical = (type[0] & 0x20) == 0;
+        if (crc32(crc32(0L, Z_NULL, 0), type, len + 4) != be32(data + len)) {
+            if (critical) return VISO_ERR_ARG;
+            o += (size_t)len + 12;
+            continue;
+        }
         if (!std::memcmp(type, "IHDR", 4)) {
             if (len != 13) return VISO_ERR_ARG;
             png.w = be32(data);
@@ -59,10 +70,10 @@ int parse(const uint8_t* d, size_t n, Png& png) {
     const int d8 = png.depth;
     switch (png.ctype) {
         case 0: png.ch = 1; if (d8 != 1 && d8 != 2 && d8 != 4 && d8 != 8 && d8 != 16) return VISO_ERR_ARG; break;
-        case 2: png.ch = 3; if (d8 != 8) return VISO_ERR_ARG; break;  // 16-bit colour: unsupported
+        case 2: png.ch = 3; if (d8 != 8 && d8 != 16) return VISO_ERR_ARG; break;
         case 3: png.ch = 1; if (d8 != 1 && d8 != 2 && d8 != 4 && d8 != 8) return VISO_ERR_ARG; break;
         case 4: png.ch = 2; if (d8 != 8 && d8 != 16) return VISO_ERR_ARG; break;
-        case 6: png.ch = 4; if (d8 != 8) return VISO_ERR_ARG; break;
+        case 6: png.ch = 4; if (d8 != 8 && d8 != 16) return VISO_ERR_ARG; break;
         default: return VISO_ERR_ARG;
     }
     if (png.ctype == 3 && (png.plte.empty() || png.plte.size() % 3)) return VISO_ERR_ARG;
@@ -122,7 +133,11 @@ inline uint8_t grey_of(const Png& png, const uint8_t* raw, size_t i) {
         return rgb_to_gray(png.plte[k], png.plte[k + 1], png.plte[k + 2]);
     }
     if (png.ctype == 4) return d == 16 ? raw[4 * i] : raw[2 * i];  // alpha stripped
-    const uint8_t* p = raw + (size_t)png.ch * i;                     // RGB / RGBA
+    if (d == 16) {  // png_set_strip_16: the high byte of every sample
+        const uint8_t* p = raw + 2 * (size_t)png.ch * i;
+        return rgb_to_gray(p[0], p[2], p[4]);
+    }
+    const uint8_t* p = raw + (size_t)png.ch * i;  // RGB / RGBA
     return rgb_to_gray(p[0], p[1], p[2]);
 }
 

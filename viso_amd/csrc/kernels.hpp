@@ -17,9 +17,6 @@ constexpr int kPyrBatch = 128;
 // Three streaming launches (one per level).
 void launch_pyramid_frames(const PyrGeom& g, const uint8_t* const* l0, uint8_t* const* slot,
                            int n, hipStream_t stream);
-// Single fused launch (LDS tiles), kept for A/B timing.
-void launch_pyramid_frames_fused(const PyrGeom& g, const uint8_t* const* l0, uint8_t* const* slot,
-                                 int n, hipStream_t stream);
 
 struct FastScratch {
     int* row_count = nullptr;   // [h]
