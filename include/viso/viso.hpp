@@ -10,7 +10,10 @@
 //   Viso::OnNewFrame(Keyframe::Ptr)   src/viso.cpp:7-145
 //   Viso::poses                       include/viso.h:54 (Tcw, R row-major + t)
 //   Viso::GetPoints()                 include/viso.h:60-67
-//   VisualOdometryStereo::process(left, right, dims)   north-star facade
+//   StereoViso::process(left, right, dims)   the reference path with the
+//                                     stereo initialisation (viso_set_stereo)
+// The north-star VisualOdometryStereo / Matcher (the SVO engine) are in
+// viso_svo.hpp, the multi-camera photometric rig (VisoRig) in viso_rig.hpp.
 // No Eigen / Sophus / OpenCV types: poses are std::array<double, 12>.
 #ifndef VISO_HPP
 #define VISO_HPP
@@ -129,11 +132,16 @@ protected:
     viso_ctx* ctx_ = nullptr;
 };
 
-// North-star facade: the left image drives the reference path, the right
-// image is ingested (pyramid) for the stereo stage.
-class VisualOdometryStereo : public Viso {
+// The reference path fed with stereo pairs: the left image drives
+// OnNewFrame; while initialising, the right image gives the metric stereo
+// initialisation (viso_set_stereo, enabled with SetStereo) in place of the
+// 2D-2D one (src/viso.cpp:178-256).
+class StereoViso : public Viso {
 public:
     using Viso::Viso;
+    void SetStereo(double baseline, int max_disp = 128, int min_disp = 1) {
+        check(viso_set_stereo(ctx_, baseline, max_disp, min_disp), "viso_set_stereo");
+    }
     bool process(const uint8_t* left, const uint8_t* right, const int32_t* dims) {
         return viso_process_stereo(ctx_, left, right, dims) == VISO_OK;
     }

@@ -88,7 +88,9 @@ class Viso(FrameHandler):
 
     # ----------------------------------------------------------- north-star API
     def process(self, left: np.ndarray, right: np.ndarray) -> None:
-        """VisualOdometryStereo::process(left, right) facade."""
+        """A stereo pair through the reference path (viso_process_stereo): the
+        left image drives OnNewFrame, the right one the stereo initialisation
+        (the north-star VisualOdometryStereo is viso_amd.svo)."""
         left = np.ascontiguousarray(left, dtype=np.uint8)
         right = np.ascontiguousarray(right, dtype=np.uint8)
         h, w = left.shape
