@@ -89,7 +89,8 @@ int viso_ctx::init() {
                      o_hc = b.take(4 * (size_t)std::max(p.ransac_h_iters, 1)),
                      o_hmk = b.take((size_t)cap), o_si = b.take((size_t)kMaxCandidates * cap),
                      o_sp = b.take(24 * (size_t)kMaxCandidates * cap), o_in = b.take((size_t)cap),
-                     o_po = b.take(24 * (size_t)cap);
+                     o_po = b.take(24 * (size_t)cap), o_rp = b.take(8 * 24), o_rpg = b.take(16),
+                     o_hmom = b.take(8 * 45 * (size_t)cap), o_hM = b.take(8 * 81);
         rc = geo_buf.ensure(b.off);
         if (rc) return rc;
         char* base = (char*)geo_buf.ptr;
@@ -113,6 +114,10 @@ int viso_ctx::init() {
         a.sel_pts = (double*)(base + o_sp);
         a.inliers = (uint8_t*)(base + o_in);
         a.points_out = (double*)(base + o_po);
+        a.rp = (double*)(base + o_rp);
+        a.rp_good = (int*)(base + o_rpg);
+        a.hm = (double*)(base + o_hmom);
+        a.hM = (double*)(base + o_hM);
         a.cap = cap;
         const double K[9] = {p.fx, 0, p.cx, 0, p.fy, p.cy, 0, 0, 1};
         eigen_inverse3(K, Kinv);

@@ -347,109 +347,142 @@ __global__ __launch_bounds__(256) void scan_kernel(GeoArgs a) {
 }
 
 // ---------------------------------------------------------------- recoverPose
-__global__ __launch_bounds__(256) void recover_pose_kernel(GeoArgs a) {
-    __shared__ double s_R[2][9], s_t[3];
-    __shared__ int s_good[4][4];
+// cv::recoverPose(E, ...) in three launches: the decomposition (one
+// thread), the cheirality test of every point under the four motions (one
+// thread per point over the whole grid; integer counts, so the atomic adds
+// are order-free and exact), and the pick.
+__global__ __launch_bounds__(64) void recover_setup_kernel(GeoArgs a) {
     GeoCtl* c = a.ctl;
     if (!c->gate || c->e_best < 0) return;
+    if (threadIdx.x < 4) a.rp_good[threadIdx.x] = 0;
+    if (threadIdx.x != 0) return;
+    const double* E = a.e_models + 9 * (size_t)c->e_best;
+    double U[9], s[3], V[9];
+    svd3(E, U, s, V);
+    if (det3(U) < 0)
+        for (int k = 0; k < 9; ++k) U[k] = -U[k];
+    double Vt[9];
+    transpose3(V, Vt);
+    if (det3(Vt) < 0)
+        for (int k = 0; k < 9; ++k) Vt[k] = -Vt[k];
+    const double W[9] = {0, 1, 0, -1, 0, 0, 0, 0, 1};
+    double Wt[9], UW[9];
+    transpose3(W, Wt);
+    matmul3(U, W, UW);
+    matmul3(UW, Vt, a.rp);
+    matmul3(U, Wt, UW);
+    matmul3(UW, Vt, a.rp + 9);
+    a.rp[18] = U[2] * 1.0;
+    a.rp[19] = U[5] * 1.0;
+    a.rp[20] = U[8] * 1.0;
+}
+
+__global__ __launch_bounds__(256) void recover_count_kernel(GeoArgs a) {
+    const GeoCtl* c = a.ctl;
+    if (!c->gate || c->e_best < 0) return;
     const int n = c->n;
-    if (threadIdx.x == 0) {
-        const double* E = a.e_models + 9 * (size_t)c->e_best;
-        double U[9], s[3], V[9];
-        svd3(E, U, s, V);
-        if (det3(U) < 0)
-            for (int k = 0; k < 9; ++k) U[k] = -U[k];
-        double Vt[9];
-        transpose3(V, Vt);
-        if (det3(Vt) < 0)
-            for (int k = 0; k < 9; ++k) Vt[k] = -Vt[k];
-        const double W[9] = {0, 1, 0, -1, 0, 0, 0, 0, 1};
-        double Wt[9], UW[9];
-        transpose3(W, Wt);
-        matmul3(U, W, UW);
-        matmul3(UW, Vt, s_R[0]);
-        matmul3(U, Wt, UW);
-        matmul3(UW, Vt, s_R[1]);
-        s_t[0] = U[2] * 1.0;
-        s_t[1] = U[5] * 1.0;
-        s_t[2] = U[8] * 1.0;
-    }
-    __syncthreads();
-    const double sg[4] = {1, 1, -1, -1};
-    int good[4] = {0, 0, 0, 0};
-    for (int i = threadIdx.x; i < n; i += 256) {
+    // thread = (point, motion): lane l holds motion l & 3 of point l >> 2
+    const int g = blockIdx.x * 256 + threadIdx.x;
+    if ((int)blockIdx.x * 64 >= n) return;  // workgroup-uniform
+    const int i = g >> 2, m = g & 3;
+    bool ok = false;
+    if (i < n) {
+        const double sg = m < 2 ? 1.0 : -1.0;
+        const double* R = a.rp + 9 * (m & 1);
+        const double* s_t = a.rp + 18;
         const double x1 = a.q1[2 * i], y1 = a.q1[2 * i + 1], x2 = a.q2[2 * i], y2 = a.q2[2 * i + 1];
-        uint8_t m4 = 0;
-        for (int m = 0; m < 4; ++m) {
-            const double* R = s_R[m & 1];
-            const double tt[3] = {sg[m] * s_t[0], sg[m] * s_t[1], sg[m] * s_t[2]};
-            double X[4];
-            triangulate_h(R, tt, x1, y1, x2, y2, X);
-            bool ok = X[2] * X[3] > 0;
-            const double Q[3] = {X[0] / X[3], X[1] / X[3], X[2] / X[3]};
-            ok = (Q[2] < 50.0) && ok;
-            const double z2 = R[6] * Q[0] + R[7] * Q[1] + R[8] * Q[2] + tt[2] * 1.0;
-            ok = (z2 > 0) && ok;
-            ok = (z2 < 50.0) && ok;
-            ok = ok && a.e_mask[i];
-            good[m] += ok ? 1 : 0;
-        }
-        (void)m4;
+        const double tt[3] = {sg * s_t[0], sg * s_t[1], sg * s_t[2]};
+        double X[4];
+        triangulate_h(R, tt, x1, y1, x2, y2, X);
+        ok = X[2] * X[3] > 0;
+        const double Q[3] = {X[0] / X[3], X[1] / X[3], X[2] / X[3]};
+        ok = (Q[2] < 50.0) && ok;
+        const double z2 = R[6] * Q[0] + R[7] * Q[1] + R[8] * Q[2] + tt[2] * 1.0;
+        ok = (z2 > 0) && ok;
+        ok = (z2 < 50.0) && ok;
+        ok = ok && a.e_mask[i];
     }
-    for (int m = 0; m < 4; ++m) {
-        int g = wave_sum_int(good[m]);
-        if ((threadIdx.x & 63) == 0) s_good[m][threadIdx.x >> 6] = g;
+    // per motion: the lanes l with l & 3 == m
+    const unsigned long long b = __ballot(ok);
+    const unsigned long long sel = 0x1111111111111111ULL;
+    if ((threadIdx.x & 63) < 4) {
+        const int cnt = __popcll(b & (sel << (threadIdx.x & 3)));
+        if (cnt) atomicAdd(&a.rp_good[threadIdx.x & 3], cnt);
     }
-    __syncthreads();
+}
+
+__global__ __launch_bounds__(64) void recover_pick_kernel(GeoArgs a) {
+    GeoCtl* c = a.ctl;
+    if (!c->gate || c->e_best < 0 || threadIdx.x != 0) return;
+    int G[4];
+    for (int m = 0; m < 4; ++m) G[m] = a.rp_good[m];
+    int pick;
+    if (G[0] >= G[1] && G[0] >= G[2] && G[0] >= G[3])
+        pick = 0;
+    else if (G[1] >= G[0] && G[1] >= G[2] && G[1] >= G[3])
+        pick = 1;
+    else if (G[2] >= G[0] && G[2] >= G[1] && G[2] >= G[3])
+        pick = 2;
+    else
+        pick = 3;
+    double* cand = c->cand[c->n_cand];
+    for (int k = 0; k < 9; ++k) cand[k] = a.rp[9 * (pick & 1) + k];
+    for (int k = 0; k < 3; ++k) cand[9 + k] = pick >= 2 ? -a.rp[18 + k] : a.rp[18 + k];
+    c->n_cand += 1;
+}
+
+// ---------------------------------------------------------------- H refine moments
+// The least-squares DLT refinement's 9 x 9 moment matrix M = sum_i (ra ra^T +
+// rb rb^T) over the winner's inliers: the 45 upper-triangle leaves of every
+// point in one pass (thread per point), then the 45 canonical trees in
+// parallel (workgroup per entry), each exactly block_tree_sum's.
+__global__ __launch_bounds__(256) void h_moment_leaves_kernel(GeoArgs a) {
+    const GeoCtl* c = a.ctl;
+    if (!c->gate || c->h_best < 0 || c->h_count < 4) return;
+    const int n = c->n;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    double ra[9], rb[9];
+    h_rows(a.q1[2 * i], a.q1[2 * i + 1], a.q2[2 * i], a.q2[2 * i + 1], ra, rb);
+    const bool in = a.h_mask[i] != 0;
+    int k = 0;
+    for (int r = 0; r < 9; ++r)
+        for (int col = r; col < 9; ++col, ++k)
+            a.hm[(size_t)k * a.cap + i] = in ? ra[r] * ra[col] + rb[r] * rb[col] : 0.0;
+}
+
+__global__ __launch_bounds__(256) void h_moment_sums_kernel(GeoArgs a) {
+    __shared__ double s_red[4];
+    const GeoCtl* c = a.ctl;
+    if (!c->gate || c->h_best < 0 || c->h_count < 4) return;
+    const int n = c->n;
+    const int k = blockIdx.x;  // upper-triangle entry, row-major
+    int r = 0, e = k;
+    while (e >= 9 - r) {
+        e -= 9 - r;
+        ++r;
+    }
+    const int col = r + e;
+    const double* leaf = a.hm + (size_t)k * a.cap;
+    const double s = block_tree_sum(n, [&](int i) { return leaf[i]; }, s_red);
     if (threadIdx.x == 0) {
-        int G[4];
-        for (int m = 0; m < 4; ++m) G[m] = (s_good[m][0] + s_good[m][1]) + (s_good[m][2] + s_good[m][3]);
-        int pick;
-        if (G[0] >= G[1] && G[0] >= G[2] && G[0] >= G[3])
-            pick = 0;
-        else if (G[1] >= G[0] && G[1] >= G[2] && G[1] >= G[3])
-            pick = 1;
-        else if (G[2] >= G[0] && G[2] >= G[1] && G[2] >= G[3])
-            pick = 2;
-        else
-            pick = 3;
-        double* cand = c->cand[c->n_cand];
-        for (int k = 0; k < 9; ++k) cand[k] = s_R[pick & 1][k];
-        for (int k = 0; k < 3; ++k) cand[9 + k] = pick >= 2 ? -s_t[k] : s_t[k];
-        c->n_cand += 1;
+        a.hM[9 * r + col] = s;
+        a.hM[9 * col + r] = s;
     }
 }
 
 // ---------------------------------------------------------------- H refine + decompose
-__global__ __launch_bounds__(256) void h_refine_decompose_kernel(GeoArgs a) {
-    __shared__ double s_red[4];
-    __shared__ double s_M[81];
+__global__ __launch_bounds__(64) void h_refine_decompose_kernel(GeoArgs a) {
     GeoCtl* c = a.ctl;
     if (!c->gate || c->h_best < 0) return;
-    const int n = c->n;
     const int good = c->h_count;
-    if (good >= 4) {
-        for (int r = 0; r < 9; ++r)
-            for (int col = r; col < 9; ++col) {
-                const double s = block_tree_sum(n, [&](int i) {
-                    double ra[9], rb[9];
-                    h_rows(a.q1[2 * i], a.q1[2 * i + 1], a.q2[2 * i], a.q2[2 * i + 1], ra, rb);
-                    return a.h_mask[i] ? ra[r] * ra[col] + rb[r] * rb[col] : 0.0;
-                }, s_red);
-                if (threadIdx.x == 0) {
-                    s_M[9 * r + col] = s;
-                    s_M[9 * col + r] = s;
-                }
-            }
-    }
-    __syncthreads();
     if (threadIdx.x != 0) return;
     double H[9];
     const double* Hb = a.h_models + 9 * (size_t)c->h_best;
     for (int k = 0; k < 9; ++k) H[k] = Hb[k];
     if (good >= 4) {
         double M[81], ev[9], V[81];
-        for (int k = 0; k < 81; ++k) M[k] = s_M[k];
+        for (int k = 0; k < 81; ++k) M[k] = a.hM[k];
         jacobi_eigen<9>(M, ev, V);
         for (int k = 0; k < 9; ++k) H[k] = V[9 * k + 8];
     }
@@ -701,13 +734,17 @@ void launch_pose_2d2d(const GeoArgs& a, hipStream_t stream, Timing* timing) {
         e_hyp_kernel<<<(a.e_iters + 63) / 64, 64, 0, stream>>>(a);
         score_kernel<true><<<a.e_iters, 256, 0, stream>>>(a);
         scan_kernel<true><<<1, 256, 0, stream>>>(a);
-        recover_pose_kernel<<<1, 256, 0, stream>>>(a);
+        recover_setup_kernel<<<1, 64, 0, stream>>>(a);
+        recover_count_kernel<<<(4 * a.cap + 255) / 256, 256, 0, stream>>>(a);
+        recover_pick_kernel<<<1, 64, 0, stream>>>(a);
     }
     if (a.h_iters > 0) {
         h_hyp_kernel<<<(a.h_iters + 63) / 64, 64, 0, stream>>>(a);
         score_kernel<false><<<a.h_iters, 256, 0, stream>>>(a);
         scan_kernel<false><<<1, 256, 0, stream>>>(a);
-        h_refine_decompose_kernel<<<1, 256, 0, stream>>>(a);
+        h_moment_leaves_kernel<<<(a.cap + 255) / 256, 256, 0, stream>>>(a);
+        h_moment_sums_kernel<<<45, 256, 0, stream>>>(a);
+        h_refine_decompose_kernel<<<1, 64, 0, stream>>>(a);
     }
     const int total = 5 * a.cap;
     select_points_kernel<<<(total + 255) / 256, 256, 0, stream>>>(a);

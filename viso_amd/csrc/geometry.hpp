@@ -61,6 +61,14 @@ struct GeoArgs {
     double* sel_pts;   // kMaxCandidates x cap x 3
     uint8_t* inliers;  // cap (best motion's inlier flags)
     double* points_out;  // cap x 3 (normalised inlier points, compacted)
+    // recoverPose: the two rotations and t of E's decomposition (2 x 9 + 3)
+    // and the four motions' cheirality counts
+    double* rp = nullptr;
+    int* rp_good = nullptr;
+    // homography refinement: the 45 upper-triangle moment leaves per point
+    // ([45][cap]) and their canonical tree sums (9 x 9, symmetric)
+    double* hm = nullptr;
+    double* hM = nullptr;
 };
 
 void launch_pose_2d2d(const GeoArgs& a, hipStream_t stream, Timing* timing);

@@ -69,19 +69,26 @@ __device__ inline void null_vector_jacobi(const double* Ain, double* v_out) {
 
 template <int N>
 __device__ inline void jacobi_eigen(const double* Ain, double* evals, double* evecs) {
+    // every index below is a compile-time constant (all loops unrolled but
+    // the sweeps), so A and V live in registers instead of scratch
     double A[N * N], V[N * N];
+#pragma unroll
     for (int i = 0; i < N * N; ++i) {
         A[i] = Ain[i];
         V[i] = (i % (N + 1) == 0) ? 1.0 : 0.0;
     }
     for (int sweep = 0; sweep < 50; ++sweep) {
         double off = 0, diag = 0;
+#pragma unroll
         for (int p = 0; p < N; ++p) {
             diag = diag + A[N * p + p] * A[N * p + p];
+#pragma unroll
             for (int q = p + 1; q < N; ++q) off = off + A[N * p + q] * A[N * p + q];
         }
         if (off <= 1e-30 * diag || off == 0.0) break;
+#pragma unroll
         for (int p = 0; p < N - 1; ++p)
+#pragma unroll
             for (int q = p + 1; q < N; ++q) {
                 const double apq = A[N * p + q];
                 if (apq == 0.0) continue;
@@ -89,16 +96,19 @@ __device__ inline void jacobi_eigen(const double* Ain, double* evals, double* ev
                 const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
                 const double c = 1.0 / sqrt(t * t + 1.0);
                 const double s = t * c;
+#pragma unroll
                 for (int k = 0; k < N; ++k) {
                     const double akp = A[N * k + p], akq = A[N * k + q];
                     A[N * k + p] = c * akp - s * akq;
                     A[N * k + q] = s * akp + c * akq;
                 }
+#pragma unroll
                 for (int k = 0; k < N; ++k) {
                     const double apk = A[N * p + k], aqk = A[N * q + k];
                     A[N * p + k] = c * apk - s * aqk;
                     A[N * q + k] = s * apk + c * aqk;
                 }
+#pragma unroll
                 for (int k = 0; k < N; ++k) {
                     const double vkp = V[N * k + p], vkq = V[N * k + q];
                     V[N * k + p] = c * vkp - s * vkq;
@@ -106,19 +116,40 @@ __device__ inline void jacobi_eigen(const double* Ain, double* evals, double* ev
                 }
             }
     }
-    int idx[N];
-    for (int i = 0; i < N; ++i) idx[i] = i;
+    // descending eigenvalues, the first maximum first (a selection sort of
+    // the diagonal with the columns of V carried along by predicated swaps)
+    double d[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) d[i] = A[N * i + i];
+#pragma unroll
     for (int i = 0; i < N; ++i) {
         int m = i;
+        double dm = d[i];
+#pragma unroll
         for (int j = i + 1; j < N; ++j)
-            if (A[N * idx[j] + idx[j]] > A[N * idx[m] + idx[m]]) m = j;
-        const int tmp = idx[i];
-        idx[i] = idx[m];
-        idx[m] = tmp;
+            if (d[j] > dm) {
+                m = j;
+                dm = d[j];
+            }
+#pragma unroll
+        for (int j = i + 1; j < N; ++j)
+            if (j == m) {
+                const double td = d[i];
+                d[i] = d[j];
+                d[j] = td;
+#pragma unroll
+                for (int r = 0; r < N; ++r) {
+                    const double tv = V[N * r + i];
+                    V[N * r + i] = V[N * r + j];
+                    V[N * r + j] = tv;
+                }
+            }
     }
+#pragma unroll
     for (int j = 0; j < N; ++j) {
-        evals[j] = A[N * idx[j] + idx[j]];
-        for (int i = 0; i < N; ++i) evecs[N * i + j] = V[N * i + idx[j]];
+        evals[j] = d[j];
+#pragma unroll
+        for (int i = 0; i < N; ++i) evecs[N * i + j] = V[N * i + j];
     }
 }
 
