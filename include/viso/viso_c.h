@@ -237,6 +237,22 @@ int viso_set_stereo(viso_ctx* ctx, double baseline, int32_t max_disp, int32_t mi
  * reference's frozen map. */
 int viso_set_keyframes(viso_ctx* ctx, int32_t interval, int32_t ngood_permille);
 
+/* Photometric bundle adjustment (the repo's own spec of the BA that
+ * include/bundle_adjuster.h:22-106 sketches with g2o, SURVEY.md §8(f) row 4;
+ * oracle/oracle_ba.cpp): after every stereo keyframe insertion, `iterations`
+ * Levenberg-Marquardt steps refine every keyframe pose but the first and
+ * every map point over 16-residual 4x4 patch edges (each point against every
+ * keyframe but its host), points marginalised (Schur complement).
+ * 0 = off (default). */
+int viso_set_bundle_adjust(viso_ctx* ctx, int32_t iterations);
+/* Stage entry (parity tests): the same BA on host data.  kf_images: n_kf
+ * (2..8) level-0 images of the context's size; kf_poses: n_kf x 12 (in/out;
+ * keyframe 0 fixed); points: n x 3 world (in/out); host: n keyframe indices;
+ * report (may be NULL): iterations x 4 (cost, candidate cost, damping,
+ * accepted).  src: bundle_adjuster.h:58-100 (EdgeDirectProjection). */
+int viso_photometric_ba(viso_ctx* ctx, const uint8_t* const* kf_images, int32_t n_kf, double* kf_poses,
+                        double* points, const int32_t* host, int32_t n, int32_t iterations, double* report);
+
 /* Library build/version string (e.g. "viso_amd 0.1 gfx950"). */
 const char* viso_version(void);
 

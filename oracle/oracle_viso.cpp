@@ -82,6 +82,10 @@ struct oracle_viso {
     // maintenance)
     int kf_interval = 0, kf_permille = 0;
     long long track_cnt = 0;
+    // photometric BA after every keyframe insertion (viso_set_bundle_adjust;
+    // oracle_ba.cpp): LM iterations (0 = off) and each point's host keyframe
+    int ba_iterations = 0;
+    std::vector<int32_t> point_host;
 };
 
 extern "C" {
@@ -141,6 +145,7 @@ bool stereo_init(oracle_viso* v, const FramePtr& cur, const uint8_t* right) {
     v->keyframes.clear();
     v->keyframes.push_back(cur);
     v->points.assign(pts.begin(), pts.begin() + 3 * (size_t)m);
+    v->point_host.assign((size_t)m, 0);
     v->state = v->p.enable_tracking ? 1 : 2;
     v->stats[3] = -2;  // stereo initialisation
     v->stats[12] = 1;
@@ -217,6 +222,7 @@ void on_new(oracle_viso* v, const uint8_t* img, const uint8_t* right) {
                     for (int i = 0; i < m; ++i)
                         if (v->success[(size_t)i])
                             for (int k = 0; k < 3; ++k) v->points.push_back(pts[(size_t)3 * i + k]);
+                    v->point_host.assign(v->points.size() / 3, 0);  // in keyframe 0's (ref) frame
                     v->state = v->p.enable_tracking ? 1 : 2;  // kRunning : kFinished (src/viso.cpp:97)
                     v->stats[12] = 1;
                     break;
@@ -303,7 +309,27 @@ void on_new(oracle_viso* v, const uint8_t* img, const uint8_t* right) {
                         v->points.push_back((R[k] * d0 + R[3 + k] * d1) + R[6 + k] * d2);
                 }
                 v->keyframes.push_back(cur);
+                v->point_host.resize(v->points.size() / 3, (int32_t)v->keyframes.size() - 1);
                 v->stats[14] = m;
+                if (v->ba_iterations > 0) {
+                    // photometric BA over every keyframe and the map
+                    // (oracle_ba.cpp); the refined poses stay on the keyframes
+                    // (the current frame's is the next frame's `last` pose)
+                    const int nk = (int)v->keyframes.size();
+                    std::vector<const uint8_t*> imgs((size_t)nk);
+                    std::vector<double> kp((size_t)12 * nk);
+                    for (int j = 0; j < nk; ++j) {
+                        imgs[(size_t)j] = v->keyframes[(size_t)j]->pyr.data();
+                        std::memcpy(&kp[(size_t)12 * j], v->keyframes[(size_t)j]->pose(), 12 * sizeof(double));
+                    }
+                    oracle_photometric_ba(imgs.data(), nk, w, h, v->K4, kp.data(), v->points.data(),
+                                          v->point_host.data(), (int)(v->points.size() / 3), v->ba_iterations,
+                                          nullptr);
+                    for (int j = 1; j < nk; ++j) {
+                        std::memcpy(v->keyframes[(size_t)j]->R, &kp[(size_t)12 * j], 9 * sizeof(double));
+                        std::memcpy(v->keyframes[(size_t)j]->T, &kp[(size_t)12 * j + 9], 3 * sizeof(double));
+                    }
+                }
             }
             v->stats[15] = (double)v->keyframes.size();
             break;
@@ -324,6 +350,8 @@ void oracle_viso_on_new_frame(oracle_viso* v, const uint8_t* img) { on_new(v, im
 void oracle_viso_on_new_stereo(oracle_viso* v, const uint8_t* left, const uint8_t* right) {
     on_new(v, left, right);
 }
+
+void oracle_viso_set_bundle_adjust(oracle_viso* v, int iterations) { v->ba_iterations = iterations; }
 
 void oracle_viso_set_keyframes(oracle_viso* v, int interval, int ngood_permille) {
     v->kf_interval = interval;

@@ -185,6 +185,10 @@ void oracle_viso_on_new_stereo(oracle_viso* v, const uint8_t* left, const uint8_
 // R^T (Pc - T)) are appended to the map and the frame becomes a keyframe (at
 // most 8 keyframes, 16384 points).  interval 0 = off (default).
 void oracle_viso_set_keyframes(oracle_viso* v, int interval, int ngood_permille);
+// Photometric BA (oracle_photometric_ba) over every keyframe and the map after
+// each keyframe insertion, `iterations` LM iterations (0 = off, default); the
+// refined keyframe poses replace the keyframes' (keyframe 0 fixed).
+void oracle_viso_set_bundle_adjust(oracle_viso* v, int iterations);
 int oracle_viso_state(const oracle_viso* v);
 int oracle_viso_num_poses(const oracle_viso* v);
 void oracle_viso_poses(const oracle_viso* v, double* out12);
@@ -225,6 +229,14 @@ int oracle_rig_num_points(const oracle_rig* r, int cam);
 void oracle_rig_points(const oracle_rig* r, int cam, double* out3);
 // [4 levels][50]: nGood, cost / nGood, H (36), b (6), update (6) of the last step
 void oracle_rig_level_stats(const oracle_rig* r, double* out200);
+
+// ---------------------------------------------------------------- photometric BA
+// The repo's own spec of include/bundle_adjuster.h:22-106 (oracle_ba.cpp
+// header): keyframe poses (keyframe 0 fixed) and map points, 16-residual 4x4
+// patch edges point -> every non-host keyframe, Levenberg-Marquardt with the
+// points marginalised.  Returns the number of active edges.
+int oracle_photometric_ba(const uint8_t* const* kf_img, int n_kf, int w, int h, const double K[4], double* kf_poses,
+                          double* points, const int32_t* host, int n, int iterations, double* report);
 
 #ifdef __cplusplus
 }

@@ -45,6 +45,8 @@ SIG = {
     "oracle_recover_pose": ([_vp, _vp, _vp, _i, _vp, _vp, _vp], _i),
     "oracle_default_params": ([_vp, _d, _d, _d, _d, _i, _i], None),
     "oracle_viso_create": ([_vp], _vp),
+    "oracle_photometric_ba": ([_vp, _i, _i, _i, _vp, _vp, _vp, _vp, _i, _i, _vp], _i),
+    "oracle_viso_set_bundle_adjust": ([_vp, _i], None),
     "oracle_rig_compose": ([_vp, _vp, _vp], None),
     "oracle_rig_adjoint": ([_vp, _vp], None),
     "oracle_rig_direct": ([_i, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp], None),
@@ -312,6 +314,9 @@ class Viso:
 
     def set_keyframes(self, interval, ngood_permille=500):
         self.lib.oracle_viso_set_keyframes(self.v, int(interval), int(ngood_permille))
+
+    def set_bundle_adjust(self, iterations):
+        self.lib.oracle_viso_set_bundle_adjust(self.v, int(iterations))
 
     def on_new_stereo(self, left, right):
         left = np.ascontiguousarray(left, np.uint8)
@@ -665,3 +670,20 @@ def rig_direct(last_pyrs, cur_pyrs, w, h, K, points, E, cam_last, pose_seed):
     load().oracle_rig_direct(n, P(*[ptr(x) for x in lp]), P(*[ptr(x) for x in cp]), w, h, ptr(k),
                              P(*[ptr(x) for x in pts]), ptr(npts), ptr(E), ptr(cl), ptr(pose), ptr(stats))
     return pose, stats
+
+
+# ----------------------------------------------------------------- photometric BA
+def photometric_ba(kf_imgs, kf_poses, points, host, K, iterations=5):
+    """oracle/oracle_ba.cpp: returns (poses (k, 12), points (n, 3), report
+    (iterations, 4): cost, candidate cost, mu, accepted; active edges)."""
+    imgs = [np.ascontiguousarray(x, np.uint8) for x in kf_imgs]
+    h, w = imgs[0].shape
+    P = ctypes.c_void_p * len(imgs)
+    poses = np.ascontiguousarray(kf_poses, np.float64).reshape(-1, 12).copy()
+    pts = np.ascontiguousarray(points, np.float64).reshape(-1, 3).copy()
+    hst = np.ascontiguousarray(host, np.int32)
+    rep = np.zeros((max(iterations, 1), 4))
+    k = np.asarray(K, np.float64)
+    na = load().oracle_photometric_ba(P(*[ptr(x) for x in imgs]), len(imgs), w, h, ptr(k), ptr(poses), ptr(pts),
+                                      ptr(hst), len(pts), iterations, ptr(rep))
+    return poses, pts, rep[:iterations], na

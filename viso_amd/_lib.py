@@ -78,6 +78,8 @@ SIGNATURES = {
     "viso_stereo_match": [_vp, _vp, _vp, _i32, _i32, _vp, _vp, _i32, _i32, _vp, _vp],
     "viso_set_stereo": [_vp, _d, _i32, _i32],
     "viso_set_keyframes": [_vp, _i32, _i32],
+    "viso_set_bundle_adjust": [_vp, _i32],
+    "viso_photometric_ba": [_vp, _vp, _i32, _vp, _vp, _vp, _i32, _i32, _vp],
     "viso_version": [],
     # north-star stereo VO (include/viso/viso_svo.h)
     "viso_svo_default_params": [_vp, _i32, _i32, _d, _d, _d, _d, _d],

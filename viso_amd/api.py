@@ -165,6 +165,20 @@ class Context:
         return d, s
 
     # ------------------------------------------------------------ timing
+    def photometric_ba(self, kf_images, kf_poses, points, host, iterations: int = 5):
+        """viso_photometric_ba: the BA of include/bundle_adjuster.h:22-106 on
+        host data; returns (poses (k, 12), points (n, 3), report
+        (iterations, 4): cost, candidate cost, damping, accepted)."""
+        imgs = [np.ascontiguousarray(x, np.uint8) for x in kf_images]
+        P = ctypes.c_void_p * len(imgs)
+        poses = np.ascontiguousarray(kf_poses, np.float64).reshape(-1, 12).copy()
+        pts = np.ascontiguousarray(points, np.float64).reshape(-1, 3).copy()
+        hst = np.ascontiguousarray(host, np.int32)
+        rep = np.zeros((iterations, 4))
+        _lib.call("viso_photometric_ba", self.h, P(*[x.ctypes.data for x in imgs]), len(imgs), _p(poses), _p(pts),
+                  _p(hst), len(pts), iterations, _p(rep))
+        return poses, pts, rep
+
     def timing_enable(self, on: bool = True):
         _lib.call("viso_timing_enable", self.h, 1 if on else 0)
 

@@ -366,6 +366,51 @@ extern "C" int viso_set_keyframes(viso_ctx* c, int32_t interval, int32_t ngood_p
     return VISO_OK;
 }
 
+extern "C" int viso_set_bundle_adjust(viso_ctx* c, int32_t iterations) {
+    if (!c || iterations < 0 || iterations > 100) return VISO_ERR_ARG;
+    c->ba_iterations = iterations;
+    return VISO_OK;
+}
+
+extern "C" int viso_photometric_ba(viso_ctx* c, const uint8_t* const* kf_images, int32_t n_kf, double* kf_poses,
+                                   double* points, const int32_t* host, int32_t n, int32_t iterations,
+                                   double* report) {
+    if (!c || !kf_images || !kf_poses || !points || !host) return VISO_ERR_ARG;
+    if (n_kf < 2 || n_kf > kMaxKeyframes || n < 1 || iterations < 1 || iterations > 100) return VISO_ERR_ARG;
+    for (int i = 0; i < n; ++i)
+        if (host[i] < 0 || host[i] >= n_kf) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipSetDevice(c->device));
+    const int w = c->p.width, h = c->p.height;
+    const size_t npx = (size_t)w * h;
+    Bump b;
+    const size_t o_img = b.take(npx * n_kf), o_pose = b.take(96 * (size_t)n_kf), o_pts = b.take(24 * (size_t)n),
+                 o_host = b.take(4 * (size_t)n), o_rep = b.take(32 * (size_t)iterations);
+    int rc = c->scratch_a.ensure(b.off);
+    if (!rc) rc = c->ba_scratch.ensure(ba_scratch_bytes(n));
+    if (rc) return rc;
+    char* base = (char*)c->scratch_a.ptr;
+    const uint8_t* l0[kMaxKeyframes];
+    for (int k = 0; k < n_kf; ++k) {
+        VISO_HIP_CHECK(hipMemcpyAsync(base + o_img + npx * k, kf_images[k], npx, hipMemcpyHostToDevice, c->stream));
+        l0[k] = (const uint8_t*)(base + o_img + npx * k);
+    }
+    VISO_HIP_CHECK(hipMemcpyAsync(base + o_pose, kf_poses, 96 * (size_t)n_kf, hipMemcpyHostToDevice, c->stream));
+    VISO_HIP_CHECK(hipMemcpyAsync(base + o_pts, points, 24 * (size_t)n, hipMemcpyHostToDevice, c->stream));
+    VISO_HIP_CHECK(hipMemcpyAsync(base + o_host, host, 4 * (size_t)n, hipMemcpyHostToDevice, c->stream));
+    const double K[4] = {c->p.fx, c->p.fy, c->p.cx, c->p.cy};
+    if (launch_photometric_ba(l0, n_kf, w, h, K, (double*)(base + o_pose), (double*)(base + o_pts),
+                              (const int*)(base + o_host), n, iterations, c->ba_scratch.ptr,
+                              (double*)(base + o_rep), c->stream))
+        return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipGetLastError());
+    VISO_HIP_CHECK(hipMemcpyAsync(kf_poses, base + o_pose, 96 * (size_t)n_kf, hipMemcpyDeviceToHost, c->stream));
+    VISO_HIP_CHECK(hipMemcpyAsync(points, base + o_pts, 24 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    if (report)
+        VISO_HIP_CHECK(hipMemcpyAsync(report, base + o_rep, 32 * (size_t)iterations, hipMemcpyDeviceToHost, c->stream));
+    VISO_HIP_CHECK(hipStreamSynchronize(c->stream));
+    return VISO_OK;
+}
+
 extern "C" int viso_stereo_match(viso_ctx* c, const uint8_t* left, const uint8_t* right,
                                  int32_t width, int32_t height, const int32_t* xs,
                                  const int32_t* ys, int32_t n, int32_t max_disp,

@@ -196,6 +196,13 @@ struct viso_ctx {
     // kf_permille / 1000 of the map
     int kf_interval = 0, kf_permille = 0;
     int64_t track_cnt = 0;
+    // photometric BA after each keyframe insertion (viso_set_bundle_adjust;
+    // ba.hip): LM iterations (0 = off) and each map point's host keyframe
+    int ba_iterations = 0;
+    std::vector<int32_t> point_host;
+    viso::DevBuf point_host_dev, ba_scratch;
+    int sync_point_hosts(int first);
+    int bundle_adjust();
     int stereo_points_into(int cur, double* out, int cap, int* kept);
     int insert_keyframe(int cur);
 

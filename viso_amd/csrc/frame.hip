@@ -394,6 +394,34 @@ int viso_ctx::stereo_points_into(int cur, double* out, int cap, int* kept) {
     return VISO_OK;
 }
 
+// Photometric BA over every keyframe and the map (ba.hip; oracle_viso.cpp's
+// insertion branch): keyframe poses and points refined in place on the
+// context stream; the refined poses go back to the keyframes' frames (the
+// current frame's is the next frame's `last` pose and seed).
+int viso_ctx::bundle_adjust() {
+    const int nk = (int)kf_slots.size();
+    if (nk < 2 || n_map < 1) return VISO_OK;
+    int rc = point_host_dev.ensure(4 * (size_t)kMaxMapPoints);
+    if (!rc) rc = ba_scratch.ensure(ba_scratch_bytes(kMaxMapPoints));
+    if (rc) return rc;
+    VISO_HIP_CHECK(hipMemcpyAsync(point_host_dev.ptr, point_host.data(), 4 * (size_t)n_map, hipMemcpyHostToDevice,
+                                  stream));
+    const uint8_t* l0[kMaxKeyframes];
+    for (int k = 0; k < nk; ++k) l0[k] = frame(kf_slots[(size_t)k]).l[0];
+    const double K[4] = {p.fx, p.fy, p.cx, p.cy};
+    if (launch_photometric_ba(l0, nk, geom.w[0], geom.h[0], K, (double*)kf_poses.ptr, (double*)map_pts.ptr,
+                              (const int*)point_host_dev.ptr, n_map, ba_iterations, ba_scratch.ptr, nullptr,
+                              stream))
+        return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipGetLastError());
+    for (int k = 1; k < nk; ++k)
+        VISO_HIP_CHECK(hipMemcpyAsync(pose_of(kf_slots[(size_t)k]), (char*)kf_poses.ptr + 96 * k, 96,
+                                      hipMemcpyDeviceToDevice, stream));
+    // the host array must outlive the async upload
+    VISO_HIP_CHECK(hipStreamSynchronize(stream));
+    return VISO_OK;
+}
+
 // Stereo keyframe insertion (oracle_viso.cpp, the kRunning case): the frame's
 // pose is final (resolve_direct) and every earlier tracking frame's LK
 // alignment has been launched against the old map (flush_lk); then its
@@ -415,6 +443,11 @@ int viso_ctx::insert_keyframe(int cur) {
     hold(cur);
     VISO_HIP_CHECK(hipMemcpyAsync((char*)kf_poses.ptr + 96 * (kf_slots.size() - 1), pose_of(cur), 96,
                                   hipMemcpyDeviceToDevice, stream));
+    point_host.resize((size_t)n_map, (int32_t)kf_slots.size() - 1);
+    if (ba_iterations > 0) {
+        rc = bundle_adjust();
+        if (rc) return rc;
+    }
     rc = build_lk_templates();
     if (rc) return rc;
     stats[14] = m;
@@ -438,6 +471,7 @@ int viso_ctx::stereo_init(int cur, bool* made) {
     kf_slots.push_back(cur);
     hold(cur);
     n_map = std::min(m, kMaxMapPoints);
+    point_host.assign((size_t)n_map, 0);
     VISO_HIP_CHECK(hipMemcpyAsync(kf_poses.ptr, pose_of(cur), 96, hipMemcpyDeviceToDevice, stream));
     rc = build_lk_templates();
     if (rc) return rc;
@@ -526,6 +560,7 @@ int viso_ctx::on_new_frame(int cur) {
                     std::memcpy(pose + 9, initT, sizeof(initT));
                     launch_set_pose(pose_of(cur), pose, stream);
                     n_map = std::min(nr_inliers, kMaxMapPoints);
+                    point_host.assign((size_t)n_map, 0);  // in keyframe 0's (ref) frame
                     VISO_HIP_CHECK(hipMemcpyAsync(map_pts.ptr, geo.points_out, 24 * (size_t)n_map,
                                                   hipMemcpyDeviceToDevice, stream));
                     for (size_t j = 0; j < kf_slots.size(); ++j)

@@ -164,6 +164,19 @@ size_t rig_scratch_bytes();
 int launch_rig_direct(const RigCamDev* cams, int n_cams, const PyrGeom& g, const double K[4], double* state,
                       const double* seed12, double* stats, double* pose_out, double* log, int log_index,
                       double* cam_last, hipStream_t stream, int precision);
+// ---------------------------------------------------------------- photometric BA
+// The BA include/bundle_adjuster.h:22-106 sketches (SURVEY.md §8(f) row 4;
+// spec oracle/oracle_ba.cpp): keyframe poses (n_kf x 12 device, keyframe 0
+// fixed) and map points (n x 3 device) refined in place by `iterations`
+// Levenberg-Marquardt steps over 16-residual 4x4 patch edges point -> every
+// non-host keyframe (host: n device ints).  kf_l0: the keyframes' level-0
+// images (device).  report (device, may be null): [iterations][4] cost,
+// candidate cost, mu, accepted.  scratch: ba_scratch_bytes(n).  Returns -1
+// on bad sizes.
+size_t ba_scratch_bytes(int n);
+int launch_photometric_ba(const uint8_t* const* kf_l0, int n_kf, int w, int h, const double K[4], double* poses,
+                          double* pts, const int* host, int n, int iterations, void* scratch, double* report,
+                          hipStream_t stream);
 // dst (12 doubles, device) <- src (host values, passed by value)
 void launch_set_pose(double* dst, const double src[12], hipStream_t stream);
 

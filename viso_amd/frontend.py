@@ -108,6 +108,12 @@ class Viso(FrameHandler):
         the map adds its stereo points and becomes a keyframe."""
         _lib.call("viso_set_keyframes", self.ctx.h, int(interval), int(ngood_permille))
 
+    def set_bundle_adjust(self, iterations: int) -> None:
+        """Photometric BA (viso_set_bundle_adjust) after every keyframe
+        insertion: `iterations` Levenberg-Marquardt steps over the keyframe
+        poses and map points (0 = off)."""
+        _lib.call("viso_set_bundle_adjust", self.ctx.h, int(iterations))
+
     def process_device(self, d_left: int, d_right: int | None, n: int, frame_stride: int):
         """Batched ingest of n frames resident in HBM (device pointers)."""
         _lib.call("viso_process_frames_device", self.ctx.h, d_left, d_right, n, frame_stride)
