@@ -570,11 +570,11 @@ def pyramid_traffic(W, H, imgs_per_launch):
 
 def pmc_evidence(W, H, breakdown, stereo_vo):
     """The north star's two other rocprof figures, from the committed PMC passes
-    (tools/gpu_pmc.sh -> tools/pmc_kernels.py -> profiles/r01_gn_svo_pmc.json),
+    (tools/gpu_pmc.sh -> tools/pmc_kernels.py -> profiles/r02_gn_svo_pmc.json),
     profiled at 1242x375 only: occupancy of the GN reduction (direct_level_kernel)
     and HBM traffic of the matching pass (svo_circle_kernel).  Live durations
     come from this run's HIP events where the bench has them."""
-    f = os.path.join(ROOT, "profiles", "r01_gn_svo_pmc.json")
+    f = os.path.join(ROOT, "profiles", "r02_gn_svo_pmc.json")
     if (W, H) != (1242, 375) or not os.path.exists(f):
         return None, None
     with open(f) as fh:
@@ -596,7 +596,7 @@ def pmc_evidence(W, H, breakdown, stereo_vo):
               "fp64_flop_per_launch": flop,
               "fp64_tflops": round(flop / (live_us * 1e-6) / 1e12, 2) if flop else None,
               "fp64_peak_tflops": d.get("fp64_peak_tflops"),
-              "source": "profiles/r01_gn_svo_pmc.json (SQ_WAVES, SQ_WAVE_CYCLES, SQ_ACTIVE_INST_VALU, "
+              "source": "profiles/r02_gn_svo_pmc.json (SQ_WAVES, SQ_WAVE_CYCLES, SQ_ACTIVE_INST_VALU, "
                         "SQ_INSTS_VALU_*_F64)"}
     mp = None
     c = t.get("svo", {}).get("svo_circle_kernel")
@@ -608,7 +608,7 @@ def pmc_evidence(W, H, breakdown, stereo_vo):
               "achieved_GBps": round(gbs, 1), "peak_GBps": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4),
               "bound": "latency / VALU (four dependent best-SAD searches per feature over a cache-resident "
                        "descriptor set), not HBM",
-              "source": "profiles/r01_gn_svo_pmc.json (FETCH_SIZE x2 + WRITE_SIZE)"}
+              "source": "profiles/r02_gn_svo_pmc.json (FETCH_SIZE x2 + WRITE_SIZE)"}
     return gn, mp
 
 

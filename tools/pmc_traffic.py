@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes for the image pass.
 
-Usage: tools/pmc_traffic.py FETCH_DIR WRITE_DIR [OUT_JSON]
+Usage: [IMAGES=n SOURCE=...] tools/pmc_traffic.py FETCH_DIR WRITE_DIR [OUT_JSON]
+(OUT_JSON is a table of entries keyed by frame size and images per launch,
+profiles/pyramid_traffic.json for bench.py)
 
 Each directory holds a run_counter_collection.csv of one `rocprofv3 --pmc`
 pass over `bench.py`.  MI355X_MICROARCH.md §HBM: FETCH_SIZE (KB) reports half
@@ -63,17 +65,27 @@ def main():
     scale = float(os.environ.get("FETCH_SCALE", "2"))
     fetch = scale * 1024 * sum(fc) / len(fc)
     write = 1024.0 * sum(wc) / len(wc)
+    imgs = int(os.environ.get("IMAGES", "100"))
     res = {"width": int(os.environ.get("WIDTH", "1242")), "height": int(os.environ.get("HEIGHT", "375")),
-           "images_per_launch": 100,
+           "images_per_launch": imgs, "source": os.environ.get("SOURCE", fdir),
            "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
            "traffic_bytes_per_launch": fetch + write, "chunks": len(fc),
            "fetch_scale": scale,
            "note": "FETCH_SIZE x fetch_scale + WRITE_SIZE (KB -> bytes) summed over the three "
-                   "pyrDown launches of one 100-image chunk (tools/pmc_traffic.py)",
+                   f"pyrDown launches of one {imgs}-image chunk (tools/pmc_traffic.py)",
            "raw_fetch_kb_per_level": per_level(f, fg), "raw_write_kb_per_level": per_level(w, wg)}
     print(json.dumps(res, indent=1))
     if out:
-        json.dump(res, open(out, "w"), indent=1)
+        # a table of entries (bench.py pyramid_traffic looks up its own size
+        # and chunk): replace the entry of this size / chunk, keep the others
+        table = {"entries": []}
+        if os.path.exists(out):
+            old = json.load(open(out))
+            table = old if "entries" in old else table
+        table["entries"] = [e for e in table["entries"]
+                            if (e["width"], e["height"], e["images_per_launch"]) !=
+                            (res["width"], res["height"], res["images_per_launch"])] + [res]
+        json.dump(table, open(out, "w"), indent=1)
 
 
 if __name__ == "__main__":
