@@ -498,16 +498,24 @@ __device__ inline int sobel_q(const uint8_t* I, int w, int x, int y, bool du) {
     return (d >> 3) + 128;
 }
 
-// 16 lanes per feature (lane j: sample offset j): the 32-byte descriptor;
-// grid (blocks per image, images), grid-stride over the image's features
+// 16 lanes per feature (lane j: sample offset j): the 32-byte descriptor.
+// kDescWg workgroups per image, grid-stride over its features; the 1-D grid
+// is dealt so that all of an image's workgroups share one XCD (blocks are
+// dealt round-robin over the 8 XCDs: block b runs on XCD b % 8; speed only):
+// every image row is then fetched into one L2, not into all eight.
+constexpr int kDescWg = 16;
+
 __global__ __launch_bounds__(256) void svo_describe_kernel(ImgSrc src, SvoDev p,
                                                            const FeatDev* __restrict__ sets, int ring,
-                                                           int pair0) {
-    const uint8_t* __restrict__ img = src.at(blockIdx.y, p.ncam);
-    const FeatDev F = set_of(sets, ring, p.ncam, pair0, blockIdx.y);
+                                                           int pair0, int n_img) {
+    const int xcd = blockIdx.x & 7, q = blockIdx.x >> 3;
+    const int wg = q % kDescWg, image = 8 * (q / kDescWg) + xcd;
+    if (image >= n_img) return;
+    const uint8_t* __restrict__ img = src.at(image, p.ncam);
+    const FeatDev F = set_of(sets, ring, p.ncam, pair0, image);
     const int n = *F.n;
     const int j = threadIdx.x & 15;
-    for (int o = blockIdx.x * 16 + (threadIdx.x >> 4); o < n; o += gridDim.x * 16) {
+    for (int o = wg * 16 + (threadIdx.x >> 4); o < n; o += kDescWg * 16) {
         const int sx = F.u[o] + c_p16[j][0], sy = F.v[o] + c_p16[j][1];
         const uint8_t du = (uint8_t)sobel_q(img, p.w, sx, sy, true), dv = (uint8_t)sobel_q(img, p.w, sx, sy, false);
         const size_t bp = (size_t)F.bpos[o] * kDesc;
@@ -1648,7 +1656,7 @@ struct viso_svo {
         const bool dom = p.margin < p.nms_n + 2;
         launch_detect(p.nms_n, dom, g, stream, imgs, d, d_sets, ring, pair0, seg_cap);
         svo_scan_kernel<<<ni, 1024, 0, stream>>>(d, d_sets, ring, pair0, 4 * tiles, seg_cap);
-        svo_describe_kernel<<<dim3(16, ni), 256, 0, stream>>>(imgs, d, d_sets, ring, pair0);
+        svo_describe_kernel<<<8 * kDescWg * ((ni + 7) / 8), 256, 0, stream>>>(imgs, d, d_sets, ring, pair0, ni);
         if (timed) {
             VISO_HIP_CHECK(hipEventRecord(tev[2 * tev_n + 1], stream));
             ++tev_n;
