@@ -423,13 +423,14 @@ def main():
     roofline = None
     if "pyramid" in timing:
         # one timed region = the image pass of one ingest chunk (the chunk's
-        # left images; no stage reads a right pyramid): the pyr_down launches
-        # back to back on the context stream
+        # left images; no stage reads a right pyramid): the level-1 launch and
+        # the levels 2-3 tail launch back to back on the context stream
         imgs_per_launch = steps / timing["pyramid"]["launches"]
         bytes_per_launch = algo_bytes_img * imgs_per_launch
         achieved = bytes_per_launch / (timing["pyramid"]["avg_ms"] * 1e-3) / 1e9
         traffic, tsrc = pyramid_traffic(W, H, imgs_per_launch)
-        roofline = {"kernel": "pyr_down image pass of one ingest chunk (algorithmic bytes = "
+        roofline = {"kernel": "image pass of one ingest chunk: pyr_down_sk (level 1) + pyr_tail (levels 2-3) "
+                              "(algorithmic bytes = "
                               "L0 read + L1..L3 write per image)", "bound": "hbm",
                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

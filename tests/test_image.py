@@ -88,10 +88,14 @@ def test_fast_order_row_major():
 @pytest.mark.gpu
 # sizes: the bench frame, odd/even widths, strip edges of the 248-column
 # waves (dst widths 248k +- 1), levels under 8 columns (scalar form) and
-# between 8 and 16 (packed form with both borders in one strip)
+# between 8 and 16 (packed form with both borders in one strip).  Levels 2
+# and 3 of images at least 16 columns wide come from the tail launch (bands
+# of level-3 rows sized to the chunk: 3 images here, 11 and 133 in the
+# batched test); narrower images (15, 8 columns) take per-level launches.
 @pytest.mark.parametrize("h,w", [(375, 1242), (61, 97), (1080, 1920), (16, 16), (187, 621),
                                  (8, 8), (9, 17), (20, 15), (50, 497), (30, 993), (12, 994),
-                                 (9, 1001), (41, 2047), (33, 31), (18, 64)])
+                                 (9, 1001), (41, 2047), (33, 31), (18, 64),
+                                 (24, 4000), (67, 16), (300, 4096)])
 def test_gpu_pyramid_bitexact(h, w):
     from viso_amd import default_context
     ctx = default_context()
@@ -99,6 +103,20 @@ def test_gpu_pyramid_bitexact(h, w):
     got = ctx.pyramid(imgs)
     for i in range(3):
         assert np.array_equal(got[i], oracle_lib.pyramid(imgs[i]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,h,w", [(11, 375, 1242), (133, 61, 97)])
+def test_gpu_pyramid_batched(n, h, w):
+    """Chunks of >= 8 images deal the bands of an image to one XCD (the
+    tail launch's block -> (image, band) map, idle blocks past the last
+    image); more than kPyrBatch = 128 images split into launches."""
+    from viso_amd import default_context
+    ctx = default_context()
+    imgs = np.stack([images.mixed(h, w, seed=100 + s) for s in range(n)])
+    got = ctx.pyramid(imgs)
+    for i in range(n):
+        assert np.array_equal(got[i], oracle_lib.pyramid(imgs[i])), i
 
 
 @pytest.mark.gpu

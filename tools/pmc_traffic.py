@@ -8,14 +8,16 @@ profiles/pyramid_traffic.json for bench.py)
 Each directory holds a run_counter_collection.csv of one `rocprofv3 --pmc`
 pass over `bench.py`.  MI355X_MICROARCH.md §HBM: FETCH_SIZE (KB) reports half
 the bytes of 16-byte-per-lane streaming reads on gfx950; other widths are
-uncalibrated.  The pyrDown kernels read 8 bytes per lane.  The raw
+uncalibrated.  The level-1 kernel reads 8 bytes per lane, the tail kernel
+(levels 2-3) 16 bytes.  The raw
 FETCH_SIZE of the level-0 pass of a 100-image chunk is below the 46.6 MB of
 level 0 it must read at least once (round 1: 39.9 MB for the first streaming
 kernel), while the doubled value lies between that and the bytes of the
 128-byte lines its loads touch, so the same factor 2 is applied (FETCH_SCALE
 overrides; the per-launch raw values are printed for the check).  WRITE_SIZE (KB) is
 taken as is.  The per-chunk traffic of the image pass is the sum over its
-three launches, averaged over the full-size chunks.
+launches (LAUNCHES, default 2: level 1 + tail; 3 for the round-1 per-level
+form), averaged over the full-size chunks.
 """
 from __future__ import annotations
 
@@ -30,7 +32,8 @@ def per_dispatch(path, counter):
     vals = collections.defaultdict(float)
     grid = {}
     for r in csv.DictReader(open(os.path.join(path, "run_counter_collection.csv"))):
-        if "pyr_down_" not in r["Kernel_Name"] or r["Counter_Name"] != counter:
+        if ("pyr_down_" not in r["Kernel_Name"] and "pyr_tail_" not in r["Kernel_Name"]) or \
+                r["Counter_Name"] != counter:
             continue
         d = int(r["Dispatch_Id"])
         vals[d] += float(r["Counter_Value"])
@@ -38,10 +41,13 @@ def per_dispatch(path, counter):
     return vals, grid
 
 
+LAUNCHES = int(os.environ.get("LAUNCHES", "2"))
+
+
 def big_groups(vals, grid):
-    """Dispatch-id triples (L1, L2, L3 of one chunk) of the full-size chunks."""
+    """Dispatch-id groups (the launches of one chunk) of the full-size chunks."""
     ids = sorted(vals)
-    groups = [ids[i:i + 3] for i in range(0, len(ids) - len(ids) % 3, 3)]
+    groups = [ids[i:i + LAUNCHES] for i in range(0, len(ids) - len(ids) % LAUNCHES, LAUNCHES)]
     big = max(grid[g[0]][0] for g in groups)
     return [g for g in groups if grid[g[0]][0] == big]
 
@@ -49,7 +55,7 @@ def big_groups(vals, grid):
 def per_level(vals, grid):
     """Mean raw counter value (KB) per launch of each level over the full-size chunks."""
     gs = big_groups(vals, grid)
-    return [round(sum(vals[g[k]] for g in gs) / len(gs), 1) for k in range(3)]
+    return [round(sum(vals[g[k]] for g in gs) / len(gs), 1) for k in range(LAUNCHES)]
 
 
 def main():
@@ -71,9 +77,9 @@ def main():
            "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
            "traffic_bytes_per_launch": fetch + write, "chunks": len(fc),
            "fetch_scale": scale,
-           "note": "FETCH_SIZE x fetch_scale + WRITE_SIZE (KB -> bytes) summed over the three "
-                   f"pyrDown launches of one {imgs}-image chunk (tools/pmc_traffic.py)",
-           "raw_fetch_kb_per_level": per_level(f, fg), "raw_write_kb_per_level": per_level(w, wg)}
+           "note": f"FETCH_SIZE x fetch_scale + WRITE_SIZE (KB -> bytes) summed over the {LAUNCHES} "
+                   f"image-pass launches of one {imgs}-image chunk (tools/pmc_traffic.py)",
+           "raw_fetch_kb_per_launch": per_level(f, fg), "raw_write_kb_per_launch": per_level(w, wg)}
     print(json.dumps(res, indent=1))
     if out:
         # a table of entries (bench.py pyramid_traffic looks up its own size

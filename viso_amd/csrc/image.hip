@@ -2,11 +2,13 @@
 // and FAST-9/16 + NMS (cv::FAST restated).  Integer arithmetic, bit-exact
 // against the oracle (oracle/oracle_image.cpp).
 //
-// Pyramid: one launch per level, batched over every image of a chunk:
-// pyr_down_sk_kernel (register-only streaming bands, below) for source levels
-// at least 8 columns wide, pyr_down_stream_kernel (LDS-staged rows) for the
-// tiny levels of small images.  HBM-bound: algorithmic bytes per image =
-// level-0 read + levels 1..3 written.
+// Pyramid: two launches per chunk, batched over every image of it:
+// pyr_down_sk_kernel (register-only streaming bands) for level 1, then
+// pyr_tail_kernel (levels 2 and 3, one workgroup per band of an image, the
+// level-2 halo recomputed in LDS).  pyr_down_stream_kernel (LDS-staged rows)
+// covers the levels of images whose level 1 is under 8 columns.  HBM-bound:
+// algorithmic bytes per image = level-0 read + levels 1..3 written
+// (DESIGN.md §4).
 //
 // FAST: one workgroup per image row y.  It scores rows y-1, y, y+1 from a
 // 9-row LDS window, applies the strict 3x3 NMS to row y and appends the
@@ -20,8 +22,9 @@
 #include "kernels.hpp"
 
 #ifdef VISO_PROBE
-// wave timeline of the last level-1 pyrDown launch: start, end (s_memrealtime,
-// 100 MHz), HW_ID, XCC_ID per wave (dev instrumentation)
+// dev instrumentation: per-wave timeline of the last level-1 launch (start,
+// end, HW_ID, XCC_ID) and per-block timeline of the last tail launch
+// (start, phase ends, HW_ID | XCC_ID << 32); s_memrealtime, 100 MHz
 __device__ unsigned long long g_pyr_tl[8192][5];
 #endif
 
@@ -155,6 +158,20 @@ struct PkEdge {
     uint32_t sel0, sel1, sel2;
 };
 
+// horizontal sums for 4 destination columns from their 11 source taps
+// (bytes 0..10 of w0, w1, w2)
+__device__ inline void pk_hsum3(uint32_t w0, uint32_t w1, uint32_t w2, u16x2 (&h)[2]) {
+    constexpr uint32_t K = 0x04060401u;  // taps 0..3 of [1 4 6 4 1]
+    const uint32_t a1 = __builtin_amdgcn_alignbyte(w1, w0, 2);  // t2..t5
+    const uint32_t a3 = __builtin_amdgcn_alignbyte(w2, w1, 2);  // t6..t9
+    const uint32_t h0 = __builtin_amdgcn_udot4(w1, 0x00000001u, __builtin_amdgcn_udot4(w0, K, 0, false), false);
+    const uint32_t h1 = __builtin_amdgcn_udot4(w1, 0x00010000u, __builtin_amdgcn_udot4(a1, K, 0, false), false);
+    const uint32_t h2 = __builtin_amdgcn_udot4(w2, 0x00000001u, __builtin_amdgcn_udot4(w1, K, 0, false), false);
+    const uint32_t h3 = __builtin_amdgcn_udot4(w2, 0x00010000u, __builtin_amdgcn_udot4(a3, K, 0, false), false);
+    h[0] = as_u16x2(__builtin_amdgcn_perm(h1, h0, 0x05040100u));
+    h[1] = as_u16x2(__builtin_amdgcn_perm(h3, h2, 0x05040100u));
+}
+
 // horizontal sums of one source row for the lane's 4 destination columns
 template <bool EDGE>
 __device__ inline void pk_hsum(uint2 r, const PkEdge& e, u16x2 (&h)[2]) {
@@ -169,15 +186,7 @@ __device__ inline void pk_hsum(uint2 r, const PkEdge& e, u16x2 (&h)[2]) {
         w0 = e0;
         w1 = e1;
     }
-    constexpr uint32_t K = 0x04060401u;  // taps 0..3 of [1 4 6 4 1]
-    const uint32_t a1 = __builtin_amdgcn_alignbyte(w1, w0, 2);  // t2..t5
-    const uint32_t a3 = __builtin_amdgcn_alignbyte(w2, w1, 2);  // t6..t9
-    const uint32_t h0 = __builtin_amdgcn_udot4(w1, 0x00000001u, __builtin_amdgcn_udot4(w0, K, 0, false), false);
-    const uint32_t h1 = __builtin_amdgcn_udot4(w1, 0x00010000u, __builtin_amdgcn_udot4(a1, K, 0, false), false);
-    const uint32_t h2 = __builtin_amdgcn_udot4(w2, 0x00000001u, __builtin_amdgcn_udot4(w1, K, 0, false), false);
-    const uint32_t h3 = __builtin_amdgcn_udot4(w2, 0x00010000u, __builtin_amdgcn_udot4(a3, K, 0, false), false);
-    h[0] = as_u16x2(__builtin_amdgcn_perm(h1, h0, 0x05040100u));
-    h[1] = as_u16x2(__builtin_amdgcn_perm(h3, h2, 0x05040100u));
+    pk_hsum3(w0, w1, w2, h);
 }
 
 // vertical 5-tap of two destination columns, rounded: (sum + 128) >> 8
@@ -194,11 +203,12 @@ __device__ inline u16x2 pk_vsum(u16x2 h0, u16x2 h1, u16x2 h2, u16x2 h3, u16x2 h4
 // few SALU ops per row: the scalar unit is shared by the CU's waves and was
 // this kernel's first bottleneck.  Bands whose source rows need no
 // reflect-101 and no load clamping (INTERIOR) walk running row pointers.
-constexpr int kSkRing = 8;
 constexpr int kSkW = 244;  // destination columns per wave (lanes 0..60; 61 = right context)
-// band heights per level: short bands keep ~7 waves per SIMD in flight
-// (measured: 24/12/6-row bands with a 16-row ring ran 30% slower)
-constexpr int kSkBH1 = 8, kSkBH2 = 4, kSkBH3 = 4;
+// 8-row bands keep ~7 waves per SIMD in flight (measured in round 1:
+// 24/12/6-row bands with a 16-row ring ran 30% slower); a 20-row ring holds
+// all 19 source rows of a band, so each wave makes one memory round trip
+// (round 2: 13.5 against 14.8 us per 50-image launch with an 8-row ring)
+constexpr int kSkBH1 = 8, kSkRing1 = 20;
 
 struct SkBand {
     const uint8_t* src;
@@ -394,6 +404,240 @@ __global__ __launch_bounds__(256) void pyr_down_sk_kernel(PyrLevelArgs a) {
 #endif
 }
 
+// ---------------------------------------------------------------- pyramid tail
+// Levels 2 and 3 of every image of a chunk in ONE launch after the level-1
+// launch, no workgroup waiting for another.  A workgroup owns a band of B
+// level-3 rows of one image and the 2B level-2 rows above them (the image's
+// last band: all remaining rows), and recomputes the level-2 halo rows its
+// level-3 rows need:
+//   phase 1  level-1 rows [c1a, c1b) from HBM -> LDS (16-byte loads, all in
+//            flight at once)
+//   phase 2  level-2 rows [c2a, c2b) from the LDS level 1 -> LDS (own rows -> HBM)
+//   phase 3  the own level-3 rows from the LDS level 2 -> HBM
+// A work item is 4 destination columns x RG destination rows (the register
+// ring of sk_band: two new horizontal sums per destination row, v_dot4 +
+// packed 16-bit vertical sums).  Staged rows carry reflect-101 pad bytes at
+// both ends, so no phase has edge code.  Barriers wait for LDS only (own
+// global stores are never re-read).  B is sized so the chunk's bands fill
+// the resident workgroup slots once.  Against the per-level launches of
+// round 1 the tail replaces two launches (each ~6 us, latency-bound at 50
+// images) by one of ~9 us; one launch for all three levels from level 0
+// (the level-0 halo staged slice by slice) measured 31 us, VALU-bound on the
+// level-1 halo recompute.
+constexpr int kPfThreads = 512;
+constexpr int kPfRG2 = 2;                 // level-2 rows per work item
+constexpr int kPfStage1 = 8;              // 16-byte level-1 loads per thread (max)
+constexpr int kPfPad = 16;                // LDS bytes left of a staged row's column 0
+constexpr int kPfSlots = 512;             // resident workgroups the band height is sized for (2 per CU)
+constexpr size_t kPfLdsMax = 80 * 1024;   // two workgroups per CU
+
+typedef uint32_t pf_u32x4 __attribute__((ext_vector_type(4)));
+
+struct PyrTailArgs {
+    uint8_t* slot[kPyrBatch];
+    size_t off1, off2, off3;
+    int w1, h1, w2, h2, w3, h3;
+    int n, nb, band, xcd_map;  // images, bands per image, level-3 rows per band, XCD map
+    int s1, s2;                // LDS row strides of staged levels 1 / 2
+    int lds1;                  // byte offset of the level-1 rows (level 2 below it)
+};
+
+// own rows [o?a, o?b) and computed rows [c?a, c?b) of band b per level
+struct PfBand {
+    int o2a, o2b, o3a, o3b, c1a, c1b, c2a, c2b;
+};
+
+__host__ __device__ inline PfBand pf_band(int b, int nb, int band, int h1, int h2, int h3) {
+    PfBand r;
+    const bool last = b == nb - 1;
+    r.o3a = band * b;
+    r.o3b = last ? h3 : r.o3a + band;
+    r.o2a = 2 * band * b;
+    r.o2b = last ? h2 : r.o2a + 2 * band;
+    // destination row y reads source rows 2y-2 .. 2y+2 (reflect-101 at the
+    // borders lands within 3 rows of the border, inside the range then)
+    r.c2a = min(r.o2a, max(0, 2 * r.o3a - 2));
+    r.c2b = max(r.o2b, min(h2, 2 * (r.o3b - 1) + 3));
+    r.c1a = max(0, 2 * r.c2a - 2);
+    r.c1b = min(h1, 2 * (r.c2b - 1) + 3);
+    return r;
+}
+
+// workgroup barrier for LDS hand-offs: waits for this wave's LDS traffic only
+// (__syncthreads() would also wait for the wave's global stores)
+__device__ inline void pf_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// 4 destination bytes (two packed pairs) -> one dword
+__device__ inline uint32_t pf_pack(const u16x2 (&H)[5][2]) {
+    const u16x2 o0 = pk_vsum(H[0][0], H[1][0], H[2][0], H[3][0], H[4][0]);
+    const u16x2 o1 = pk_vsum(H[0][1], H[1][1], H[2][1], H[3][1], H[4][1]);
+    return __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, o1), __builtin_bit_cast(uint32_t, o0), 0x06040200u);
+}
+
+// destination rows y0 .. y0+cnt-1 (cnt <= RG) of one item: fetch(i, w)
+// yields the taps of source row 2*y0 - 2 + i, emit(j, dword) takes row y0 + j
+template <int RG, class Fetch, class Emit>
+__device__ inline void pf_rows(int cnt, Fetch&& fetch, Emit&& emit) {
+    u16x2 H[5][2];
+    uint32_t w[3];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        fetch(i, w);
+        pk_hsum3(w[0], w[1], w[2], H[i]);
+    }
+#pragma unroll
+    for (int j = 0; j < RG; ++j) {
+        if (j < cnt) {
+            emit(j, pf_pack(H));
+            if (j + 1 < cnt) {
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    H[0][q] = H[2][q];
+                    H[1][q] = H[3][q];
+                    H[2][q] = H[4][q];
+                }
+                fetch(5 + 2 * j, w);
+                pk_hsum3(w[0], w[1], w[2], H[3]);
+                fetch(6 + 2 * j, w);
+                pk_hsum3(w[0], w[1], w[2], H[4]);
+            }
+        }
+    }
+}
+
+// store the dword of destination columns x .. x+3 of a row of width dw
+__device__ inline void pf_store(uint8_t* row, int x, int dw, uint32_t v) {
+    if (x + 4 <= dw) {
+        *reinterpret_cast<__attribute__((address_space(1))) uint32_t*>(reinterpret_cast<uintptr_t>(row + x)) = v;
+    } else {
+        for (int q = 0; q < dw - x; ++q) row[x + q] = (uint8_t)(v >> (8 * q));
+    }
+}
+
+// the taps of staged source row `row` (index into the LDS rows) for
+// destination columns 4g .. 4g+3: bytes kPfPad + 8g - 2 .. + 10
+__device__ inline void pf_lds_taps(const uint8_t* lds, int stride, int row, int g, uint32_t (&w)[3]) {
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(lds + (size_t)row * stride + kPfPad - 4 + 8 * g);
+    const uint32_t d0 = p[0], d1 = p[1], d2 = p[2], d3 = p[3];
+    w[0] = __builtin_amdgcn_alignbyte(d1, d0, 2);
+    w[1] = __builtin_amdgcn_alignbyte(d2, d1, 2);
+    w[2] = __builtin_amdgcn_alignbyte(d3, d2, 2);
+}
+
+// reflect-101 pad bytes (columns -2, -1, w, w+1) of staged rows
+__device__ inline void pf_pads(uint8_t* lds, int stride, int rows, int w, int tid) {
+    for (int t = tid; t < 4 * rows; t += kPfThreads) {
+        const int row = t >> 2, k = t & 3;
+        const int c = k < 2 ? k - 2 : w + k - 2;
+        uint8_t* base = lds + (size_t)row * stride + kPfPad;
+        base[c] = base[reflect101(c, w)];
+    }
+}
+
+__global__ __launch_bounds__(kPfThreads) void pyr_tail_kernel(PyrTailArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_pf[];
+    int img, band;
+    if (a.xcd_map) {  // blocks are dealt to the 8 XCDs round-robin: all bands of an image on one XCD
+        const int q = (int)blockIdx.x >> 3;
+        band = q % a.nb;
+        img = 8 * (q / a.nb) + ((int)blockIdx.x & 7);
+    } else {
+        band = (int)blockIdx.x % a.nb;
+        img = (int)blockIdx.x / a.nb;
+    }
+    if (img >= a.n) return;  // block-uniform, before any barrier
+#ifdef VISO_PROBE
+    const unsigned long long pr_t0 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long pr_t1 = 0, pr_t2 = 0;
+#endif
+    const PfBand r = pf_band(band, a.nb, a.band, a.h1, a.h2, a.h3);
+    const uint8_t* l1 = a.slot[img] + a.off1;
+    uint8_t* l2 = a.slot[img] + a.off2;
+    uint8_t* l3 = a.slot[img] + a.off3;
+    uint8_t* lds1 = s_pf + a.lds1;
+    uint8_t* lds2 = s_pf;
+    const int tid = (int)threadIdx.x;
+    // ---- phase 1: level-1 rows [c1a, c1b) from HBM (a chunk past a row end
+    // reads into the next row or level 2 of the slot)
+    {
+        const int C = (a.w1 + 15) >> 4, rows = r.c1b - r.c1a;
+        pf_u32x4 q[kPfStage1];
+        int off[kPfStage1];
+#pragma unroll
+        for (int k = 0; k < kPfStage1; ++k) {
+            const int t = tid + k * kPfThreads, i = t / C, c = t - i * C;
+            off[k] = i < rows ? i * a.s1 + kPfPad + 16 * c : -1;
+            if (i < rows)
+                q[k] = *reinterpret_cast<const __attribute__((address_space(1))) pf_u32x4*>(
+                    reinterpret_cast<uintptr_t>(l1 + (size_t)(r.c1a + i) * a.w1 + 16 * c));
+        }
+#pragma unroll
+        for (int k = 0; k < kPfStage1; ++k)
+            if (off[k] >= 0) *reinterpret_cast<pf_u32x4*>(lds1 + off[k]) = q[k];
+        pf_barrier();
+#ifdef VISO_PROBE
+        pr_t1 = __builtin_amdgcn_s_memrealtime();
+#endif
+        pf_pads(lds1, a.s1, rows, a.w1, tid);
+        pf_barrier();
+    }
+    // ---- phase 2: level 2
+    {
+        const int G = (a.w2 + 3) >> 2, rows = r.c2b - r.c2a, nrg = (rows + kPfRG2 - 1) / kPfRG2;
+        for (int it = tid; it < nrg * G; it += kPfThreads) {
+            const int rg = it / G, g = it - rg * G;
+            const int y0 = r.c2a + rg * kPfRG2;
+            // source rows 2y0-2 .. 2y0+4 inside level 1: consecutive staged rows
+            const bool inner = 2 * y0 - 2 >= 0 && 2 * y0 + 4 < a.h1;
+            auto fetch = [&](int i, uint32_t (&w)[3]) {
+                const int row = inner ? 2 * y0 - 2 + i : reflect101(2 * y0 - 2 + i, a.h1);
+                pf_lds_taps(lds1, a.s1, row - r.c1a, g, w);
+            };
+            auto emit = [&](int j, uint32_t val) {
+                const int y = y0 + j;
+                *reinterpret_cast<uint32_t*>(lds2 + (size_t)(y - r.c2a) * a.s2 + kPfPad + 4 * g) = val;
+                if (y >= r.o2a && y < r.o2b) pf_store(l2 + (size_t)y * a.w2, 4 * g, a.w2, val);
+            };
+            pf_rows<kPfRG2>(min(kPfRG2, r.c2b - y0), fetch, emit);
+        }
+        pf_barrier();
+#ifdef VISO_PROBE
+        pr_t2 = __builtin_amdgcn_s_memrealtime();
+#endif
+        pf_pads(lds2, a.s2, rows, a.w2, tid);
+        pf_barrier();
+    }
+    // ---- phase 3: level 3 (own rows only)
+    {
+        const int G = (a.w3 + 3) >> 2, rows = r.o3b - r.o3a;
+        for (int it = tid; it < rows * G; it += kPfThreads) {
+            const int y = r.o3a + it / G, g = it % G;
+            auto fetch = [&](int i, uint32_t (&w)[3]) {
+                pf_lds_taps(lds2, a.s2, reflect101(2 * y - 2 + i, a.h2) - r.c2a, g, w);
+            };
+            auto emit = [&](int, uint32_t val) { pf_store(l3 + (size_t)y * a.w3, 4 * g, a.w3, val); };
+            pf_rows<1>(1, fetch, emit);
+        }
+    }
+#ifdef VISO_PROBE
+    // block timeline: start, phase 1 done, phase 2 done, end (100 MHz), HW_ID | XCC_ID << 32
+    __syncthreads();
+    const int w = img * a.nb + band;
+    if (tid == 0 && w < 8192) {
+        g_pyr_tl[w][0] = pr_t0;
+        g_pyr_tl[w][1] = pr_t1;
+        g_pyr_tl[w][2] = pr_t2;
+        g_pyr_tl[w][3] = __builtin_amdgcn_s_memrealtime();
+        g_pyr_tl[w][4] = (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
+                         ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32);
+    }
+#endif
+}
+
 // ---------------------------------------------------------------- FAST
 __constant__ int c_circle_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
 __constant__ int c_circle_dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
@@ -556,44 +800,97 @@ __global__ __launch_bounds__(256) void fast_compact_kernel(const int* __restrict
     if (y == h - 1 && tid == 0) *n_out = base + cnt;
 }
 
+// Tail-launch plan for n images of a geometry; false (level 1 narrower than
+// 8 columns) = per-level launches.  The band height starts from the one that
+// fills kPfSlots once and shrinks until the staged rows fit the per-thread
+// load slots and the LDS budget (B = 2 fits any level 0 up to kMaxWidth).
+bool pf_plan(const PyrGeom& g, int n, PyrTailArgs& a, size_t& lds) {
+    static_assert(kLevels == 4, "pyramid tail: levels 2..3");
+    if (g.w[1] < 8 || g.w[3] < 1 || g.h[3] < 1) return false;
+    a.w1 = g.w[1];
+    a.h1 = g.h[1];
+    a.w2 = g.w[2];
+    a.h2 = g.h[2];
+    a.w3 = g.w[3];
+    a.h3 = g.h[3];
+    a.off1 = g.off[1];
+    a.off2 = g.off[2];
+    a.off3 = g.off[3];
+    // a staged row holds its pads, the dword writes of every group of its
+    // level and the 16-byte tap reads of every group of the next level
+    auto stride = [](int w, int g_self, int g_next) {
+        const int s = std::max(kPfPad + w + 2, std::max(kPfPad + 4 * g_self, kPfPad + 8 * g_next + 4));
+        return (s + 15) & ~15;
+    };
+    a.s1 = std::max(stride(a.w1, 0, (a.w2 + 3) / 4), (kPfPad + 16 * ((a.w1 + 15) / 16) + 15) & ~15);
+    a.s2 = stride(a.w2, (a.w2 + 3) / 4, (a.w3 + 3) / 4);
+    const int nb_target = std::max(1, kPfSlots / std::max(n, 1));
+    for (a.band = std::max(2, (g.h[3] + nb_target - 1) / nb_target);; --a.band) {
+        a.nb = (g.h[3] + a.band - 1) / a.band;
+        int r1 = 0, r2 = 0;
+        for (int b = 0; b < a.nb; ++b) {
+            const PfBand r = pf_band(b, a.nb, a.band, a.h1, a.h2, a.h3);
+            r1 = std::max(r1, r.c1b - r.c1a);
+            r2 = std::max(r2, r.c2b - r.c2a);
+        }
+        a.lds1 = r2 * a.s2;
+        lds = (size_t)a.lds1 + (size_t)r1 * a.s1;
+        const bool fits = (size_t)r1 * ((a.w1 + 15) / 16) <= (size_t)kPfStage1 * kPfThreads && lds <= kPfLdsMax;
+        if (fits) return true;
+        if (a.band == 1) return false;
+    }
+}
+
+// one per-level launch (level l from level l-1) over nb images: the
+// register-only streaming form for level 1 at least 8 columns wide, the
+// LDS-staged form for the tiny levels of images the tail does not take
+void launch_pyr_level(const PyrGeom& g, int l, const uint8_t* const* l0, uint8_t* const* slot, int nb,
+                      hipStream_t stream) {
+    PyrLevelArgs a;
+    for (int i = 0; i < nb; ++i) {
+        a.src[i] = l == 1 ? l0[i] : slot[i] + g.off[l - 1];
+        a.dst[i] = slot[i] + g.off[l];
+    }
+    a.sw = g.w[l - 1];
+    a.sh = g.h[l - 1];
+    a.dw = g.w[l];
+    a.dh = g.h[l];
+    if (l == 1 && a.sw >= 8) {
+        a.bands = (a.dh + kSkBH1 - 1) / kSkBH1;
+        a.units = a.bands * ((a.dw + kSkW - 1) / kSkW);
+        pyr_down_sk_kernel<kSkBH1, kSkRing1><<<dim3((a.units + 3) / 4, nb), 256, 0, stream>>>(a);
+        return;
+    }
+    const int bh = l == 1 ? 8 : (l == 2 ? 4 : 2);
+    a.bands = (a.dh + bh - 1) / bh;
+    a.units = a.bands * ((a.dw + kPsW - 1) / kPsW);
+    const dim3 grid((a.units + 3) / 4, nb);
+    if (l == 1)
+        pyr_down_stream_kernel<8><<<grid, 256, 0, stream>>>(a);
+    else if (l == 2)
+        pyr_down_stream_kernel<4><<<grid, 256, 0, stream>>>(a);
+    else
+        pyr_down_stream_kernel<2><<<grid, 256, 0, stream>>>(a);
+}
+
 }  // namespace
 
 void launch_pyramid_frames(const PyrGeom& g, const uint8_t* const* l0, uint8_t* const* slot,
                            int n, hipStream_t stream) {
     for (int b0 = 0; b0 < n; b0 += kPyrBatch) {
         const int nb = (n - b0) < kPyrBatch ? (n - b0) : kPyrBatch;
-        for (int l = 1; l < kLevels; ++l) {
-            PyrLevelArgs a;
-            for (int i = 0; i < nb; ++i) {
-                a.src[i] = l == 1 ? l0[b0 + i] : slot[b0 + i] + g.off[l - 1];
-                a.dst[i] = slot[b0 + i] + g.off[l];
-            }
-            a.sw = g.w[l - 1];
-            a.sh = g.h[l - 1];
-            a.dw = g.w[l];
-            a.dh = g.h[l];
-            const int bh = l == 1 ? 8 : (l == 2 ? 4 : 2);
-            a.bands = (a.dh + bh - 1) / bh;
-            a.units = a.bands * ((a.dw + kPsW - 1) / kPsW);
-            const dim3 grid((a.units + 3) / 4, nb);
-            if (a.sw >= 8) {  // register-only streaming form; the scalar form covers tiny levels
-                const int sbh = l == 1 ? kSkBH1 : (l == 2 ? kSkBH2 : kSkBH3);
-                a.bands = (a.dh + sbh - 1) / sbh;
-                a.units = a.bands * ((a.dw + kSkW - 1) / kSkW);
-                const dim3 sgrid((a.units + 3) / 4, nb);
-                if (l == 1)
-                    pyr_down_sk_kernel<kSkBH1, kSkRing><<<sgrid, 256, 0, stream>>>(a);
-                else if (l == 2)
-                    pyr_down_sk_kernel<kSkBH2, kSkRing><<<sgrid, 256, 0, stream>>>(a);
-                else
-                    pyr_down_sk_kernel<kSkBH3, kSkRing><<<sgrid, 256, 0, stream>>>(a);
-            } else if (l == 1) {
-                pyr_down_stream_kernel<8><<<grid, 256, 0, stream>>>(a);
-            } else if (l == 2) {
-                pyr_down_stream_kernel<4><<<grid, 256, 0, stream>>>(a);
-            } else {
-                pyr_down_stream_kernel<2><<<grid, 256, 0, stream>>>(a);
-            }
+        launch_pyr_level(g, 1, l0 + b0, slot + b0, nb, stream);
+        PyrTailArgs ta;
+        size_t lds = 0;
+        if (pf_plan(g, nb, ta, lds)) {
+            for (int i = 0; i < nb; ++i) ta.slot[i] = slot[b0 + i];
+            ta.n = nb;
+            ta.xcd_map = nb >= 8;
+            const int grid = ta.xcd_map ? 8 * ta.nb * ((nb + 7) / 8) : ta.nb * nb;
+            pyr_tail_kernel<<<grid, kPfThreads, lds, stream>>>(ta);
+        } else {
+            launch_pyr_level(g, 2, l0 + b0, slot + b0, nb, stream);
+            launch_pyr_level(g, 3, l0 + b0, slot + b0, nb, stream);
         }
     }
 }

@@ -14,7 +14,7 @@ void launch_pyramid(const PyrGeom& g, uint8_t* base, int n_images, size_t img_st
 // Batched pyramid over frames whose level 0 is at l0[i] and whose levels
 // 1..3 go to slot[i] + g.off[l] (n <= kPyrBatch per launch; more are split).
 constexpr int kPyrBatch = 128;
-// Three streaming launches (one per level).
+// Two launches: level 1 (streaming bands), levels 2-3 (pyr_tail_kernel).
 void launch_pyramid_frames(const PyrGeom& g, const uint8_t* const* l0, uint8_t* const* slot,
                            int n, hipStream_t stream);
 
