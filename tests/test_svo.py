@@ -197,6 +197,32 @@ def test_gpu_features_bitexact(kind, h, w, tau, n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cap", [700, 1999])
+def test_gpu_sequence_truncated_capacity(synth_frames, cap):
+    """More candidates than max_features: the first `cap` in row-major order
+    are kept (the segment that straddles the cap partly), in the features and
+    in the class-band index the matching reads (matches of the whole
+    sequence identical to the spec)."""
+    from viso_amd import svo
+    seq, frames = synth_frames
+    p = svo.default_params(1242, 375, *seq.K, seq.p.baseline, max_features=cap)
+    q = ol.svo_params(1242, 375, *seq.K, seq.p.baseline, max_features=cap)
+    vo = svo.VisualOdometryStereo(p)
+    got = vo.features(frames[0][0])
+    exp = ol.svo_features(frames[0][0], q)
+    assert len(got) == len(exp) == cap
+    for a in ("u", "v", "cls", "desc"):
+        assert np.array_equal(getattr(got, a), getattr(exp, a)), a
+    S = ol.SvoSequence(q)
+    for f, (l, r) in enumerate(frames):
+        assert vo.process(l, r) == S.process(l, r)
+        assert vo.stats().tolist() == S.stats
+        if f > 0:
+            uv8, inl = vo.getMatches()
+            assert np.array_equal(uv8, S.matches) and np.array_equal(inl, S.inliers)
+
+
+@pytest.mark.gpu
 def test_gpu_match_bitexact(gpu_vo, synth_frames):
     seq, frames = synth_frames
     p = _params()

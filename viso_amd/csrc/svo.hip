@@ -491,6 +491,133 @@ __global__ __launch_bounds__(1024) void svo_scan_kernel(SvoDev p, const FeatDev*
     }
 }
 
+// The same scan with the per-segment tables in LDS (images whose h x segs
+// candidate counts fit kScanLds ints: 1242x375 has 9,000): the counts are
+// read from HBM once, coalesced, and every prefix walk runs in LDS.  The
+// class-band index is built column by column, one wave per column: a wave
+// scan over 64 rows at a time gives each row's brow0, stored coalesced.
+// Same outputs as svo_scan_kernel, bit for bit (integer work).
+constexpr int kScanLds = 12288;
+
+__global__ __launch_bounds__(1024) void svo_scan_lds_kernel(SvoDev p, const FeatDev* __restrict__ sets, int ring,
+                                                            int pair0, int segs, int seg_cap) {
+    const FeatDev F = set_of(sets, ring, p.ncam, pair0, blockIdx.x);
+    extern __shared__ int s_dyn[];
+    __shared__ int s_w[16];
+    __shared__ int s_total;
+    const int h = p.h, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, cap = p.cap;
+    const int n = h * segs, ncol = 4 * segs;
+    int* s_cnt = s_dyn;          // [h][segs] candidate counts (4 classes, 8 bits each)
+    int* s_off = s_cnt + n;      // [h][segs] first feature index of the segment
+    int* s_rs = s_off + n;       // [h] row starts
+    int* s_col = s_rs + h;       // [4 segs] first index position of each class-band column
+    for (int i = tid; i < n; i += 1024) s_cnt[i] = F.cnt[i];
+    __syncthreads();
+    // ---- 1: offsets within the row, row totals
+    for (int y = tid; y < h; y += 1024) {
+        int acc = 0;
+        for (int s = 0; s < segs; ++s) {
+            s_off[y * segs + s] = acc;
+            acc += bytesum(s_cnt[y * segs + s]);
+        }
+        s_rs[y] = acc;
+    }
+    __syncthreads();
+    // ---- 2: row starts
+    {
+        const int per = (h + 1023) / 1024, b = min(tid * per, h), e = min(b + per, h);
+        int sum = 0;
+        for (int y = b; y < e; ++y) sum += s_rs[y];
+        int total;
+        int acc = block_excl_scan(sum, s_w, total);
+        for (int y = b; y < e; ++y) {
+            const int t = s_rs[y];
+            s_rs[y] = acc;
+            acc += t;
+        }
+        if (tid == 0) {
+            F.row0[h] = min(total, cap);
+            *F.n = min(total, cap);
+            s_total = total;
+        }
+    }
+    __syncthreads();
+    for (int y = tid; y < h; y += 1024) F.row0[y] = min(s_rs[y], cap);
+    for (int i = tid; i < n; i += 1024) s_off[i] += s_rs[i / segs];
+    __syncthreads();
+    // ---- 3: class-band index (column kb = class k x band s, rows ascending)
+    const bool full = s_total <= cap;
+    auto kept = [&](int y, int s, int k) {
+        const int i = y * segs + s;
+        const int c4 = s_cnt[i];
+        if (full) return (c4 >> (8 * k)) & 0xff;
+        const int c = bytesum(c4), lim = min(c, max(cap - s_off[i], 0));
+        if (lim == c) return (c4 >> (8 * k)) & 0xff;
+        const int* list = F.list + (size_t)i * seg_cap;
+        int r = 0;
+        for (int q = 0; q < lim; ++q) r += (list[q] >> 16) == k ? 1 : 0;
+        return r;
+    };
+    for (int col = wave; col < ncol; col += 16) {  // column totals
+        const int k = col / segs, s = col - k * segs;
+        int t = 0;
+        for (int y = lane; y < h; y += 64) t += kept(y, s, k);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+        if (lane == 0) s_col[col] = t;
+    }
+    __syncthreads();
+    {
+        const int v = tid < ncol ? s_col[tid] : 0;
+        int total;
+        const int e = block_excl_scan(v, s_w, total);
+        if (tid < ncol) s_col[tid] = e;
+    }
+    __syncthreads();
+    for (int col = wave; col < ncol; col += 16) {
+        const int k = col / segs, s = col - k * segs;
+        int* b0 = F.brow0 + (size_t)col * (h + 1);
+        int base = s_col[col];
+        for (int y0 = 0; y0 < h; y0 += 64) {
+            const int y = y0 + lane;
+            const int v = y < h ? kept(y, s, k) : 0;
+            int incl = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int t = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += t;
+            }
+            if (y < h) b0[y] = base + incl - v;
+            base += __shfl(incl, 63, 64);
+        }
+        if (lane == 0) b0[h] = base;
+    }
+    __syncthreads();
+    // ---- 4: thread per segment: the features and their index entries
+    for (int i = tid; i < n; i += 1024) {
+        const int c4 = s_cnt[i];
+        if (!c4) continue;
+        const int y = i / segs, s = i - y * segs;
+        const int c = bytesum(c4), o0 = s_off[i], lim = min(c, max(cap - o0, 0));
+        const int* list = F.list + (size_t)i * seg_cap;
+        int rank[4] = {0, 0, 0, 0};
+        for (int q = 0; q < c; ++q) {
+            const int o = o0 + q;
+            if (o >= cap) break;
+            const int ent = list[q], k = ent >> 16, u = ent & 0xffff;
+            F.u[o] = u;
+            F.v[o] = y;
+            F.c[o] = k;
+            if (q < lim) {
+                const int pos = F.brow0[(size_t)(k * segs + s) * (h + 1) + y] + rank[k]++;
+                F.bidx[pos] = o;
+                F.buc[pos] = pack_uvc(u, y, k);
+                F.bpos[o] = pos;
+            }
+        }
+    }
+}
+
 __device__ inline int sobel_q(const uint8_t* I, int w, int x, int y, bool du) {
     auto px = [&](int dx, int dy) { return (int)I[(size_t)(y + dy) * w + x + dx]; };
     const int d = du ? (px(1, -1) + 2 * px(1, 0) + px(1, 1)) - (px(-1, -1) + 2 * px(-1, 0) + px(-1, 1))
@@ -1655,7 +1782,12 @@ struct viso_svo {
         // responses outside [2, w-3] x [2, h-3] reach the NMS only if margin < n + 2
         const bool dom = p.margin < p.nms_n + 2;
         launch_detect(p.nms_n, dom, g, stream, imgs, d, d_sets, ring, pair0, seg_cap);
-        svo_scan_kernel<<<ni, 1024, 0, stream>>>(d, d_sets, ring, pair0, 4 * tiles, seg_cap);
+        const int segs = 4 * tiles;
+        if ((long long)p.height * segs <= kScanLds)
+            svo_scan_lds_kernel<<<ni, 1024, (size_t)(2 * p.height * segs + p.height + 4 * segs) * sizeof(int), stream>>>(
+                d, d_sets, ring, pair0, segs, seg_cap);
+        else
+            svo_scan_kernel<<<ni, 1024, 0, stream>>>(d, d_sets, ring, pair0, segs, seg_cap);
         svo_describe_kernel<<<8 * kDescWg * ((ni + 7) / 8), 256, 0, stream>>>(imgs, d, d_sets, ring, pair0, ni);
         if (timed) {
             VISO_HIP_CHECK(hipEventRecord(tev[2 * tev_n + 1], stream));
