@@ -593,28 +593,30 @@ __global__ __launch_bounds__(1024) void svo_scan_lds_kernel(SvoDev p, const Feat
         if (lane == 0) b0[h] = base;
     }
     __syncthreads();
-    // ---- 4: thread per segment: the features and their index entries
-    for (int i = tid; i < n; i += 1024) {
-        const int c4 = s_cnt[i];
-        if (!c4) continue;
-        const int y = i / segs, s = i - y * segs;
-        const int c = bytesum(c4), o0 = s_off[i], lim = min(c, max(cap - o0, 0));
-        const int* list = F.list + (size_t)i * seg_cap;
-        int rank[4] = {0, 0, 0, 0};
-        for (int q = 0; q < c; ++q) {
-            const int o = o0 + q;
-            if (o >= cap) break;
-            const int ent = list[q], k = ent >> 16, u = ent & 0xffff;
-            F.u[o] = u;
-            F.v[o] = y;
-            F.c[o] = k;
-            if (q < lim) {
-                const int pos = F.brow0[(size_t)(k * segs + s) * (h + 1) + y] + rank[k]++;
-                F.bidx[pos] = o;
-                F.buc[pos] = pack_uvc(u, y, k);
-                F.bpos[o] = pos;
-            }
+    // ---- 4: thread per stored feature o (row-major index < cap): its segment
+    // is the last one starting at or before o (binary search over the LDS
+    // offsets), its class rank among the segment's earlier entries gives its
+    // index position; u / v / class / bpos stores are coalesced
+    const int nf = min(s_total, cap);
+    for (int o = tid; o < nf; o += 1024) {
+        int lo = 0, hi = n - 1;  // s_off[lo] <= o < s_off[hi + 1]
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_off[mid] <= o) lo = mid;
+            else hi = mid - 1;
         }
+        const int i = lo, y = i / segs, s = i - y * segs, q = o - s_off[i];
+        const int* list = F.list + (size_t)i * seg_cap;
+        const int ent = list[q], k = ent >> 16, u = ent & 0xffff;
+        int rank = 0;
+        for (int r = 0; r < q; ++r) rank += (list[r] >> 16) == k ? 1 : 0;
+        F.u[o] = u;
+        F.v[o] = y;
+        F.c[o] = k;
+        const int pos = F.brow0[(size_t)(k * segs + s) * (h + 1) + y] + rank;
+        F.bidx[pos] = o;
+        F.buc[pos] = pack_uvc(u, y, k);
+        F.bpos[o] = pos;
     }
 }
 
