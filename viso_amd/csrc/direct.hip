@@ -65,12 +65,16 @@ __device__ unsigned long long g_probe[128];
 #define PROBE_ABS(i)
 #endif
 
+#ifndef VISO_DIRECT_CONT
+#define VISO_DIRECT_CONT 1
+#endif
 namespace viso {
 
 namespace {
 
 constexpr int kSums = 28;
-constexpr int kWaves = 8;  // waves per workgroup
+constexpr int kWaves = 16;  // waves per workgroup (one map point per wave at tile 16)
+constexpr int kMinTile = 8;  // smallest tile (the canonical tree's leaves: max(8, P / 256) points)
 constexpr int kThreads = kWaves * 64;
 constexpr int kMaxTiles = 256;
 constexpr int kMaxTile = kMaxMapPoints / kMaxTiles;  // 64 points
@@ -466,56 +470,6 @@ __device__ inline float fast_lval(uint32_t t, double ur, double vr) {
                       xx, yy);
 }
 
-// Tile b of level lv (a.tile points) -> part[b][28], good[b].  Called by
-// every thread of the workgroup.  `pre` (may be null) is the prefetched
-// RefSample of this wave's first point of the tile (valid when has_pre).
-__device__ void direct_tile(const DirectArgs& a, const LevelPair& fp, int lv, const double* cur_pose,
-                            int b,
-                            const RefSample& pre, bool has_pre, const uint8_t* win,
-                            const CurWin& cw, double* part, int* good, double* s_pts,
-                            int* s_good, bool zeroed = false) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    int first, T;
-    tile_range(a, b, &first, &T);
-    if (!zeroed) {
-        if (threadIdx.x == 0) *s_good = 0;
-        __syncthreads();
-    }
-    int good_cnt = 0;
-    for (int local = wave; local < T; local += kWaves) {
-        const int i = first + local;
-        double f = 0.0;
-        int idx = -1;
-        bool ok = false;
-        if (i < a.n) {
-            if (has_pre && local == wave) {
-                ok = direct_point_rs(a, fp, lv, cur_pose, pre, win, cw, &f, &idx);
-            } else {
-                RefSample r;
-                ref_sample(a, fp, lv, i, r);
-                CurWin none{};
-                ok = direct_point_rs(a, fp, lv, cur_pose, r, nullptr, none, &f, &idx);
-            }
-        }
-        if (!ok) {
-            if (lane < kSums) s_pts[local * kSums + lane] = 0.0;
-        } else if (lane < 32 && idx >= 0) {
-            s_pts[local * kSums + idx] = f;
-        }
-        good_cnt += ok ? 1 : 0;
-    }
-    if (lane == 0 && good_cnt) atomicAdd(s_good, good_cnt);
-    __syncthreads();
-    // tree over the tile's T points (lanes >= T hold +0.0)
-    for (int k = wave; k < kSums; k += kWaves) {
-        const double v = lane < T ? s_pts[lane * kSums + k] : 0.0;
-        const double r = wave_tree_sum_dpp(v);
-        if (lane == 0) part[(size_t)b * kSums + k] = r;
-    }
-    if (threadIdx.x == 0) good[b] = *s_good;
-    __syncthreads();
-}
-
 // Prologue prefetch of a whole tile, in LDS: per point j of the tile its
 // world point, its projection into the last frame (ur, vr, the bounds test)
 // and the four `last` patch taps of every lane (sample_px's bytes, packed),
@@ -582,8 +536,8 @@ __device__ inline void pf_store(int j, bool ref, const PfPoint& q, PfLds& pf) {
 // is solved in this launch) a prediction, checked per lane in the tile phase.
 template <bool LV16 = false>
 __device__ void prefetch_tile(const DirectArgs& a, int lv, int b, const double* pred, const double* pose_last,
-                              bool ref, int first, int stride, PfLds& pf) {
-    LevelPair fp = level_pair(a.fp, lv);
+                              bool ref, int first, int stride, PfLds& pf, const FramePair* fpair = nullptr) {
+    LevelPair fp = level_pair(fpair ? *fpair : a.fp, lv);
     fp.pose_last = pose_last;
     int p0, T;
     tile_range(a, b, &p0, &T);
@@ -777,42 +731,40 @@ __device__ inline void reduce_partials(const double* v, int gg, SolveLds& L) {
     __syncthreads();
 }
 
-// Continuation (faithful, rare): this workgroup re-evaluates every tile of
-// level lv of frame pair fp at T21 = state into its own scratch.
-__device__ void continue_tiles(const DirectArgs& a, const LevelPair& fp, int lv,
-                               const double* state, double* s_pose, double* s_pts, int* s_good) {
-    double* part = a.s.cont_part + (size_t)blockIdx.x * kMaxTiles * kSums;
-    int* good = a.s.cont_good + (size_t)blockIdx.x * kMaxTiles;
-    if (threadIdx.x == 0) state_to_pose(state, s_pose);
-    __syncthreads();
-    double pose[12];
-    for (int k = 0; k < 12; ++k) pose[k] = s_pose[k];
-    RefSample none{};
-    CurWin off{};
-    for (int b = 0; b < a.n_tiles; ++b)
-        direct_tile(a, fp, lv, pose, b, none, false, nullptr, off, part, good, s_pts, s_good);
-    __threadfence_block();
-    __syncthreads();
-}
-
 // Barrier for LDS hand-offs only: waits for this wave's LDS operations, not
 // for its global loads, so loads issued before it stay in flight (a
 // __syncthreads() also drains vmcnt).
 __device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // GN iterations 1.. of level lv (the faithful continuation, rare): every
-// workgroup re-evaluates all tiles itself at the new T21 and solves again.
+// workgroup re-evaluates all tiles of level lv of frame pair fpair itself at
+// the new T21, into its own scratch, and solves again.  The tiles go through
+// the tile phase's own prefetch + evaluation (all waves prefetch, then
+// evaluate), so this rare path adds no register pressure to the kernel.
 template <bool FAST>
-__device__ void solve_continue(const DirectArgs& a, const LevelPair& fp, int lv, SolveLds& L,
-                               double* stats, double* s_pose, double* s_pts, int* s_good) {
+__device__ void solve_continue(const DirectArgs& a, const FramePair& fpair, int lv, SolveLds& L,
+                               double* stats, double* s_pose, double* s_pts, int* s_good, PfLds& pf) {
     const int t = threadIdx.x, wave = t >> 6;
+    double* part = a.s.cont_part + (size_t)blockIdx.x * kMaxTiles * kSums;
+    int* good = a.s.cont_good + (size_t)blockIdx.x * kMaxTiles;
+    const LevelPair fp = level_pair(fpair, lv);
     for (int iter = 1; iter < 100 && L.cont; ++iter) {
-        continue_tiles(a, fp, lv, L.state, s_pose, s_pts, s_good);
+        if (t == 0) state_to_pose(L.state, s_pose);
+        __syncthreads();
+        double pose[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) pose[k] = s_pose[k];
+        for (int b = 0; b < a.n_tiles; ++b) {
+            if (t == 0) *s_good = 0;
+            prefetch_tile(a, lv, b, pose, fpair.pose_last, true, wave, kWaves, pf, &fpair);
+            __syncthreads();
+            direct_tile_pf<FAST>(a, fp, lv, pose, b, pf, false, part, good, s_pts, s_good);
+        }
+        __threadfence_block();
+        __syncthreads();
         double v[kSums];
         int gg = 0;
-        if (t < 256)
-            load_partials(a.s.cont_part + (size_t)blockIdx.x * kMaxTiles * kSums,
-                          a.s.cont_good + (size_t)blockIdx.x * kMaxTiles, a.n_tiles, v, gg);
+        if (t < 256) load_partials(part, good, a.n_tiles, v, gg);
         reduce_partials(v, gg, L);
         if (wave == 0) {
             if (FAST)
@@ -999,14 +951,22 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
     }
     if (wave == 0 && lane == 0 && !L.cont) after_solve(a, merged, L, s_last, s_pose);
     __syncthreads();  // B2
-    if (solve && L.cont) {
+    if (VISO_DIRECT_CONT && solve && L.cont) {
         // the continuation needs every thread; it leaves s_good dirty
         double* stp = (a.stats && blockIdx.x == 0) ? a.stats + (size_t)kStats * sl : nullptr;
-        const LevelPair cfp = merged ? level_pair(a.prev, sl) : level_pair(a.fp, sl);
-        solve_continue<FAST>(a, cfp, sl, L, stp, s_pose, s_pts, &s_good);
+        solve_continue<FAST>(a, merged ? a.prev : a.fp, sl, L, stp, s_pose, s_pts, &s_good, s_pf);
         if (t == 0) {
             after_solve(a, merged, L, s_last, s_pose);
             s_good = 0;
+        }
+        __syncthreads();
+        // the continuation used the prefetch buffer: this tile's again, at
+        // the solved pose (and, merged, the solved `last` pose)
+        if (tiles) {
+            double pose[12];
+#pragma unroll
+            for (int k = 0; k < 12; ++k) pose[k] = s_pose[k];
+            prefetch_tile(a, lv, blockIdx.x, pose, merged ? s_last : a.fp.pose_last, true, wave, kWaves, s_pf);
         }
         __syncthreads();
     }
@@ -1344,7 +1304,7 @@ DirectArgs direct_args(const FrameDev& last_pyr, const FrameDev& cur_pyr, const 
     a.pose_seed = pose_seed12;
     int P = 1;
     while (P < n) P <<= 1;
-    a.tile = P / kMaxTiles > kWaves ? P / kMaxTiles : kWaves;
+    a.tile = P / kMaxTiles > kMinTile ? P / kMaxTiles : kMinTile;
     a.n_tiles = (n + a.tile - 1) / a.tile;
     if (split && n > 0) {
         a.split = 1;
@@ -1408,7 +1368,7 @@ void launch_direct_final(const FrameDev& last_pyr, const FrameDev& cur_pyr, cons
 static void rig_tiling(int n, int max_tiles, bool split, int* tile, int* n_tiles) {
     int P = 1;
     while (P < n) P <<= 1;
-    int T = P / kRigTiles > kWaves ? P / kRigTiles : kWaves;
+    int T = P / kRigTiles > kMinTile ? P / kRigTiles : kMinTile;
     while ((n + T - 1) / T > max_tiles && T < kMaxTile) T <<= 1;
     *tile = T;
     *n_tiles = (n + T - 1) / T;
