@@ -898,9 +898,10 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
     // the windows are predicted at is the seed (unsolved L(3)) or the T21
     // level sl was evaluated at
     const bool solver = solve && wave == 0;
-    // the solver's SIMD (waves 0 and 4) is left to the solver: wave 4 joins
-    // the prefetch only when there is no solve
-    const bool pf_wave = !solve || (wave != 0 && wave != 4);
+    // the solver's SIMD (waves 0, 4, 8, 12: wave w runs on SIMD w % 4) is
+    // left to the solver; its waves join the prefetch only when there is no
+    // solve
+    const bool pf_wave = !solve || (wave & 3) != 0;
     if (tiles && pf_wave) {
         double pred[12];
         if (!solve) {
@@ -910,8 +911,8 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
             for (int k = 0; k < 7; ++k) sp[k] = a.s.state[sl * kStateStride + k];
             state_to_pose(sp, pred);
         }
-        const int first = solve ? wave - 1 - (wave > 4 ? 1 : 0) : wave;
-        const int stride = solve ? kWaves - 2 : kWaves;
+        const int first = solve ? wave - (wave >> 2) - 1 : wave;
+        const int stride = solve ? kWaves - kWaves / 4 : kWaves;
         // merged: the `last` pose is this launch's solve of the previous
         // frame's level 0, predicted by the T21 that level was evaluated at
         prefetch_tile(a, lv, blockIdx.x, pred, merged ? pred : a.fp.pose_last, true, first, stride, s_pf);
@@ -1185,7 +1186,7 @@ __global__ __launch_bounds__(kThreads) void rig_level_kernel(RigArgs ra) {
         atomicAdd(&s_arrive, 1);
     }
     // ---- prefetch of this workgroup's tile at the predicted camera pose
-    const bool pf_wave = !solve || (wave != 0 && wave != 4);
+    const bool pf_wave = !solve || (wave & 3) != 0;
     if (tiles && pf_wave) {
         double T[12], pred[12];
         if (!solve) {
@@ -1196,8 +1197,8 @@ __global__ __launch_bounds__(kThreads) void rig_level_kernel(RigArgs ra) {
             state_to_pose(sp, T);
         }
         rig_compose(ra.cam[c].E, T, pred);
-        const int first = solve ? wave - 1 - (wave > 4 ? 1 : 0) : wave;
-        const int stride = solve ? kWaves - 2 : kWaves;
+        const int first = solve ? wave - (wave >> 2) - 1 : wave;
+        const int stride = solve ? kWaves - kWaves / 4 : kWaves;
         prefetch_tile<FAST>(a, lv, bt, pred, a.fp.pose_last, true, first, stride, s_pf);
     }
     // ---- the solve (wave 0)
