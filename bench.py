@@ -285,9 +285,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = world > 1
+    # VISO_DIST_BACKEND=gloo: host-tensor collectives, ranks may share a GPU
+    # (device = local rank mod the visible GPUs) -- the rehearsal of the N>1
+    # path on a one-GPU box (tests/test_multi.py); the product path is RCCL
+    backend = os.environ.get("VISO_DIST_BACKEND", "nccl")
     if distributed:
+        local = local % max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    coll_dev = f"cuda:{local}" if backend == "nccl" else None
 
     import viso_amd
     from viso_amd import _lib
@@ -374,7 +383,7 @@ def main():
     if distributed:
         # warm the gather's collectives (all-reduce + all-gather at the timed
         # region's shape) so no communicator / channel setup lands in the clock
-        gather_poses(np.zeros((steps, 12)), device=f"cuda:{local}")
+        gather_poses(np.zeros((steps, 12)), device=coll_dev)
         dist.barrier()
     torch.cuda.synchronize()
     v.synchronize()
@@ -384,18 +393,23 @@ def main():
     poses = v.poses
     if distributed:
         # the trivial result gather over RCCL (viso_amd/shard.py)
-        gathered = gather_poses(poses[n_pose_before:], device=f"cuda:{local}")
+        gathered = gather_poses(poses[n_pose_before:], device=coll_dev)
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     if distributed:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev or "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     # every tracking frame pushes one pose (src/viso.cpp:137); any other timed
     # frame would be an initialisation frame
     tracking_timed = len(poses) - n_pose_before
+    gather = None
+    if distributed:
+        gather = {"backend": "rccl" if backend == "nccl" else backend,
+                  "frames_per_rank": [int(g.shape[0]) for g in gathered],
+                  "own_log_exact": bool(np.array_equal(gathered[rank], poses[n_pose_before:]))}
     frames_by_state = {"initialization": steps - tracking_timed, "running": tracking_timed}
 
     # ---------------------------------------------------------- kernel timing
@@ -532,6 +546,7 @@ def main():
             "other_precision": other,
             "stereo_vo": stereo_vo,
             "rig_direct": rig_direct,
+            "pose_gather": gather,
             "last_frame_stats": {"direct_nGood": st[9], "lk_pairs": st[6], "lk_success": st[7]},
         }
         print(json.dumps(out), flush=True)

@@ -98,3 +98,29 @@ def test_sequence_seed_distinct():
 
     seeds = [sequence_seed(r) for r in range(8)]
     assert len(set(seeds)) == 8
+
+
+@pytest.mark.gpu
+def test_gpu_bench_two_ranks_share_one_gpu(tmp_path):
+    """bench.py's N>1 path on hardware: two ranks (torchrun, gloo collectives,
+    both on the box's one GPU) each track their own sequence; rank 0 prints
+    the line with value = 2 x steps / max-over-ranks time and the gathered
+    pose logs of both ranks."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, VISO_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(root, "bench.py"),
+           "--gpus", "2", "--steps", "20", "--warmup", "5", "--no-cpu", "--no-svo", "--no-other",
+           "--rig-steps", "0"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["steps"] == 20
+    assert line["init_frames_timed"] == 0
+    assert abs(line["value"] - 2 * 20 / (line["ms_per_step"] * 20 * 1e-3)) / line["value"] < 1e-3
+    g = line["pose_gather"]
+    assert g["frames_per_rank"] == [20, 20] and g["own_log_exact"]
