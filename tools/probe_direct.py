@@ -84,6 +84,9 @@ def main():
     c = p[16 + 2]
     print("L(1) solve_wave0 (us from entry): LU %.2f  inverse %.2f  update %.2f  exp %.2f" %
           tuple(us(p[90 + k], c) for k in range(4)))
+    if p[96]:
+        print("L(1) solve: %.0f shader clocks in %.2f us -> %.2f GHz" %
+              (p[95] / max(c, 1), us(p[96], c), p[95] / (10.0 * p[96])))
     stamps = [x for x in p[64:84] if x]
     t0 = min(stamps)
     print("last frame timeline (us from the first launch entry):")

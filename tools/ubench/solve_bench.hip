@@ -27,7 +27,7 @@ template <bool LDLT>
 __global__ void bench(const double* S28, const double* st7, double* out, unsigned long long* ticks) {
     __shared__ SolveLds L;
     const int lane = threadIdx.x & 63;
-    unsigned long long acc = 0;
+    unsigned long long acc = 0, clk = 0;
     for (int r = 0; r < REPS; ++r) {
         if (threadIdx.x < kSolveSums) L.S[threadIdx.x] = S28[threadIdx.x];
         if (threadIdx.x == 0) {
@@ -40,6 +40,7 @@ __global__ void bench(const double* S28, const double* st7, double* out, unsigne
         __syncthreads();
         if (threadIdx.x < 64) {
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            const unsigned long long c0 = __builtin_amdgcn_s_memtime();
 #ifdef VISO_PROBE
             unsigned long long stamps[4] = {t0, t0, t0, t0};
             if (LDLT)
@@ -54,6 +55,7 @@ __global__ void bench(const double* S28, const double* st7, double* out, unsigne
 #endif
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             acc += __builtin_amdgcn_s_memrealtime() - t0;
+            clk += __builtin_amdgcn_s_memtime() - c0;
 #ifdef VISO_PROBE
             if (lane == 0)
                 for (int k = 0; k < 4; ++k) g_probe[k] += stamps[k] - t0;
@@ -62,7 +64,8 @@ __global__ void bench(const double* S28, const double* st7, double* out, unsigne
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        *ticks = acc;
+        ticks[0] = acc;
+        ticks[1] = clk;
         for (int k = 0; k < 7; ++k) out[k] = L.state[k];
         out[7] = L.cost;
     }
@@ -93,7 +96,7 @@ int main() {
     hipMalloc(&dS, sizeof(S));
     hipMalloc(&dst, sizeof(st));
     hipMalloc(&dout, 8 * sizeof(double));
-    hipMalloc(&dt, sizeof(unsigned long long));
+    hipMalloc(&dt, 2 * sizeof(unsigned long long));
     hipMemcpy(dS, S, sizeof(S), hipMemcpyHostToDevice);
     hipMemcpy(dst, st, sizeof(st), hipMemcpyHostToDevice);
     for (int variant = 0; variant < 4; ++variant) {
@@ -106,9 +109,11 @@ int main() {
                 bench<false><<<1, threads>>>(dS, dst, dout, dt);
             hipDeviceSynchronize();
         }
-        unsigned long long t;
+        unsigned long long tt[2];
         double out[8];
-        hipMemcpy(&t, dt, sizeof(t), hipMemcpyDeviceToHost);
+        hipMemcpy(tt, dt, sizeof(tt), hipMemcpyDeviceToHost);
+        const unsigned long long t = tt[0];
+        printf("  shader clock %.2f GHz (%.0f clocks per solve)\n", tt[1] / (10.0 * t), (double)tt[1] / REPS);
         hipMemcpy(out, dout, sizeof(out), hipMemcpyDeviceToHost);
         unsigned long long bits = 0;
         for (int k = 0; k < 8; ++k) {

@@ -929,13 +929,18 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
         PROBE(32 + 6 * (lv + 1) + 1);
         double* stp = (a.stats && blockIdx.x == 0) ? a.stats + (size_t)kStats * sl : nullptr;
 #ifdef VISO_PROBE
+        // shader clock over the solve: s_memtime (core clock) vs s_memrealtime (100 MHz)
+        const unsigned long long clk0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
         unsigned long long stamps[4] = {probe_t0, probe_t0, probe_t0, probe_t0};
         if (FAST)
             solve_wave0_ldlt(L, 0, stp, lv == 1 ? stamps : nullptr);
         else
             solve_wave0(L, 0, stp, lv == 1 ? stamps : nullptr);
-        if (lv == 1 && lane == 0 && blockIdx.x == 0)
+        if (lv == 1 && lane == 0 && blockIdx.x == 0) {
             for (int k = 0; k < 4; ++k) g_probe[90 + k] += stamps[k] - probe_t0;
+            g_probe[95] += __builtin_amdgcn_s_memtime() - clk0;
+            g_probe[96] += __builtin_amdgcn_s_memrealtime() - rt0;
+        }
 #else
         if (FAST)
             solve_wave0_ldlt(L, 0, stp);
