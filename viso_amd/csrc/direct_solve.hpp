@@ -35,7 +35,7 @@ struct SolveLds {
 // The rest of one GN step after `update` (src/viso.cpp:735-753): SE3::exp,
 // T21 = exp(update) * T21, cost /= nGood and the loop decision; stats of
 // block 0.  `h`: this lane's H element (lane < 36, row-major) for stats.
-__device__ inline void solve_finish(SolveLds& L, const double* update, double h, int iter, double* stats,
+__device__ __attribute__((always_inline)) inline void solve_finish(SolveLds& L, const double* update, double h, int iter, double* stats,
                                     unsigned long long* stamps) {
     const int lane = threadIdx.x & 63;
     const bool in = lane < 36;
@@ -138,7 +138,7 @@ __device__ inline void solve_finish(SolveLds& L, const double* update, double h,
 
 // One GN step of one level on wave 0 (all 64 lanes): L.S -> update, the new
 // L.state and the loop decision L.cont (src/viso.cpp:731-753).
-__device__ inline void solve_wave0(SolveLds& L, int iter, double* stats,
+__device__ __attribute__((always_inline)) inline void solve_wave0(SolveLds& L, int iter, double* stats,
                                    unsigned long long* stamps = nullptr) {
     const int lane = threadIdx.x & 63;
     const int row = lane / 6, col = lane - 6 * (lane / 6);
@@ -238,7 +238,7 @@ __device__ inline void solve_wave0(SolveLds& L, int iter, double* stats,
 // inverse: ~1/4 of the faithful PartialPivLU chain).  A non-positive or
 // non-finite pivot gives a NaN update, which reverts the level as the
 // reference's isnan(update[0]) test does.  Then solve_finish as faithful.
-__device__ inline void solve_wave0_ldlt(SolveLds& L, int iter, double* stats,
+__device__ __attribute__((always_inline)) inline void solve_wave0_ldlt(SolveLds& L, int iter, double* stats,
                                         unsigned long long* stamps = nullptr) {
     const int lane = threadIdx.x & 63;
     const int row = lane / 6, col = lane - 6 * (lane / 6);
