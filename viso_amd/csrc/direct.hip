@@ -65,9 +65,6 @@ __device__ unsigned long long g_probe[128];
 #define PROBE_ABS(i)
 #endif
 
-#ifndef VISO_DIRECT_CONT
-#define VISO_DIRECT_CONT 1
-#endif
 namespace viso {
 
 namespace {
@@ -210,12 +207,6 @@ __device__ inline void ref_finish(RefSample& r) {
     r.lval = r.ok ? double((1 - xx) * (1 - yy) * d0 + xx * (1 - yy) * d1 + (1 - xx) * yy * d2 +
                            xx * yy * d3)
                   : 0.0;
-}
-
-__device__ inline void ref_sample(const DirectArgs& a, const LevelPair& fp, int lv, int i,
-                                  RefSample& r) {
-    ref_issue(a, fp, lv, i, r);
-    ref_finish(r);
 }
 
 // Per-wave LDS window (16 x 16 bytes) of the current image around the
@@ -957,7 +948,7 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
     }
     if (wave == 0 && lane == 0 && !L.cont) after_solve(a, merged, L, s_last, s_pose);
     __syncthreads();  // B2
-    if (VISO_DIRECT_CONT && solve && L.cont) {
+    if (solve && L.cont) {
         // the continuation needs every thread; it leaves s_good dirty
         double* stp = (a.stats && blockIdx.x == 0) ? a.stats + (size_t)kStats * sl : nullptr;
         solve_continue<FAST>(a, merged ? a.prev : a.fp, sl, L, stp, s_pose, s_pts, &s_good, s_pf);
