@@ -239,3 +239,43 @@ def test_gpu_failed_stereo_init_keeps_mono_tracks():
     assert 0 in states and states[-1] == 1  # fallback frames, then the mono map
     assert np.array_equal(gv.GetPoints(), ov.points())
     assert _rel(gv.poses, ov.poses()) < 1e-10
+
+
+@pytest.mark.gpu
+def test_gpu_repeated_frames_take_the_continuation():
+    """A frame identical to the last one gives a photometric cost of exactly 0
+    at every level: the reference's loop then continues (cost / lastCost is
+    0 / 0, src/viso.cpp:751) for 99 more GN iterations.  Both continuation
+    paths of the direct-pose kernel run here: in a level launch's prologue
+    (levels 3..1) and, under batched ingest, in the next frame's merged L(3)
+    (level 0).  GPU == oracle frame by frame, per-frame and batched."""
+    import torch
+
+    import viso_amd
+    order = [0, 1, 2, 3, 3, 3, 4, 5, 6]
+    lefts = np.stack([seqdata.image(f) for f in order])
+    rights = np.stack([seqdata.image(f, cam=1) for f in order])
+    seq = seqdata.sequence(0)
+    ov = oracle_lib.Viso(seq.K, W, H, enable_tracking=1)
+    ov.set_stereo(seq.p.baseline, MAX_DISP, 1)
+    gv = viso_amd.Viso(*seq.K, width=W, height=H, enable_tracking=1)
+    gv.set_stereo(seq.p.baseline, MAX_DISP, 1)
+    for k in range(len(order)):
+        ov.on_new_stereo(lefts[k], rights[k])
+        gv.process(lefts[k], rights[k])
+        gv.synchronize()
+        assert gv.state == ov.state == 1, k
+    oP = ov.poses()
+    assert len(oP) == len(order) - 1
+    # no motion on the repeats (up to the SE3(R, t) -> matrix round trip)
+    assert np.allclose(oP[3], oP[2], rtol=0, atol=1e-14) and np.allclose(oP[4], oP[2], rtol=0, atol=1e-14)
+    assert _rel(gv.poses, oP) < 1e-10
+    dl = torch.from_numpy(lefts).cuda()
+    dr = torch.from_numpy(rights).cuda()
+    torch.cuda.synchronize()
+    bat = viso_amd.Viso(*seq.K, width=W, height=H, enable_tracking=1, batch_frames=len(order))
+    bat.set_stereo(seq.p.baseline, MAX_DISP, 1)
+    bat.process_device(dl.data_ptr(), dr.data_ptr(), len(order), W * H)
+    bat.synchronize()
+    assert bat.state == 1
+    assert np.array_equal(bat.poses, gv.poses)
