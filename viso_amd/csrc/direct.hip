@@ -948,7 +948,7 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
     }
     if (wave == 0 && lane == 0 && !L.cont) after_solve(a, merged, L, s_last, s_pose);
     __syncthreads();  // B2
-    if (solve && L.cont) {
+    if (__builtin_expect(solve && L.cont, 0)) {
         // the continuation needs every thread; it leaves s_good dirty
         double* stp = (a.stats && blockIdx.x == 0) ? a.stats + (size_t)kStats * sl : nullptr;
         solve_continue<FAST>(a, merged ? a.prev : a.fp, sl, L, stp, s_pose, s_pts, &s_good, s_pf);
