@@ -258,9 +258,9 @@ __device__ inline void win_store(uint8_t* lds, const CurWin& c) {
 __device__ inline double sample_cw(const uint8_t* __restrict__ img, int w, int h, double x,
                                    double y, const uint8_t* win, const CurWin& c) {
     const bool finite = (x > -1e9 && x < 1e9 && y > -1e9 && y < 1e9);
-    if (finite && c.on) {
+    if (__builtin_expect(finite && c.on, 1)) {
         const int ix = (int)x, iy = (int)y;
-        if (ix >= c.x0 && ix + 1 < c.x0 + kCW && iy >= c.y0 && iy + 1 < c.y0 + kCW) {
+        if (__builtin_expect(ix >= c.x0 && ix + 1 < c.x0 + kCW && iy >= c.y0 && iy + 1 < c.y0 + kCW, 1)) {
             const int o = (iy - c.y0) * kCW + (ix - c.x0);
             const double d0 = (double)ld_lds_u8(win, o), d1 = (double)ld_lds_u8(win, o + 1);
             const double d2 = (double)ld_lds_u8(win, o + kCW), d3 = (double)ld_lds_u8(win, o + kCW + 1);
@@ -589,7 +589,7 @@ __device__ inline void merged_ref(const DirectArgs& a, const LevelPair& fp, int 
     const long long base = (long long)(int)y * (long long)w + (long long)(int)x;
     const double xp = pf.ur[j] + px, yp = pf.vr[j] + py;
     const long long bp = pf.ok[j] ? (long long)(int)yp * (long long)w + (long long)(int)xp : -(1LL << 40);
-    if (base == bp) {
+    if (__builtin_expect(base == bp, 1)) {
         const uint32_t t = pf.taps[j][lane];
         r.t0 = (int)(t & 0xff);
         r.t1 = (int)((t >> 8) & 0xff);
