@@ -105,9 +105,9 @@ __device__ inline Window load_window(uint8_t* lds, const uint8_t* img, int w, in
 __device__ inline double sample_win(const uint8_t* __restrict__ img, int w, int h, double x,
                                     double y, const Window& win) {
     const bool finite = (x > -1e9 && x < 1e9 && y > -1e9 && y < 1e9);
-    if (finite && win.lds) {
+    if (__builtin_expect(finite && win.lds != nullptr, 1)) {
         const int ix = (int)x, iy = (int)y;
-        if (ix >= win.x0 && ix + 1 < win.x0 + kWinW && iy >= win.y0 && iy + 1 < win.y0 + kWinH) {
+        if (__builtin_expect(ix >= win.x0 && ix + 1 < win.x0 + kWinW && iy >= win.y0 && iy + 1 < win.y0 + kWinH, 1)) {
             const int o = (iy - win.y0) * kWinW + (ix - win.x0);
             const double d0 = (double)ld_lds_u8(win.lds, o), d1 = (double)ld_lds_u8(win.lds, o + 1);
             const double d2 = (double)ld_lds_u8(win.lds, o + kWinW);
@@ -238,7 +238,8 @@ __device__ inline LkResult lk_iterate_fast(float I1, float J0, float J1, const f
         const float xx = (float)(X - fX), yy = (float)(Y - fY);
         const int ix = (int)fX + px, iy = (int)fY + py;
         float t0, t1, t2, t3;
-        if (win.lds && ix >= win.x0 && ix + 1 < win.x0 + kWinW && iy >= win.y0 && iy + 1 < win.y0 + kWinH) {
+        if (__builtin_expect(win.lds && ix >= win.x0 && ix + 1 < win.x0 + kWinW && iy >= win.y0 &&
+                             iy + 1 < win.y0 + kWinH, 1)) {
             const int o = (iy - win.y0) * kWinW + (ix - win.x0);
             t0 = (float)ld_lds_u8(win.lds, o);
             t1 = (float)ld_lds_u8(win.lds, o + 1);
