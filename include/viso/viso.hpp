@@ -104,19 +104,50 @@ public:
               "viso_process_frame");
     }
 
-    std::vector<Pose> poses() const {
-        size_t n = 0;
-        check(viso_get_poses(ctx_, nullptr, 0, &n), "viso_get_poses");
-        std::vector<Pose> out(n);
-        if (n) check(viso_get_poses(ctx_, out.front().data(), n, &n), "viso_get_poses");
-        return out;
-    }
+    // The pose log.  The reference exposes it as a public field
+    // (`std::vector<Sophus::SE3d> poses`, include/viso.h:54; src/main.cpp:50
+    // passes `viso.poses` to DrawMap and iterates it), so `poses` is a member
+    // that reads like that field -- `viso.poses.size()`, `viso.poses[i]`,
+    // `for (auto& Tcw : viso.poses)`, `const std::vector<Pose>& p =
+    // viso.poses` -- and also keeps the call form `viso.poses()`.  Every use
+    // copies the log from the device (synchronising the context); range-for
+    // and indexing work on that snapshot, refreshed by size() / begin().
+    class PoseLog {
+       public:
+        explicit PoseLog(const Viso* v) : v_(v) {}
+        PoseLog(const PoseLog&) = delete;
+        PoseLog& operator=(const PoseLog&) = delete;
+        std::vector<Pose> operator()() const { return v_->fetch_poses(); }
+        operator std::vector<Pose>() const { return v_->fetch_poses(); }
+        size_t size() const { return refresh().size(); }
+        bool empty() const { return size() == 0; }
+        const Pose& operator[](size_t i) const { return cache_.size() > i ? cache_[i] : refresh()[i]; }
+        std::vector<Pose>::const_iterator begin() const { return refresh().begin(); }
+        std::vector<Pose>::const_iterator end() const { return cache_.end(); }
+
+       private:
+        const std::vector<Pose>& refresh() const {
+            cache_ = v_->fetch_poses();
+            return cache_;
+        }
+        const Viso* v_;
+        mutable std::vector<Pose> cache_;
+    };
+    PoseLog poses{this};
 
     std::vector<V3d> GetPoints() const {
         size_t n = 0;
         check(viso_get_points(ctx_, nullptr, 0, &n), "viso_get_points");
         std::vector<V3d> out(n);
         if (n) check(viso_get_points(ctx_, out.front().data(), n, &n), "viso_get_points");
+        return out;
+    }
+
+    std::vector<Pose> fetch_poses() const {
+        size_t n = 0;
+        check(viso_get_poses(ctx_, nullptr, 0, &n), "viso_get_poses");
+        std::vector<Pose> out(n);
+        if (n) check(viso_get_poses(ctx_, out.front().data(), n, &n), "viso_get_poses");
         return out;
     }
 

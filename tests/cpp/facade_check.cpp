@@ -32,6 +32,13 @@ int main(int argc, char** argv) {
         svo_ok += svo.process(l.data(), r.data(), dims) ? 1 : 0;
     }
     std::printf("viso: state %d points %zu poses %zu\n", vo.state(), vo.GetPoints().size(), vo.poses().size());
+    // the reference's field form (src/main.cpp:50, :75): viso.poses, iterated
+    {
+        const std::vector<viso::Pose>& log = vo.poses;
+        size_t n = 0;
+        for (const auto& Tcw : vo.poses) n += (Tcw[0] == Tcw[0]) ? 1 : 0;
+        if (n != log.size() || vo.poses.size() != log.size() || (n && vo.poses[n - 1] != log[n - 1])) return 1;
+    }
     std::printf("svo: ok %d poses %zu matches %zu\n", svo_ok, svo.poses().size(), svo.getMatches().size());
     // the photometric rig, 2 cameras
     const int nc = 2;
