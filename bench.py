@@ -15,10 +15,13 @@ kRunning (bounded; otherwise exit 3), so the K timed frames are tracking
 frames at any --warmup (init_frames_timed in the line counts any that are
 not).
 
-Multi-GPU (torchrun, one process per GPU): independent sequences, no
-data-path collective; after the timed frames the per-rank pose logs are
-all-gathered over RCCL (the trivial result gather of BASELINE.json config 4).
-value = total frames / max-over-ranks time (weak scaling).
+Multi-GPU (one process per GPU): independent sequences, no data-path
+collective; after the timed frames the per-rank pose logs are all-gathered
+over RCCL (the trivial result gather of BASELINE.json config 4).  value =
+total frames / max-over-ranks time (weak scaling).  Under an external
+torchrun WORLD_SIZE must equal --gpus (exit 2 otherwise); `bench.py --gpus N`
+without one starts the N ranks itself (torch.distributed.run as a child
+process, before this process touches the GPU).
 
 Prints ONE JSON line on rank 0 (the driver's contract), including:
   roofline     — the HBM-bound image pass (pyramid),
@@ -276,13 +279,41 @@ def measure_rig_direct(args, W, H, log):
     return out
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` without an external launcher: start N ranks (one
+    process per GPU) through torch.distributed.run as a child process and
+    return its exit code.  Nothing in this process has touched the GPU (no
+    HIP call, no torch.cuda query), so the ranks own their devices outright."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    log(f"[launcher] --gpus {n}: {' '.join(cmd[1:])}")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        log(f"error: --gpus {args.gpus} but the launcher started {world} rank(s) (WORLD_SIZE)")
+        sys.exit(2)
     import torch
     import torch.distributed as dist
 
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = world > 1
     # VISO_DIST_BACKEND=gloo: host-tensor collectives, ranks may share a GPU
@@ -407,7 +438,10 @@ def main():
     tracking_timed = len(poses) - n_pose_before
     gather = None
     if distributed:
-        gather = {"backend": "rccl" if backend == "nccl" else backend,
+        pg_backend = str(dist.get_backend())
+        gather = {"backend": "rccl" if pg_backend == "nccl" else pg_backend,
+                  "process_group_backend": pg_backend,
+                  "world_size": dist.get_world_size(),
                   "frames_per_rank": [int(g.shape[0]) for g in gathered],
                   "own_log_exact": bool(np.array_equal(gathered[rank], poses[n_pose_before:]))}
     frames_by_state = {"initialization": steps - tracking_timed, "running": tracking_timed}

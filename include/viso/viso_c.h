@@ -247,9 +247,11 @@ int viso_set_keyframes(viso_ctx* ctx, int32_t interval, int32_t ngood_permille);
 int viso_set_bundle_adjust(viso_ctx* ctx, int32_t iterations);
 /* Stage entry (parity tests): the same BA on host data.  kf_images: n_kf
  * (2..8) level-0 images of the context's size; kf_poses: n_kf x 12 (in/out;
- * keyframe 0 fixed); points: n x 3 world (in/out); host: n keyframe indices;
- * report (may be NULL): iterations x 4 (cost, candidate cost, damping,
- * accepted).  src: bundle_adjuster.h:58-100 (EdgeDirectProjection). */
+ * keyframe 0 fixed); points: n x 3 world (in/out), 1 <= n <= 16384; host: n
+ * keyframe indices (an edge's host pose stays at its value from the start of
+ * the call); report (may be NULL): iterations x 4 (cost, candidate cost,
+ * damping, accepted).  src: bundle_adjuster.h:58-100 (EdgeDirectProjection).
+ * VISO_ERR_ARG on any out-of-range argument. */
 int viso_photometric_ba(viso_ctx* ctx, const uint8_t* const* kf_images, int32_t n_kf, double* kf_poses,
                         double* points, const int32_t* host, int32_t n, int32_t iterations, double* report);
 

@@ -18,8 +18,11 @@
 // GetGradient at the tap, Jpi(Pc) = [[fx/z, 0, -fx x/z^2], [0, fy/z, -fy y/z^2]],
 //   dr/dX = g_s Jpi(T_h X) R_h - g_t Jpi(T_t X) R_t,
 //   dr/dxi_t = -g_t dPixeldXi(T_t X)  (src/viso.cpp:640-658; T_t <- exp(xi) T_t,
-//   VertexPose::oplusImpl, bundle_adjuster.h:48-53; the host pose is fixed
-//   in the edge, as in the sketch's binary edge).
+//   VertexPose::oplusImpl, bundle_adjuster.h:48-53).  The host pose is fixed
+//   in the edge, as in the sketch's binary edge: the source projection reads
+//   T_h as it was when the call started (srcFrame->Project uses the
+//   Keyframe's own R_, T_, which g2o never updates), in the linearisation and
+//   in the candidate cost alike.
 // Solver: Levenberg-Marquardt as g2o's OptimizationAlgorithmLevenberg
 // (bundle_adjuster.h:111-115) with the points marginalised (Schur
 // complement, setMarginalized(true)):
@@ -127,7 +130,7 @@ inline void taps(double u, double v, int p, float* fu, float* fv) {
 
 bool edge_active(const BaProblem& P, const double* poses, const double* X, int host, int tgt) {
     double us[2], ut[2], Pc[3];
-    source_uv(poses + 12 * host, P.K, X, us, Pc);
+    source_uv(poses + 12 * host, P.K, X, us, Pc);  // at the call's start: host0 == poses
     target_uv(poses + 12 * tgt, P.K, X, ut, Pc);
     for (int p = 0; p < kBaPx; ++p) {
         float u1, v1, u2, v2;
@@ -138,13 +141,15 @@ bool edge_active(const BaProblem& P, const double* poses, const double* X, int h
     return true;
 }
 
-// the 55 sums of edge (X, host, tgt) at the given estimates
-void edge_sums(const BaProblem& P, const double* poses, const double* X, int host, int tgt, double* out) {
+// the 55 sums of edge (X, host, tgt) at the given estimates (host0: the
+// fixed host poses)
+void edge_sums(const BaProblem& P, const double* host0, const double* poses, const double* X, int host, int tgt,
+               double* out) {
     double us[2], ut[2], Ps[3], Pt[3];
-    source_uv(poses + 12 * host, P.K, X, us, Ps);
+    source_uv(host0 + 12 * host, P.K, X, us, Ps);
     target_uv(poses + 12 * tgt, P.K, X, ut, Pt);
     double Ds[6], Dt[6], Jx[12];
-    dproj_dX(P.K, Ps, poses + 12 * host, Ds);
+    dproj_dX(P.K, Ps, host0 + 12 * host, Ds);
     dproj_dX(P.K, Pt, poses + 12 * tgt, Dt);
     dpixel_dxi(P.K, Pt, Jx);
     double leaf[kBaEdgeSums][kBaPx];
@@ -175,9 +180,9 @@ void edge_sums(const BaProblem& P, const double* poses, const double* X, int hos
     for (int k = 0; k < kBaEdgeSums; ++k) out[k] = tree16(leaf[k]);
 }
 
-double edge_cost(const BaProblem& P, const double* poses, const double* X, int host, int tgt) {
+double edge_cost(const BaProblem& P, const double* host0, const double* poses, const double* X, int host, int tgt) {
     double us[2], ut[2], Pc[3];
-    source_uv(poses + 12 * host, P.K, X, us, Pc);
+    source_uv(host0 + 12 * host, P.K, X, us, Pc);
     target_uv(poses + 12 * tgt, P.K, X, ut, Pc);
     double leaf[kBaPx];
     for (int p = 0; p < kBaPx; ++p) {
@@ -233,6 +238,7 @@ int oracle_photometric_ba(const uint8_t* const* kf_img, int n_kf, int w, int h, 
     double mu = -1.0, nu = 2.0;
     std::vector<double> E((size_t)n * n_kf * kBaEdgeSums), V((size_t)n * 6), bp((size_t)n * 3), leaf((size_t)n);
     std::vector<double> poses_c((size_t)12 * n_kf), pts_c((size_t)3 * n);
+    const std::vector<double> host0(kf_poses, kf_poses + (size_t)12 * n_kf);
     for (int it = 0; it < iterations; ++it) {
         // linearise
         double cost_cur_pts_dummy = 0;
@@ -246,7 +252,7 @@ int oracle_photometric_ba(const uint8_t* const* kf_img, int n_kf, int w, int h, 
                     for (int q = 0; q < kBaEdgeSums; ++q) e[q] = 0.0;
                     continue;
                 }
-                edge_sums(P, kf_poses, points + 3 * i, host[i], k, e);
+                edge_sums(P, host0.data(), kf_poses, points + 3 * i, host[i], k, e);
                 for (int q = 0; q < 6; ++q) V[6 * (size_t)i + q] = first ? e[q] : V[6 * (size_t)i + q] + e[q];
                 for (int q = 0; q < 3; ++q) bp[3 * (size_t)i + q] = first ? e[45 + q] : bp[3 * (size_t)i + q] + e[45 + q];
                 pcost[(size_t)i] = first ? e[54] : pcost[(size_t)i] + e[54];
@@ -369,7 +375,7 @@ int oracle_photometric_ba(const uint8_t* const* kf_img, int n_kf, int w, int h, 
             bool first = true;
             for (int k = 0; k < n_kf; ++k) {
                 if (!active[(size_t)i * n_kf + k]) continue;
-                const double e = edge_cost(P, poses_c.data(), &pts_c[3 * (size_t)i], host[i], k);
+                const double e = edge_cost(P, host0.data(), poses_c.data(), &pts_c[3 * (size_t)i], host[i], k);
                 c = first ? e : c + e;
                 first = false;
             }

@@ -4,10 +4,14 @@ there) as the repo's own spec, oracle/oracle_ba.cpp: keyframe poses
 (keyframe 0 fixed) and map points, 16-residual 4x4 patch edges
 (EdgeDirectProjection, :58-100) from every point to every keyframe but its
 host, Levenberg-Marquardt with the points marginalised (Schur complement).
+An edge's host (source) pose stays at its value from the start of the call,
+as in the sketch's binary edge (srcFrame->Project reads the Keyframe's own
+R_, T_, which g2o never updates).
 Parity unpinned vs the reference (no runnable counterpart): the oracle is
 pinned by the problem it solves (the photometric cost falls on every
 accepted step; perturbed keyframe poses move back toward the renderer's
-ground truth); the GPU (viso_amd/csrc/ba.hip) reproduces the oracle's
+ground truth: a keyframe hosting no points all the way, one whose own
+points are projected from its fixed perturbed pose part of the way); the GPU (viso_amd/csrc/ba.hip) reproduces the oracle's
 decisions exactly and its estimates to <= 1e-9 relative (libm of SE3::exp
 aside, the same operations in the same order)."""
 import numpy as np
@@ -76,11 +80,24 @@ def test_oracle_ba_reduces_cost_and_recovers_poses(oracle_ba):
     assert acc.any()
     assert (rep[acc, 1] < rep[acc, 0]).all()  # accepted steps lower the cost
     assert rep[-1, 1] < 0.9 * rep[0, 0]
-    for k in (1, 2):
+    # keyframe 1 hosts points, keyframe 2 none: keyframe 2 is pulled by the
+    # points keyframe 1 hosts from its fixed (perturbed) pose, so it only
+    # moves part of the way back within one call
+    for k, frac in ((1, 0.3), (2, 0.6)):
         before = np.abs(poses[k][9:] - gt[k][9:]).max()
         after = np.abs(P[k][9:] - gt[k][9:]).max()
-        assert after < 0.3 * before, (k, before, after)
+        assert after < frac * before, (k, before, after)
     assert np.array_equal(P[0], poses[0])  # the gauge
+
+
+def test_oracle_ba_recovers_a_perturbed_keyframe_with_exact_hosts():
+    seq, imgs, gt, poses, pts, host = _problem()
+    poses[1] = gt[1]  # every host pose exact: only keyframe 2 is perturbed
+    P, X, rep, na = oracle_lib.photometric_ba(imgs, poses, pts, host, seq.K, ITERS)
+    before = np.abs(poses[2][9:] - gt[2][9:]).max()
+    after = np.abs(P[2][9:] - gt[2][9:]).max()
+    assert after < 0.1 * before, (before, after)
+    assert np.abs(P[1][9:] - gt[1][9:]).max() < 0.05 * before
 
 
 def test_oracle_ba_without_free_camera_or_points_is_a_no_op():

@@ -100,27 +100,73 @@ def test_sequence_seed_distinct():
     assert len(set(seeds)) == 8
 
 
+def test_bench_rejects_gpus_world_size_mismatch():
+    """An external launcher whose WORLD_SIZE differs from --gpus is an error
+    (exit 2) caught before anything touches the GPU, so it runs here."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "1", "--steps", "1"],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE" in r.stderr
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "4", "--steps", "1"],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2
+
+
+def _bench_line(r):
+    import json
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+
+
+_BENCH_SMALL = ["--steps", "20", "--warmup", "5", "--no-cpu", "--no-svo", "--no-other", "--rig-steps", "0"]
+
+
 @pytest.mark.gpu
 def test_gpu_bench_two_ranks_share_one_gpu(tmp_path):
-    """bench.py's N>1 path on hardware: two ranks (torchrun, gloo collectives,
-    both on the box's one GPU) each track their own sequence; rank 0 prints
-    the line with value = 2 x steps / max-over-ranks time and the gathered
-    pose logs of both ranks."""
-    import json
+    """bench.py's N>1 path on hardware, launched the way the driver does it
+    (an external torch.distributed.run): two ranks (gloo collectives, both on
+    the box's one GPU) each track their own sequence; rank 0 prints the line
+    with value = 2 x steps / max-over-ranks time and the gathered pose logs of
+    both ranks."""
     import subprocess
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, VISO_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    env.pop("WORLD_SIZE", None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(root, "bench.py"),
-           "--gpus", "2", "--steps", "20", "--warmup", "5", "--no-cpu", "--no-svo", "--no-other",
-           "--rig-steps", "0"]
-    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=100)
-    assert r.returncode == 0, r.stderr[-3000:]
-    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+           "--gpus", "2"] + _BENCH_SMALL
+    line = _bench_line(subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=100))
     assert line["n_gpus"] == 2 and line["steps"] == 20
     assert line["init_frames_timed"] == 0
     assert abs(line["value"] - 2 * 20 / (line["ms_per_step"] * 20 * 1e-3)) / line["value"] < 1e-3
     g = line["pose_gather"]
     assert g["frames_per_rank"] == [20, 20] and g["own_log_exact"]
+    assert g["world_size"] == 2 and g["process_group_backend"] == "gloo"
+
+
+@pytest.mark.gpu
+def test_gpu_bench_gpus_flag_launches_ranks(tmp_path):
+    """`bench.py --gpus 2` with no external launcher starts its two ranks
+    itself (torch.distributed.run as a child, before any GPU call) and prints
+    one line with n_gpus 2."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, VISO_DIST_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"] + _BENCH_SMALL
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=100)
+    line = _bench_line(r)
+    assert sum(ln.startswith("{") for ln in r.stdout.splitlines()) == 1
+    assert line["n_gpus"] == 2 and line["init_frames_timed"] == 0
+    g = line["pose_gather"]
+    assert g["world_size"] == 2 and g["frames_per_rank"] == [20, 20] and g["own_log_exact"]

@@ -38,6 +38,10 @@ struct BaDev {
     double K[4];
     double* poses;    // n_kf x 12 (in/out)
     double* poses_c;  // candidates
+    double* poses0;   // the poses at the start of the call: every edge's host
+                      // (source) pose stays fixed there (the sketch's binary
+                      // edge, bundle_adjuster.h:58-100; g2o never moves the
+                      // Keyframe's own R_, T_ that srcFrame->Project reads)
     double* pts;      // n x 3 (in/out)
     double* pts_c;
     const int* host;
@@ -124,6 +128,7 @@ __device__ inline double tree16(double v) {
 // ---------------------------------------------------------------- edge set
 __global__ __launch_bounds__(256) void ba_active_kernel(BaDev a) {
     const int g = blockIdx.x * 256 + threadIdx.x;
+    if (g < 12 * a.n_kf) a.poses0[g] = a.poses[g];
     const int i = g / kMaxKeyframes, k = g - kMaxKeyframes * (g / kMaxKeyframes);
     if (i >= a.n) return;
     uint8_t on = 0;
@@ -165,7 +170,7 @@ __global__ __launch_bounds__(256) void ba_edges_kernel(BaDev a) {
         {
             const int kk = on ? k : hst;  // a valid pose for inactive lanes
             double us[2], ut[2], Ps[3], Pt[3];
-            ba_source_uv(poses + 12 * hst, a.K, X, us, Ps);
+            ba_source_uv(a.poses0 + 12 * hst, a.K, X, us, Ps);
             ba_target_uv(poses + 12 * kk, a.K, X, ut, Pt);
             double u1, v1, u2, v2;
             ba_taps(ut[0], ut[1], p, &u1, &v1);
@@ -175,7 +180,7 @@ __global__ __launch_bounds__(256) void ba_edges_kernel(BaDev a) {
             const double r = sample_px(Si, a.w, a.h, u2, v2) - sample_px(Ti, a.w, a.h, u1, v1);
             if (LINEARISE) {
                 double Ds[6], Dt[6], Jx[12];
-                ba_dproj_dX(a.K, Ps, poses + 12 * hst, Ds);
+                ba_dproj_dX(a.K, Ps, a.poses0 + 12 * hst, Ds);
                 ba_dproj_dX(a.K, Pt, poses + 12 * kk, Dt);
                 ba_dpixel_dxi(a.K, Pt, Jx);
                 double gsx, gsy, gtx, gty;
@@ -497,7 +502,7 @@ __global__ __launch_bounds__(256) void ba_commit_kernel(BaDev a) {
 size_t ba_scratch_bytes(int n) {
     const size_t N = (size_t)(n > 0 ? n : 1);
     return 256 * 40 + N * (kMaxKeyframes + 8 * (kMaxKeyframes * kEs + 6 + 3 + 9 + 3 + 3)) +
-           8 * (size_t)kBaMaxM * kBaMaxM + 8 * 8 * kBaMaxM + 8 * 64 + 8 * 12 * kMaxKeyframes;
+           8 * (size_t)kBaMaxM * kBaMaxM + 8 * 8 * kBaMaxM + 8 * 64 + 2 * 8 * 12 * kMaxKeyframes + 256;
 }
 
 int launch_photometric_ba(const uint8_t* const* kf_l0, int n_kf, int w, int h, const double K[4], double* poses,
@@ -538,6 +543,7 @@ int launch_photometric_ba(const uint8_t* const* kf_l0, int n_kf, int w, int h, c
     a.dc = (double*)take(8 * kBaMaxM);
     a.ctl = (double*)take(8 * 8);
     a.poses_c = (double*)take(8 * 12 * kMaxKeyframes);
+    a.poses0 = (double*)take(8 * 12 * kMaxKeyframes);
     a.report = report;
     const int gp = (n + 255) / 256, gw = (n + 3) / 4;
     ba_active_kernel<<<(n * kMaxKeyframes + 255) / 256, 256, 0, stream>>>(a);

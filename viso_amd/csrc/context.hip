@@ -376,7 +376,10 @@ extern "C" int viso_photometric_ba(viso_ctx* c, const uint8_t* const* kf_images,
                                    double* points, const int32_t* host, int32_t n, int32_t iterations,
                                    double* report) {
     if (!c || !kf_images || !kf_poses || !points || !host) return VISO_ERR_ARG;
-    if (n_kf < 2 || n_kf > kMaxKeyframes || n < 1 || iterations < 1 || iterations > 100) return VISO_ERR_ARG;
+    // n bounded as the pipeline's map (the block trees' stack depth and the
+    // launch grids are sized for kMaxMapPoints)
+    if (n_kf < 2 || n_kf > kMaxKeyframes || n < 1 || n > kMaxMapPoints || iterations < 1 || iterations > 100)
+        return VISO_ERR_ARG;
     for (int i = 0; i < n; ++i)
         if (host[i] < 0 || host[i] >= n_kf) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(c->device));
