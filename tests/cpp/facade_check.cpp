@@ -1,6 +1,7 @@
 // Compile/link check of the C++ facades (include/viso/viso.hpp, viso_svo.hpp,
 // viso_rig.hpp) against the C ABI; with a GPU (any argument) it runs a few
 // synthetic frames through each engine.
+#include <cmath>
 #include <cstdio>
 #include <vector>
 
@@ -8,6 +9,59 @@
 #include "viso/viso_rig.hpp"
 #include "viso/viso_svo.hpp"
 #include "viso/viso_synth.h"
+
+// A FrameHandler written against the reference's Keyframe accessors
+// (include/keyframe.h:50-112): it samples every frame the way Viso's loops do.
+struct SamplingHandler : viso::FrameSequence::FrameHandler {
+    double acc = 0.0;
+    void OnNewFrame(viso::Keyframe::Ptr kf) override {
+        kf->SetK({718.856, 0, 607.19, 0, 718.856, 185.22, 0, 0, 1});
+        const viso::V3d P{1.0, -0.5, 12.0};
+        for (int level = 0; level < 4; ++level) {
+            if (!kf->IsInside(P, level)) continue;
+            const viso::V2d uv = kf->Project(P, level);
+            const viso::V2d g = kf->GetGradient(uv[0], uv[1], level);
+            acc += kf->GetPixelValue(uv[0], uv[1], level) + g[0] + g[1] + kf->GetScale(level);
+        }
+        acc += kf->ViewingAngle(P) + (double)kf->Mat().cols + (double)kf->Pyramids().size();
+    }
+};
+
+// Keyframe accessors on frame 0 -> `path`: the four pyramid levels (as
+// Pyramids() returns them), then per sample (x, y, level): GetPixelValue,
+// GetGradient (2) -- compared with the oracle by tests/test_stereo_abi.py.
+static int dump_keyframe(const uint8_t* img, int W, int H, const char* path) {
+    viso::Keyframe kf(img, W, H, W);
+    const auto& pyr = kf.Pyramids();
+    if (pyr.size() != 4 || kf.Mat().data != kf.Data()) return 1;
+    std::FILE* f = std::fopen(path, "wb");
+    if (!f) return 1;
+    for (const auto& m : pyr) std::fwrite(m.data, 1, m.step * m.rows, f);
+    const double xs[5] = {10.25, 100.5, 333.75, 64.0, 140.125};
+    const double ys[5] = {7.5, 40.25, 20.0, 80.75, 30.5};
+    for (int level = 0; level < 4; ++level)
+        for (int k = 0; k < 5; ++k) {
+            const double s = kf.GetScale(level);
+            const double x = xs[k] * s * 2.0, y = ys[k] * s * 2.0;
+            const viso::V2d g = kf.GetGradient(x, y, level);
+            const double v[3] = {kf.GetPixelValue(x, y, level), g[0], g[1]};
+            std::fwrite(v, sizeof(double), 3, f);
+        }
+    // Project / IsInside / ViewingAngle with a pose and K (include/keyframe.h:82-98)
+    kf.SetR({0.8, -0.6, 0, 0.6, 0.8, 0, 0, 0, 1});
+    kf.SetT({0.1, -0.2, 0.3});
+    kf.SetK({718.856, 0, 607.19, 0, 718.856, 185.22, 0, 0, 1});
+    const viso::V3d P{1.0, -0.5, 12.0};
+    for (int level = 0; level < 4; ++level) {
+        const viso::V2d uv = kf.Project(P, level);
+        const double v[3] = {uv[0], uv[1], kf.IsInside(P, level) ? 1.0 : 0.0};
+        std::fwrite(v, sizeof(double), 3, f);
+    }
+    const double va = kf.ViewingAngle(P);
+    std::fwrite(&va, sizeof(double), 1, f);
+    std::fclose(f);
+    return 0;
+}
 
 int main(int argc, char** argv) {
     if (argc < 2) {
@@ -19,6 +73,21 @@ int main(int argc, char** argv) {
     viso_synth_default(&sp, W, H);
     std::vector<uint8_t> l(W * H), r(W * H);
     const int32_t dims[3] = {W, H, W};
+    viso_synth_render(&sp, 0, 0, l.data(), 4);
+    if (argc > 2 && dump_keyframe(l.data(), W, H, argv[2])) return 1;
+    {
+        // the reference's plugin shape: FrameSequence -> FrameHandler(Keyframe::Ptr)
+        SamplingHandler h;
+        viso::FrameSequence seq("frame", &h, [&](const std::string&, std::vector<uint8_t>* g, int* w, int* hh) {
+            *g = l;
+            *w = W;
+            *hh = H;
+            return true;
+        });
+        seq.RunOnce();
+        if (!(h.acc == h.acc) || h.acc == 0.0) return 1;
+        std::printf("handler: %.6f\n", h.acc);
+    }
     // the reference path, stereo-initialised
     viso::StereoViso vo(sp.fx, sp.fy, sp.cx, sp.cy, W, H, 0, true);
     vo.SetStereo(sp.baseline);

@@ -171,3 +171,51 @@ def test_gpu_rig_rejects_bad_arguments():
     g.process([img, img], [img, img])
     assert g.state == viso_amd._lib.STATE_INITIALIZATION
     assert len(g.poses) == 0
+
+
+@pytest.fixture(scope="module")
+def dense_rig_run():
+    """Two cameras at FAST threshold 20: > 4096 map points per camera, so a
+    camera spans more than 64 tiles of the largest tile size (64 points)."""
+    from viso_amd.synth import RigSequence
+    seq = RigSequence(W, H, seed=0, n_cams=2)
+    frames = [seq.frame(f) for f in range(3)]
+    r = oracle_lib.Rig(seq.K, W, H, seq.extrinsics(), seq.p.baseline, fast_thresh=20)
+    stats = []
+    for ls, rs in frames:
+        r.process(ls, rs)
+        stats.append(r.level_stats())
+    return seq, frames, r, stats
+
+
+def test_dense_rig_oracle_has_cameras_past_4096_points(dense_rig_run):
+    _, _, r, _ = dense_rig_run
+    assert r.state == 1
+    assert min(len(r.points(c)) for c in range(2)) > 4096
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["faithful", "fast"])
+def test_gpu_rig_past_4096_points_per_camera(dense_rig_run, precision):
+    """Cameras past 4096 points (tiles must stay <= 64 points):
+    faithful bit-exact map / nGood and poses <= 1e-10; tolerance mode <= 1e-4."""
+    import torch
+
+    import viso_amd
+    from viso_amd.rig import VisoRig
+    seq, frames, r, stats = dense_rig_run
+    prec = viso_amd.PRECISION_FAITHFUL if precision == "faithful" else viso_amd.PRECISION_FAST
+    g = VisoRig(*seq.K, W, H, seq.extrinsics(), precision=prec, fast_thresh=20)
+    g.set_stereo(seq.p.baseline, 128, 1)
+    for ls, rs in frames:
+        g.process(ls, rs)
+    torch.cuda.synchronize()
+    assert g.state == r.state == 1
+    for c in range(2):
+        assert np.array_equal(g.points(c), r.points(c)), c
+    rel = _rel(g.poses, r.poses)
+    if precision == "faithful":
+        assert rel.max() <= 1e-10, rel
+        assert np.array_equal(g.level_stats()[:, 0], stats[-1][:, 0])
+    else:
+        assert rel.max() < 1e-4, rel

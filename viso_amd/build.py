@@ -73,7 +73,7 @@ def build(verbose: bool = False) -> str:
     if os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(o) for o in objs):
         return LIB
     tmp = LIB + ".tmp"
-    cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", tmp, *objs, "-lpthread", "-lz"]
+    cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", tmp, *objs, "-lpthread", "-lz", "-lrocprofiler-sdk-roctx"]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -7,6 +7,7 @@
 #include "../../include/viso/viso_c.h"
 #include "geometry.hpp"
 #include "kernels.hpp"
+#include "trace.hpp"
 
 namespace viso {
 
@@ -80,11 +81,12 @@ struct Bump {
 };
 
 struct TimedRegion {
+    RoctxRange range;
     Timing& t;
     int kernel;
     hipStream_t s;
     hipEvent_t a = nullptr, b = nullptr;
-    TimedRegion(Timing& t_, int k, hipStream_t s_) : t(t_), kernel(k), s(s_) {
+    TimedRegion(Timing& t_, int k, hipStream_t s_) : range(phase_name(k)), t(t_), kernel(k), s(s_) {
         if (t.on(kernel)) {
             a = t.get_event();
             b = t.get_event();

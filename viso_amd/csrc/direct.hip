@@ -2,17 +2,21 @@
 // (DirectPoseEstimationSingleLayer / MultiLayer + dPixeldXi,
 // src/viso.cpp:640-766).
 //
-// One frame = five launches on one stream:
-//   L(3), L(2), L(1), L(0), F
-// L(l) (one workgroup of 8 waves per tile):
+// One frame = four launches on one stream in steady state:
+//   L(3), L(2), L(1), L(0)   (+ F, the final level-0 solve, which normally
+//   runs fused into the next frame's L(3); only the last frame of an ingest
+//   call gets a standalone F launch)
+// L(l) (one 16-wave workgroup per tile):
 //   prologue — every workgroup solves level l+1 from that level's tile
 //     partials (written by L(l+1)) and gets T21 for level l.  All workgroups
 //     compute the same bits, so no grid-wide hand-off is needed beyond the
 //     kernel boundary.  L(3) instead seeds T21 = SE3(R, t) of the last
-//     frame's pose (src/viso.cpp:114).
+//     frame's pose (src/viso.cpp:114), or, fused, solves the previous
+//     frame's level 0 first.
 //     Work that does not depend on T21 is issued first: the tile partial
-//     loads of level l+1, the wave's map point, its projection into the last
-//     frame and the `last` patch sample.
+//     loads of level l+1, and (waves off the solver's SIMD) the tile's map
+//     points, their projections into the last frame, the `last` patch taps
+//     and a current-image window around the predicted projection.
 //   tiles — one wave per map point, lane = patch pixel: J = -grad^T *
 //     dPixel/dXi, the 28 sums (21 upper-triangle J J^T, 6 -e J, e^2) by
 //     reduce-scatter (the canonical wave tree, common.hpp).  A workgroup owns
@@ -1009,7 +1013,14 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
 // (unchanged when the update is NaN).  Launches per frame: L(3..0) + F, the
 // tiles of all cameras in one grid (workgroup = one tile of one camera), the
 // prologue of L(l) solving level l+1 from every camera's tile partials.
-constexpr int kRigTiles = 64;  // tiles per camera (one wave reduces them)
+// Tiles per camera: up to 256 (T <= 64 points each covers kMaxMapPoints);
+// a camera's partials are reduced by 1, 2 or 4 waves (64 tiles each) and
+// the waves' sums folded as the canonical tree's top levels.
+constexpr int kRigTiles = kMaxTiles;
+constexpr int kRigTargetTiles = 64;  // faithful tiling aims at this many tiles per camera
+
+// waves reducing a camera of n_tiles tiles (the canonical tree over 64 q tiles)
+__device__ __host__ inline int rig_reduce_waves(int n_tiles) { return n_tiles <= 64 ? 1 : n_tiles <= 128 ? 2 : 4; }
 
 struct RigCamArgs {
     DirectArgs d;       // the camera's pyramids (fp: last, cur; fp.pose_last =
@@ -1051,12 +1062,25 @@ __device__ inline int rig_camera(const RigArgs& ra, int b) {
     return c;
 }
 
-// Wave 0 (after every camera's S_c is in red[c]): the rig's 28 sums into
-// L.S and nGood into L.ngood.  Lane e < 21 (upper-triangle entry (i, j)),
-// 21 + i (b_i) or 27 (cost) folds the cameras in ascending order.
-__device__ inline void rig_combine(const RigArgs& ra, const double (*red)[kSums], const int* g, double* sM,
+// Wave 0 (after every camera's wave sums are in red[c][0..q_c)): the rig's
+// 28 sums into L.S and nGood into L.ngood.  First S_c = the top of camera
+// c's canonical tree over its q_c waves (r0; r0 + r1; (r0 + r1) + (r2 + r3))
+// into red[c][0]; then lane e < 21 (upper-triangle entry (i, j)), 21 + i
+// (b_i) or 27 (cost) folds the cameras in ascending order.
+__device__ inline void rig_combine(const RigArgs& ra, double (*red)[4][kSums], const int (*g)[4], double* sM,
                                    SolveLds& L) {
     const int lane = threadIdx.x & 63;
+    int ng = 0;
+    for (int c = 0; c < ra.n_cams; ++c) {
+        const int q = rig_reduce_waves(ra.cam[c].d.n_tiles);
+        if (q > 1 && lane < kSums) {
+            const double v = q == 2 ? red[c][0][lane] + red[c][1][lane]
+                                    : (red[c][0][lane] + red[c][1][lane]) + (red[c][2][lane] + red[c][3][lane]);
+            red[c][0][lane] = v;
+        }
+        for (int j = 0; j < q; ++j) ng += g[c][j];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     // (i, j) of upper entry e, row-major over i <= j
     int ei = 0, ej = 0;
     {
@@ -1070,7 +1094,7 @@ __device__ inline void rig_combine(const RigArgs& ra, const double (*red)[kSums]
     }
     double acc = 0.0;
     for (int c = 0; c < ra.n_cams; ++c) {
-        const double* S = red[c];
+        const double* S = red[c][0];
         const double* Ad = ra.cam[c].Ad;
         // M = H_c Ad (lane l < 36: M[l / 6][l % 6])
         if (lane < 36) {
@@ -1101,19 +1125,15 @@ __device__ inline void rig_combine(const RigArgs& ra, const double (*red)[kSums]
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
     if (lane < kSums) L.S[lane] = acc;
-    if (lane == 0) {
-        int ng = 0;
-        for (int c = 0; c < ra.n_cams; ++c) ng += g[c];
-        L.ngood = ng;
-    }
+    if (lane == 0) L.ngood = ng;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
 template <bool FAST>
 __global__ __launch_bounds__(kThreads) void rig_level_kernel(RigArgs ra) {
     __shared__ SolveLds L;
-    __shared__ double s_red[kMaxRigCams][kSums];
-    __shared__ int s_g[kMaxRigCams];
+    __shared__ double s_red[kMaxRigCams][4][kSums];
+    __shared__ int s_g[kMaxRigCams][4];
     __shared__ double s_M[36];
     __shared__ double s_pose[12];
     __shared__ double s_pts[kMaxTile * kSums];
@@ -1133,30 +1153,34 @@ __global__ __launch_bounds__(kThreads) void rig_level_kernel(RigArgs ra) {
         s_good = 0;
     }
     lds_barrier();
-    // ---- every camera's tile partials of level sl (wave w: camera w)
-    if (solve && wave < ra.n_cams) {
-        const DirectArgs& aw = ra.cam[wave].d;
+    // ---- every camera's tile partials of level sl (wave w: camera w / 4,
+    // tiles 64 (w % 4) .. +63 of it, when the camera has that many waves)
+    static_assert(kWaves >= 4 * kMaxRigCams, "four reduce waves per camera");
+    const int rc = wave >> 2, rq = wave & 3;
+    if (solve && rc < ra.n_cams && rq < rig_reduce_waves(ra.cam[rc].d.n_tiles)) {
+        const DirectArgs& aw = ra.cam[rc].d;
+        const int tl = 64 * rq + lane;
         double v[kSums];
         int gg = 0;
-        if (lane < aw.n_tiles) {
+        if (tl < aw.n_tiles) {
             const double2* src =
-                reinterpret_cast<const double2*>(aw.s.part + ((size_t)sl * kRigTiles + lane) * kSums);
+                reinterpret_cast<const double2*>(aw.s.part + ((size_t)sl * kRigTiles + tl) * kSums);
 #pragma unroll
             for (int k = 0; k < kSums / 2; ++k) {
                 const double2 d = src[k];
                 v[2 * k] = d.x;
                 v[2 * k + 1] = d.y;
             }
-            gg = aw.s.good[sl * kRigTiles + lane];
+            gg = aw.s.good[sl * kRigTiles + tl];
         } else {
 #pragma unroll
             for (int k = 0; k < kSums; ++k) v[k] = 0.0;
         }
         int idx;
         const double f = reduce_scatter_28(v, &idx);
-        if (lane < 32 && idx >= 0) s_red[wave][idx] = f;
+        if (lane < 32 && idx >= 0) s_red[rc][rq][idx] = f;
         const int g = wave_sum_int(gg);
-        if (lane == 0) s_g[wave] = g;
+        if (lane == 0) s_g[rc][rq] = g;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (lane == 0) atomicAdd(&s_arrive, 1);
     }
@@ -1199,7 +1223,9 @@ __global__ __launch_bounds__(kThreads) void rig_level_kernel(RigArgs ra) {
     }
     // ---- the solve (wave 0)
     if (wave == 0) {
-        const int need = solve ? ra.n_cams + 1 : 1;
+        int need = 1;
+        if (solve)
+            for (int cc = 0; cc < ra.n_cams; ++cc) need += rig_reduce_waves(ra.cam[cc].d.n_tiles);
         while (__hip_atomic_load(&s_arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
             __builtin_amdgcn_s_sleep(1);
         if (solve) {
@@ -1359,20 +1385,29 @@ void launch_direct_final(const FrameDev& last_pyr, const FrameDev& cur_pyr, cons
         direct_level_kernel<false><<<1, kThreads, 0, stream>>>(a);
 }
 
-// Tiles of a rig camera with n points under a cap of max_tiles (<= 64):
-// faithful: the smallest power-of-two tile >= max(8, P / 64) that fits;
-// tolerance mode: min(n, max_tiles) even slices.
-static void rig_tiling(int n, int max_tiles, bool split, int* tile, int* n_tiles) {
+// Tiles of a rig camera with n <= kMaxMapPoints points:
+// faithful: T = min(max(8, P / 64), kMaxTile) (a power of two, so tiles are
+// aligned subtrees of the camera's canonical tree): 64 tiles up to 4096
+// points, up to kRigTiles above;
+// tolerance mode: min(n, 64) even slices, more when a slice would exceed
+// kMaxTile points.
+static int rig_tiling(int n, bool split, int* tile, int* n_tiles) {
+    if (n < 0 || n > kMaxMapPoints) return -1;
     int P = 1;
     while (P < n) P <<= 1;
-    int T = P / kRigTiles > kMinTile ? P / kRigTiles : kMinTile;
-    while ((n + T - 1) / T > max_tiles && T < kMaxTile) T <<= 1;
+    int T = P / kRigTargetTiles > kMinTile ? P / kRigTargetTiles : kMinTile;
+    if (T > kMaxTile) T = kMaxTile;  // more than 64 tiles then (P > 4096)
+    while ((n + T - 1) / T > kRigTiles && T < kMaxTile) T <<= 1;
     *tile = T;
     *n_tiles = (n + T - 1) / T;
     if (split && n > 0) {
-        *n_tiles = n < max_tiles ? n : max_tiles;
-        *tile = (n + *n_tiles - 1) / *n_tiles;
+        int nt = n < kRigTargetTiles ? n : kRigTargetTiles;
+        if ((n + nt - 1) / nt > kMaxTile) nt = (n + kMaxTile - 1) / kMaxTile;
+        *n_tiles = nt;
+        *tile = (n + nt - 1) / nt;
     }
+    // the prefetch and tile tree hold at most kMaxTile points per workgroup
+    return (*tile <= kMaxTile && *n_tiles <= kRigTiles) ? 0 : -1;
 }
 
 size_t rig_scratch_bytes() { return (size_t)kLevels * kRigTiles * kSums * 8 + (size_t)kLevels * kRigTiles * 4; }
@@ -1384,7 +1419,6 @@ int launch_rig_direct(const RigCamDev* cams, int n_cams, const PyrGeom& g, const
     const bool fast = precision == VISO_PRECISION_FAST;
     RigArgs ra{};
     ra.n_cams = n_cams;
-    const int cap = std::min(kRigTiles, kMaxTiles / n_cams);
     int off = 0;
     for (int c = 0; c < n_cams; ++c) {
         const RigCamDev& cd = cams[c];
@@ -1396,7 +1430,7 @@ int launch_rig_direct(const RigCamDev* cams, int n_cams, const PyrGeom& g, const
         a.K = Intrinsics{K[0], K[1], K[2], K[3]};
         a.points = cd.points;
         a.n = cd.n;
-        rig_tiling(cd.n, cap, fast, &a.tile, &a.n_tiles);
+        if (rig_tiling(cd.n, fast, &a.tile, &a.n_tiles) != 0) return -1;
         a.split = fast && cd.n > 0 ? 1 : 0;
         a.s.part = (double*)cd.scratch;
         a.s.good = (int*)((char*)cd.scratch + (size_t)kLevels * kRigTiles * kSums * 8);

@@ -484,6 +484,7 @@ int viso_ctx::stereo_init(int cur, bool* made) {
 
 // ------------------------------------------------------------------ OnNewFrame
 int viso_ctx::on_new_frame(int cur) {
+    RoctxRange range("viso:frame");
     const PyrGeom& g = geom;
     hold(cur);  // the "cur_frame" shared_ptr, released on every return
     struct CurRef {
@@ -736,6 +737,7 @@ int viso_process_frames_device(viso_ctx* c, const uint8_t* d_left, const uint8_t
     VISO_HIP_CHECK(hipSetDevice(c->device));
     const int B = c->p.batch_frames;
     for (int f0 = 0; f0 < n; f0 += B) {
+        RoctxRange range("viso:ingest_chunk");
         const int nb = std::min(B, n - f0);
         std::vector<int> sl;
         std::vector<const uint8_t*> l0;

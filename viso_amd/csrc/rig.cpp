@@ -161,6 +161,7 @@ int viso_rig::stereo_init(const uint8_t* const* right_l0, bool* made) {
 }
 
 int viso_rig::step(const uint8_t* const* left_l0, const uint8_t* const* right_l0) {
+    RoctxRange range("rig:timestep");
     const PyrGeom& g = geom;
     const size_t npx = (size_t)g.w[0] * g.h[0];
     const uint8_t* l0[kMaxRigCams];

@@ -33,6 +33,7 @@
 
 #include "../../include/viso/viso_svo.h"
 #include "common.hpp"
+#include "trace.hpp"
 
 namespace viso {
 namespace {
@@ -1819,6 +1820,7 @@ struct viso_svo {
     }
     // a batch of nb <= tb timesteps: features, motions, poses
     int batch(const ImgSrc& imgs, int nb) {
+        RoctxRange range("svo:batch");
         int rc = detect(imgs, nb);
         if (rc) return rc;
         const int b0 = frame == 0 ? 1 : 0;
