@@ -40,8 +40,12 @@ def main():
     if stereo:  # the bench path: stereo-initialised map
         v.set_stereo(seq.p.baseline, 128, 1)
     lib = _lib.load()
-    lib.viso_debug_probe.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
-    buf = (ctypes.c_ulonglong * 128)()
+    lib.viso_debug_probe_ring.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                          ctypes.c_int]
+    cap = 4096
+    log = np.zeros((cap, 16), np.uint64)
+    exits = np.zeros(cap, np.uint64)
+    nl = ctypes.c_int(0)
 
     def run(f0, m):
         f = f0
@@ -55,45 +59,54 @@ def main():
     lkbuf = (ctypes.c_ulonglong * 16)()
     run(0, warm)
     v.synchronize()
-    lib.viso_debug_probe(buf, 128, 1)
+    assert lib.viso_debug_probe_ring(log.ctypes.data, exits.ctypes.data, cap, ctypes.byref(nl), 1) == 0
     lib.viso_debug_probe_lk(lkbuf, 1)
     run(warm, steps)
     v.synchronize()
     print(f"map points {len(v.GetPoints())}, state {v.state}")
-    assert lib.viso_debug_probe(buf, 128, 0) == 0
+    assert lib.viso_debug_probe_ring(log.ctypes.data, exits.ctypes.data, cap, ctypes.byref(nl), 0) == 0
+    n = min(nl.value, cap)
+    log, exits = log[:n].astype(np.int64), exits[:n].astype(np.int64)
     lib.viso_debug_probe_lk(lkbuf, 0)
     q = list(lkbuf)
     print("LK alignment: mean GN iterations per (pair, level):",
           ", ".join(f"L{l} {q[l] / max(q[4 + l], 1):.2f} ({q[4 + l]} calls)" for l in range(4)))
-    print(f"  (pair, level) with >= 10 iterations: {q[8]}")
-    calls = max(sum(q[4:8]), 1)
-    print(f"  per (pair, level): template+window {10.0 * q[12] / calls / 1e3:.2f} us, "
-          f"iterations {10.0 * q[13] / calls / 1e3:.2f} us; per pair (4 levels) "
-          f"{10.0 * q[14] / max(q[15], 1) / 1e3:.2f} us")
-    p = list(buf)
-    us = lambda x, c: 10.0 * x / max(c, 1) / 1e3  # 100 MHz ticks -> us
-    print("launch  count  prologue-done  block0-done   (us from entry, block 0)")
-    for k, name in enumerate(["F", "L(0)", "L(1)", "L(2)", "L(3)"]):
-        c = p[16 + k]
-        print(f"{name:6s} {c:6d}  {us(p[k], c):12.2f}  {us(p[8 + k], c):11.2f}")
-    print("prologue phases (us from entry): B1  S-combined  solved  prologue-done")
-    for k, name in enumerate(["F", "L(0)", "L(1)", "L(2)", "L(3)"]):
-        c = p[16 + k]
-        ph = [us(p[32 + 6 * k + j], c) for j in range(3)]
-        print(f"{name:6s} {ph[0]:8.2f} {ph[1]:8.2f} {ph[2]:8.2f} {us(p[k], c):8.2f}")
-    c = p[16 + 2]
-    print("L(1) solve_wave0 (us from entry): LU %.2f  inverse %.2f  update %.2f  exp %.2f" %
-          tuple(us(p[90 + k], c) for k in range(4)))
-    if p[96]:
-        print("L(1) solve: %.0f shader clocks in %.2f us -> %.2f GHz" %
-              (p[95] / max(c, 1), us(p[96], c), p[95] / (10.0 * p[96])))
-    stamps = [x for x in p[64:84] if x]
-    t0 = min(stamps)
-    print("last frame timeline (us from the first launch entry):")
-    for k, name in [(4, "L(3)"), (3, "L(2)"), (2, "L(1)"), (1, "L(0)"), (0, "F")]:
-        a, b = (p[64 + 4 * k] - t0) * 0.01, (p[65 + 4 * k] - t0) * 0.01
-        last = (p[100 + k] - t0) * 0.01
-        print(f"  {name:5s} entry {a:7.2f}  block0 exit {b:7.2f}  last block exit {last:7.2f}")
+    us = 0.01  # 100 MHz ticks -> us
+    meta = log[:, 15]
+    lvl = (meta & 0xff) - 1
+    merged = (meta >> 8) & 0xff
+    tiles = meta >> 16
+    entry = log[:, 0]
+    print(f"{n} launches; tiles per launch {int(np.median(tiles))}")
+    names = ["partials reduced (w0)", "solver starts", "LU", "inverse", "update", "SE3 exp", "solve done",
+             "after B2", "prefetch done (last wave)", "-", "block 0 exit"]
+    print("phase (us from block 0 entry; mean over launches)      " +
+          "  ".join(f"{x:>7s}" for x in ["F", "L0", "L1", "L2", "L3m", "L3"]))
+    kinds = [(lvl == -1), (lvl == 0), (lvl == 1), (lvl == 2), (lvl == 3) & (merged == 1), (lvl == 3) & (merged == 0)]
+    for k, name in enumerate(names, start=1):
+        if name == "-":
+            continue
+        row = []
+        for m in kinds:
+            sel = m & (log[:, k] > 0)
+            row.append(f"{(log[sel, k] - entry[sel]).mean() * us:7.2f}" if sel.any() else "      -")
+        print(f"  {name:52s}" + "  ".join(row))
+    row = []
+    for m in kinds:
+        sel = m & (exits > 0)
+        row.append(f"{(exits[sel] - entry[sel]).mean() * us:7.2f}" if sel.any() else "      -")
+    print(f"  {'last block exit':52s}" + "  ".join(row))
+    # boundaries: consecutive launches of one frame's chain
+    gaps = {}
+    for i in range(n - 1):
+        a, b = lvl[i], lvl[i + 1]
+        if (a, b) in [(3, 2), (2, 1), (1, 0), (0, 3)] and exits[i] > 0:
+            gaps.setdefault((a, b), []).append((entry[i + 1] - exits[i]) * us)
+    print("boundary: last block exit -> next launch's block 0 entry (us): " +
+          ", ".join(f"L{a}->L{b} {np.mean(g):.2f} (n={len(g)})" for (a, b), g in sorted(gaps.items())))
+    per = [(entry[i + 1] - entry[i]) * us for i in range(n - 1) if (lvl[i], lvl[i + 1]) in [(3, 2), (2, 1), (1, 0), (0, 3)]]
+    print(f"entry-to-entry per launch in the chain: {np.mean(per):.2f} us")
+
 
 if __name__ == "__main__":
     main()

@@ -31,6 +31,10 @@ COMMON = ["-std=c++17", "-O3", "-fPIC", "-ffp-contract=off", f"--offload-arch={A
           "-Wno-unused-variable", "-Wno-unused-result"]
 if VARIANT == "probe":
     COMMON.append("-DVISO_PROBE")
+# experiment builds (dev): extra -D flags for a variant library, e.g.
+# VISO_VARIANT=lk4 VISO_DEFS="-DVISO_LK_MIN_WAVES=4"
+if VARIANT and os.environ.get("VISO_DEFS"):
+    COMMON.extend(os.environ["VISO_DEFS"].split())
 
 
 def _headers():

@@ -123,12 +123,23 @@ __device__ inline double wave_tree_sum(double v) {
     return v;
 }
 
-// DPP move of both halves of a double (all 64 lanes must be active).
+// DPP move of both halves of a double (all 64 lanes must be active).  Lanes
+// without a source lane read 0 (bound_ctrl), so no "old" value has to be
+// materialised first.
 template <int CTRL>
 __device__ inline double dpp_f64(double v) {
     const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffLL), CTRL, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffffLL), CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, true);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// A wave-uniform value made visibly uniform to the compiler (exact: every
+// lane holds the same bits), so branches on it need no EXEC bookkeeping.
+__device__ inline double uniform_f64(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffffLL));
+    const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
@@ -283,7 +294,7 @@ __device__ inline double reduce_scatter_28(const double* v, int* value_index) {
 // ---- fp32 forms (tolerance mode, VISO_PRECISION_FAST)
 template <int CTRL>
 __device__ inline float dpp_f32(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
 }
 
 __device__ inline void permlane16_swap_f32(float a, float b, float& ra, float& rb) {

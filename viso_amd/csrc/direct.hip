@@ -43,30 +43,33 @@
 #include "direct_solve.hpp"
 #include "kernels.hpp"
 
-// Phase probes (build with VISO_VARIANT=probe; tools/probe_direct.py): block
-// 0, thread 0 accumulates s_memrealtime (100 MHz) deltas from kernel entry
-// and records absolute entry/exit stamps of the last frame's launches.
+// Phase probes (build with VISO_VARIANT=probe; tools/probe_direct.py).
+// Block 0 keeps s_memrealtime stamps (100 MHz) of its phases in scalar
+// registers (every lane of the stamping wave takes the same value) and
+// stores them once, with plain stores, at its exit into a ring slot per
+// launch; every block's thread 0 raises the launch's exit stamp by a
+// non-returning atomic max.  No stamp waits on memory, so the probe does not
+// lengthen the phases it measures.  Stamps: 0 entry, 1 wave 0's partials
+// reduced, 2 the solver starts (S combined), 3 LU, 4 inverse, 5 update,
+// 6 SE3 exp, 7 solve finished, 8 after B2, 9 the last prefetch wave of block
+// 0 done (LDS max), 10 block 0's tiles evaluated, 11 block 0 exit; 15 meta =
+// (level + 1) | merged << 8 | n_tiles << 16.
 #ifdef VISO_PROBE
-__device__ unsigned long long g_probe[128];
-#define PROBE_T0() const unsigned long long probe_t0 = __builtin_amdgcn_s_memrealtime()
-#define PROBE(i)                                                                        \
-    do {                                                                                \
-        if (threadIdx.x == 0 && blockIdx.x == 0)                                        \
-            g_probe[(i)] += __builtin_amdgcn_s_memrealtime() - probe_t0;                \
-    } while (0)
-#define PROBE_ABS(i)                                                                    \
-    do {                                                                                \
-        if (threadIdx.x == 0 && blockIdx.x == 0) g_probe[(i)] = __builtin_amdgcn_s_memrealtime(); \
-    } while (0)
-#define PROBE_MAX(i)                                                                    \
-    do {                                                                                \
-        if (threadIdx.x == 0) atomicMax(&g_probe[(i)], __builtin_amdgcn_s_memrealtime()); \
+constexpr int kPRing = 4096;
+constexpr int kPSt = 16;
+__device__ unsigned long long g_plog[kPRing][kPSt];
+__device__ unsigned long long g_pexit[kPRing];
+#define PROBE_DECL()                                \
+    __shared__ unsigned long long pst[kPSt];        \
+    const unsigned long long probe_t0 = __builtin_amdgcn_s_memrealtime()
+// lane 0 of the calling wave (block 0) records stamp k in LDS
+#define PST(k)                                                                       \
+    do {                                                                             \
+        if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) pst[(k)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #else
-#define PROBE_MAX(i)
-#define PROBE_T0()
-#define PROBE(i)
-#define PROBE_ABS(i)
+#define PROBE_DECL()
+#define PST(k)
 #endif
 
 namespace viso {
@@ -124,6 +127,7 @@ struct DirectArgs {
     // prologue solves the previous frame's level 0, writes its pose (+ log),
     // and seeds T21 from it (it is this frame's `last` pose)
     int merged;
+    int probe_seq;   // probe builds: the launch's ring slot
     FramePair prev;  // the previous frame's pair (its rare continuation)
     double* prev_pose_out;
     double* prev_log;
@@ -829,8 +833,7 @@ __device__ inline void after_solve(const DirectArgs& a, bool merged, SolveLds& L
 //   barrier) hands the new pose to every wave; then the tiles.
 template <bool FAST>
 __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
-    PROBE_T0();
-    PROBE_ABS(64 + 4 * (a.level + 1));
+    PROBE_DECL();
     __shared__ SolveLds L;
     __shared__ double s_pose[12];
     __shared__ double s_last[12];  // merged L(3): this frame's `last` pose
@@ -848,6 +851,10 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
     if (t == 0) {
         s_arrive = 0;
         s_good = 0;
+#ifdef VISO_PROBE
+        for (int k = 0; k < kPSt; ++k) pst[k] = 0;
+        pst[0] = probe_t0;
+#endif
     }
     lds_barrier();  // nothing is in flight yet
 
@@ -887,7 +894,7 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (lane == 0) atomicAdd(&s_arrive, 1);
     }
-    PROBE(32 + 6 * (lv + 1));
+    if (wave == 0) PST(1);
 
     // ---- prefetch of the whole tile (every wave but the solver): the pose
     // the windows are predicted at is the seed (unsolved L(3)) or the T21
@@ -911,6 +918,10 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
         // merged: the `last` pose is this launch's solve of the previous
         // frame's level 0, predicted by the T21 that level was evaluated at
         prefetch_tile(a, lv, blockIdx.x, pred, merged ? pred : a.fp.pose_last, true, first, stride, s_pf);
+#ifdef VISO_PROBE
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        if (blockIdx.x == 0 && lane == 0) atomicMax(&pst[9], __builtin_amdgcn_s_memrealtime());
+#endif
     }
 
     // ---- the solve (wave 0)
@@ -921,28 +932,23 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
         // canonical tree, last level: (w0 + w1) + (w2 + w3)
         if (lane < kSums) L.S[lane] = (L.red[0][lane] + L.red[1][lane]) + (L.red[2][lane] + L.red[3][lane]);
         if (lane == 0) L.ngood = (L.g[0] + L.g[1]) + (L.g[2] + L.g[3]);
-        PROBE(32 + 6 * (lv + 1) + 1);
+        PST(2);
         double* stp = (a.stats && blockIdx.x == 0) ? a.stats + (size_t)kStats * sl : nullptr;
 #ifdef VISO_PROBE
-        // shader clock over the solve: s_memtime (core clock) vs s_memrealtime (100 MHz)
-        const unsigned long long clk0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
         unsigned long long stamps[4] = {probe_t0, probe_t0, probe_t0, probe_t0};
         if (FAST)
-            solve_wave0_ldlt(L, 0, stp, lv == 1 ? stamps : nullptr);
+            solve_wave0_ldlt(L, 0, stp, stamps);
         else
-            solve_wave0(L, 0, stp, lv == 1 ? stamps : nullptr);
-        if (lv == 1 && lane == 0 && blockIdx.x == 0) {
-            for (int k = 0; k < 4; ++k) g_probe[90 + k] += stamps[k] - probe_t0;
-            g_probe[95] += __builtin_amdgcn_s_memtime() - clk0;
-            g_probe[96] += __builtin_amdgcn_s_memrealtime() - rt0;
-        }
+            solve_wave0(L, 0, stp, stamps);
+        if (blockIdx.x == 0 && lane == 0)
+            for (int k = 0; k < 4; ++k) pst[3 + k] = stamps[k];
 #else
         if (FAST)
             solve_wave0_ldlt(L, 0, stp);
         else
             solve_wave0(L, 0, stp);
 #endif
-        PROBE(32 + 6 * (lv + 1) + 2);
+        PST(7);
         __builtin_amdgcn_s_setprio(0);
     }
     if (!solve && wave == 0 && lane == 0) {
@@ -971,7 +977,7 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
         }
         __syncthreads();
     }
-    PROBE(lv + 1);
+    if (wave == 0) PST(8);
     const int out = lv >= 0 ? lv : kLevels;
     if (blockIdx.x == 0 && t == 0 && !merged) {
         for (int k = 0; k < 7; ++k) a.s.state[out * kStateStride + k] = L.state[k];
@@ -993,11 +999,18 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
         direct_tile_pf<FAST>(a, fp, lv, pose, blockIdx.x, s_pf, merged, a.s.part + (size_t)lv * kMaxTiles * kSums,
                        a.s.good + lv * kMaxTiles, s_pts, &s_good);
     }
-    PROBE(8 + lv + 1);
-    PROBE_ABS(65 + 4 * (a.level + 1));
-    PROBE_MAX(100 + lv + 1);
 #ifdef VISO_PROBE
-    if (threadIdx.x == 0 && blockIdx.x == 0) g_probe[16 + lv + 1] += 1;
+    // block 0 exit: its stamps to the launch's ring slot; every block raises
+    // the launch's exit stamp (non-returning atomic)
+    const unsigned long long t_exit = __builtin_amdgcn_s_memrealtime();
+    const int slot = a.probe_seq & (kPRing - 1);
+    if (t == 0) atomicMax(&g_pexit[slot], t_exit);
+    if (blockIdx.x == 0 && t == 0) {
+        pst[11] = t_exit;
+        pst[15] = (unsigned long long)(lv + 1) | ((unsigned long long)merged << 8) |
+                  ((unsigned long long)a.n_tiles << 16);
+        for (int k = 0; k < kPSt; ++k) g_plog[slot][k] = pst[k];
+    }
 #endif
 }
 
@@ -1313,6 +1326,14 @@ DirectScratch direct_scratch_at(void* base) {
 }
 
 namespace {
+// probe builds: ring slot of the next direct-pose launch (0 otherwise)
+#ifdef VISO_PROBE
+static unsigned g_probe_host_seq = 0;
+int next_probe_seq() { return (int)(g_probe_host_seq++); }
+#else
+int next_probe_seq() { return 0; }
+#endif
+
 DirectArgs direct_args(const FrameDev& last_pyr, const FrameDev& cur_pyr, const PyrGeom& g,
                        const double K[4], const double* points, int n, const double* pose_last12,
                        const double* pose_seed12, const DirectScratch& s, double* stats, bool split) {
@@ -1361,6 +1382,7 @@ void launch_direct_levels(const FrameDev& last_pyr, const FrameDev& cur_pyr, con
     const int grid = a.n_tiles > 0 ? a.n_tiles : 1;
     for (int level = kLevels - 1; level >= 0; --level) {
         a.level = level;
+        a.probe_seq = next_probe_seq();
         if (precision == VISO_PRECISION_FAST)
             direct_level_kernel<true><<<grid, kThreads, 0, stream>>>(a);
         else
@@ -1379,6 +1401,7 @@ void launch_direct_final(const FrameDev& last_pyr, const FrameDev& cur_pyr, cons
     a.log = log;
     a.log_index = log ? log_index : -1;
     a.level = -1;
+    a.probe_seq = next_probe_seq();
     if (precision == VISO_PRECISION_FAST)
         direct_level_kernel<true><<<1, kThreads, 0, stream>>>(a);
     else
@@ -1478,13 +1501,29 @@ void launch_direct_pose(const FrameDev& last_pyr, const FrameDev& cur_pyr, const
 }  // namespace viso
 
 #ifdef VISO_PROBE
-extern "C" int viso_debug_probe(unsigned long long* out, int n, int reset) {
-    if (n > 128) n = 128;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_probe), sizeof(unsigned long long) * n) != hipSuccess)
-        return -2;
+// The direct-pose probe ring: *n_launches = launches since the last reset;
+// log (cap x 16 stamps) and exits (cap) in launch order for the last
+// min(cap, n, 4096) launches.
+extern "C" int viso_debug_probe_ring(unsigned long long* log, unsigned long long* exits, int cap, int* n_launches,
+                                     int reset) {
+    using namespace viso;
+    static unsigned long long hlog[kPRing][kPSt], hexit[kPRing];
+    if (hipDeviceSynchronize() != hipSuccess) return -2;
+    if (hipMemcpyFromSymbol(hlog, HIP_SYMBOL(g_plog), sizeof(hlog)) != hipSuccess) return -2;
+    if (hipMemcpyFromSymbol(hexit, HIP_SYMBOL(g_pexit), sizeof(hexit)) != hipSuccess) return -2;
+    const int n = (int)g_probe_host_seq;
+    const int m = std::min(std::min(cap, n), kPRing);
+    for (int i = 0; i < m; ++i) {
+        const int s = (n - m + i) & (kPRing - 1);
+        for (int k = 0; k < kPSt; ++k) log[(size_t)i * kPSt + k] = hlog[s][k];
+        exits[i] = hexit[s];
+    }
+    *n_launches = n;
     if (reset) {
-        static unsigned long long zero[128] = {};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_probe), zero, sizeof(zero)) != hipSuccess) return -2;
+        static unsigned long long z1[kPRing][kPSt] = {}, z2[kPRing] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_plog), z1, sizeof(z1)) != hipSuccess) return -2;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_pexit), z2, sizeof(z2)) != hipSuccess) return -2;
+        g_probe_host_seq = 0;
     }
     return 0;
 }

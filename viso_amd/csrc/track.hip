@@ -101,24 +101,29 @@ __device__ inline Window load_window(uint8_t* lds, const uint8_t* img, int w, in
     return window_commit(lds, window_issue(img, w, h, cx, cy));
 }
 
-// sample_px with the tap fetch served from the window when possible
+// sample_px with the tap fetch served from the window when possible.  The
+// window test is taken for the whole wave (one ballot): in the common case
+// every lane's taps are in the window and the wave runs the LDS path without
+// per-lane branching; otherwise each lane takes its own path.  Requires all
+// 64 lanes active (the LK engines' wave-uniform control flow).
+__device__ inline double win_bilinear(const Window& win, double x, double y, int ix, int iy) {
+    const int o = (iy - win.y0) * kWinW + (ix - win.x0);
+    const double d0 = (double)ld_lds_u8(win.lds, o), d1 = (double)ld_lds_u8(win.lds, o + 1);
+    const double d2 = (double)ld_lds_u8(win.lds, o + kWinW);
+    const double d3 = (double)ld_lds_u8(win.lds, o + kWinW + 1);
+    const double xx = x - floor(x);
+    const double yy = y - floor(y);
+    return double((1 - xx) * (1 - yy) * d0 + xx * (1 - yy) * d1 + (1 - xx) * yy * d2 + xx * yy * d3);
+}
+
 __device__ inline double sample_win(const uint8_t* __restrict__ img, int w, int h, double x,
                                     double y, const Window& win) {
     const bool finite = (x > -1e9 && x < 1e9 && y > -1e9 && y < 1e9);
-    if (__builtin_expect(finite && win.lds != nullptr, 1)) {
-        const int ix = (int)x, iy = (int)y;
-        if (__builtin_expect(ix >= win.x0 && ix + 1 < win.x0 + kWinW && iy >= win.y0 && iy + 1 < win.y0 + kWinH, 1)) {
-            const int o = (iy - win.y0) * kWinW + (ix - win.x0);
-            const double d0 = (double)ld_lds_u8(win.lds, o), d1 = (double)ld_lds_u8(win.lds, o + 1);
-            const double d2 = (double)ld_lds_u8(win.lds, o + kWinW);
-            const double d3 = (double)ld_lds_u8(win.lds, o + kWinW + 1);
-            const double xx = x - floor(x);
-            const double yy = y - floor(y);
-            return double((1 - xx) * (1 - yy) * d0 + xx * (1 - yy) * d1 + (1 - xx) * yy * d2 +
-                          xx * yy * d3);
-        }
-    }
-    return sample_px(img, w, h, x, y);
+    const int ix = finite ? (int)x : 0, iy = finite ? (int)y : 0;
+    const bool in = finite && win.lds != nullptr && ix >= win.x0 && ix + 1 < win.x0 + kWinW && iy >= win.y0 &&
+                    iy + 1 < win.y0 + kWinH;
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(!in) == 0, 1)) return win_bilinear(win, x, y, ix, iy);
+    return in ? win_bilinear(win, x, y, ix, iy) : sample_px(img, w, h, x, y);
 }
 
 // The per-level template of the inverse-compositional LK: this lane's
@@ -166,6 +171,14 @@ __device__ inline LkResult lk_iterate(const LkTemplate& t, int w1, int h1,
                                       double cur_x, double cur_y, double bx, double by, double dx,
                                       double dy, double thresh, const Window& win) {
     const double hp = 4.0;
+    // the control values are wave-uniform (the sums are read from one lane):
+    // said so to the compiler, the loop's branches need no EXEC bookkeeping
+    bx = uniform_f64(bx);
+    by = uniform_f64(by);
+    dx = uniform_f64(dx);
+    dy = uniform_f64(dy);
+    const double i00 = uniform_f64(t.i00), i01 = uniform_f64(t.i01), i10 = uniform_f64(t.i10),
+                 i11 = uniform_f64(t.i11);
     double cost = 0, lastCost = 0;
     bool succ = true;
     int iter = 0;
@@ -184,8 +197,8 @@ __device__ inline LkResult lk_iterate(const LkTemplate& t, int w1, int h1,
         const double e = t.I1 - sample_win(img2, w2, h2, cur_x + dx, cur_y + dy, win);
         double B0, B1;
         wave_tree_sum3(-t.J0 * e, -t.J1 * e, e * e, B0, B1, cost);
-        const double u0 = t.i00 * B0 + t.i01 * B1;
-        const double u1 = t.i10 * B0 + t.i11 * B1;
+        const double u0 = i00 * B0 + i01 * B1;
+        const double u1 = i10 * B0 + i11 * B1;
         if (isnan(u0)) {
             succ = false;
             break;
@@ -276,7 +289,7 @@ __global__ __launch_bounds__(256) void klt_kernel(FrameDev ref, FrameDev cur, Py
                                                   uint8_t* __restrict__ success, int n,
                                                   double thresh) {
     __shared__ uint8_t s_win[4][kWinW * kWinH];
-    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int i = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     if (i >= n) return;  // wave-uniform
     const int lane = threadIdx.x & 63;
     const int px = (lane >> 3) - 4, py = (lane & 7) - 4;
@@ -404,10 +417,14 @@ __global__ __launch_bounds__(256) void lk_template_kernel(LkAlignArgs a) {
 // x are point groups; the grid's x extent is a multiple of 8, so a point
 // group stays on one XCD for every frame and its templates stay in that
 // XCD's L2.
+// waves per SIMD the register allocation must allow (5: <= 96 VGPRs)
+#ifndef VISO_LK_MIN_WAVES
+#define VISO_LK_MIN_WAVES 5
+#endif
 template <bool FAST>
-__global__ __launch_bounds__(256, 4) void lk_align_kernel(LkAlignArgs a) {
+__global__ __launch_bounds__(256, VISO_LK_MIN_WAVES) void lk_align_kernel(LkAlignArgs a) {
     __shared__ uint8_t s_win[4][2][kWinW * kWinH];
-    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int i = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     if (i >= a.n) return;
     // frame of the batch (blockIdx.y): its pyramid, pose and output rows
     // run-time indices into the kernel argument are read straight from the
