@@ -317,7 +317,7 @@ int oracle_ransac_homography(const double* p1, const double* p2, int n, double t
                 ++idx;
             }
         double ev[9], V[81];
-        jacobi_eigen<9>(M, ev, V);
+        jacobi_eigen_rr<9>(M, ev, V);  // the device's parallel (round-robin) ordering
         for (int k = 0; k < 9; ++k) H[k] = V[9 * k + 8];
     }
     if (std::fabs(H[8]) > 1e-12) {

@@ -119,6 +119,101 @@ inline void jacobi_eigen(const double* Ain, double* evals, double* evecs) {
     }
 }
 
+// Parallel-ordered (round-robin) Jacobi eigen-decomposition of a symmetric
+// N x N matrix: the device's ordering of the 9 x 9 H-refine moment matrix
+// (viso_amd/csrc/linalg.hpp jacobi_eigen_rr9).  Players 0..N-1 (+ a dummy
+// when N is odd) in M - 1 rounds of the circle method: round r pairs
+// arr[i] with arr[M-1-i], arr = {0, 1 + (j - 1 + r) mod (M-1) for j = 1..M-1};
+// pairs with the dummy are dropped.  Within a round every rotation (c, s) is
+// computed from the round's starting A (a pair with a_pq == 0 is skipped),
+// then every column pair of A is rotated, then every row pair, then the
+// column pairs of V -- the same operations a lane per (pair, index) does on
+// the device.  Sweep test, stop rule and the descending sort as
+// jacobi_eigen.
+template <int N>
+inline void jacobi_eigen_rr(const double* Ain, double* evals, double* evecs) {
+    constexpr int M = N + (N & 1), R = M - 1, P = M / 2;
+    double A[N * N], V[N * N];
+    for (int i = 0; i < N * N; ++i) {
+        A[i] = Ain[i];
+        V[i] = (i % (N + 1) == 0) ? 1.0 : 0.0;
+    }
+    for (int sweep = 0; sweep < 50; ++sweep) {
+        double off = 0, diag = 0;
+        for (int p = 0; p < N; ++p) {
+            diag = diag + A[N * p + p] * A[N * p + p];
+            for (int q = p + 1; q < N; ++q) off = off + A[N * p + q] * A[N * p + q];
+        }
+        if (off <= 1e-30 * diag || off == 0.0) break;
+        for (int r = 0; r < R; ++r) {
+            int arr[M];
+            arr[0] = 0;
+            for (int j = 1; j < M; ++j) arr[j] = 1 + (j - 1 + r) % (M - 1);
+            int pp[P], qq[P];
+            double cc[P], ss[P];
+            bool act[P];
+            for (int i = 0; i < P; ++i) {
+                const int a = arr[i], b = arr[M - 1 - i];
+                pp[i] = a < b ? a : b;
+                qq[i] = a < b ? b : a;
+                act[i] = qq[i] < N && A[N * pp[i] + qq[i]] != 0.0;
+                cc[i] = ss[i] = 0.0;
+                if (!act[i]) continue;
+                const int p = pp[i], q = qq[i];
+                const double apq = A[N * p + q];
+                const double theta = (A[N * q + q] - A[N * p + p]) / (2.0 * apq);
+                const double t = (theta >= 0 ? 1.0 : -1.0) / (std::fabs(theta) + std::sqrt(theta * theta + 1.0));
+                cc[i] = 1.0 / std::sqrt(t * t + 1.0);
+                ss[i] = t * cc[i];
+            }
+            for (int i = 0; i < P; ++i) {  // columns of A
+                if (!act[i]) continue;
+                const int p = pp[i], q = qq[i];
+                const double c = cc[i], s = ss[i];
+                for (int k = 0; k < N; ++k) {
+                    const double akp = A[N * k + p], akq = A[N * k + q];
+                    A[N * k + p] = c * akp - s * akq;
+                    A[N * k + q] = s * akp + c * akq;
+                }
+            }
+            for (int i = 0; i < P; ++i) {  // rows of A
+                if (!act[i]) continue;
+                const int p = pp[i], q = qq[i];
+                const double c = cc[i], s = ss[i];
+                for (int k = 0; k < N; ++k) {
+                    const double apk = A[N * p + k], aqk = A[N * q + k];
+                    A[N * p + k] = c * apk - s * aqk;
+                    A[N * q + k] = s * apk + c * aqk;
+                }
+            }
+            for (int i = 0; i < P; ++i) {  // columns of V
+                if (!act[i]) continue;
+                const int p = pp[i], q = qq[i];
+                const double c = cc[i], s = ss[i];
+                for (int k = 0; k < N; ++k) {
+                    const double vkp = V[N * k + p], vkq = V[N * k + q];
+                    V[N * k + p] = c * vkp - s * vkq;
+                    V[N * k + q] = s * vkp + c * vkq;
+                }
+            }
+        }
+    }
+    int idx[N];
+    for (int i = 0; i < N; ++i) idx[i] = i;
+    for (int i = 0; i < N; ++i) {
+        int m = i;
+        for (int j = i + 1; j < N; ++j)
+            if (A[N * idx[j] + idx[j]] > A[N * idx[m] + idx[m]]) m = j;
+        int tmp = idx[i];
+        idx[i] = idx[m];
+        idx[m] = tmp;
+    }
+    for (int j = 0; j < N; ++j) {
+        evals[j] = A[N * idx[j] + idx[j]];
+        for (int i = 0; i < N; ++i) evecs[N * i + j] = V[N * i + idx[j]];
+    }
+}
+
 // Null vector of an 8 x 9 system by Gauss-Jordan elimination with complete
 // pivoting (first maximal |a| in row-major scan).  Returns false when the
 // system has rank < 8 (degenerate minimal sample).

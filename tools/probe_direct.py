@@ -104,6 +104,34 @@ def main():
             gaps.setdefault((a, b), []).append((entry[i + 1] - exits[i]) * us)
     print("boundary: last block exit -> next launch's block 0 entry (us): " +
           ", ".join(f"L{a}->L{b} {np.mean(g):.2f} (n={len(g)})" for (a, b), g in sorted(gaps.items())))
+    # per-block stamps of the last launches: dispatch skew and phase durations
+    lib.viso_debug_probe_blocks.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    blk = np.zeros((512, 256, 4), np.uint64)
+    mb = lib.viso_debug_probe_blocks(blk.ctypes.data, 512)
+    blk = blk[:mb].astype(np.int64)
+    lv_b = lvl[n - mb:]
+    nt = tiles[n - mb:]
+    for L in (3, 2, 1, 0):
+        sel = np.where(lv_b == L)[0]
+        if not len(sel):
+            continue
+        T = int(nt[sel[0]])
+        B = blk[sel, :T, :]
+        e0 = B[:, :1, 0]
+        rel = (B - e0[:, :, None]) * us  # us from block 0's entry
+        pro = (B[:, :, 1] - B[:, :, 0]) * us
+        til = (B[:, :, 2] - B[:, :, 1]) * us
+        tree = (B[:, :, 3] - B[:, :, 2]) * us
+        ex = rel[:, :, 3]
+        print(f"L({L}) {T} blocks, mean over launches: entry skew max {rel[:, :, 0].max(axis=1).mean():.2f}; "
+              f"prologue (entry -> B2) p50 {np.median(pro):.2f} max {pro.max(axis=1).mean():.2f}; "
+              f"tiles (B2 -> wave 0's points) p50 {np.median(til):.2f} max {til.max(axis=1).mean():.2f}; "
+              f"tile tree + store p50 {np.median(tree):.2f} max {tree.max(axis=1).mean():.2f}; "
+              f"exit p50 {np.median(ex):.2f} max {ex.max(axis=1).mean():.2f}")
+        for name, arr in [("prologue", pro), ("tiles", til), ("exit", ex)]:
+            m = arr.mean(axis=0)
+            print(f"      {name:8s} by block: first 8 {np.round(m[:8], 2).tolist()} last 8 {np.round(m[-8:], 2).tolist()} "
+                  f"by XCD (b % 8) {np.round([m[x::8].mean() for x in range(8)], 2).tolist()}")
     per = [(entry[i + 1] - entry[i]) * us for i in range(n - 1) if (lvl[i], lvl[i + 1]) in [(3, 2), (2, 1), (1, 0), (0, 3)]]
     print(f"entry-to-entry per launch in the chain: {np.mean(per):.2f} us")
 

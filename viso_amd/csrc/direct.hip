@@ -22,7 +22,7 @@
 //     reduce-scatter (the canonical wave tree, common.hpp).  A workgroup owns
 //     an aligned tile of T = max(8, P/256) points (P = next pow2 of the point
 //     count), so there are at most 256 tiles; the tile's 28 sums are a tree
-//     over its points, stored tile-major per level.
+//     over its points, stored k-major per level ([28][256]).
 // F (one workgroup): solves level 0 and writes the pose (+ pose log).
 //
 // The solve (one level, one workgroup): tile t's partials in thread t, a
@@ -59,6 +59,9 @@ constexpr int kPRing = 4096;
 constexpr int kPSt = 16;
 __device__ unsigned long long g_plog[kPRing][kPSt];
 __device__ unsigned long long g_pexit[kPRing];
+// per-block entry / exit stamps of the last kPRingB launches
+constexpr int kPRingB = 512;
+__device__ unsigned long long g_pblk[kPRingB][256][4];  // entry, after B2, wave 0's points done, exit
 #define PROBE_DECL()                                \
     __shared__ unsigned long long pst[kPSt];        \
     const unsigned long long probe_t0 = __builtin_amdgcn_s_memrealtime()
@@ -674,11 +677,14 @@ __device__ void direct_tile_pf(const DirectArgs& a, const LevelPair& fp, int lv,
         good_cnt += ok ? 1 : 0;
     }
     if (lane == 0 && good_cnt) atomicAdd(s_good, good_cnt);
+#ifdef VISO_PROBE
+    if (threadIdx.x == 0 && blockIdx.x < 256) g_pblk[a.probe_seq & (kPRingB - 1)][blockIdx.x][2] = __builtin_amdgcn_s_memrealtime();
+#endif
     __syncthreads();
     for (int k = wave; k < kSums; k += kWaves) {
         const double v = lane < T ? s_pts[lane * kSums + k] : 0.0;
         const double r = wave_tree_sum_dpp(v);
-        if (lane == 0) part[(size_t)b * kSums + k] = r;
+        if (lane == 0) part[(size_t)k * kMaxTiles + b] = r;  // k-major: [28][256]
     }
     if (threadIdx.x == 0) good[b] = *s_good;
     __syncthreads();
@@ -694,18 +700,16 @@ __device__ inline void state_to_pose(const double* st, double* pose) {
 
 // ---------------------------------------------------------------- solve
 
-// Thread t < 256 loads tile t's partials (zeros beyond n_tiles).
+// Thread t < 256 loads tile t's partials (zeros beyond n_tiles).  The
+// partials of a level are stored k-major ([28][256]: sum k of tile t at
+// k * 256 + t), so each of a wave's 28 loads is one coalesced 512-byte run
+// (4 cache lines) rather than 64 lines strided by a tile record.
 __device__ inline void load_partials(const double* __restrict__ part, const int* __restrict__ good,
                                      int n_tiles, double* v, int& gg) {
     const int t = threadIdx.x;
     if (t < n_tiles) {
-        const double2* src = reinterpret_cast<const double2*>(part + (size_t)t * kSums);
 #pragma unroll
-        for (int k = 0; k < kSums / 2; ++k) {
-            const double2 d = src[k];
-            v[2 * k] = d.x;
-            v[2 * k + 1] = d.y;
-        }
+        for (int k = 0; k < kSums; ++k) v[k] = part[(size_t)k * kMaxTiles + t];
         gg = good[t];
     } else {
 #pragma unroll
@@ -854,6 +858,7 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
 #ifdef VISO_PROBE
         for (int k = 0; k < kPSt; ++k) pst[k] = 0;
         pst[0] = probe_t0;
+        if (blockIdx.x < 256) g_pblk[a.probe_seq & (kPRingB - 1)][blockIdx.x][0] = probe_t0;
 #endif
     }
     lds_barrier();  // nothing is in flight yet
@@ -978,6 +983,9 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
         __syncthreads();
     }
     if (wave == 0) PST(8);
+#ifdef VISO_PROBE
+    if (t == 0 && blockIdx.x < 256) g_pblk[a.probe_seq & (kPRingB - 1)][blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+#endif
     const int out = lv >= 0 ? lv : kLevels;
     if (blockIdx.x == 0 && t == 0 && !merged) {
         for (int k = 0; k < 7; ++k) a.s.state[out * kStateStride + k] = L.state[k];
@@ -1005,6 +1013,7 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
     const unsigned long long t_exit = __builtin_amdgcn_s_memrealtime();
     const int slot = a.probe_seq & (kPRing - 1);
     if (t == 0) atomicMax(&g_pexit[slot], t_exit);
+    if (t == 0 && blockIdx.x < 256) g_pblk[a.probe_seq & (kPRingB - 1)][blockIdx.x][3] = t_exit;
     if (blockIdx.x == 0 && t == 0) {
         pst[11] = t_exit;
         pst[15] = (unsigned long long)(lv + 1) | ((unsigned long long)merged << 8) |
@@ -1029,7 +1038,7 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
 // Tiles per camera: up to 256 (T <= 64 points each covers kMaxMapPoints);
 // a camera's partials are reduced by 1, 2 or 4 waves (64 tiles each) and
 // the waves' sums folded as the canonical tree's top levels.
-constexpr int kRigTiles = kMaxTiles;
+constexpr int kRigTiles = kMaxTiles;  // also the k-major partial stride of direct_tile_pf
 constexpr int kRigTargetTiles = 64;  // faithful tiling aims at this many tiles per camera
 
 // waves reducing a camera of n_tiles tiles (the canonical tree over 64 q tiles)
@@ -1176,14 +1185,9 @@ __global__ __launch_bounds__(kThreads) void rig_level_kernel(RigArgs ra) {
         double v[kSums];
         int gg = 0;
         if (tl < aw.n_tiles) {
-            const double2* src =
-                reinterpret_cast<const double2*>(aw.s.part + ((size_t)sl * kRigTiles + tl) * kSums);
+            const double* src = aw.s.part + (size_t)sl * kRigTiles * kSums;  // k-major [28][256]
 #pragma unroll
-            for (int k = 0; k < kSums / 2; ++k) {
-                const double2 d = src[k];
-                v[2 * k] = d.x;
-                v[2 * k + 1] = d.y;
-            }
+            for (int k = 0; k < kSums; ++k) v[k] = src[(size_t)k * kRigTiles + tl];
             gg = aw.s.good[sl * kRigTiles + tl];
         } else {
 #pragma unroll
@@ -1520,11 +1524,30 @@ extern "C" int viso_debug_probe_ring(unsigned long long* log, unsigned long long
     }
     *n_launches = n;
     if (reset) {
+        static unsigned long long z3[kPRingB][256][4] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_pblk), z3, sizeof(z3)) != hipSuccess) return -2;
         static unsigned long long z1[kPRing][kPSt] = {}, z2[kPRing] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_plog), z1, sizeof(z1)) != hipSuccess) return -2;
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_pexit), z2, sizeof(z2)) != hipSuccess) return -2;
         g_probe_host_seq = 0;
     }
     return 0;
+}
+
+// Per-block stamps of the last min(cap, n, 512) launches, in launch order:
+// out[i][b][0..3] = entry, after B2, wave 0's points evaluated, exit.
+extern "C" int viso_debug_probe_blocks(unsigned long long* out, int cap) {
+    using namespace viso;
+    static unsigned long long h[kPRingB][256][4];
+    if (hipDeviceSynchronize() != hipSuccess) return -2;
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_pblk), sizeof(h)) != hipSuccess) return -2;
+    const int n = (int)g_probe_host_seq;
+    const int m = std::min(std::min(cap, n), kPRingB);
+    for (int i = 0; i < m; ++i) {
+        const int s = (n - m + i) & (kPRingB - 1);
+        for (int b = 0; b < 256; ++b)
+            for (int k = 0; k < 4; ++k) out[((size_t)i * 256 + b) * 4 + k] = h[s][b][k];
+    }
+    return m;
 }
 #endif

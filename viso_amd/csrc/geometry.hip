@@ -472,20 +472,121 @@ __global__ __launch_bounds__(256) void h_moment_sums_kernel(GeoArgs a) {
 }
 
 // ---------------------------------------------------------------- H refine + decompose
+// LDS hand-off between the lanes of one wave
+__device__ inline void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// The eigenvector of the smallest eigenvalue of the symmetric 9 x 9 moment
+// matrix (the least-squares DLT refinement of the winning homography) by a
+// round-robin (parallel-ordered) cyclic Jacobi on one wave: per round the
+// four disjoint rotations are computed by lanes 0-4 from the round's A, then
+// lane per (pair, index) rotates the column pairs of A and V, then the row
+// pairs of A.  Restated step for step by oracle_linalg.hpp jacobi_eigen_rr
+// (sweep test, stop rule, descending selection sort).  All lanes return it.
+__device__ void smallest_eigvec9_rr(const double* __restrict__ Min, double* out) {
+    constexpr int N = 9, M = 10, R = 9, P = 5;
+    __shared__ double sA[81], sV[81], sc[P], ss[P];
+    __shared__ int sp[P], sq[P], sact[P];
+    const int lane = threadIdx.x & 63;
+    for (int k = lane; k < 81; k += 64) {
+        sA[k] = Min[k];
+        sV[k] = (k % (N + 1) == 0) ? 1.0 : 0.0;
+    }
+    wave_lds_sync();
+    for (int sweep = 0; sweep < 50; ++sweep) {
+        // every lane forms the same sums (the oracle's order)
+        double off = 0, diag = 0;
+        for (int p = 0; p < N; ++p) {
+            diag = diag + sA[N * p + p] * sA[N * p + p];
+            for (int q = p + 1; q < N; ++q) off = off + sA[N * p + q] * sA[N * p + q];
+        }
+        off = uniform_f64(off);
+        diag = uniform_f64(diag);
+        if (off <= 1e-30 * diag || off == 0.0) break;
+        for (int r = 0; r < R; ++r) {
+            if (lane < P) {
+                // circle method: arr[0] = 0, arr[j] = 1 + (j - 1 + r) mod 9; pair i = (arr[i], arr[9 - i])
+                const int a0 = lane == 0 ? 0 : 1 + (lane - 1 + r) % (M - 1);
+                const int b0 = 1 + (M - 1 - lane - 1 + r) % (M - 1);
+                const int p = a0 < b0 ? a0 : b0, q = a0 < b0 ? b0 : a0;
+                const bool act = q < N && sA[N * p + q] != 0.0;
+                double cc = 0.0, sn = 0.0;
+                if (act) {
+                    const double apq = sA[N * p + q];
+                    const double theta = (sA[N * q + q] - sA[N * p + p]) / (2.0 * apq);
+                    const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                    cc = 1.0 / sqrt(t * t + 1.0);
+                    sn = t * cc;
+                }
+                sp[lane] = p;
+                sq[lane] = q;
+                sact[lane] = act ? 1 : 0;
+                sc[lane] = cc;
+                ss[lane] = sn;
+            }
+            wave_lds_sync();
+            // column pairs of A (tasks 0..44) and of V (45..89)
+            for (int task = lane; task < 2 * P * N; task += 64) {
+                const int u = task < P * N ? task : task - P * N;
+                const int i = u / N, k = u - N * (u / N);
+                if (!sact[i]) continue;
+                double* X = task < P * N ? sA : sV;
+                const int p = sp[i], q = sq[i];
+                const double c = sc[i], s = ss[i];
+                const double xkp = X[N * k + p], xkq = X[N * k + q];
+                X[N * k + p] = c * xkp - s * xkq;
+                X[N * k + q] = s * xkp + c * xkq;
+            }
+            wave_lds_sync();
+            // row pairs of A
+            if (lane < P * N) {
+                const int i = lane / N, k = lane - N * (lane / N);
+                if (sact[i]) {
+                    const int p = sp[i], q = sq[i];
+                    const double c = sc[i], s = ss[i];
+                    const double apk = sA[N * p + k], aqk = sA[N * q + k];
+                    sA[N * p + k] = c * apk - s * aqk;
+                    sA[N * q + k] = s * apk + c * aqk;
+                }
+            }
+            wave_lds_sync();
+        }
+    }
+    // descending selection sort of the diagonal (first maximum first); the
+    // last position's column
+    int idx[N];
+    double d[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        idx[i] = i;
+        d[i] = sA[N * i + i];
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        int m = i;
+#pragma unroll
+        for (int j = i + 1; j < N; ++j)
+            if (d[idx[j]] > d[idx[m]]) m = j;
+        const int tmp = idx[i];
+        idx[i] = idx[m];
+        idx[m] = tmp;
+    }
+    const int last = idx[N - 1];
+    for (int k = 0; k < N; ++k) out[k] = sV[N * k + last];
+}
+
 __global__ __launch_bounds__(64) void h_refine_decompose_kernel(GeoArgs a) {
     GeoCtl* c = a.ctl;
     if (!c->gate || c->h_best < 0) return;
     const int good = c->h_count;
-    if (threadIdx.x != 0) return;
     double H[9];
     const double* Hb = a.h_models + 9 * (size_t)c->h_best;
     for (int k = 0; k < 9; ++k) H[k] = Hb[k];
-    if (good >= 4) {
-        double M[81], ev[9], V[81];
-        for (int k = 0; k < 81; ++k) M[k] = a.hM[k];
-        jacobi_eigen<9>(M, ev, V);
-        for (int k = 0; k < 9; ++k) H[k] = V[9 * k + 8];
-    }
+    if (good >= 4) smallest_eigvec9_rr(a.hM, H);  // the whole wave
+    if (threadIdx.x != 0) return;
     if (fabs(H[8]) > 1e-12) {
         const double d = H[8];
         for (int k = 0; k < 9; ++k) H[k] = H[k] / d;

@@ -154,10 +154,20 @@ __device__ inline FeatDev set_of(const FeatDev* sets, int ring, int nc, int pair
     return sets[2 * (((pair0 + z / (2 * nc)) % ring) * nc + (z >> 1) % nc) + (z & 1)];
 }
 
+// The 1-D grid is dealt so that all tiles of one image share one XCD (block
+// b runs on XCD b % 8, round-robin; speed only): the halo rows and columns
+// that neighbouring tiles both stage are then fetched into one L2, not into
+// several.  Block b: xcd = b % 8, q = b / 8, tile q % (tiles_x * tiles_y) of
+// image 8 (q / (tiles_x * tiles_y)) + xcd.
 template <int R, bool DOM>
 __global__ __launch_bounds__(256) void svo_detect_kernel(ImgSrc src, SvoDev p,
                                                          const FeatDev* __restrict__ sets, int ring,
-                                                         int pair0, int seg_cap) {
+                                                         int pair0, int seg_cap, int tiles_x, int tiles_y,
+                                                         int n_img) {
+    const int xcd = blockIdx.x & 7, q = blockIdx.x >> 3, tpi = tiles_x * tiles_y;
+    const int image = 8 * (q / tpi) + xcd, tile = q % tpi;
+    if (image >= n_img) return;
+    const int bx_ = tile % tiles_x, by_ = tile / tiles_x;
     constexpr int SW = 64 - 2 * R;    // output columns per wave strip
     constexpr int OW = 4 * SW;        // output columns per tile
     constexpr int RR = kDTH + 2 * R;  // response rows
@@ -166,10 +176,10 @@ __global__ __launch_bounds__(256) void svo_detect_kernel(ImgSrc src, SvoDev p,
     __shared__ uint32_t s_img[IR * kImgDw];
     __shared__ uint32_t s_rx[4][64 + 2 * R];                   // per wave: P (max view)
     __shared__ uint32_t s_rn[DOM ? 4 : 1][DOM ? 64 + 2 * R : 1];  // P (min view, DOM only)
-    const uint8_t* __restrict__ img = src.at(blockIdx.z, p.ncam);
-    const FeatDev F = set_of(sets, ring, p.ncam, pair0, blockIdx.z);
+    const uint8_t* __restrict__ img = src.at(image, p.ncam);
+    const FeatDev F = set_of(sets, ring, p.ncam, pair0, image);
     const int w = p.w, h = p.h;
-    const int x0 = blockIdx.x * OW, y0 = blockIdx.y * kDTH;
+    const int x0 = bx_ * OW, y0 = by_ * kDTH;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     // ---- stage image rows y0-R-2 .. y0+kDTH+R+1, columns x0-R-2 .. x0-R+257
     // (the tile uses OW + 2R + 4 <= 260 of them):
@@ -212,7 +222,7 @@ __global__ __launch_bounds__(256) void svo_detect_kernel(ImgSrc src, SvoDev p,
     const int sh = 8 * (col & 3);
     const uint32_t* srow = s_img + (col >> 2);
     uint32_t* bx = s_rx[wave];
-    const int tiles = gridDim.x;
+    const int tiles = tiles_x;
     // Row rings of length L (image row i lives in slot i % L): the row loop is
     // unrolled L times, so every ring index is a compile-time constant and no
     // register moves are needed.  Vertical strict-neighbour extrema through a
@@ -307,7 +317,7 @@ __global__ __launch_bounds__(256) void svo_detect_kernel(ImgSrc src, SvoDev p,
             }
             const unsigned long long q0 = __ballot(flags & 1), q1 = __ballot(flags & 2),
                                      q2 = __ballot(flags & 4), q3 = __ballot(flags & 8);
-            const size_t seg = ((size_t)yc * tiles + blockIdx.x) * 4 + wave;
+            const size_t seg = ((size_t)yc * tiles + bx_) * 4 + wave;
             if (q0 | q1 | q2 | q3) {
                 int pos = (mbcnt64(q0) + mbcnt64(q1)) + (mbcnt64(q2) + mbcnt64(q3));
                 int* list = F.list + seg * seg_cap;
@@ -1608,8 +1618,13 @@ void launch_ransac(const SvoDev& d, const PairArgs& pa, int b0, int np, hipStrea
 template <int R>
 void launch_detect_r(bool dom, dim3 g, hipStream_t st, const ImgSrc& imgs, const SvoDev& d,
                      const FeatDev* sets, int ring, int pair0, int seg_cap) {
-    if (dom) svo_detect_kernel<R, true><<<g, kDW, 0, st>>>(imgs, d, sets, ring, pair0, seg_cap);
-    else svo_detect_kernel<R, false><<<g, kDW, 0, st>>>(imgs, d, sets, ring, pair0, seg_cap);
+    // g = (tiles_x, tiles_y, images) -> the XCD-dealt 1-D grid
+    const int tpi = (int)(g.x * g.y), ni = (int)g.z;
+    const dim3 g1(8 * tpi * ((ni + 7) / 8));
+    if (dom)
+        svo_detect_kernel<R, true><<<g1, kDW, 0, st>>>(imgs, d, sets, ring, pair0, seg_cap, g.x, g.y, ni);
+    else
+        svo_detect_kernel<R, false><<<g1, kDW, 0, st>>>(imgs, d, sets, ring, pair0, seg_cap, g.x, g.y, ni);
 }
 
 void launch_detect(int R, bool dom, dim3 g, hipStream_t st, const ImgSrc& imgs, const SvoDev& d,
