@@ -54,6 +54,34 @@ inline double tree_sum(const double* v, int n) {
     return t[0];
 }
 
+// Canonical order of a sum over MAP POINTS (the direct pose's 28 sums and
+// the rig's per-camera sums): points in tiles of T = min(64, max(1,
+// ceil(n / groups))) consecutive points, each tile a pairwise tree
+// (tree_sum over its count), then the pairwise tree over the ceil(n / T)
+// tile sums.  The device gives one workgroup per tile (groups = 256 for the
+// direct pose: one tile per CU; 256 / pow2(n_cams) per rig camera), so the
+// order is independent of the launch but fills the chip; pairwise trees
+// with zero padding make the device's 64-lane and 256-lane trees equal to
+// these.
+inline int map_tile(int n, int groups) {
+    int t = (n + groups - 1) / groups;
+    if (t < 1) t = 1;
+    if (t > 64) t = 64;
+    return t;
+}
+
+inline double map_tree_sum(const double* v, int n, int groups) {
+    if (n <= 0) return 0.0;
+    const int T = map_tile(n, groups);
+    const int nt = (n + T - 1) / T;
+    std::vector<double> tiles((size_t)nt);
+    for (int t = 0; t < nt; ++t) {
+        const int c = (t + 1) * T <= n ? T : n - t * T;
+        tiles[(size_t)t] = tree_sum(v + (size_t)t * T, c);
+    }
+    return tree_sum(tiles.data(), nt);
+}
+
 // Summation order switch (oracle_set_sum_order, viso_oracle.h).  0: the
 // canonical pairwise tree the device reproduces bit for bit; 1: "literal",
 // the reference's own running sums in loop order (H += ..., b += ...,

@@ -87,9 +87,10 @@ void pose12_of_se3(const SE3& s, double* out) {
     for (int i = 0; i < 3; ++i) out[9 + i] = s.t[i];
 }
 
-// Camera c's 28 canonical sums at cur_pose; returns nGood
+// Camera c's 28 canonical sums at cur_pose (map_tree_sum over its points,
+// groups = 256 / pow2(n_cams): the device's tiles per camera); returns nGood
 int camera_sums(const PyrView& last, const PyrView& cur, const double K[4], const double* points, int n,
-                const Pose& last_pose, const Pose& cur_pose, int level, double S[28]) {
+                const Pose& last_pose, const Pose& cur_pose, int level, int groups, double S[28]) {
     std::vector<double> part((size_t)n * 28), leaf((size_t)n);
     int good = 0;
     for (int i = 0; i < n; ++i) {
@@ -101,7 +102,7 @@ int camera_sums(const PyrView& last, const PyrView& cur, const double K[4], cons
     }
     for (int k = 0; k < 28; ++k) {
         for (int i = 0; i < n; ++i) leaf[(size_t)i] = part[(size_t)i * 28 + k];
-        S[k] = tree_sum(leaf.data(), n);
+        S[k] = map_tree_sum(leaf.data(), n, groups);
     }
     return good;
 }
@@ -156,6 +157,9 @@ void oracle_rig_direct(int n_cams, const uint8_t* const* last_pyrs, const uint8_
         oracle_rig_adjoint(extrinsics + 12 * c, Ad[(size_t)c].data());
     }
     SE3 T = se3_from_Rt(pose_io, pose_io + 9);
+    int pc = 1;
+    while (pc < n_cams) pc <<= 1;
+    const int groups = 256 / pc;
     for (int level = 3; level >= 0; --level) {
         double T12[12];
         pose12_of_se3(T, T12);
@@ -166,7 +170,7 @@ void oracle_rig_direct(int n_cams, const uint8_t* const* last_pyrs, const uint8_
             oracle_rig_compose(extrinsics + 12 * c, T12, Tc);
             double S[28], V[28];
             ngood += camera_sums(L[(size_t)c], C[(size_t)c], K, points[c], n_points[c],
-                                 pose_of12(cam_last + 12 * c), pose_of12(Tc), level, S);
+                                 pose_of12(cam_last + 12 * c), pose_of12(Tc), level, groups, S);
             transform_sums(Ad[(size_t)c].data(), S, V);
             for (int k = 0; k < 28; ++k) acc[k] = c == 0 ? V[k] : acc[k] + V[k];
         }

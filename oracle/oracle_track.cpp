@@ -204,7 +204,7 @@ void direct_single_layer(const PyrView& last, const PyrView& cur, const double K
             }
             for (int k = 0; k < 28; ++k) {
                 for (int i = 0; i < n; ++i) leaf[(size_t)i] = part[(size_t)i * 28 + k];
-                S[k] = tree_sum(leaf.data(), n);
+                S[k] = map_tree_sum(leaf.data(), n, 256);  // one tile per workgroup
             }
         }
         double H[36], b[6];

@@ -16,9 +16,12 @@
 // Spec decisions that make GPU-vs-oracle parity exact:
 //  * every float expression follows the reference's operand order and is
 //    compiled with -ffp-contract=off (no FMA contraction on either side);
-//  * every sum over patch pixels / points is the canonical pairwise tree over
-//    the index range padded to a power of two (leaf i+1 added to leaf i, then
-//    pairs of pairs, ...), not the reference's running sum; skipped items are
+//  * every sum over patch pixels is the canonical pairwise tree over the
+//    index range padded to a power of two (leaf i+1 added to leaf i, then
+//    pairs of pairs, ...), not the reference's running sum; a sum over map
+//    points (direct pose, rig) is two-level: pairwise trees over tiles of
+//    T = min(64, ceil(n / groups)) consecutive points, then the pairwise tree
+//    over the tile sums (oracle_common.hpp map_tree_sum); skipped items are
 //    +0.0 leaves;
 //  * out-of-buffer bilinear taps read 0 (the reference reads past the
 //    cv::Mat; include/common.h:35-41 — UB there).

@@ -134,6 +134,11 @@ __device__ inline double dpp_f64(double v) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// This thread's wave in the workgroup, visibly wave-uniform to the compiler
+// (so values indexed by it stay scalar and branches on them need no EXEC
+// bookkeeping).
+__device__ inline int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
+
 // A wave-uniform value made visibly uniform to the compiler (exact: every
 // lane holds the same bits), so branches on it need no EXEC bookkeeping.
 __device__ inline double uniform_f64(double v) {

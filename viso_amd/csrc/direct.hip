@@ -81,10 +81,16 @@ namespace {
 
 constexpr int kSums = 28;
 constexpr int kWaves = 16;  // waves per workgroup (one map point per wave at tile 16)
-constexpr int kMinTile = 8;  // smallest tile (the canonical tree's leaves: max(8, P / 256) points)
 constexpr int kThreads = kWaves * 64;
 constexpr int kMaxTiles = 256;
 constexpr int kMaxTile = kMaxMapPoints / kMaxTiles;  // 64 points
+
+// Points per tile of the canonical map tree (oracle_common.hpp map_tile):
+// min(64, max(1, ceil(n / groups))).
+inline int map_tile(int n, int groups) {
+    int t = (n + groups - 1) / groups;
+    return t < 1 ? 1 : (t > kMaxTile ? kMaxTile : t);
+}
 constexpr int kStats = 50;
 constexpr int kStateStride = 8;
 
@@ -116,7 +122,7 @@ struct DirectArgs {
     int n;
     const double* pose_seed;  // level 3 starts at SE3(R, t) of this pose (12)
     int level;                // tiles of this level; -1: final solve only
-    int tile;                 // points per tile (power of two, >= kWaves); split: the max
+    int tile;                 // points per tile (map_tile(n, 256) <= 64); split: the max
     int n_tiles;              // <= 256
     int split;                // tolerance mode: workgroup b owns points
                               // [b n / n_tiles, (b + 1) n / n_tiles) (all CUs busy;
@@ -343,10 +349,32 @@ __device__ inline bool direct_point_rs(const DirectArgs& a, const LevelPair& fp,
     const double Jp[12] = {Q[2], 0.0, Q[3], Q[4], Q[5], Q[6], 0.0, Q[7], Q[8], Q[9], Q[10], Q[11]};
     const uint8_t* C = fp.cur;
     const double x = uc + px, y = vc + py;
-    const double error = r.lval - sample_cw(C, w, h, x, y, win, cw);
-    // GetGradient (include/keyframe.h:57-64)
-    const double g0 = 0.5 * (sample_cw(C, w, h, x + 1, y, win, cw) - sample_cw(C, w, h, x - 1, y, win, cw));
-    const double g1 = 0.5 * (sample_cw(C, w, h, x, y + 1, win, cw) - sample_cw(C, w, h, x, y - 1, win, cw));
+    double error, g0, g1;
+    // Whole patch in the window (wave-uniform, conservative: every lane's
+    // samples at x, x +- 1 have int() bases in [floor(uc) - 6, floor(uc) + 5],
+    // likewise in y): the five samples read LDS with no per-lane tests;
+    // otherwise sample_cw decides per sample.
+    const int fu = (int)floor(uc), fv = (int)floor(vc);
+    if (__builtin_expect(cw.on && fu - 6 >= cw.x0 && fu + 5 <= cw.x0 + kCW - 2 && fv - 6 >= cw.y0 &&
+                             fv + 5 <= cw.y0 + kCW - 2,
+                         1)) {
+        auto smp = [&](double sx, double sy) {
+            const int o = ((int)sy - cw.y0) * kCW + ((int)sx - cw.x0);
+            const double d0 = (double)ld_lds_u8(win, o), d1 = (double)ld_lds_u8(win, o + 1);
+            const double d2 = (double)ld_lds_u8(win, o + kCW), d3 = (double)ld_lds_u8(win, o + kCW + 1);
+            const double xx = sx - floor(sx);
+            const double yy = sy - floor(sy);
+            return double((1 - xx) * (1 - yy) * d0 + xx * (1 - yy) * d1 + (1 - xx) * yy * d2 + xx * yy * d3);
+        };
+        error = r.lval - smp(x, y);
+        // GetGradient (include/keyframe.h:57-64)
+        g0 = 0.5 * (smp(x + 1, y) - smp(x - 1, y));
+        g1 = 0.5 * (smp(x, y + 1) - smp(x, y - 1));
+    } else {
+        error = r.lval - sample_cw(C, w, h, x, y, win, cw);
+        g0 = 0.5 * (sample_cw(C, w, h, x + 1, y, win, cw) - sample_cw(C, w, h, x - 1, y, win, cw));
+        g1 = 0.5 * (sample_cw(C, w, h, x, y + 1, win, cw) - sample_cw(C, w, h, x, y - 1, win, cw));
+    }
     double J[6];
 #pragma unroll
     for (int k = 0; k < 6; ++k) J[k] = -g0 * Jp[k] + -g1 * Jp[6 + k];
@@ -623,7 +651,7 @@ template <bool FAST, bool LV16 = false>
 __device__ void direct_tile_pf(const DirectArgs& a, const LevelPair& fp, int lv, const double* cur_pose, int b,
                                const PfLds& pf, bool merged, double* part, int* good, double* s_pts,
                                int* s_good) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = wave_id(), lane = threadIdx.x & 63;
     int first, T;
     tile_range(a, b, &first, &T);
     int good_cnt = 0;
@@ -1039,7 +1067,6 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
 // a camera's partials are reduced by 1, 2 or 4 waves (64 tiles each) and
 // the waves' sums folded as the canonical tree's top levels.
 constexpr int kRigTiles = kMaxTiles;  // also the k-major partial stride of direct_tile_pf
-constexpr int kRigTargetTiles = 64;  // faithful tiling aims at this many tiles per camera
 
 // waves reducing a camera of n_tiles tiles (the canonical tree over 64 q tiles)
 __device__ __host__ inline int rig_reduce_waves(int n_tiles) { return n_tiles <= 64 ? 1 : n_tiles <= 128 ? 2 : 4; }
@@ -1350,9 +1377,9 @@ DirectArgs direct_args(const FrameDev& last_pyr, const FrameDev& cur_pyr, const 
     a.points = points;
     a.n = n;
     a.pose_seed = pose_seed12;
-    int P = 1;
-    while (P < n) P <<= 1;
-    a.tile = P / kMaxTiles > kMinTile ? P / kMaxTiles : kMinTile;
+    // the canonical map tree's tiles (oracle_common.hpp map_tree_sum, groups
+    // = 256): one workgroup per tile, <= 256 tiles of <= 64 points
+    a.tile = map_tile(n, kMaxTiles);
     a.n_tiles = (n + a.tile - 1) / a.tile;
     if (split && n > 0) {
         a.split = 1;
@@ -1412,23 +1439,17 @@ void launch_direct_final(const FrameDev& last_pyr, const FrameDev& cur_pyr, cons
         direct_level_kernel<false><<<1, kThreads, 0, stream>>>(a);
 }
 
-// Tiles of a rig camera with n <= kMaxMapPoints points:
-// faithful: T = min(max(8, P / 64), kMaxTile) (a power of two, so tiles are
-// aligned subtrees of the camera's canonical tree): 64 tiles up to 4096
-// points, up to kRigTiles above;
-// tolerance mode: min(n, 64) even slices, more when a slice would exceed
-// kMaxTile points.
-static int rig_tiling(int n, bool split, int* tile, int* n_tiles) {
+// Tiles of a rig camera with n <= kMaxMapPoints points: faithful, the
+// canonical map tree's tiles with groups = 256 / pow2(n_cams) (T =
+// map_tile(n, groups) <= kMaxTile points, <= kRigTiles tiles); tolerance
+// mode, min(n, groups) even slices (more when a slice would exceed kMaxTile).
+static int rig_tiling(int n, int groups, bool split, int* tile, int* n_tiles) {
     if (n < 0 || n > kMaxMapPoints) return -1;
-    int P = 1;
-    while (P < n) P <<= 1;
-    int T = P / kRigTargetTiles > kMinTile ? P / kRigTargetTiles : kMinTile;
-    if (T > kMaxTile) T = kMaxTile;  // more than 64 tiles then (P > 4096)
-    while ((n + T - 1) / T > kRigTiles && T < kMaxTile) T <<= 1;
+    const int T = map_tile(n, groups);
     *tile = T;
     *n_tiles = (n + T - 1) / T;
     if (split && n > 0) {
-        int nt = n < kRigTargetTiles ? n : kRigTargetTiles;
+        int nt = n < groups ? n : groups;
         if ((n + nt - 1) / nt > kMaxTile) nt = (n + kMaxTile - 1) / kMaxTile;
         *n_tiles = nt;
         *tile = (n + nt - 1) / nt;
@@ -1446,6 +1467,9 @@ int launch_rig_direct(const RigCamDev* cams, int n_cams, const PyrGeom& g, const
     const bool fast = precision == VISO_PRECISION_FAST;
     RigArgs ra{};
     ra.n_cams = n_cams;
+    int pc = 1;
+    while (pc < n_cams) pc <<= 1;
+    const int groups = kMaxTiles / pc;  // tiles per camera: the cameras fill 256 workgroups
     int off = 0;
     for (int c = 0; c < n_cams; ++c) {
         const RigCamDev& cd = cams[c];
@@ -1457,7 +1481,7 @@ int launch_rig_direct(const RigCamDev* cams, int n_cams, const PyrGeom& g, const
         a.K = Intrinsics{K[0], K[1], K[2], K[3]};
         a.points = cd.points;
         a.n = cd.n;
-        if (rig_tiling(cd.n, fast, &a.tile, &a.n_tiles) != 0) return -1;
+        if (rig_tiling(cd.n, groups, fast, &a.tile, &a.n_tiles) != 0) return -1;
         a.split = fast && cd.n > 0 ? 1 : 0;
         a.s.part = (double*)cd.scratch;
         a.s.good = (int*)((char*)cd.scratch + (size_t)kLevels * kRigTiles * kSums * 8);
