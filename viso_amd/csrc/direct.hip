@@ -80,8 +80,15 @@ namespace viso {
 namespace {
 
 constexpr int kSums = 28;
-constexpr int kWaves = 16;  // waves per workgroup (one map point per wave at tile 16)
+// waves per workgroup of the direct pose (one map point per wave) and of
+// the rig (four partial-reduction waves per camera)
+#ifndef VISO_DIRECT_WAVES
+#define VISO_DIRECT_WAVES 16
+#endif
+constexpr int kWaves = VISO_DIRECT_WAVES;
 constexpr int kThreads = kWaves * 64;
+constexpr int kRigWaves = 16;
+constexpr int kRigThreads = kRigWaves * 64;
 constexpr int kMaxTiles = 256;
 constexpr int kMaxTile = kMaxMapPoints / kMaxTiles;  // 64 points
 
@@ -647,7 +654,7 @@ __device__ inline void merged_ref(const DirectArgs& a, const LevelPair& fp, int 
 // Tile b of level lv from the prologue's prefetch (the tile phase of
 // direct_level_kernel; direct_tile's arithmetic and tree; FAST: the
 // tolerance-mode point sums).
-template <bool FAST, bool LV16 = false>
+template <bool FAST, bool LV16 = false, int W = kWaves>
 __device__ void direct_tile_pf(const DirectArgs& a, const LevelPair& fp, int lv, const double* cur_pose, int b,
                                const PfLds& pf, bool merged, double* part, int* good, double* s_pts,
                                int* s_good) {
@@ -655,7 +662,7 @@ __device__ void direct_tile_pf(const DirectArgs& a, const LevelPair& fp, int lv,
     int first, T;
     tile_range(a, b, &first, &T);
     int good_cnt = 0;
-    for (int local = wave; local < T; local += kWaves) {
+    for (int local = wave; local < T; local += W) {
         const int i = first + local;
         double f = 0.0;
         int idx = -1;
@@ -709,7 +716,7 @@ __device__ void direct_tile_pf(const DirectArgs& a, const LevelPair& fp, int lv,
     if (threadIdx.x == 0 && blockIdx.x < 256) g_pblk[a.probe_seq & (kPRingB - 1)][blockIdx.x][2] = __builtin_amdgcn_s_memrealtime();
 #endif
     __syncthreads();
-    for (int k = wave; k < kSums; k += kWaves) {
+    for (int k = wave; k < kSums; k += W) {
         const double v = lane < T ? s_pts[lane * kSums + k] : 0.0;
         const double r = wave_tree_sum_dpp(v);
         if (lane == 0) part[(size_t)k * kMaxTiles + b] = r;  // k-major: [28][256]
@@ -1179,7 +1186,7 @@ __device__ inline void rig_combine(const RigArgs& ra, double (*red)[4][kSums], c
 }
 
 template <bool FAST>
-__global__ __launch_bounds__(kThreads) void rig_level_kernel(RigArgs ra) {
+__global__ __launch_bounds__(kRigThreads) void rig_level_kernel(RigArgs ra) {
     __shared__ SolveLds L;
     __shared__ double s_red[kMaxRigCams][4][kSums];
     __shared__ int s_g[kMaxRigCams][4];
@@ -1204,7 +1211,7 @@ __global__ __launch_bounds__(kThreads) void rig_level_kernel(RigArgs ra) {
     lds_barrier();
     // ---- every camera's tile partials of level sl (wave w: camera w / 4,
     // tiles 64 (w % 4) .. +63 of it, when the camera has that many waves)
-    static_assert(kWaves >= 4 * kMaxRigCams, "four reduce waves per camera");
+    static_assert(kRigWaves >= 4 * kMaxRigCams, "four reduce waves per camera");
     const int rc = wave >> 2, rq = wave & 3;
     if (solve && rc < ra.n_cams && rq < rig_reduce_waves(ra.cam[rc].d.n_tiles)) {
         const DirectArgs& aw = ra.cam[rc].d;
@@ -1262,7 +1269,7 @@ __global__ __launch_bounds__(kThreads) void rig_level_kernel(RigArgs ra) {
         }
         rig_compose(ra.cam[c].E, T, pred);
         const int first = solve ? wave - (wave >> 2) - 1 : wave;
-        const int stride = solve ? kWaves - kWaves / 4 : kWaves;
+        const int stride = solve ? kRigWaves - kRigWaves / 4 : kRigWaves;
         prefetch_tile<FAST>(a, lv, bt, pred, a.fp.pose_last, true, first, stride, s_pf);
     }
     // ---- the solve (wave 0)
@@ -1311,7 +1318,7 @@ __global__ __launch_bounds__(kThreads) void rig_level_kernel(RigArgs ra) {
         double pose[12];
 #pragma unroll
         for (int k = 0; k < 12; ++k) pose[k] = s_pose[k];
-        direct_tile_pf<FAST, FAST>(a, fp, lv, pose, bt, s_pf, false, a.s.part + (size_t)lv * kRigTiles * kSums,
+        direct_tile_pf<FAST, FAST, kRigWaves>(a, fp, lv, pose, bt, s_pf, false, a.s.part + (size_t)lv * kRigTiles * kSums,
                                    a.s.good + lv * kRigTiles, s_pts, &s_good);
     }
 }
@@ -1508,9 +1515,9 @@ int launch_rig_direct(const RigCamDev* cams, int n_cams, const PyrGeom& g, const
         }
         const int gl = level < 0 ? 1 : grid;
         if (fast)
-            rig_level_kernel<true><<<gl, kThreads, 0, stream>>>(ra);
+            rig_level_kernel<true><<<gl, kRigThreads, 0, stream>>>(ra);
         else
-            rig_level_kernel<false><<<gl, kThreads, 0, stream>>>(ra);
+            rig_level_kernel<false><<<gl, kRigThreads, 0, stream>>>(ra);
     }
     return 0;
 }
