@@ -77,6 +77,11 @@ __host__ __device__ inline void mat3_vec(const double* R, const double* p, doubl
 __device__ inline uint8_t ld_global_u8(const uint8_t* p, long long i) {
     return ((const __attribute__((address_space(1))) uint8_t*)p)[i];
 }
+// Byte at a wave-uniform base + a 32-bit unsigned per-lane offset (the
+// global_load saddr form: no 64-bit address arithmetic per lane).
+__device__ inline uint8_t ld_global_u8_off(const uint8_t* base, uint32_t off) {
+    return ((const __attribute__((address_space(1))) uint8_t*)base)[off];
+}
 // Byte i of a buffer of n bytes, 0 outside it.  The load is unconditional
 // (index clamped, value selected): a conditional load compiles to a branch
 // with its own s_waitcnt, which serialises a lane's taps.

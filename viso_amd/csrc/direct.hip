@@ -654,10 +654,18 @@ __device__ inline void merged_ref(const DirectArgs& a, const LevelPair& fp, int 
 // Tile b of level lv from the prologue's prefetch (the tile phase of
 // direct_level_kernel; direct_tile's arithmetic and tree; FAST: the
 // tolerance-mode point sums).
+// Tiles of <= 16 points (maps up to 4,096 points) end without a block
+// barrier: each wave that evaluated points adds itself to an LDS arrival
+// count after its sums are in LDS, and the wave that arrives last forms the
+// tile's 28 trees (lane k: tree over the 16 point slots, zeros past T, then
+// the two +0 levels of the 64-lane tree, the same operations as
+// wave_tree_sum_dpp on T slots) and stores them; the other waves are done.
+// `last_arriver` = false (the continuation, which reuses s_pts in a loop)
+// keeps the block-barrier form.
 template <bool FAST, bool LV16 = false, int W = kWaves>
 __device__ void direct_tile_pf(const DirectArgs& a, const LevelPair& fp, int lv, const double* cur_pose, int b,
                                const PfLds& pf, bool merged, double* part, int* good, double* s_pts,
-                               int* s_good) {
+                               int* s_good, int* s_cnt = nullptr) {
     const int wave = wave_id(), lane = threadIdx.x & 63;
     int first, T;
     tile_range(a, b, &first, &T);
@@ -715,6 +723,30 @@ __device__ void direct_tile_pf(const DirectArgs& a, const LevelPair& fp, int lv,
 #ifdef VISO_PROBE
     if (threadIdx.x == 0 && blockIdx.x < 256) g_pblk[a.probe_seq & (kPRingB - 1)][blockIdx.x][2] = __builtin_amdgcn_s_memrealtime();
 #endif
+    if (s_cnt && T <= 16) {
+        const int nw = T < W ? T : W;  // waves that evaluated points
+        if (wave >= nw) return;
+        int prev = 0;
+        if (lane == 0)
+            prev = __hip_atomic_fetch_add(s_cnt, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+        prev = __builtin_amdgcn_readfirstlane(prev);
+        if (prev != nw - 1) return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if (lane < kSums) {
+            double v[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) v[j] = j < T ? s_pts[j * kSums + lane] : 0.0;
+#pragma unroll
+            for (int st = 1; st < 16; st <<= 1)
+#pragma unroll
+                for (int j = 0; j < 16; j += 2 * st) v[j] = v[j] + v[j + st];
+            double r = v[0] + 0.0;  // lanes 16..31 (+0)
+            r = r + 0.0;            // the other half wave (+0)
+            part[(size_t)lane * kMaxTiles + b] = r;  // k-major: [28][256]
+        }
+        if (lane == 0) good[b] = __hip_atomic_load(s_good, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return;
+    }
     __syncthreads();
     for (int k = wave; k < kSums; k += W) {
         const double v = lane < T ? s_pts[lane * kSums + k] : 0.0;
@@ -878,6 +910,7 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
     __shared__ double s_last[12];  // merged L(3): this frame's `last` pose
     __shared__ double s_pts[kMaxTile * kSums];
     __shared__ int s_good;
+    __shared__ int s_cnt;  // waves done with their points (last-arriver tile tree)
     __shared__ int s_arrive;
     __shared__ PfLds s_pf;
     const int lv = a.level;
@@ -890,6 +923,7 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
     if (t == 0) {
         s_arrive = 0;
         s_good = 0;
+        s_cnt = 0;
 #ifdef VISO_PROBE
         for (int k = 0; k < kPSt; ++k) pst[k] = 0;
         pst[0] = probe_t0;
@@ -1040,7 +1074,7 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
 #pragma unroll
         for (int k = 0; k < 12; ++k) pose[k] = s_pose[k];
         direct_tile_pf<FAST>(a, fp, lv, pose, blockIdx.x, s_pf, merged, a.s.part + (size_t)lv * kMaxTiles * kSums,
-                       a.s.good + lv * kMaxTiles, s_pts, &s_good);
+                       a.s.good + lv * kMaxTiles, s_pts, &s_good, &s_cnt);
     }
 #ifdef VISO_PROBE
     // block 0 exit: its stamps to the launch's ring slot; every block raises
@@ -1194,6 +1228,7 @@ __global__ __launch_bounds__(kRigThreads) void rig_level_kernel(RigArgs ra) {
     __shared__ double s_pose[12];
     __shared__ double s_pts[kMaxTile * kSums];
     __shared__ int s_good;
+    __shared__ int s_cnt;
     __shared__ int s_arrive;
     __shared__ PfLds s_pf;
     const int lv = ra.level;
@@ -1207,6 +1242,7 @@ __global__ __launch_bounds__(kRigThreads) void rig_level_kernel(RigArgs ra) {
     if (t == 0) {
         s_arrive = 0;
         s_good = 0;
+        s_cnt = 0;
     }
     lds_barrier();
     // ---- every camera's tile partials of level sl (wave w: camera w / 4,
@@ -1319,7 +1355,7 @@ __global__ __launch_bounds__(kRigThreads) void rig_level_kernel(RigArgs ra) {
 #pragma unroll
         for (int k = 0; k < 12; ++k) pose[k] = s_pose[k];
         direct_tile_pf<FAST, FAST, kRigWaves>(a, fp, lv, pose, bt, s_pf, false, a.s.part + (size_t)lv * kRigTiles * kSums,
-                                   a.s.good + lv * kRigTiles, s_pts, &s_good);
+                                   a.s.good + lv * kRigTiles, s_pts, &s_good, &s_cnt);
     }
 }
 static_assert(sizeof(RigArgs) <= 4096, "rig kernel arguments exceed 4 KB");

@@ -68,12 +68,16 @@ __device__ inline WinRegs window_issue(const uint8_t* img, int w, int h, double 
     int y0 = (int)floor(cy) - kWinH / 2 + 1;
     x0 = min(max(x0, 0), w - kWinW);
     y0 = min(max(y0, 0), h - kWinH);
+    // byte e = lane + 64 k of the row-major window: row e / 24, column e % 24
+    // (compile-time per k up to the lane), 32-bit offsets from the window's
+    // first byte (a level is far below 2^31 bytes)
     const int lane = threadIdx.x & 63;
+    const uint8_t* base = img + ((size_t)y0 * (size_t)w + (size_t)x0);
 #pragma unroll
     for (int k = 0; k < kWinPer; ++k) {
         const int e = lane + 64 * k;
         const int rr = e / kWinW, c = e - rr * kWinW;
-        r.v[k] = ld_global_u8(img, (long long)(y0 + rr) * w + (x0 + c));
+        r.v[k] = ld_global_u8_off(base, (uint32_t)(rr * w + c));
     }
     r.x0 = x0;
     r.y0 = y0;
