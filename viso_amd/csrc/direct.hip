@@ -920,6 +920,29 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
     const int sl = merged ? 0 : prev;  // level solved in the prologue
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const bool tiles = lv >= 0 && (int)blockIdx.x < a.n_tiles;
+    // ---- the loads that need no LDS are issued first, so they are in flight
+    // while the workgroup's waves arrive at the first barrier: the partials
+    // of level sl (waves 0-3) and the T21 that level was evaluated at (thread
+    // 256; every prefetch wave for its prediction)
+    double v[kSums];
+    int gg = 0;
+    if (solve && t < 256)
+        load_partials(a.s.part + (size_t)sl * kMaxTiles * kSums, a.s.good + sl * kMaxTiles,
+                      a.n_tiles, v, gg);
+    const bool pf_wave = !solve || (wave & 3) != 0;
+    double st[7];
+    if (t == 256 || (solve && tiles && pf_wave)) {
+        if (!solve) {
+            // Sophus::SE3d(R, t): R -> quaternion
+            quat_from_matrix(a.pose_seed, st);
+            st[4] = a.pose_seed[9];
+            st[5] = a.pose_seed[10];
+            st[6] = a.pose_seed[11];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 7; ++k) st[k] = a.s.state[sl * kStateStride + k];
+        }
+    }
     if (t == 0) {
         s_arrive = 0;
         s_good = 0;
@@ -930,25 +953,9 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
         if (blockIdx.x < 256) g_pblk[a.probe_seq & (kPRingB - 1)][blockIdx.x][0] = probe_t0;
 #endif
     }
-    lds_barrier();  // nothing is in flight yet
+    lds_barrier();  // the LDS words above; the global loads stay in flight
 
-    // ---- partials of level sl (waves 0-3) and the starting T21 (thread 256)
-    double v[kSums];
-    int gg = 0;
-    if (solve && t < 256)
-        load_partials(a.s.part + (size_t)sl * kMaxTiles * kSums, a.s.good + sl * kMaxTiles,
-                      a.n_tiles, v, gg);
     if (t == 256) {
-        double st[7];
-        if (!solve) {
-            // Sophus::SE3d(R, t): R -> quaternion
-            quat_from_matrix(a.pose_seed, st);
-            st[4] = a.pose_seed[9];
-            st[5] = a.pose_seed[10];
-            st[6] = a.pose_seed[11];
-        } else {
-            for (int k = 0; k < 7; ++k) st[k] = a.s.state[sl * kStateStride + k];
-        }
         for (int k = 0; k < 7; ++k) {
             L.state[k] = st[k];
             L.best[k] = st[k];
@@ -977,15 +984,12 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
     // the solver's SIMD (waves 0, 4, 8, 12: wave w runs on SIMD w % 4) is
     // left to the solver; its waves join the prefetch only when there is no
     // solve
-    const bool pf_wave = !solve || (wave & 3) != 0;
     if (tiles && pf_wave) {
         double pred[12];
         if (!solve) {
             for (int k = 0; k < 12; ++k) pred[k] = a.pose_seed[k];
         } else {
-            double sp[7];
-            for (int k = 0; k < 7; ++k) sp[k] = a.s.state[sl * kStateStride + k];
-            state_to_pose(sp, pred);
+            state_to_pose(st, pred);  // loaded above
         }
         const int first = solve ? wave - (wave >> 2) - 1 : wave;
         const int stride = solve ? kWaves - kWaves / 4 : kWaves;
