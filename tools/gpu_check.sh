@@ -14,4 +14,5 @@ timeout -k 10 300 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { ec
 cat $OUT/bench.json
 timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench_driver.json 2> $OUT/bench_driver.err || { echo "bench (driver args) failed"; tail -30 $OUT/bench_driver.err; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python -u bench.py --no-cpu --svo-cpu-pairs 0 > $OUT/bench_rocprof.json 2> $OUT/bench_rocprof.err || { echo "rocprof failed"; tail -30 $OUT/bench_rocprof.err; exit 1; }
-find $OUT/prof -name '*kernel_stats.csv' | head -3
+
+python tools/db2stats.py $(find $OUT/prof -name '*results.db' | head -1) $OUT/bench_kernel_stats.csv && echo "kernel stats: $OUT/bench_kernel_stats.csv"
