@@ -47,10 +47,20 @@ inline double tree_sum(const double* v, int n) {
     if (n <= 0) return 0.0;
     int p = 1;
     while (p < n) p <<= 1;
-    std::vector<double> t((size_t)p, 0.0);
-    for (int i = 0; i < n; ++i) t[(size_t)i] = v[i];
+    // small trees (the 64-pixel patch sums, map tiles) on the stack: the
+    // CPU baseline times this restatement, so it must not be dominated by
+    // allocations the reference's running sums never make
+    double stack[256];
+    std::vector<double> heap;
+    double* t = stack;
+    if (p > 256) {
+        heap.assign((size_t)p, 0.0);
+        t = heap.data();
+    }
+    for (int i = 0; i < n; ++i) t[i] = v[i];
+    for (int i = n; i < p; ++i) t[i] = 0.0;
     for (int s = 1; s < p; s <<= 1)
-        for (int i = 0; i < p; i += 2 * s) t[(size_t)i] = t[(size_t)i] + t[(size_t)(i + s)];
+        for (int i = 0; i < p; i += 2 * s) t[i] = t[i] + t[i + s];
     return t[0];
 }
 
@@ -74,12 +84,18 @@ inline double map_tree_sum(const double* v, int n, int groups) {
     if (n <= 0) return 0.0;
     const int T = map_tile(n, groups);
     const int nt = (n + T - 1) / T;
-    std::vector<double> tiles((size_t)nt);
+    std::vector<double> heap;
+    double stack[256];
+    double* tiles = stack;
+    if (nt > 256) {
+        heap.resize((size_t)nt);
+        tiles = heap.data();
+    }
     for (int t = 0; t < nt; ++t) {
         const int c = (t + 1) * T <= n ? T : n - t * T;
-        tiles[(size_t)t] = tree_sum(v + (size_t)t * T, c);
+        tiles[t] = tree_sum(v + (size_t)t * T, c);
     }
-    return tree_sum(tiles.data(), nt);
+    return tree_sum(tiles, nt);
 }
 
 // Summation order switch (oracle_set_sum_order, viso_oracle.h).  0: the
