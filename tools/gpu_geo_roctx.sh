@@ -21,7 +21,12 @@ for t in mt:
     cols = [r[1] for r in c.execute(f"pragma table_info('{t}')")]
     if 'name' in cols and 'start' in cols and 'end' in cols:
         cnt = collections.Counter(); dur = collections.Counter()
-        for n, s, e in c.execute(f"select name, start, end from '{t}'"):
+        has_ext = 'extdata' in cols
+        q = f"select {'extdata' if has_ext else 'name'}, start, end from '{t}'"
+        for n, s, e in c.execute(q):
+            if has_ext:
+                import json
+                n = json.loads(n).get("message", n)
             cnt[n] += 1; dur[n] += (e - s)
         for n in sorted(cnt, key=lambda k: -dur[k])[:12]:
             print(f"  {t}: {n:22s} n={cnt[n]:6d} mean {dur[n] / cnt[n] / 1e3:9.2f} us")
