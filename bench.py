@@ -547,7 +547,7 @@ def main():
                       "rmse_translation": float(np.sqrt(np.mean(np.sum((gP[:m, 9:] - oP[:m, 9:]) ** 2, 1))))}
 
     if rank == 0:
-        gn_ev, mp_ev = pmc_evidence(W, H, breakdown, stereo_vo)
+        gn_ev, mp_ev = pmc_evidence(W, H, breakdown, stereo_vo, n_map)
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
             "steps": steps, "warmup": args.warmup,
@@ -618,13 +618,13 @@ def pyramid_traffic(W, H, imgs_per_launch):
     return None, None
 
 
-def pmc_evidence(W, H, breakdown, stereo_vo):
+def pmc_evidence(W, H, breakdown, stereo_vo, n_map=None):
     """The north star's two other rocprof figures, from the committed PMC passes
-    (tools/gpu_pmc.sh -> tools/pmc_kernels.py -> profiles/r02_gn_svo_pmc.json),
+    (tools/gpu_pmc.sh -> tools/pmc_kernels.py -> profiles/r03_gn_svo_pmc.json),
     profiled at 1242x375 only: occupancy of the GN reduction (direct_level_kernel)
     and HBM traffic of the matching pass (svo_circle_kernel).  Live durations
     come from this run's HIP events where the bench has them."""
-    f = os.path.join(ROOT, "profiles", "r02_gn_svo_pmc.json")
+    f = os.path.join(ROOT, "profiles", "r03_gn_svo_pmc.json")
     if (W, H) != (1242, 375) or not os.path.exists(f):
         return None, None
     with open(f) as fh:
@@ -634,7 +634,15 @@ def pmc_evidence(W, H, breakdown, stereo_vo):
     if d:
         # breakdown["direct"] = one frame's four level launches per "launch"
         live_us = 1e3 * breakdown["direct"]["avg_ms"] / 4 if "direct" in breakdown else d["pmc_duration_us"]
-        flop = d.get("fp64_flop_per_dispatch")
+        executed = d.get("fp64_flop_per_dispatch")
+        # algorithmic fp64 work of one level launch: every map point's 64 patch
+        # pixels x the reference's per-pixel operations (five bilinear samples
+        # 5 x 15, error 1, gradient 4, J 18, the 28 products and 28 tree adds;
+        # DirectPoseEstimationSingleLayer, src/viso.cpp:697-729) = 154 flop;
+        # the replicated solve of every workgroup is executed work, not
+        # algorithmic, and is in fp64_flop_per_launch_executed
+        n_pts = n_map
+        flop = n_pts * 64 * 154 if n_pts else None
         gn = {"kernel": "direct_level_kernel (one pyramid level of the photometric GN: tiles + J^T J / J^T e "
                         "reduction + the replicated 6x6 solve)",
               "bound": "latency (serial reduce -> solve chain per level)",
@@ -642,11 +650,15 @@ def pmc_evidence(W, H, breakdown, stereo_vo):
               "waves_per_launch": d["waves"], "mean_resident_waves_per_cu": d["mean_resident_waves_per_cu"],
               "max_waves_per_cu": d["max_waves_per_cu"],
               "occupancy": round(d["mean_resident_waves_per_cu"] / d["max_waves_per_cu"], 4),
-              "valu_busy": d["valu_busy"], "vgpr": d["vgpr"], "lds_bytes": d["lds_bytes"],
+              "valu_busy": d["valu_busy"], "vgpr": d.get("vgpr_code_object", d["vgpr"]),
+              "vgpr_source": "code object (compiler resource usage)" if "vgpr_code_object" in d else "PMC",
+              "lds_bytes": d["lds_bytes"],
               "fp64_flop_per_launch": flop,
+              "fp64_flop_per_launch_basis": f"algorithmic: {n_pts} map points x 64 px x 154 flop",
+              "fp64_flop_per_launch_executed": executed,
               "fp64_tflops": round(flop / (live_us * 1e-6) / 1e12, 2) if flop else None,
               "fp64_peak_tflops": d.get("fp64_peak_tflops"),
-              "source": "profiles/r02_gn_svo_pmc.json (SQ_WAVES, SQ_WAVE_CYCLES, SQ_ACTIVE_INST_VALU, "
+              "source": "profiles/r03_gn_svo_pmc.json (SQ_WAVES, SQ_WAVE_CYCLES, SQ_ACTIVE_INST_VALU, "
                         "SQ_INSTS_VALU_*_F64)"}
     mp = None
     c = t.get("svo", {}).get("svo_circle_kernel")
@@ -658,7 +670,7 @@ def pmc_evidence(W, H, breakdown, stereo_vo):
               "achieved_GBps": round(gbs, 1), "peak_GBps": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4),
               "bound": "latency / VALU (four dependent best-SAD searches per feature over a cache-resident "
                        "descriptor set), not HBM",
-              "source": "profiles/r02_gn_svo_pmc.json (FETCH_SIZE x2 + WRITE_SIZE)"}
+              "source": "profiles/r03_gn_svo_pmc.json (FETCH_SIZE x2 + WRITE_SIZE)"}
     return gn, mp
 
 

@@ -421,12 +421,18 @@ __global__ __launch_bounds__(256) void lk_template_kernel(LkAlignArgs a) {
 // x are point groups; the grid's x extent is a multiple of 8, so a point
 // group stays on one XCD for every frame and its templates stay in that
 // XCD's L2.
-// waves per SIMD the register allocation must allow (5: <= 96 VGPRs)
+// waves per SIMD the register allocation must allow: faithful 5 (<= 96
+// VGPRs, no spills; 6 spills and was 7 % slower), tolerance mode 6 (80 VGPRs,
+// no spills: 4 % faster than 5)
 #ifndef VISO_LK_MIN_WAVES
 #define VISO_LK_MIN_WAVES 5
 #endif
+#ifndef VISO_LK_MIN_WAVES_FAST
+#define VISO_LK_MIN_WAVES_FAST 6
+#endif
 template <bool FAST>
-__global__ __launch_bounds__(256, VISO_LK_MIN_WAVES) void lk_align_kernel(LkAlignArgs a) {
+__global__ __launch_bounds__(256, FAST ? VISO_LK_MIN_WAVES_FAST : VISO_LK_MIN_WAVES) void lk_align_kernel(
+    LkAlignArgs a) {
     __shared__ uint8_t s_win[4][2][kWinW * kWinH];
     const int i = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     if (i >= a.n) return;
