@@ -1136,6 +1136,14 @@ struct RigArgs {
     double* log;
     int log_index;
     double* cam_last;               // F: n_cams x 12, E_c T (next frame's `last` poses)
+    // L(3) fused with the previous timestep's F (merged != 0): the prologue
+    // solves the previous timestep's level 0, writes its pose / log / cam_last
+    // (block 0), seeds T with SE3(R, t) of it, and takes each camera's `last`
+    // pose E_c T_prev from it
+    int merged;
+    double* prev_pose_out;
+    double* prev_log;
+    int prev_log_index;
 };
 
 // Tc = E T (R row-major + t): Rc = Re R, tc = Re t + te
@@ -1223,21 +1231,23 @@ __device__ inline void rig_combine(const RigArgs& ra, double (*red)[4][kSums], c
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
-template <bool FAST>
+template <bool FAST, bool MERGED>
 __global__ __launch_bounds__(kRigThreads) void rig_level_kernel(RigArgs ra) {
     __shared__ SolveLds L;
     __shared__ double s_red[kMaxRigCams][4][kSums];
     __shared__ int s_g[kMaxRigCams][4];
     __shared__ double s_M[36];
     __shared__ double s_pose[12];
+    __shared__ double s_last[12];  // merged L(3): this workgroup's camera `last` pose E_c T_prev
     __shared__ double s_pts[kMaxTile * kSums];
     __shared__ int s_good;
     __shared__ int s_cnt;
     __shared__ int s_arrive;
     __shared__ PfLds s_pf;
     const int lv = ra.level;
-    const bool solve = lv < kLevels - 1;  // L(3) is seeded
-    const int sl = lv + 1;                // level solved in the prologue (F: 0)
+    const bool merged = MERGED;  // launched for L(3) only
+    const bool solve = lv < kLevels - 1 || merged;  // an unmerged L(3) is seeded
+    const int sl = merged ? 0 : lv + 1;              // level solved in the prologue (F: 0)
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const int c = rig_camera(ra, blockIdx.x);
     const int bt = (int)blockIdx.x - ra.tile_off[c];
@@ -1296,7 +1306,9 @@ __global__ __launch_bounds__(kRigThreads) void rig_level_kernel(RigArgs ra) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         atomicAdd(&s_arrive, 1);
     }
-    // ---- prefetch of this workgroup's tile at the predicted camera pose
+    // ---- prefetch of this workgroup's tile at the predicted camera pose (a
+    // merged L(3) also predicts its `last` pose: E_c times the T the previous
+    // level 0 was evaluated at; the tile phase re-checks every lane's taps)
     const bool pf_wave = !solve || (wave & 3) != 0;
     if (tiles && pf_wave) {
         double T[12], pred[12];
@@ -1310,7 +1322,7 @@ __global__ __launch_bounds__(kRigThreads) void rig_level_kernel(RigArgs ra) {
         rig_compose(ra.cam[c].E, T, pred);
         const int first = solve ? wave - (wave >> 2) - 1 : wave;
         const int stride = solve ? kRigWaves - kRigWaves / 4 : kRigWaves;
-        prefetch_tile<FAST>(a, lv, bt, pred, a.fp.pose_last, true, first, stride, s_pf);
+        prefetch_tile<FAST>(a, lv, bt, pred, merged ? pred : a.fp.pose_last, true, first, stride, s_pf);
     }
     // ---- the solve (wave 0)
     if (wave == 0) {
@@ -1334,32 +1346,49 @@ __global__ __launch_bounds__(kRigThreads) void rig_level_kernel(RigArgs ra) {
             // continuation) is not part of the rig spec
             double T[12];
             state_to_pose(L.state, T);
-            rig_compose(ra.cam[c].E, T, s_pose);
-            if (blockIdx.x == 0) {
-                const int out = lv >= 0 ? lv : kLevels;
-                for (int k = 0; k < 7; ++k) ra.state[out * kStateStride + k] = L.state[k];
-                if (lv < 0) {
-                    if (ra.pose_out)
-                        for (int k = 0; k < 12; ++k) ra.pose_out[k] = T[k];
-                    if (ra.log && ra.log_index >= 0)
-                        for (int k = 0; k < 12; ++k) ra.log[12 * (size_t)ra.log_index + k] = T[k];
-                    for (int cc = 0; cc < ra.n_cams; ++cc) {
-                        double Tc[12];
-                        rig_compose(ra.cam[cc].E, T, Tc);
-                        for (int k = 0; k < 12; ++k) ra.cam_last[12 * cc + k] = Tc[k];
-                    }
+            const bool fin = lv < 0 || merged;  // the solve just done finished a timestep
+            if (fin && blockIdx.x == 0) {
+                double* po = merged ? ra.prev_pose_out : ra.pose_out;
+                double* lg = merged ? ra.prev_log : ra.log;
+                const int li = merged ? ra.prev_log_index : ra.log_index;
+                for (int k = 0; k < 7; ++k) ra.state[kLevels * kStateStride + k] = L.state[k];
+                if (po)
+                    for (int k = 0; k < 12; ++k) po[k] = T[k];
+                if (lg && li >= 0)
+                    for (int k = 0; k < 12; ++k) lg[12 * (size_t)li + k] = T[k];
+                for (int cc = 0; cc < ra.n_cams; ++cc) {
+                    double Tc[12];
+                    rig_compose(ra.cam[cc].E, T, Tc);
+                    for (int k = 0; k < 12; ++k) ra.cam_last[12 * cc + k] = Tc[k];
                 }
             }
+            if (merged) {
+                // this camera's `last` pose, and SE3(R, t) of the previous
+                // timestep's pose as this timestep's seed (src/viso.cpp:114)
+                rig_compose(ra.cam[c].E, T, s_last);
+                double q[4];
+                quat_from_matrix(T, q);
+                for (int k = 0; k < 4; ++k) L.state[k] = q[k];
+                L.state[4] = T[9];
+                L.state[5] = T[10];
+                L.state[6] = T[11];
+                state_to_pose(L.state, T);
+            }
+            rig_compose(ra.cam[c].E, T, s_pose);
+            if (blockIdx.x == 0 && lv >= 0)
+                for (int k = 0; k < 7; ++k) ra.state[lv * kStateStride + k] = L.state[k];
         }
     }
     __syncthreads();  // B2
     if (tiles) {
-        const LevelPair fp = level_pair(a.fp, lv);
+        LevelPair fp = level_pair(a.fp, lv);
+        if (merged) fp.pose_last = s_last;
         double pose[12];
 #pragma unroll
         for (int k = 0; k < 12; ++k) pose[k] = s_pose[k];
-        direct_tile_pf<FAST, FAST, kRigWaves>(a, fp, lv, pose, bt, s_pf, false, a.s.part + (size_t)lv * kRigTiles * kSums,
-                                   a.s.good + lv * kRigTiles, s_pts, &s_good, &s_cnt);
+        direct_tile_pf<FAST, FAST, kRigWaves>(a, fp, lv, pose, bt, s_pf, merged,
+                                              a.s.part + (size_t)lv * kRigTiles * kSums, a.s.good + lv * kRigTiles,
+                                              s_pts, &s_good, &s_cnt);
     }
 }
 static_assert(sizeof(RigArgs) <= 4096, "rig kernel arguments exceed 4 KB");
@@ -1509,7 +1538,8 @@ size_t rig_scratch_bytes() { return (size_t)kLevels * kRigTiles * kSums * 8 + (s
 
 int launch_rig_direct(const RigCamDev* cams, int n_cams, const PyrGeom& g, const double K[4], double* state,
                       const double* seed12, double* stats, double* pose_out, double* log, int log_index,
-                      double* cam_last, hipStream_t stream, int precision) {
+                      double* cam_last, hipStream_t stream, int precision, int merge_prev, int prev_log_index,
+                      int levels, int final_solve) {
     if (n_cams < 1 || n_cams > kMaxRigCams) return -1;
     const bool fast = precision == VISO_PRECISION_FAST;
     RigArgs ra{};
@@ -1544,20 +1574,35 @@ int launch_rig_direct(const RigCamDev* cams, int n_cams, const PyrGeom& g, const
     ra.seed = seed12;
     ra.stats = stats;
     ra.log_index = -1;
+    ra.cam_last = cam_last;
+    ra.prev_log_index = -1;
     const int grid = off > 0 ? off : 1;
-    for (int level = kLevels - 1; level >= -1; --level) {
+    for (int level = levels ? kLevels - 1 : -1; level >= -1; --level) {
         ra.level = level;
+        ra.merged = 0;
+        if (level == kLevels - 1 && merge_prev) {
+            ra.merged = 1;
+            ra.prev_pose_out = pose_out;
+            ra.prev_log = log;
+            ra.prev_log_index = log ? prev_log_index : -1;
+        }
         if (level < 0) {
+            if (!final_solve) break;
             ra.pose_out = pose_out;
             ra.log = log;
             ra.log_index = log ? log_index : -1;
-            ra.cam_last = cam_last;
         }
         const int gl = level < 0 ? 1 : grid;
-        if (fast)
-            rig_level_kernel<true><<<gl, kRigThreads, 0, stream>>>(ra);
-        else
-            rig_level_kernel<false><<<gl, kRigThreads, 0, stream>>>(ra);
+        if (ra.merged) {
+            if (fast)
+                rig_level_kernel<true, true><<<gl, kRigThreads, 0, stream>>>(ra);
+            else
+                rig_level_kernel<false, true><<<gl, kRigThreads, 0, stream>>>(ra);
+        } else if (fast) {
+            rig_level_kernel<true, false><<<gl, kRigThreads, 0, stream>>>(ra);
+        } else {
+            rig_level_kernel<false, false><<<gl, kRigThreads, 0, stream>>>(ra);
+        }
     }
     return 0;
 }

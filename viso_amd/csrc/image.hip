@@ -57,6 +57,11 @@ struct PyrLevelArgs {
     uint8_t* dst[kPyrBatch];
     int sw, sh, dw, dh;
     int bands, units;
+    // XCD dealing (pyr_down_sk_kernel, xcd_per > 0): the chunk's work list
+    // (image-major, 4 units per block) is cut into 8 contiguous runs, block
+    // L takes item (L & 7) * xcd_per + (L >> 3), so the bands and strips of
+    // an image (which share halo rows and boundary lines) run on one XCD's L2
+    int xcd_per, bpi, n_img;
 };
 
 // 8 source bytes at offset off, never reading outside [0, n).
@@ -339,14 +344,21 @@ __global__ __launch_bounds__(256) void pyr_down_sk_kernel(PyrLevelArgs a) {
     // everything that depends only on the wave's unit is wave-uniform: keep
     // it in SGPRs (readfirstlane) so the VALU only does the per-lane work
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int unit = blockIdx.x * 4 + wave;
+    int img = (int)blockIdx.y, blk = (int)blockIdx.x;
+    if (a.xcd_per > 0) {
+        const int w = ((int)blockIdx.x & 7) * a.xcd_per + ((int)blockIdx.x >> 3);
+        img = w / a.bpi;
+        blk = w - img * a.bpi;
+        if (img >= a.n_img) return;  // block-uniform (no barrier in this kernel)
+    }
+    const int unit = blk * 4 + wave;
     if (unit >= a.units) return;
 #ifdef VISO_PROBE
     const unsigned long long pr_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
     SkBand b;
-    b.src = a.src[blockIdx.y];
-    b.dst = a.dst[blockIdx.y];
+    b.src = a.src[img];
+    b.dst = a.dst[img];
     b.sw = a.sw;
     b.sh = a.sh;
     b.dw = a.dw;
@@ -392,7 +404,7 @@ __global__ __launch_bounds__(256) void pyr_down_sk_kernel(PyrLevelArgs a) {
     }
 #ifdef VISO_PROBE
     if (lane == 0) {
-        const long long w = (long long)blockIdx.y * a.units + unit;
+        const long long w = (long long)img * a.units + unit;
         if (w < 8192) {
             g_pyr_tl[w][0] = pr_t0;
             g_pyr_tl[w][1] = __builtin_amdgcn_s_memrealtime();
@@ -858,12 +870,21 @@ void launch_pyr_level(const PyrGeom& g, int l, const uint8_t* const* l0, uint8_t
     if (l == 1 && a.sw >= 8) {
         a.bands = (a.dh + kSkBH1 - 1) / kSkBH1;
         a.units = a.bands * ((a.dw + kSkW - 1) / kSkW);
-        pyr_down_sk_kernel<kSkBH1, kSkRing1><<<dim3((a.units + 3) / 4, nb), 256, 0, stream>>>(a);
+        a.bpi = (a.units + 3) / 4;
+        a.n_img = nb;
+#ifndef VISO_PYR_NOXCD
+        a.xcd_per = (a.bpi * nb + 7) / 8;
+        pyr_down_sk_kernel<kSkBH1, kSkRing1><<<8 * a.xcd_per, 256, 0, stream>>>(a);
+#else  // dev A/B: the image-major 2-D grid
+        a.xcd_per = 0;
+        pyr_down_sk_kernel<kSkBH1, kSkRing1><<<dim3(a.bpi, nb), 256, 0, stream>>>(a);
+#endif
         return;
     }
     const int bh = l == 1 ? 8 : (l == 2 ? 4 : 2);
     a.bands = (a.dh + bh - 1) / bh;
     a.units = a.bands * ((a.dw + kPsW - 1) / kPsW);
+    a.xcd_per = 0;
     const dim3 grid((a.units + 3) / 4, nb);
     if (l == 1)
         pyr_down_stream_kernel<8><<<grid, 256, 0, stream>>>(a);

@@ -161,9 +161,15 @@ size_t rig_scratch_bytes();
 // state: [kLevels + 1][8] device; seed12: last rig pose (device); stats:
 // [kLevels][50] or null; cam_last: n_cams x 12 device.  Returns -1 on a bad
 // camera count.
+// One rig timestep's direct pose: levels (L(3..0), when `levels`) and the
+// final level-0 solve F (when `final_solve`); merge_prev: L(3) first solves
+// the previous timestep's level 0 (its F, deferred) and logs it at
+// prev_log_index.  An F alone (levels = 0, final_solve = 1) flushes a
+// deferred one.
 int launch_rig_direct(const RigCamDev* cams, int n_cams, const PyrGeom& g, const double K[4], double* state,
                       const double* seed12, double* stats, double* pose_out, double* log, int log_index,
-                      double* cam_last, hipStream_t stream, int precision);
+                      double* cam_last, hipStream_t stream, int precision, int merge_prev = 0,
+                      int prev_log_index = -1, int levels = 1, int final_solve = 1);
 // ---------------------------------------------------------------- photometric BA
 // The BA include/bundle_adjuster.h:22-106 sketches (SURVEY.md §8(f) row 4;
 // spec oracle/oracle_ba.cpp): keyframe poses (n_kf x 12 device, keyframe 0

@@ -67,13 +67,33 @@ struct viso_rig {
     int* h_int = nullptr;
     DevBuf staging;  // host-image upload (viso_rig_process)
     int state_ = VISO_STATE_INITIALIZATION;
+    // the last tracked timestep's final level-0 solve (F), deferred into the
+    // next timestep's L(3) within one ingest call, else launched by flush()
+    bool pending = false;
+    RigCamDev pending_cams[kMaxRigCams];
+    int pending_log = -1;
 
     uint8_t* slot(int b, int c) const { return (uint8_t*)pyr.ptr + geom.slot * (size_t)(b * n + c); }
     int init();
     void release();
     int stereo_init(const uint8_t* const* right_l0, bool* made);
     int step(const uint8_t* const* left_l0, const uint8_t* const* right_l0);
+    int flush();
 };
+
+int viso_rig::flush() {
+    if (!pending) return VISO_OK;
+    pending = false;
+    const double K[4] = {p.fx, p.fy, p.cx, p.cy};
+    const int rc = launch_rig_direct(pending_cams, n, geom, K, (double*)state.ptr, (const double*)rig_pose.ptr,
+                                     (double*)stats.ptr, (double*)rig_pose.ptr,
+                                     pending_log >= 0 ? (double*)log.ptr : nullptr, pending_log,
+                                     (double*)cam_last.ptr, stream, p.precision, 0, -1, /*levels=*/0,
+                                     /*final_solve=*/1);
+    if (rc) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipGetLastError());
+    return VISO_OK;
+}
 
 int viso_rig::init() {
     const PyrGeom& g = geom;
@@ -195,12 +215,17 @@ int viso_rig::step(const uint8_t* const* left_l0, const uint8_t* const* right_l0
             d.scratch = (char*)scratch.ptr + rig_scratch_bytes() * (size_t)c;
         }
         const bool logged = n_poses < p.max_poses;
+        // L(3..0); this timestep's F is deferred (merged into the next
+        // timestep's L(3), or flushed at the end of the ingest call)
         const int rc = launch_rig_direct(cams, n, g, K, (double*)state.ptr, (const double*)rig_pose.ptr,
-                                         (double*)stats.ptr, (double*)rig_pose.ptr,
-                                         logged ? (double*)log.ptr : nullptr, n_poses, (double*)cam_last.ptr,
-                                         stream, p.precision);
+                                         (double*)stats.ptr, (double*)rig_pose.ptr, (double*)log.ptr, n_poses,
+                                         (double*)cam_last.ptr, stream, p.precision, pending ? 1 : 0,
+                                         pending ? pending_log : -1, /*levels=*/1, /*final_solve=*/0);
         if (rc) return VISO_ERR_ARG;
         VISO_HIP_CHECK(hipGetLastError());
+        pending = true;
+        for (int c = 0; c < n; ++c) pending_cams[c] = cams[c];
+        pending_log = logged ? n_poses : -1;
         if (logged) ++n_poses;
     }
     cur = 1 - cur;
@@ -270,9 +295,12 @@ int viso_rig_process_device(viso_rig* r, const uint8_t* d_left, const uint8_t* d
             R[c] = d_right ? d_right + o : nullptr;
         }
         const int rc = r->step(L, d_right ? R : nullptr);
-        if (rc) return rc;
+        if (rc) {
+            r->flush();
+            return rc;
+        }
     }
-    return VISO_OK;
+    return r->flush();  // the last timestep's final solve
 }
 
 int viso_rig_process(viso_rig* r, const uint8_t* const* lefts, const uint8_t* const* rights,
@@ -303,7 +331,9 @@ int viso_rig_process(viso_rig* r, const uint8_t* const* lefts, const uint8_t* co
         L[c] = base + npx * c;
         R[c] = base + npx * (r->n + c);
     }
-    return r->step(L, rights ? R : nullptr);
+    rc = r->step(L, rights ? R : nullptr);
+    const int rf = r->flush();  // one timestep per call: its final solve now
+    return rc ? rc : rf;
 }
 
 int viso_rig_synchronize(viso_rig* r) {
