@@ -1164,23 +1164,33 @@ __device__ inline int rig_camera(const RigArgs& ra, int b) {
     return c;
 }
 
-// Wave 0 (after every camera's wave sums are in red[c][0..q_c)): the rig's
-// 28 sums into L.S and nGood into L.ngood.  First S_c = the top of camera
-// c's canonical tree over its q_c waves (r0; r0 + r1; (r0 + r1) + (r2 + r3))
-// into red[c][0]; then lane e < 21 (upper-triangle entry (i, j)), 21 + i
-// (b_i) or 27 (cost) folds the cameras in ascending order.
-__device__ inline void rig_combine(const RigArgs& ra, double (*red)[4][kSums], const int (*g)[4], double* sM,
-                                   SolveLds& L) {
+// Camera c's contribution to the rig's 28 sums, by the camera's leader
+// reduce wave once its q_c waves' sums are in red[0..q_c): first S_c = the
+// top of the camera's canonical tree over its waves (r0; r0 + r1; (r0 + r1) +
+// (r2 + r3)) into red[0]; then M = H_c Ad (lane l < 36: M[l / 6][l % 6])
+// and lane e < 21 (upper-triangle entry (i, j) of Ad^T M), 21 + i
+// ((Ad^T b_c)_i) or 27 (cost_c) into con.  The cameras' leaders run
+// concurrently; wave 0 folds their contributions in ascending camera order
+// (rig_fold).  Ad: row-major Ad(E_c), staged in LDS.
+__device__ inline void rig_contrib(int q, double (*red)[kSums], const double* Ad, double* sM, double* con) {
     const int lane = threadIdx.x & 63;
-    int ng = 0;
-    for (int c = 0; c < ra.n_cams; ++c) {
-        const int q = rig_reduce_waves(ra.cam[c].d.n_tiles);
-        if (q > 1 && lane < kSums) {
-            const double v = q == 2 ? red[c][0][lane] + red[c][1][lane]
-                                    : (red[c][0][lane] + red[c][1][lane]) + (red[c][2][lane] + red[c][3][lane]);
-            red[c][0][lane] = v;
+    if (q > 1 && lane < kSums) {
+        const double v = q == 2 ? red[0][lane] + red[1][lane]
+                                : (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+        red[0][lane] = v;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const double* S = red[0];
+    if (lane < 36) {
+        const int i = lane / 6, j = lane - 6 * (lane / 6);
+        double m = 0.0;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const int a = i < k ? i : k, bb = i < k ? k : i;
+            const double h = S[a * 6 - (a * (a - 1)) / 2 + (bb - a)];
+            m = k == 0 ? h * Ad[j] : m + h * Ad[6 * k + j];
         }
-        for (int j = 0; j < q; ++j) ng += g[c][j];
+        sM[lane] = m;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     // (i, j) of upper entry e, row-major over i <= j
@@ -1194,39 +1204,35 @@ __device__ inline void rig_combine(const RigArgs& ra, double (*red)[4][kSums], c
         ei = r;
         ej = r + e;
     }
-    double acc = 0.0;
-    for (int c = 0; c < ra.n_cams; ++c) {
-        const double* S = red[c][0];
-        const double* Ad = ra.cam[c].Ad;
-        // M = H_c Ad (lane l < 36: M[l / 6][l % 6])
-        if (lane < 36) {
-            const int i = lane / 6, j = lane - 6 * (lane / 6);
-            double m = 0.0;
+    double v = 0.0;
+    if (lane < 21) {
 #pragma unroll
-            for (int k = 0; k < 6; ++k) {
-                const int a = i < k ? i : k, bb = i < k ? k : i;
-                const double h = S[a * 6 - (a * (a - 1)) / 2 + (bb - a)];
-                m = k == 0 ? h * Ad[j] : m + h * Ad[6 * k + j];
-            }
-            sM[lane] = m;
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        double v = 0.0;
-        if (lane < 21) {
-            // Ad^T M: entry (ei, ej)
+        for (int k = 0; k < 6; ++k) v = k == 0 ? Ad[ei] * sM[ej] : v + Ad[6 * k + ei] * sM[6 * k + ej];
+    } else if (lane < 27) {
+        const int i = lane - 21;
 #pragma unroll
-            for (int k = 0; k < 6; ++k) v = k == 0 ? Ad[ei] * sM[ej] : v + Ad[6 * k + ei] * sM[6 * k + ej];
-        } else if (lane < 27) {
-            const int i = lane - 21;
-#pragma unroll
-            for (int k = 0; k < 6; ++k) v = k == 0 ? Ad[i] * S[21] : v + Ad[6 * k + i] * S[21 + k];
-        } else if (lane == 27) {
-            v = S[27];
-        }
-        acc = c == 0 ? v : acc + v;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        for (int k = 0; k < 6; ++k) v = k == 0 ? Ad[i] * S[21] : v + Ad[6 * k + i] * S[21 + k];
+    } else if (lane == 27) {
+        v = S[27];
     }
-    if (lane < kSums) L.S[lane] = acc;
+    if (lane < kSums) con[lane] = v;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+// Wave 0, every camera's contribution in: the rig's 28 sums (cameras
+// ascending) into L.S and nGood into L.ngood
+__device__ inline void rig_fold(const RigArgs& ra, const double (*con)[kSums], const int (*g)[4], SolveLds& L) {
+    const int lane = threadIdx.x & 63;
+    int ng = 0;
+    for (int c = 0; c < ra.n_cams; ++c) {
+        const int q = rig_reduce_waves(ra.cam[c].d.n_tiles);
+        for (int j = 0; j < q; ++j) ng += g[c][j];
+    }
+    if (lane < kSums) {
+        double acc = con[0][lane];
+        for (int c = 1; c < ra.n_cams; ++c) acc = acc + con[c][lane];
+        L.S[lane] = acc;
+    }
     if (lane == 0) L.ngood = ng;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
@@ -1236,7 +1242,10 @@ __global__ __launch_bounds__(kRigThreads) void rig_level_kernel(RigArgs ra) {
     __shared__ SolveLds L;
     __shared__ double s_red[kMaxRigCams][4][kSums];
     __shared__ int s_g[kMaxRigCams][4];
-    __shared__ double s_M[36];
+    __shared__ double s_M[kMaxRigCams][36];
+    __shared__ double s_Ad[kMaxRigCams][36];
+    __shared__ double s_con[kMaxRigCams][kSums];
+    __shared__ int s_camarr[kMaxRigCams];
     __shared__ double s_pose[12];
     __shared__ double s_last[12];  // merged L(3): this workgroup's camera `last` pose E_c T_prev
     __shared__ double s_pts[kMaxTile * kSums];
@@ -1244,6 +1253,7 @@ __global__ __launch_bounds__(kRigThreads) void rig_level_kernel(RigArgs ra) {
     __shared__ int s_cnt;
     __shared__ int s_arrive;
     __shared__ PfLds s_pf;
+    PROBE_DECL();
     const int lv = ra.level;
     const bool merged = MERGED;  // launched for L(3) only
     const bool solve = lv < kLevels - 1 || merged;  // an unmerged L(3) is seeded
@@ -1257,17 +1267,27 @@ __global__ __launch_bounds__(kRigThreads) void rig_level_kernel(RigArgs ra) {
         s_arrive = 0;
         s_good = 0;
         s_cnt = 0;
+#ifdef VISO_PROBE
+        for (int k = 0; k < kPSt; ++k) pst[k] = 0;
+        pst[0] = probe_t0;
+        if (blockIdx.x < 256) g_pblk[a.probe_seq & (kPRingB - 1)][blockIdx.x][0] = probe_t0;
+#endif
     }
-    lds_barrier();
+    if (t < kMaxRigCams) s_camarr[t] = 0;
     // ---- every camera's tile partials of level sl (wave w: camera w / 4,
-    // tiles 64 (w % 4) .. +63 of it, when the camera has that many waves)
+    // tiles 64 (w % 4) .. +63 of it, when the camera has that many waves),
+    // issued before the first LDS barrier (it waits for LDS traffic only)
     static_assert(kRigWaves >= 4 * kMaxRigCams, "four reduce waves per camera");
     const int rc = wave >> 2, rq = wave & 3;
-    if (solve && rc < ra.n_cams && rq < rig_reduce_waves(ra.cam[rc].d.n_tiles)) {
+    const int q_rc = rc < ra.n_cams ? rig_reduce_waves(ra.cam[rc].d.n_tiles) : 0;
+    const bool rwave = solve && rq < q_rc;
+    double v[kSums];
+    int gg = 0;
+    double ad = 0.0;  // the leader stages Ad(E_c) (its load overlaps the partials')
+    if (rwave) {
         const DirectArgs& aw = ra.cam[rc].d;
         const int tl = 64 * rq + lane;
-        double v[kSums];
-        int gg = 0;
+        if (rq == 0 && lane < 36) ad = ra.cam[rc].Ad[lane];
         if (tl < aw.n_tiles) {
             const double* src = aw.s.part + (size_t)sl * kRigTiles * kSums;  // k-major [28][256]
 #pragma unroll
@@ -1277,16 +1297,29 @@ __global__ __launch_bounds__(kRigThreads) void rig_level_kernel(RigArgs ra) {
 #pragma unroll
             for (int k = 0; k < kSums; ++k) v[k] = 0.0;
         }
+    }
+    lds_barrier();
+    if (rwave) {
         int idx;
         const double f = reduce_scatter_28(v, &idx);
         if (lane < 32 && idx >= 0) s_red[rc][rq][idx] = f;
         const int g = wave_sum_int(gg);
         if (lane == 0) s_g[rc][rq] = g;
+        if (rq == 0 && lane < 36) s_Ad[rc][lane] = ad;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane == 0) atomicAdd(&s_arrive, 1);
+        if (rq > 0) {
+            if (lane == 0) atomicAdd(&s_camarr[rc], 1);
+        } else {
+            // the camera's other waves, then its contribution
+            while (__hip_atomic_load(&s_camarr[rc], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < q_rc - 1)
+                __builtin_amdgcn_s_sleep(1);
+            rig_contrib(q_rc, s_red[rc], s_Ad[rc], s_M[rc], s_con[rc]);
+            if (lane == 0) atomicAdd(&s_arrive, 1);
+        }
     }
-    // ---- the T this level starts from (thread 256)
-    if (t == 256) {
+    // ---- the T this level starts from (thread 192: wave 3 reduces only for
+    // a camera of more than 192 tiles)
+    if (t == 192) {
         double st[7];
         if (!solve) {
             quat_from_matrix(ra.seed, st);
@@ -1326,14 +1359,14 @@ __global__ __launch_bounds__(kRigThreads) void rig_level_kernel(RigArgs ra) {
     }
     // ---- the solve (wave 0)
     if (wave == 0) {
-        int need = 1;
-        if (solve)
-            for (int cc = 0; cc < ra.n_cams; ++cc) need += rig_reduce_waves(ra.cam[cc].d.n_tiles);
+        const int need = 1 + (solve ? ra.n_cams : 0);  // the start T, each camera's contribution
         while (__hip_atomic_load(&s_arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
             __builtin_amdgcn_s_sleep(1);
+        PST(1);
         if (solve) {
             __builtin_amdgcn_s_setprio(3);
-            rig_combine(ra, s_red, s_g, s_M, L);
+            rig_fold(ra, s_con, s_g, L);
+            PST(2);
             double* stp = (ra.stats && blockIdx.x == 0) ? ra.stats + (size_t)kStats * sl : nullptr;
             if (FAST)
                 solve_wave0_ldlt(L, 0, stp);
@@ -1378,8 +1411,13 @@ __global__ __launch_bounds__(kRigThreads) void rig_level_kernel(RigArgs ra) {
             if (blockIdx.x == 0 && lv >= 0)
                 for (int k = 0; k < 7; ++k) ra.state[lv * kStateStride + k] = L.state[k];
         }
+        PST(7);
     }
     __syncthreads();  // B2
+    if (wave == 0) PST(8);
+#ifdef VISO_PROBE
+    if (t == 0 && blockIdx.x < 256) g_pblk[a.probe_seq & (kPRingB - 1)][blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+#endif
     if (tiles) {
         LevelPair fp = level_pair(a.fp, lv);
         if (merged) fp.pose_last = s_last;
@@ -1390,6 +1428,18 @@ __global__ __launch_bounds__(kRigThreads) void rig_level_kernel(RigArgs ra) {
                                               a.s.part + (size_t)lv * kRigTiles * kSums, a.s.good + lv * kRigTiles,
                                               s_pts, &s_good, &s_cnt);
     }
+#ifdef VISO_PROBE
+    const unsigned long long t_exit = __builtin_amdgcn_s_memrealtime();
+    const int slot = a.probe_seq & (kPRing - 1);
+    if (t == 0) atomicMax(&g_pexit[slot], t_exit);
+    if (t == 0 && blockIdx.x < 256) g_pblk[a.probe_seq & (kPRingB - 1)][blockIdx.x][3] = t_exit;
+    if (blockIdx.x == 0 && t == 0) {
+        pst[11] = t_exit;
+        pst[15] = (unsigned long long)(lv + 1) | ((unsigned long long)merged << 8) |
+                  ((unsigned long long)a.n_tiles << 16);
+        for (int k = 0; k < kPSt; ++k) g_plog[slot][k] = pst[k];
+    }
+#endif
 }
 static_assert(sizeof(RigArgs) <= 4096, "rig kernel arguments exceed 4 KB");
 
@@ -1579,6 +1629,12 @@ int launch_rig_direct(const RigCamDev* cams, int n_cams, const PyrGeom& g, const
     const int grid = off > 0 ? off : 1;
     for (int level = levels ? kLevels - 1 : -1; level >= -1; --level) {
         ra.level = level;
+#ifdef VISO_PROBE
+        {
+            const int seq = next_probe_seq();
+            for (int c = 0; c < n_cams; ++c) ra.cam[c].d.probe_seq = seq;
+        }
+#endif
         ra.merged = 0;
         if (level == kLevels - 1 && merge_prev) {
             ra.merged = 1;

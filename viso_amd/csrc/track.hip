@@ -120,9 +120,13 @@ __device__ inline double win_bilinear(const Window& win, double x, double y, int
     return double((1 - xx) * (1 - yy) * d0 + xx * (1 - yy) * d1 + (1 - xx) * yy * d2 + xx * yy * d3);
 }
 
+// FINITE: the caller guarantees |x|, |y| < 1e9 (LKAlignment: the bounds test
+// passed, so d is within a level of the patch), which sample_px's own guard
+// would find true
+template <bool FINITE = false>
 __device__ inline double sample_win(const uint8_t* __restrict__ img, int w, int h, double x,
                                     double y, const Window& win) {
-    const bool finite = (x > -1e9 && x < 1e9 && y > -1e9 && y < 1e9);
+    const bool finite = FINITE || (x > -1e9 && x < 1e9 && y > -1e9 && y < 1e9);
     const int ix = finite ? (int)x : 0, iy = finite ? (int)y : 0;
     const bool in = finite && win.lds != nullptr && ix >= win.x0 && ix + 1 < win.x0 + kWinW && iy >= win.y0 &&
                     iy + 1 < win.y0 + kWinH;
@@ -183,6 +187,14 @@ __device__ inline LkResult lk_iterate(const LkTemplate& t, int w1, int h1,
     dy = uniform_f64(dy);
     const double i00 = uniform_f64(t.i00), i01 = uniform_f64(t.i01), i10 = uniform_f64(t.i10),
                  i11 = uniform_f64(t.i11);
+    // LKAlignment's bounds test (both corners, 8 comparisons of uniform
+    // values) runs lane-parallel: lane l tests coordinate l & 1 (x, y) of
+    // corner l & 2 (-hp, +hp), (b + d) + (-+hp) in [0, w or h), the same
+    // operations as inside_px on (b + d) -+ hp
+    const int lq = threadIdx.x & 3;
+    const double b_l = (lq & 1) ? by : bx;
+    const double off_l = (lq & 2) ? hp : -hp;
+    const double lim_l = (double)((lq & 1) ? h1 : w1);
     double cost = 0, lastCost = 0;
     bool succ = true;
     int iter = 0;
@@ -191,14 +203,14 @@ __device__ inline LkResult lk_iterate(const LkTemplate& t, int w1, int h1,
         if (KLT_BOUNDS) {  // src/viso.cpp:286
             out = bx + dx <= hp || bx + dx >= w1 - hp || by + dy <= hp || by + dy >= h1 - hp;
         } else {  // src/viso.cpp:869-873 (ref coords + d, both corners)
-            out = !inside_px(bx + dx - hp, by + dy - hp, w1, h1) ||
-                  !inside_px(bx + dx + hp, by + dy + hp, w1, h1);
+            const double q = (b_l + ((lq & 1) ? dy : dx)) + off_l;
+            out = __builtin_amdgcn_ballot_w64(!(q >= 0 && q < lim_l)) != 0;
         }
         if (out) {
             succ = false;
             break;
         }
-        const double e = t.I1 - sample_win(img2, w2, h2, cur_x + dx, cur_y + dy, win);
+        const double e = t.I1 - sample_win<!KLT_BOUNDS>(img2, w2, h2, cur_x + dx, cur_y + dy, win);
         double B0, B1;
         wave_tree_sum3(-t.J0 * e, -t.J1 * e, e * e, B0, B1, cost);
         const double u0 = i00 * B0 + i01 * B1;
@@ -245,8 +257,14 @@ __device__ inline LkResult lk_iterate_fast(float I1, float J0, float J1, const f
     bool succ = true;
     int iter = 0;
     const long long n2 = (long long)w2 * h2;
+    // the bounds test lane-parallel, as in lk_iterate
+    const int lq = threadIdx.x & 3;
+    const double b_l = (lq & 1) ? by : bx;
+    const double off_l = (lq & 2) ? hp : -hp;
+    const double lim_l = (double)((lq & 1) ? h1 : w1);
     for (; iter < MAXIT; ++iter) {
-        if (!inside_px(bx + dx - hp, by + dy - hp, w1, h1) || !inside_px(bx + dx + hp, by + dy + hp, w1, h1)) {
+        const double q = (b_l + ((lq & 1) ? dy : dx)) + off_l;
+        if (__builtin_amdgcn_ballot_w64(!(q >= 0 && q < lim_l)) != 0) {
             succ = false;
             break;
         }
