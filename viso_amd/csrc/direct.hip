@@ -1157,10 +1157,15 @@ __device__ inline void rig_compose(const double* E, const double* T, double* out
     }
 }
 
+// (unrolled with unconditional kernarg reads: the loads issue together
+// instead of one dependent round trip per camera)
 __device__ inline int rig_camera(const RigArgs& ra, int b) {
     int c = 0;
-    for (int k = 1; k < ra.n_cams; ++k)
-        if (b >= ra.tile_off[k]) c = k;
+#pragma unroll
+    for (int k = 1; k < kMaxRigCams; ++k) {
+        const int off = ra.tile_off[k];
+        if (k < ra.n_cams && b >= off) c = k;
+    }
     return c;
 }
 
@@ -1254,11 +1259,47 @@ __global__ __launch_bounds__(kRigThreads) void rig_level_kernel(RigArgs ra) {
     __shared__ int s_arrive;
     __shared__ PfLds s_pf;
     PROBE_DECL();
-    const int lv = ra.level;
+    // wave-uniform in SGPRs: ra.cam[wave / 4] is then read with scalar loads
+    const int t = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
+    // ---- every camera's tile partials of level sl (wave w: camera w / 4,
+    // tiles 64 (w % 4) .. +63 of it, when the camera has that many waves),
+    // issued first (before the workgroup's own camera is looked up and
+    // before the first LDS barrier, which waits for LDS traffic only)
+    static_assert(kRigWaves >= 4 * kMaxRigCams, "four reduce waves per camera");
+    const int rc = wave >> 2, rq = wave & 3;
+    // the kernel arguments this wave's loads need, read unconditionally
+    // (cam[rc] exists for every rc < kMaxRigCams) so the scalar loads issue
+    // together: one argument round trip before the partial loads
+    const int rc_tiles = ra.cam[rc].d.n_tiles;
+    const double* rc_part = ra.cam[rc].d.s.part;
+    const int* rc_good = ra.cam[rc].d.s.good;
+    const double* rc_ad = ra.cam[rc].Ad;
+    int lv_arg = ra.level;
+    // (the empty asm takes every argument at once and hands the level on:
+    // nothing derived from it is scheduled between the scalar loads)
+    asm volatile("" : "+s"(lv_arg) : "s"(rc_tiles), "s"(rc_part), "s"(rc_good), "s"(rc_ad));
+    const int lv = lv_arg;
     const bool merged = MERGED;  // launched for L(3) only
     const bool solve = lv < kLevels - 1 || merged;  // an unmerged L(3) is seeded
     const int sl = merged ? 0 : lv + 1;              // level solved in the prologue (F: 0)
-    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+    const int q_rc = rc < ra.n_cams ? rig_reduce_waves(rc_tiles) : 0;
+    const bool rwave = solve && rq < q_rc;
+    double v[kSums];
+    int gg = 0;
+    double ad = 0.0;  // the leader stages Ad(E_c) (its load overlaps the partials')
+    if (rwave) {
+        const int tl = 64 * rq + lane;
+        if (rq == 0 && lane < 36) ad = rc_ad[lane];
+        if (tl < rc_tiles) {
+            const double* src = rc_part + (size_t)sl * kRigTiles * kSums;  // k-major [28][256]
+#pragma unroll
+            for (int k = 0; k < kSums; ++k) v[k] = src[(size_t)k * kRigTiles + tl];
+            gg = rc_good[sl * kRigTiles + tl];
+        } else {
+#pragma unroll
+            for (int k = 0; k < kSums; ++k) v[k] = 0.0;
+        }
+    }
     const int c = rig_camera(ra, blockIdx.x);
     const int bt = (int)blockIdx.x - ra.tile_off[c];
     const DirectArgs& a = ra.cam[c].d;
@@ -1274,30 +1315,6 @@ __global__ __launch_bounds__(kRigThreads) void rig_level_kernel(RigArgs ra) {
 #endif
     }
     if (t < kMaxRigCams) s_camarr[t] = 0;
-    // ---- every camera's tile partials of level sl (wave w: camera w / 4,
-    // tiles 64 (w % 4) .. +63 of it, when the camera has that many waves),
-    // issued before the first LDS barrier (it waits for LDS traffic only)
-    static_assert(kRigWaves >= 4 * kMaxRigCams, "four reduce waves per camera");
-    const int rc = wave >> 2, rq = wave & 3;
-    const int q_rc = rc < ra.n_cams ? rig_reduce_waves(ra.cam[rc].d.n_tiles) : 0;
-    const bool rwave = solve && rq < q_rc;
-    double v[kSums];
-    int gg = 0;
-    double ad = 0.0;  // the leader stages Ad(E_c) (its load overlaps the partials')
-    if (rwave) {
-        const DirectArgs& aw = ra.cam[rc].d;
-        const int tl = 64 * rq + lane;
-        if (rq == 0 && lane < 36) ad = ra.cam[rc].Ad[lane];
-        if (tl < aw.n_tiles) {
-            const double* src = aw.s.part + (size_t)sl * kRigTiles * kSums;  // k-major [28][256]
-#pragma unroll
-            for (int k = 0; k < kSums; ++k) v[k] = src[(size_t)k * kRigTiles + tl];
-            gg = aw.s.good[sl * kRigTiles + tl];
-        } else {
-#pragma unroll
-            for (int k = 0; k < kSums; ++k) v[k] = 0.0;
-        }
-    }
     lds_barrier();
     if (rwave) {
         int idx;
