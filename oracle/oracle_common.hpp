@@ -80,9 +80,9 @@ inline int map_tile(int n, int groups) {
     return t;
 }
 
-inline double map_tree_sum(const double* v, int n, int groups) {
+// the two-level sum over tiles of T points (the last tile ragged)
+inline double map_tree_sum_tiles(const double* v, int n, int T) {
     if (n <= 0) return 0.0;
-    const int T = map_tile(n, groups);
     const int nt = (n + T - 1) / T;
     std::vector<double> heap;
     double stack[256];
@@ -96,6 +96,10 @@ inline double map_tree_sum(const double* v, int n, int groups) {
         tiles[t] = tree_sum(v + (size_t)t * T, c);
     }
     return tree_sum(tiles, nt);
+}
+
+inline double map_tree_sum(const double* v, int n, int groups) {
+    return n <= 0 ? 0.0 : map_tree_sum_tiles(v, n, map_tile(n, groups));
 }
 
 // Summation order switch (oracle_set_sum_order, viso_oracle.h).  0: the

@@ -87,10 +87,11 @@ void pose12_of_se3(const SE3& s, double* out) {
     for (int i = 0; i < 3; ++i) out[9 + i] = s.t[i];
 }
 
-// Camera c's 28 canonical sums at cur_pose (map_tree_sum over its points,
-// groups = 256 / pow2(n_cams): the device's tiles per camera); returns nGood
+// Camera c's 28 canonical sums at cur_pose (the two-level map tree over its
+// points in tiles of `tile` points: the device's workgroup tiles); returns
+// nGood
 int camera_sums(const PyrView& last, const PyrView& cur, const double K[4], const double* points, int n,
-                const Pose& last_pose, const Pose& cur_pose, int level, int groups, double S[28]) {
+                const Pose& last_pose, const Pose& cur_pose, int level, int tile, double S[28]) {
     std::vector<double> part((size_t)n * 28), leaf((size_t)n);
     int good = 0;
     for (int i = 0; i < n; ++i) {
@@ -102,7 +103,7 @@ int camera_sums(const PyrView& last, const PyrView& cur, const double K[4], cons
     }
     for (int k = 0; k < 28; ++k) {
         for (int i = 0; i < n; ++i) leaf[(size_t)i] = part[(size_t)i * 28 + k];
-        S[k] = map_tree_sum(leaf.data(), n, groups);
+        S[k] = map_tree_sum_tiles(leaf.data(), n, tile);
     }
     return good;
 }
@@ -157,9 +158,12 @@ void oracle_rig_direct(int n_cams, const uint8_t* const* last_pyrs, const uint8_
         oracle_rig_adjoint(extrinsics + 12 * c, Ad[(size_t)c].data());
     }
     SE3 T = se3_from_Rt(pose_io, pose_io + 9);
-    int pc = 1;
-    while (pc < n_cams) pc <<= 1;
-    const int groups = 256 / pc;
+    // one tile size for every camera, from the rig's total map: the cameras'
+    // tiles then fill the device's 256 workgroups in proportion to their
+    // points (a one-camera rig tiles exactly as the direct pose)
+    int n_total = 0;
+    for (int c = 0; c < n_cams; ++c) n_total += n_points[c];
+    const int tile = map_tile(n_total, 256);
     for (int level = 3; level >= 0; --level) {
         double T12[12];
         pose12_of_se3(T, T12);
@@ -170,7 +174,7 @@ void oracle_rig_direct(int n_cams, const uint8_t* const* last_pyrs, const uint8_
             oracle_rig_compose(extrinsics + 12 * c, T12, Tc);
             double S[28], V[28];
             ngood += camera_sums(L[(size_t)c], C[(size_t)c], K, points[c], n_points[c],
-                                 pose_of12(cam_last + 12 * c), pose_of12(Tc), level, groups, S);
+                                 pose_of12(cam_last + 12 * c), pose_of12(Tc), level, tile, S);
             transform_sums(Ad[(size_t)c].data(), S, V);
             for (int k = 0; k < 28; ++k) acc[k] = c == 0 ? V[k] : acc[k] + V[k];
         }

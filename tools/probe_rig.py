@@ -57,7 +57,8 @@ def main():
     kinds = [("L3m", keep & (lvl == 3) & (merged == 1)), ("L2", keep & (lvl == 2)), ("L1", keep & (lvl == 1)),
              ("L0", keep & (lvl == 0)), ("F", keep & (lvl == -1))]
     print("phase (us from block 0 entry)       " + "  ".join(f"{k:>7s}" for k, _ in kinds))
-    for k, name in [(1, "partials in (w0)"), (2, "combine done"), (7, "solve done"), (8, "after B2"), (11, "block 0 exit")]:
+    for k, name in [(3, "w0: its partial loads landed"), (4, "w0: camera 0 contribution"),
+                    (1, "every contribution in (w0)"), (2, "fold done"), (7, "solve done"), (8, "after B2"), (11, "block 0 exit")]:
         row = []
         for _, sel0 in kinds:
             sel = sel0 & (log[:, k] > 0)

@@ -1105,12 +1105,15 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
 // points; a rig perturbation xi moves camera c by Ad(E_c) xi, so
 //   H = sum_c Ad_c^T H_c Ad_c,  b = sum_c Ad_c^T b_c,  cost = sum_c cost_c
 // (cameras ascending), then the direct pose's solve and T <- exp(update) T
-// (unchanged when the update is NaN).  Launches per frame: L(3..0) + F, the
-// tiles of all cameras in one grid (workgroup = one tile of one camera), the
-// prologue of L(l) solving level l+1 from every camera's tile partials.
-// Tiles per camera: up to 256 (T <= 64 points each covers kMaxMapPoints);
-// a camera's partials are reduced by 1, 2 or 4 waves (64 tiles each) and
-// the waves' sums folded as the canonical tree's top levels.
+// (unchanged when the update is NaN).  Launches per timestep: L(3..0), the
+// final solve merged into the next timestep's L(3) within an ingest call
+// (F at the call's end); the tiles of all cameras in one grid (workgroup =
+// one tile of one camera), the prologue of L(l) solving level l+1 from
+// every camera's tile partials.  Tiles: one size T = map_tile(rig total,
+// 256) for every camera, so the cameras share the 256 workgroups in
+// proportion to their points; up to 256 per camera (T <= 64 points covers
+// kMaxMapPoints); a camera's partials are reduced by 1, 2 or 4 waves (64
+// tiles each) and the waves' sums folded as the canonical tree's top levels.
 constexpr int kRigTiles = kMaxTiles;  // also the k-major partial stride of direct_tile_pf
 
 // waves reducing a camera of n_tiles tiles (the canonical tree over 64 q tiles)
@@ -1316,6 +1319,12 @@ __global__ __launch_bounds__(kRigThreads) void rig_level_kernel(RigArgs ra) {
     }
     if (t < kMaxRigCams) s_camarr[t] = 0;
     lds_barrier();
+#ifdef VISO_PROBE
+    if (rwave && wave == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        PST(3);
+    }
+#endif
     if (rwave) {
         int idx;
         const double f = reduce_scatter_28(v, &idx);
@@ -1331,6 +1340,7 @@ __global__ __launch_bounds__(kRigThreads) void rig_level_kernel(RigArgs ra) {
             while (__hip_atomic_load(&s_camarr[rc], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < q_rc - 1)
                 __builtin_amdgcn_s_sleep(1);
             rig_contrib(q_rc, s_red[rc], s_Ad[rc], s_M[rc], s_con[rc]);
+            if (wave == 0) PST(4);
             if (lane == 0) atomicAdd(&s_arrive, 1);
         }
     }
@@ -1582,21 +1592,14 @@ void launch_direct_final(const FrameDev& last_pyr, const FrameDev& cur_pyr, cons
         direct_level_kernel<false><<<1, kThreads, 0, stream>>>(a);
 }
 
-// Tiles of a rig camera with n <= kMaxMapPoints points: faithful, the
-// canonical map tree's tiles with groups = 256 / pow2(n_cams) (T =
-// map_tile(n, groups) <= kMaxTile points, <= kRigTiles tiles); tolerance
-// mode, min(n, groups) even slices (more when a slice would exceed kMaxTile).
-static int rig_tiling(int n, int groups, bool split, int* tile, int* n_tiles) {
+// A rig camera of n points in tiles of T points (T shared by the cameras,
+// map_tile of the rig's total; oracle_rig.cpp); tolerance mode (split) evens
+// the points over the same number of tiles
+static int rig_tiling(int n, int T, bool split, int* tile, int* n_tiles) {
     if (n < 0 || n > kMaxMapPoints) return -1;
-    const int T = map_tile(n, groups);
     *tile = T;
     *n_tiles = (n + T - 1) / T;
-    if (split && n > 0) {
-        int nt = n < groups ? n : groups;
-        if ((n + nt - 1) / nt > kMaxTile) nt = (n + kMaxTile - 1) / kMaxTile;
-        *n_tiles = nt;
-        *tile = (n + nt - 1) / nt;
-    }
+    if (split && n > 0) *tile = (n + *n_tiles - 1) / *n_tiles;
     // the prefetch and tile tree hold at most kMaxTile points per workgroup
     return (*tile <= kMaxTile && *n_tiles <= kRigTiles) ? 0 : -1;
 }
@@ -1611,9 +1614,11 @@ int launch_rig_direct(const RigCamDev* cams, int n_cams, const PyrGeom& g, const
     const bool fast = precision == VISO_PRECISION_FAST;
     RigArgs ra{};
     ra.n_cams = n_cams;
-    int pc = 1;
-    while (pc < n_cams) pc <<= 1;
-    const int groups = kMaxTiles / pc;  // tiles per camera: the cameras fill 256 workgroups
+    // tiles of one size for every camera (map_tile of the rig's total map):
+    // the cameras' tiles fill the 256 workgroups in proportion to their points
+    int n_total = 0;
+    for (int c = 0; c < n_cams; ++c) n_total += cams[c].n > 0 ? cams[c].n : 0;
+    const int T = map_tile(n_total, kMaxTiles);
     int off = 0;
     for (int c = 0; c < n_cams; ++c) {
         const RigCamDev& cd = cams[c];
@@ -1625,7 +1630,7 @@ int launch_rig_direct(const RigCamDev* cams, int n_cams, const PyrGeom& g, const
         a.K = Intrinsics{K[0], K[1], K[2], K[3]};
         a.points = cd.points;
         a.n = cd.n;
-        if (rig_tiling(cd.n, groups, fast, &a.tile, &a.n_tiles) != 0) return -1;
+        if (rig_tiling(cd.n, T, fast, &a.tile, &a.n_tiles) != 0) return -1;
         a.split = fast && cd.n > 0 ? 1 : 0;
         a.s.part = (double*)cd.scratch;
         a.s.good = (int*)((char*)cd.scratch + (size_t)kLevels * kRigTiles * kSums * 8);
