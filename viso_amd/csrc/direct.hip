@@ -1264,12 +1264,14 @@ __global__ __launch_bounds__(kRigThreads) void rig_level_kernel(RigArgs ra) {
     PROBE_DECL();
     // wave-uniform in SGPRs: ra.cam[wave / 4] is then read with scalar loads
     const int t = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
-    // ---- every camera's tile partials of level sl (wave w: camera w / 4,
-    // tiles 64 (w % 4) .. +63 of it, when the camera has that many waves),
+    // ---- every camera's tile partials of level sl (wave w: camera w % 4,
+    // tiles 64 (w / 4) .. +63 of it, when the camera has that many waves:
+    // the cameras' leaders 0..3 sit on different SIMDs, so their reductions
+    // and transforms run side by side),
     // issued first (before the workgroup's own camera is looked up and
     // before the first LDS barrier, which waits for LDS traffic only)
     static_assert(kRigWaves >= 4 * kMaxRigCams, "four reduce waves per camera");
-    const int rc = wave >> 2, rq = wave & 3;
+    const int rc = wave & 3, rq = wave >> 2;
     // the kernel arguments this wave's loads need, read unconditionally
     // (cam[rc] exists for every rc < kMaxRigCams) so the scalar loads issue
     // together: one argument round trip before the partial loads
