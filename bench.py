@@ -8,7 +8,10 @@ seed = rank); they are rendered on the host and uploaded to HBM before the
 timed region.  A "step" is one stereo frame through
 viso_process_frames_device (batched pyramid build of the left images, then
 Viso::OnNewFrame on the left image, src/viso.cpp:7-145, with tracking
-enabled so the direct-pose GN and LK alignment run every frame).  Stereo
+enabled so the direct-pose GN and LK alignment run every frame).  Frames are
+ingested in chunks of --batch (default 128, two chunks in the default 256
+timed frames): a chunk's image pass and LK alignment are one launch each,
+its poses come back when the chunk is done.  Stereo
 initialisation (viso_set_stereo) creates the map from frame 0's pair; the
 warmup runs W frames and then, if needed, single frames until the state is
 kRunning (bounded; otherwise exit 3), so the K timed frames are tracking
@@ -58,11 +61,12 @@ def log(*a):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=256)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--width", type=int, default=1242)
     ap.add_argument("--height", type=int, default=375)
-    ap.add_argument("--batch", type=int, default=50, help="frames per batched ingest call")
+    ap.add_argument("--batch", type=int, default=128,
+                    help="frames per batched ingest call (the engine's maximum image-pass chunk, kPyrBatch)")
     ap.add_argument("--cpu-frames", type=int, default=200,
                     help="timed tracking frames of the CPU oracle sample (0 = skip)")
     ap.add_argument("--no-cpu", action="store_true")

@@ -12,7 +12,7 @@ tail -1 $OUT/pytest.log
 for lib in prod $2; do
   if [ "$lib" != prod ]; then export VISO_LIB=$lib; fi
   tag=$(basename $lib .so)
-  for n in 50 20; do
+  for n in ${NS:-50 20}; do
     IMAGES=$n REPS=10 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $OUT/${tag}_k$n -o run -- python -u tools/bench_pyramid.py > $OUT/${tag}_k$n.log 2>&1 || { tail -20 $OUT/${tag}_k$n.log; exit 1; }
     python tools/db2stats.py $OUT/${tag}_k$n/run_results.db $OUT/${tag}_k$n.csv
     echo "$tag $n images"; grep -E "pyr_" $OUT/${tag}_k$n.csv | cut -c1-200
