@@ -1,5 +1,6 @@
 #!/bin/bash
 # Dev experiment: LK alignment beside the direct chain (side stream, CU split).
+# (The VISO_EXP_* hooks this script drives were removed after the experiment; see DESIGN.md, round-3 log.)
 set -o pipefail
 OUT=gpurun_out/${1:-lkov}
 mkdir -p $OUT
