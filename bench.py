@@ -675,6 +675,12 @@ def pmc_evidence(W, H, breakdown, stereo_vo, n_map=None):
               "bound": "latency / VALU (four dependent best-SAD searches per feature over a cache-resident "
                        "descriptor set), not HBM",
               "source": "profiles/r03_gn_svo_pmc.json (FETCH_SIZE x2 + WRITE_SIZE)"}
+        if c.get("valu_busy") is not None:
+            mp.update({"valu_busy": c["valu_busy"], "valu_insts": c["valu_insts"],
+                       "valu_insts_per_us": c["valu_insts_per_us"],
+                       "mean_resident_waves_per_cu": c["mean_resident_waves_per_cu"],
+                       "sq_source": "profiles/r03_gn_svo_pmc.json (SQ_INSTS_VALU, SQ_ACTIVE_INST_VALU in "
+                                    "quad-cycles, SQ_WAVE_CYCLES; separate rocprofv3 pass)"})
     return gn, mp
 
 

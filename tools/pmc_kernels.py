@@ -59,6 +59,7 @@ def main():
     run, out = sys.argv[1], sys.argv[2]
     occ, f64 = load(os.path.join(run, "gn_occ")), load(os.path.join(run, "gn_f64"))
     sf, sw = load(os.path.join(run, "svo_f")), load(os.path.join(run, "svo_w"))
+    sq = load(os.path.join(run, "svo_sq"))
     res = {"source": f"rocprofv3 --pmc passes of tools/gpu_pmc.sh ({os.path.basename(run.rstrip('/'))})",
            "cus": CUS, "clock_ghz": CLK_GHZ, "gn": {}, "svo": {}}
     for k in ("direct_level_kernel", "lk_align_kernel", "pyr_down_sk_kernel"):
@@ -94,6 +95,18 @@ def main():
                          "write_bytes": round(1024 * wb) if wb is not None else None,
                          "traffic_bytes": round(2 * 1024 * fb + 1024 * wb) if fb is not None and wb is not None else None,
                          "pmc_duration_us": round(mean(sf.get(k, sw.get(k)), "_dur_ns") / 1e3, 2)}
+        if k in sq:
+            ds = sq[k]
+            dur = mean(ds, "_dur_ns")
+            cyc = dur * CLK_GHZ
+            res["svo"][k].update({
+                "sq_duration_us": round(dur / 1e3, 2),
+                "valu_insts": round(mean(ds, "SQ_INSTS_VALU")), "salu_insts": round(mean(ds, "SQ_INSTS_SALU")),
+                "lds_insts": round(mean(ds, "SQ_INSTS_LDS")),
+                "valu_insts_per_us": round(mean(ds, "SQ_INSTS_VALU") / (dur / 1e3), 1),
+                # SQ_ACTIVE_INST_VALU counts quad-cycles: the fraction of SIMD cycles issuing VALU
+                "valu_busy": round(4 * mean(ds, "SQ_ACTIVE_INST_VALU") / (cyc * CUS * 4), 4),
+                "mean_resident_waves_per_cu": round(4 * mean(ds, "SQ_WAVE_CYCLES") / (cyc * CUS), 2)})
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 

@@ -489,7 +489,7 @@ __device__ inline void wave_lds_sync() {
 __device__ void smallest_eigvec9_rr(const double* __restrict__ Min, double* out) {
     constexpr int N = 9, M = 10, R = 9, P = 5;
     __shared__ double sA[81], sV[81], sc[P], ss[P];
-    __shared__ int sp[P], sq[P], sact[P];
+    __shared__ int sact[P];
     const int lane = threadIdx.x & 63;
     for (int k = lane; k < 81; k += 64) {
         sA[k] = Min[k];
@@ -521,35 +521,46 @@ __device__ void smallest_eigvec9_rr(const double* __restrict__ Min, double* out)
                     cc = 1.0 / sqrt(t * t + 1.0);
                     sn = t * cc;
                 }
-                sp[lane] = p;
-                sq[lane] = q;
                 sact[lane] = act ? 1 : 0;
                 sc[lane] = cc;
                 ss[lane] = sn;
             }
             wave_lds_sync();
-            // column pairs of A (tasks 0..44) and of V (45..89)
-            for (int task = lane; task < 2 * P * N; task += 64) {
-                const int u = task < P * N ? task : task - P * N;
-                const int i = u / N, k = u - N * (u / N);
-                if (!sact[i]) continue;
-                double* X = task < P * N ? sA : sV;
-                const int p = sp[i], q = sq[i];
-                const double c = sc[i], s = ss[i];
-                const double xkp = X[N * k + p], xkq = X[N * k + q];
-                X[N * k + p] = c * xkp - s * xkq;
-                X[N * k + q] = s * xkp + c * xkq;
+            // lane (i, k) < 45: pair i's rotation of column pairs (p, q) of A
+            // and of V at row k, then of A's row pairs at column k; (p, q)
+            // from the circle method in registers, so a lane's loads need
+            // one LDS round trip (rotation + operands together)
+            if (lane < P * N) {
+                const int i = lane / N, k = lane - N * (lane / N);
+                const int a0 = i == 0 ? 0 : 1 + (i - 1 + r) % (M - 1);
+                const int b0 = 1 + (M - 1 - i - 1 + r) % (M - 1);
+                const int p = a0 < b0 ? a0 : b0, q0 = a0 < b0 ? b0 : a0;
+                const int q = q0 < N ? q0 : p;  // the idle pair (q0 = 9) loads in bounds, stores nothing
+                const bool act = sact[i] != 0;
+                const double c = sc[i], sn = ss[i];
+                const double akp = sA[N * k + p], akq = sA[N * k + q];
+                const double vkp = sV[N * k + p], vkq = sV[N * k + q];
+                if (act) {
+                    sA[N * k + p] = c * akp - sn * akq;
+                    sA[N * k + q] = sn * akp + c * akq;
+                    sV[N * k + p] = c * vkp - sn * vkq;
+                    sV[N * k + q] = sn * vkp + c * vkq;
+                }
             }
             wave_lds_sync();
             // row pairs of A
             if (lane < P * N) {
                 const int i = lane / N, k = lane - N * (lane / N);
-                if (sact[i]) {
-                    const int p = sp[i], q = sq[i];
-                    const double c = sc[i], s = ss[i];
-                    const double apk = sA[N * p + k], aqk = sA[N * q + k];
-                    sA[N * p + k] = c * apk - s * aqk;
-                    sA[N * q + k] = s * apk + c * aqk;
+                const int a0 = i == 0 ? 0 : 1 + (i - 1 + r) % (M - 1);
+                const int b0 = 1 + (M - 1 - i - 1 + r) % (M - 1);
+                const int p = a0 < b0 ? a0 : b0, q0 = a0 < b0 ? b0 : a0;
+                const int q = q0 < N ? q0 : p;
+                const bool act = sact[i] != 0;
+                const double c = sc[i], sn = ss[i];
+                const double apk = sA[N * p + k], aqk = sA[N * q + k];
+                if (act) {
+                    sA[N * p + k] = c * apk - sn * aqk;
+                    sA[N * q + k] = sn * apk + c * aqk;
                 }
             }
             wave_lds_sync();
