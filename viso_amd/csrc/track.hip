@@ -59,15 +59,19 @@ struct WinRegs {
     bool on;
 };
 
+// (cx, cy) is the wave's patch centre (the same in every lane): the window's
+// placement is taken into SGPRs, so every window test downstream is a
+// wave-uniform branch, not an EXEC-mask sequence
 __device__ inline WinRegs window_issue(const uint8_t* img, int w, int h, double cx, double cy) {
     WinRegs r;
-    r.on = !(w < kWinW || h < kWinH || !(cx > -1e6 && cx < 1e6 && cy > -1e6 && cy < 1e6));
+    r.on = __builtin_amdgcn_readfirstlane(
+               !(w < kWinW || h < kWinH || !(cx > -1e6 && cx < 1e6 && cy > -1e6 && cy < 1e6)) ? 1 : 0) != 0;
     r.x0 = r.y0 = 0;
     if (!r.on) return r;
     int x0 = (int)floor(cx) - kWinW / 2 + 1;
     int y0 = (int)floor(cy) - kWinH / 2 + 1;
-    x0 = min(max(x0, 0), w - kWinW);
-    y0 = min(max(y0, 0), h - kWinH);
+    x0 = __builtin_amdgcn_readfirstlane(min(max(x0, 0), w - kWinW));
+    y0 = __builtin_amdgcn_readfirstlane(min(max(y0, 0), h - kWinH));
     // byte e = lane + 64 k of the row-major window: row e / 24, column e % 24
     // (compile-time per k up to the lane), 32-bit offsets from the window's
     // first byte (a level is far below 2^31 bytes)
@@ -126,11 +130,14 @@ __device__ inline double win_bilinear(const Window& win, double x, double y, int
 template <bool FINITE = false>
 __device__ inline double sample_win(const uint8_t* __restrict__ img, int w, int h, double x,
                                     double y, const Window& win) {
+    if (!win.lds) return sample_px(img, w, h, x, y);  // wave-uniform (window_issue)
     const bool finite = FINITE || (x > -1e9 && x < 1e9 && y > -1e9 && y < 1e9);
     const int ix = finite ? (int)x : 0, iy = finite ? (int)y : 0;
-    const bool in = finite && win.lds != nullptr && ix >= win.x0 && ix + 1 < win.x0 + kWinW && iy >= win.y0 &&
-                    iy + 1 < win.y0 + kWinH;
-    if (__builtin_expect(__builtin_amdgcn_ballot_w64(!in) == 0, 1)) return win_bilinear(win, x, y, ix, iy);
+    // (unsigned offsets: one compare per axis; every lane is active here, so
+    // "all lanes in" is the ballot of `in` equal to the full mask)
+    const bool in = finite && (unsigned)(ix - win.x0) < (unsigned)(kWinW - 1) &&
+                    (unsigned)(iy - win.y0) < (unsigned)(kWinH - 1);
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(in) == ~0ull, 1)) return win_bilinear(win, x, y, ix, iy);
     return in ? win_bilinear(win, x, y, ix, iy) : sample_px(img, w, h, x, y);
 }
 
@@ -315,7 +322,7 @@ __global__ __launch_bounds__(256) void klt_kernel(FrameDev ref, FrameDev cur, Py
     if (i >= n) return;  // wave-uniform
     const int lane = threadIdx.x & 63;
     const int px = (lane >> 3) - 4, py = (lane & 7) - 4;
-    uint8_t* my_win = s_win[threadIdx.x >> 6];
+    uint8_t* my_win = s_win[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
     const float2 k1 = kp1[i];
     float2 k2 = kp2[i];
     // kp2[j].pt *= scales[3]  (saturate_cast<float>(x * 0.125))
@@ -464,8 +471,8 @@ __global__ __launch_bounds__(256, FAST ? VISO_LK_MIN_WAVES_FAST : VISO_LK_MIN_WA
     const double* cur_pose = fr.pose;
     const size_t o = (size_t)blockIdx.y * a.out_stride;
     const int lane = threadIdx.x & 63;
-    uint8_t* my_win0 = s_win[threadIdx.x >> 6][0];
-    uint8_t* my_win1 = s_win[threadIdx.x >> 6][1];
+    uint8_t* my_win0 = s_win[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)][0];
+    uint8_t* my_win1 = s_win[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)][1];
     const int px = (lane >> 3) - 4, py = (lane & 7) - 4;
     const double P[3] = {a.points[3 * i], a.points[3 * i + 1], a.points[3 * i + 2]};
     const Intrinsics K{a.K[0], a.K[1], a.K[2], a.K[3]};
