@@ -85,28 +85,36 @@ def main():
             e["fp64_flop_per_dispatch"] = round(ops)
             e["fp64_peak_tflops"] = FP64_PEAK_TFLOPS
         res["gn"][k] = e
+    # stereo-VO kernels: tools/bench_svo.py runs a 10-pair warm-up batch and
+    # then the measured 100-pair batch; the figures are the 100-pair
+    # dispatch's (each kernel's last), never a mean over the two sizes
+    def big(ds):
+        return ds[max(ds)] if ds else None
+
     for k in sorted(set(sf) | set(sw)):
         if not k.startswith("svo_"):
             continue
-        fb = mean(sf[k], "FETCH_SIZE") if k in sf else None
-        wb = mean(sw[k], "WRITE_SIZE") if k in sw else None
-        res["svo"][k] = {"dispatches": len(sf.get(k, sw.get(k, {}))),
+        f, wr = big(sf.get(k, {})), big(sw.get(k, {}))
+        fb = f.get("FETCH_SIZE") if f else None
+        wb = wr.get("WRITE_SIZE") if wr else None
+        res["svo"][k] = {"batch": "100 pairs (the last dispatch of tools/bench_svo.py)",
+                         "fetch_raw_kb": round(fb, 1) if fb is not None else None,
                          "fetch_bytes": round(2 * 1024 * fb) if fb is not None else None,
                          "write_bytes": round(1024 * wb) if wb is not None else None,
                          "traffic_bytes": round(2 * 1024 * fb + 1024 * wb) if fb is not None and wb is not None else None,
-                         "pmc_duration_us": round(mean(sf.get(k, sw.get(k)), "_dur_ns") / 1e3, 2)}
-        if k in sq:
-            ds = sq[k]
-            dur = mean(ds, "_dur_ns")
+                         "pmc_duration_us": round((f or wr)["_dur_ns"] / 1e3, 2)}
+        q = big(sq.get(k, {}))
+        if q:
+            dur = q["_dur_ns"]
             cyc = dur * CLK_GHZ
             res["svo"][k].update({
                 "sq_duration_us": round(dur / 1e3, 2),
-                "valu_insts": round(mean(ds, "SQ_INSTS_VALU")), "salu_insts": round(mean(ds, "SQ_INSTS_SALU")),
-                "lds_insts": round(mean(ds, "SQ_INSTS_LDS")),
-                "valu_insts_per_us": round(mean(ds, "SQ_INSTS_VALU") / (dur / 1e3), 1),
+                "valu_insts": round(q.get("SQ_INSTS_VALU", 0)), "salu_insts": round(q.get("SQ_INSTS_SALU", 0)),
+                "lds_insts": round(q.get("SQ_INSTS_LDS", 0)),
+                "valu_insts_per_us": round(q.get("SQ_INSTS_VALU", 0) / (dur / 1e3), 1),
                 # SQ_ACTIVE_INST_VALU counts quad-cycles: the fraction of SIMD cycles issuing VALU
-                "valu_busy": round(4 * mean(ds, "SQ_ACTIVE_INST_VALU") / (cyc * CUS * 4), 4),
-                "mean_resident_waves_per_cu": round(4 * mean(ds, "SQ_WAVE_CYCLES") / (cyc * CUS), 2)})
+                "valu_busy": round(4 * q.get("SQ_ACTIVE_INST_VALU", 0) / (cyc * CUS * 4), 4),
+                "mean_resident_waves_per_cu": round(4 * q.get("SQ_WAVE_CYCLES", 0) / (cyc * CUS), 2)})
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
