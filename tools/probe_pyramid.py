@@ -25,7 +25,7 @@ def main():
     from viso_amd import _lib
     from viso_amd.synth import Sequence
 
-    W, H, n = 1242, 375, 100
+    W, H, n = 1242, 375, int(os.environ.get("IMAGES", "100"))
     seq = Sequence(W, H, seed=0)
     frames = np.stack([seq.image(f % 16, f % 2) for f in range(n)])
     d = torch.from_numpy(frames).cuda()
