@@ -365,18 +365,43 @@ __device__ inline bool direct_point_rs(const DirectArgs& a, const LevelPair& fp,
     if (__builtin_expect(cw.on && fu - 6 >= cw.x0 && fu + 5 <= cw.x0 + kCW - 2 && fv - 6 >= cw.y0 &&
                              fv + 5 <= cw.y0 + kCW - 2,
                          1)) {
-        auto smp = [&](double sx, double sy) {
-            const int o = ((int)sy - cw.y0) * kCW + ((int)sx - cw.x0);
-            const double d0 = (double)ld_lds_u8(win, o), d1 = (double)ld_lds_u8(win, o + 1);
-            const double d2 = (double)ld_lds_u8(win, o + kCW), d3 = (double)ld_lds_u8(win, o + kCW + 1);
-            const double xx = sx - floor(sx);
-            const double yy = sy - floor(sy);
-            return double((1 - xx) * (1 - yy) * d0 + xx * (1 - yy) * d1 + (1 - xx) * yy * d2 + xx * yy * d3);
-        };
-        error = r.lval - smp(x, y);
-        // GetGradient (include/keyframe.h:57-64)
-        g0 = 0.5 * (smp(x + 1, y) - smp(x - 1, y));
-        g1 = 0.5 * (smp(x, y + 1) - smp(x, y - 1));
+        // uc - 6 .. uc + 6 (and vc's) in one binade: every lane's sample
+        // coordinate uc + px + {-1, 0, 1} is then exact, its int() is
+        // floor(uc) + px + {-1, 0, 1} (positive: the window test) and its
+        // fraction is exactly frac(uc), so all five samples of all lanes share
+        // one set of bilinear weights (the same products as the per-sample
+        // form) and read 12 distinct taps per lane
+        const bool one_binade = (__double_as_longlong(uc - 6.0) >> 52) == (__double_as_longlong(uc + 6.0) >> 52) &&
+                                (__double_as_longlong(vc - 6.0) >> 52) == (__double_as_longlong(vc + 6.0) >> 52);
+        if (__builtin_expect(one_binade, 1)) {
+            const double xx = uc - floor(uc), yy = vc - floor(vc);
+            const double w00 = (1 - xx) * (1 - yy), w10 = xx * (1 - yy), w01 = (1 - xx) * yy, w11 = xx * yy;
+            const int o = (fv + py - cw.y0) * kCW + (fu + px - cw.x0);  // tap (0, 0) of this lane
+            auto tap = [&](int dx, int dy) { return (double)ld_lds_u8(win, o + dy * kCW + dx); };
+            const double tm0 = tap(-1, 0), t00 = tap(0, 0), t10 = tap(1, 0), t20 = tap(2, 0);
+            const double tm1 = tap(-1, 1), t01 = tap(0, 1), t11 = tap(1, 1), t21 = tap(2, 1);
+            const double t0m = tap(0, -1), t1m = tap(1, -1), t02 = tap(0, 2), t12 = tap(1, 2);
+            auto bil = [&](double d0, double d1, double d2, double d3) {
+                return double(w00 * d0 + w10 * d1 + w01 * d2 + w11 * d3);
+            };
+            error = r.lval - bil(t00, t10, t01, t11);
+            // GetGradient (include/keyframe.h:57-64)
+            g0 = 0.5 * (bil(t10, t20, t11, t21) - bil(tm0, t00, tm1, t01));
+            g1 = 0.5 * (bil(t01, t11, t02, t12) - bil(t0m, t1m, t00, t10));
+        } else {
+            auto smp = [&](double sx, double sy) {
+                const int o = ((int)sy - cw.y0) * kCW + ((int)sx - cw.x0);
+                const double d0 = (double)ld_lds_u8(win, o), d1 = (double)ld_lds_u8(win, o + 1);
+                const double d2 = (double)ld_lds_u8(win, o + kCW), d3 = (double)ld_lds_u8(win, o + kCW + 1);
+                const double sxx = sx - floor(sx);
+                const double syy = sy - floor(sy);
+                return double((1 - sxx) * (1 - syy) * d0 + sxx * (1 - syy) * d1 + (1 - sxx) * syy * d2 +
+                              sxx * syy * d3);
+            };
+            error = r.lval - smp(x, y);
+            g0 = 0.5 * (smp(x + 1, y) - smp(x - 1, y));
+            g1 = 0.5 * (smp(x, y + 1) - smp(x, y - 1));
+        }
     } else {
         error = r.lval - sample_cw(C, w, h, x, y, win, cw);
         g0 = 0.5 * (sample_cw(C, w, h, x + 1, y, win, cw) - sample_cw(C, w, h, x - 1, y, win, cw));
