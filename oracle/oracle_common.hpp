@@ -64,6 +64,17 @@ inline double tree_sum(const double* v, int n) {
     return t[0];
 }
 
+// The direct pose's 64-pixel patch sums (round 3): the pairwise tree with
+// the levels in descending stride order (p + 32 first, then + 16, ... + 1),
+// the device's reduce_scatter_28_desc.
+inline double tree_sum_desc64(const double* v) {
+    double t[64];
+    for (int i = 0; i < 64; ++i) t[i] = v[i];
+    for (int s = 32; s >= 1; s >>= 1)
+        for (int i = 0; i < s; ++i) t[i] = t[i] + t[i + s];
+    return t[0];
+}
+
 // Canonical order of a sum over MAP POINTS (the direct pose's 28 sums and
 // the rig's per-camera sums): points in tiles of T = min(64, max(1,
 // ceil(n / groups))) consecutive points, each tile a pairwise tree

@@ -147,7 +147,7 @@ bool direct_point_partials(const PyrView& last, const PyrView& cur, const Pose& 
                 for (int k = 0; k < 28; ++k) running[k] = running[k] + leaf[k][p];
         }
     if (!running)
-        for (int k = 0; k < 28; ++k) out[k] = tree_sum(leaf[k], 64);
+        for (int k = 0; k < 28; ++k) out[k] = tree_sum_desc64(leaf[k]);  // device reduce_scatter_28_desc
     return true;
 }
 

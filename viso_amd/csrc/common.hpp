@@ -301,6 +301,61 @@ __device__ inline double reduce_scatter_28(const double* v, int* value_index) {
     return f;
 }
 
+// The direct pose's 28 patch-pixel sums (round 3): the same reduce-scatter
+// with the butterfly levels in DESCENDING xor order (partner lane ^ 32, ^ 16,
+// ^ 8, ^ 4, ^ 2, ^ 1), i.e. the pairwise tree that adds pixels p and p + 32
+// first (oracle_common.hpp tree_sum_desc64).  The first two levels are then
+// v_permlane32_swap / v_permlane16_swap of two values, which leave each lane
+// its own and its partner's copy of the half it keeps with no selects: ~3
+// instructions per pair instead of ~7.  On return lane l holds value index
+// 14*b5 + 7*b4 + 4*b3 + 2*b2 + b1 (b = bits of l) when 4*b3 + 2*b2 + b1 < 7
+// and b0 == 0 (lane l ^ 1 holds a copy; *value_index = -1 there and in the
+// padded class).
+__device__ inline double reduce_scatter_28_desc(const double* v, int* value_index) {
+    const int lane = threadIdx.x & 63;
+    const bool b0 = lane & 1, b1 = lane & 2, b2 = lane & 4, b3 = lane & 8, b4 = lane & 16, b5 = lane & 32;
+    double a[14];
+#pragma unroll
+    for (int k = 0; k < 14; ++k) {  // xor 32: halves keep k / 14 + k
+        double ra, rb;
+        permlane32_swap_f64(v[k], v[14 + k], ra, rb);
+        a[k] = ra + rb;
+    }
+    double c[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {  // xor 16: even / odd rows keep k / 7 + k
+        double ra, rb;
+        permlane16_swap_f64(a[k], a[7 + k], ra, rb);
+        c[k] = ra + rb;
+    }
+    double d[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // xor 8 (row_shr / row_shl by 8): 7 -> 4 (slot 7 a +0 pad)
+        const double hi = k < 3 ? c[4 + k] : 0.0;
+        const double send = dsel(b3, c[k], hi);
+        const double keep = dsel(b3, hi, c[k]);
+        const double recv = dsel(b3, dpp_f64<0x118>(send), dpp_f64<0x108>(send));
+        d[k] = keep + recv;
+    }
+    double e[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {  // xor 4 (row_shr / row_shl by 4)
+        const double send = dsel(b2, d[k], d[2 + k]);
+        const double keep = dsel(b2, d[2 + k], d[k]);
+        const double recv = dsel(b2, dpp_f64<0x114>(send), dpp_f64<0x104>(send));
+        e[k] = keep + recv;
+    }
+    // xor 2 (quad_perm [2,3,0,1])
+    const double send = dsel(b1, e[0], e[1]);
+    const double keep = dsel(b1, e[1], e[0]);
+    double f = keep + dpp_f64<0x4E>(send);
+    // xor 1 (quad_perm [1,0,3,2]): both lanes of the pair end with the sum
+    f = f + dpp_f64<0xB1>(f);
+    const int local = (b3 ? 4 : 0) + (b2 ? 2 : 0) + (b1 ? 1 : 0);
+    *value_index = (b0 || local >= 7) ? -1 : (b5 ? 14 : 0) + (b4 ? 7 : 0) + local;
+    return f;
+}
+
 // ---- fp32 forms (tolerance mode, VISO_PRECISION_FAST)
 template <int CTRL>
 __device__ inline float dpp_f32(float v) {

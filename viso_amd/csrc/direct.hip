@@ -297,8 +297,8 @@ __device__ inline double sample_cw(const uint8_t* __restrict__ img, int w, int h
     return sample_px(img, w, h, x, y);
 }
 
-// The 28 sums of one map point by reduce-scatter: returns good; lane l < 32
-// with *idx >= 0 holds sum *idx in *out.
+// The 28 sums of one map point by reduce-scatter: returns good; a lane with
+// *idx >= 0 holds sum *idx in *out (reduce_scatter_28_desc).
 // The twelve quotients of one map point's projection (project_px) and
 // dPixel/dXi (d_pixel_d_xi), each with those functions' exact operations,
 // one per lane (lane k < 12) so that a single division sequence serves all
@@ -419,7 +419,7 @@ __device__ inline bool direct_point_rs(const DirectArgs& a, const LevelPair& fp,
 #pragma unroll
     for (int k = 0; k < 6; ++k) leaf[21 + k] = -error * J[k];
     leaf[27] = error * error;
-    *out = reduce_scatter_28(leaf, idx);
+    *out = reduce_scatter_28_desc(leaf, idx);  // descending-xor pixel tree (oracle tree_sum_desc64)
     return true;
 }
 
@@ -739,7 +739,7 @@ __device__ void direct_tile_pf(const DirectArgs& a, const LevelPair& fp, int lv,
         }
         if (!ok) {
             if (lane < kSums) s_pts[local * kSums + lane] = 0.0;
-        } else if (lane < 32 && idx >= 0) {
+        } else if ((!FAST || lane < 32) && idx >= 0) {  // faithful: reduce_scatter_28_desc's map
             s_pts[local * kSums + idx] = f;
         }
         good_cnt += ok ? 1 : 0;
