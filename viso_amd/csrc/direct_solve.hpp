@@ -218,14 +218,27 @@ __device__ __attribute__((always_inline)) inline void solve_wave0(SolveLds& L, i
     }
     SPROBE(1);
     // ---- update = H^-1 * b (row-wise, ascending columns); H^-1[r][c] is
-    // lane c's x[r]
+    // lane c's x[r]: transposed through LDS (L.red is free once L.S is
+    // formed), lane r < 6 forms row r's dot product, then every lane reads
+    // the six results (the same products and sums as a per-row loop over
+    // readlanes, a quarter of the instructions)
     double update[6];
+    {
+        double* Tt = &L.red[0][0];
+        if (lane < 6) {
 #pragma unroll
-    for (int r = 0; r < 6; ++r) {
-        double s = readlane_f64(x[r], 0) * L.S[21];
+            for (int r = 0; r < 6; ++r) Tt[6 * r + lane] = x[r];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        double s = 0.0;
+        if (lane < 6) {
+            const double* row = Tt + 6 * lane;
+            s = row[0] * L.S[21];
 #pragma unroll
-        for (int c = 1; c < 6; ++c) s = s + readlane_f64(x[r], c) * L.S[21 + c];
-        update[r] = s;
+            for (int c = 1; c < 6; ++c) s = s + row[c] * L.S[21 + c];
+        }
+#pragma unroll
+        for (int r = 0; r < 6; ++r) update[r] = readlane_f64(s, r);
     }
     SPROBE(2);
     solve_finish(L, update, h, iter, stats, stamps);
