@@ -137,6 +137,12 @@ inline double acc_sum(const double* v, int n) {
     return sum_literal() ? running_sum(v, n) : tree_sum(v, n);
 }
 
+// The same for a 64-pixel patch summed by the descending-stride tree (LK
+// alignment's per-iteration sums, round 3).
+inline double acc_sum_desc64(const double* v) {
+    return sum_literal() ? running_sum(v, 64) : tree_sum_desc64(v);
+}
+
 // GetPixelValue (include/common.h:35-42, include/keyframe.h:50-57).  Base
 // pointer uses int() truncation, weights use x - floor(x).  Taps outside the
 // continuous level buffer read 0 (reference: reads outside the cv::Mat).

@@ -285,8 +285,10 @@ void lk_pair_level(const PyrView& ref, const PyrView& cur, int level, const doub
             }
         const double H00 = acc_sum(hxx, 64), H01 = acc_sum(hxy, 64), H10 = acc_sum(hyx, 64),
                      H11 = acc_sum(hyy, 64);
-        const double B0 = acc_sum(b0, 64), B1 = acc_sum(b1, 64);
-        cost = acc_sum(cc, 64);
+        // the per-iteration sums by the descending-stride tree (device
+        // wave_tree_sum3_desc); H keeps the ascending tree (device lk_prepare)
+        const double B0 = acc_sum_desc64(b0), B1 = acc_sum_desc64(b1);
+        cost = acc_sum_desc64(cc);
         const double invdet = 1.0 / (H00 * H11 - H10 * H01);
         const double i00 = H11 * invdet, i10 = -H10 * invdet, i01 = -H01 * invdet, i11 = H00 * invdet;
         const double u0 = i00 * B0 + i01 * B1;

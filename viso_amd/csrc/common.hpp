@@ -233,6 +233,33 @@ __device__ inline void wave_tree_sum3(double a, double b, double c, double& ra, 
     rc = readlane_f64(v, 2);
 }
 
+// LK alignment's three per-iteration sums (round 3): the descending-stride
+// pairwise tree (pixels p and p + 32 first; oracle tree_sum_desc64).  xor 32
+// pairs a (lanes < 32) and b (lanes >= 32) with one v_permlane32_swap and c
+// everywhere with another; xor 16 keeps a / b in even rows and c in odd rows;
+// then xor 8 / 4 by DPP row shifts + select and xor 2 / 1 by quad_perm.
+// Results read from lanes 0 (a), 32 (b), 16 (c).  Requires EXEC = all lanes.
+__device__ inline void wave_tree_sum3_desc(double a, double b, double c, double& ra, double& rb, double& rc) {
+    const int lane = threadIdx.x & 63;
+    const bool b2 = lane & 4, b3 = lane & 8;
+    double x, y;
+    permlane32_swap_f64(a, b, x, y);
+    const double ab = x + y;
+    permlane32_swap_f64(c, c, x, y);
+    const double cc = x + y;
+    permlane16_swap_f64(ab, cc, x, y);
+    double v = x + y;
+    const double r8 = dpp_f64<0x118>(v), l8 = dpp_f64<0x108>(v);  // row_shr / row_shl by 8
+    v = v + dsel(b3, r8, l8);                                        // lane ^ 8
+    const double r4 = dpp_f64<0x114>(v), l4 = dpp_f64<0x104>(v);  // row_shr / row_shl by 4
+    v = v + dsel(b2, r4, l4);                                        // lane ^ 4
+    v = v + dpp_f64<0x4E>(v);                                        // lane ^ 2
+    v = v + dpp_f64<0xB1>(v);                                        // lane ^ 1
+    ra = readlane_f64(v, 0);
+    rb = readlane_f64(v, 32);
+    rc = readlane_f64(v, 16);
+}
+
 // 28 canonical wave trees at once by reduce-scatter: at butterfly level s
 // (partner lane ^ 2^s, ascending) every lane keeps half of its remaining
 // values and adds the partner's copy of that half, so each value's partial

@@ -219,7 +219,10 @@ __device__ inline LkResult lk_iterate(const LkTemplate& t, int w1, int h1,
         }
         const double e = t.I1 - sample_win<!KLT_BOUNDS>(img2, w2, h2, cur_x + dx, cur_y + dy, win);
         double B0, B1;
-        wave_tree_sum3(-t.J0 * e, -t.J1 * e, e * e, B0, B1, cost);
+        if (KLT_BOUNDS)
+            wave_tree_sum3(-t.J0 * e, -t.J1 * e, e * e, B0, B1, cost);
+        else  // LK alignment: the descending-stride tree (oracle tree_sum_desc64)
+            wave_tree_sum3_desc(-t.J0 * e, -t.J1 * e, e * e, B0, B1, cost);
         const double u0 = i00 * B0 + i01 * B1;
         const double u1 = i10 * B0 + i11 * B1;
         if (isnan(u0)) {
