@@ -299,7 +299,7 @@ __device__ inline LkResult lk_iterate_fast(float I1, float J0, float J1, const f
         }
         const float e = I1 - bilerp_f32(t0, t1, t2, t3, xx, yy);
         float B0, B1, cost;
-        wave_tree_sum3_f32(-J0 * e, -J1 * e, e * e, B0, B1, cost);
+        wave_tree_sum3_f32_desc(-J0 * e, -J1 * e, e * e, B0, B1, cost);
         const float u0 = ih[0] * B0 + ih[1] * B1;
         const float u1 = ih[2] * B0 + ih[3] * B1;
         if (isnan(u0)) {
