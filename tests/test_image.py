@@ -106,17 +106,32 @@ def test_gpu_pyramid_bitexact(h, w):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,h,w", [(11, 375, 1242), (133, 61, 97)])
+@pytest.mark.parametrize("n,h,w", [(11, 375, 1242), (133, 61, 97), (20, 375, 1242), (32, 187, 621),
+                                   (33, 375, 1242)])
 def test_gpu_pyramid_batched(n, h, w):
     """Chunks of >= 8 images deal the bands of an image to one XCD (the
     tail launch's block -> (image, band) map, idle blocks past the last
-    image); more than kPyrBatch = 128 images split into launches."""
+    image); more than kPyrBatch = 128 images split into launches.  Chunks of
+    <= 32 images take 4-row level-1 bands, 33 the 8-row ones."""
     from viso_amd import default_context
     ctx = default_context()
     imgs = np.stack([images.mixed(h, w, seed=100 + s) for s in range(n)])
     got = ctx.pyramid(imgs)
     for i in range(n):
         assert np.array_equal(got[i], oracle_lib.pyramid(imgs[i])), i
+
+
+@pytest.mark.gpu
+def test_gpu_pyramid_chunk_sizes_repeated():
+    """Back-to-back chunks of different sizes (both level-1 band heights)
+    and images stay bit-exact."""
+    from viso_amd import default_context
+    ctx = default_context()
+    for rep, n in enumerate([20, 1, 32, 40, 7, 20]):
+        imgs = np.stack([images.mixed(375, 1242, seed=300 + 40 * rep + s) for s in range(n)])
+        got = ctx.pyramid(imgs)
+        for i in range(n):
+            assert np.array_equal(got[i], oracle_lib.pyramid(imgs[i])), (rep, i)
 
 
 @pytest.mark.gpu

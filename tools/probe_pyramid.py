@@ -35,7 +35,10 @@ def main():
     v.synchronize()
     lib = _lib.load()
     lib.viso_debug_pyr_timeline.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    units = 72 * n
+    bh = 4 if n <= 32 else 8  # image.hip kSkSmallBatch / kSkBHs / kSkBH1
+    bands = -(-(H // 2) // bh)
+    upi = 3 * bands
+    units = min(upi * n, 8192)
     buf = np.zeros((8192, 5), np.uint64)
     assert lib.viso_debug_pyr_timeline(buf.ctypes.data, 8192) == 0
     tl = buf[:units].astype(np.int64)
@@ -65,9 +68,19 @@ def main():
     for t in np.arange(0, en.max() + 0.5, 1.0):
         live = int(np.sum((st <= t) & (en > t)))
         print(f"  t={t:5.1f} us live waves {live}")
+    # per XCC (HW_REG XCC_ID low bits): a late group on some XCCs would be a
+    # clock offset between the XCDs' realtime counters, not a dispatch stall
+    for x in np.unique(xcc & 0xF):
+        m = (xcc & 0xF) == x
+        print(f"xcc {x:2d}: waves {m.sum():5d}  start min/med/max {st[m].min():6.2f} {np.median(st[m]):6.2f} "
+              f"{st[m].max():6.2f}  end max {en[m].max():6.2f}")
+    late = st > 0.5 * st.max()
+    if late.any():
+        img = np.arange(units) // upi
+        print("late waves:", int(late.sum()), "images", np.unique(img[late])[:40])
     # by strip (unit // bands): edge strips vs interior
-    unit = np.arange(units) % 72
-    strip = unit // 24
+    unit = np.arange(units) % upi
+    strip = unit // bands
     for s in range(3):
         print(f"strip {s}: median duration {np.median(dur[strip == s]):.2f} us")
 

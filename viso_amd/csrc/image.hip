@@ -214,6 +214,10 @@ constexpr int kSkW = 244;  // destination columns per wave (lanes 0..60; 61 = ri
 // all 19 source rows of a band, so each wave makes one memory round trip
 // (round 2: 13.5 against 14.8 us per 50-image launch with an 8-row ring)
 constexpr int kSkBH1 = 8, kSkRing1 = 20;
+// chunks of <= kSkSmallBatch images (under 1.5 waves per SIMD with 8-row
+// bands; the launch is latency-bound): 4-row bands, twice the waves and half
+// the chain per wave (20 images: 11.2 -> 8.3-8.8 us; 32: 12.2 -> 11.0 us)
+constexpr int kSkSmallBatch = 32, kSkBHs = 4, kSkRings = 2 * kSkBHs + 4;
 
 struct SkBand {
     const uint8_t* src;
@@ -868,17 +872,17 @@ void launch_pyr_level(const PyrGeom& g, int l, const uint8_t* const* l0, uint8_t
     a.dw = g.w[l];
     a.dh = g.h[l];
     if (l == 1 && a.sw >= 8) {
-        a.bands = (a.dh + kSkBH1 - 1) / kSkBH1;
+        const bool small = nb <= kSkSmallBatch;
+        const int bh = small ? kSkBHs : kSkBH1;
+        a.bands = (a.dh + bh - 1) / bh;
         a.units = a.bands * ((a.dw + kSkW - 1) / kSkW);
         a.bpi = (a.units + 3) / 4;
         a.n_img = nb;
-#ifndef VISO_PYR_NOXCD
         a.xcd_per = (a.bpi * nb + 7) / 8;
-        pyr_down_sk_kernel<kSkBH1, kSkRing1><<<8 * a.xcd_per, 256, 0, stream>>>(a);
-#else  // dev A/B: the image-major 2-D grid
-        a.xcd_per = 0;
-        pyr_down_sk_kernel<kSkBH1, kSkRing1><<<dim3(a.bpi, nb), 256, 0, stream>>>(a);
-#endif
+        if (small)
+            pyr_down_sk_kernel<kSkBHs, kSkRings><<<8 * a.xcd_per, 256, 0, stream>>>(a);
+        else
+            pyr_down_sk_kernel<kSkBH1, kSkRing1><<<8 * a.xcd_per, 256, 0, stream>>>(a);
         return;
     }
     const int bh = l == 1 ? 8 : (l == 2 ? 4 : 2);
