@@ -319,7 +319,10 @@ def main():
 
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    distributed = world > 1
+    # VISO_DIST_FORCE=1 (under a launcher): the process group, the max-over-
+    # ranks timing and the RCCL pose gather also at one rank, so the RCCL
+    # path runs on a one-GPU box (tests/test_multi.py)
+    distributed = world > 1 or (os.environ.get("VISO_DIST_FORCE") == "1" and "MASTER_PORT" in os.environ)
     # VISO_DIST_BACKEND=gloo: host-tensor collectives, ranks may share a GPU
     # (device = local rank mod the visible GPUs) -- the rehearsal of the N>1
     # path on a one-GPU box (tests/test_multi.py); the product path is RCCL

@@ -152,6 +152,29 @@ def test_gpu_bench_two_ranks_share_one_gpu(tmp_path):
 
 
 @pytest.mark.gpu
+def test_gpu_bench_rccl_process_group_one_rank(tmp_path):
+    """The product N>1 path's RCCL leg on the box's one GPU: torch.distributed.run
+    with one rank and VISO_DIST_FORCE=1 builds the nccl (= RCCL) process group,
+    takes the max-over-ranks time by an RCCL all-reduce and gathers the pose
+    log through RCCL (viso_amd/shard.py); the gathered log equals the rank's own."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, VISO_DIST_FORCE="1", MASTER_ADDR="127.0.0.1")
+    env.pop("VISO_DIST_BACKEND", None)
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(root, "bench.py"),
+           "--gpus", "1"] + _BENCH_SMALL
+    line = _bench_line(subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=100))
+    assert line["n_gpus"] == 1 and line["init_frames_timed"] == 0
+    g = line["pose_gather"]
+    assert g["backend"] == "rccl" and g["process_group_backend"] == "nccl"
+    assert g["world_size"] == 1 and g["frames_per_rank"] == [20] and g["own_log_exact"]
+
+
+@pytest.mark.gpu
 def test_gpu_bench_gpus_flag_launches_ranks(tmp_path):
     """`bench.py --gpus 2` with no external launcher starts its two ranks
     itself (torch.distributed.run as a child, before any GPU call) and prints
