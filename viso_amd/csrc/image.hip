@@ -213,7 +213,10 @@ constexpr int kSkW = 244;  // destination columns per wave (lanes 0..60; 61 = ri
 // 24/12/6-row bands with a 16-row ring ran 30% slower); a 20-row ring holds
 // all 19 source rows of a band, so each wave makes one memory round trip
 // (round 2: 13.5 against 14.8 us per 50-image launch with an 8-row ring)
-constexpr int kSkBH1 = 8, kSkRing1 = 20;
+#ifndef VISO_SK_BH1
+#define VISO_SK_BH1 8
+#endif
+constexpr int kSkBH1 = VISO_SK_BH1, kSkRing1 = 2 * kSkBH1 + 4;
 // chunks of <= kSkSmallBatch images (under 1.5 waves per SIMD with 8-row
 // bands; the launch is latency-bound): 4-row bands, twice the waves and half
 // the chain per wave (20 images: 11.2 -> 8.3-8.8 us; 32: 12.2 -> 11.0 us)
@@ -444,8 +447,12 @@ constexpr int kPfThreads = 512;
 constexpr int kPfRG2 = 2;                 // level-2 rows per work item
 constexpr int kPfStage1 = 8;              // 16-byte level-1 loads per thread (max)
 constexpr int kPfPad = 16;                // LDS bytes left of a staged row's column 0
-constexpr int kPfSlots = 512;             // resident workgroups the band height is sized for (2 per CU)
-constexpr size_t kPfLdsMax = 80 * 1024;   // two workgroups per CU
+#ifndef VISO_PF_SLOTS
+#define VISO_PF_SLOTS 512
+#endif
+constexpr int kPfSlots = VISO_PF_SLOTS;   // resident workgroups the band height is sized for (2 per CU)
+constexpr size_t kPfLdsMax = (size_t)160 * 1024 / (kPfSlots / 256);  // the CU's 160 KB LDS over its slots
+static_assert(kPfSlots % 256 == 0 && kPfSlots <= 1024, "pyramid tail: 1..4 workgroups per CU");
 
 typedef uint32_t pf_u32x4 __attribute__((ext_vector_type(4)));
 
