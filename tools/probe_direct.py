@@ -26,7 +26,7 @@ def main():
     from viso_amd import _lib
     from viso_amd.synth import Sequence
 
-    W, H, warm, steps, batch = 1242, 375, 20, int(os.environ.get("STEPS", "200")), 50
+    W, H, warm, steps, batch = 1242, 375, 20, int(os.environ.get("STEPS", "200")), int(os.environ.get("BATCH", "50"))
     seq = Sequence(W, H, seed=0)
     n = warm + steps
     left = np.stack([seq.image(f, 0) for f in range(n)])
@@ -71,6 +71,9 @@ def main():
     q = list(lkbuf)
     print("LK alignment: mean GN iterations per (pair, level):",
           ", ".join(f"L{l} {q[l] / max(q[4 + l], 1):.2f} ({q[4 + l]} calls)" for l in range(4)))
+    print(f"LK alignment: points {q[15]}, mean {q[14] / max(q[15], 1) * 0.01:.2f} us per point, slowest point "
+          f"{q[9] * 0.01:.1f} us, most GN iterations of a point {q[10]}, points >= 20 us: {q[11]}, "
+          f">= 10 iterations on a level: {q[8]}")
     us = 0.01  # 100 MHz ticks -> us
     meta = log[:, 15]
     lvl = (meta & 0xff) - 1

@@ -589,7 +589,11 @@ __global__ __launch_bounds__(256, FAST ? VISO_LK_MIN_WAVES_FAST : VISO_LK_MIN_WA
                 atomicAdd(&g_probe_lk[8], pr_long);
                 atomicAdd(&g_probe_lk[12], pr_win);
                 atomicAdd(&g_probe_lk[13], pr_iter);
-                atomicAdd(&g_probe_lk[14], __builtin_amdgcn_s_memrealtime() - pr_t0);
+                const unsigned long long pr_el = __builtin_amdgcn_s_memrealtime() - pr_t0;
+                atomicAdd(&g_probe_lk[14], pr_el);
+                atomicMax(&g_probe_lk[9], pr_el);  // slowest point (100 MHz ticks)
+                atomicMax(&g_probe_lk[10], pr_it[0] + pr_it[1] + pr_it[2] + pr_it[3]);
+                if (pr_el >= 2000) atomicAdd(&g_probe_lk[11], 1ull);  // points >= 20 us
                 atomicAdd(&g_probe_lk[15], 1ull);
             }
 #endif
