@@ -28,7 +28,10 @@ ARCH = os.environ.get("VISO_OFFLOAD_ARCH", "gfx950")
 
 COMMON = ["-std=c++17", "-O3", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}",
           "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-Wall", "-Wno-unused-function",
-          "-Wno-unused-variable", "-Wno-unused-result"]
+          "-Wno-unused-variable", "-Wno-unused-result",
+          # leading scalar kernel arguments arrive in SGPRs (direct_level_kernel's
+          # prologue pointers): no kernel-argument load ahead of the first loads
+          "-mllvm", "-amdgpu-kernarg-preload-count=5"]
 if VARIANT == "probe":
     COMMON.append("-DVISO_PROBE")
 # experiment builds (dev): extra -D flags for a variant library, e.g.

@@ -927,8 +927,15 @@ __device__ inline void after_solve(const DirectArgs& a, bool merged, SolveLds& L
 //   prefetches (their map point, `last` patch taps and current-image window;
 //   wave 4 also prefetches wave 0's point) stay off its path.  B2 (block
 //   barrier) hands the new pose to every wave; then the tiles.
+// The three leading arguments repeat what the prologue's first loads need
+// (the partials of the level it solves, their nGood counts, n_tiles | solve
+// << 16): scalar arguments ahead of the by-value struct are preloaded into
+// SGPRs at wave launch (-amdgpu-kernarg-preload-count, viso_amd/build.py), so
+// the partial loads issue without waiting for a kernel-argument load.
 template <bool FAST>
-__global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
+__global__ __launch_bounds__(kThreads) void direct_level_kernel(const double* __restrict__ pre_part,
+                                                                 const int* __restrict__ pre_good, int pre_hdr,
+                                                                 DirectArgs a) {
     PROBE_DECL();
     __shared__ SolveLds L;
     __shared__ double s_pose[12];
@@ -951,9 +958,7 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(DirectArgs a) {
     // 256; every prefetch wave for its prediction)
     double v[kSums];
     int gg = 0;
-    if (solve && t < 256)
-        load_partials(a.s.part + (size_t)sl * kMaxTiles * kSums, a.s.good + sl * kMaxTiles,
-                      a.n_tiles, v, gg);
+    if (((pre_hdr >> 16) & 1) && t < 256) load_partials(pre_part, pre_good, pre_hdr & 0xffff, v, gg);
     const bool pf_wave = !solve || (wave & 3) != 0;
     double st[7];
     if (t == 256 || (solve && tiles && pf_wave)) {
@@ -1594,10 +1599,16 @@ void launch_direct_levels(const FrameDev& last_pyr, const FrameDev& cur_pyr, con
     for (int level = kLevels - 1; level >= 0; --level) {
         a.level = level;
         a.probe_seq = next_probe_seq();
+        const bool merged = a.merged && level == kLevels - 1;
+        const bool solve = level + 1 < kLevels || merged;
+        const int sl = merged ? 0 : level + 1;
+        const double* pp = solve ? a.s.part + (size_t)sl * kMaxTiles * kSums : nullptr;
+        const int* pg = solve ? a.s.good + sl * kMaxTiles : nullptr;
+        const int hdr = a.n_tiles | (solve ? 1 << 16 : 0);
         if (precision == VISO_PRECISION_FAST)
-            direct_level_kernel<true><<<grid, kThreads, 0, stream>>>(a);
+            direct_level_kernel<true><<<grid, kThreads, 0, stream>>>(pp, pg, hdr, a);
         else
-            direct_level_kernel<false><<<grid, kThreads, 0, stream>>>(a);
+            direct_level_kernel<false><<<grid, kThreads, 0, stream>>>(pp, pg, hdr, a);
         a.merged = 0;
     }
 }
@@ -1613,10 +1624,12 @@ void launch_direct_final(const FrameDev& last_pyr, const FrameDev& cur_pyr, cons
     a.log_index = log ? log_index : -1;
     a.level = -1;
     a.probe_seq = next_probe_seq();
+    // F solves level 0
+    const int hdr = a.n_tiles | (1 << 16);
     if (precision == VISO_PRECISION_FAST)
-        direct_level_kernel<true><<<1, kThreads, 0, stream>>>(a);
+        direct_level_kernel<true><<<1, kThreads, 0, stream>>>(a.s.part, a.s.good, hdr, a);
     else
-        direct_level_kernel<false><<<1, kThreads, 0, stream>>>(a);
+        direct_level_kernel<false><<<1, kThreads, 0, stream>>>(a.s.part, a.s.good, hdr, a);
 }
 
 // A rig camera of n points in tiles of T points (T shared by the cameras,
