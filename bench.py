@@ -80,6 +80,12 @@ def parse():
                     help="tracking-stage precision of the headline run (viso_params.precision)")
     ap.add_argument("--no-other", action="store_true",
                     help="skip the run at the other precision (other_precision in the line)")
+    ap.add_argument("--no-init", action="store_true",
+                    help="skip the reference's monocular initialisation leg (init_frame_us)")
+    ap.add_argument("--no-config2", action="store_true",
+                    help="skip the configs[2] leg (1920x1080 reference path + 2048-hypothesis stereo VO)")
+    ap.add_argument("--dump-poses", default="",
+                    help="rank 0 writes every rank's timed pose log (the gather's result) to this .npz")
     ap.add_argument("--rig-steps", type=int, default=64,
                     help="timesteps of the 4-camera rig measurements (configs[4]: SVO rig and the reference-path photometric rig; 0 = skip)")
     return ap.parse_args()
@@ -280,6 +286,229 @@ def measure_rig_direct(args, W, H, log):
             gP = poses[name][:m]
             rel = np.linalg.norm(gP - oP, axis=1) / np.maximum(np.linalg.norm(oP, axis=1), 1e-300)
             out[name]["parity_vs_oracle"] = {"timesteps": int(m), "max_rel_frobenius": float(rel.max())}
+    return out
+
+
+def _rel_rows(a, b):
+    """Per-row relative Frobenius distance of two (n, 12) pose stacks."""
+    return np.linalg.norm(a - b, axis=1) / np.maximum(np.linalg.norm(b, axis=1), 1e-300)
+
+
+def run_reference_init(seq, W, H, d_left, n_cap, n_track, batch):
+    """The reference's monocular path from frame 0 (no stereo): the FAST frame,
+    the KLT + PoseEstimation2d2d + SelectMotion frames up to the map creation
+    (Viso::OnNewFrame, src/viso.cpp:14-111), then n_track tracking frames in
+    one batched ingest call.  Init frames are ingested one at a time, each
+    timed on the host clock around the call (an init frame ends in a device ->
+    host read of the 2D-2D result, src/viso.cpp:76-98 decides the next frame's
+    kernels); frames are resident in HBM.  Returns the context, per-frame
+    microseconds of the init frames and the tracking frames' seconds."""
+    import viso_amd
+    fb = W * H
+    v = viso_amd.Viso(*seq.K, width=W, height=H, enable_tracking=1, batch_frames=batch,
+                      max_poses=max(1024, n_track + 16))
+    v.ctx.timing_enable(True)
+    per = []
+    f = 0
+    while v.state != 1 and f < n_cap:
+        t0 = time.perf_counter()
+        v.process_device(d_left.data_ptr() + f * fb, None, 1, fb)
+        v.synchronize()
+        per.append(1e6 * (time.perf_counter() - t0))
+        f += 1
+    dt = None
+    if v.state == 1 and n_track > 0:
+        t0 = time.perf_counter()
+        v.process_device(d_left.data_ptr() + f * fb, None, n_track, fb)
+        v.synchronize()
+        dt = time.perf_counter() - t0
+    return v, per, f, dt
+
+
+def init_kernels(v):
+    """HIP-event kernel groups of the init frames (avg / max-free sums)."""
+    out = {}
+    for k in ("fast", "klt", "ransac", "select"):
+        n_l, ms = v.ctx.timing(k)
+        if n_l:
+            out[k] = {"launches": n_l, "avg_us": round(1e3 * ms / n_l, 2)}
+    return out
+
+
+def measure_init_frames(args, seq, W, H, d_left, left, log):
+    """init_frame_us: the reference's own monocular
+    initialisation (src/viso.cpp:14-111: FAST, then per frame KLT, failed-track
+    erase, PoseEstimation2d2d with the E-1000 / H-2000 RANSAC, SelectMotion,
+    map creation) on the headline's sequence, GPU vs oracle frame by frame."""
+    cap = 12
+    run_reference_init(seq, W, H, d_left, cap, 0, 8)  # warm-up (first launches)
+    v, per, n_init, _ = run_reference_init(seq, W, H, d_left, cap, 0, 8)
+    out = {"workload": f"configs[1] sequence {W}x{H}, monocular reference initialisation from frame 0 "
+                       "(no stereo): frame 0 FAST, frames 1.. KLT + 2D-2D (E-1000 / H-2000 RANSAC) + "
+                       "SelectMotion until the map is created; one frame per call, host clock around "
+                       "each call (frames resident in HBM)",
+           "frames": n_init, "state": v.state,
+           "per_frame_us": [round(x, 1) for x in per],
+           "detect_frame_us": round(per[0], 1) if per else None,
+           "init_frame_us": round(float(np.mean(per[1:])), 1) if len(per) > 1 else None,
+           "init_frame_us_max": round(float(np.max(per[1:])), 1) if len(per) > 1 else None,
+           "kernels": init_kernels(v)}
+    if not args.no_cpu:
+        from tests import oracle_lib
+        ov = oracle_lib.Viso(seq.K, W, H, enable_tracking=1)
+        g = viso_amd_fresh(seq, W, H)
+        eq_frames = masks = 0
+        t_cpu = 0.0
+        for f in range(n_init):
+            g.OnNewFrame(left[f])
+            t0 = time.perf_counter()
+            ov.on_new_frame(left[f])
+            t_cpu += time.perf_counter() - t0
+            gs, os_ = g.stats(), ov.stats()
+            same = g.state == ov.state and all(gs[k] == os_[k] for k in (1, 2, 3, 4, 12))
+            if f > 0:
+                gk1, gk2, gsu = g.tracks()
+                ok1, ok2, osu = ov.tracks()
+                same = same and np.array_equal(gk1.view(np.uint32), ok1.view(np.uint32)) and \
+                    np.array_equal(gk2.view(np.uint32), ok2.view(np.uint32)) and np.array_equal(gsu, osu)
+                masks += int(gs[2] > 0 and np.array_equal(gsu, osu))
+            eq_frames += int(same)
+        gp, op = g.GetPoints(), ov.points()
+        out["parity_vs_oracle"] = {
+            "frames": n_init, "frames_identical": eq_frames,
+            "ransac_inlier_masks_equal": masks,
+            "map_points": int(len(op)),
+            "map_max_rel": float(np.linalg.norm(gp - op) / max(np.linalg.norm(op), 1e-300))
+            if gp.shape == op.shape and len(op) else None}
+        out["cpu_baseline"] = {"value_us_per_frame": round(1e6 * t_cpu / max(n_init, 1), 1), "cores": 1,
+                               "kind": "port", "sample": f"oracle/ C++ restatement, frames 0-{n_init - 1}"}
+    log(f"[init] {out['init_frame_us']} us per KLT + 2D-2D frame, {n_init} frames")
+    return out
+
+
+def viso_amd_fresh(seq, W, H):
+    import viso_amd
+    return viso_amd.Viso(*seq.K, width=W, height=H, enable_tracking=1)
+
+
+def measure_config2(args, log):
+    """BASELINE.json configs[2]: synthetic 1920x1080,
+    ~8k FAST corners per frame.  (1) The reference path: the monocular
+    initialisation with the E-1000 / H-2000 RANSAC (src/viso.cpp:14-111), then
+    tracking frames (direct pose + LK alignment) in one batched call;
+    init_frame_us and tracking frames/s, GPU vs oracle frame by frame on the
+    init frames and the first tracking frames.  (2) The 2D-2D stage (KLT,
+    PoseEstimation2d2d + SelectMotion, src/viso.cpp:16-52,178-256,520-638) on
+    three frame pairs: inlier masks GPU vs oracle.  (3) The north-star stereo
+    VO with 2048 RANSAC hypotheses: pairs/s and GPU vs spec."""
+    import torch
+
+    from viso_amd import default_context, svo
+    from viso_amd.synth import Sequence
+    W, H = 1920, 1080
+    n_track = 16
+    seq = Sequence(W, H, seed=0, block_m=0.35)  # ~8.2k FAST@50 corners on frame 0
+    t0 = time.time()
+    n_frames = 6 + n_track
+    left = np.stack([seq.image(f, 0) for f in range(n_frames)])
+    n_svo = 8
+    right = np.stack([seq.image(f, 1) for f in range(n_svo)])
+    log(f"[config2] rendered {n_frames + n_svo} 1080p images in {time.time() - t0:.1f}s")
+    d_left = torch.from_numpy(left).cuda()
+    d_right = torch.from_numpy(right).cuda()
+    torch.cuda.synchronize()
+    fb = W * H
+    # (1) reference path: init + tracking
+    run_reference_init(seq, W, H, d_left, 6, 2, n_track)  # warm-up
+    v, per, n_init, dt = run_reference_init(seq, W, H, d_left, 6, n_track, n_track)
+    out = {"workload": "configs[2]: synthetic 1920x1080 grey sequence, ~8k FAST@50 corners per frame, "
+                       "reference path (monocular init with E-1000 / H-2000 RANSAC, then direct pose + LK "
+                       "alignment), frames resident in HBM",
+           "fast_corners_frame0": None, "init_frames": n_init, "state": v.state,
+           "init_per_frame_us": [round(x, 1) for x in per],
+           "detect_frame_us": round(per[0], 1) if per else None,
+           "init_frame_us": round(float(np.mean(per[1:])), 1) if len(per) > 1 else None,
+           "tracking_frames": n_track if dt else 0,
+           "tracking_frames_per_s": round(n_track / dt, 1) if dt else None,
+           "map_points": int(len(v.GetPoints())),
+           "init_kernels": init_kernels(v)}
+    log(f"[config2] init {out['init_frame_us']} us/frame, tracking {out['tracking_frames_per_s']} frames/s")
+    gP = v.poses
+    # (3) stereo VO, 2048 hypotheses
+    p = svo.default_params(W, H, *seq.K, seq.p.baseline, ransac_iters=2048)
+    vo = svo.VisualOdometryStereo(p)
+    vo.process_device(d_left.data_ptr(), d_right.data_ptr(), 2, fb)  # warm-up
+    vo.synchronize()
+    vo = svo.VisualOdometryStereo(p)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    vo.process_device(d_left.data_ptr(), d_right.data_ptr(), n_svo, fb)
+    vo.synchronize()
+    dts = time.perf_counter() - t0
+    out["stereo_vo_2048"] = {"pairs": n_svo, "ransac_hypotheses": 2048, "pairs_per_s": round(n_svo / dts, 1),
+                             "features_last_pair": vo.stats().tolist()[:2]}
+    log(f"[config2] stereo VO 2048 hyps: {out['stereo_vo_2048']['pairs_per_s']} pairs/s")
+    if args.no_cpu:
+        return out
+    from tests import oracle_lib
+    # (1) parity: frame by frame over the init frames and 2 tracking frames
+    g = viso_amd_fresh(seq, W, H)
+    ov = oracle_lib.Viso(seq.K, W, H, enable_tracking=1)
+    eq_frames = 0
+    n_chk = n_init + 2
+    for f in range(n_chk):
+        g.OnNewFrame(left[f])
+        ov.on_new_frame(left[f])
+        gs, os_ = g.stats(), ov.stats()
+        if f == 0:
+            out["fast_corners_frame0"] = int(os_[1])
+        same = g.state == ov.state and all(gs[k] == os_[k] for k in (1, 2, 3, 4, 9, 12))
+        if ov.state == 0 and f > 0:
+            gk1, gk2, gsu = g.tracks()
+            ok1, ok2, osu = ov.tracks()
+            same = same and np.array_equal(gk2.view(np.uint32), ok2.view(np.uint32)) and np.array_equal(gsu, osu)
+        eq_frames += int(same)
+    oP = ov.poses()
+    m = min(len(oP), len(gP))
+    out["parity_vs_oracle"] = {"frames": n_chk, "frames_identical": eq_frames,
+                               "tracking_poses": int(m),
+                               "pose_max_rel_frobenius": float(_rel_rows(gP[:m], oP[:m]).max()) if m else None,
+                               "bar": 1e-4}
+    # (2) the 2D-2D stage on three pairs (frame 0 -> 4, 5, 6): KLT tracks, then
+    # E / H RANSAC + SelectMotion; inlier masks GPU vs oracle
+    ctx = default_context(K=seq.K, width=W, height=H)
+    K = seq.K
+    Kinv = np.linalg.inv(np.array([[K[0], 0, K[2]], [0, K[1], K[3]], [0, 0, 1]]))
+    kx, ky, _ = oracle_lib.fast(left[0], 50)
+    kp1 = np.c_[kx, ky].astype(np.float32)
+    pyr0 = oracle_lib.pyramid(left[0])
+    pairs = []
+    for f in (4, 5, 6):
+        pyr = oracle_lib.pyramid(left[f])
+        k2o, so = oracle_lib.klt(pyr0, pyr, W, H, kp1, kp1.copy())
+        k2g, sg = ctx.klt(ctx.pyramid(left[0])[0], ctx.pyramid(left[f])[0], W, H, kp1, kp1.copy())
+        tracks_eq = bool(np.array_equal(k2o.view(np.uint32), k2g.view(np.uint32)) and np.array_equal(so, sg))
+        ok = so.astype(bool)
+        p1 = np.c_[kp1[ok].astype(np.float64), np.ones(ok.sum())] @ Kinv.T
+        p2 = np.c_[k2o[ok].astype(np.float64), np.ones(ok.sum())] @ Kinv.T
+        t0 = time.perf_counter()
+        got = ctx.pose_2d2d(p1, p2)
+        gpu_us = 1e6 * (time.perf_counter() - t0)
+        exp = oracle_lib.pose_2d2d(p1, p2, K, W, H)
+        pairs.append({"frames": [0, f], "tracks": int(ok.sum()), "klt_tracks_equal": tracks_eq,
+                      "e_inliers": int(exp["stats"][4]), "h_inliers": int(exp["stats"][5]),
+                      "selected_inliers": int(exp["stats"][0]),
+                      "inlier_mask_equal": bool(np.array_equal(got["inliers"], exp["inliers"])),
+                      "stats_equal": bool(all(got["stats"][k] == exp["stats"][k] for k in (0, 1, 2, 4, 5, 6, 7))),
+                      "R_max_abs_diff": float(np.abs(got["R"] - exp["R"]).max()),
+                      "stage_call_us": round(gpu_us, 1)})
+    out["pose_2d2d_pairs"] = pairs
+    # (3) parity of the stereo VO on the first 2 pairs
+    S = oracle_lib.SvoSequence(oracle_lib.svo_params(W, H, *seq.K, seq.p.baseline, ransac_iters=2048))
+    for f in range(2):
+        S.process(left[f], right[f])
+    out["stereo_vo_2048"]["parity_vs_oracle"] = {
+        "pairs": 2, "pose_max_abs_diff": float(np.abs(vo.poses[:2] - np.array(S.poses[:2])).max())}
     return out
 
 
@@ -512,6 +741,17 @@ def main():
     rig_direct = None
     if rank == 0 and args.rig_steps > 0 and (W, H) == (1242, 375):
         rig_direct = measure_rig_direct(args, W, H, log)
+    # the reference's own monocular initialisation on the same sequence, and
+    # configs[2] (after the timed region; their oracle checks after their clocks)
+    init_leg = None
+    if rank == 0 and not args.no_init:
+        init_leg = measure_init_frames(args, seq, W, H, d_left, left, log)
+    config2 = None
+    if rank == 0 and not args.no_config2 and not args.kitti:
+        config2 = measure_config2(args, log)
+    if rank == 0 and args.dump_poses:
+        logs = gathered if distributed else [poses[n_pose_before:]]
+        np.savez(args.dump_poses, warm=warm, world=world, **{f"rank{r}": p for r, p in enumerate(logs)})
 
     # ---------------------------------------------------------- CPU baseline + parity
     cpu = None
@@ -563,6 +803,10 @@ def main():
             "dtype": "f64" if args.precision == "faithful" else "f32 per-pixel, f64 sums and solve",
             "precision": args.precision,
             "data": "synthetic" if source == "synthetic" else f"KITTI-format PNG pairs ({source})",
+            "units_note": ("a frame = one stereo pair through the reference path (Viso::OnNewFrame on the "
+                           "left image); frames are resident in HBM before the clock (no PCIe in value); the "
+                           "right image is consumed only by the stereo initialisation (warm-up), as the "
+                           "reference never reads one; every timed frame is a tracking frame"),
             "config": {"workload": (f"configs[1]: one {W}x{H} grey stereo sequence per GPU, "
                                     "KITTI seq-00 intrinsics" if (W, H) == (1242, 375) else
                                     f"one {W}x{H} grey stereo sequence per GPU (configs[2] size "
@@ -587,6 +831,9 @@ def main():
             "other_precision": other,
             "stereo_vo": stereo_vo,
             "rig_direct": rig_direct,
+            "init_frame_us": init_leg["init_frame_us"] if init_leg else None,
+            "init_path": init_leg,
+            "config2": config2,
             "pose_gather": gather,
             "last_frame_stats": {"direct_nGood": st[9], "lk_pairs": st[6], "lk_success": st[7]},
         }

@@ -123,55 +123,13 @@ def _bench_line(r):
     return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
 
 
-_BENCH_SMALL = ["--steps", "20", "--warmup", "5", "--no-cpu", "--no-svo", "--no-other", "--rig-steps", "0"]
+_BENCH_SMALL = ["--steps", "20", "--warmup", "5", "--no-cpu", "--no-svo", "--no-other", "--rig-steps", "0",
+                "--no-init", "--no-config2"]
 
 
-@pytest.mark.gpu
-def test_gpu_bench_two_ranks_share_one_gpu(tmp_path):
-    """bench.py's N>1 path on hardware, launched the way the driver does it
-    (an external torch.distributed.run): two ranks (gloo collectives, both on
-    the box's one GPU) each track their own sequence; rank 0 prints the line
-    with value = 2 x steps / max-over-ranks time and the gathered pose logs of
-    both ranks."""
-    import subprocess
-    import sys
-
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, VISO_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
-    env.pop("WORLD_SIZE", None)
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(root, "bench.py"),
-           "--gpus", "2"] + _BENCH_SMALL
-    line = _bench_line(subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=100))
-    assert line["n_gpus"] == 2 and line["steps"] == 20
-    assert line["init_frames_timed"] == 0
-    assert abs(line["value"] - 2 * 20 / (line["ms_per_step"] * 20 * 1e-3)) / line["value"] < 1e-3
-    g = line["pose_gather"]
-    assert g["frames_per_rank"] == [20, 20] and g["own_log_exact"]
-    assert g["world_size"] == 2 and g["process_group_backend"] == "gloo"
-
-
-@pytest.mark.gpu
-def test_gpu_bench_rccl_process_group_one_rank(tmp_path):
-    """The product N>1 path's RCCL leg on the box's one GPU: torch.distributed.run
-    with one rank and VISO_DIST_FORCE=1 builds the nccl (= RCCL) process group,
-    takes the max-over-ranks time by an RCCL all-reduce and gathers the pose
-    log through RCCL (viso_amd/shard.py); the gathered log equals the rank's own."""
-    import subprocess
-    import sys
-
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, VISO_DIST_FORCE="1", MASTER_ADDR="127.0.0.1")
-    env.pop("VISO_DIST_BACKEND", None)
-    env.pop("WORLD_SIZE", None)
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(root, "bench.py"),
-           "--gpus", "1"] + _BENCH_SMALL
-    line = _bench_line(subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=100))
-    assert line["n_gpus"] == 1 and line["init_frames_timed"] == 0
-    g = line["pose_gather"]
-    assert g["backend"] == "rccl" and g["process_group_backend"] == "nccl"
-    assert g["world_size"] == 1 and g["frames_per_rank"] == [20] and g["own_log_exact"]
+# The driver-shaped N>1 runs (two gloo ranks on the box's GPU, the RCCL group
+# at one rank), each checked against the oracle, are configs[3] in
+# tests/test_00_configs.py.
 
 
 @pytest.mark.gpu
