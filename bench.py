@@ -907,10 +907,11 @@ def pmc_evidence(W, H, breakdown, stereo_vo, n_map=None):
               "valu_busy": d["valu_busy"], "vgpr": d.get("vgpr_code_object", d["vgpr"]),
               "vgpr_source": "code object (compiler resource usage)" if "vgpr_code_object" in d else "PMC",
               "lds_bytes": d["lds_bytes"],
-              "fp64_flop_per_launch": flop,
-              "fp64_flop_per_launch_basis": f"algorithmic: {n_pts} map points x 64 px x 154 flop",
-              "fp64_flop_per_launch_executed": executed,
-              "fp64_tflops": round(flop / (live_us * 1e-6) / 1e12, 2) if flop else None,
+              # r02 basis kept: the PMC-executed count (replicated solves included)
+              "fp64_flop_per_launch": executed,
+              "fp64_flop_per_launch_algorithmic": flop,
+              "fp64_flop_per_launch_algorithmic_basis": f"{n_pts} map points x 64 px x 154 flop",
+              "fp64_tflops_algorithmic": round(flop / (live_us * 1e-6) / 1e12, 2) if flop else None,
               "fp64_peak_tflops": d.get("fp64_peak_tflops"),
               "source": "profiles/r03_gn_svo_pmc.json (SQ_WAVES, SQ_WAVE_CYCLES, SQ_ACTIVE_INST_VALU, "
                         "SQ_INSTS_VALU_*_F64)"}

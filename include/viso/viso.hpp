@@ -26,6 +26,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <mutex>
 #include <vector>
 
 #include "viso_c.h"
@@ -57,14 +58,19 @@ struct GreyView {
 };
 
 namespace detail {
-// A library context per (device 0) image size that builds Keyframe pyramids
-// with the same pyrDown kernels as the frame path (viso_pyramid).
+// A library context per image size that builds Keyframe pyramids with the
+// same pyrDown kernels as the frame path (viso_pyramid).  Keyframe has no
+// device argument (the reference's Keyframe(cv::Mat) has none), so these
+// contexts live on device 0; they are created once per size, shared by every
+// thread (the cache is guarded by a mutex) and released only at process exit.
 inline viso_ctx* pyramid_ctx(int w, int h) {
     struct Entry {
         int w, h;
         viso_ctx* ctx;
     };
+    static std::mutex mu;
     static std::vector<Entry> cache;
+    std::lock_guard<std::mutex> lock(mu);
     for (const Entry& e : cache)
         if (e.w == w && e.h == h) return e.ctx;
     viso_params p;
@@ -268,7 +274,8 @@ public:
         bool empty() const { return size() == 0; }
         const Pose& operator[](size_t i) const { return current()[i]; }
         std::vector<Pose>::const_iterator begin() const { return current().begin(); }
-        std::vector<Pose>::const_iterator end() const { return cache_.end(); }
+        // both iterators come from the same snapshot whichever is evaluated first
+        std::vector<Pose>::const_iterator end() const { return current().end(); }
 
        private:
         const std::vector<Pose>& current() const {

@@ -76,14 +76,20 @@ def test_oracle_keyframes_off_is_the_frozen_map():
     assert np.array_equal(a.poses(), b.poses()) and (sa[:, 14] == 0).all()
 
 
+@pytest.fixture(scope="module")
+def oracle_kf():
+    """The oracle's 120 frames with insertion, shared by both GPU variants."""
+    return _oracle(_seq(), N)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("batched", [False, True])
-def test_gpu_keyframe_insertion_matches_oracle(batched):
+def test_gpu_keyframe_insertion_matches_oracle(batched, oracle_kf):
     import torch
 
     import viso_amd
     seq = _seq()
-    ov, ost = _oracle(seq, N)
+    ov, ost = oracle_kf
     gv = viso_amd.Viso(*seq.K, width=W, height=H, enable_tracking=1, batch_frames=32)
     gv.set_stereo(seq.p.baseline, 128, 1)
     gv.set_keyframes(INTERVAL, PERMILLE)

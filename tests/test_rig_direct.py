@@ -195,10 +195,13 @@ def test_dense_rig_oracle_has_cameras_past_4096_points(dense_rig_run):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("precision", ["faithful", "fast"])
-def test_gpu_rig_past_4096_points_per_camera(dense_rig_run, precision):
+@pytest.mark.parametrize("precision,device_ingest", [("faithful", False), ("faithful", True), ("fast", False)])
+def test_gpu_rig_past_4096_points_per_camera(dense_rig_run, precision, device_ingest):
     """Cameras past 4096 points (tiles must stay <= 64 points):
-    faithful bit-exact map / nGood and poses <= 1e-10; tolerance mode <= 1e-4."""
+    faithful bit-exact map / nGood and poses <= 1e-10; tolerance mode <= 1e-4.
+    With device ingest the timesteps run in one call, so every
+    timestep's final solve is merged into the next one's L(3) with cameras of
+    more than one reduce wave."""
     import torch
 
     import viso_amd
@@ -207,8 +210,16 @@ def test_gpu_rig_past_4096_points_per_camera(dense_rig_run, precision):
     prec = viso_amd.PRECISION_FAITHFUL if precision == "faithful" else viso_amd.PRECISION_FAST
     g = VisoRig(*seq.K, W, H, seq.extrinsics(), precision=prec, fast_thresh=20)
     g.set_stereo(seq.p.baseline, 128, 1)
-    for ls, rs in frames:
-        g.process(ls, rs)
+    if device_ingest:
+        dl = torch.from_numpy(np.stack([im for ls, _ in frames for im in ls])).cuda()
+        dr = torch.from_numpy(np.stack([im for _, rs in frames for im in rs])).cuda()
+        torch.cuda.synchronize()
+        g.process_device(dl.data_ptr(), dr.data_ptr(), len(frames), W * H)
+        g.synchronize()
+        del dl, dr
+    else:
+        for ls, rs in frames:
+            g.process(ls, rs)
     torch.cuda.synchronize()
     assert g.state == r.state == 1
     for c in range(2):

@@ -20,18 +20,19 @@
 //   tiles — one wave per map point, lane = patch pixel: J = -grad^T *
 //     dPixel/dXi, the 28 sums (21 upper-triangle J J^T, 6 -e J, e^2) by
 //     reduce-scatter (the canonical wave tree, common.hpp).  A workgroup owns
-//     an aligned tile of T = max(8, P/256) points (P = next pow2 of the point
-//     count), so there are at most 256 tiles; the tile's 28 sums are a tree
-//     over its points, stored k-major per level ([28][256]).
+//     a tile of T = map_tile(n, 256) = min(64, ceil(n / 256)) consecutive
+//     points (247 tiles of 10 at 2,465 points), so there are at most 256
+//     tiles; the tile's 28 sums are a tree over its points, stored k-major
+//     per level ([28][256]).
 // F (one workgroup): solves level 0 and writes the pose (+ pose log).
 //
-// The solve (one level, one workgroup): tile t's partials in thread t, a
-// canonical tree over the tiles (reduce-scatter per wave, then the 4 waves);
-// then on wave 0 alone: Eigen PartialPivLU of H with one lane per matrix
-// element, the inverse by column-parallel forward / backward substitution
-// (one lane per element), update = H^-1 b, SE3::exp(update) * T21 (sin/cos
-// of theta/2 and theta in two lanes at once), cost / nGood and the checks of
-// :741-753.  Every element sees the same operations in the same order as the
+// The solve (one level, replicated in every workgroup): tile t's partials in
+// thread t, a canonical tree over the tiles (reduce-scatter per wave, then
+// the 4 waves); then on wave 0 alone: Eigen PartialPivLU of H replicated in
+// every lane's registers (direct_solve.hpp; the pivot row made wave-uniform),
+// the inverse with lane c solving column c, update = H^-1 b,
+// SE3::exp(update) * T21 (sin/cos of theta/2 and theta in two lanes at once),
+// cost / nGood and the checks of :741-753.  Every element sees the same operations in the same order as the
 // sequential oracle, so the result is bit-identical.
 // As shipped the loop takes exactly one GN step per level (cost is never
 // reset, src/viso.cpp:673); the rare continuation (a level
@@ -1376,8 +1377,10 @@ __global__ __launch_bounds__(kRigThreads) void rig_level_kernel(RigArgs ra) {
             if (lane == 0) atomicAdd(&s_arrive, 1);
         }
     }
-    // ---- the T this level starts from (thread 192: wave 3 reduces only for
-    // a camera of more than 192 tiles)
+    // ---- the T this level starts from (thread 192: wave 3 is camera 3's
+    // leader reduce wave, so for a 4-camera rig this write waits behind that
+    // camera's reduction; wave 0 needs both before it solves, so only the
+    // order, not the result, depends on it)
     if (t == 192) {
         double st[7];
         if (!solve) {
