@@ -180,16 +180,13 @@ int viso_fast(viso_ctx* c, const uint8_t* image, int32_t width, int32_t height, 
     if (!c || !image || width < 8 || height < 8 || width > kMaxWidth) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(c->device));
     const size_t npx = (size_t)width * height;
-    const size_t row_cap = fast_row_cap(width);
     const size_t kcap = std::max<size_t>(cap, 1);
     int rc = c->scratch_a.ensure(npx);
-    if (!rc) rc = c->scratch_b.ensure(sizeof(int) * (height + 1) + sizeof(int4) * row_cap * height);
+    if (!rc) rc = c->scratch_b.ensure(fast_scratch_bytes(width, height));
     if (!rc) rc = c->scratch_c.ensure(sizeof(int4) * kcap + sizeof(int));
     if (rc) return rc;
     uint8_t* d_img = (uint8_t*)c->scratch_a.ptr;
-    FastScratch s;
-    s.row_count = (int*)c->scratch_b.ptr;
-    s.row_list = (int4*)((char*)c->scratch_b.ptr + ((sizeof(int) * (height + 1) + 15) & ~(size_t)15));
+    FastScratch s = fast_scratch_at(c->scratch_b.ptr, width, height);
     int4* d_raw = (int4*)c->scratch_c.ptr;
     int* d_n = (int*)((char*)c->scratch_c.ptr + sizeof(int4) * kcap);
     VISO_HIP_CHECK(hipMemcpyAsync(d_img, image, npx, hipMemcpyHostToDevice, c->stream));

@@ -68,12 +68,9 @@ int viso_ctx::init() {
     if (!rc) rc = kp2b.ensure(kbytes);
     if (!rc) rc = track_success.ensure((size_t)cap);
     if (!rc) rc = n_track_dev.ensure(256);
-    const size_t row_cap = fast_row_cap(g.w[0]);
-    const size_t rows_off = ((sizeof(int) * (g.h[0] + 1)) + 255) & ~(size_t)255;
-    if (!rc) rc = fast_rows.ensure(rows_off + sizeof(int4) * row_cap * g.h[0]);
+    if (!rc) rc = fast_rows.ensure(fast_scratch_bytes(g.w[0], g.h[0]));
     if (rc) return rc;
-    fast.row_count = (int*)fast_rows.ptr;
-    fast.row_list = (int4*)((char*)fast_rows.ptr + rows_off);
+    fast = fast_scratch_at(fast_rows.ptr, g.w[0], g.h[0]);
     // geometry
     {
         Bump b;

@@ -14,6 +14,7 @@
 //  * select-motion: one lane per (candidate, point) triangulation + tests,
 //    one workgroup for the strict-max choice and the mean-depth tree.
 #include <cfloat>
+#include <climits>
 
 #include "device_math.hpp"
 #include "geometry.hpp"
@@ -49,6 +50,45 @@ __device__ inline void draw_subset(uint64_t seed, int h, int t, int n, int* idx)
         }
         idx[k] = chosen;
     }
+}
+
+// draw_subset<M> on one wave (every lane gets the same idx): the 64 attempts
+// of a sample are hashed by the 64 lanes at once and the first attempt that
+// is not a duplicate wins, as in the sequential loop; if all 64 are
+// duplicates, the first free index in 0..n-1, as there.
+template <int M>
+__device__ inline void draw_subset_wave(uint64_t seed, int h, int t, int n, int* idx) {
+    const int lane = threadIdx.x & 63;
+    for (int k = 0; k < M; ++k) {
+        const int cand = (int)(sample_hash(seed, h, t, k, lane) % (uint64_t)n);
+        bool dup = false;
+        for (int j = 0; j < k; ++j) dup |= (idx[j] == cand);
+        unsigned long long ok = __ballot(!dup);
+        int chosen = -1;
+        if (ok) {
+            chosen = __builtin_amdgcn_readlane(cand, __ffsll((long long)ok) - 1);
+        } else {
+            for (int c0 = 0; c0 < n && chosen < 0; c0 += 64) {
+                const int c = c0 + lane;
+                bool d2 = c >= n;
+                for (int j = 0; j < k; ++j) d2 |= (idx[j] == c);
+                ok = __ballot(!d2);
+                if (ok) chosen = __builtin_amdgcn_readlane(c, __ffsll((long long)ok) - 1);
+            }
+        }
+        idx[k] = chosen;
+    }
+}
+
+// the uniform array entry v[i] at a per-lane index i < M (a select chain:
+// no scratch)
+template <int M>
+__device__ inline int pick_uniform(const int* v, int i) {
+    int r = v[0];
+#pragma unroll
+    for (int k = 1; k < M; ++k)
+        if (i == k) r = v[k];
+    return r;
 }
 
 // ---------------------------------------------------------------- normalise
@@ -148,19 +188,59 @@ __device__ inline float sampson_err(const double* E, double x1, double y1, doubl
     return (float)(x2tEx1 * x2tEx1 / (aa + b + c + d));
 }
 
-__global__ __launch_bounds__(64) void e_hyp_kernel(GeoArgs a) {
-    const int h = blockIdx.x * 64 + threadIdx.x;
+// One wave per hypothesis (4 per workgroup, so the 1000 hypotheses spread
+// over 250 workgroups): the 8-point subset drawn lane-parallel, lane l
+// builds elements l and 64 + l of the 8x9 system, the null vector by the
+// wave's complete-pivot elimination (null_vector_8x9_wave: each element sees
+// the sequential routine's operations), then svd3 and the (1, 1, 0)
+// projection on every lane (uniform), exactly as essential_from_8.
+__global__ __launch_bounds__(256) void e_hyp_kernel(GeoArgs a) {
+    __shared__ double s_m[4][72];
+    const int wave = wave_id(), lane = threadIdx.x & 63;
+    const int h = blockIdx.x * 4 + wave;
     if (h >= a.e_iters) return;
     const GeoCtl* c = a.ctl;
     if (!c->gate) return;
     const int n = c->n;
-    double* E = a.e_models + 9 * (size_t)h;
     int idx[8];
-    if (n == 8)
+    if (n == 8) {
         for (int k = 0; k < 8; ++k) idx[k] = k;
-    else
-        draw_subset<8>(a.seed, h, 0, n, idx);
-    a.e_valid[h] = essential_from_8(a.q1, a.q2, idx, E) ? 1 : 0;
+    } else {
+        draw_subset_wave<8>(a.seed, h, 0, n, idx);
+    }
+    auto elem = [&](int i) -> double {
+        const int r = i / 9, col = i - 9 * (i / 9);
+        const int p = pick_uniform<8>(idx, r);
+        const double x1 = a.q1[2 * p], y1 = a.q1[2 * p + 1];
+        const double x2 = a.q2[2 * p], y2 = a.q2[2 * p + 1];
+        switch (col) {
+            case 0: return x2 * x1;
+            case 1: return x2 * y1;
+            case 2: return x2;
+            case 3: return y2 * x1;
+            case 4: return y2 * y1;
+            case 5: return y2;
+            case 6: return x1;
+            case 7: return y1;
+            default: return 1.0;
+        }
+    };
+    double A[2] = {elem(lane), lane < 8 ? elem(64 + lane) : 0.0};
+    double e[9];
+    bool ok = null_vector_8x9_wave(A, s_m[wave], e);
+    double E[9];
+    if (ok) {
+        double U[9], sv[3], V[9];
+        svd3(e, U, sv, V);
+        ok = sv[1] > 0;
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) E[3 * i + j] = U[3 * i + 0] * V[3 * j + 0] + U[3 * i + 1] * V[3 * j + 1];
+    }
+    if (lane == 0) {
+        if (ok)
+            for (int k = 0; k < 9; ++k) a.e_models[9 * (size_t)h + k] = E[k];
+        a.e_valid[h] = ok ? 1 : 0;
+    }
 }
 
 // ---------------------------------------------------------------- H RANSAC
@@ -223,31 +303,64 @@ __device__ inline float transfer_err(const double* H, double x1, double y1, doub
     return (float)(dx * dx + dy * dy);
 }
 
-__global__ __launch_bounds__(64) void h_hyp_kernel(GeoArgs a) {
-    const int h = blockIdx.x * 64 + threadIdx.x;
+// One wave per hypothesis: the up to 100 sampling tries of the sequential
+// loop run 64 at a time, one per lane (a try's subset depends only on its
+// index), the first try whose subset passes checkSubset wins; then the 8x9
+// DLT system (two rows per point, h_rows) and the wave's null vector.
+__global__ __launch_bounds__(256) void h_hyp_kernel(GeoArgs a) {
+    __shared__ double s_m[4][72];
+    const int wave = wave_id(), lane = threadIdx.x & 63;
+    const int h = blockIdx.x * 4 + wave;
     if (h >= a.h_iters) return;
     const GeoCtl* c = a.ctl;
     if (!c->gate) return;
     const int n = c->n;
-    int idx[4];
+    int idx[4] = {0, 1, 2, 3};
     bool ok = false;
-    for (int t = 0; t < 100 && !ok; ++t) {
-        if (n == 4)
-            for (int k = 0; k < 4; ++k) idx[k] = k;
-        else
-            draw_subset<4>(a.seed ^ 0x4848484848484848ULL, h, t, n, idx);
+    if (n == 4) {
         ok = subset_ok_h(a.q1, a.q2, idx);
-        if (n == 4) break;
+    } else {
+        for (int t0 = 0; t0 < 100 && !ok; t0 += 64) {
+            const int t = t0 + lane;
+            int my[4] = {0, 0, 0, 0};
+            bool good = false;
+            if (t < 100) {
+                draw_subset<4>(a.seed ^ 0x4848484848484848ULL, h, t, n, my);
+                good = subset_ok_h(a.q1, a.q2, my);
+            }
+            const unsigned long long b = __ballot(good);
+            if (b) {
+                const int L = __ffsll((long long)b) - 1;
+                for (int k = 0; k < 4; ++k) idx[k] = __builtin_amdgcn_readlane(my[k], L);
+                ok = true;
+            }
+        }
     }
     if (!ok) {
-        a.h_valid[h] = 0;
+        if (lane == 0) a.h_valid[h] = 0;
         return;
     }
-    double A[72];
-    for (int r = 0; r < 4; ++r)
-        h_rows(a.q1[2 * idx[r]], a.q1[2 * idx[r] + 1], a.q2[2 * idx[r]], a.q2[2 * idx[r] + 1],
-               A + 18 * r, A + 18 * r + 9);
-    a.h_valid[h] = null_vector_8x9(A, a.h_models + 9 * (size_t)h) ? 1 : 0;
+    auto elem = [&](int i) -> double {
+        const int r = i / 9, col = i - 9 * (i / 9);
+        const int p = pick_uniform<4>(idx, r >> 1);
+        const double x1 = a.q1[2 * p], y1 = a.q1[2 * p + 1];
+        const double x2 = a.q2[2 * p], y2 = a.q2[2 * p + 1];
+        double ra[9], rb[9];
+        h_rows(x1, y1, x2, y2, ra, rb);
+        double v = 0.0;
+#pragma unroll
+        for (int k = 0; k < 9; ++k)
+            if (col == k) v = (r & 1) ? rb[k] : ra[k];
+        return v;
+    };
+    double A[2] = {elem(lane), lane < 8 ? elem(64 + lane) : 0.0};
+    double e[9];
+    const bool nv = null_vector_8x9_wave(A, s_m[wave], e);
+    if (lane == 0) {
+        if (nv)
+            for (int k = 0; k < 9; ++k) a.h_models[9 * (size_t)h + k] = e[k];
+        a.h_valid[h] = nv ? 1 : 0;
+    }
 }
 
 // ---------------------------------------------------------------- scoring
@@ -299,48 +412,160 @@ __device__ inline int update_num_iters(double p, double ep, int modelPoints, int
     return denom >= 0 || -num >= maxIters * (-denom) ? maxIters : (int)rint(num / denom);
 }
 
-// OpenCV's sequential RANSAC loop over the precomputed counts (one lane),
-// then the winner's inlier mask (all lanes).
+// OpenCV's sequential RANSAC loop over the precomputed counts, without
+// walking them one by one: a hypothesis changes the loop state only where
+// its count beats max(modelPoints - 1, every earlier count) (a strict prefix
+// maximum, "record"), and the loop's bound niters only shrinks, so the loop
+// is the walk over the records in order until one lies at or past niters.
+// The counts are scanned in segments of 2048 (8 per thread: a block max-scan
+// finds the records, an exclusive sum scan places them in LDS), the
+// records' RANSACUpdateNumIters logs are computed lane-parallel, and thread 0
+// applies the cheap part of each update in order.  Same state sequence as
+// the sequential loop; then the winner's inlier mask (all lanes).
+constexpr int kScanSeg = 2048;
+constexpr int kScanPer = kScanSeg / 256;
+
+__device__ inline int block_excl_scan_max(int v, int* s_w, int* total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int incl = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int o = __shfl_up(incl, d);
+        if (lane >= d) incl = max(incl, o);
+    }
+    const int excl_w = __shfl_up(incl, 1);
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    int pre = INT_MIN;
+    for (int k = 0; k < wave; ++k) pre = max(pre, s_w[k]);
+    *total = max(max(s_w[0], s_w[1]), max(s_w[2], s_w[3]));
+    __syncthreads();
+    return lane == 0 ? pre : max(pre, excl_w);
+}
+
+__device__ inline int block_excl_scan_sum(int v, int* s_w, int* total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int incl = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int o = __shfl_up(incl, d);
+        if (lane >= d) incl += o;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    int pre = 0;
+    for (int k = 0; k < wave; ++k) pre += s_w[k];
+    *total = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    __syncthreads();
+    return pre + incl - v;
+}
+
 template <bool IS_E>
 __global__ __launch_bounds__(256) void scan_kernel(GeoArgs a) {
-    __shared__ int s_best;
+    __shared__ int s_w[4];
+    __shared__ int s_rec[kScanSeg];
+    __shared__ double s_ln[kScanSeg];  // log(denom) of each record's update (or +inf: returns 0)
+    __shared__ int s_q[kScanSeg];      // rint(num / denom)
+    __shared__ int s_state[4];         // niters, best, maxGood, last
+    __shared__ int s_done;
     GeoCtl* c = a.ctl;
     if (!c->gate) return;
     const int n = c->n;
     const int modelPoints = IS_E ? 8 : 4;
     const int maxIters = IS_E ? a.e_iters : a.h_iters;
     const int* counts = IS_E ? a.e_counts : a.h_counts;
-    if (threadIdx.x == 0) {
-        int niters = maxIters, maxGood = 0, best = -1, h = 0;
-        const bool enough = n >= modelPoints && (!IS_E || n >= 8);
-        if (enough) {
-            for (h = 0; h < niters; ++h) {
-                const int cc = counts[h];
-                if (cc < 0) continue;
-                if (cc > max(maxGood, modelPoints - 1)) {
-                    maxGood = cc;
-                    best = h;
-                    niters = update_num_iters(a.confidence, (double)(n - cc) / n, modelPoints, niters);
-                }
-            }
-        }
-        if (IS_E) {
-            c->e_count = best >= 0 ? maxGood : 0;
-            c->e_best = best;
-            c->e_iters = enough ? h : 0;
-        } else {
-            c->h_count = best >= 0 ? maxGood : 0;
-            c->h_best = best;
-            c->h_iters = enough ? h : 0;
-        }
-        s_best = best;
+    const bool enough = n >= modelPoints && (!IS_E || n >= 8);
+    const int t = threadIdx.x;
+    // log(1 - p), the update's numerator (p = confidence, clamped)
+    const double p = fmin(fmax(a.confidence, 0.), 1.);
+    const double ln_num = log(fmax(1. - p, DBL_MIN));
+    if (t == 0) {
+        s_state[0] = maxIters;
+        s_state[1] = -1;
+        s_state[2] = 0;
+        s_state[3] = -1;
+        s_done = enough ? 0 : 1;
     }
     __syncthreads();
-    const int best = s_best;
+    int run_base = modelPoints - 1;  // max(modelPoints - 1, counts before the segment)
+    for (int seg = 0; seg < maxIters && !s_done; seg += kScanSeg) {
+        const int lo = seg + kScanPer * t, hi = min(lo + kScanPer, maxIters);
+        int cc[kScanPer], m = INT_MIN;
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) {
+            cc[k] = lo + k < hi ? counts[lo + k] : -1;
+            m = max(m, cc[k]);
+        }
+        int seg_max;
+        const int pre = max(run_base, block_excl_scan_max(m, s_w, &seg_max));
+        int run = pre, nrec = 0;
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k)
+            if (cc[k] > run) {
+                run = cc[k];
+                ++nrec;
+            }
+        int n_total;
+        int pos = block_excl_scan_sum(nrec, s_w, &n_total);
+        run = pre;
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k)
+            if (cc[k] > run) {
+                run = cc[k];
+                // cv::RANSACUpdateNumIters(p, (n - count) / n, modelPoints, .): the
+                // part that does not depend on the current niters
+                const double ep = fmin(fmax((double)(n - cc[k]) / n, 0.), 1.);
+                const double denom = 1. - pow(1. - ep, (double)modelPoints);
+                const double ln_den = denom < DBL_MIN ? INFINITY : log(denom);
+                s_rec[pos] = lo + k;
+                s_ln[pos] = ln_den;
+                s_q[pos] = denom < DBL_MIN ? 0 : (int)rint(ln_num / ln_den);
+                ++pos;
+            }
+        __syncthreads();
+        if (t == 0) {
+            int niters = s_state[0], best = s_state[1], maxGood = s_state[2], last = s_state[3];
+            for (int i = 0; i < n_total; ++i) {
+                const int h = s_rec[i];
+                if (h >= niters) {
+                    s_done = 1;
+                    break;
+                }
+                best = h;
+                maxGood = counts[h];
+                last = h;
+                const double ld = s_ln[i];
+                if (ld == INFINITY)
+                    niters = 0;  // denom < DBL_MIN
+                else if (!(ld >= 0 || -ln_num >= niters * (-ld)))
+                    niters = s_q[i];
+            }
+            s_state[0] = niters;
+            s_state[1] = best;
+            s_state[2] = maxGood;
+            s_state[3] = last;
+        }
+        run_base = max(run_base, seg_max);
+        __syncthreads();
+    }
+    const int best = s_state[1];
+    if (t == 0) {
+        // the loop variable at exit: the first h >= niters after the last record
+        const int h_exit = max(s_state[0], s_state[3] + 1);
+        if (IS_E) {
+            c->e_count = best >= 0 ? s_state[2] : 0;
+            c->e_best = best;
+            c->e_iters = enough ? h_exit : 0;
+        } else {
+            c->h_count = best >= 0 ? s_state[2] : 0;
+            c->h_best = best;
+            c->h_iters = enough ? h_exit : 0;
+        }
+    }
     if (best < 0) return;
     const double* M = (IS_E ? a.e_models : a.h_models) + 9 * (size_t)best;
     uint8_t* mask = IS_E ? a.e_mask : a.h_mask;
-    for (int i = threadIdx.x; i < n; i += 256) {
+    for (int i = t; i < n; i += 256) {
         const double x1 = a.q1[2 * i], y1 = a.q1[2 * i + 1], x2 = a.q2[2 * i], y2 = a.q2[2 * i + 1];
         mask[i] = (IS_E ? sampson_err(M, x1, y1, x2, y2) : transfer_err(M, x1, y1, x2, y2)) <= a.t2;
     }
@@ -843,7 +1068,7 @@ __global__ __launch_bounds__(256) void select_output_kernel(GeoArgs a) {
 void launch_pose_2d2d(const GeoArgs& a, hipStream_t stream, Timing* timing) {
     normalize_kernel<<<1, 256, 0, stream>>>(a);
     if (a.e_iters > 0) {
-        e_hyp_kernel<<<(a.e_iters + 63) / 64, 64, 0, stream>>>(a);
+        e_hyp_kernel<<<(a.e_iters + 3) / 4, 256, 0, stream>>>(a);
         score_kernel<true><<<a.e_iters, 256, 0, stream>>>(a);
         scan_kernel<true><<<1, 256, 0, stream>>>(a);
         recover_setup_kernel<<<1, 64, 0, stream>>>(a);
@@ -851,7 +1076,7 @@ void launch_pose_2d2d(const GeoArgs& a, hipStream_t stream, Timing* timing) {
         recover_pick_kernel<<<1, 64, 0, stream>>>(a);
     }
     if (a.h_iters > 0) {
-        h_hyp_kernel<<<(a.h_iters + 63) / 64, 64, 0, stream>>>(a);
+        h_hyp_kernel<<<(a.h_iters + 3) / 4, 256, 0, stream>>>(a);
         score_kernel<false><<<a.h_iters, 256, 0, stream>>>(a);
         scan_kernel<false><<<1, 256, 0, stream>>>(a);
         h_moment_leaves_kernel<<<(a.cap + 255) / 256, 256, 0, stream>>>(a);

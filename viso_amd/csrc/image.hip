@@ -10,11 +10,8 @@
 // algorithmic bytes per image = level-0 read + levels 1..3 written
 // (DESIGN.md §4).
 //
-// FAST: one workgroup per image row y.  It scores rows y-1, y, y+1 from a
-// 9-row LDS window, applies the strict 3x3 NMS to row y and appends the
-// surviving corners in ascending x with a ballot/popcount prefix (row-major
-// order is then restored across rows by fast_compact, an exclusive prefix
-// over per-row counts).
+// FAST: a tiled scoring / NMS launch and an ordering launch (see the FAST
+// section below).
 #include <algorithm>
 #include <type_traits>
 #include <vector>
@@ -662,51 +659,49 @@ __global__ __launch_bounds__(kPfThreads) void pyr_tail_kernel(PyrTailArgs a) {
 }
 
 // ---------------------------------------------------------------- FAST
-__constant__ int c_circle_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
-__constant__ int c_circle_dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+// Two launches per image (cv::FAST(img, kp, t) with NMS, src/viso.cpp:104;
+// OpenCV 3.x FAST_t<16> + cornerScore<16> restated):
+//
+// fast_tile_kernel — workgroup = tile of kFtCols output columns x kFtRows
+//   output rows.  The tile's pixel rows (+3 circle, +1 NMS halo each side) are
+//   staged in LDS once, in two copies offset by two bytes so that every lane's
+//   8-byte window starts dword-aligned in one of them.  A lane scores two
+//   adjacent pixels at once in packed 16-bit halves: per circle position one
+//   v_perm builds the pixel pair, packed subtractions give the brighter /
+//   darker sign bits, shifted into two 16-bit arc masks; the 9-contiguous test
+//   is three rotate-and-ANDs (runs of 2, 4, 8) and one with the mask rotated
+//   by 8 (equivalent to OpenCV's scan over 25 circle samples: a 9-run always
+//   covers one of each opposite pair, so its early-outs never change the
+//   result).  Corners (~2 % of pixels) are compacted into a per-wave list and
+//   scored densely, one lane per corner (cornerScore's min / max arcs).  Then
+//   the strict 3x3 NMS over the tile's score rows in LDS; the survivors of each
+//   (row, tile) are appended in ascending x by ballot ranks to a slot of
+//   kFtCap, with the row's count and the tile's total.
+// fast_order_kernel — workgroup = band of kFtRows rows: its offset is the sum
+//   of every earlier band's tile totals, an exclusive scan over its (row,
+//   tile) counts places each slot, and the keypoints are copied out in
+//   row-major, ascending-x order (cv::FAST's order).  The last band writes
+//   the total.
+// Every pixel is scored once (plus the one-pixel NMS ring of each tile), the
+// image is read from L2 once per tile, and no step walks rows serially.
+constexpr int kFtCols = 126;                 // output columns of a tile (lanes 0..62, 2 each)
+#ifndef VISO_FT_ROWS
+#define VISO_FT_ROWS 8
+#endif
+constexpr int kFtRows = VISO_FT_ROWS;        // output rows of a tile
+constexpr int kFtSRows = kFtRows + 2;        // score rows (NMS halo)
+constexpr int kFtPRows = kFtRows + 8;        // pixel rows (circle + NMS halo)
+constexpr int kFtChunks = 17;                // 8-byte chunks of a staged row (136 bytes)
+constexpr int kFtPStride = 8 * kFtChunks;
+constexpr int kFtCap = 64;                   // keypoints per (row, tile): strict NMS keeps <= 63
+constexpr int kFtList = 192;                 // corner list per wave (scored at >= 64)
+constexpr int kFtMaxTx = (kMaxWidth + kFtCols - 1) / kFtCols;
 
-// OpenCV FAST_t<16> arc test + cornerScore<16>; returns 0 or the score.
-__device__ inline int fast_score(const uint8_t* rows, int rstride, int x, int thresh) {
-    // rows points at the centre row of a >= 7 row window
-    const int v = rows[x];
-    int circ[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) circ[k] = rows[c_circle_dy[k] * rstride + x + c_circle_dx[k]];
-    auto cls = [&](int p) { int d = p - v; return d < -thresh ? 1 : (d > thresh ? 2 : 0); };
-    int d = cls(circ[0]) | cls(circ[8]);
-    if (d == 0) return 0;
-    d &= cls(circ[2]) | cls(circ[10]);
-    d &= cls(circ[4]) | cls(circ[12]);
-    d &= cls(circ[6]) | cls(circ[14]);
-    if (d == 0) return 0;
-    d &= cls(circ[1]) | cls(circ[9]);
-    d &= cls(circ[3]) | cls(circ[11]);
-    d &= cls(circ[5]) | cls(circ[13]);
-    d &= cls(circ[7]) | cls(circ[15]);
-    if (d == 0) return 0;
-    bool corner = false;
-    if (d & 1) {
-        int vt = v - thresh, count = 0;
-        for (int k = 0; k < 25; ++k) {
-            if (circ[k & 15] < vt) {
-                if (++count > 8) { corner = true; break; }
-            } else
-                count = 0;
-        }
-    }
-    if (!corner && (d & 2)) {
-        int vt = v + thresh, count = 0;
-        for (int k = 0; k < 25; ++k) {
-            if (circ[k & 15] > vt) {
-                if (++count > 8) { corner = true; break; }
-            } else
-                count = 0;
-        }
-    }
-    if (!corner) return 0;
-    int dd[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) dd[k] = v - circ[k];
+constexpr int kCircleDx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+constexpr int kCircleDy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+
+// cornerScore<16> (OpenCV fast_score.cpp) of a corner from dd[k] = v - circle[k]
+__device__ inline int fast_corner_score(const int (&dd)[16], int thresh) {
     int a0 = thresh;
 #pragma unroll
     for (int k = 0; k < 16; k += 2) {
@@ -728,99 +723,212 @@ __device__ inline int fast_score(const uint8_t* rows, int rstride, int x, int th
     return -b0 - 1;
 }
 
-__global__ __launch_bounds__(256) void fast_rows_kernel(const uint8_t* __restrict__ img, int w,
-                                                        int h, int thresh,
-                                                        int* __restrict__ row_count,
-                                                        int4* __restrict__ row_list,
-                                                        int row_cap) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint8_t* s_img = smem;                   // 9 rows (y-4 .. y+4)
-    uint8_t* s_sc = smem + 9 * (size_t)w;    // 3 score rows (y-1 .. y+1)
-    __shared__ int s_wave[4];
-    __shared__ int s_base;
-    const int y = blockIdx.x;
-    const int tid = threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6;
-    // stage the 9 input rows (rows outside the image are never read)
-    for (int r = 0; r < 9; ++r) {
-        int gy = y - 4 + r;
-        if (gy < 0 || gy >= h) continue;
-        const uint8_t* src = img + (size_t)gy * w;
-        for (int x = tid; x < w; x += 256) s_img[r * w + x] = src[x];
-    }
-    __syncthreads();
-    // scores of rows y-1, y, y+1 (candidates: rows 3..h-4, cols 3..w-4)
-    for (int r = 0; r < 3; ++r) {
-        int gy = y - 1 + r;
-        bool row_ok = gy >= 3 && gy < h - 3;
-        const uint8_t* centre = s_img + (size_t)(r + 3) * w;  // window row of gy
-        for (int x = tid; x < w; x += 256) {
-            int s = 0;
-            if (row_ok && x >= 3 && x < w - 3) s = fast_score(centre, w, x, thresh);
-            s_sc[r * w + x] = (uint8_t)s;
-        }
-    }
-    if (tid == 0) s_base = 0;
-    __syncthreads();
-    // strict 3x3 NMS on row y, ordered append
-    for (int x0 = 0; x0 < w; x0 += 256) {
-        int x = x0 + tid;
-        int sc = 0;
-        bool keep = false;
-        if (x < w) {
-            sc = s_sc[w + x];
-            if (sc > 0) {
-                auto at = [&](int rr, int xx) -> int {
-                    return (xx < 0 || xx >= w) ? 0 : (int)s_sc[rr * w + xx];
-                };
-                keep = sc > at(1, x + 1) && sc > at(1, x - 1) && sc > at(0, x - 1) &&
-                       sc > at(0, x) && sc > at(0, x + 1) && sc > at(2, x - 1) &&
-                       sc > at(2, x) && sc > at(2, x + 1);
-            }
-        }
-        unsigned long long m = __ballot(keep);
-        int before = __popcll(m & ((1ULL << lane) - 1ULL));
-        if (lane == 0) s_wave[wave] = __popcll(m);
-        __syncthreads();
-        int off = s_base;
-        for (int k = 0; k < wave; ++k) off += s_wave[k];
-        if (keep) {
-            int idx = off + before;
-            if (idx < row_cap) row_list[(size_t)y * row_cap + idx] = make_int4(x, y, sc, 0);
-        }
-        __syncthreads();
-        if (tid == 0) s_base += s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
-        __syncthreads();
-    }
-    if (tid == 0) row_count[y] = min(s_base, row_cap);
+// v_perm selector: window bytes m, m + 1 into the low bytes of the two halves
+__device__ constexpr uint32_t ft_sel(int m) {
+    return (uint32_t)m | (0x0cu << 8) | ((uint32_t)(m + 1) << 16) | (0x0cu << 24);
 }
 
-// Exclusive prefix over the per-row counts, then copy (row-major order).
-__global__ __launch_bounds__(256) void fast_compact_kernel(const int* __restrict__ row_count,
-                                                           const int4* __restrict__ row_list,
-                                                           int row_cap, int h, int cap,
-                                                           float2* __restrict__ kp_out,
-                                                           int4* __restrict__ raw_out,
-                                                           int* __restrict__ n_out) {
-    __shared__ int s_part[4];
-    const int y = blockIdx.x;
-    const int tid = threadIdx.x;
-    int acc = 0;
-    for (int r = tid; r < y; r += 256) acc += row_count[r];
-    acc = viso::wave_sum_int(acc);
-    if ((tid & 63) == 0) s_part[tid >> 6] = acc;
+// rotate each 16-bit half right by s (circle positions k + s -> k)
+template <int S>
+__device__ inline u16x2 ft_rot(u16x2 m) {
+    return (m >> (u16x2)S) | (m << (u16x2)(16 - S));
+}
+
+// 9 contiguous set bits anywhere on the 16-position circle, per half
+__device__ inline u16x2 ft_run9(u16x2 m) {
+    const u16x2 a1 = m & ft_rot<1>(m);
+    const u16x2 a2 = a1 & ft_rot<2>(a1);
+    const u16x2 a3 = a2 & ft_rot<4>(a2);
+    return a3 & ft_rot<8>(m);
+}
+
+__global__ __launch_bounds__(256) void fast_tile_kernel(const uint8_t* __restrict__ img, int w, int h,
+                                                        int thresh, int ntx, int* __restrict__ cnt,
+                                                        int* __restrict__ tot, int* __restrict__ lst) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_pa[kFtPRows][kFtPStride];  // pixel index i at i
+    __shared__ __attribute__((aligned(16))) uint8_t s_pb[kFtPRows][kFtPStride];  // pixel index i at i - 2
+    __shared__ __attribute__((aligned(16))) uint8_t s_sc[kFtSRows][128];
+    __shared__ uint16_t s_list[4][kFtList];
+    __shared__ int s_tot;
+    const int tx = blockIdx.x, ty = blockIdx.y;
+    // output columns [ox, ox + 126), rows [oy, oy + kFtRows); score column j
+    // is x = ox - 1 + j, score row r is y = oy - 1 + r; pixel index i is
+    // x = ox - 4 + i, pixel row q is y = oy - 4 + q
+    const int ox = tx * kFtCols, oy = ty * kFtRows;
+    const int t = threadIdx.x, lane = t & 63, wave = wave_id();
+    const long long npx = (long long)w * h;
+    for (int i = t; i < 2 * kFtPRows * kFtChunks; i += 256) {
+        const int cp = i >= kFtPRows * kFtChunks;
+        const int k = i - (cp ? kFtPRows * kFtChunks : 0);
+        const int q = k / kFtChunks, c = k - q * kFtChunks;
+        const int y = oy - 4 + q;
+        uint2 v = make_uint2(0u, 0u);
+        // bytes outside [0, w) of a row are read but never used by a candidate
+        if (y >= 0 && y < h) v = ps_load(img, (long long)y * w + (ox - 4 + 8 * c + 2 * cp), npx);
+        *reinterpret_cast<uint2*>((cp ? s_pb[q] : s_pa[q]) + 8 * c) = v;
+    }
+    for (int i = t; i < kFtSRows * 32; i += 256) reinterpret_cast<uint32_t*>(&s_sc[0][0])[i] = 0u;
+    if (t == 0) s_tot = 0;
     __syncthreads();
-    const int base = s_part[0] + s_part[1] + s_part[2] + s_part[3];
-    const int cnt = row_count[y];
-    for (int i = tid; i < cnt; i += 256) {
-        int o = base + i;
-        if (o < cap) {
-            int4 k = row_list[(size_t)y * row_cap + i];
-            if (kp_out) kp_out[o] = make_float2((float)k.x, (float)k.y);
-            if (raw_out) raw_out[o] = k;
+
+    // ---- corner test, two pixels (score columns 2l, 2l + 1) per lane
+    const uint8_t* win = (lane & 1) ? &s_pb[0][2 * lane - 2] : &s_pa[0][2 * lane];
+    const int x_lo = ox - 1 + 2 * lane;
+    const bool ok_lo = x_lo >= 3 && x_lo < w - 3, ok_hi = x_lo + 1 >= 3 && x_lo + 1 < w - 3;
+    const u16x2 T = (u16x2)(unsigned short)thresh;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    int nl = 0;  // wave-uniform list length
+    auto score_list = [&](int first, int m) {
+        __builtin_amdgcn_wave_barrier();
+        if (lane < m) {
+            const int e = s_list[wave][first + lane];
+            const int r = e >> 8, j = e & 255;
+            const uint8_t* cen = &s_pa[r + 3][j + 3];
+            const int v = cen[0];
+            int dd[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) dd[k] = v - (int)cen[kCircleDy[k] * kFtPStride + kCircleDx[k]];
+            s_sc[r][j] = (uint8_t)fast_corner_score(dd, thresh);
+        }
+        __builtin_amdgcn_wave_barrier();
+    };
+    for (int r = wave; r < kFtSRows; r += 4) {
+        const int y = oy - 1 + r;
+        if (y < 3 || y >= h - 3) continue;  // wave-uniform: no candidate row
+        uint32_t e0[7], e1[7];
+#pragma unroll
+        for (int d = 0; d < 7; ++d) {
+            const uint32_t* p = reinterpret_cast<const uint32_t*>(win + (r + d) * kFtPStride);
+            e0[d] = p[0];
+            e1[d] = p[1];
+        }
+        const u16x2 V = as_u16x2(__builtin_amdgcn_perm(e1[3], e0[3], ft_sel(3)));
+        const u16x2 VB = V + T, VD = V - T;  // wrapping; every difference below is within +-510
+        u16x2 mb = (u16x2)0, md = (u16x2)0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int d = kCircleDy[k] + 3;
+            const u16x2 C = as_u16x2(__builtin_amdgcn_perm(e1[d], e0[d], ft_sel(3 + kCircleDx[k])));
+            const u16x2 db = VB - C;  // sign: brighter (C > v + t)
+            const u16x2 dk = C - VD;  // sign: darker (C < v - t)
+            mb = (mb >> (u16x2)1) | (db & (u16x2)0x8000);
+            md = (md >> (u16x2)1) | (dk & (u16x2)0x8000);
+        }
+        const uint32_t run = __builtin_bit_cast(uint32_t, ft_run9(mb) | ft_run9(md));
+        const bool c_lo = ok_lo && (run & 0xffffu) != 0u, c_hi = ok_hi && (run >> 16) != 0u;
+        const unsigned long long b_lo = __ballot(c_lo), b_hi = __ballot(c_hi);
+        if ((b_lo | b_hi) == 0ull) continue;
+        const int n_lo = __popcll(b_lo);
+        if (c_lo) s_list[wave][nl + __popcll(b_lo & lt)] = (uint16_t)((r << 8) | (2 * lane));
+        if (c_hi) s_list[wave][nl + n_lo + __popcll(b_hi & lt)] = (uint16_t)((r << 8) | (2 * lane + 1));
+        nl += n_lo + __popcll(b_hi);
+        while (nl >= 64) {
+            nl -= 64;
+            score_list(nl, 64);
         }
     }
-    if (y == h - 1 && tid == 0) *n_out = base + cnt;
+    if (nl > 0) score_list(0, nl);
+    __syncthreads();
+
+    // ---- strict 3x3 NMS on output rows 1..kFtRows, columns 2l + 1, 2l + 2
+    int wave_total = 0;
+    for (int r = 1 + wave; r <= kFtRows; r += 4) {
+        const int y = oy + r - 1;
+        if (y >= h) break;
+        bool k0 = false, k1 = false;
+        int s0 = 0, s1 = 0;
+        if (lane < 63) {
+            int sv[3][4];
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                const uint16_t* p = reinterpret_cast<const uint16_t*>(&s_sc[r - 1 + d][2 * lane]);
+                const uint32_t a = p[0], b = p[1];
+                sv[d][0] = a & 255;
+                sv[d][1] = a >> 8;
+                sv[d][2] = b & 255;
+                sv[d][3] = b >> 8;
+            }
+            s0 = sv[1][1];
+            s1 = sv[1][2];
+            k0 = s0 > 0 && s0 > sv[1][0] && s0 > sv[1][2] && s0 > sv[0][0] && s0 > sv[0][1] && s0 > sv[0][2] &&
+                 s0 > sv[2][0] && s0 > sv[2][1] && s0 > sv[2][2];
+            k1 = s1 > 0 && s1 > sv[1][1] && s1 > sv[1][3] && s1 > sv[0][1] && s1 > sv[0][2] && s1 > sv[0][3] &&
+                 s1 > sv[2][1] && s1 > sv[2][2] && s1 > sv[2][3];
+        }
+        const unsigned long long b0 = __ballot(k0), b1 = __ballot(k1);
+        const int n = __popcll(b0) + __popcll(b1);
+        const size_t e = (size_t)y * ntx + tx;
+        const int rank = __popcll(b0 & lt) + __popcll(b1 & lt);
+        if (k0) lst[e * kFtCap + rank] = (ox + 2 * lane) | (s0 << 16);
+        if (k1) lst[e * kFtCap + rank + (k0 ? 1 : 0)] = (ox + 2 * lane + 1) | (s1 << 16);
+        if (lane == 0) cnt[e] = n;
+        wave_total += n;
+    }
+    if (lane == 0) atomicAdd(&s_tot, wave_total);
+    __syncthreads();
+    if (t == 0) tot[(size_t)ty * ntx + tx] = s_tot;
+}
+
+__global__ __launch_bounds__(256) void fast_order_kernel(int h, int ntx, int nty, const int* __restrict__ cnt,
+                                                         const int* __restrict__ tot,
+                                                         const int* __restrict__ lst, int cap,
+                                                         float2* __restrict__ kp_out,
+                                                         int4* __restrict__ raw_out, int* __restrict__ n_out) {
+    __shared__ int s_off[kFtRows * kFtMaxTx + 1];
+    __shared__ int s_w[4], s_b[4];
+    const int ty = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = wave_id();
+    const int oy = ty * kFtRows;
+    const int nr = min(kFtRows, h - oy);
+    const int E = nr * ntx;  // (row, tile) slots of the band, row-major
+    int acc = 0;
+    for (int i = t; i < ty * ntx; i += 256) acc += tot[i];
+    acc = wave_sum_int(acc);
+    constexpr int kPer = (kFtRows * kFtMaxTx + 255) / 256;
+    int c[kPer], sum = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int e = kPer * t + k;
+        c[k] = e < E ? cnt[(size_t)oy * ntx + e] : 0;
+        sum += c[k];
+    }
+    int incl = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int o = __shfl_up(incl, d);
+        if (lane >= d) incl += o;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    if (lane == 0) s_b[wave] = acc;
+    __syncthreads();
+    int off = incl - sum;
+    for (int k = 0; k < wave; ++k) off += s_w[k];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int e = kPer * t + k;
+        if (e < E) s_off[e] = off;
+        off += c[k];
+    }
+    const int total = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    const int base = s_b[0] + s_b[1] + s_b[2] + s_b[3];
+    if (t == 0) s_off[E] = total;
+    __syncthreads();
+    for (int i = t; i < total; i += 256) {
+        int lo = 0, hi = E;  // largest e with s_off[e] <= i
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (s_off[mid] <= i) lo = mid; else hi = mid;
+        }
+        const int o = base + i;
+        if (o < cap) {
+            const int rr = lo / ntx, tx = lo - rr * ntx;
+            const int y = oy + rr;
+            const int v = lst[((size_t)y * ntx + tx) * kFtCap + (i - s_off[lo])];
+            const int x = v & 0xffff, sc = v >> 16;
+            if (kp_out) kp_out[o] = make_float2((float)x, (float)y);
+            if (raw_out) raw_out[o] = make_int4(x, y, sc, 0);
+        }
+    }
+    if (ty == nty - 1 && t == 0) *n_out = base + total;
 }
 
 // Tail-launch plan for n images of a geometry; false (level 1 narrower than
@@ -938,16 +1046,36 @@ void launch_pyramid(const PyrGeom& g, uint8_t* base, int n_images, size_t img_st
     launch_pyramid_frames(g, l0.data(), slot.data(), n_images, stream);
 }
 
-size_t fast_row_cap(int w) { return (size_t)(w / 2 + 2); }
+static void fast_dims(int w, int h, int* ntx, int* nty) {
+    *ntx = (w + kFtCols - 1) / kFtCols;
+    *nty = (h + kFtRows - 1) / kFtRows;
+}
+
+size_t fast_scratch_bytes(int w, int h) {
+    int ntx, nty;
+    fast_dims(w, h, &ntx, &nty);
+    const size_t slots = (size_t)h * ntx;
+    return ((sizeof(int) * (slots + (size_t)nty * ntx) + 255) & ~(size_t)255) + sizeof(int) * slots * kFtCap;
+}
+
+FastScratch fast_scratch_at(void* base, int w, int h) {
+    int ntx, nty;
+    fast_dims(w, h, &ntx, &nty);
+    const size_t slots = (size_t)h * ntx;
+    FastScratch s;
+    s.cnt = (int*)base;
+    s.tot = s.cnt + slots;
+    s.lst = (int*)((char*)base + ((sizeof(int) * (slots + (size_t)nty * ntx) + 255) & ~(size_t)255));
+    return s;
+}
 
 void launch_fast(const uint8_t* img, int w, int h, int thresh, FastScratch& s, float2* kp_out,
                  int4* raw_out, int cap, int* n_out, hipStream_t stream) {
-    int row_cap = (int)fast_row_cap(w);
-    size_t smem = 12 * (size_t)w;
+    int ntx, nty;
+    fast_dims(w, h, &ntx, &nty);
     thresh = thresh < 0 ? 0 : (thresh > 255 ? 255 : thresh);
-    fast_rows_kernel<<<h, 256, smem, stream>>>(img, w, h, thresh, s.row_count, s.row_list, row_cap);
-    fast_compact_kernel<<<h, 256, 0, stream>>>(s.row_count, s.row_list, row_cap, h, cap, kp_out,
-                                               raw_out, n_out);
+    fast_tile_kernel<<<dim3(ntx, nty), 256, 0, stream>>>(img, w, h, thresh, ntx, s.cnt, s.tot, s.lst);
+    fast_order_kernel<<<nty, 256, 0, stream>>>(h, ntx, nty, s.cnt, s.tot, s.lst, cap, kp_out, raw_out, n_out);
 }
 
 }  // namespace viso

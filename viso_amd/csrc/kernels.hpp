@@ -18,11 +18,15 @@ constexpr int kPyrBatch = 128;
 void launch_pyramid_frames(const PyrGeom& g, const uint8_t* const* l0, uint8_t* const* slot,
                            int n, hipStream_t stream);
 
+// FAST device scratch (image.hip): per (row, tile) keypoint counts and
+// slots, per-tile totals; carved from fast_scratch_bytes(w, h) bytes.
 struct FastScratch {
-    int* row_count = nullptr;   // [h]
-    int4* row_list = nullptr;   // [h * fast_row_cap(w)]
+    int* cnt = nullptr;  // [h][tiles across]
+    int* tot = nullptr;  // [bands][tiles across]
+    int* lst = nullptr;  // [h][tiles across][64]
 };
-size_t fast_row_cap(int w);
+size_t fast_scratch_bytes(int w, int h);
+FastScratch fast_scratch_at(void* base, int w, int h);
 // FAST + NMS on a level-0 image; writes up to cap keypoints (float2 and/or
 // raw int4 {x, y, score, 0}) and the total count to *n_out (device).
 void launch_fast(const uint8_t* img, int w, int h, int thresh, FastScratch& s, float2* kp_out,

@@ -205,6 +205,102 @@ __device__ inline bool null_vector_8x9(const double* Ain, double* e) {
     return true;
 }
 
+// null_vector_8x9 on one wave: lane l owns elements l and 64 + l (l < 8) of
+// the row-major 8x9 matrix (A[0] / A[1] on entry, the eliminated matrix on
+// return) and performs exactly the sequential routine's operations on them:
+// the complete pivot is the first maximum |M| of the trailing submatrix in
+// row-major order (a (value, index) wave maximum; NaN is never chosen), the
+// row / column swaps are a permuted re-read of the matrix staged in `lds`
+// (72 doubles, the wave's own), the pivot row divided by the pivot, and
+// every other row r with f = M[r][k] != 0 updated as M[r][j] - f * M[k][j].
+// On success every lane receives the null vector in e[9].
+__device__ inline bool null_vector_8x9_wave(double (&A)[2], double* lds, double* e) {
+    const int lane = threadIdx.x & 63;
+    const int i0 = lane, i1 = 64 + lane;  // element i1 exists for lane < 8
+    const int r0 = i0 / 9, c0 = i0 - 9 * r0, r1 = 7, c1 = i1 - 63;
+    const bool has1 = lane < 8;
+    int cp = lane;  // lane j < 9: the column permutation cp[j]
+    for (int k = 0; k < 8; ++k) {
+        // ---- pivot: the first maximum of |M[r][c]|, r >= k, c >= k
+        double best = -2.0;
+        int bi = 1 << 20;
+        if (r0 >= k && c0 >= k) {
+            const double a = fabs(A[0]);
+            best = a > -1.0 ? a : -1.0;
+            bi = i0;
+        }
+        if (has1 && c1 >= k) {
+            const double a = fabs(A[1]);
+            const double v = a > -1.0 ? a : -1.0;
+            if (v > best) {
+                best = v;
+                bi = i1;
+            }
+        }
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const double ob = __shfl_xor(best, d);
+            const int oi = __shfl_xor(bi, d);
+            if (ob > best || (ob == best && oi < bi)) {
+                best = ob;
+                bi = oi;
+            }
+        }
+        if (!(best > 1e-300)) return false;  // wave-uniform
+        const int pr = bi / 9, pc = bi - 9 * pr;
+        // ---- stage, then re-read through the row swap k <-> pr and column swap k <-> pc
+        __builtin_amdgcn_wave_barrier();
+        lds[i0] = A[0];
+        if (has1) lds[i1] = A[1];
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+        __builtin_amdgcn_wave_barrier();
+        auto src = [&](int r, int c) {
+            const int rr = r == k ? pr : (r == pr ? k : r);
+            const int cc = c == k ? pc : (c == pc ? k : c);
+            return lds[9 * rr + cc];
+        };
+        const double piv = src(k, k);
+        double m0 = src(r0, c0), f0 = src(r0, k), p0 = src(k, c0);
+        double m1 = 0.0, p1 = 0.0, f1 = 0.0;
+        if (has1) {
+            m1 = src(r1, c1);
+            f1 = src(r1, k);
+            p1 = src(k, c1);
+        }
+        {
+            const int ck = __shfl(cp, k), cpc = __shfl(cp, pc);
+            if (lane == k) cp = cpc;
+            if (lane == pc) cp = ck;
+        }
+        // ---- normalise the pivot row, eliminate the other rows
+        auto upd = [&](int r, int c, double m, double f, double p) -> double {
+            if (r == k) return c > k ? m / piv : (c == k ? 1.0 : m);
+            if (c < k || f == 0.0) return m;
+            return c == k ? 0.0 : m - f * (p / piv);
+        };
+        A[0] = upd(r0, c0, m0, f0, p0);
+        if (has1) A[1] = upd(r1, c1, m1, f1, p1);
+    }
+    // e[cp[j]] = ep[j]: ep[k] = -M[k][8] (k < 8), ep[8] = 1
+    __builtin_amdgcn_wave_barrier();
+    if (c0 == 8) lds[r0] = -A[0];
+    if (has1 && c1 == 8) lds[r1] = -A[1];
+    if (lane == 8) lds[8] = 1.0;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    const double epj = lane < 9 ? lds[lane] : 0.0;
+    __builtin_amdgcn_wave_barrier();
+    if (lane < 9) lds[16 + cp] = epj;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < 9; ++j) e[j] = lds[16 + j];
+    return true;
+}
+
 __device__ inline double det3(const double* m) {
     return m[0] * (m[4] * m[8] - m[5] * m[7]) - m[1] * (m[3] * m[8] - m[5] * m[6]) +
            m[2] * (m[3] * m[7] - m[4] * m[6]);

@@ -109,12 +109,9 @@ int viso_rig::init() {
     if (!rc) rc = log.ensure(96 * (size_t)std::max(p.max_poses, 1));
     if (!rc) rc = kp.ensure(sizeof(float2) * (size_t)p.max_features);
     if (!rc) rc = counts.ensure(256);
-    const size_t row_cap = fast_row_cap(g.w[0]);
-    const size_t rows_off = ((sizeof(int) * (g.h[0] + 1)) + 255) & ~(size_t)255;
-    if (!rc) rc = fast_rows.ensure(rows_off + sizeof(int4) * row_cap * g.h[0]);
+    if (!rc) rc = fast_rows.ensure(fast_scratch_bytes(g.w[0], g.h[0]));
     if (rc) return rc;
-    fast.row_count = (int*)fast_rows.ptr;
-    fast.row_list = (int4*)((char*)fast_rows.ptr + rows_off);
+    fast = fast_scratch_at(fast_rows.ptr, g.w[0], g.h[0]);
     VISO_HIP_CHECK(hipHostMalloc((void**)&h_int, 64 * sizeof(int)));
     std::vector<double> Ad(36 * (size_t)n);
     for (int c = 0; c < n; ++c) rig_adjoint_host(E[c], &Ad[36 * (size_t)c]);
