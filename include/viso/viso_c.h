@@ -52,7 +52,7 @@ typedef struct viso_params {
     int32_t ransac_h_iters;           /* 2000 (src/viso.cpp:240) */
     double ransac_confidence;         /* 0.99 (src/viso.cpp:222,240) */
     uint64_t ransac_seed;             /* counter-RNG seed of the samplers */
-    int32_t max_features;             /* capacity of FAST / KLT arrays */
+    int32_t max_features;             /* capacity of FAST / KLT arrays (1..65536) */
     int32_t max_poses;                /* capacity of the pose log */
     int32_t batch_frames;             /* frames per viso_process_frames_device
                                          chunk (frame-slot pool size) */

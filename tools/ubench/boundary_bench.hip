@@ -32,6 +32,7 @@ __device__ unsigned long long g_first_exit[kRing];
 template <int AB>
 struct Args {
     int seq;
+    int spin;  // ticks (100 MHz) every block waits before its exit stamp
     int pad[AB / 4];
 };
 
@@ -48,6 +49,8 @@ __global__ __launch_bounds__(THREADS) void chain_kernel(const double* __restrict
         __syncthreads();
         if (s[(threadIdx.x + 1) % (LDS / 8)] < -1.0 && pre) ((double*)pre)[0] = 1.0;  // never true
     }
+    if (a.spin > 0)
+        while (__builtin_amdgcn_s_memrealtime() < t0 + (unsigned long long)a.spin) __builtin_amdgcn_s_sleep(2);
     if (threadIdx.x == 0) {
         const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
         atomicMax(&g_exit[slot], t1);
@@ -62,13 +65,14 @@ struct Result {
 };
 
 template <int THREADS, int LDS, bool VG128, int AB>
-int run(const char* name, int blocks, int n, Result* out) {
+int run(const char* name, int blocks, int n, Result* out, int spin = 0, bool graph = false) {
     std::vector<unsigned long long> zero(kRing, 0), big(kRing, ~0ull);
     CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_exit), zero.data(), sizeof(unsigned long long) * kRing));
     CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_first_exit), big.data(), sizeof(unsigned long long) * kRing));
     hipStream_t st;
     CHECK(hipStreamCreate(&st));
     Args<AB> a{};
+    a.spin = spin;
     double* pre = nullptr;
     int* g = nullptr;
     for (int w = 0; w < 50; ++w) {  // warm-up (code object, queues)
@@ -81,10 +85,28 @@ int run(const char* name, int blocks, int n, Result* out) {
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
     CHECK(hipEventCreate(&e1));
+    hipGraphExec_t gx = nullptr;
+    if (graph) {
+        hipGraph_t gr;
+        CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal));
+        for (int i = 0; i < n; ++i) {
+            a.seq = i;
+            chain_kernel<THREADS, LDS, VG128, AB><<<blocks, THREADS, 0, st>>>(pre, g, i, a);
+        }
+        CHECK(hipStreamEndCapture(st, &gr));
+        CHECK(hipGraphInstantiate(&gx, gr, nullptr, nullptr, 0));
+        CHECK(hipGraphLaunch(gx, st));  // warm replay
+        CHECK(hipStreamSynchronize(st));
+        CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_exit), zero.data(), sizeof(unsigned long long) * kRing));
+    }
     CHECK(hipEventRecord(e0, st));
-    for (int i = 0; i < n; ++i) {
-        a.seq = i;
-        chain_kernel<THREADS, LDS, VG128, AB><<<blocks, THREADS, 0, st>>>(pre, g, i, a);
+    if (graph) {
+        CHECK(hipGraphLaunch(gx, st));
+    } else {
+        for (int i = 0; i < n; ++i) {
+            a.seq = i;
+            chain_kernel<THREADS, LDS, VG128, AB><<<blocks, THREADS, 0, st>>>(pre, g, i, a);
+        }
     }
     CHECK(hipEventRecord(e1, st));
     CHECK(hipStreamSynchronize(st));
@@ -104,9 +126,9 @@ int run(const char* name, int blocks, int n, Result* out) {
     out->gap_p50 = gap[gap.size() / 2];
     out->gap_mean = gm / gap.size();
     out->span_p50 = span[span.size() / 2];
-    printf("{\"variant\": \"%s\", \"blocks\": %d, \"threads\": %d, \"lds\": %d, \"vgpr128\": %d, \"arg_bytes\": %d, "
+    printf("{\"variant\": \"%s\", \"spin_us\": %.1f, \"graph\": %d, \"blocks\": %d, \"threads\": %d, \"lds\": %d, \"vgpr128\": %d, \"arg_bytes\": %d, "
            "\"us_per_launch\": %.3f, \"gap_p50_us\": %.3f, \"gap_mean_us\": %.3f, \"span_p50_us\": %.3f}\n",
-           name, blocks, THREADS, LDS, (int)VG128, AB, out->us_per_launch, out->gap_p50, out->gap_mean, out->span_p50);
+           name, spin / 100.0, (int)graph, blocks, THREADS, LDS, (int)VG128, AB, out->us_per_launch, out->gap_p50, out->gap_mean, out->span_p50);
     CHECK(hipStreamDestroy(st));
     return 0;
 }
@@ -126,5 +148,11 @@ int main() {
     rc |= run<256, 0, false, 16>("256-bare", 256, n, &r);
     rc |= run<64, 0, false, 16>("64-bare", 256, n, &r);
     rc |= run<1024, 68 * 1024, true, 600>("direct-like-again", 247, n, &r);
+    // kernels long enough (10 us) that the host stays ahead: the GPU-side boundary
+    rc |= run<1024, 68 * 1024, true, 600>("direct-like-10us", 247, n, &r, 1000);
+    rc |= run<256, 0, false, 16>("256-bare-10us", 256, n, &r, 1000);
+    rc |= run<1024, 68 * 1024, true, 600>("direct-like-graph", 247, n, &r, 0, true);
+    rc |= run<1024, 68 * 1024, true, 600>("direct-like-10us-graph", 247, n, &r, 1000, true);
+    rc |= run<256, 0, false, 16>("256-bare-graph", 256, n, &r, 0, true);
     return rc;
 }

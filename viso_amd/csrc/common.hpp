@@ -204,6 +204,10 @@ __device__ inline double wave_tree_sum_dpp(double v) {
 
 __device__ inline double dsel(bool c, double a, double b) { return c ? a : b; }
 
+#ifndef VISO_TREE3_ROR
+#define VISO_TREE3_ROR 1
+#endif
+
 // The canonical wave trees of three values at once: reduce-scatter over the
 // xor-1 / xor-2 levels (lane class (b1, b0) = (0,0) / (0,1) / (1,0) keeps a /
 // b / c, (1,1) a zero), then true xor-4 / xor-8 partners (DPP row_shr /
@@ -221,8 +225,7 @@ __device__ inline void wave_tree_sum3(double a, double b, double c, double& ra, 
     // under a partial EXEC and read inactive lanes), then selected
     const double r4 = dpp_f64<0x114>(v), l4 = dpp_f64<0x104>(v);  // row_shr / row_shl by 4
     v = v + dsel(b2, r4, l4);                                        // lane ^ 4
-    const double r8 = dpp_f64<0x118>(v), l8 = dpp_f64<0x108>(v);  // row_shr / row_shl by 8
-    v = v + dsel(b3, r8, l8);                                        // lane ^ 8
+    v = v + dpp_f64<0x128>(v);  // lane ^ 8 (row_ror:8 is exactly the xor-8 partner)
     double x, y;
     permlane16_swap_f64(v, v, x, y);
     v = x + y;
@@ -237,7 +240,8 @@ __device__ inline void wave_tree_sum3(double a, double b, double c, double& ra, 
 // pairwise tree (pixels p and p + 32 first; oracle tree_sum_desc64).  xor 32
 // pairs a (lanes < 32) and b (lanes >= 32) with one v_permlane32_swap and c
 // everywhere with another; xor 16 keeps a / b in even rows and c in odd rows;
-// then xor 8 / 4 by DPP row shifts + select and xor 2 / 1 by quad_perm.
+// then xor 8 / 4 by DPP row_ror (xor 8 exactly; xor 4 because the xor-8
+// level leaves lanes l and l ^ 8 equal) and xor 2 / 1 by quad_perm.
 // Results read from lanes 0 (a), 32 (b), 16 (c).  Requires EXEC = all lanes.
 __device__ inline void wave_tree_sum3_desc(double a, double b, double c, double& ra, double& rb, double& rc) {
     const int lane = threadIdx.x & 63;
@@ -249,10 +253,17 @@ __device__ inline void wave_tree_sum3_desc(double a, double b, double c, double&
     const double cc = x + y;
     permlane16_swap_f64(ab, cc, x, y);
     double v = x + y;
+#if VISO_TREE3_ROR
+    v = v + dpp_f64<0x128>(v);  // lane ^ 8: row_ror:8 is exactly the xor-8 partner
+    // lane ^ 4: lanes l and l ^ 8 now hold the same sum, so row_ror:4 (lane
+    // (l - 4) mod 16, i.e. l ^ 4 or its xor-8 twin) delivers the xor-4 partner's
+    v = v + dpp_f64<0x124>(v);
+#else
     const double r8 = dpp_f64<0x118>(v), l8 = dpp_f64<0x108>(v);  // row_shr / row_shl by 8
     v = v + dsel(b3, r8, l8);                                        // lane ^ 8
     const double r4 = dpp_f64<0x114>(v), l4 = dpp_f64<0x104>(v);  // row_shr / row_shl by 4
     v = v + dsel(b2, r4, l4);                                        // lane ^ 4
+#endif
     v = v + dpp_f64<0x4E>(v);                                        // lane ^ 2
     v = v + dpp_f64<0xB1>(v);                                        // lane ^ 1
     ra = readlane_f64(v, 0);
@@ -312,7 +323,7 @@ __device__ inline double reduce_scatter_28(const double* v, int* value_index) {
     for (int k = 0; k < 2; ++k) {
         const double send = dsel(b3, d[k], d[2 + k]);
         const double keep = dsel(b3, d[2 + k], d[k]);
-        const double recv = dsel(b3, dpp_f64<0x118>(send), dpp_f64<0x108>(send));  // row_shr:8 / row_shl:8
+        const double recv = dpp_f64<0x128>(send);  // row_ror:8 = the xor-8 partner
         e[k] = keep + recv;
     }
     // xor 16: row pairs (0,1), (2,3); even rows keep e[0], odd rows e[1]
@@ -361,7 +372,7 @@ __device__ inline double reduce_scatter_28_desc(const double* v, int* value_inde
         const double hi = k < 3 ? c[4 + k] : 0.0;
         const double send = dsel(b3, c[k], hi);
         const double keep = dsel(b3, hi, c[k]);
-        const double recv = dsel(b3, dpp_f64<0x118>(send), dpp_f64<0x108>(send));
+        const double recv = dpp_f64<0x128>(send);  // row_ror:8 = the xor-8 partner
         d[k] = keep + recv;
     }
     double e[2];
@@ -438,9 +449,7 @@ __device__ inline float reduce_scatter_28_f32(const float* v, int* value_index) 
     for (int k = 0; k < 2; ++k) {
         const float send = b3 ? d[k] : d[2 + k];
         const float keep = b3 ? d[2 + k] : d[k];
-        const float r8 = dpp_f32<0x118>(send), l8 = dpp_f32<0x108>(send);
-        const float recv = b3 ? r8 : l8;
-        e[k] = keep + recv;
+        e[k] = keep + dpp_f32<0x128>(send);  // row_ror:8 = the xor-8 partner
     }
     float ra, rb;
     permlane16_swap_f32(e[0], e[1], ra, rb);
@@ -462,8 +471,7 @@ __device__ inline void wave_tree_sum3_f32(float a, float b, float c, float& ra, 
     float v = (b1 ? q : p) + dpp_f32<0x4E>(b1 ? p : q);
     const float r4 = dpp_f32<0x114>(v), l4 = dpp_f32<0x104>(v);
     v = v + (b2 ? r4 : l4);
-    const float r8 = dpp_f32<0x118>(v), l8 = dpp_f32<0x108>(v);
-    v = v + (b3 ? r8 : l8);
+    v = v + dpp_f32<0x128>(v);  // row_ror:8 = the xor-8 partner
     float x, y;
     permlane16_swap_f32(v, v, x, y);
     v = x + y;
@@ -488,10 +496,8 @@ __device__ inline void wave_tree_sum3_f32_desc(float a, float b, float c, float&
     const float cc = x + y;
     permlane16_swap_f32(ab, cc, x, y);
     float v = x + y;
-    const float r8 = dpp_f32<0x118>(v), l8 = dpp_f32<0x108>(v);
-    v = v + (b3 ? r8 : l8);
-    const float r4 = dpp_f32<0x114>(v), l4 = dpp_f32<0x104>(v);
-    v = v + (b2 ? r4 : l4);
+    v = v + dpp_f32<0x128>(v);  // lane ^ 8 (row_ror:8)
+    v = v + dpp_f32<0x124>(v);  // lane ^ 4 (row_ror:4 after the duplicated xor-8 level)
     v = v + dpp_f32<0x4E>(v);
     v = v + dpp_f32<0xB1>(v);
     ra = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));

@@ -89,7 +89,7 @@ int viso_create(const viso_params* p, int device, viso_ctx** out) {
     if (!p || !out) return VISO_ERR_ARG;
     *out = nullptr;
     if (p->width < 16 || p->height < 16 || p->width > kMaxWidth) return VISO_ERR_ARG;
-    if (p->max_features <= 0 || p->batch_frames <= 0) return VISO_ERR_ARG;
+    if (p->max_features <= 0 || p->max_features > 65536 || p->batch_frames <= 0) return VISO_ERR_ARG;
     if (p->precision != VISO_PRECISION_FAITHFUL && p->precision != VISO_PRECISION_FAST) return VISO_ERR_ARG;
     int rc = check_device_present();
     if (rc != VISO_OK) return rc;

@@ -521,13 +521,27 @@ int viso_ctx::on_new_frame(int cur) {
                 geo.kp1 = (const float2*)kp1.ptr;
                 geo.kp2 = (const float2*)kp2.ptr;
                 geo.p1_in = geo.p2_in = nullptr;
+                // the gates of PoseEstimation2d2d (src/viso.cpp:184, 216) are read
+                // first: most initialisation frames stop there (too little
+                // disparity yet), and then none of the ~17 RANSAC / motion
+                // kernels is launched; a frame past the gates pays one more
+                // host round trip
                 {
                     TimedRegion t(timing, VISO_KERNEL_RANSAC, stream);
-                    launch_pose_2d2d(geo, stream, &timing);
+                    launch_pose_2d2d_gate(geo, stream);
                 }
                 VISO_HIP_CHECK(hipGetLastError());
                 VISO_HIP_CHECK(hipMemcpyAsync(h_ctl, geo.ctl, sizeof(GeoCtl), hipMemcpyDeviceToHost, stream));
                 VISO_HIP_CHECK(hipStreamSynchronize(stream));
+                if (h_ctl->gate) {
+                    {
+                        TimedRegion t(timing, VISO_KERNEL_RANSAC, stream);
+                        launch_pose_2d2d_body(geo, stream);
+                    }
+                    VISO_HIP_CHECK(hipGetLastError());
+                    VISO_HIP_CHECK(hipMemcpyAsync(h_ctl, geo.ctl, sizeof(GeoCtl), hipMemcpyDeviceToHost, stream));
+                    VISO_HIP_CHECK(hipStreamSynchronize(stream));
+                }
                 const GeoCtl& c = *h_ctl;
                 n_track = c.n;
                 int nr_inliers = 0;

@@ -94,43 +94,72 @@ __device__ inline int pick_uniform(const int* v, int i) {
 // ---------------------------------------------------------------- normalise
 // p = K_inv * (x, y, 1) (src/viso.cpp:45-48); q = float-rounded (cv::Point2f,
 // :204-205); disparity = canonical tree of |p2 - p1|^2 (:199-211).
-__global__ __launch_bounds__(256) void normalize_kernel(GeoArgs a) {
-    __shared__ double s_red[4];
+// One 1,024-thread workgroup: thread t owns the C = P / 1024 consecutive
+// points [t C, t C + C) of the padded count P (C <= 64: max_features <=
+// 65536), normalises them, and folds their leaves into its subtree in
+// registers (binary-counter stack with compile-time slots); then the wave
+// trees and the 16 waves' pairwise top.  The same pairwise tree over the P
+// padded leaves as block_tree_sum (+0.0 leaves past n, and past P up to
+// 1,024 leaves: adding +0.0 to a sum of squares is exact).
+constexpr int kNormThreads = 1024;
+constexpr int kNormMaxC = 64;
+
+__global__ __launch_bounds__(kNormThreads) void normalize_kernel(GeoArgs a) {
+    __shared__ double s_w[kNormThreads / 64];
     const int n = *a.n_dev;
     const double* Ki = a.Kinv;
-    for (int i = threadIdx.x; i < n; i += 256) {
-        double p1[3], p2[3];
-        if (a.p1_in) {
-            for (int r = 0; r < 3; ++r) {
-                p1[r] = a.p1_in[3 * i + r];
-                p2[r] = a.p2_in[3 * i + r];
+    int P = 1;
+    while (P < n) P <<= 1;
+    const int C = P > kNormThreads ? P / kNormThreads : 1;
+    const int t = threadIdx.x;
+    double stack[7];  // log2(kNormMaxC) + 1 slots
+#pragma unroll
+    for (int j = 0; j < kNormMaxC; ++j) {
+        if (j >= C) break;
+        const int i = t * C + j;
+        double leaf = 0.0;
+        if (i < n) {
+            double p1[3], p2[3];
+            if (a.p1_in) {
+                for (int r = 0; r < 3; ++r) {
+                    p1[r] = a.p1_in[3 * i + r];
+                    p2[r] = a.p2_in[3 * i + r];
+                }
+            } else {
+                const float2 k1 = a.kp1[i], k2 = a.kp2[i];
+                const double u1[3] = {(double)k1.x, (double)k1.y, 1};
+                const double u2[3] = {(double)k2.x, (double)k2.y, 1};
+                for (int r = 0; r < 3; ++r) {
+                    p1[r] = Ki[3 * r] * u1[0] + Ki[3 * r + 1] * u1[1] + Ki[3 * r + 2] * u1[2];
+                    p2[r] = Ki[3 * r] * u2[0] + Ki[3 * r + 1] * u2[1] + Ki[3 * r + 2] * u2[2];
+                }
             }
-        } else {
-            const float2 k1 = a.kp1[i], k2 = a.kp2[i];
-            const double u1[3] = {(double)k1.x, (double)k1.y, 1};
-            const double u2[3] = {(double)k2.x, (double)k2.y, 1};
             for (int r = 0; r < 3; ++r) {
-                p1[r] = Ki[3 * r] * u1[0] + Ki[3 * r + 1] * u1[1] + Ki[3 * r + 2] * u1[2];
-                p2[r] = Ki[3 * r] * u2[0] + Ki[3 * r + 1] * u2[1] + Ki[3 * r + 2] * u2[2];
+                a.p1[3 * i + r] = p1[r];
+                a.p2[3 * i + r] = p2[r];
             }
+            a.q1[2 * i] = (double)(float)p1[0];
+            a.q1[2 * i + 1] = (double)(float)p1[1];
+            a.q2[2 * i] = (double)(float)p2[0];
+            a.q2[2 * i + 1] = (double)(float)p2[1];
+            const double dx = p2[0] - p1[0];
+            const double dy = p2[1] - p1[1];
+            leaf = dx * dx + dy * dy;
         }
-        for (int r = 0; r < 3; ++r) {
-            a.p1[3 * i + r] = p1[r];
-            a.p2[3 * i + r] = p2[r];
-        }
-        a.q1[2 * i] = (double)(float)p1[0];
-        a.q1[2 * i + 1] = (double)(float)p1[1];
-        a.q2[2 * i] = (double)(float)p2[0];
-        a.q2[2 * i + 1] = (double)(float)p2[1];
+        // binary counter: leaf j closes the subtrees of its trailing one bits
+        int sp = __builtin_popcount(j);
+#pragma unroll
+        for (int k = j; k & 1; k >>= 1) leaf = stack[--sp] + leaf;
+        stack[sp] = leaf;
     }
+    double v = wave_tree_sum(stack[0]);
+    if ((t & 63) == 0) s_w[t >> 6] = v;
     __syncthreads();
-    const double s = block_tree_sum(n, [&](int i) {
-        const double dx = a.p2[3 * i] - a.p1[3 * i];
-        const double dy = a.p2[3 * i + 1] - a.p1[3 * i + 1];
-        return dx * dx + dy * dy;
-    }, s_red);
-    if (threadIdx.x == 0) {
-        double d = s;
+    if (t == 0) {
+        double l1[8], l2[4];
+        for (int k = 0; k < 8; ++k) l1[k] = s_w[2 * k] + s_w[2 * k + 1];
+        for (int k = 0; k < 4; ++k) l2[k] = l1[2 * k] + l1[2 * k + 1];
+        double d = (l2[0] + l2[1]) + (l2[2] + l2[3]);
         const double f = (a.K[0] + a.K[1]) / 2;
         if (d != 0) {
             d /= n;
@@ -1065,8 +1094,11 @@ __global__ __launch_bounds__(256) void select_output_kernel(GeoArgs a) {
 
 }  // namespace
 
-void launch_pose_2d2d(const GeoArgs& a, hipStream_t stream, Timing* timing) {
-    normalize_kernel<<<1, 256, 0, stream>>>(a);
+void launch_pose_2d2d_gate(const GeoArgs& a, hipStream_t stream) {
+    normalize_kernel<<<1, kNormThreads, 0, stream>>>(a);
+}
+
+void launch_pose_2d2d_body(const GeoArgs& a, hipStream_t stream) {
     if (a.e_iters > 0) {
         e_hyp_kernel<<<(a.e_iters + 3) / 4, 256, 0, stream>>>(a);
         score_kernel<true><<<a.e_iters, 256, 0, stream>>>(a);
@@ -1087,6 +1119,11 @@ void launch_pose_2d2d(const GeoArgs& a, hipStream_t stream, Timing* timing) {
     select_points_kernel<<<(total + 255) / 256, 256, 0, stream>>>(a);
     select_reduce_kernel<<<1, 256, 0, stream>>>(a);
     select_output_kernel<<<1, 256, 0, stream>>>(a);
+}
+
+void launch_pose_2d2d(const GeoArgs& a, hipStream_t stream, Timing* timing) {
+    launch_pose_2d2d_gate(a, stream);
+    launch_pose_2d2d_body(a, stream);
     (void)timing;
 }
 

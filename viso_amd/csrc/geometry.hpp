@@ -72,5 +72,12 @@ struct GeoArgs {
 };
 
 void launch_pose_2d2d(const GeoArgs& a, hipStream_t stream, Timing* timing);
+// The same in two parts: the normalisation and the gates of
+// src/viso.cpp:184, 216 (GeoCtl n / disparity / gate), then the RANSACs,
+// recoverPose / decomposition and SelectMotion.  Every kernel of the body
+// returns at once when the gate is closed; a caller that has read the gate
+// on the host may skip the body.
+void launch_pose_2d2d_gate(const GeoArgs& a, hipStream_t stream);
+void launch_pose_2d2d_body(const GeoArgs& a, hipStream_t stream);
 
 }  // namespace viso

@@ -180,11 +180,30 @@ __device__ inline LkTemplate lk_prepare(const uint8_t* __restrict__ img1, int w1
 //   cur_x/cur_y: current-image coordinate of this lane's pixel without d;
 //   bx/by: coordinate whose +d is bounds-checked (per engine); w1/h1: the
 //   size the bounds test uses.
+#ifndef VISO_LK_SHARED
+#define VISO_LK_SHARED 1
+#endif
+// One binade around v (v > 0 assumed by the callers' `>= 1` tests): v - 6
+// and v + 6 have the same exponent.
+__device__ inline bool one_binade6(double v) {
+    return (__double_as_longlong(v - 6.0) >> 52) == (__double_as_longlong(v + 6.0) >> 52);
+}
+
+// LK alignment (!KLT_BOUNDS) with (ax, ay) = the patch centre in the current
+// level (uniform; cur_x = ax + px, cur_y = ay + py per lane): when ax - 6 ..
+// ax + 6 lie in one binade (so ax + px is exact) and so do X - 6 .. X + 6
+// for X = ax + dx (so (ax + px) + dx == X + px exactly), every lane's sample
+// coordinate is X + px: its int() and floor() are floor(X) + px and its
+// fraction is exactly X - floor(X).  The wave then forms the four bilinear
+// weights once and each lane reads its four taps from the window at a fixed
+// offset -- the same products and sums as sample_px, bit for bit.  Otherwise
+// (and near the window's edge) the per-lane sample.
 template <int MAXIT, bool KLT_BOUNDS>
 __device__ inline LkResult lk_iterate(const LkTemplate& t, int w1, int h1,
                                       const uint8_t* __restrict__ img2, int w2, int h2,
                                       double cur_x, double cur_y, double bx, double by, double dx,
-                                      double dy, double thresh, const Window& win) {
+                                      double dy, double thresh, const Window& win, double ax = 0.0,
+                                      double ay = 0.0, int lane_off = 0) {
     const double hp = 4.0;
     // the control values are wave-uniform (the sums are read from one lane):
     // said so to the compiler, the loop's branches need no EXEC bookkeeping
@@ -217,7 +236,28 @@ __device__ inline LkResult lk_iterate(const LkTemplate& t, int w1, int h1,
             succ = false;
             break;
         }
-        const double e = t.I1 - sample_win<!KLT_BOUNDS>(img2, w2, h2, cur_x + dx, cur_y + dy, win);
+        double e;
+        bool shared = false;
+        if (!KLT_BOUNDS && VISO_LK_SHARED && win.lds) {
+            const double X = uniform_f64(ax + dx), Y = uniform_f64(ay + dy);
+            if (ax - 6.0 >= 1.0 && ay - 6.0 >= 1.0 && X - 6.0 >= 1.0 && Y - 6.0 >= 1.0 && one_binade6(ax) &&
+                one_binade6(ay) && one_binade6(X) && one_binade6(Y)) {
+                const double fX = floor(X), fY = floor(Y);
+                const int ix = (int)fX - win.x0, iy = (int)fY - win.y0;
+                // every lane's taps (offsets -4 .. +4) inside the window
+                if (ix - 4 >= 0 && ix + 4 < kWinW && iy - 4 >= 0 && iy + 4 < kWinH) {
+                    shared = true;
+                    const double xx = X - fX, yy = Y - fY;
+                    const double w0 = (1 - xx) * (1 - yy), w1 = xx * (1 - yy), w2 = (1 - xx) * yy, w3 = xx * yy;
+                    const int o = iy * kWinW + ix + lane_off;
+                    const double d0 = (double)ld_lds_u8(win.lds, o), d1 = (double)ld_lds_u8(win.lds, o + 1);
+                    const double d2 = (double)ld_lds_u8(win.lds, o + kWinW);
+                    const double d3 = (double)ld_lds_u8(win.lds, o + kWinW + 1);
+                    e = t.I1 - (w0 * d0 + w1 * d1 + w2 * d2 + w3 * d3);
+                }
+            }
+        }
+        if (!shared) e = t.I1 - sample_win<!KLT_BOUNDS>(img2, w2, h2, cur_x + dx, cur_y + dy, win);
         double B0, B1;
         if (KLT_BOUNDS)
             wave_tree_sum3(-t.J0 * e, -t.J1 * e, e * e, B0, B1, cost);
@@ -568,7 +608,8 @@ __global__ __launch_bounds__(256, FAST ? VISO_LK_MIN_WAVES_FAST : VISO_LK_MIN_WA
                 const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
 #endif
                 LkResult r = lk_iterate<100, false>(t, w, h, level_ptr(cur, level), w, h, cx, cy, bu * s,
-                                                    bv * s, 0.0, 0.0, a.thresh, wcur);
+                                                    bv * s, 0.0, 0.0, a.thresh, wcur, cu * s, cv * s,
+                                                    py * kWinW + px);
                 succ = r.succ;
 #ifdef VISO_PROBE
                 pr_it[level] += (unsigned long long)r.iters;
@@ -612,43 +653,46 @@ __global__ __launch_bounds__(256, FAST ? VISO_LK_MIN_WAVES_FAST : VISO_LK_MIN_WA
     }
 }
 
-// One workgroup: ballot/popcount prefix in chunks of 256 keeps the order.
-__global__ __launch_bounds__(256) void compact_tracks_kernel(const float2* __restrict__ kp1,
-                                                             const float2* __restrict__ kp2,
-                                                             const uint8_t* __restrict__ success,
-                                                             int n, float2* __restrict__ o1,
-                                                             float2* __restrict__ o2,
-                                                             int* __restrict__ n_out) {
-    __shared__ int s_wave[4];
-    __shared__ int s_base;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (threadIdx.x == 0) s_base = 0;
-    __syncthreads();
-    for (int i0 = 0; i0 < n; i0 += 256) {
-        const int i = i0 + threadIdx.x;
-        const bool keep = i < n && success[i] != 0;
-        const unsigned long long m = __ballot(keep);
-        const int before = __popcll(m & ((1ULL << lane) - 1ULL));
-        if (lane == 0) s_wave[wave] = __popcll(m);
-        __syncthreads();
-        int off = s_base;
-        for (int k = 0; k < wave; ++k) off += s_wave[k];
-        if (keep) {
-            o1[off + before] = kp1[i];
-            o2[off + before] = kp2[i];
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) s_base += (s_wave[0] + s_wave[1]) + (s_wave[2] + s_wave[3]);
-        __syncthreads();
+// One 1,024-thread workgroup: thread t owns the ceil(n / 1024) consecutive
+// tracks [t C, t C + C), counts its survivors, one block-wide exclusive scan
+// places them, and each thread copies its own in order (src/viso.cpp:23-40
+// erase, order kept).
+__global__ __launch_bounds__(1024) void compact_tracks_kernel(const float2* __restrict__ kp1,
+                                                              const float2* __restrict__ kp2,
+                                                              const uint8_t* __restrict__ success,
+                                                              int n, float2* __restrict__ o1,
+                                                              float2* __restrict__ o2,
+                                                              int* __restrict__ n_out) {
+    __shared__ int s_w[16];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int C = (n + 1023) / 1024;
+    const int lo = min(t * C, n), hi = min(lo + C, n);
+    int cnt = 0;
+    for (int i = lo; i < hi; ++i) cnt += success[i] != 0;
+    int incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int o = __shfl_up(incl, d);
+        if (lane >= d) incl += o;
     }
-    if (threadIdx.x == 0) *n_out = s_base;
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    int off = incl - cnt;
+    for (int k = 0; k < wave; ++k) off += s_w[k];
+    for (int i = lo; i < hi; ++i)
+        if (success[i]) {
+            o1[off] = kp1[i];
+            o2[off] = kp2[i];
+            ++off;
+        }
+    if (t == 1023) *n_out = off;
 }
 
 }  // namespace
 
 void launch_compact_tracks(const float2* kp1, const float2* kp2, const uint8_t* success, int n,
                            float2* kp1_out, float2* kp2_out, int* n_out, hipStream_t stream) {
-    compact_tracks_kernel<<<1, 256, 0, stream>>>(kp1, kp2, success, n, kp1_out, kp2_out, n_out);
+    compact_tracks_kernel<<<1, 1024, 0, stream>>>(kp1, kp2, success, n, kp1_out, kp2_out, n_out);
 }
 
 void launch_klt(const FrameDev& ref, const FrameDev& cur, const PyrGeom& g, const float2* kp1,
