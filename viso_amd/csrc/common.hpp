@@ -204,10 +204,6 @@ __device__ inline double wave_tree_sum_dpp(double v) {
 
 __device__ inline double dsel(bool c, double a, double b) { return c ? a : b; }
 
-#ifndef VISO_TREE3_ROR
-#define VISO_TREE3_ROR 1
-#endif
-
 // The canonical wave trees of three values at once: reduce-scatter over the
 // xor-1 / xor-2 levels (lane class (b1, b0) = (0,0) / (0,1) / (1,0) keeps a /
 // b / c, (1,1) a zero), then true xor-4 / xor-8 partners (DPP row_shr /
@@ -253,17 +249,10 @@ __device__ inline void wave_tree_sum3_desc(double a, double b, double c, double&
     const double cc = x + y;
     permlane16_swap_f64(ab, cc, x, y);
     double v = x + y;
-#if VISO_TREE3_ROR
     v = v + dpp_f64<0x128>(v);  // lane ^ 8: row_ror:8 is exactly the xor-8 partner
     // lane ^ 4: lanes l and l ^ 8 now hold the same sum, so row_ror:4 (lane
     // (l - 4) mod 16, i.e. l ^ 4 or its xor-8 twin) delivers the xor-4 partner's
     v = v + dpp_f64<0x124>(v);
-#else
-    const double r8 = dpp_f64<0x118>(v), l8 = dpp_f64<0x108>(v);  // row_shr / row_shl by 8
-    v = v + dsel(b3, r8, l8);                                        // lane ^ 8
-    const double r4 = dpp_f64<0x114>(v), l4 = dpp_f64<0x104>(v);  // row_shr / row_shl by 4
-    v = v + dsel(b2, r4, l4);                                        // lane ^ 4
-#endif
     v = v + dpp_f64<0x4E>(v);                                        // lane ^ 2
     v = v + dpp_f64<0xB1>(v);                                        // lane ^ 1
     ra = readlane_f64(v, 0);

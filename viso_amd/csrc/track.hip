@@ -180,30 +180,11 @@ __device__ inline LkTemplate lk_prepare(const uint8_t* __restrict__ img1, int w1
 //   cur_x/cur_y: current-image coordinate of this lane's pixel without d;
 //   bx/by: coordinate whose +d is bounds-checked (per engine); w1/h1: the
 //   size the bounds test uses.
-#ifndef VISO_LK_SHARED
-#define VISO_LK_SHARED 1
-#endif
-// One binade around v (v > 0 assumed by the callers' `>= 1` tests): v - 6
-// and v + 6 have the same exponent.
-__device__ inline bool one_binade6(double v) {
-    return (__double_as_longlong(v - 6.0) >> 52) == (__double_as_longlong(v + 6.0) >> 52);
-}
-
-// LK alignment (!KLT_BOUNDS) with (ax, ay) = the patch centre in the current
-// level (uniform; cur_x = ax + px, cur_y = ay + py per lane): when ax - 6 ..
-// ax + 6 lie in one binade (so ax + px is exact) and so do X - 6 .. X + 6
-// for X = ax + dx (so (ax + px) + dx == X + px exactly), every lane's sample
-// coordinate is X + px: its int() and floor() are floor(X) + px and its
-// fraction is exactly X - floor(X).  The wave then forms the four bilinear
-// weights once and each lane reads its four taps from the window at a fixed
-// offset -- the same products and sums as sample_px, bit for bit.  Otherwise
-// (and near the window's edge) the per-lane sample.
 template <int MAXIT, bool KLT_BOUNDS>
 __device__ inline LkResult lk_iterate(const LkTemplate& t, int w1, int h1,
                                       const uint8_t* __restrict__ img2, int w2, int h2,
                                       double cur_x, double cur_y, double bx, double by, double dx,
-                                      double dy, double thresh, const Window& win, double ax = 0.0,
-                                      double ay = 0.0, int lane_off = 0) {
+                                      double dy, double thresh, const Window& win) {
     const double hp = 4.0;
     // the control values are wave-uniform (the sums are read from one lane):
     // said so to the compiler, the loop's branches need no EXEC bookkeeping
@@ -236,28 +217,7 @@ __device__ inline LkResult lk_iterate(const LkTemplate& t, int w1, int h1,
             succ = false;
             break;
         }
-        double e;
-        bool shared = false;
-        if (!KLT_BOUNDS && VISO_LK_SHARED && win.lds) {
-            const double X = uniform_f64(ax + dx), Y = uniform_f64(ay + dy);
-            if (ax - 6.0 >= 1.0 && ay - 6.0 >= 1.0 && X - 6.0 >= 1.0 && Y - 6.0 >= 1.0 && one_binade6(ax) &&
-                one_binade6(ay) && one_binade6(X) && one_binade6(Y)) {
-                const double fX = floor(X), fY = floor(Y);
-                const int ix = (int)fX - win.x0, iy = (int)fY - win.y0;
-                // every lane's taps (offsets -4 .. +4) inside the window
-                if (ix - 4 >= 0 && ix + 4 < kWinW && iy - 4 >= 0 && iy + 4 < kWinH) {
-                    shared = true;
-                    const double xx = X - fX, yy = Y - fY;
-                    const double w0 = (1 - xx) * (1 - yy), w1 = xx * (1 - yy), w2 = (1 - xx) * yy, w3 = xx * yy;
-                    const int o = iy * kWinW + ix + lane_off;
-                    const double d0 = (double)ld_lds_u8(win.lds, o), d1 = (double)ld_lds_u8(win.lds, o + 1);
-                    const double d2 = (double)ld_lds_u8(win.lds, o + kWinW);
-                    const double d3 = (double)ld_lds_u8(win.lds, o + kWinW + 1);
-                    e = t.I1 - (w0 * d0 + w1 * d1 + w2 * d2 + w3 * d3);
-                }
-            }
-        }
-        if (!shared) e = t.I1 - sample_win<!KLT_BOUNDS>(img2, w2, h2, cur_x + dx, cur_y + dy, win);
+        const double e = t.I1 - sample_win<!KLT_BOUNDS>(img2, w2, h2, cur_x + dx, cur_y + dy, win);
         double B0, B1;
         if (KLT_BOUNDS)
             wave_tree_sum3(-t.J0 * e, -t.J1 * e, e * e, B0, B1, cost);
@@ -608,8 +568,7 @@ __global__ __launch_bounds__(256, FAST ? VISO_LK_MIN_WAVES_FAST : VISO_LK_MIN_WA
                 const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
 #endif
                 LkResult r = lk_iterate<100, false>(t, w, h, level_ptr(cur, level), w, h, cx, cy, bu * s,
-                                                    bv * s, 0.0, 0.0, a.thresh, wcur, cu * s, cv * s,
-                                                    py * kWinW + px);
+                                                    bv * s, 0.0, 0.0, a.thresh, wcur);
                 succ = r.succ;
 #ifdef VISO_PROBE
                 pr_it[level] += (unsigned long long)r.iters;
