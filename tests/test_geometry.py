@@ -112,6 +112,79 @@ def test_oracle_pose_2d2d_gates():
     assert out["ran"] == 0 and out["stats"][3] == 0
 
 
+# ------------------------------------------------------------------ CPU: the device RANSAC scan
+_DBL_MIN = 2.2250738585072014e-308
+
+
+def _update_num_iters(p, ep, mp, max_iters):
+    """cv::RANSACUpdateNumIters as oracle_geom.cpp ransac_update_num_iters."""
+    import math
+    p = min(max(p, 0.0), 1.0)
+    ep = min(max(ep, 0.0), 1.0)
+    num = max(1.0 - p, _DBL_MIN)
+    den = 1.0 - math.pow(1.0 - ep, mp)
+    if den < _DBL_MIN:
+        return 0
+    num, den = math.log(num), math.log(den)
+    return max_iters if (den >= 0 or -num >= max_iters * (-den)) else int(round(num / den))
+
+
+def _scan_sequential(counts, n, mp, max_iters, conf):
+    niters, max_good, best, h = max_iters, 0, -1, 0
+    while h < niters:
+        c = counts[h]
+        if c >= 0 and c > max(max_good, mp - 1):
+            max_good, best = c, h
+            niters = _update_num_iters(conf, (n - c) / n, mp, niters)
+        h += 1
+    return best, max_good, h
+
+
+def _scan_records(counts, n, mp, max_iters, conf):
+    """scan_kernel's form (geometry.hip): only the strict prefix-maximum
+    records can change the loop state, and niters only shrinks, so the loop
+    is the in-order walk over the records until one lies at or past niters;
+    the loop variable at exit is max(niters, last record + 1)."""
+    import math
+    ln_num = math.log(max(1.0 - min(max(conf, 0.0), 1.0), _DBL_MIN))
+    run, recs = mp - 1, []
+    for h in range(max_iters):
+        if counts[h] > run:
+            run = counts[h]
+            recs.append(h)
+    niters, best, max_good, last = max_iters, -1, 0, -1
+    for h in recs:
+        if h >= niters:
+            break
+        best, max_good, last = h, counts[h], h
+        ep = min(max((n - counts[h]) / n, 0.0), 1.0)
+        den = 1.0 - math.pow(1.0 - ep, mp)
+        if den < _DBL_MIN:
+            niters = 0
+            continue
+        ld = math.log(den)
+        if not (ld >= 0 or -ln_num >= niters * (-ld)):
+            niters = int(round(ln_num / ld))
+    return best, max_good, max(niters, last + 1)
+
+
+def test_ransac_scan_record_walk_is_the_sequential_loop():
+    rng = np.random.default_rng(1)
+    for trial in range(4000):
+        n = int(rng.integers(10, 3000))
+        mp = int(rng.choice([4, 8]))
+        max_iters = int(rng.choice([7, 50, 1000, 2000]))
+        mode = trial % 3
+        if mode == 0:
+            counts = rng.integers(-1, n + 1, max_iters)
+        elif mode == 1:
+            counts = np.minimum(np.sort(rng.integers(-1, n + 1, max_iters)), n)
+        else:
+            counts = (rng.random(max_iters) * n * rng.random()).astype(int)
+        counts = [int(c) for c in counts]
+        assert _scan_sequential(counts, n, mp, max_iters, 0.99) == _scan_records(counts, n, mp, max_iters, 0.99)
+
+
 # ------------------------------------------------------------------ GPU parity
 def _check_same(got, exp):
     st_g, st_e = got["stats"], exp["stats"]

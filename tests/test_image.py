@@ -13,6 +13,66 @@ from tests import images, oracle_lib
 SIZES = [(375, 1242), (61, 97), (17, 33), (120, 160), (187, 621), (46, 155), (16, 16)]
 
 
+# ------------------------------------------------------------------ CPU: the device FAST formulation
+_DX = [0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1]
+_DY = [3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3]
+
+
+def _rot16(m, s):
+    return ((m >> s) | (m << (16 - s))) & 0xFFFF
+
+
+def _run9(m):
+    a1 = m & _rot16(m, 1)
+    a2 = a1 & _rot16(a1, 2)
+    a3 = a2 & _rot16(a2, 4)
+    return a3 & _rot16(m, 8)
+
+
+@pytest.mark.parametrize("thresh", [0, 20, 50, 255])
+def test_fast_packed_arc_test_matches_oracle_score_map(thresh):
+    """fast_tile_kernel's corner test, restated in numpy with its 16-bit
+    wrapping arithmetic (image.hip): per circle position k the sign bits of
+    (v + t) - C_k and C_k - (v - t) shifted into two 16-bit masks, and a run of
+    >= 9 contiguous set bits found by rotate-and-AND (runs of 2, 4, 8, then 9);
+    the corners' cornerScore (min / max arcs) then reproduces the oracle's
+    score map exactly (OpenCV's scan over 25 circle samples with its
+    early-outs is the same predicate)."""
+    img = images.mixed(120, 300, seed=3).astype(np.int64)
+    h, w = img.shape
+    v = img[3:h - 3, 3:w - 3]
+    vb, vd = (v + thresh) & 0xFFFF, (v - thresh) & 0xFFFF
+    mb = np.zeros_like(v)
+    md = np.zeros_like(v)
+    circ = [img[3 + _DY[k]:h - 3 + _DY[k], 3 + _DX[k]:w - 3 + _DX[k]] for k in range(16)]
+    for k in range(16):
+        mb = (mb >> 1) | (((vb - circ[k]) & 0xFFFF) & 0x8000)
+        md = (md >> 1) | (((circ[k] - vd) & 0xFFFF) & 0x8000)
+    corner = (_run9(mb) | _run9(md)) != 0
+    dd = [v - c for c in circ]
+    a0 = np.full(v.shape, thresh)
+    for k in range(0, 16, 2):
+        a = np.minimum(dd[(k + 1) % 16], dd[(k + 2) % 16])
+        for j in range(3, 9):
+            a = np.minimum(a, dd[(k + j) % 16])
+        a0 = np.maximum(a0, np.minimum(a, dd[k]))
+        a0 = np.maximum(a0, np.minimum(a, dd[(k + 9) % 16]))
+    b0 = -a0
+    for k in range(0, 16, 2):
+        b = np.maximum(dd[(k + 1) % 16], dd[(k + 2) % 16])
+        for j in range(3, 9):
+            b = np.maximum(b, dd[(k + j) % 16])
+        b0 = np.minimum(b0, np.maximum(b, dd[k]))
+        b0 = np.minimum(b0, np.maximum(b, dd[(k + 9) % 16]))
+    score = np.where(corner, -b0 - 1, 0).astype(np.uint8)
+    lib = oracle_lib.load()
+    smap = np.zeros(h * w, np.uint8)
+    im8 = np.ascontiguousarray(img.astype(np.uint8))
+    lib.oracle_fast_score_map(im8.ctypes.data, w, h, thresh, smap.ctypes.data)
+    exp = smap.reshape(h, w)[3:h - 3, 3:w - 3]
+    assert np.array_equal(score, exp)
+
+
 # ------------------------------------------------------------------ CPU: oracle pinning
 @pytest.mark.parametrize("h,w", SIZES)
 def test_oracle_pyramid_vs_numpy(h, w):
