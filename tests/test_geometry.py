@@ -185,6 +185,61 @@ def test_ransac_scan_record_walk_is_the_sequential_loop():
         assert _scan_sequential(counts, n, mp, max_iters, 0.99) == _scan_records(counts, n, mp, max_iters, 0.99)
 
 
+def _pairwise(x):
+    """The canonical pairwise tree over a power-of-two count of leaves."""
+    x = list(x)
+    while len(x) > 1:
+        x = [x[2 * i] + x[2 * i + 1] for i in range(len(x) // 2)]
+    return x[0]
+
+
+def _normalize_kernel_sum(leaves, threads=1024):
+    """normalize_kernel's disparity sum (geometry.hip): P = next pow2 >= n,
+    thread t owns C = max(1, P / 1024) consecutive leaves folded by a
+    binary-counter stack, the ascending-xor wave tree over 64 threads, then
+    the pairwise top over the 16 waves; +0.0 leaves past n."""
+    n = len(leaves)
+    P = 1
+    while P < n:
+        P <<= 1
+    C = P // threads if P > threads else 1
+    per_thread = []
+    for t in range(threads):
+        stack = []
+        for j in range(C):
+            i = t * C + j
+            x = leaves[i] if i < n else 0.0
+            k = j
+            while k & 1:
+                x = stack.pop() + x
+                k >>= 1
+            stack.append(x)
+        per_thread.append(stack[0])
+    waves = []
+    for w in range(threads // 64):
+        v = per_thread[64 * w:64 * w + 64]
+        off = 1
+        while off < 64:  # ascending xor butterfly: every lane ends with the tree sum
+            v = [v[i] + v[i ^ off] for i in range(64)]
+            off <<= 1
+        waves.append(v[0])
+    return _pairwise(waves)
+
+
+@pytest.mark.parametrize("n", [1, 10, 255, 256, 700, 1024, 1025, 5000, 8192, 32768])
+def test_normalize_disparity_tree_is_the_canonical_tree(n):
+    """The 1,024-thread normalisation sums the same pairwise tree over the P
+    padded leaves as the oracle's tree_sum (sums of squares: adding +0.0
+    leaves and subtrees is exact), so the disparity gate decides alike."""
+    rng = np.random.default_rng(n)
+    leaves = list(rng.random(n) ** 3 * 1e-3)
+    P = 1
+    while P < n:
+        P <<= 1
+    exp = _pairwise(leaves + [0.0] * (P - n))
+    assert _normalize_kernel_sum(leaves) == exp
+
+
 # ------------------------------------------------------------------ GPU parity
 def _check_same(got, exp):
     st_g, st_e = got["stats"], exp["stats"]
