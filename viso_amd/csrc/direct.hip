@@ -1276,8 +1276,22 @@ __device__ inline void rig_fold(const RigArgs& ra, const double (*con)[kSums], c
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
+// bytes of one camera's scratch (rig_scratch_bytes): tile partials
+// [kLevels][28][256] f64, then nGood counts [kLevels][256]
+constexpr size_t kRigPartBytes = (size_t)kLevels * kRigTiles * kSums * 8;
+constexpr size_t kRigScratchBytes = kRigPartBytes + (size_t)kLevels * kRigTiles * 4;
+
+// The leading arguments repeat what the reduce waves' first loads need, so
+// they arrive in SGPRs at wave launch (-amdgpu-kernarg-preload-count; the
+// direct pose's prologue does the same): every camera's scratch and Ad(E_c)
+// at fixed strides from two bases, pre_hdr = (level + 1) | n_cams << 8 |
+// 1 << 16 when the cameras' scratch / Ad are laid out that way (rig.cpp;
+// else the by-value arguments are read), and the cameras' tile counts in
+// 16-bit halves of pre_t01 / pre_t23.
 template <bool FAST, bool MERGED>
-__global__ __launch_bounds__(kRigThreads) void rig_level_kernel(RigArgs ra) {
+__global__ __launch_bounds__(kRigThreads) void rig_level_kernel(const char* __restrict__ pre_scratch,
+                                                                const double* __restrict__ pre_ad, int pre_hdr,
+                                                                int pre_t01, int pre_t23, RigArgs ra) {
     __shared__ SolveLds L;
     __shared__ double s_red[kMaxRigCams][4][kSums];
     __shared__ int s_g[kMaxRigCams][4];
@@ -1306,19 +1320,35 @@ __global__ __launch_bounds__(kRigThreads) void rig_level_kernel(RigArgs ra) {
     // the kernel arguments this wave's loads need, read unconditionally
     // (cam[rc] exists for every rc < kMaxRigCams) so the scalar loads issue
     // together: one argument round trip before the partial loads
-    const int rc_tiles = ra.cam[rc].d.n_tiles;
-    const double* rc_part = ra.cam[rc].d.s.part;
-    const int* rc_good = ra.cam[rc].d.s.good;
-    const double* rc_ad = ra.cam[rc].Ad;
-    int lv_arg = ra.level;
-    // (the empty asm takes every argument at once and hands the level on:
-    // nothing derived from it is scheduled between the scalar loads)
-    asm volatile("" : "+s"(lv_arg) : "s"(rc_tiles), "s"(rc_part), "s"(rc_good), "s"(rc_ad));
+    int rc_tiles, n_cams, lv_arg;
+    const double* rc_part;
+    const int* rc_good;
+    const double* rc_ad;
+    if (pre_hdr & (1 << 16)) {
+        // preloaded: no kernel-argument load in front of the partial loads
+        lv_arg = (pre_hdr & 0xff) - 1;
+        n_cams = (pre_hdr >> 8) & 0xff;
+        rc_tiles = ((rc < 2 ? pre_t01 : pre_t23) >> (16 * (rc & 1))) & 0xffff;
+        const char* sc = pre_scratch + (size_t)rc * kRigScratchBytes;
+        rc_part = (const double*)sc;
+        rc_good = (const int*)(sc + kRigPartBytes);
+        rc_ad = pre_ad + 36 * rc;
+    } else {
+        rc_tiles = ra.cam[rc].d.n_tiles;
+        rc_part = ra.cam[rc].d.s.part;
+        rc_good = ra.cam[rc].d.s.good;
+        rc_ad = ra.cam[rc].Ad;
+        n_cams = ra.n_cams;
+        lv_arg = ra.level;
+        // (the empty asm takes every argument at once and hands the level on:
+        // nothing derived from it is scheduled between the scalar loads)
+        asm volatile("" : "+s"(lv_arg) : "s"(rc_tiles), "s"(rc_part), "s"(rc_good), "s"(rc_ad));
+    }
     const int lv = lv_arg;
     const bool merged = MERGED;  // launched for L(3) only
     const bool solve = lv < kLevels - 1 || merged;  // an unmerged L(3) is seeded
     const int sl = merged ? 0 : lv + 1;              // level solved in the prologue (F: 0)
-    const int q_rc = rc < ra.n_cams ? rig_reduce_waves(rc_tiles) : 0;
+    const int q_rc = rc < n_cams ? rig_reduce_waves(rc_tiles) : 0;
     const bool rwave = solve && rq < q_rc;
     double v[kSums];
     int gg = 0;
@@ -1647,7 +1677,7 @@ static int rig_tiling(int n, int T, bool split, int* tile, int* n_tiles) {
     return (*tile <= kMaxTile && *n_tiles <= kRigTiles) ? 0 : -1;
 }
 
-size_t rig_scratch_bytes() { return (size_t)kLevels * kRigTiles * kSums * 8 + (size_t)kLevels * kRigTiles * 4; }
+size_t rig_scratch_bytes() { return kRigScratchBytes; }
 
 int launch_rig_direct(const RigCamDev* cams, int n_cams, const PyrGeom& g, const double K[4], double* state,
                       const double* seed12, double* stats, double* pose_out, double* log, int log_index,
@@ -1692,6 +1722,19 @@ int launch_rig_direct(const RigCamDev* cams, int n_cams, const PyrGeom& g, const
     ra.cam_last = cam_last;
     ra.prev_log_index = -1;
     const int grid = off > 0 ? off : 1;
+    // the preloaded prologue arguments (rig_level_kernel): valid when every
+    // camera's scratch and Ad(E_c) sit at fixed strides from camera 0's
+#ifndef VISO_RIG_PRELOAD
+#define VISO_RIG_PRELOAD 1
+#endif
+    bool pre_ok = VISO_RIG_PRELOAD != 0;
+    int tl[kMaxRigCams] = {0, 0, 0, 0};
+    for (int c = 0; c < n_cams; ++c) {
+        pre_ok = pre_ok && (const char*)cams[c].scratch == (const char*)cams[0].scratch + kRigScratchBytes * c &&
+                 cams[c].Ad == cams[0].Ad + 36 * c;
+        tl[c] = ra.cam[c].d.n_tiles;
+    }
+    const int t01 = (tl[0] & 0xffff) | (tl[1] << 16), t23 = (tl[2] & 0xffff) | (tl[3] << 16);
     for (int level = levels ? kLevels - 1 : -1; level >= -1; --level) {
         ra.level = level;
 #ifdef VISO_PROBE
@@ -1714,15 +1757,18 @@ int launch_rig_direct(const RigCamDev* cams, int n_cams, const PyrGeom& g, const
             ra.log_index = log ? log_index : -1;
         }
         const int gl = level < 0 ? 1 : grid;
+        const int hdr = ((level + 1) & 0xff) | (n_cams << 8) | (pre_ok ? 1 << 16 : 0);
+        const char* psc = (const char*)cams[0].scratch;
+        const double* pad = cams[0].Ad;
         if (ra.merged) {
             if (fast)
-                rig_level_kernel<true, true><<<gl, kRigThreads, 0, stream>>>(ra);
+                rig_level_kernel<true, true><<<gl, kRigThreads, 0, stream>>>(psc, pad, hdr, t01, t23, ra);
             else
-                rig_level_kernel<false, true><<<gl, kRigThreads, 0, stream>>>(ra);
+                rig_level_kernel<false, true><<<gl, kRigThreads, 0, stream>>>(psc, pad, hdr, t01, t23, ra);
         } else if (fast) {
-            rig_level_kernel<true, false><<<gl, kRigThreads, 0, stream>>>(ra);
+            rig_level_kernel<true, false><<<gl, kRigThreads, 0, stream>>>(psc, pad, hdr, t01, t23, ra);
         } else {
-            rig_level_kernel<false, false><<<gl, kRigThreads, 0, stream>>>(ra);
+            rig_level_kernel<false, false><<<gl, kRigThreads, 0, stream>>>(psc, pad, hdr, t01, t23, ra);
         }
     }
     return 0;
