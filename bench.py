@@ -874,13 +874,16 @@ def pyramid_traffic(W, H, imgs_per_launch):
 
 def pmc_evidence(W, H, breakdown, stereo_vo, n_map=None):
     """The north star's two other rocprof figures, from the committed PMC passes
-    (tools/gpu_pmc.sh -> tools/pmc_kernels.py -> profiles/r03_gn_svo_pmc.json),
+    (tools/gpu_pmc.sh -> tools/pmc_kernels.py -> profiles/r0N_gn_svo_pmc.json),
     profiled at 1242x375 only: occupancy of the GN reduction (direct_level_kernel)
     and HBM traffic of the matching pass (svo_circle_kernel).  Live durations
     come from this run's HIP events where the bench has them."""
-    f = os.path.join(ROOT, "profiles", "r03_gn_svo_pmc.json")
-    if (W, H) != (1242, 375) or not os.path.exists(f):
+    # the newest committed pass (round 4 refresh, else round 3's)
+    rel = next((r for r in ("profiles/r04_gn_svo_pmc.json", "profiles/r03_gn_svo_pmc.json")
+                if os.path.exists(os.path.join(ROOT, r))), None)
+    if (W, H) != (1242, 375) or rel is None:
         return None, None
+    f = os.path.join(ROOT, rel)
     with open(f) as fh:
         t = json.load(fh)
     gn = None
@@ -913,8 +916,7 @@ def pmc_evidence(W, H, breakdown, stereo_vo, n_map=None):
               "fp64_flop_per_launch_algorithmic_basis": f"{n_pts} map points x 64 px x 154 flop",
               "fp64_tflops_algorithmic": round(flop / (live_us * 1e-6) / 1e12, 2) if flop else None,
               "fp64_peak_tflops": d.get("fp64_peak_tflops"),
-              "source": "profiles/r03_gn_svo_pmc.json (SQ_WAVES, SQ_WAVE_CYCLES, SQ_ACTIVE_INST_VALU, "
-                        "SQ_INSTS_VALU_*_F64)"}
+              "source": f"{rel} (SQ_WAVES, SQ_WAVE_CYCLES, SQ_ACTIVE_INST_VALU, SQ_INSTS_VALU_*_F64)"}
     mp = None
     c = t.get("svo", {}).get("svo_circle_kernel")
     if c and c.get("traffic_bytes"):
@@ -925,13 +927,13 @@ def pmc_evidence(W, H, breakdown, stereo_vo, n_map=None):
               "achieved_GBps": round(gbs, 1), "peak_GBps": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4),
               "bound": "latency / VALU (four dependent best-SAD searches per feature over a cache-resident "
                        "descriptor set), not HBM",
-              "source": "profiles/r03_gn_svo_pmc.json (FETCH_SIZE x2 + WRITE_SIZE)"}
+              "source": f"{rel} (FETCH_SIZE x2 + WRITE_SIZE)"}
         if c.get("valu_busy") is not None:
             mp.update({"valu_busy": c["valu_busy"], "valu_insts": c["valu_insts"],
                        "valu_insts_per_us": c["valu_insts_per_us"],
                        "mean_resident_waves_per_cu": c["mean_resident_waves_per_cu"],
-                       "sq_source": "profiles/r03_gn_svo_pmc.json (SQ_INSTS_VALU, SQ_ACTIVE_INST_VALU in "
-                                    "quad-cycles, SQ_WAVE_CYCLES; separate rocprofv3 pass)"})
+                       "sq_source": f"{rel} (SQ_INSTS_VALU, SQ_ACTIVE_INST_VALU in quad-cycles, "
+                                    "SQ_WAVE_CYCLES; separate rocprofv3 pass)"})
     return gn, mp
 
 
