@@ -240,6 +240,25 @@ struct viso_ctx {
     int resolve_direct();
     // end of an ingest call: pending final solve, then the LK batch on `s`
     int finish_call(hipStream_t s);
+    // LK alignment of a device-ingest chunk in the background of its
+    // direct-pose chain (track.hip lk_item_kernel): bg_begin after the chunk's
+    // pyramid when the context is tracking (frames of the chunk: their slots),
+    // bg_end once the chunk's last pose is launched
+    int bg_begin(const std::vector<int>& chunk);
+    int bg_end();
+    bool bg_active = false;
+    int bg_mode = -1;        // VISO_LK_BG: 0 off, 1 on (read once; -1 unread)
+    int bg_nb = 0;           // frames of the chunk
+    int bg_cur = -1;         // chunk index of the frame on_new_frame is processing
+    int dpend_bg = -1;       // chunk index of the pending final solve's frame
+    int n_cu = 0;            // compute units (one background workgroup each)
+    std::vector<int> bg_slots;  // tracking frames held until the kernel is done
+    viso::DevBuf bg_buf;        // ready flags [kLkBatch], next item, error
+    hipEvent_t bg_done = nullptr;
+    viso::LkAlignArgs bg_args{};  // the chunk's launch (the drain reuses it)
+    int* bg_ready(int idx) const {
+        return (bg_active && idx >= 0) ? (int*)bg_buf.ptr + idx : nullptr;
+    }
     // LKAlignment arguments common to the template and alignment launches
     viso::LkAlignArgs lk_args();
 };

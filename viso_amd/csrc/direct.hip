@@ -101,6 +101,11 @@ inline int map_tile(int n, int groups) {
 }
 constexpr int kStats = 50;
 constexpr int kStateStride = 8;
+// wave priority of the direct pose outside the solve (the solver runs at 3);
+// dev: raised above a co-resident background grid's 0
+#ifndef VISO_DIRECT_PRIO
+#define VISO_DIRECT_PRIO 0
+#endif
 
 // The two frames of one DirectPoseEstimation call and the `last` pose the
 // patches are taken at (Keyframe::Project of last_frame, src/viso.cpp:697).
@@ -149,7 +154,24 @@ struct DirectArgs {
     double* prev_pose_out;
     double* prev_log;
     int prev_log_index;
+    // background LK alignment (track.hip lk_item_kernel): raised (agent scope)
+    // once the frame pose (pose_out / prev_pose_out) is stored; may be null
+    int* ready;
+    int* prev_ready;
 };
+
+// The frame pose of a direct-pose launch: 12 agent-scope (sc1) stores by one
+// lane, then, when a background LK alignment waits for it, that lane's
+// vmcnt(0) and the frame's ready flag (MI355X_MICROARCH.md, first row of the
+// sc1 hand-off table).  The plain-launch readers see it either way.
+__device__ inline void store_frame_pose(double* dst, const double* pose, int* ready) {
+#pragma unroll
+    for (int k = 0; k < 12; ++k) __hip_atomic_store(dst + k, pose[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (ready) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
 
 // The map points of workgroup (tile) b: [*first, *first + *cnt).
 __device__ inline void tile_range(const DirectArgs& a, int b, int* first, int* cnt) {
@@ -904,8 +926,7 @@ __device__ inline void after_solve(const DirectArgs& a, bool merged, SolveLds& L
         state_to_pose(L.state, s_last);
         if (blockIdx.x == 0) {
             for (int k = 0; k < 7; ++k) a.s.state[kLevels * kStateStride + k] = L.state[k];
-            if (a.prev_pose_out)
-                for (int k = 0; k < 12; ++k) a.prev_pose_out[k] = s_last[k];
+            if (a.prev_pose_out) store_frame_pose(a.prev_pose_out, s_last, a.prev_ready);
             if (a.prev_log && a.prev_log_index >= 0)
                 for (int k = 0; k < 12; ++k) a.prev_log[12 * (size_t)a.prev_log_index + k] = s_last[k];
         }
@@ -934,10 +955,17 @@ __device__ inline void after_solve(const DirectArgs& a, bool merged, SolveLds& L
 // SGPRs at wave launch (-amdgpu-kernarg-preload-count, viso_amd/build.py), so
 // the partial loads issue without waiting for a kernel-argument load.
 template <bool FAST>
+// (dev: VISO_DIRECT_MINW caps the registers of a narrower workgroup so a
+// background workgroup can share the CU; tools/ubench/bg_filler.hip)
+#ifdef VISO_DIRECT_MINW
+__global__ __launch_bounds__(kThreads, VISO_DIRECT_MINW) void direct_level_kernel(const double* __restrict__ pre_part,
+#else
 __global__ __launch_bounds__(kThreads) void direct_level_kernel(const double* __restrict__ pre_part,
+#endif
                                                                  const int* __restrict__ pre_good, int pre_hdr,
                                                                  DirectArgs a) {
     PROBE_DECL();
+    if (VISO_DIRECT_PRIO) __builtin_amdgcn_s_setprio(VISO_DIRECT_PRIO);
     __shared__ SolveLds L;
     __shared__ double s_pose[12];
     __shared__ double s_last[12];  // merged L(3): this frame's `last` pose
@@ -1058,7 +1086,7 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(const double* __
             solve_wave0(L, 0, stp);
 #endif
         PST(7);
-        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_setprio(VISO_DIRECT_PRIO);
     }
     if (!solve && wave == 0 && lane == 0) {
         // seeded level: no solve, T21 is the seed (thread 256 wrote it)
@@ -1094,7 +1122,7 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(const double* __
     if (blockIdx.x == 0 && t == 0 && !merged) {
         for (int k = 0; k < 7; ++k) a.s.state[out * kStateStride + k] = L.state[k];
         if (lv < 0 && a.pose_out) {
-            for (int k = 0; k < 12; ++k) a.pose_out[k] = s_pose[k];
+            store_frame_pose(a.pose_out, s_pose, a.ready);
             if (a.log && a.log_index >= 0)
                 for (int k = 0; k < 12; ++k) a.log[12 * (size_t)a.log_index + k] = s_pose[k];
         }
@@ -1612,6 +1640,8 @@ DirectArgs direct_args(const FrameDev& last_pyr, const FrameDev& cur_pyr, const 
 }
 }  // namespace
 
+bool direct_fits_background() { return kThreads <= 768; }
+
 void launch_direct_levels(const FrameDev& last_pyr, const FrameDev& cur_pyr, const PyrGeom& g,
                           const double K[4], const double* points, int n,
                           const double* pose_last12, const double* pose_seed12,
@@ -1627,6 +1657,7 @@ void launch_direct_levels(const FrameDev& last_pyr, const FrameDev& cur_pyr, con
         a.prev_pose_out = merge->pose_out;
         a.prev_log = merge->log;
         a.prev_log_index = merge->log ? merge->log_index : -1;
+        a.prev_ready = merge->ready;
     }
     const int grid = a.n_tiles > 0 ? a.n_tiles : 1;
     for (int level = kLevels - 1; level >= 0; --level) {
@@ -1649,10 +1680,12 @@ void launch_direct_levels(const FrameDev& last_pyr, const FrameDev& cur_pyr, con
 void launch_direct_final(const FrameDev& last_pyr, const FrameDev& cur_pyr, const PyrGeom& g,
                          const double K[4], const double* points, int n,
                          const double* pose_last12, const DirectScratch& s, double* stats,
-                         double* pose_out, double* log, int log_index, hipStream_t stream, int precision) {
+                         double* pose_out, double* log, int log_index, hipStream_t stream, int precision,
+                         int* ready) {
     DirectArgs a = direct_args(last_pyr, cur_pyr, g, K, points, n, pose_last12, pose_last12, s,
                                stats, precision == VISO_PRECISION_FAST);
     a.pose_out = pose_out;
+    a.ready = ready;
     a.log = log;
     a.log_index = log ? log_index : -1;
     a.level = -1;

@@ -163,12 +163,14 @@ void viso_ctx::release() {
         if (e) (void)hipEventDestroy(e);
         e = nullptr;
     }
+    if (bg_done) (void)hipEventDestroy(bg_done);
+    bg_done = nullptr;
     if (lk_stream) (void)hipStreamDestroy(lk_stream);
     lk_stream = nullptr;
     DevBuf* bufs[] = {&scratch_a, &scratch_b, &scratch_c, &scratch_d, &slot_pool, &slot_pose,
                       &kp1, &kp2, &kp1b, &kp2b, &track_success, &n_track_dev, &fast_rows,
                       &geo_buf, &map_pts, &kf_poses, &direct_buf, &direct_stats,
-                      &lk_pair, &lk_succ, &lk_before, &lk_after, &lk_tmpl, &lk_tmpl_h,
+                      &bg_buf, &lk_pair, &lk_succ, &lk_before, &lk_after, &lk_tmpl, &lk_tmpl_h,
                       &lk_tmpl_kf, &lk_tmpl_uv, &pose_log};
     for (DevBuf* b : bufs) b->release();
     if (h_ctl) (void)hipHostFree(h_ctl);
@@ -327,7 +329,7 @@ int viso_ctx::resolve_direct() {
     launch_direct_final(frame(dpend_last), frame(dpend_cur), geom, K, (const double*)map_pts.ptr,
                         n_map, pose_of(dpend_last), direct, (double*)direct_stats.ptr,
                         pose_of(dpend_cur), dpend_log >= 0 ? (double*)pose_log.ptr : nullptr,
-                        dpend_log, stream, p.precision);
+                        dpend_log, stream, p.precision, bg_ready(dpend_bg));
     VISO_HIP_CHECK(hipGetLastError());
     drop(dpend_cur);
     drop(dpend_last);
@@ -338,7 +340,87 @@ int viso_ctx::resolve_direct() {
 int viso_ctx::finish_call(hipStream_t ls) {
     int rc = resolve_direct();
     if (rc) return rc;
+    if (bg_active) {
+        rc = bg_end();
+        if (rc) return rc;
+    }
     return flush_lk(ls);
+}
+
+// Background LK alignment: eligible when the context is
+// tracking at the chunk's start with a map and its LK templates, no keyframe
+// insertion can change the map mid-chunk, and the direct pose's workgroup
+// leaves a CU room for the background one (direct_fits_background).  Every
+// frame of such a chunk is a tracking frame, so every ready flag is raised:
+// frame f's by frame f+1's merged level-3 launch, the last by the final solve.
+int viso_ctx::bg_begin(const std::vector<int>& chunk) {
+    if (bg_mode < 0) {
+        const char* e = getenv("VISO_LK_BG");
+        bg_mode = (e && e[0] == '0') ? 0 : 1;
+    }
+    const int nb = (int)chunk.size();
+    if (!bg_mode || !direct_fits_background() || state != VISO_STATE_RUNNING || n_map <= 0 || !lk_tmpl.ptr ||
+        nb < 1 || nb > kLkBatch || kf_interval > 0 || dpend || !lk_pending.empty())
+        return VISO_OK;
+    if (!n_cu) {
+        VISO_HIP_CHECK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
+        VISO_HIP_CHECK(hipEventCreateWithFlags(&bg_done, hipEventDisableTiming));
+    }
+    int rc = bg_buf.ensure(sizeof(int) * (kLkBatch + 64));
+    if (rc) return rc;
+    LkAlignArgs a = lk_args();
+    a.n_frames = nb;
+    for (int f = 0; f < nb; ++f) {
+        a.frames[f].cur = frame(chunk[(size_t)f]);
+        a.frames[f].pose = pose_of(chunk[(size_t)f]);
+    }
+    a.out_stride = kMaxMapPoints;
+    a.pair_kf = (int32_t*)lk_pair.ptr;
+    a.success = (uint8_t*)lk_succ.ptr;
+    a.uv_before = (double*)lk_before.ptr;
+    a.uv_after = (double*)lk_after.ptr;
+    a.bg_ready = (int*)bg_buf.ptr;
+    a.bg_next = a.bg_ready + kLkBatch;
+    a.bg_err = a.bg_ready + kLkBatch + 1;
+    a.bg_items = nb * n_map;
+    // flags and counter cleared behind the chunk's pyramid; the kernel starts
+    // after both (the frames' pyramids are its input)
+    VISO_HIP_CHECK(hipMemsetAsync(bg_buf.ptr, 0, sizeof(int) * (kLkBatch + 64), stream));
+    VISO_HIP_CHECK(hipEventRecord(bg_done, stream));
+    VISO_HIP_CHECK(hipStreamWaitEvent(lk_stream, bg_done, 0));
+    {
+        TimedRegion t(timing, VISO_KERNEL_LKALIGN, lk_stream);
+        launch_lk_bg(a, n_cu, lk_stream);
+    }
+    VISO_HIP_CHECK(hipGetLastError());
+    VISO_HIP_CHECK(hipEventRecord(bg_done, lk_stream));
+    bg_args = a;
+    bg_active = true;
+    bg_nb = nb;
+    bg_slots.clear();
+    return VISO_OK;
+}
+
+// The chunk's last pose is launched: the items the resident grid has not
+// taken run on the rest of the chip (the drain, behind the final solve on the
+// context stream), then the context stream waits for the resident grid (its
+// outputs, the held frames), which is the latest LK batch of the flush_lk
+// bookkeeping.
+int viso_ctx::bg_end() {
+    launch_lk_drain(bg_args, 3 * n_cu, stream);
+    VISO_HIP_CHECK(hipGetLastError());
+    VISO_HIP_CHECK(hipStreamWaitEvent(stream, bg_done, 0));
+    lk_last_rows = bg_nb;
+    lk_last_pts = n_map;
+    VISO_HIP_CHECK(hipEventRecord(lk_ring[lk_seq % kLkRing], lk_stream));
+    for (int s : bg_slots) slots[(size_t)s].lk_use = lk_seq;
+    for (int s : kf_slots) slots[(size_t)s].lk_use = lk_seq;
+    ++lk_seq;
+    for (int s : bg_slots) drop(s);
+    bg_slots.clear();
+    bg_active = false;
+    dpend_bg = -1;
+    return VISO_OK;
 }
 
 int viso_ctx::build_lk_templates() {
@@ -630,6 +712,7 @@ int viso_ctx::on_new_frame(int cur) {
                     m.pose_out = pose_of(dpend_cur);
                     m.log = dpend_log >= 0 ? (double*)pose_log.ptr : nullptr;
                     m.log_index = dpend_log;
+                    m.ready = bg_ready(dpend_bg);
                 }
                 launch_direct_levels(frame(last_slot), frame(cur), g, K, (const double*)map_pts.ptr,
                                      n_map, pose_of(last_slot), pose_of(last_slot), direct,
@@ -645,14 +728,20 @@ int viso_ctx::on_new_frame(int cur) {
             hold(cur);
             hold(last_slot);
             dpend_log = log ? n_poses : -1;
+            dpend_bg = bg_active ? bg_cur : -1;
             if (log) ++n_poses;
-            // LKAlignment (src/viso.cpp:121, 768-843): queued for the batched
-            // launch at the end of this ingest call
+            // LKAlignment (src/viso.cpp:121, 768-843): run by the chunk's
+            // background kernel, or queued for the batched launch at the end
+            // of this ingest call
             hold(cur);
-            lk_pending.push_back(cur);
-            if ((int)lk_pending.size() == kLkBatch) {
-                int rc = finish_call(stream);
-                if (rc) return rc;
+            if (bg_active) {
+                bg_slots.push_back(cur);
+            } else {
+                lk_pending.push_back(cur);
+                if ((int)lk_pending.size() == kLkBatch) {
+                    int rc = finish_call(stream);
+                    if (rc) return rc;
+                }
             }
             ran_tracking = true;
             // stereo keyframe insertion (oracle_viso.cpp): every
@@ -775,6 +864,13 @@ int viso_process_frames_device(viso_ctx* c, const uint8_t* d_left, const uint8_t
             launch_pyramid_frames(c->geom, l0.data(), dst.data(), (int)l0.size(), c->stream);
         }
         VISO_HIP_CHECK(hipGetLastError());
+        {
+            const int rc = c->bg_begin(sl);
+            if (rc) {
+                for (int s : sl) c->drop(s);
+                return rc;
+            }
+        }
         // end of the chunk, also on an error: launch what still reads the
         // chunk's borrowed frames (the pending final solve, the LK batch),
         // give retained frames their own level 0, release the chunk's holds
@@ -795,6 +891,7 @@ int viso_process_frames_device(viso_ctx* c, const uint8_t* d_left, const uint8_t
         };
         for (int i = 0; i < nb; ++i) {
             c->right_l0 = d_right ? d_right + frame_stride * (size_t)(f0 + i) : nullptr;
+            c->bg_cur = i;
             const int rc = c->on_new_frame(sl[(size_t)i]);
             c->right_l0 = nullptr;
             if (rc) return end_chunk(rc);

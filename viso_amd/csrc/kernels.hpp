@@ -76,8 +76,20 @@ struct LkAlignArgs {
     // tolerance mode (VISO_PRECISION_FAST): tmpl / tmpl_h hold floats, same
     // layout; the iterations run in fp32 (lk_align_kernel<true>)
     int fast = 0;
+    // background mode (launch_lk_bg): items = frames x n in frame order, taken
+    // from *bg_next; frame f's pose is valid once bg_ready[f] != 0
+    int* bg_ready = nullptr;
+    int* bg_next = nullptr;
+    int* bg_err = nullptr;
+    int bg_items = 0;
 };
 void launch_lk_align(const LkAlignArgs& a, hipStream_t stream);
+// LK alignment of an ingest chunk's frames beside its direct-pose chain: grid
+// workgroups (one per CU) resident for the chunk (track.hip lk_item_kernel)
+void launch_lk_bg(const LkAlignArgs& a, int grid, hipStream_t stream);
+// the items of a background launch it has not taken yet, at full occupancy
+// (after the chunk's last pose): grid workgroups pull from the same counter
+void launch_lk_drain(const LkAlignArgs& a, int grid, hipStream_t stream);
 // Keyframe choice + per-level templates of every map point (once per map).
 void launch_lk_template(const LkAlignArgs& a, hipStream_t stream);
 
@@ -134,7 +146,11 @@ struct DirectPrev {
     double* pose_out;           // its pose (= this frame's pose_last12)
     double* log;
     int log_index;
+    int* ready = nullptr;  // background LK alignment's flag for that pose (or null)
 };
+// true when a direct-pose workgroup leaves its CU room for the background LK
+// alignment's (12 waves of 128 VGPRs + <= 76 KB LDS beside 4 waves + 84 KB)
+bool direct_fits_background();
 void launch_direct_levels(const FrameDev& last, const FrameDev& cur, const PyrGeom& g,
                           const double K[4], const double* points, int n,
                           const double* pose_last12, const double* pose_seed12,
@@ -144,7 +160,7 @@ void launch_direct_final(const FrameDev& last, const FrameDev& cur, const PyrGeo
                          const double K[4], const double* points, int n,
                          const double* pose_last12, const DirectScratch& s, double* stats,
                          double* pose_out, double* log, int log_index, hipStream_t stream,
-                         int precision = VISO_PRECISION_FAITHFUL);
+                         int precision = VISO_PRECISION_FAITHFUL, int* ready = nullptr);
 // ---------------------------------------------------------------- rig direct pose
 // Multi-camera photometric rig (the repo's own spec;
 // oracle/oracle_rig.cpp): levels 3..0 of one rig Gauss-Newton step each over

@@ -238,19 +238,6 @@ __device__ inline LkResult lk_iterate(const LkTemplate& t, int w1, int h1,
     return {dx, dy, succ, iter};
 }
 
-// One level of the inverse-compositional LK used by both engines.
-//   ref_x/ref_y: template coordinate of THIS lane's pixel (already offset).
-template <int MAXIT, bool KLT_BOUNDS>
-__device__ inline LkResult lk_level(const uint8_t* __restrict__ img1, int w1, int h1,
-                                    const uint8_t* __restrict__ img2, int w2, int h2,
-                                    double ref_x, double ref_y, double cur_x, double cur_y,
-                                    double bx, double by, double dx, double dy, double thresh,
-                                    const Window& win) {
-    const LkTemplate t = lk_prepare(img1, w1, h1, ref_x, ref_y);
-    return lk_iterate<MAXIT, KLT_BOUNDS>(t, w1, h1, img2, w2, h2, cur_x, cur_y, bx, by, dx, dy,
-                                         thresh, win);
-}
-
 // Tolerance mode (VISO_PRECISION_FAST) GN iterations of one LKAlignment
 // level: the same control flow (bounds test on ref coords + d, NaN / cost-
 // increase stops, success = last accepted cost <= thresh) in fp32.  The
@@ -338,10 +325,14 @@ __global__ __launch_bounds__(256) void klt_kernel(FrameDev ref, FrameDev cur, Py
         const double dx0 = (double)(k2.x - kx), dy0 = (double)(k2.y - ky);
         const float fx = kx + (float)px, fy = ky + (float)py;  // float + int
         const int w = g.w[level], h = g.h[level];
-        const Window win = load_window(my_win, cur.l[level], w, h, (double)kx + dx0, (double)ky + dy0);
-        LkResult r = lk_level<10, true>(ref.l[level], w, h, cur.l[level], w, h,
-                                        (double)fx, (double)fy, (double)fx, (double)fy,
-                                        (double)kx, (double)ky, dx0, dy0, thresh, win);
+        // the current-image window's loads and the template's (reference
+        // image) loads are in flight together: one memory round trip per
+        // level instead of two
+        const WinRegs wr = window_issue(cur.l[level], w, h, (double)kx + dx0, (double)ky + dy0);
+        const LkTemplate t = lk_prepare(ref.l[level], w, h, (double)fx, (double)fy);
+        const Window win = window_commit(my_win, wr);
+        LkResult r = lk_iterate<10, true>(t, w, h, cur.l[level], w, h, (double)fx, (double)fy,
+                                          (double)kx, (double)ky, dx0, dy0, thresh, win);
         succ = r.succ;
         k2.x = kx + (float)r.dx;
         k2.y = ky + (float)r.dy;
@@ -458,24 +449,16 @@ __global__ __launch_bounds__(256) void lk_template_kernel(LkAlignArgs a) {
 #ifndef VISO_LK_MIN_WAVES_FAST
 #define VISO_LK_MIN_WAVES_FAST 6
 #endif
+// One (frame, map point) of LKAlignment: the wave's point i against frame
+// `cur` at pose cur_pose (12 doubles), outputs at row offset o.  `ka` is the
+// kernel argument in the kernarg segment (run-time indices into its arrays are
+// read from there: a run-time index into the by-value struct would copy it per
+// thread to scratch).
 template <bool FAST>
-__global__ __launch_bounds__(256, FAST ? VISO_LK_MIN_WAVES_FAST : VISO_LK_MIN_WAVES) void lk_align_kernel(
-    LkAlignArgs a) {
-    __shared__ uint8_t s_win[4][2][kWinW * kWinH];
-    const int i = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-    if (i >= a.n) return;
-    // frame of the batch (blockIdx.y): its pyramid, pose and output rows
-    // run-time indices into the kernel argument are read straight from the
-    // kernarg segment (`a` is the only argument, at offset 0): a run-time
-    // index into the by-value struct would copy it per thread to scratch
-    const LkAlignArgs* ka = (const LkAlignArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-    const LkFrame& fr = ka->frames[blockIdx.y];
-    const FrameDev cur = fr.cur;
-    const double* cur_pose = fr.pose;
-    const size_t o = (size_t)blockIdx.y * a.out_stride;
+__device__ __attribute__((always_inline)) inline void lk_point(const LkAlignArgs& a, const LkAlignArgs* ka,
+                                                               const FrameDev& cur, const double* cur_pose, int i,
+                                                               size_t o, uint8_t* my_win0, uint8_t* my_win1) {
     const int lane = threadIdx.x & 63;
-    uint8_t* my_win0 = s_win[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)][0];
-    uint8_t* my_win1 = s_win[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)][1];
     const int px = (lane >> 3) - 4, py = (lane & 7) - 4;
     const double P[3] = {a.points[3 * i], a.points[3 * i + 1], a.points[3 * i + 2]};
     const Intrinsics K{a.K[0], a.K[1], a.K[2], a.K[3]};
@@ -612,6 +595,77 @@ __global__ __launch_bounds__(256, FAST ? VISO_LK_MIN_WAVES_FAST : VISO_LK_MIN_WA
     }
 }
 
+template <bool FAST>
+__global__ __launch_bounds__(256, FAST ? VISO_LK_MIN_WAVES_FAST : VISO_LK_MIN_WAVES) void lk_align_kernel(
+    LkAlignArgs a) {
+    __shared__ uint8_t s_win[4][2][kWinW * kWinH];
+    const int i = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    if (i >= a.n) return;
+    // frame of the batch (blockIdx.y): its pyramid, pose and output rows
+    const LkAlignArgs* ka = (const LkAlignArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    const LkFrame& fr = ka->frames[blockIdx.y];
+    const FrameDev cur = fr.cur;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    lk_point<FAST>(a, ka, cur, fr.pose, i, (size_t)blockIdx.y * a.out_stride, s_win[wave][0], s_win[wave][1]);
+}
+
+// LK alignment in the background of an ingest chunk (viso_ctx::bg_begin;
+// lk_item_kernel):
+// one 256-thread workgroup per CU, resident for the whole chunk beside the
+// direct pose's workgroups (its LDS request, static + dynamic, caps it at one
+// per CU; <= 128 VGPRs: the spare wave slot of each SIMD beside three
+// 128-VGPR direct-pose waves).  Each wave takes
+// (frame, point) items in frame order from a counter, waits for the frame's
+// pose (the direct pose raises the frame's ready flag after storing it, both
+// agent-scope: MI355X_MICROARCH.md's first sc1 hand-off row), and runs that
+// point's LKAlignment with the batched kernel's exact per-point code.  Every
+// wait is bounded: a flag not raised within kBgWaitTicks sets *bg_err and the
+// wave stops, so the grid always drains.
+// The chunk's drain (launch_lk_drain) is the same kernel without the LDS
+// padding, launched after the chunk's last pose: the items the resident grid
+// has not reached run beside it on every CU's remaining wave slots.
+constexpr unsigned long long kBgWaitTicks = 20000000ull;  // 200 ms of s_memrealtime
+template <bool FAST>
+__global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
+    __shared__ uint8_t s_win[4][2][kWinW * kWinH];
+    __shared__ double s_pose[4][12];  // the wave's current frame pose
+    const LkAlignArgs* ka = (const LkAlignArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    int f_loaded = -1;
+    for (;;) {
+        int item = 0;
+        if (lane == 0) item = atomicAdd(a.bg_next, 1);
+        item = __builtin_amdgcn_readfirstlane(item);
+        if (item >= a.bg_items) break;
+        const int f = item / a.n, i = item - f * a.n;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        bool ok = true;
+        while (__builtin_amdgcn_readfirstlane(
+                   __hip_atomic_load(a.bg_ready + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > kBgWaitTicks) {
+                ok = false;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (!ok) {
+            if (lane == 0) atomicOr(a.bg_err, 1);
+            break;
+        }
+        const LkFrame& fr = ka->frames[f];
+        if (f != f_loaded) {  // wave-uniform
+            if (lane < 12)
+                s_pose[wave][lane] = __hip_atomic_load(fr.pose + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            f_loaded = f;
+        }
+        const FrameDev cur = fr.cur;
+        lk_point<FAST>(a, ka, cur, s_pose[wave], i, (size_t)f * a.out_stride, s_win[wave][0], s_win[wave][1]);
+    }
+}
+
 // One 1,024-thread workgroup: thread t owns the ceil(n / 1024) consecutive
 // tracks [t C, t C + C), counts its survivors, one block-wide exclusive scan
 // places them, and each thread copies its own in order (src/viso.cpp:23-40
@@ -668,6 +722,35 @@ void launch_lk_align(const LkAlignArgs& a, hipStream_t stream) {
         lk_align_kernel<true><<<dim3(gx, a.n_frames), 256, 0, stream>>>(a);
     else
         lk_align_kernel<false><<<dim3(gx, a.n_frames), 256, 0, stream>>>(a);
+}
+
+// the background kernel's LDS request: static windows + dynamic = 84 KB, so
+// two never share a CU (2 x 84 > 160 KB) while one leaves room for a 12-wave
+// direct-pose workgroup (84 + 68 <= 160 KB)
+constexpr size_t kBgLdsTotal = 84 * 1024;
+void launch_lk_bg(const LkAlignArgs& a, int grid, hipStream_t stream) {
+    if (a.n <= 0 || a.bg_items <= 0 || grid <= 0) return;
+    const size_t dyn = kBgLdsTotal - sizeof(uint8_t) * 4 * 2 * kWinW * kWinH;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)lk_item_kernel<true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+        (void)hipFuncSetAttribute((const void*)lk_item_kernel<false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+        attr = true;
+    }
+    if (a.fast)
+        lk_item_kernel<true><<<grid, 256, dyn, stream>>>(a);
+    else
+        lk_item_kernel<false><<<grid, 256, dyn, stream>>>(a);
+}
+
+void launch_lk_drain(const LkAlignArgs& a, int grid, hipStream_t stream) {
+    if (a.n <= 0 || a.bg_items <= 0 || grid <= 0) return;
+    if (a.fast)
+        lk_item_kernel<true><<<grid, 256, 0, stream>>>(a);
+    else
+        lk_item_kernel<false><<<grid, 256, 0, stream>>>(a);
 }
 
 void launch_lk_template(const LkAlignArgs& a, hipStream_t stream) {
