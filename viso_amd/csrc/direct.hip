@@ -6,7 +6,7 @@
 //   L(3), L(2), L(1), L(0)   (+ F, the final level-0 solve, which normally
 //   runs fused into the next frame's L(3); only the last frame of an ingest
 //   call gets a standalone F launch)
-// L(l) (one 16-wave workgroup per tile):
+// L(l) (one 12-wave workgroup per tile):
 //   prologue — every workgroup solves level l+1 from that level's tile
 //     partials (written by L(l+1)) and gets T21 for level l.  All workgroups
 //     compute the same bits, so no grid-wide hand-off is needed beyond the
@@ -81,10 +81,12 @@ namespace viso {
 namespace {
 
 constexpr int kSums = 28;
-// waves per workgroup of the direct pose (one map point per wave) and of
+// waves per workgroup of the direct pose (one map point per wave; 12: three
+// 128-VGPR waves per SIMD, so a CU keeps one wave slot per SIMD and LDS for
+// the background LK alignment's workgroup, track.hip lk_item_kernel) and of
 // the rig (four partial-reduction waves per camera)
 #ifndef VISO_DIRECT_WAVES
-#define VISO_DIRECT_WAVES 16
+#define VISO_DIRECT_WAVES 12
 #endif
 constexpr int kWaves = VISO_DIRECT_WAVES;
 constexpr int kThreads = kWaves * 64;
@@ -101,11 +103,9 @@ inline int map_tile(int n, int groups) {
 }
 constexpr int kStats = 50;
 constexpr int kStateStride = 8;
-// wave priority of the direct pose outside the solve (the solver runs at 3);
-// dev: raised above a co-resident background grid's 0
-#ifndef VISO_DIRECT_PRIO
-#define VISO_DIRECT_PRIO 0
-#endif
+// pre_hdr bit 17: a background LK alignment grid shares the CUs (its waves
+// run at priority 0): the direct pose's waves run at 1 (the solver at 3)
+constexpr int kHdrBg = 1 << 17;
 
 // The two frames of one DirectPoseEstimation call and the `last` pose the
 // patches are taken at (Keyframe::Project of last_frame, src/viso.cpp:697).
@@ -955,17 +955,12 @@ __device__ inline void after_solve(const DirectArgs& a, bool merged, SolveLds& L
 // SGPRs at wave launch (-amdgpu-kernarg-preload-count, viso_amd/build.py), so
 // the partial loads issue without waiting for a kernel-argument load.
 template <bool FAST>
-// (dev: VISO_DIRECT_MINW caps the registers of a narrower workgroup so a
-// background workgroup can share the CU; tools/ubench/bg_filler.hip)
-#ifdef VISO_DIRECT_MINW
-__global__ __launch_bounds__(kThreads, VISO_DIRECT_MINW) void direct_level_kernel(const double* __restrict__ pre_part,
-#else
-__global__ __launch_bounds__(kThreads) void direct_level_kernel(const double* __restrict__ pre_part,
-#endif
+// (at most 128 VGPRs: four waves per SIMD, the fourth the background's)
+__global__ __launch_bounds__(kThreads, 4) void direct_level_kernel(const double* __restrict__ pre_part,
                                                                  const int* __restrict__ pre_good, int pre_hdr,
                                                                  DirectArgs a) {
     PROBE_DECL();
-    if (VISO_DIRECT_PRIO) __builtin_amdgcn_s_setprio(VISO_DIRECT_PRIO);
+    if (pre_hdr & kHdrBg) __builtin_amdgcn_s_setprio(1);
     __shared__ SolveLds L;
     __shared__ double s_pose[12];
     __shared__ double s_last[12];  // merged L(3): this frame's `last` pose
@@ -1086,7 +1081,10 @@ __global__ __launch_bounds__(kThreads) void direct_level_kernel(const double* __
             solve_wave0(L, 0, stp);
 #endif
         PST(7);
-        __builtin_amdgcn_s_setprio(VISO_DIRECT_PRIO);
+        if (pre_hdr & kHdrBg)
+            __builtin_amdgcn_s_setprio(1);
+        else
+            __builtin_amdgcn_s_setprio(0);
     }
     if (!solve && wave == 0 && lane == 0) {
         // seeded level: no solve, T21 is the seed (thread 256 wrote it)
@@ -1646,7 +1644,7 @@ void launch_direct_levels(const FrameDev& last_pyr, const FrameDev& cur_pyr, con
                           const double K[4], const double* points, int n,
                           const double* pose_last12, const double* pose_seed12,
                           const DirectScratch& s, double* stats, const DirectPrev* merge,
-                          hipStream_t stream, int precision) {
+                          hipStream_t stream, int precision, bool bg) {
     DirectArgs a = direct_args(last_pyr, cur_pyr, g, K, points, n, pose_last12, pose_seed12, s,
                                stats, precision == VISO_PRECISION_FAST);
     if (merge) {
@@ -1668,7 +1666,7 @@ void launch_direct_levels(const FrameDev& last_pyr, const FrameDev& cur_pyr, con
         const int sl = merged ? 0 : level + 1;
         const double* pp = solve ? a.s.part + (size_t)sl * kMaxTiles * kSums : nullptr;
         const int* pg = solve ? a.s.good + sl * kMaxTiles : nullptr;
-        const int hdr = a.n_tiles | (solve ? 1 << 16 : 0);
+        const int hdr = a.n_tiles | (solve ? 1 << 16 : 0) | (bg ? kHdrBg : 0);
         if (precision == VISO_PRECISION_FAST)
             direct_level_kernel<true><<<grid, kThreads, 0, stream>>>(pp, pg, hdr, a);
         else
@@ -1691,7 +1689,7 @@ void launch_direct_final(const FrameDev& last_pyr, const FrameDev& cur_pyr, cons
     a.level = -1;
     a.probe_seq = next_probe_seq();
     // F solves level 0
-    const int hdr = a.n_tiles | (1 << 16);
+    const int hdr = a.n_tiles | (1 << 16) | (ready ? kHdrBg : 0);
     if (precision == VISO_PRECISION_FAST)
         direct_level_kernel<true><<<1, kThreads, 0, stream>>>(a.s.part, a.s.good, hdr, a);
     else

@@ -366,7 +366,9 @@ int viso_ctx::bg_begin(const std::vector<int>& chunk) {
         VISO_HIP_CHECK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
         VISO_HIP_CHECK(hipEventCreateWithFlags(&bg_done, hipEventDisableTiming));
     }
-    int rc = bg_buf.ensure(sizeof(int) * (kLkBatch + 64));
+    // ready flags [kLkBatch], eight heads on lines of their own, error word
+    const size_t bg_words = kLkBatch + 8 * 32 + 32;
+    int rc = bg_buf.ensure(sizeof(int) * bg_words);
     if (rc) return rc;
     LkAlignArgs a = lk_args();
     a.n_frames = nb;
@@ -381,11 +383,11 @@ int viso_ctx::bg_begin(const std::vector<int>& chunk) {
     a.uv_after = (double*)lk_after.ptr;
     a.bg_ready = (int*)bg_buf.ptr;
     a.bg_next = a.bg_ready + kLkBatch;
-    a.bg_err = a.bg_ready + kLkBatch + 1;
+    a.bg_err = a.bg_next + 8 * 32;
     a.bg_items = nb * n_map;
     // flags and counter cleared behind the chunk's pyramid; the kernel starts
     // after both (the frames' pyramids are its input)
-    VISO_HIP_CHECK(hipMemsetAsync(bg_buf.ptr, 0, sizeof(int) * (kLkBatch + 64), stream));
+    VISO_HIP_CHECK(hipMemsetAsync(bg_buf.ptr, 0, sizeof(int) * bg_words, stream));
     VISO_HIP_CHECK(hipEventRecord(bg_done, stream));
     VISO_HIP_CHECK(hipStreamWaitEvent(lk_stream, bg_done, 0));
     {
@@ -716,7 +718,8 @@ int viso_ctx::on_new_frame(int cur) {
                 }
                 launch_direct_levels(frame(last_slot), frame(cur), g, K, (const double*)map_pts.ptr,
                                      n_map, pose_of(last_slot), pose_of(last_slot), direct,
-                                     (double*)direct_stats.ptr, dpend ? &m : nullptr, stream, p.precision);
+                                     (double*)direct_stats.ptr, dpend ? &m : nullptr, stream, p.precision,
+                                     bg_active);
             }
             if (dpend) {
                 drop(dpend_cur);

@@ -76,8 +76,9 @@ struct LkAlignArgs {
     // tolerance mode (VISO_PRECISION_FAST): tmpl / tmpl_h hold floats, same
     // layout; the iterations run in fp32 (lk_align_kernel<true>)
     int fast = 0;
-    // background mode (launch_lk_bg): items = frames x n in frame order, taken
-    // from *bg_next; frame f's pose is valid once bg_ready[f] != 0
+    // background mode (launch_lk_bg): items = frames x n, taken from eight
+    // heads bg_next[32 x] (one per XCD, each a segment of every frame's points,
+    // frames in order); frame f's pose is valid once bg_ready[f] != 0
     int* bg_ready = nullptr;
     int* bg_next = nullptr;
     int* bg_err = nullptr;
@@ -155,7 +156,7 @@ void launch_direct_levels(const FrameDev& last, const FrameDev& cur, const PyrGe
                           const double K[4], const double* points, int n,
                           const double* pose_last12, const double* pose_seed12,
                           const DirectScratch& s, double* stats, const DirectPrev* merge,
-                          hipStream_t stream, int precision = VISO_PRECISION_FAITHFUL);
+                          hipStream_t stream, int precision = VISO_PRECISION_FAITHFUL, bool bg = false);
 void launch_direct_final(const FrameDev& last, const FrameDev& cur, const PyrGeom& g,
                          const double K[4], const double* points, int n,
                          const double* pose_last12, const DirectScratch& s, double* stats,

@@ -615,7 +615,7 @@ __global__ __launch_bounds__(256, FAST ? VISO_LK_MIN_WAVES_FAST : VISO_LK_MIN_WA
 // direct pose's workgroups (its LDS request, static + dynamic, caps it at one
 // per CU; <= 128 VGPRs: the spare wave slot of each SIMD beside three
 // 128-VGPR direct-pose waves).  Each wave takes
-// (frame, point) items in frame order from a counter, waits for the frame's
+// (frame, point) items in frame order from the work heads, waits for the frame's
 // pose (the direct pose raises the frame's ready flag after storing it, both
 // agent-scope: MI355X_MICROARCH.md's first sc1 hand-off row), and runs that
 // point's LKAlignment with the batched kernel's exact per-point code.  Every
@@ -632,37 +632,49 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
     const LkAlignArgs* ka = (const LkAlignArgs*)__builtin_amdgcn_kernarg_segment_ptr();
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     int f_loaded = -1;
-    for (;;) {
-        int item = 0;
-        if (lane == 0) item = atomicAdd(a.bg_next, 1);
-        item = __builtin_amdgcn_readfirstlane(item);
-        if (item >= a.bg_items) break;
-        const int f = item / a.n, i = item - f * a.n;
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        bool ok = true;
-        while (__builtin_amdgcn_readfirstlane(
-                   __hip_atomic_load(a.bg_ready + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0) {
-            if (__builtin_amdgcn_s_memrealtime() - t0 > kBgWaitTicks) {
-                ok = false;
+    // eight work heads, one per XCD (one head saturates near 88 dequeues per
+    // us, MI355X_MICROARCH.md "dequeue"): head x holds segment x of every
+    // frame's points (points [x seg, (x + 1) seg)), frames in order; a wave
+    // drains its own XCD's head, then the others'
+    const int seg = (a.n + 7) / 8;
+    const int per_head = a.n_frames * seg;
+    const int xcc = (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 7);  // HW_REG_XCC_ID
+    bool ok = true;
+    for (int h = 0; h < 8 && ok; ++h) {
+        const int head = (xcc + h) & 7;
+        for (;;) {
+            int k = 0;
+            if (lane == 0) k = atomicAdd(a.bg_next + 32 * head, 1);
+            k = __builtin_amdgcn_readfirstlane(k);
+            if (k >= per_head) break;
+            const int f = k / seg, i = head * seg + (k - f * seg);
+            if (i >= a.n) continue;
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            while (__builtin_amdgcn_readfirstlane(
+                       __hip_atomic_load(a.bg_ready + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > kBgWaitTicks) {
+                    ok = false;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(4);
+            }
+            if (!ok) {
+                if (lane == 0) atomicOr(a.bg_err, 1);
                 break;
             }
-            __builtin_amdgcn_s_sleep(2);
+            const LkFrame& fr = ka->frames[f];
+            if (f != f_loaded) {  // wave-uniform
+                if (lane < 12)
+                    s_pose[wave][lane] =
+                        __hip_atomic_load(fr.pose + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                f_loaded = f;
+            }
+            const FrameDev cur = fr.cur;
+            lk_point<FAST>(a, ka, cur, s_pose[wave], i, (size_t)f * a.out_stride, s_win[wave][0], s_win[wave][1]);
         }
-        if (!ok) {
-            if (lane == 0) atomicOr(a.bg_err, 1);
-            break;
-        }
-        const LkFrame& fr = ka->frames[f];
-        if (f != f_loaded) {  // wave-uniform
-            if (lane < 12)
-                s_pose[wave][lane] = __hip_atomic_load(fr.pose + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            f_loaded = f;
-        }
-        const FrameDev cur = fr.cur;
-        lk_point<FAST>(a, ka, cur, s_pose[wave], i, (size_t)f * a.out_stride, s_win[wave][0], s_win[wave][1]);
     }
 }
 
