@@ -126,7 +126,7 @@ int viso_synchronize(viso_ctx* c) {
     if (!c) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipStreamSynchronize(c->stream));
     if (c->lk_stream) VISO_HIP_CHECK(hipStreamSynchronize(c->lk_stream));
-    return VISO_OK;
+    return c->bg_check();
 }
 
 int viso_timing_enable(viso_ctx* c, int32_t enable) {

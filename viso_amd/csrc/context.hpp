@@ -244,8 +244,14 @@ struct viso_ctx {
     // direct-pose chain (track.hip lk_item_kernel): bg_begin after the chunk's
     // pyramid when the context is tracking (frames of the chunk: their slots),
     // bg_end once the chunk's last pose is launched
+    bool bg_eligible();
     int bg_begin(const std::vector<int>& chunk);
     int bg_end();
+    // after a host sync: VISO_ERR_HIP if a background launch since the last
+    // check timed out waiting for a pose (its LK outputs are then invalid)
+    int bg_check();
+    int bg_launch();
+    bool bg_unchecked = false;
     bool bg_active = false;
     int bg_mode = -1;        // VISO_LK_BG: 0 off, 1 on (read once; -1 unread)
     int bg_nb = 0;           // frames of the chunk

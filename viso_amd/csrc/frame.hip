@@ -182,9 +182,28 @@ void viso_ctx::release() {
 }
 
 // The context stream and the LK-alignment side stream (single-frame calls).
+// The side stream gets a hardware queue of its own: a stream created with a
+// CU mask (here every CU) is never mapped onto a queue another stream uses,
+// while plain streams share the process's few queues (GPU_MAX_HW_QUEUES)
+// round-robin — and a chunk-resident LK grid on a queue shared with the
+// context stream would sit in front of the very chain it waits for.  When
+// the masked stream cannot be made, the background mode stays off.
 int viso_ctx::create_streams() {
     if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return VISO_ERR_HIP;
-    if (hipStreamCreateWithFlags(&lk_stream, hipStreamNonBlocking) != hipSuccess) return VISO_ERR_HIP;
+    int cus = 0;
+    const char* q = getenv("VISO_LK_QUEUE");  // dev: "shared" = a plain stream
+    if (!(q && q[0] == 's') &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0) {
+        std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
+        for (int c = 0; c < cus; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
+        if (hipExtStreamCreateWithCUMask(&lk_stream, (uint32_t)mask.size(), mask.data()) != hipSuccess)
+            lk_stream = nullptr;
+    }
+    if (!lk_stream) {
+        (void)hipGetLastError();
+        if (!(q && q[0] == 's')) bg_mode = 0;
+        if (hipStreamCreateWithFlags(&lk_stream, hipStreamNonBlocking) != hipSuccess) return VISO_ERR_HIP;
+    }
     return VISO_OK;
 }
 
@@ -353,21 +372,29 @@ int viso_ctx::finish_call(hipStream_t ls) {
 // leaves a CU room for the background one (direct_fits_background).  Every
 // frame of such a chunk is a tracking frame, so every ready flag is raised:
 // frame f's by frame f+1's merged level-3 launch, the last by the final solve.
-int viso_ctx::bg_begin(const std::vector<int>& chunk) {
+bool viso_ctx::bg_eligible() {
     if (bg_mode < 0) {
+        // off on request, and when kernels are serialised (the resident grid
+        // would wait out its flag timeouts behind the chain it waits for)
         const char* e = getenv("VISO_LK_BG");
-        bg_mode = (e && e[0] == '0') ? 0 : 1;
+        const char* ser = getenv("AMD_SERIALIZE_KERNEL");
+        const char* blk = getenv("HIP_LAUNCH_BLOCKING");
+        bg_mode = (e && e[0] == '0') || (ser && ser[0] && ser[0] != '0') || (blk && blk[0] && blk[0] != '0') ? 0 : 1;
     }
+    return bg_mode && direct_fits_background() && state == VISO_STATE_RUNNING && n_map > 0 && lk_tmpl.ptr &&
+           kf_interval <= 0 && !dpend && lk_pending.empty();
+}
+
+int viso_ctx::bg_begin(const std::vector<int>& chunk) {
     const int nb = (int)chunk.size();
-    if (!bg_mode || !direct_fits_background() || state != VISO_STATE_RUNNING || n_map <= 0 || !lk_tmpl.ptr ||
-        nb < 1 || nb > kLkBatch || kf_interval > 0 || dpend || !lk_pending.empty())
-        return VISO_OK;
+    if (!bg_eligible() || nb < 1 || nb > kLkBatch) return VISO_OK;
     if (!n_cu) {
         VISO_HIP_CHECK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
         VISO_HIP_CHECK(hipEventCreateWithFlags(&bg_done, hipEventDisableTiming));
     }
-    // ready flags [kLkBatch], eight heads on lines of their own, error word
-    const size_t bg_words = kLkBatch + 8 * 32 + 32;
+    // ready flags [kLkBatch], eight heads on lines of their own, error word,
+    // leftover list (cursor, count, 4096 items)
+    const size_t bg_words = kLkBatch + 8 * 32 + 32 + 32 + 4096;
     int rc = bg_buf.ensure(sizeof(int) * bg_words);
     if (rc) return rc;
     LkAlignArgs a = lk_args();
@@ -384,23 +411,38 @@ int viso_ctx::bg_begin(const std::vector<int>& chunk) {
     a.bg_ready = (int*)bg_buf.ptr;
     a.bg_next = a.bg_ready + kLkBatch;
     a.bg_err = a.bg_next + 8 * 32;
+    a.bg_left = a.bg_err + 32;
     a.bg_items = nb * n_map;
-    // flags and counter cleared behind the chunk's pyramid; the kernel starts
-    // after both (the frames' pyramids are its input)
+    // flags, heads and leftovers cleared behind the chunk's pyramid; the grid
+    // (on the side stream's own hardware queue, create_streams) starts behind
+    // them
     VISO_HIP_CHECK(hipMemsetAsync(bg_buf.ptr, 0, sizeof(int) * bg_words, stream));
+    bg_args = a;
+    bg_active = true;
+    bg_unchecked = true;
+    bg_nb = nb;
+    bg_slots.clear();
+    return bg_launch();
+}
+
+int viso_ctx::bg_launch() {
     VISO_HIP_CHECK(hipEventRecord(bg_done, stream));
     VISO_HIP_CHECK(hipStreamWaitEvent(lk_stream, bg_done, 0));
     {
         TimedRegion t(timing, VISO_KERNEL_LKALIGN, lk_stream);
-        launch_lk_bg(a, n_cu, lk_stream);
+        launch_lk_bg(bg_args, n_cu, lk_stream);
     }
     VISO_HIP_CHECK(hipGetLastError());
     VISO_HIP_CHECK(hipEventRecord(bg_done, lk_stream));
-    bg_args = a;
-    bg_active = true;
-    bg_nb = nb;
-    bg_slots.clear();
     return VISO_OK;
+}
+
+int viso_ctx::bg_check() {
+    if (!bg_unchecked || !bg_buf.ptr) return VISO_OK;
+    int err = 0;
+    VISO_HIP_CHECK(hipMemcpy(&err, (int*)bg_buf.ptr + kLkBatch + 8 * 32, sizeof(int), hipMemcpyDeviceToHost));
+    bg_unchecked = false;
+    return err ? VISO_ERR_HIP : VISO_OK;
 }
 
 // The chunk's last pose is launched: the items the resident grid has not
@@ -409,7 +451,9 @@ int viso_ctx::bg_begin(const std::vector<int>& chunk) {
 // outputs, the held frames), which is the latest LK batch of the flush_lk
 // bookkeeping.
 int viso_ctx::bg_end() {
-    launch_lk_drain(bg_args, 3 * n_cu, stream);
+    LkAlignArgs d = bg_args;
+    d.bg_drain = 1;
+    launch_lk_drain(d, 3 * n_cu, stream);
     VISO_HIP_CHECK(hipGetLastError());
     VISO_HIP_CHECK(hipStreamWaitEvent(stream, bg_done, 0));
     lk_last_rows = bg_nb;
@@ -839,9 +883,11 @@ int viso_process_frames_device(viso_ctx* c, const uint8_t* d_left, const uint8_t
     if (frame_stride < (size_t)c->geom.w[0] * c->geom.h[0]) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(c->device));
     const int B = c->p.batch_frames;
-    for (int f0 = 0; f0 < n; f0 += B) {
+    for (int f0 = 0, nb = 0; f0 < n; f0 += nb) {
         RoctxRange range("viso:ingest_chunk");
-        const int nb = std::min(B, n - f0);
+        // a tracking context's chunks run LK alignment in the background,
+        // which covers at most kLkBatch frames: chunks are cut to that
+        nb = std::min(c->bg_eligible() ? std::min(B, kLkBatch) : B, n - f0);
         std::vector<int> sl;
         std::vector<const uint8_t*> l0;
         std::vector<uint8_t*> dst;
@@ -962,6 +1008,7 @@ int viso_get_alignment(viso_ctx* c, int32_t* pair_kf, uint8_t* success, double* 
     if (!c) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(c->device));
     VISO_HIP_CHECK(hipStreamSynchronize(c->lk_stream));
+    if (int rc = c->bg_check()) return rc;
     const size_t m = c->ran_tracking ? std::min(cap, (size_t)c->lk_last_pts) : 0;
     const size_t o = (size_t)std::max(c->lk_last_rows - 1, 0) * kMaxMapPoints;
     if (m > 0) {
@@ -982,6 +1029,7 @@ int viso_get_frame_stats(viso_ctx* c, double out[16]) {
     if (c->state == VISO_STATE_RUNNING && c->stats[12] == 0 && c->ran_tracking) {
         // last frame was a tracking frame: level-0 direct stats + LK counts
         VISO_HIP_CHECK(hipStreamSynchronize(c->lk_stream));
+        if (int rc = c->bg_check()) return rc;
         const int m = c->lk_last_pts;
         const size_t o = (size_t)std::max(c->lk_last_rows - 1, 0) * kMaxMapPoints;
         std::vector<int32_t> pk((size_t)m);

@@ -83,6 +83,9 @@ struct LkAlignArgs {
     int* bg_next = nullptr;
     int* bg_err = nullptr;
     int bg_items = 0;
+    // leftovers: [0] drain cursor, [1] count, [32 ..] items (head * per_head + k)
+    int* bg_left = nullptr;
+    int bg_drain = 0;  // this launch is the end-of-chunk drain
 };
 void launch_lk_align(const LkAlignArgs& a, hipStream_t stream);
 // LK alignment of an ingest chunk's frames beside its direct-pose chain: grid

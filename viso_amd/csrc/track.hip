@@ -619,12 +619,17 @@ __global__ __launch_bounds__(256, FAST ? VISO_LK_MIN_WAVES_FAST : VISO_LK_MIN_WA
 // pose (the direct pose raises the frame's ready flag after storing it, both
 // agent-scope: MI355X_MICROARCH.md's first sc1 hand-off row), and runs that
 // point's LKAlignment with the batched kernel's exact per-point code.  Every
-// wait is bounded: a flag not raised within kBgWaitTicks sets *bg_err and the
-// wave stops, so the grid always drains.
+// wait is bounded: a resident wave whose item's frame is not ready within
+// kBgIdleTicks hands the item to the leftover list and leaves (the end-of-
+// chunk drain runs the leftovers first, then whatever the heads still hold),
+// so a grid that some serialisation of the queues put in the chain's way
+// steps aside; the drain's own waits beyond kBgWaitTicks set *bg_err.
 // The chunk's drain (launch_lk_drain) is the same kernel without the LDS
 // padding, launched after the chunk's last pose: the items the resident grid
 // has not reached run beside it on every CU's remaining wave slots.
 constexpr unsigned long long kBgWaitTicks = 20000000ull;  // 200 ms of s_memrealtime
+constexpr unsigned long long kBgIdleTicks = 30000ull;      // 300 us: ~6 frames of the chain
+constexpr int kBgLeftCap = 4096;                           // leftover items (one per resident wave at most)
 template <bool FAST>
 __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
     __shared__ uint8_t s_win[4][2][kWinW * kWinH];
@@ -639,42 +644,93 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
     const int seg = (a.n + 7) / 8;
     const int per_head = a.n_frames * seg;
     const int xcc = (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 7);  // HW_REG_XCC_ID
-    bool ok = true;
-    for (int h = 0; h < 8 && ok; ++h) {
-        const int head = (xcc + h) & 7;
-        for (;;) {
-            int k = 0;
+    auto ready = [&](int f) {
+        return __builtin_amdgcn_readfirstlane(
+                   __hip_atomic_load(a.bg_ready + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0;
+    };
+    // one item: wait for its frame (the resident grid at most kBgIdleTicks,
+    // then the item goes to the leftover list and the wave leaves; the drain,
+    // which runs once every pose is launched, at most kBgWaitTicks, an error),
+    // then align the point
+    auto run_item = [&](int head, int k) __attribute__((always_inline)) -> bool {
+        const int f = k / seg, i = head * seg + (k - f * seg);
+        if (i >= a.n) return true;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (!ready(f)) {
+            const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t0;
+            if (!a.bg_drain && dt > kBgIdleTicks) {
+                if (lane == 0) {
+                    // reserve a slot, then publish the item (+1: 0 = not yet
+                    // written; the drain may read the count first)
+                    const int j = atomicAdd(a.bg_left + 1, 1);
+                    if (j < kBgLeftCap)
+                        __hip_atomic_store(a.bg_left + 32 + j, head * per_head + k + 1, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    else
+                        atomicOr(a.bg_err, 1);
+                }
+                return false;
+            }
+            if (a.bg_drain && dt > kBgWaitTicks) {
+                if (lane == 0) atomicOr(a.bg_err, 1);
+                return false;
+            }
+            __builtin_amdgcn_s_sleep(4);
+        }
+        const LkFrame& fr = ka->frames[f];
+        if (f != f_loaded) {  // wave-uniform
+            if (lane < 12)
+                s_pose[wave][lane] = __hip_atomic_load(fr.pose + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            f_loaded = f;
+        }
+        const FrameDev cur = fr.cur;
+        lk_point<FAST>(a, ka, cur, s_pose[wave], i, (size_t)f * a.out_stride, s_win[wave][0], s_win[wave][1]);
+        return true;
+    };
+    // the items resident waves gave back (the drain only), then the heads;
+    // one loop, so the per-point code is inlined once
+    const int n_left = a.bg_drain ? min(__builtin_amdgcn_readfirstlane(__hip_atomic_load(
+                                            a.bg_left + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
+                                        kBgLeftCap)
+                                  : 0;
+    bool left_phase = n_left > 0;
+    int h = 0;
+    for (;;) {
+        int head = 0, k = 0;
+        if (left_phase) {
+            int j = 0;
+            if (lane == 0) j = atomicAdd(a.bg_left, 1);
+            j = __builtin_amdgcn_readfirstlane(j);
+            if (j >= n_left) {
+                left_phase = false;
+                continue;
+            }
+            int e = 0;
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            while ((e = __builtin_amdgcn_readfirstlane(
+                        __hip_atomic_load(a.bg_left + 32 + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) == 0) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > kBgWaitTicks) {
+                    if (lane == 0) atomicOr(a.bg_err, 1);
+                    return;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            head = (e - 1) / per_head;
+            k = (e - 1) - head * per_head;
+        } else {
+            if (h >= 8) break;
+            head = (xcc + h) & 7;
             if (lane == 0) k = atomicAdd(a.bg_next + 32 * head, 1);
             k = __builtin_amdgcn_readfirstlane(k);
-            if (k >= per_head) break;
-            const int f = k / seg, i = head * seg + (k - f * seg);
-            if (i >= a.n) continue;
-            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-            while (__builtin_amdgcn_readfirstlane(
-                       __hip_atomic_load(a.bg_ready + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0) {
-                if (__builtin_amdgcn_s_memrealtime() - t0 > kBgWaitTicks) {
-                    ok = false;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(4);
+            if (k >= per_head) {
+                ++h;
+                continue;
             }
-            if (!ok) {
-                if (lane == 0) atomicOr(a.bg_err, 1);
-                break;
-            }
-            const LkFrame& fr = ka->frames[f];
-            if (f != f_loaded) {  // wave-uniform
-                if (lane < 12)
-                    s_pose[wave][lane] =
-                        __hip_atomic_load(fr.pose + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                f_loaded = f;
-            }
-            const FrameDev cur = fr.cur;
-            lk_point<FAST>(a, ka, cur, s_pose[wave], i, (size_t)f * a.out_stride, s_win[wave][0], s_win[wave][1]);
         }
+        if (!run_item(head, k)) return;
     }
 }
 
