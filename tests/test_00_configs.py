@@ -62,22 +62,51 @@ def _oracle_stereo_poses(seed, n, W=1242, H=375):
 
 
 # ------------------------------------------------------------------ configs[1]
+_C1 = dict(W=1242, H=375, warm=5, steps=20)
+
+
+def _config1_oracle():
+    """The oracle's run of the config-1 workload (cached: the LK-mode variants
+    below compare against the same run)."""
+    if "oracle" not in _C1:
+        from viso_amd.shard import sequence_seed
+        from viso_amd.synth import Sequence
+        W, H, n = _C1["W"], _C1["H"], _C1["warm"] + _C1["steps"]
+        seq = Sequence(W, H, seed=sequence_seed(0))
+        left = np.stack([seq.image(f, 0) for f in range(n)])
+        right = np.stack([seq.image(f, 1) for f in range(n)])
+        ov = oracle_lib.Viso(seq.K, W, H, enable_tracking=1)
+        ov.set_stereo(seq.p.baseline, STEREO_MAX_DISP, 1)
+        for f in range(n):
+            ov.on_new_stereo(left[f], right[f])
+        _C1.update(seq=seq, left=left, right=right,
+                   oracle=dict(state=ov.state, points=ov.points(), poses=ov.poses(), stats=ov.stats(),
+                               alignment=ov.alignment()))
+    return _C1["oracle"]
+
+
 @pytest.mark.gpu
-def test_gpu_config1_bench_workload_matches_oracle():
+@pytest.mark.parametrize("lk", ["background", "leftovers", "batched"])
+def test_gpu_config1_bench_workload_matches_oracle(lk, monkeypatch):
     """bench.py --warmup 5 --steps 20 on one GPU, as the driver runs it: 5
     warm-up frames (frame 0's stereo pair creates the map), then one 20-frame
     chunk through viso_process_frames_device.  Every pose, the map, the last
-    frame's direct-pose nGood and LK alignment against the oracle."""
+    frame's direct-pose nGood and LK alignment against the oracle.  LK
+    alignment of the chunk in each of its forms: the chunk-
+    resident background grid (the product), the same with the resident waves'
+    patience cut to 1 us so the leftover list and the drain carry most items,
+    and the batched launch after the chain (VISO_LK_BG=0)."""
     import torch
 
     import viso_amd
-    from viso_amd.shard import sequence_seed
-    from viso_amd.synth import Sequence
-    W, H, warm, steps = 1242, 375, 5, 20
+    if lk == "leftovers":
+        monkeypatch.setenv("VISO_LK_BG_IDLE_US", "1")
+    if lk == "batched":
+        monkeypatch.setenv("VISO_LK_BG", "0")
+    o = _config1_oracle()
+    seq, left, right = _C1["seq"], _C1["left"], _C1["right"]
+    W, H, warm, steps = _C1["W"], _C1["H"], _C1["warm"], _C1["steps"]
     n = warm + steps
-    seq = Sequence(W, H, seed=sequence_seed(0))
-    left = np.stack([seq.image(f, 0) for f in range(n)])
-    right = np.stack([seq.image(f, 1) for f in range(n)])
     dl, dr = torch.from_numpy(left).cuda(), torch.from_numpy(right).cuda()
     torch.cuda.synchronize()
     v = viso_amd.Viso(*seq.K, width=W, height=H, enable_tracking=1, batch_frames=128)
@@ -88,21 +117,17 @@ def test_gpu_config1_bench_workload_matches_oracle():
     assert v.state == 1
     v.process_device(dl.data_ptr() + warm * fb, dr.data_ptr() + warm * fb, steps, fb)
     v.synchronize()
-    ov = oracle_lib.Viso(seq.K, W, H, enable_tracking=1)
-    ov.set_stereo(seq.p.baseline, STEREO_MAX_DISP, 1)
-    for f in range(n):
-        ov.on_new_stereo(left[f], right[f])
-    assert v.state == ov.state == 1
-    gp, op = v.GetPoints(), ov.points()
+    assert v.state == o["state"] == 1
+    gp, op = v.GetPoints(), o["points"]
     assert len(op) > 2000 and np.array_equal(gp, op)
-    gP, oP = v.poses, ov.poses()
+    gP, oP = v.poses, o["poses"]
     assert gP.shape == oP.shape == (n - 1, 12)
     assert _rel_rows(gP, oP).max() <= 1e-10  # north star: 1e-4
-    gs, os_ = v.stats(), ov.stats()
+    gs, os_ = v.stats(), o["stats"]
     for k in (6, 7, 9):  # LK pairs, LK successes, direct nGood (level 0)
         assert gs[k] == os_[k], (k, gs, os_)
     pk, sc, ub, ua = v.alignment()
-    opk, osc, oub, oua = ov.alignment()
+    opk, osc, oub, oua = o["alignment"]
     assert np.array_equal(pk, opk) and np.array_equal(sc, osc)
     assert np.max(np.abs(ua - oua)) < 1e-6
 

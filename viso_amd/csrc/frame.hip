@@ -413,6 +413,12 @@ int viso_ctx::bg_begin(const std::vector<int>& chunk) {
     a.bg_err = a.bg_next + 8 * 32;
     a.bg_left = a.bg_err + 32;
     a.bg_items = nb * n_map;
+    // tests: VISO_LK_BG_IDLE_US shortens the resident waves' patience, so the
+    // leftover list and the drain carry most items
+    if (const char* idle = getenv("VISO_LK_BG_IDLE_US")) {
+        const long us = strtol(idle, nullptr, 10);
+        if (us > 0 && us < 1000000) a.bg_idle = (unsigned int)(us * 100);
+    }
     // flags, heads and leftovers cleared behind the chunk's pyramid; the grid
     // (on the side stream's own hardware queue, create_streams) starts behind
     // them

@@ -86,6 +86,9 @@ struct LkAlignArgs {
     // leftovers: [0] drain cursor, [1] count, [32 ..] items (head * per_head + k)
     int* bg_left = nullptr;
     int bg_drain = 0;  // this launch is the end-of-chunk drain
+    // a resident wave's longest wait for its item's frame before handing the
+    // item to the drain (s_memrealtime ticks, 100 MHz)
+    unsigned int bg_idle = 30000;
 };
 void launch_lk_align(const LkAlignArgs& a, hipStream_t stream);
 // LK alignment of an ingest chunk's frames beside its direct-pose chain: grid

@@ -620,7 +620,8 @@ __global__ __launch_bounds__(256, FAST ? VISO_LK_MIN_WAVES_FAST : VISO_LK_MIN_WA
 // agent-scope: MI355X_MICROARCH.md's first sc1 hand-off row), and runs that
 // point's LKAlignment with the batched kernel's exact per-point code.  Every
 // wait is bounded: a resident wave whose item's frame is not ready within
-// kBgIdleTicks hands the item to the leftover list and leaves (the end-of-
+// LkAlignArgs::bg_idle (300 us: ~6 frames of the chain) hands the item to the
+// leftover list and leaves (the end-of-
 // chunk drain runs the leftovers first, then whatever the heads still hold),
 // so a grid that some serialisation of the queues put in the chain's way
 // steps aside; the drain's own waits beyond kBgWaitTicks set *bg_err.
@@ -628,7 +629,6 @@ __global__ __launch_bounds__(256, FAST ? VISO_LK_MIN_WAVES_FAST : VISO_LK_MIN_WA
 // padding, launched after the chunk's last pose: the items the resident grid
 // has not reached run beside it on every CU's remaining wave slots.
 constexpr unsigned long long kBgWaitTicks = 20000000ull;  // 200 ms of s_memrealtime
-constexpr unsigned long long kBgIdleTicks = 30000ull;      // 300 us: ~6 frames of the chain
 constexpr int kBgLeftCap = 4096;                           // leftover items (one per resident wave at most)
 template <bool FAST>
 __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
@@ -648,7 +648,7 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
         return __builtin_amdgcn_readfirstlane(
                    __hip_atomic_load(a.bg_ready + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0;
     };
-    // one item: wait for its frame (the resident grid at most kBgIdleTicks,
+    // one item: wait for its frame (the resident grid at most a.bg_idle ticks,
     // then the item goes to the leftover list and the wave leaves; the drain,
     // which runs once every pose is launched, at most kBgWaitTicks, an error),
     // then align the point
@@ -658,7 +658,7 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         while (!ready(f)) {
             const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t0;
-            if (!a.bg_drain && dt > kBgIdleTicks) {
+            if (!a.bg_drain && dt > (unsigned long long)a.bg_idle) {
                 if (lane == 0) {
                     // reserve a slot, then publish the item (+1: 0 = not yet
                     // written; the drain may read the count first)
