@@ -12,6 +12,7 @@
 // reference's shared_ptr<Keyframe> roles (ref_frame, last_frame, map
 // keyframes) are slot reference counts.
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <vector>
 
@@ -445,10 +446,12 @@ int viso_ctx::bg_launch() {
 
 int viso_ctx::bg_check() {
     if (!bg_unchecked || !bg_buf.ptr) return VISO_OK;
-    int err = 0;
-    VISO_HIP_CHECK(hipMemcpy(&err, (int*)bg_buf.ptr + kLkBatch + 8 * 32, sizeof(int), hipMemcpyDeviceToHost));
+    int w[3] = {0, 0, 0};  // error, items the drain ran, leftover cursor
+    VISO_HIP_CHECK(hipMemcpy(w, (int*)bg_buf.ptr + kLkBatch + 8 * 32, 2 * sizeof(int), hipMemcpyDeviceToHost));
     bg_unchecked = false;
-    return err ? VISO_ERR_HIP : VISO_OK;
+    if (getenv("VISO_LK_BG_STATS"))  // dev: how much of the last chunk the drain carried
+        fprintf(stderr, "viso lk-bg: %d frames x %d points, drain ran %d items, error %d\n", bg_nb, n_map, w[1], w[0]);
+    return w[0] ? VISO_ERR_HIP : VISO_OK;
 }
 
 // The chunk's last pose is launched: the items the resident grid has not

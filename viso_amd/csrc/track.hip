@@ -629,6 +629,10 @@ __global__ __launch_bounds__(256, FAST ? VISO_LK_MIN_WAVES_FAST : VISO_LK_MIN_WA
 // padding, launched after the chunk's last pose: the items the resident grid
 // has not reached run beside it on every CU's remaining wave slots.
 constexpr unsigned long long kBgWaitTicks = 20000000ull;  // 200 ms of s_memrealtime
+#ifndef VISO_LK_BG_TAKE
+#define VISO_LK_BG_TAKE 2
+#endif
+constexpr int kBgTake = VISO_LK_BG_TAKE;  // items per head dequeue (1 or 2)
 constexpr int kBgLeftCap = 4096;                           // leftover items (one per resident wave at most)
 template <bool FAST>
 __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
@@ -652,6 +656,18 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
     // then the item goes to the leftover list and the wave leaves; the drain,
     // which runs once every pose is launched, at most kBgWaitTicks, an error),
     // then align the point
+    auto give_back = [&](int head, int k) {
+        if (lane == 0) {
+            // reserve a slot, then publish the item (+1: 0 = not yet written;
+            // the drain may read the count first)
+            const int j = atomicAdd(a.bg_left + 1, 1);
+            if (j < kBgLeftCap)
+                __hip_atomic_store(a.bg_left + 32 + j, head * per_head + k + 1, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            else
+                atomicOr(a.bg_err, 1);
+        }
+    };
     auto run_item = [&](int head, int k) __attribute__((always_inline)) -> bool {
         const int f = k / seg, i = head * seg + (k - f * seg);
         if (i >= a.n) return true;
@@ -659,16 +675,7 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
         while (!ready(f)) {
             const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t0;
             if (!a.bg_drain && dt > (unsigned long long)a.bg_idle) {
-                if (lane == 0) {
-                    // reserve a slot, then publish the item (+1: 0 = not yet
-                    // written; the drain may read the count first)
-                    const int j = atomicAdd(a.bg_left + 1, 1);
-                    if (j < kBgLeftCap)
-                        __hip_atomic_store(a.bg_left + 32 + j, head * per_head + k + 1, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-                    else
-                        atomicOr(a.bg_err, 1);
-                }
+                give_back(head, k);
                 return false;
             }
             if (a.bg_drain && dt > kBgWaitTicks) {
@@ -698,9 +705,14 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
                                   : 0;
     bool left_phase = n_left > 0;
     int h = 0;
+    int pend_head = -1, pend_k = 0;  // the second item of the last dequeue
     for (;;) {
         int head = 0, k = 0;
-        if (left_phase) {
+        if (pend_head >= 0) {
+            head = pend_head;
+            k = pend_k;
+            pend_head = -1;
+        } else if (left_phase) {
             int j = 0;
             if (lane == 0) j = atomicAdd(a.bg_left, 1);
             j = __builtin_amdgcn_readfirstlane(j);
@@ -723,14 +735,23 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
         } else {
             if (h >= 8) break;
             head = (xcc + h) & 7;
-            if (lane == 0) k = atomicAdd(a.bg_next + 32 * head, 1);
+            // two items per dequeue: half the head round trips per item
+            if (lane == 0) k = atomicAdd(a.bg_next + 32 * head, kBgTake);
             k = __builtin_amdgcn_readfirstlane(k);
             if (k >= per_head) {
                 ++h;
                 continue;
             }
+            if (kBgTake > 1 && k + 1 < per_head) {
+                pend_head = head;
+                pend_k = k + 1;
+            }
         }
-        if (!run_item(head, k)) return;
+        if (!run_item(head, k)) {
+            if (pend_head >= 0) give_back(pend_head, pend_k);
+            return;
+        }
+        if (a.bg_drain && lane == 0) atomicAdd(a.bg_err + 1, 1);  // items the drain ran (stats)
     }
 }
 
