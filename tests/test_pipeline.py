@@ -41,6 +41,39 @@ def d_init_frame():
     return seqdata.initialised()["init_frame"]
 
 
+def _bg_items(n_frames, n, take=2):
+    """track.hip lk_item_kernel's work decomposition, restated: eight heads,
+    head x holding points [x seg, (x + 1) seg) of every frame, frames in
+    order; dequeues of `take` items; a leftover item published as
+    head * per_head + k + 1."""
+    seg = (n + 7) // 8
+    per_head = n_frames * seg
+    seen = []
+    for head in range(8):
+        last_f = -1
+        for k0 in range(0, per_head, take):
+            for k in range(k0, min(k0 + take, per_head)):
+                f = k // seg
+                i = head * seg + (k - f * seg)
+                assert f >= last_f  # frames in order within a head
+                last_f = f
+                e = head * per_head + k + 1  # leftover encoding round trip
+                assert ((e - 1) // per_head, (e - 1) % per_head) == (head, k)
+                if i < n:
+                    seen.append((f, i))
+    return seen
+
+
+@pytest.mark.parametrize("n_frames,n", [(1, 1), (20, 2465), (64, 2465), (3, 7), (5, 8), (2, 5666)])
+def test_background_lk_items_cover_every_point_once(n_frames, n):
+    """The background LK grid's eight heads cover every (frame, point) of a
+    chunk exactly once, with the frames in order within each head, so every
+    point's alignment is computed whichever wave (resident or drain) takes it."""
+    seen = _bg_items(n_frames, n)
+    assert len(seen) == n_frames * n
+    assert len(set(seen)) == n_frames * n
+
+
 def test_oracle_tracking_follows_ground_truth_rotation():
     seq = seqdata.sequence(0)
     v = oracle_lib.Viso(seq.K, W, H, enable_tracking=1)
