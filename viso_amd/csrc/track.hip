@@ -633,6 +633,12 @@ constexpr unsigned long long kBgWaitTicks = 20000000ull;  // 200 ms of s_memreal
 #define VISO_LK_BG_TAKE 2
 #endif
 constexpr int kBgTake = VISO_LK_BG_TAKE;  // items per head dequeue (1 or 2)
+// s_sleep quanta (64 cycles) between polls of a frame's ready flag: a
+// thousand waiting waves polling one line share the memory system with the
+// chain they wait for
+#ifndef VISO_LK_BG_POLL
+#define VISO_LK_BG_POLL 4
+#endif
 constexpr int kBgLeftCap = 4096;                           // leftover items (one per resident wave at most)
 template <bool FAST>
 __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
@@ -682,7 +688,7 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
                 if (lane == 0) atomicOr(a.bg_err, 1);
                 return false;
             }
-            __builtin_amdgcn_s_sleep(4);
+            __builtin_amdgcn_s_sleep(VISO_LK_BG_POLL);
         }
         const LkFrame& fr = ka->frames[f];
         if (f != f_loaded) {  // wave-uniform
