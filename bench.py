@@ -822,6 +822,11 @@ def main():
             "speedup_vs_cpu": round(value / world / cpu["value"], 1) if cpu else None,
             "kernels": {k: {"launches": t["launches"], "avg_ms": round(t["avg_ms"], 5)}
                         for k, t in timing.items()},
+            "kernels_note": ("lkalign: with the background LK grid (default; VISO_LK_BG=0 turns it off) "
+                             "one launch is the chunk-resident grid, so avg_ms spans its lifetime while "
+                             "it runs beside the direct chain, not the LK work of one frame"
+                             if os.environ.get("VISO_LK_BG", "1") != "0" else
+                             "lkalign: one launch = one batch of frames' LK alignment"),
             "kernels_breakdown_chunk": breakdown,
             "warmup_frames_run": warm,
             "init_frames_timed": frames_by_state["initialization"],

@@ -56,7 +56,7 @@ def main():
             f += k
 
     lib.viso_debug_probe_lk.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    lkbuf = (ctypes.c_ulonglong * 16)()
+    lkbuf = (ctypes.c_ulonglong * 24)()
     run(0, warm)
     v.synchronize()
     assert lib.viso_debug_probe_ring(log.ctypes.data, exits.ctypes.data, cap, ctypes.byref(nl), 1) == 0
@@ -74,6 +74,15 @@ def main():
     print(f"LK alignment: points {q[15]}, mean {q[14] / max(q[15], 1) * 0.01:.2f} us per point, slowest point "
           f"{q[9] * 0.01:.1f} us, most GN iterations of a point {q[10]}, points >= 20 us: {q[11]}, "
           f">= 10 iterations on a level: {q[8]}")
+    if q[19]:  # background LK: the last frame of the (last) chunk
+        first = (~q[16]) & 0xFFFFFFFFFFFFFFFF
+        print(f"background LK last frame: {q[19]} items ({q[20]} by the drain), first ready sighting -> last "
+              f"completion {(q[17] - first) * 0.01:.1f} us, last item start {(q[21] - first) * 0.01:.1f} us, "
+              f"slowest item {q[18] * 0.01:.1f} us")
+        if q[22]:
+            d0 = (~q[22]) & 0xFFFFFFFFFFFFFFFF
+            print(f"background LK drain: first drain wave -> last item of the chunk {(q[23] - d0) * 0.01:.1f} us; "
+                  f"last frame first sighted {(first - d0) * 0.01:+.1f} us from the first drain wave")
     us = 0.01  # 100 MHz ticks -> us
     meta = log[:, 15]
     lvl = (meta & 0xff) - 1

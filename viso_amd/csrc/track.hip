@@ -20,7 +20,7 @@
 
 #ifdef VISO_PROBE
 // [level] iterations summed, [4 + level] calls, [8 + level] window misses
-__device__ unsigned long long g_probe_lk[16];
+__device__ unsigned long long g_probe_lk[24];
 #endif
 
 namespace viso {
@@ -700,7 +700,28 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
             f_loaded = f;
         }
         const FrameDev cur = fr.cur;
+#ifdef VISO_PROBE
+        // the chunk's last frame: first ready sighting (16, stored inverted
+        // for atomicMax), last completion (17), slowest item (18), items (19),
+        // items the drain ran (20), last item start (21)
+        const bool pr_last = f == a.n_frames - 1;
+        const unsigned long long pr_s = __builtin_amdgcn_s_memrealtime();
+        if (pr_last && lane == 0) {
+            atomicMax(&g_probe_lk[16], ~pr_s);
+            atomicMax(&g_probe_lk[21], pr_s);
+        }
+#endif
         lk_point<FAST>(a, ka, cur, s_pose[wave], i, (size_t)f * a.out_stride, s_win[wave][0], s_win[wave][1]);
+#ifdef VISO_PROBE
+        if (lane == 0) atomicMax(&g_probe_lk[23], __builtin_amdgcn_s_memrealtime());  // any item's end
+        if (pr_last && lane == 0) {
+            const unsigned long long pr_e = __builtin_amdgcn_s_memrealtime();
+            atomicMax(&g_probe_lk[17], pr_e);
+            atomicMax(&g_probe_lk[18], pr_e - pr_s);
+            atomicAdd(&g_probe_lk[19], 1ull);
+            if (a.bg_drain) atomicAdd(&g_probe_lk[20], 1ull);
+        }
+#endif
         return true;
     };
     // the items resident waves gave back (the drain only), then the heads;
@@ -710,6 +731,9 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
                                         kBgLeftCap)
                                   : 0;
     bool left_phase = n_left > 0;
+#ifdef VISO_PROBE
+    if (a.bg_drain && lane == 0) atomicMax(&g_probe_lk[22], ~__builtin_amdgcn_s_memrealtime());  // drain start
+#endif
     int h = 0;
     int pend_head = -1, pend_k = 0;  // the second item of the last dequeue
     for (;;) {
@@ -857,10 +881,10 @@ void launch_lk_template(const LkAlignArgs& a, hipStream_t stream) {
 
 #ifdef VISO_PROBE
 extern "C" int viso_debug_probe_lk(unsigned long long* out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_probe_lk), sizeof(unsigned long long) * 16) != hipSuccess)
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_probe_lk), sizeof(unsigned long long) * 24) != hipSuccess)
         return -2;
     if (reset) {
-        static unsigned long long zero[16] = {};
+        static unsigned long long zero[24] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_probe_lk), zero, sizeof(zero)) != hipSuccess) return -2;
     }
     return 0;
