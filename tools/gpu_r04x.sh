@@ -1,0 +1,27 @@
+#!/bin/bash
+# Round-4 dev A/B: LK windows that follow a drifting point (the follow
+# variant) against HEAD's library: the LK / KLT / pipeline / config parity
+# tests on the variant, its background-grid tail probe, then driver-argument
+# and default bench lines for both libraries.
+set -o pipefail
+OUT=gpurun_out/${1:-r04x}
+mkdir -p $OUT
+export TMPDIR=/tmp
+F=$PWD/viso_amd/libviso_amd_follow.so
+VISO_LIB=$F timeout -k 10 300 python -u -m pytest tests/test_00_configs.py tests/test_track.py tests/test_pipeline.py tests/test_golden.py tests/test_fast_mode.py tests/test_keyframes.py -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest.log; exit 1; }
+tail -1 $OUT/pytest.log
+BATCH=20 STEPS=20 timeout -k 10 120 python -u tools/probe_direct.py > $OUT/probe_20.log 2>&1 || { tail -20 $OUT/probe_20.log; exit 1; }
+grep "LK" $OUT/probe_20.log
+summ() { python -c "
+import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+b=d['kernels_breakdown_chunk']
+print(f\"{sys.argv[2]:22s} {d['value']:9.1f} frames/s  ms/step {d['ms_per_step']:.4f}  direct {b['direct']['avg_ms']*1e3:6.2f} us/frame  parity {d['parity_vs_oracle']['max_rel_frobenius'] if d.get('parity_vs_oracle') else '-'}\")" $1 $2; }
+for rep in 1 2; do
+for lib in follow head; do
+  if [ $lib = follow ]; then export VISO_LIB=$F; else unset VISO_LIB; fi
+  timeout -k 10 200 python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu --no-svo --rig-steps 0 > $OUT/${lib}_d$rep.json 2> $OUT/${lib}_d$rep.err || { tail -20 $OUT/${lib}_d$rep.err; exit 1; }
+  summ $OUT/${lib}_d$rep.json "$lib-driverargs"
+  timeout -k 10 200 python -u bench.py --no-cpu --no-svo --rig-steps 0 > $OUT/${lib}_f$rep.json 2> $OUT/${lib}_f$rep.err || { tail -20 $OUT/${lib}_f$rep.err; exit 1; }
+  summ $OUT/${lib}_f$rep.json "$lib-default"
+done
+done

@@ -56,7 +56,7 @@ def main():
             f += k
 
     lib.viso_debug_probe_lk.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    lkbuf = (ctypes.c_ulonglong * 24)()
+    lkbuf = (ctypes.c_ulonglong * 32)()
     run(0, warm)
     v.synchronize()
     assert lib.viso_debug_probe_ring(log.ctypes.data, exits.ctypes.data, cap, ctypes.byref(nl), 1) == 0
@@ -74,6 +74,8 @@ def main():
     print(f"LK alignment: points {q[15]}, mean {q[14] / max(q[15], 1) * 0.01:.2f} us per point, slowest point "
           f"{q[9] * 0.01:.1f} us, most GN iterations of a point {q[10]}, points >= 20 us: {q[11]}, "
           f">= 10 iterations on a level: {q[8]}")
+    print(f"LK alignment: slowest point {(q[24] >> 16) * 0.01:.1f} us with {q[24] & 0xffff} GN iterations; "
+          f"most-iterated point {q[25] >> 40} iterations in {(q[25] & ((1 << 40) - 1)) * 0.01:.1f} us")
     if q[19]:  # background LK: the last frame of the (last) chunk
         first = (~q[16]) & 0xFFFFFFFFFFFFFFFF
         print(f"background LK last frame: {q[19]} items ({q[20]} by the drain), first ready sighting -> last "

@@ -20,7 +20,7 @@
 
 #ifdef VISO_PROBE
 // [level] iterations summed, [4 + level] calls, [8 + level] window misses
-__device__ unsigned long long g_probe_lk[24];
+__device__ unsigned long long g_probe_lk[32];
 #endif
 
 namespace viso {
@@ -577,6 +577,10 @@ __device__ __attribute__((always_inline)) inline void lk_point(const LkAlignArgs
                 atomicMax(&g_probe_lk[9], pr_el);  // slowest point (100 MHz ticks)
                 atomicMax(&g_probe_lk[10], pr_it[0] + pr_it[1] + pr_it[2] + pr_it[3]);
                 if (pr_el >= 2000) atomicAdd(&g_probe_lk[11], 1ull);  // points >= 20 us
+                const unsigned long long pr_n = pr_it[0] + pr_it[1] + pr_it[2] + pr_it[3];
+                // the slowest point's iterations (24), the most-iterated point's time (25)
+                atomicMax(&g_probe_lk[24], (pr_el << 16) | (pr_n < 65535 ? pr_n : 65535));
+                atomicMax(&g_probe_lk[25], (pr_n << 40) | (pr_el < (1ull << 40) ? pr_el : (1ull << 40) - 1));
                 atomicAdd(&g_probe_lk[15], 1ull);
             }
 #endif
@@ -881,10 +885,10 @@ void launch_lk_template(const LkAlignArgs& a, hipStream_t stream) {
 
 #ifdef VISO_PROBE
 extern "C" int viso_debug_probe_lk(unsigned long long* out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_probe_lk), sizeof(unsigned long long) * 24) != hipSuccess)
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_probe_lk), sizeof(unsigned long long) * 32) != hipSuccess)
         return -2;
     if (reset) {
-        static unsigned long long zero[24] = {};
+        static unsigned long long zero[32] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_probe_lk), zero, sizeof(zero)) != hipSuccess) return -2;
     }
     return 0;
