@@ -1,14 +1,14 @@
 #!/bin/bash
 # Round-4 dev A/B: LK windows that follow a drifting point (the follow
 # variant) against HEAD's library: the LK / KLT / pipeline / config parity
-# tests on the variant, its background-grid tail probe, then driver-argument
+# tests (the whole GPU suite) on the variant, its background-grid tail probe, then driver-argument
 # and default bench lines for both libraries.
 set -o pipefail
 OUT=gpurun_out/${1:-r04x}
 mkdir -p $OUT
 export TMPDIR=/tmp
 F=$PWD/viso_amd/libviso_amd_follow.so
-VISO_LIB=$F timeout -k 10 300 python -u -m pytest tests/test_00_configs.py tests/test_track.py tests/test_pipeline.py tests/test_golden.py tests/test_fast_mode.py tests/test_keyframes.py -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest.log; exit 1; }
+VISO_LIB=$F timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread --durations=25 > $OUT/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest.log; exit 1; }
 tail -1 $OUT/pytest.log
 BATCH=20 STEPS=20 timeout -k 10 120 python -u tools/probe_direct.py > $OUT/probe_20.log 2>&1 || { tail -20 $OUT/probe_20.log; exit 1; }
 grep "LK" $OUT/probe_20.log

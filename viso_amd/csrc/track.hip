@@ -40,9 +40,10 @@ struct LkResult {
 };
 
 // Per-wave LDS window of the current image around the patch's starting
-// position.  A sample whose four taps lie inside the window (which itself
-// lies inside the image, so no tap wraps a row or leaves the buffer) reads
-// the same bytes from LDS; any other sample takes sample_px's global path.
+// position (inside the image), re-placed by window_follow when the point
+// leaves it.  A sample whose four taps lie inside the window reads the same
+// bytes from LDS as sample_px would from the buffer; any other sample takes
+// sample_px's global path.
 constexpr int kWinW = 24, kWinH = 24;
 
 struct Window {
@@ -109,11 +110,7 @@ __device__ inline Window load_window(uint8_t* lds, const uint8_t* img, int w, in
     return window_commit(lds, window_issue(img, w, h, cx, cy));
 }
 
-// sample_px with the tap fetch served from the window when possible.  The
-// window test is taken for the whole wave (one ballot): in the common case
-// every lane's taps are in the window and the wave runs the LDS path without
-// per-lane branching; otherwise each lane takes its own path.  Requires all
-// 64 lanes active (the LK engines' wave-uniform control flow).
+// GetPixelValue's bilinear sample with its four taps read from the window
 __device__ inline double win_bilinear(const Window& win, double x, double y, int ix, int iy) {
     const int o = (iy - win.y0) * kWinW + (ix - win.x0);
     const double d0 = (double)ld_lds_u8(win.lds, o), d1 = (double)ld_lds_u8(win.lds, o + 1);
@@ -124,20 +121,69 @@ __device__ inline double win_bilinear(const Window& win, double x, double y, int
     return double((1 - xx) * (1 - yy) * d0 + xx * (1 - yy) * d1 + (1 - xx) * yy * d2 + xx * yy * d3);
 }
 
-// FINITE: the caller guarantees |x|, |y| < 1e9 (LKAlignment: the bounds test
-// passed, so d is within a level of the patch), which sample_px's own guard
-// would find true
+// The GN iterations' window follows the point: once the wave's taps leave
+// the window, it is re-placed at the patch's new position and refilled, so
+// the following iterations read LDS instead of paying a global round trip
+// each.  A re-placed window is a window of the level's continuous buffer, not
+// of the image: its origin (x0, y0) is not clamped to the image, and byte
+// (r, c) is buffer[(y0 + r) w + x0 + c], 0 outside the buffer — exactly the
+// byte sample_px's tap (x0 + c, y0 + r) reads (its row-wrapping and zero
+// rules included), so points at or over the image border (the slowest ones:
+// up to ~130 GN iterations) are served from LDS too.  Lane 0 holds the
+// patch's smallest (ix, iy) (the lanes' integer offsets on a common base).
+// Returns false (window unchanged) when some lane's coordinates are not
+// finite; the caller then takes its global path.  A wave only overwrites its
+// own window, whose earlier reads have all returned (their values fed the
+// previous update).
+__device__ inline bool window_follow(const uint8_t* __restrict__ img, int w, int h, int ix, int iy, bool ok,
+                                    Window& win) {
+    if (__builtin_amdgcn_ballot_w64(!ok) != 0) return false;
+    // the patch spans <= 9 taps per axis: 7 to spare on each side
+    const int x0 = __builtin_amdgcn_readfirstlane(ix) - 7;
+    const int y0 = __builtin_amdgcn_readfirstlane(iy) - 7;
+    const bool in = (unsigned)(ix - x0) < (unsigned)(kWinW - 1) && (unsigned)(iy - y0) < (unsigned)(kWinH - 1);
+    if (__builtin_amdgcn_ballot_w64(in) != ~0ull) return false;
+    // the nine loads, then the LDS stores (window_issue / window_commit's
+    // forms).  The lane index is made opaque here: its nine window offsets
+    // would otherwise be hoisted out of the GN loop and held in registers.
+    int lane = threadIdx.x & 63;
+    asm volatile("" : "+v"(lane));
+    const long long n = (long long)w * (long long)h;
+    const long long base = (long long)y0 * (long long)w + (long long)x0;
+    uint8_t v[kWinPer];
+#pragma unroll
+    for (int k = 0; k < kWinPer; ++k) {
+        const int e = lane + 64 * k;
+        const int rr = e / kWinW, c = e - rr * kWinW;
+        v[k] = (uint8_t)ld_u8_or0(img, n, base + (long long)rr * w + c);
+    }
+    uint8_t* lds = const_cast<uint8_t*>(win.lds);
+#pragma unroll
+    for (int k = 0; k < kWinPer; ++k) st_lds_u8(lds, lane + 64 * k, v[k]);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    win.x0 = x0;
+    win.y0 = y0;
+    return true;
+}
+
+// sample_px with the tap fetch served from the window (re-placed by
+// window_follow when the wave leaves it).  The window test is taken for the
+// whole wave (one ballot, every lane active: the LK engines' wave-uniform
+// control flow).  FINITE: the caller guarantees |x|, |y| < 1e9 (LKAlignment:
+// the bounds test passed, so d is within a level of the patch), which
+// sample_px's own guard would find true.
 template <bool FINITE = false>
-__device__ inline double sample_win(const uint8_t* __restrict__ img, int w, int h, double x,
-                                    double y, const Window& win) {
+__device__ inline double sample_win_follow(const uint8_t* __restrict__ img, int w, int h, double x,
+                                           double y, Window& win) {
     if (!win.lds) return sample_px(img, w, h, x, y);  // wave-uniform (window_issue)
     const bool finite = FINITE || (x > -1e9 && x < 1e9 && y > -1e9 && y < 1e9);
     const int ix = finite ? (int)x : 0, iy = finite ? (int)y : 0;
-    // (unsigned offsets: one compare per axis; every lane is active here, so
-    // "all lanes in" is the ballot of `in` equal to the full mask)
     const bool in = finite && (unsigned)(ix - win.x0) < (unsigned)(kWinW - 1) &&
                     (unsigned)(iy - win.y0) < (unsigned)(kWinH - 1);
     if (__builtin_expect(__builtin_amdgcn_ballot_w64(in) == ~0ull, 1)) return win_bilinear(win, x, y, ix, iy);
+    if (window_follow(img, w, h, ix, iy, finite, win)) return win_bilinear(win, x, y, ix, iy);
     return in ? win_bilinear(win, x, y, ix, iy) : sample_px(img, w, h, x, y);
 }
 
@@ -184,7 +230,7 @@ template <int MAXIT, bool KLT_BOUNDS>
 __device__ inline LkResult lk_iterate(const LkTemplate& t, int w1, int h1,
                                       const uint8_t* __restrict__ img2, int w2, int h2,
                                       double cur_x, double cur_y, double bx, double by, double dx,
-                                      double dy, double thresh, const Window& win) {
+                                      double dy, double thresh, Window win) {
     const double hp = 4.0;
     // the control values are wave-uniform (the sums are read from one lane):
     // said so to the compiler, the loop's branches need no EXEC bookkeeping
@@ -217,7 +263,7 @@ __device__ inline LkResult lk_iterate(const LkTemplate& t, int w1, int h1,
             succ = false;
             break;
         }
-        const double e = t.I1 - sample_win<!KLT_BOUNDS>(img2, w2, h2, cur_x + dx, cur_y + dy, win);
+        const double e = t.I1 - sample_win_follow<!KLT_BOUNDS>(img2, w2, h2, cur_x + dx, cur_y + dy, win);
         double B0, B1;
         if (KLT_BOUNDS)
             wave_tree_sum3(-t.J0 * e, -t.J1 * e, e * e, B0, B1, cost);
@@ -247,7 +293,7 @@ template <int MAXIT>
 __device__ inline LkResult lk_iterate_fast(float I1, float J0, float J1, const float* ih, int w1, int h1,
                                            const uint8_t* __restrict__ img2, int w2, int h2, double ox,
                                            double oy, int px, int py, double bx, double by, double thresh,
-                                           const Window& win) {
+                                           Window win) {
     const double hp = 4.0;
     double dx = 0.0, dy = 0.0;
     float lastCost = 0.0f;
@@ -270,8 +316,11 @@ __device__ inline LkResult lk_iterate_fast(float I1, float J0, float J1, const f
         const float xx = (float)(X - fX), yy = (float)(Y - fY);
         const int ix = (int)fX + px, iy = (int)fY + py;
         float t0, t1, t2, t3;
-        if (__builtin_expect(win.lds && ix >= win.x0 && ix + 1 < win.x0 + kWinW && iy >= win.y0 &&
-                             iy + 1 < win.y0 + kWinH, 1)) {
+        bool in = win.lds && ix >= win.x0 && ix + 1 < win.x0 + kWinW && iy >= win.y0 && iy + 1 < win.y0 + kWinH;
+        // (X, Y finite: the bounds test passed)
+        if (win.lds && __builtin_amdgcn_ballot_w64(in) != ~0ull && window_follow(img2, w2, h2, ix, iy, true, win))
+            in = true;
+        if (__builtin_expect(in, 1)) {
             const int o = (iy - win.y0) * kWinW + (ix - win.x0);
             t0 = (float)ld_lds_u8(win.lds, o);
             t1 = (float)ld_lds_u8(win.lds, o + 1);
