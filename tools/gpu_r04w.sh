@@ -16,4 +16,3 @@ timeout -k 10 300 python -u bench.py > $OUT/bench_default.json 2> $OUT/bench_def
 echo default ok
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o bench -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu > $OUT/bench_prof.json 2> $OUT/bench_prof.err || { tail -20 $OUT/bench_prof.err; exit 1; }
 echo prof ok
-bash tools/gpu_r04v.sh ${1:-r04w}_probe
