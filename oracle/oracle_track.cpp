@@ -247,6 +247,19 @@ void direct_single_layer(const PyrView& last, const PyrView& cur, const double K
     }
 }
 
+// Optional per-iteration trace of LKAlignment (analysis tooling only,
+// tools/lk_trace.py): rows of (point, level, iter, X, Y, cost) where (X, Y)
+// is the patch origin's current-image coordinate the iteration samples at.
+struct LkTrace {
+    double* buf = nullptr;
+    long cap = 0, n = 0;
+    int point = -1;
+};
+LkTrace& lk_trace() {
+    static LkTrace t;
+    return t;
+}
+
 // LKAlignmentSingle for one pair at one level (src/viso.cpp:855-918)
 void lk_pair_level(const PyrView& ref, const PyrView& cur, int level, const double uv_ref[2],
                    double uv_cur[2], bool& succ_out, double thresh) {
@@ -289,6 +302,15 @@ void lk_pair_level(const PyrView& ref, const PyrView& cur, int level, const doub
         // wave_tree_sum3_desc); H keeps the ascending tree (device lk_prepare)
         const double B0 = acc_sum_desc64(b0), B1 = acc_sum_desc64(b1);
         cost = acc_sum_desc64(cc);
+        if (lk_trace().buf && lk_trace().n < lk_trace().cap) {
+            double* r = lk_trace().buf + 6 * lk_trace().n++;
+            r[0] = lk_trace().point;
+            r[1] = level;
+            r[2] = iter;
+            r[3] = uv_cur[0] * s + dx;
+            r[4] = uv_cur[1] * s + dy;
+            r[5] = cost;
+        }
         const double invdet = 1.0 / (H00 * H11 - H10 * H01);
         const double i00 = H11 * invdet, i10 = -H10 * invdet, i01 = -H01 * invdet, i11 = H00 * invdet;
         const double u0 = i00 * B0 + i01 * B1;
@@ -341,6 +363,13 @@ void oracle_klt(const uint8_t* ref_pyr, const uint8_t* cur_pyr, int w, int h, co
             for (int j = 0; j < 2 * n; ++j) kp2[j] = (float)((double)kp2[j] / 0.5);
     }
 }
+
+void oracle_lk_trace(double* buf, long cap) {
+    lk_trace().buf = buf;
+    lk_trace().cap = cap;
+    lk_trace().n = 0;
+}
+long oracle_lk_trace_count(void) { return lk_trace().n; }
 
 void oracle_se3_exp_left(const double xi[6], const double pose_in[12], double pose_out[12]) {
     SE3 a = se3_from_Rt(pose_in, pose_in + 9);
@@ -427,6 +456,7 @@ void oracle_lk_align(const uint8_t* const* kf_pyrs, const double* kf_poses, int 
         uv_before[2 * i] = uc;
         uv_before[2 * i + 1] = vc;
         PyrView R = make_view(kf_pyrs[best], w, h);
+        lk_trace().point = i;
         bool succ = false;
         for (int level = kLevels - 1; level >= 0; --level)
             lk_pair_level(R, C, level, best_uv, uvc, succ, photometric_thresh);

@@ -90,6 +90,10 @@ void oracle_se3_exp_left(const double xi[6], const double pose_in[12], double po
 //   pair_kf[i]   : chosen keyframe index or -1 (no pair)
 //   success[i]   : level-0 success of the pair (0 when no pair)
 //   uv_before[2i], uv_after[2i] : projection into cur / aligned position.
+// Analysis tooling: record LKAlignment's iterations into buf (6 doubles per
+// row: point, level, iter, X, Y, cost; at most cap rows); buf NULL disables.
+void oracle_lk_trace(double* buf, long cap);
+long oracle_lk_trace_count(void);
 void oracle_lk_align(const uint8_t* const* kf_pyrs, const double* kf_poses, int n_kf,
                      const uint8_t* cur_pyr, const double cur_pose[12], int w, int h,
                      const double K[4], const double* points, int n_points,

@@ -34,6 +34,8 @@ SIG = {
     "oracle_se3_exp_left": ([_vp, _vp, _vp], None),
     "oracle_lk_align": ([_vp, _vp, _i, _vp, _vp, _i, _i, _vp, _vp, _i, _d, _vp, _vp, _vp, _vp],
                         None),
+    "oracle_lk_trace": ([_vp, ctypes.c_long], None),
+    "oracle_lk_trace_count": ([], ctypes.c_long),
     "oracle_triangulate": ([_vp, _vp, _vp, _vp, _vp], None),
     "oracle_ransac_essential": ([_vp, _vp, _i, _d, _d, _i, ctypes.c_uint64, _vp, _vp, _vp], _i),
     "oracle_ransac_homography": ([_vp, _vp, _i, _d, _d, _i, ctypes.c_uint64, _vp, _vp, _vp], _i),

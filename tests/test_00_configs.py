@@ -86,7 +86,7 @@ def _config1_oracle():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("lk", ["background", "leftovers", "batched"])
+@pytest.mark.parametrize("lk", ["background", "leftovers", "shared-queue", "batched"])
 def test_gpu_config1_bench_workload_matches_oracle(lk, monkeypatch):
     """bench.py --warmup 5 --steps 20 on one GPU, as the driver runs it: 5
     warm-up frames (frame 0's stereo pair creates the map), then one 20-frame
@@ -95,7 +95,13 @@ def test_gpu_config1_bench_workload_matches_oracle(lk, monkeypatch):
     alignment of the chunk in each of its forms: the chunk-
     resident background grid (the product), the same with the resident waves'
     patience cut to 1 us so the leftover list and the drain carry most items,
-    and the batched launch after the chain (VISO_LK_BG=0)."""
+    the side stream as a plain stream (VISO_LK_QUEUE=shared), which can put
+    the resident grid on the context stream's hardware queue in front of the
+    chain it waits for (the round-4 failure, DESIGN.md §5: its waves time
+    out, hand their items to the leftover list and leave; the drain runs
+    them), and the batched launch after the chain (VISO_LK_BG=0).  A wait
+    that ran out sets the grid's error word, which v.synchronize() and the LK
+    getters raise, so parity here also means bg_err == 0."""
     import torch
 
     import viso_amd
@@ -103,6 +109,8 @@ def test_gpu_config1_bench_workload_matches_oracle(lk, monkeypatch):
         monkeypatch.setenv("VISO_LK_BG_IDLE_US", "1")
     if lk == "batched":
         monkeypatch.setenv("VISO_LK_BG", "0")
+    if lk == "shared-queue":
+        monkeypatch.setenv("VISO_LK_QUEUE", "shared")
     o = _config1_oracle()
     seq, left, right = _C1["seq"], _C1["left"], _C1["right"]
     W, H, warm, steps = _C1["W"], _C1["H"], _C1["warm"], _C1["steps"]

@@ -28,6 +28,11 @@ constexpr int kRing = 4096;
 __device__ unsigned long long g_entry[kRing];
 __device__ unsigned long long g_exit[kRing];
 __device__ unsigned long long g_first_exit[kRing];
+// PLAIN mode (-DPLAIN_STAMPS): exit stamps by plain stores to one slot per
+// block (no same-address atomics: 247 serialised atomicMax / atomicMin per
+// launch take several us after the last stamp and were counted as "gap")
+constexpr int kMaxBlocks = 256;
+__device__ unsigned long long g_exit_blk[kRing][kMaxBlocks];
 
 template <int AB>
 struct Args {
@@ -53,8 +58,12 @@ __global__ __launch_bounds__(THREADS) void chain_kernel(const double* __restrict
         while (__builtin_amdgcn_s_memrealtime() < t0 + (unsigned long long)a.spin) __builtin_amdgcn_s_sleep(2);
     if (threadIdx.x == 0) {
         const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+#ifdef PLAIN_STAMPS
+        g_exit_blk[slot][blockIdx.x] = t1;
+#else
         atomicMax(&g_exit[slot], t1);
         atomicMin(&g_first_exit[slot], t1);
+#endif
     }
     (void)g;
     (void)hdr;
@@ -115,6 +124,17 @@ int run(const char* name, int blocks, int n, Result* out, int spin = 0, bool gra
     std::vector<unsigned long long> en(kRing), ex(kRing);
     CHECK(hipMemcpyFromSymbol(en.data(), HIP_SYMBOL(g_entry), sizeof(unsigned long long) * kRing));
     CHECK(hipMemcpyFromSymbol(ex.data(), HIP_SYMBOL(g_exit), sizeof(unsigned long long) * kRing));
+#ifdef PLAIN_STAMPS
+    {
+        std::vector<unsigned long long> eb((size_t)kRing * kMaxBlocks);
+        CHECK(hipMemcpyFromSymbol(eb.data(), HIP_SYMBOL(g_exit_blk), sizeof(unsigned long long) * eb.size()));
+        for (int i = 0; i < n; ++i) {
+            unsigned long long m = 0;
+            for (int b = 0; b < blocks; ++b) m = std::max(m, eb[(size_t)i * kMaxBlocks + b]);
+            ex[i] = m;
+        }
+    }
+#endif
     std::vector<double> gap, span;
     for (int i = 1; i < n; ++i) gap.push_back((double)(en[i] - ex[i - 1]) / 100.0);
     for (int i = 0; i < n; ++i) span.push_back((double)(ex[i] - en[i]) / 100.0);

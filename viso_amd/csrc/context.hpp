@@ -246,7 +246,7 @@ struct viso_ctx {
     // bg_end once the chunk's last pose is launched
     bool bg_eligible();
     int bg_begin(const std::vector<int>& chunk);
-    int bg_end();
+    int bg_end(bool drain = true);
     // after a host sync: VISO_ERR_HIP if a background launch since the last
     // check timed out waiting for a pose (its LK outputs are then invalid)
     int bg_check();

@@ -1138,11 +1138,15 @@ __global__ __launch_bounds__(kThreads, 4) void direct_level_kernel(const double*
                        a.s.good + lv * kMaxTiles, s_pts, &s_good, &s_cnt);
     }
 #ifdef VISO_PROBE
-    // block 0 exit: its stamps to the launch's ring slot; every block raises
-    // the launch's exit stamp (non-returning atomic)
+    // block 0 exit: its stamps to the launch's ring slot.  The exit stamp is
+    // taken behind a block barrier, so it is the block's last wave (the
+    // last-arriver tile trees finish after wave 0's points)
+    __syncthreads();
     const unsigned long long t_exit = __builtin_amdgcn_s_memrealtime();
     const int slot = a.probe_seq & (kPRing - 1);
-    if (t == 0) atomicMax(&g_pexit[slot], t_exit);
+    // (no same-address atomic here: 247 serialised atomics per launch ran for
+    // ~2 us after the last stamp and were counted as launch boundary; the
+    // launch's exit is the maximum of the per-block stamps, host side)
     if (t == 0 && blockIdx.x < 256) g_pblk[a.probe_seq & (kPRingB - 1)][blockIdx.x][3] = t_exit;
     if (blockIdx.x == 0 && t == 0) {
         pst[11] = t_exit;
@@ -1549,7 +1553,9 @@ __global__ __launch_bounds__(kRigThreads) void rig_level_kernel(const char* __re
 #ifdef VISO_PROBE
     const unsigned long long t_exit = __builtin_amdgcn_s_memrealtime();
     const int slot = a.probe_seq & (kPRing - 1);
-    if (t == 0) atomicMax(&g_pexit[slot], t_exit);
+    // (no same-address atomic here: 247 serialised atomics per launch ran for
+    // ~2 us after the last stamp and were counted as launch boundary; the
+    // launch's exit is the maximum of the per-block stamps, host side)
     if (t == 0 && blockIdx.x < 256) g_pblk[a.probe_seq & (kPRingB - 1)][blockIdx.x][3] = t_exit;
     if (blockIdx.x == 0 && t == 0) {
         pst[11] = t_exit;
@@ -1835,6 +1841,18 @@ extern "C" int viso_debug_probe_ring(unsigned long long* log, unsigned long long
         const int s = (n - m + i) & (kPRing - 1);
         for (int k = 0; k < kPSt; ++k) log[(size_t)i * kPSt + k] = hlog[s][k];
         exits[i] = hexit[s];
+    }
+    // launch exits: the maximum of the per-block exit stamps (kept for the
+    // last kPRingB launches)
+    {
+        static unsigned long long hb[kPRingB][256][4];
+        if (hipMemcpyFromSymbol(hb, HIP_SYMBOL(g_pblk), sizeof(hb)) != hipSuccess) return -2;
+        for (int i = std::max(0, m - kPRingB); i < m; ++i) {
+            const int sb = (n - m + i) & (kPRingB - 1);
+            unsigned long long mx = 0;
+            for (int b = 0; b < 256; ++b) mx = std::max(mx, hb[sb][b][3]);
+            exits[i] = mx;
+        }
     }
     *n_launches = n;
     if (reset) {

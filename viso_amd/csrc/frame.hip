@@ -359,7 +359,12 @@ int viso_ctx::resolve_direct() {
 
 int viso_ctx::finish_call(hipStream_t ls) {
     int rc = resolve_direct();
-    if (rc) return rc;
+    if (rc) {
+        // still tear the background state down (its held frames, the pending
+        // ready-flag owner), so the next call does not inherit a dead chunk
+        if (bg_active) (void)bg_end(false);
+        return rc;
+    }
     if (bg_active) {
         rc = bg_end();
         if (rc) return rc;
@@ -446,6 +451,9 @@ int viso_ctx::bg_launch() {
 
 int viso_ctx::bg_check() {
     if (!bg_unchecked || !bg_buf.ptr) return VISO_OK;
+    // the drain runs on the context stream (bg_end): its words are final only
+    // once that stream has passed it
+    VISO_HIP_CHECK(hipStreamSynchronize(stream));
     int w[3] = {0, 0, 0};  // error, items the drain ran, leftover cursor
     VISO_HIP_CHECK(hipMemcpy(w, (int*)bg_buf.ptr + kLkBatch + 8 * 32, 2 * sizeof(int), hipMemcpyDeviceToHost));
     bg_unchecked = false;
@@ -459,11 +467,16 @@ int viso_ctx::bg_check() {
 // context stream), then the context stream waits for the resident grid (its
 // outputs, the held frames), which is the latest LK batch of the flush_lk
 // bookkeeping.
-int viso_ctx::bg_end() {
-    LkAlignArgs d = bg_args;
-    d.bg_drain = 1;
-    launch_lk_drain(d, 3 * n_cu, stream);
-    VISO_HIP_CHECK(hipGetLastError());
+int viso_ctx::bg_end(bool drain) {
+    // (drain = false: the error path of finish_call; the chunk's last pose was
+    // not launched, so no drain runs: the resident grid's waves give their
+    // items back and leave, and the context stream only waits for them)
+    if (drain) {
+        LkAlignArgs d = bg_args;
+        d.bg_drain = 1;
+        launch_lk_drain(d, 3 * n_cu, stream);
+        VISO_HIP_CHECK(hipGetLastError());
+    }
     VISO_HIP_CHECK(hipStreamWaitEvent(stream, bg_done, 0));
     lk_last_rows = bg_nb;
     lk_last_pts = n_map;

@@ -21,6 +21,13 @@
 #ifdef VISO_PROBE
 // [level] iterations summed, [4 + level] calls, [8 + level] window misses
 __device__ unsigned long long g_probe_lk[32];
+// per item of the background chunk's last frame (row = map point):
+// [0] wait start, [1] start (frame ready, pose loaded), [2..5] level 3..0
+// iteration start, [6..9] level 3..0 iteration end, [10] end, [11] GN
+// iterations L3 | L2 << 16 | L1 << 32 | L0 << 48, [12] HW_ID | XCC << 32 |
+// drain << 40 | 1 << 48, [13] window refills, [14] dequeue stamp
+constexpr int kProbeItems = 16384;
+__device__ unsigned long long g_probe_items[kProbeItems][16];
 #endif
 
 namespace viso {
@@ -506,7 +513,8 @@ __global__ __launch_bounds__(256) void lk_template_kernel(LkAlignArgs a) {
 template <bool FAST>
 __device__ __attribute__((always_inline)) inline void lk_point(const LkAlignArgs& a, const LkAlignArgs* ka,
                                                                const FrameDev& cur, const double* cur_pose, int i,
-                                                               size_t o, uint8_t* my_win0, uint8_t* my_win1) {
+                                                               size_t o, uint8_t* my_win0, uint8_t* my_win1,
+                                                               int pr_slot = -1) {
     const int lane = threadIdx.x & 63;
     const int px = (lane >> 3) - 4, py = (lane & 7) - 4;
     const double P[3] = {a.points[3 * i], a.points[3 * i + 1], a.points[3 * i + 2]};
@@ -605,14 +613,22 @@ __device__ __attribute__((always_inline)) inline void lk_point(const LkAlignArgs
 #ifdef VISO_PROBE
                 pr_it[level] += (unsigned long long)r.iters;
                 pr_win += t1 - t0;
-                pr_iter += __builtin_amdgcn_s_memrealtime() - t1;
+                const unsigned long long t2 = __builtin_amdgcn_s_memrealtime();
+                pr_iter += t2 - t1;
                 pr_long += r.iters >= 10 ? 1 : 0;
+                if (pr_slot >= 0 && lane == 0) {
+                    g_probe_items[pr_slot][2 + (3 - level)] = t1;
+                    g_probe_items[pr_slot][6 + (3 - level)] = t2;
+                }
 #endif
                 cu = cu + r.dx / s;  // pair.uv_cur += V2d{dx/s, dy/s}
                 cv = cv + r.dy / s;
                 next();
             }
 #ifdef VISO_PROBE
+            if (pr_slot >= 0 && lane == 0)
+                g_probe_items[pr_slot][11] = pr_it[3] | (pr_it[2] << 16) | (pr_it[1] << 32) | (pr_it[0] << 48);
+#ifndef VISO_PROBE_LIGHT  // (the light probe: plain per-item stores only, no same-address atomics)
             if (lane == 0) {
                 for (int l = 0; l < kLevels; ++l) {
                     atomicAdd(&g_probe_lk[l], pr_it[l]);
@@ -632,6 +648,7 @@ __device__ __attribute__((always_inline)) inline void lk_point(const LkAlignArgs
                 atomicMax(&g_probe_lk[25], (pr_n << 40) | (pr_el < (1ull << 40) ? pr_el : (1ull << 40) - 1));
                 atomicAdd(&g_probe_lk[15], 1ull);
             }
+#endif
 #endif
             succ_out = succ ? 1 : 0;
             ua[0] = cu;
@@ -693,6 +710,7 @@ constexpr int kBgTake = VISO_LK_BG_TAKE;  // items per head dequeue (1 or 2)
 #define VISO_LK_BG_POLL 4
 #endif
 constexpr int kBgLeftCap = 4096;                           // leftover items (one per resident wave at most)
+constexpr int kBgClosed = 1 << 30;                          // bg_left[1]: the drain has read the count
 template <bool FAST>
 __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
     __shared__ uint8_t s_win[4][2][kWinW * kWinH];
@@ -711,33 +729,58 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
         return __builtin_amdgcn_readfirstlane(
                    __hip_atomic_load(a.bg_ready + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0;
     };
-    // one item: wait for its frame (the resident grid at most a.bg_idle ticks,
-    // then the item goes to the leftover list and the wave leaves; the drain,
-    // which runs once every pose is launched, at most kBgWaitTicks, an error),
-    // then align the point
-    auto give_back = [&](int head, int k) {
+    // The leftover list: bg_left[1] counts the published slots and carries
+    // kBgClosed once the drain has read it.  A slot is reserved only by a CAS
+    // on an open count, so the count every drain wave reads when it closes
+    // the list (atomicOr) is final: no item can land past it.  A resident
+    // wave that finds the list closed runs its item itself — the drain starts
+    // behind the chunk's last pose, so every ready flag is raised by then.
+    // Returns false when the list is closed.
+    auto give_back = [&](int head, int k) -> bool {
+        int ok = 1;
         if (lane == 0) {
-            // reserve a slot, then publish the item (+1: 0 = not yet written;
-            // the drain may read the count first)
-            const int j = atomicAdd(a.bg_left + 1, 1);
-            if (j < kBgLeftCap)
-                __hip_atomic_store(a.bg_left + 32 + j, head * per_head + k + 1, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            else
-                atomicOr(a.bg_err, 1);
+            int c = __hip_atomic_load(a.bg_left + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (;;) {
+                if (c & kBgClosed) {
+                    ok = 0;
+                    break;
+                }
+                if (c >= kBgLeftCap) {  // (one slot per resident wave: unreachable)
+                    atomicOr(a.bg_err, 1);
+                    break;
+                }
+                const int prev = atomicCAS(a.bg_left + 1, c, c + 1);
+                if (prev == c) {
+                    // publish the item (+1: 0 = not yet written; a drain wave
+                    // that read the count may be waiting for it)
+                    __hip_atomic_store(a.bg_left + 32 + c, head * per_head + k + 1, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+                c = prev;
+            }
         }
+        return __builtin_amdgcn_readfirstlane(ok) != 0;
     };
+    unsigned long long t_deq = 0;  // (probe) the item's dequeue
+    // one item: wait for its frame (a resident wave at most a.bg_idle ticks,
+    // then the item goes to the leftover list and the wave leaves, unless the
+    // list is closed; the drain, and a resident wave whose list is closed, at
+    // most kBgWaitTicks, an error), then align the point.  Returns false when
+    // the item was handed to the leftover list or its wait failed.
     auto run_item = [&](int head, int k) __attribute__((always_inline)) -> bool {
         const int f = k / seg, i = head * seg + (k - f * seg);
         if (i >= a.n) return true;
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        bool must = a.bg_drain != 0;
         while (!ready(f)) {
             const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t0;
-            if (!a.bg_drain && dt > (unsigned long long)a.bg_idle) {
-                give_back(head, k);
-                return false;
+            if (!must && dt > (unsigned long long)a.bg_idle) {
+                if (give_back(head, k)) return false;
+                must = true;  // the list is closed: every pose is launched
+                t0 = __builtin_amdgcn_s_memrealtime();
             }
-            if (a.bg_drain && dt > kBgWaitTicks) {
+            if (must && dt > kBgWaitTicks) {
                 if (lane == 0) atomicOr(a.bg_err, 1);
                 return false;
             }
@@ -754,6 +797,19 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
         }
         const FrameDev cur = fr.cur;
 #ifdef VISO_PROBE
+        const int pr_slot = (f == a.n_frames - 1 && i < kProbeItems) ? i : -1;
+        if (pr_slot >= 0 && lane == 0) {
+            g_probe_items[pr_slot][0] = t0;
+            g_probe_items[pr_slot][1] = __builtin_amdgcn_s_memrealtime();
+            g_probe_items[pr_slot][12] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+                                         ((unsigned long long)xcc << 32) | ((unsigned long long)(a.bg_drain ? 1 : 0) << 40) |
+                                         (1ull << 48);
+            g_probe_items[pr_slot][14] = t_deq;
+        }
+#else
+        const int pr_slot = -1;
+#endif
+#if defined(VISO_PROBE) && !defined(VISO_PROBE_LIGHT)
         // the chunk's last frame: first ready sighting (16, stored inverted
         // for atomicMax), last completion (17), slowest item (18), items (19),
         // items the drain ran (20), last item start (21)
@@ -764,8 +820,12 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
             atomicMax(&g_probe_lk[21], pr_s);
         }
 #endif
-        lk_point<FAST>(a, ka, cur, s_pose[wave], i, (size_t)f * a.out_stride, s_win[wave][0], s_win[wave][1]);
+        lk_point<FAST>(a, ka, cur, s_pose[wave], i, (size_t)f * a.out_stride, s_win[wave][0], s_win[wave][1],
+                       pr_slot);
 #ifdef VISO_PROBE
+        if (pr_slot >= 0 && lane == 0) g_probe_items[pr_slot][10] = __builtin_amdgcn_s_memrealtime();
+#endif
+#if defined(VISO_PROBE) && !defined(VISO_PROBE_LIGHT)
         if (lane == 0) atomicMax(&g_probe_lk[23], __builtin_amdgcn_s_memrealtime());  // any item's end
         if (pr_last && lane == 0) {
             const unsigned long long pr_e = __builtin_amdgcn_s_memrealtime();
@@ -779,12 +839,14 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
     };
     // the items resident waves gave back (the drain only), then the heads;
     // one loop, so the per-point code is inlined once
-    const int n_left = a.bg_drain ? min(__builtin_amdgcn_readfirstlane(__hip_atomic_load(
-                                            a.bg_left + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
-                                        kBgLeftCap)
-                                  : 0;
+    // the drain closes the leftover list; the count it reads is final
+    int n_left = 0;
+    if (a.bg_drain) {
+        if (lane == 0) n_left = atomicOr(a.bg_left + 1, kBgClosed) & ~kBgClosed;
+        n_left = min(__builtin_amdgcn_readfirstlane(n_left), kBgLeftCap);
+    }
     bool left_phase = n_left > 0;
-#ifdef VISO_PROBE
+#if defined(VISO_PROBE) && !defined(VISO_PROBE_LIGHT)
     if (a.bg_drain && lane == 0) atomicMax(&g_probe_lk[22], ~__builtin_amdgcn_s_memrealtime());  // drain start
 #endif
     int h = 0;
@@ -830,8 +892,13 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
                 pend_k = k + 1;
             }
         }
+#ifdef VISO_PROBE
+        t_deq = __builtin_amdgcn_s_memrealtime();
+#endif
         if (!run_item(head, k)) {
-            if (pend_head >= 0) give_back(pend_head, pend_k);
+            // the second item of the dequeue goes to the list too, or, when
+            // the list is closed, is run here
+            if (pend_head >= 0 && !give_back(pend_head, pend_k)) (void)run_item(pend_head, pend_k);
             return;
         }
         if (a.bg_drain && lane == 0) atomicAdd(a.bg_err + 1, 1);  // items the drain ran (stats)
@@ -933,6 +1000,18 @@ void launch_lk_template(const LkAlignArgs& a, hipStream_t stream) {
 }  // namespace viso
 
 #ifdef VISO_PROBE
+extern "C" int viso_debug_probe_items(unsigned long long* out, int cap, int reset) {
+    const int n = cap < kProbeItems ? cap : kProbeItems;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_probe_items), sizeof(unsigned long long) * 16 * n) != hipSuccess)
+        return -2;
+    if (reset) {
+        void* p = nullptr;
+        if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_probe_items)) != hipSuccess) return -2;
+        if (hipMemset(p, 0, sizeof(g_probe_items)) != hipSuccess) return -2;
+    }
+    return n;
+}
+
 extern "C" int viso_debug_probe_lk(unsigned long long* out, int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_probe_lk), sizeof(unsigned long long) * 32) != hipSuccess)
         return -2;
