@@ -115,7 +115,9 @@ int viso_synchronize(viso_ctx* ctx);
 /* State (include/viso.h:44) */
 int viso_get_state(viso_ctx* ctx, int32_t* state);
 /* Viso::poses (include/viso.h:54): Tcw per tracked frame, 12 doubles each
- * (R row-major, t).  *n receives the total count. */
+ * (R row-major, t); the first min(cap, count, max_poses) are copied (one
+ * device round trip).  *n receives the total count, which is host state: with
+ * Tcw12 NULL or cap 0 the call does not touch the device. */
 int viso_get_poses(viso_ctx* ctx, double* Tcw12, size_t cap, size_t* n);
 /* Viso::GetPoints() (include/viso.h:60-67): map points, 3 doubles each. */
 int viso_get_points(viso_ctx* ctx, double* xyz, size_t cap, size_t* n);

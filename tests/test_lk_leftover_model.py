@@ -50,10 +50,21 @@ def resident_new(m: Mem, items):
             yield
 
 
-def drain_new(m: Mem):
-    n = m.count & ~CLOSED
-    m.count |= CLOSED  # atomicOr, returns the count before
-    yield
+def drain_new(m: Mem, closer: bool = True):
+    """The drain's first wave closes the list (atomicOr) and publishes the
+    count it read in one word (bg_left[2]); every other drain wave waits for
+    that word."""
+    if closer:
+        n = m.count & ~CLOSED
+        m.count |= CLOSED  # atomicOr, returns the count before
+        yield
+        m.published = n
+        yield
+    else:
+        while getattr(m, "published", None) is None:
+            yield
+        n = m.published
+        yield
     while True:
         j = m.cursor
         m.cursor += 1
@@ -123,7 +134,8 @@ def test_leftover_list_runs_every_item_once_under_random_schedules():
                     next(g)
                 except StopIteration:
                     break
-        waves = [resident_new(m, it) for it in items[1:]] + [drain_new(m) for _ in range(rng.randint(1, 3))]
+        waves = [resident_new(m, it) for it in items[1:]] + [drain_new(m, closer=(d == 0))
+                                                            for d in range(rng.randint(1, 3))]
         assert run(waves, seed=seed), f"seed {seed}: a wave never finished"
         want = sorted(x for it in items for x in it)
         assert sorted(m.ran) == want, f"seed {seed}: ran {sorted(m.ran)}"
@@ -143,3 +155,37 @@ def test_round4_protocol_loses_that_item():
     waves = [resident_old(m, [("r", 0)]), drain_old(m)]
     assert run(waves, order=[1, 0, 0, 1, 1, 1])
     assert m.ran == []  # the item landed past the count the drain read
+
+
+def decode(head, k, n, n_frames):
+    """track.hip lk_item_kernel's item numbers of head `head`: (frame, point)
+    or None (padding / the last frame's dummy numbers)."""
+    seg = (n + 7) // 8
+    base = (n_frames - 1) * seg
+    base_e = base + (base & 1)
+    if k < base:
+        f = k // seg
+        i = head * seg + (k - f * seg)
+    else:
+        r = k - base_e
+        if r < 0 or r & 1:
+            return None
+        f, i = n_frames - 1, head * seg + r // 2
+    return (f, i) if i < n else None
+
+
+def test_head_numbers_cover_every_item_once_and_split_the_last_frame():
+    for n in (1, 7, 8, 9, 2465, 5325):
+        for n_frames in (1, 2, 3, 20, 64):
+            seg = (n + 7) // 8
+            base = (n_frames - 1) * seg
+            per_head = base + (base & 1) + 2 * seg
+            seen = []
+            for head in range(8):
+                for k0 in range(0, per_head, 2):  # two-number dequeues from 0
+                    got = [decode(head, k, n, n_frames) for k in (k0, k0 + 1) if k < per_head]
+                    got = [g for g in got if g is not None]
+                    seen += got
+                    # no dequeue carries two points of the last frame
+                    assert sum(1 for f, _ in got if f == n_frames - 1) <= 1
+            assert sorted(seen) == [(f, i) for f in range(n_frames) for i in range(n)]

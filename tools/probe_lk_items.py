@@ -40,6 +40,8 @@ def main():
     v.set_stereo(seq.p.baseline, 128, 1)
     lib = _lib.load()
     lib.viso_debug_probe_items.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    lib.viso_debug_probe_waves.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    wv = np.zeros((8192, 4), np.uint64)
     cap = 16384
     rec = np.zeros((cap, 16), np.uint64)
     lib.viso_debug_probe_ring.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
@@ -57,6 +59,7 @@ def main():
     us = 0.01
     for rep in range(reps):
         lib.viso_debug_probe_items(rec.ctypes.data, cap, 1)
+        lib.viso_debug_probe_waves(wv.ctypes.data, 8192, 1)
         lib.viso_debug_probe_ring(rlog.ctypes.data, rexit.ctypes.data, rcap, ctypes.byref(nl), 1)
         torch.cuda.synchronize()
         import time
@@ -65,6 +68,7 @@ def main():
         v.synchronize()
         th = (time.perf_counter() - th) * 1e6
         lib.viso_debug_probe_items(rec.ctypes.data, cap, 0)
+        lib.viso_debug_probe_waves(wv.ctypes.data, 8192, 0)
         lib.viso_debug_probe_ring(rlog.ctypes.data, rexit.ctypes.data, rcap, ctypes.byref(nl), 0)
         nr = min(nl.value, rcap)
         rl = rlog[:nr].astype(np.int64)
@@ -92,6 +96,24 @@ def main():
         print(f"== rep {rep}: last frame {len(idx)} items ({drain.sum()} by the drain); first start -> last end "
               f"{end.max():.1f} us; last start {start.max():.1f}; dequeue before first start: "
               f"{(deq < 0).sum()} items")
+        src = R[:, 13] & 0xff
+        print(f"   sources: head {(src == 0).sum()}, leftover list {(src == 1).sum()}, second of a dequeue "
+              f"{(src == 2).sum()}")
+        W_ = wv.astype(np.int64)
+        dr = W_[1024:]
+        dr = dr[dr[:, 0] > 0]
+        if len(dr):
+            ds = (dr[:, 0] - t0) * us
+            de = np.where(dr[:, 1] > 0, (dr[:, 1] - t0) * us, np.nan)
+            print(f"   drain waves {len(dr)}: start p0 {ds.min():.1f} p50 {np.median(ds):.1f} p100 {ds.max():.1f} us; "
+                  f"end p50 {np.nanmedian(de):.1f} max {np.nanmax(de):.1f}; n_left {int(dr[:, 3].max())}; items "
+                  f"run: total {int(dr[:, 2].sum())}, waves with none {(dr[:, 2] == 0).sum()}, max {int(dr[:, 2].max())}")
+        rw = W_[:1024]
+        rw = rw[rw[:, 0] > 0]
+        if len(rw):
+            re_ = np.where(rw[:, 1] > 0, (rw[:, 1] - t0) * us, np.nan)
+            print(f"   resident waves {len(rw)}: end p50 {np.nanmedian(re_):.1f} max {np.nanmax(re_):.1f} us; "
+                  f"left early (no end stamp) {(rw[:, 1] == 0).sum()}; items run total {int(rw[:, 2].sum())}")
         q = np.percentile(dur, [50, 90, 99, 100])
         print(f"   item duration p50 {q[0]:.1f} p90 {q[1]:.1f} p99 {q[2]:.1f} max {q[3]:.1f} us; "
               f"mean iterations {its.sum(1).mean():.1f}")

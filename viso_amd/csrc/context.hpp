@@ -150,6 +150,8 @@ struct viso_ctx {
     viso::GeoCtl* h_ctl = nullptr;  // pinned
     int* h_int = nullptr;           // pinned scratch ints
     double* h_dbl = nullptr;        // pinned scratch doubles (64)
+    double* h_poses = nullptr;      // pinned staging of the pose log (viso_get_poses)
+    size_t h_poses_cap = 0;         // poses it holds
 
     // ---------------- map (Map / MapPoint, include/map.h, map_point.h)
     viso::DevBuf map_pts;  // kMaxMapPoints x 3

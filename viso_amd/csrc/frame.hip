@@ -177,9 +177,12 @@ void viso_ctx::release() {
     if (h_ctl) (void)hipHostFree(h_ctl);
     if (h_int) (void)hipHostFree(h_int);
     if (h_dbl) (void)hipHostFree(h_dbl);
+    if (h_poses) (void)hipHostFree(h_poses);
     h_ctl = nullptr;
     h_int = nullptr;
     h_dbl = nullptr;
+    h_poses = nullptr;
+    h_poses_cap = 0;
 }
 
 // The context stream and the LK-alignment side stream (single-frame calls).
@@ -400,8 +403,14 @@ int viso_ctx::bg_begin(const std::vector<int>& chunk) {
     }
     // ready flags [kLkBatch], eight heads on lines of their own, error word,
     // leftover list (cursor, count, 4096 items)
+    // + 32 words past them: the error word and the drain's item count, kept
+    // across chunks (sticky) until bg_check reads and clears them
     const size_t bg_words = kLkBatch + 8 * 32 + 32 + 32 + 4096;
-    int rc = bg_buf.ensure(sizeof(int) * bg_words);
+    const bool fresh = bg_buf.ptr == nullptr;
+    int rc = bg_buf.ensure(sizeof(int) * (bg_words + 32));
+    if (!rc && fresh) rc = hipMemsetAsync((int*)bg_buf.ptr + bg_words, 0, 32 * sizeof(int), stream) == hipSuccess
+                               ? VISO_OK
+                               : VISO_ERR_HIP;
     if (rc) return rc;
     LkAlignArgs a = lk_args();
     a.n_frames = nb;
@@ -416,8 +425,8 @@ int viso_ctx::bg_begin(const std::vector<int>& chunk) {
     a.uv_after = (double*)lk_after.ptr;
     a.bg_ready = (int*)bg_buf.ptr;
     a.bg_next = a.bg_ready + kLkBatch;
-    a.bg_err = a.bg_next + 8 * 32;
-    a.bg_left = a.bg_err + 32;
+    a.bg_left = a.bg_next + 8 * 32 + 32;
+    a.bg_err = a.bg_ready + bg_words;
     a.bg_items = nb * n_map;
     // tests: VISO_LK_BG_IDLE_US shortens the resident waves' patience, so the
     // leftover list and the drain carry most items
@@ -451,12 +460,13 @@ int viso_ctx::bg_launch() {
 
 int viso_ctx::bg_check() {
     if (!bg_unchecked || !bg_buf.ptr) return VISO_OK;
-    // the drain runs on the context stream (bg_end): its words are final only
-    // once that stream has passed it
+    // the words (error, items the drain ran) were copied into pinned memory
+    // behind the drain on the context stream (bg_end): they are final once
+    // that stream has passed the copy
     VISO_HIP_CHECK(hipStreamSynchronize(stream));
-    int w[3] = {0, 0, 0};  // error, items the drain ran, leftover cursor
-    VISO_HIP_CHECK(hipMemcpy(w, (int*)bg_buf.ptr + kLkBatch + 8 * 32, 2 * sizeof(int), hipMemcpyDeviceToHost));
+    const int w[2] = {h_int[32], h_int[33]};
     bg_unchecked = false;
+    if (w[0] || w[1]) VISO_HIP_CHECK(hipMemsetAsync(bg_args.bg_err, 0, 2 * sizeof(int), stream));
     if (getenv("VISO_LK_BG_STATS"))  // dev: how much of the last chunk the drain carried
         fprintf(stderr, "viso lk-bg: %d frames x %d points, drain ran %d items, error %d\n", bg_nb, n_map, w[1], w[0]);
     return w[0] ? VISO_ERR_HIP : VISO_OK;
@@ -478,6 +488,8 @@ int viso_ctx::bg_end(bool drain) {
         VISO_HIP_CHECK(hipGetLastError());
     }
     VISO_HIP_CHECK(hipStreamWaitEvent(stream, bg_done, 0));
+    // the error / drain-count words, for bg_check (no blocking copy at sync)
+    VISO_HIP_CHECK(hipMemcpyAsync(h_int + 32, bg_args.bg_err, 2 * sizeof(int), hipMemcpyDeviceToHost, stream));
     lk_last_rows = bg_nb;
     lk_last_pts = n_map;
     VISO_HIP_CHECK(hipEventRecord(lk_ring[lk_seq % kLkRing], lk_stream));
@@ -984,13 +996,26 @@ int viso_get_state(viso_ctx* c, int32_t* state) {
 
 int viso_get_poses(viso_ctx* c, double* Tcw12, size_t cap, size_t* n) {
     if (!c) return VISO_ERR_ARG;
-    VISO_HIP_CHECK(hipSetDevice(c->device));
-    const size_t m = std::min(cap, (size_t)c->n_poses);
-    if (m > 0 && Tcw12) {
-        VISO_HIP_CHECK(hipMemcpyAsync(Tcw12, c->pose_log.ptr, 96 * m, hipMemcpyDeviceToHost, c->stream));
-    }
-    VISO_HIP_CHECK(hipStreamSynchronize(c->stream));
+    // the count is host state (one pose per launched tracking frame): asking
+    // for it alone needs no device round trip
     if (n) *n = (size_t)c->n_poses;
+    // (the log keeps the first max_poses poses)
+    const size_t m = std::min(std::min(cap, (size_t)c->n_poses), (size_t)std::max(c->p.max_poses, 0));
+    if (m == 0 || !Tcw12) return VISO_OK;
+    VISO_HIP_CHECK(hipSetDevice(c->device));
+    // through a pinned staging buffer: one DMA and one stream sync (a
+    // pageable destination is copied through the runtime's own staging)
+    if (c->h_poses_cap < m) {
+        const size_t want = std::max(m, (size_t)4096);
+        if (c->h_poses) VISO_HIP_CHECK(hipHostFree(c->h_poses));
+        c->h_poses = nullptr;
+        c->h_poses_cap = 0;
+        VISO_HIP_CHECK(hipHostMalloc((void**)&c->h_poses, 96 * want));
+        c->h_poses_cap = want;
+    }
+    VISO_HIP_CHECK(hipMemcpyAsync(c->h_poses, c->pose_log.ptr, 96 * m, hipMemcpyDeviceToHost, c->stream));
+    VISO_HIP_CHECK(hipStreamSynchronize(c->stream));
+    std::memcpy(Tcw12, c->h_poses, 96 * m);
     return VISO_OK;
 }
 

@@ -28,6 +28,10 @@ __device__ unsigned long long g_probe_lk[32];
 // drain << 40 | 1 << 48, [13] window refills, [14] dequeue stamp
 constexpr int kProbeItems = 16384;
 __device__ unsigned long long g_probe_items[kProbeItems][16];
+// per wave of the background grid (rows 0..1023: resident, 1024..: drain):
+// [0] start, [1] end, [2] items run, [3] n_left it read
+constexpr int kProbeWaves = 8192;
+__device__ unsigned long long g_probe_waves[kProbeWaves][4];
 #endif
 
 namespace viso {
@@ -723,7 +727,14 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
     // frame's points (points [x seg, (x + 1) seg)), frames in order; a wave
     // drains its own XCD's head, then the others'
     const int seg = (a.n + 7) / 8;
-    const int per_head = a.n_frames * seg;
+    // A head's item numbers: frames 0 .. n_frames - 2 at one number per
+    // point; the last frame (whose pose only the chunk's final solve gives,
+    // so its items gate the chunk's end) at two numbers per point, the odd one
+    // a dummy, so a two-number dequeue takes ONE of its points and no wave
+    // runs two of them back to back.  The last frame starts at an even number.
+    const int base = (a.n_frames - 1) * seg;
+    const int base_e = base + (base & 1);
+    const int per_head = base_e + 2 * seg;
     const int xcc = (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 7);  // HW_REG_XCC_ID
     auto ready = [&](int f) {
         return __builtin_amdgcn_readfirstlane(
@@ -763,13 +774,23 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
         return __builtin_amdgcn_readfirstlane(ok) != 0;
     };
     unsigned long long t_deq = 0;  // (probe) the item's dequeue
+    int pr_src = 0;                // (probe) 0 head, 1 leftover list, 2 the dequeue's second item
     // one item: wait for its frame (a resident wave at most a.bg_idle ticks,
     // then the item goes to the leftover list and the wave leaves, unless the
     // list is closed; the drain, and a resident wave whose list is closed, at
     // most kBgWaitTicks, an error), then align the point.  Returns false when
     // the item was handed to the leftover list or its wait failed.
     auto run_item = [&](int head, int k) __attribute__((always_inline)) -> bool {
-        const int f = k / seg, i = head * seg + (k - f * seg);
+        int f, i;
+        if (k < base) {
+            f = k / seg;
+            i = head * seg + (k - f * seg);
+        } else {
+            const int r = k - base_e;
+            if (r < 0 || (r & 1)) return true;  // padding / the last frame's dummy numbers
+            f = a.n_frames - 1;
+            i = head * seg + (r >> 1);
+        }
         if (i >= a.n) return true;
         unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         bool must = a.bg_drain != 0;
@@ -805,6 +826,7 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
                                          ((unsigned long long)xcc << 32) | ((unsigned long long)(a.bg_drain ? 1 : 0) << 40) |
                                          (1ull << 48);
             g_probe_items[pr_slot][14] = t_deq;
+            g_probe_items[pr_slot][13] = (unsigned long long)pr_src | ((unsigned long long)head << 8);
         }
 #else
         const int pr_slot = -1;
@@ -839,13 +861,44 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
     };
     // the items resident waves gave back (the drain only), then the heads;
     // one loop, so the per-point code is inlined once
-    // the drain closes the leftover list; the count it reads is final
+    // the drain's first wave closes the leftover list (the count it reads is
+    // final) and publishes that count in bg_left[2] (one word: value and valid
+    // bit together); the other drain waves read it there — one atomic instead
+    // of one per drain wave (same-address atomics serialise, ~12 ns each:
+    // 3,072 of them would cost ~37 us at the chunk's end)
     int n_left = 0;
     if (a.bg_drain) {
-        if (lane == 0) n_left = atomicOr(a.bg_left + 1, kBgClosed) & ~kBgClosed;
-        n_left = min(__builtin_amdgcn_readfirstlane(n_left), kBgLeftCap);
+        if (blockIdx.x == 0 && wave == 0) {
+            if (lane == 0) {
+                n_left = atomicOr(a.bg_left + 1, kBgClosed) & ~kBgClosed;
+                __hip_atomic_store(a.bg_left + 2, n_left | kBgClosed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            n_left = __builtin_amdgcn_readfirstlane(n_left);
+        } else {
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            int v;
+            while (!((v = __builtin_amdgcn_readfirstlane(
+                          __hip_atomic_load(a.bg_left + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) &
+                     kBgClosed)) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > kBgWaitTicks) {
+                    if (lane == 0) atomicOr(a.bg_err, 1);
+                    return;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            n_left = v & ~kBgClosed;
+        }
+        n_left = min(n_left, kBgLeftCap);
     }
     bool left_phase = n_left > 0;
+#ifdef VISO_PROBE
+    const int pr_w = (a.bg_drain ? 1024 : 0) + (int)blockIdx.x * 4 + wave;
+    int pr_items = 0;
+    if (lane == 0 && pr_w < kProbeWaves) {
+        g_probe_waves[pr_w][0] = __builtin_amdgcn_s_memrealtime();
+        g_probe_waves[pr_w][3] = (unsigned long long)n_left;
+    }
+#endif
 #if defined(VISO_PROBE) && !defined(VISO_PROBE_LIGHT)
     if (a.bg_drain && lane == 0) atomicMax(&g_probe_lk[22], ~__builtin_amdgcn_s_memrealtime());  // drain start
 #endif
@@ -853,6 +906,9 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
     int pend_head = -1, pend_k = 0;  // the second item of the last dequeue
     for (;;) {
         int head = 0, k = 0;
+#ifdef VISO_PROBE
+        pr_src = pend_head >= 0 ? 2 : left_phase ? 1 : 0;
+#endif
         if (pend_head >= 0) {
             head = pend_head;
             k = pend_k;
@@ -878,8 +934,26 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
             head = (e - 1) / per_head;
             k = (e - 1) - head * per_head;
         } else {
-            if (h >= 8) break;
+            if (h >= 8) {
+#ifdef VISO_PROBE
+                if (lane == 0 && pr_w < kProbeWaves) {
+                    g_probe_waves[pr_w][1] = __builtin_amdgcn_s_memrealtime();
+                    g_probe_waves[pr_w][2] = (unsigned long long)pr_items;
+                }
+#endif
+                break;
+            }
             head = (xcc + h) & 7;
+            // a wave past its own head (and every drain wave) looks first: an
+            // exhausted head costs a load, not an atomic (thousands of waves
+            // walking the heads at the chunk's end would otherwise queue
+            // behind each other on eight words)
+            if ((h > 0 || a.bg_drain) &&
+                __builtin_amdgcn_readfirstlane(__hip_atomic_load(a.bg_next + 32 * head, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_AGENT)) >= per_head) {
+                ++h;
+                continue;
+            }
             // two items per dequeue: half the head round trips per item
             if (lane == 0) k = atomicAdd(a.bg_next + 32 * head, kBgTake);
             k = __builtin_amdgcn_readfirstlane(k);
@@ -902,6 +976,9 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
             return;
         }
         if (a.bg_drain && lane == 0) atomicAdd(a.bg_err + 1, 1);  // items the drain ran (stats)
+#ifdef VISO_PROBE
+        ++pr_items;
+#endif
     }
 }
 
@@ -1008,6 +1085,18 @@ extern "C" int viso_debug_probe_items(unsigned long long* out, int cap, int rese
         void* p = nullptr;
         if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_probe_items)) != hipSuccess) return -2;
         if (hipMemset(p, 0, sizeof(g_probe_items)) != hipSuccess) return -2;
+    }
+    return n;
+}
+
+extern "C" int viso_debug_probe_waves(unsigned long long* out, int cap, int reset) {
+    const int n = cap < kProbeWaves ? cap : kProbeWaves;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_probe_waves), sizeof(unsigned long long) * 4 * n) != hipSuccess)
+        return -2;
+    if (reset) {
+        void* p = nullptr;
+        if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_probe_waves)) != hipSuccess) return -2;
+        if (hipMemset(p, 0, sizeof(g_probe_waves)) != hipSuccess) return -2;
     }
     return n;
 }
