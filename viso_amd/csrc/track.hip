@@ -241,7 +241,7 @@ template <int MAXIT, bool KLT_BOUNDS>
 __device__ inline LkResult lk_iterate(const LkTemplate& t, int w1, int h1,
                                       const uint8_t* __restrict__ img2, int w2, int h2,
                                       double cur_x, double cur_y, double bx, double by, double dx,
-                                      double dy, double thresh, Window win) {
+                                      double dy, double thresh, Window win, int boost_at = -1) {
     const double hp = 4.0;
     // the control values are wave-uniform (the sums are read from one lane):
     // said so to the compiler, the loop's branches need no EXEC bookkeeping
@@ -263,6 +263,9 @@ __device__ inline LkResult lk_iterate(const LkTemplate& t, int w1, int h1,
     bool succ = true;
     int iter = 0;
     for (; iter < MAXIT; ++iter) {
+        // a point still iterating after boost_at steps (the background grid's
+        // last frame, VISO_LK_BOOST): its wave outranks the short points'
+        if (iter == boost_at) __builtin_amdgcn_s_setprio(2);
         bool out;
         if (KLT_BOUNDS) {  // src/viso.cpp:286
             out = bx + dx <= hp || bx + dx >= w1 - hp || by + dy <= hp || by + dy >= h1 - hp;
@@ -518,7 +521,7 @@ template <bool FAST>
 __device__ __attribute__((always_inline)) inline void lk_point(const LkAlignArgs& a, const LkAlignArgs* ka,
                                                                const FrameDev& cur, const double* cur_pose, int i,
                                                                size_t o, uint8_t* my_win0, uint8_t* my_win1,
-                                                               int pr_slot = -1) {
+                                                               int pr_slot = -1, int boost_at = -1) {
     const int lane = threadIdx.x & 63;
     const int px = (lane >> 3) - 4, py = (lane & 7) - 4;
     const double P[3] = {a.points[3 * i], a.points[3 * i + 1], a.points[3 * i + 2]};
@@ -612,7 +615,7 @@ __device__ __attribute__((always_inline)) inline void lk_point(const LkAlignArgs
                 const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
 #endif
                 LkResult r = lk_iterate<100, false>(t, w, h, level_ptr(cur, level), w, h, cx, cy, bu * s,
-                                                    bv * s, 0.0, 0.0, a.thresh, wcur);
+                                                    bv * s, 0.0, 0.0, a.thresh, wcur, boost_at);
                 succ = r.succ;
 #ifdef VISO_PROBE
                 pr_it[level] += (unsigned long long)r.iters;
@@ -707,6 +710,9 @@ constexpr unsigned long long kBgWaitTicks = 20000000ull;  // 200 ms of s_memreal
 #define VISO_LK_BG_TAKE 2
 #endif
 constexpr int kBgTake = VISO_LK_BG_TAKE;  // items per head dequeue (1 or 2)
+#ifndef VISO_LK_BOOST
+#define VISO_LK_BOOST 12
+#endif
 // s_sleep quanta (64 cycles) between polls of a frame's ready flag: a
 // thousand waiting waves polling one line share the memory system with the
 // chain they wait for
@@ -842,8 +848,12 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
             atomicMax(&g_probe_lk[21], pr_s);
         }
 #endif
+        // the chunk's last frame runs after the chain: its long points take
+        // issue priority over the short ones (VISO_LK_BOOST steps, 0 = off)
+        const int boost_at = (VISO_LK_BOOST > 0 && f == a.n_frames - 1) ? VISO_LK_BOOST : -1;
         lk_point<FAST>(a, ka, cur, s_pose[wave], i, (size_t)f * a.out_stride, s_win[wave][0], s_win[wave][1],
-                       pr_slot);
+                       pr_slot, boost_at);
+        if (boost_at >= 0) __builtin_amdgcn_s_setprio(0);
 #ifdef VISO_PROBE
         if (pr_slot >= 0 && lane == 0) g_probe_items[pr_slot][10] = __builtin_amdgcn_s_memrealtime();
 #endif
