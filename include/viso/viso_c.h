@@ -149,7 +149,8 @@ int viso_get_frame_stats(viso_ctx* ctx, double stats[16]);
 #define VISO_KERNEL_DIRECT 5
 #define VISO_KERNEL_LKALIGN 6
 #define VISO_KERNEL_STEREO 7
-#define VISO_KERNEL_COUNT 8
+#define VISO_KERNEL_UPLOAD 8 /* host -> device copy of a frame (viso_process_frame / _stereo) */
+#define VISO_KERNEL_COUNT 9
 int viso_timing_enable(viso_ctx* ctx, int32_t enable);
 /* Restrict timing to the kernels whose bit (1 << VISO_KERNEL_*) is set
  * (default: all).  Each timed region records two events on its stream. */
@@ -257,7 +258,9 @@ int viso_set_bundle_adjust(viso_ctx* ctx, int32_t iterations);
 int viso_photometric_ba(viso_ctx* ctx, const uint8_t* const* kf_images, int32_t n_kf, double* kf_poses,
                         double* points, const int32_t* host, int32_t n, int32_t iterations, double* report);
 
-/* Library build/version string (e.g. "viso_amd 0.1 gfx950"). */
+/* Library build/version string, "viso_amd 0.1 gfx950 (HIP) src:<hash>": the
+ * hash of the sources and flags it was built from (viso_amd/build.py
+ * source_hash), so a stale prebuilt library can be detected. */
 const char* viso_version(void);
 
 #ifdef __cplusplus

@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstddef>
 #include <cstdint>
+#include <memory>
 #include <vector>
 
 namespace oracle {
@@ -126,6 +127,46 @@ inline int& sum_literal() {
 }
 
 // Running sum in index order, starting from 0 (Eigen's Zero() then +=).
+// The reference's cost model, for the copies-included CPU baseline (SURVEY.md
+// §8(d); bench.py cpu_baseline_faithful).  Map::GetPoints() and
+// Map::Keyframes() return std::vector<shared_ptr> BY VALUE (include/map.h:
+// 18-19), and the reference calls them inside its loops: the loop condition
+// `i < map_.GetPoints().size()` and `map_.GetPoints()[i]` per point in
+// DirectPoseEstimationSingleLayer (src/viso.cpp:688,690) and LKAlignment
+// (:774,776), `auto keyframes = map_.Keyframes()` per point in LKAlignment
+// (:787) — O(N^2) shared_ptr copies per pass.  With ref_copies().on the
+// oracle makes the same copies of a mirror of the map (the arithmetic is
+// untouched; off by default).
+struct RefCopies {
+    bool on = false;
+    std::vector<std::shared_ptr<const int>> pts, kfs;
+};
+inline RefCopies& ref_copies() {
+    static RefCopies r;
+    return r;
+}
+inline void ref_sink(size_t v) {
+    static volatile size_t s;
+    s = s + v;
+}
+inline std::vector<std::shared_ptr<const int>> ref_mirror(std::vector<std::shared_ptr<const int>>& m, int n) {
+    while ((int)m.size() < n) m.push_back(std::make_shared<const int>((int)m.size()));
+    if ((int)m.size() > n) m.resize((size_t)n);
+    return m;  // by value, as Map::GetPoints() / Keyframes()
+}
+// `i < map_.GetPoints().size()`
+inline void ref_points_cond(int n) {
+    if (ref_copies().on) ref_sink(ref_mirror(ref_copies().pts, n).size());
+}
+// `map_.GetPoints()[i]`
+inline void ref_points_at(int n, int i) {
+    if (ref_copies().on) ref_sink((size_t)*ref_mirror(ref_copies().pts, n)[(size_t)i]);
+}
+// `auto keyframes = map_.Keyframes()`
+inline void ref_keyframes(int nk) {
+    if (ref_copies().on) ref_sink(ref_mirror(ref_copies().kfs, nk).size());
+}
+
 inline double running_sum(const double* v, int n) {
     double s = 0.0;
     for (int i = 0; i < n; ++i) s = s + v[i];

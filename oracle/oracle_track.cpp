@@ -190,12 +190,15 @@ void direct_single_layer(const PyrView& last, const PyrView& cur, const double K
             // running sum continues across iterations (never reset, :673)
             for (int k = 0; k < 28; ++k) S[k] = 0.0;
             S[27] = cost;
-            for (int i = 0; i < n; ++i)
+            for (int i = 0; (ref_points_cond(n), i < n); ++i) {
+                ref_points_at(n, i);
                 if (direct_point_partials(last, cur, last_pose, cur_pose, K, points + 3 * i, level,
                                           nullptr, S))
                     ++nGood;
+            }
         } else {
-            for (int i = 0; i < n; ++i) {
+            for (int i = 0; (ref_points_cond(n), i < n); ++i) {
+                ref_points_at(n, i);
                 double* o = &part[(size_t)i * 28];
                 if (direct_point_partials(last, cur, last_pose, cur_pose, K, points + 3 * i, level, o))
                     ++nGood;
@@ -364,6 +367,8 @@ void oracle_klt(const uint8_t* ref_pyr, const uint8_t* cur_pyr, int w, int h, co
     }
 }
 
+void oracle_set_reference_copies(int on) { ref_copies().on = on != 0; }
+
 void oracle_lk_trace(double* buf, long cap) {
     lk_trace().buf = buf;
     lk_trace().cap = cap;
@@ -413,7 +418,8 @@ void oracle_lk_align(const uint8_t* const* kf_pyrs, const double* kf_poses, int 
     Pose cp = pose_from12(cur_pose);
     const double max_angle = 180.0;
     const double kPi = 3.14159265358979323846;  // CV_PI
-    for (int i = 0; i < n_points; ++i) {
+    for (int i = 0; (ref_points_cond(n_points), i < n_points); ++i) {
+        ref_points_at(n_points, i);
         const double* Pw = points + 3 * i;
         pair_kf[i] = -1;
         success[i] = 0;
@@ -422,6 +428,7 @@ void oracle_lk_align(const uint8_t* const* kf_pyrs, const double* kf_poses, int 
         double uc, vc;
         project(cp, K, Pw, 0, uc, vc);
         if (!is_inside(uc, vc, w, h)) continue;  // current_frame->IsInside(Pw, 0)
+        ref_keyframes(n_kf);                     // auto keyframes = map_.Keyframes()
         double best_angle = 180.0;
         int best = -1;
         double best_uv[2] = {0, 0};

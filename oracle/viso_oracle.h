@@ -90,6 +90,11 @@ void oracle_se3_exp_left(const double xi[6], const double pose_in[12], double po
 //   pair_kf[i]   : chosen keyframe index or -1 (no pair)
 //   success[i]   : level-0 success of the pair (0 when no pair)
 //   uv_before[2i], uv_after[2i] : projection into cur / aligned position.
+// The reference's by-value Map::GetPoints() / Keyframes() copies inside the
+// direct-pose and LKAlignment loops (src/viso.cpp:688,690,774,776,787),
+// reproduced on a mirror of the map for the copies-included CPU baseline
+// (timing only; results unchanged).  Off by default.
+void oracle_set_reference_copies(int on);
 // Analysis tooling: record LKAlignment's iterations into buf (6 doubles per
 // row: point, level, iter, X, Y, cost; at most cap rows); buf NULL disables.
 void oracle_lk_trace(double* buf, long cap);

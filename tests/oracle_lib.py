@@ -35,6 +35,7 @@ SIG = {
     "oracle_lk_align": ([_vp, _vp, _i, _vp, _vp, _i, _i, _vp, _vp, _i, _d, _vp, _vp, _vp, _vp],
                         None),
     "oracle_lk_trace": ([_vp, ctypes.c_long], None),
+    "oracle_set_reference_copies": ([_i], None),
     "oracle_lk_trace_count": ([], ctypes.c_long),
     "oracle_triangulate": ([_vp, _vp, _vp, _vp, _vp], None),
     "oracle_ransac_essential": ([_vp, _vp, _i, _d, _d, _i, ctypes.c_uint64, _vp, _vp, _vp], _i),

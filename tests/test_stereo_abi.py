@@ -146,3 +146,13 @@ def test_gpu_stereo_bitexact(max_disp):
     if max_disp >= 64:
         # KITTI-like geometry: back-wall points (z ~ 32 m) have d ~ 12 px
         assert np.median(exp[0][exp[0] >= 0]) > 3
+
+
+def test_library_built_from_this_trees_sources():
+    """viso_version() carries the hash of the sources the library was built
+    from (viso_amd/build.py source_hash); it must be this tree's, so a stale
+    prebuilt library cannot pass for the current code (no GPU call)."""
+    from viso_amd import _lib
+    from viso_amd import build as vbuild
+    lib = _lib.load()
+    assert _lib.built_hash(lib) == vbuild.source_hash()

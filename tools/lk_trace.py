@@ -26,11 +26,8 @@ WIN = 24
 
 
 def level_dims(w, h):
-    d = [(w, h)]
-    for _ in range(3):
-        w, h = (w + 1) // 2, (h + 1) // 2
-        d.append((w, h))
-    return d
+    from viso_amd import api
+    return api.pyramid_dims(w, h)[0]
 
 
 def simulate(rows, dims):

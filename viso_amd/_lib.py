@@ -18,7 +18,7 @@ ERRORS = {-1: "VISO_ERR_ARG", -2: "VISO_ERR_HIP", -3: "VISO_ERR_CAPACITY",
 
 STATE_INITIALIZATION, STATE_RUNNING, STATE_FINISHED = 0, 1, 2
 KERNEL_IDS = {"pyramid": 0, "fast": 1, "klt": 2, "ransac": 3, "select": 4, "direct": 5,
-              "lkalign": 6, "stereo": 7}
+              "lkalign": 6, "stereo": 7, "upload": 8}
 
 
 class VisoError(RuntimeError):
@@ -150,6 +150,27 @@ def load(path: str | None = None):
     if path is None:
         _lib = lib
     return lib
+
+
+def built_hash(lib=None) -> str:
+    """The source hash compiled into the library (viso_version's "src:")."""
+    v = (lib or load()).viso_version().decode()
+    return v.rsplit("src:", 1)[-1] if "src:" in v else ""
+
+
+def check_source_hash(lib=None) -> str:
+    """Raise if the loaded product library was built from other sources than
+    the tree's (viso_amd/csrc, include/viso) — a stale prebuilt .so.  Returns
+    the hash.  Variant libraries (VISO_LIB) are not checked."""
+    from viso_amd import build as vbuild
+    want = vbuild.source_hash()
+    got = built_hash(lib)
+    if os.environ.get("VISO_LIB") or os.environ.get("VISO_VARIANT"):
+        return got
+    if got != want:
+        raise ImportError(f"viso_amd: {LIB_PATH} was built from sources {got!r}, the tree's are {want!r}: "
+                          "rebuild with `python -m viso_amd.build`")
+    return got
 
 
 def call(name: str, *args) -> int:

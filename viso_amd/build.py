@@ -40,6 +40,26 @@ if VARIANT and os.environ.get("VISO_DEFS"):
     COMMON.extend(os.environ["VISO_DEFS"].split())
 
 
+def source_hash() -> str:
+    """sha256 (first 16 hex digits) over the library's sources and public
+    headers (viso_amd/csrc/*, include/viso/*, by relative path and content)
+    and the build flags.  Compiled into viso_version() (-DVISO_SOURCE_HASH),
+    so a prebuilt library whose sources changed since its build is detected
+    (viso_amd._lib.check_source_hash, __graft_entry__.smoke)."""
+    import hashlib
+    h = hashlib.sha256()
+    for d in (CSRC, os.path.join(ROOT, "include", "viso")):
+        for f in sorted(os.listdir(d)):
+            if f.endswith((".hip", ".cpp", ".hpp", ".h")):
+                h.update(os.path.relpath(os.path.join(d, f), ROOT).encode())
+                with open(os.path.join(d, f), "rb") as fh:
+                    h.update(fh.read())
+    # the flags, with the tree's location taken out (the GPU box runs a copy
+    # of the tree under another path)
+    h.update(" ".join(COMMON).replace(ROOT, "<root>").encode())
+    return h.hexdigest()[:16]
+
+
 def _headers():
     hs = []
     for d in (CSRC, os.path.join(ROOT, "include", "viso")):
@@ -54,19 +74,30 @@ def _sources():
                   if f.endswith((".hip", ".cpp")))
 
 
-def _compile(src, hdr_mtime, verbose):
+def _compile(src, hdr_mtime, verbose, shash):
     obj = os.path.join(OBJ, os.path.basename(src) + ".o")
-    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hdr_mtime):
+    # context.hip carries the source hash (viso_version): rebuilt whenever the
+    # hash its object was built with differs
+    versioned = os.path.basename(src) == "context.hip"
+    stamp = obj + ".hash"
+    fresh = os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hdr_mtime)
+    if versioned and fresh:
+        fresh = os.path.exists(stamp) and open(stamp).read().strip() == shash
+    if fresh:
         return obj
-    cmd = [HIPCC, *COMMON, "-c", src, "-o", obj]
+    flags = [*COMMON, f'-DVISO_SOURCE_HASH="{shash}"'] if versioned else COMMON
+    cmd = [HIPCC, *flags, "-c", src, "-o", obj]
     if src.endswith(".cpp"):
-        cmd = [HIPCC, *COMMON, "-x", "hip", "-c", src, "-o", obj]
+        cmd = [HIPCC, *flags, "-x", "hip", "-c", src, "-o", obj]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         sys.stderr.write(r.stdout + r.stderr)
         raise RuntimeError(f"hipcc failed on {src}")
+    if versioned:
+        with open(stamp, "w") as fh:
+            fh.write(shash)
     return obj
 
 
@@ -75,8 +106,9 @@ def build(verbose: bool = False) -> str:
     srcs = _sources()
     hdr_mtime = max([os.path.getmtime(h) for h in _headers()] + [0.0])
     jobs = min(len(srcs), int(os.environ.get("MAX_JOBS", "8")))
+    shash = source_hash()
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        objs = list(ex.map(lambda s: _compile(s, hdr_mtime, verbose), srcs))
+        objs = list(ex.map(lambda s: _compile(s, hdr_mtime, verbose, shash), srcs))
     if os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(o) for o in objs):
         return LIB
     tmp = LIB + ".tmp"

@@ -44,7 +44,12 @@ static int check_device_present() {
 
 extern "C" {
 
-const char* viso_version(void) { return "viso_amd 0.1 gfx950 (HIP)"; }
+#ifndef VISO_SOURCE_HASH
+#define VISO_SOURCE_HASH "unknown"
+#endif
+// "viso_amd <version> gfx950 (HIP) src:<hash>": the hash of the sources the
+// library was built from (viso_amd/build.py source_hash)
+const char* viso_version(void) { return "viso_amd 0.1 gfx950 (HIP) src:" VISO_SOURCE_HASH; }
 
 int viso_default_params(viso_params* p, double fx, double fy, double cx, double cy, int32_t width,
                         int32_t height) {

@@ -272,6 +272,7 @@ int viso_ctx::ingest_host(const uint8_t* grey, int32_t w, int32_t h, int32_t str
     if (w != p.width || h != p.height || stride < w || !grey) return VISO_ERR_ARG;
     int s = acquire_slot();
     if (s < 0) return VISO_ERR_CAPACITY;
+    TimedRegion t(timing, VISO_KERNEL_UPLOAD, stream);
     VISO_HIP_CHECK(hipMemcpy2DAsync(slot_base(s), (size_t)w, grey, (size_t)stride, (size_t)w, (size_t)h,
                                     hipMemcpyHostToDevice, stream));
     *slot_out = s;

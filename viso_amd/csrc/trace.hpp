@@ -35,8 +35,9 @@ struct RoctxRange {
 // range names of the VISO_KERNEL_* phases (TimedRegion)
 inline const char* phase_name(int kernel) {
     static const char* const names[] = {"viso:pyramid", "viso:fast",  "viso:klt",    "viso:ransac",
-                                        "viso:select",  "viso:direct", "viso:lkalign", "viso:stereo"};
-    return (kernel >= 0 && kernel < 8) ? names[kernel] : "viso:phase";
+                                        "viso:select",  "viso:direct", "viso:lkalign", "viso:stereo",
+                                        "viso:upload"};
+    return (kernel >= 0 && kernel < 9) ? names[kernel] : "viso:phase";
 }
 
 }  // namespace viso
