@@ -7,6 +7,7 @@
 #include "../../include/viso/viso_c.h"
 #include "geometry.hpp"
 #include "kernels.hpp"
+#include "staging.hpp"
 #include "trace.hpp"
 
 namespace viso {
@@ -177,6 +178,7 @@ struct viso_ctx {
     viso::DevBuf lk_tmpl, lk_tmpl_h, lk_tmpl_kf, lk_tmpl_uv;
     hipStream_t lk_stream = nullptr;
     hipEvent_t lk_ring[viso::kLkRing] = {};  // recorded after each lk_stream batch
+    viso::HostStage stage;  // pinned staging of host-ingested frames (ingest_host)
     int64_t lk_seq = 0;                      // lk_stream batches launched
     // The last tracking frame's final direct-pose solve (F) is deferred: it
     // runs fused into the next tracking frame's L(3), or alone when the
