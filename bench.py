@@ -1008,14 +1008,29 @@ def pyramid_traffic(W, H, imgs_per_launch):
     return None, None
 
 
+def rocprof_avg_us(path, kernel):
+    """(average µs, calls) of the kernel whose name contains `kernel` in a
+    rocprofv3 --stats CSV (tools/db2stats.py), or None."""
+    import csv
+    if not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        for row in csv.DictReader(fh):
+            name = row["Name"].replace("viso::(anonymous namespace)::", "")
+            if kernel in name:
+                return float(row["AverageNs"]) / 1e3, int(row["Calls"])
+    return None
+
+
 def pmc_evidence(W, H, breakdown, stereo_vo, n_map=None):
     """The north star's two other rocprof figures, from the committed PMC passes
     (tools/gpu_pmc.sh -> tools/pmc_kernels.py -> profiles/r0N_gn_svo_pmc.json),
     profiled at 1242x375 only: occupancy of the GN reduction (direct_level_kernel)
     and HBM traffic of the matching pass (svo_circle_kernel).  Live durations
     come from this run's HIP events where the bench has them."""
-    # the newest committed pass (round 4 refresh, else round 3's)
-    rel = next((r for r in ("profiles/r04_gn_svo_pmc.json", "profiles/r03_gn_svo_pmc.json")
+    # the newest committed pass
+    rel = next((r for r in ("profiles/r05_gn_svo_pmc.json", "profiles/r04_gn_svo_pmc.json",
+                            "profiles/r03_gn_svo_pmc.json")
                 if os.path.exists(os.path.join(ROOT, r))), None)
     if (W, H) != (1242, 375) or rel is None:
         return None, None
@@ -1053,6 +1068,20 @@ def pmc_evidence(W, H, breakdown, stereo_vo, n_map=None):
               "fp64_tflops_algorithmic": round(flop / (live_us * 1e-6) / 1e12, 2) if flop else None,
               "fp64_peak_tflops": d.get("fp64_peak_tflops"),
               "source": f"{rel} (SQ_WAVES, SQ_WAVE_CYCLES, SQ_ACTIVE_INST_VALU, SQ_INSTS_VALU_*_F64)"}
+        # the HEAD's rocprofv3 kernel trace of the same workload with the
+        # background LK grid off (VISO_LK_BG=0; tools/gpu_evidence.sh): the
+        # dominant kernel's average duration and the fp64 fraction it gives
+        st = rocprof_avg_us(os.path.join(ROOT, "profiles", "r05_kernel_stats_nobg.csv"),
+                            "direct_level_kernel<false>")
+        if st and flop:
+            avg_us, calls = st
+            peak = d.get("fp64_peak_tflops") or 78.6
+            gn.update({"rocprof_avg_us_per_launch": round(avg_us, 2), "rocprof_calls": calls,
+                       "rocprof_source": "profiles/r05_kernel_stats_nobg.csv (rocprofv3 --kernel-trace --stats, "
+                                         "VISO_LK_BG=0, bench.py --steps 20 --warmup 5)",
+                       "fp64_frac": round(flop / (avg_us * 1e-6) / 1e12 / peak, 4),
+                       "fp64_frac_basis": "algorithmic flop per launch / rocprof average duration / "
+                                          f"{peak} TFLOP/s fp64 vector peak"})
     mp = None
     c = t.get("svo", {}).get("svo_circle_kernel")
     if c and c.get("traffic_bytes"):
