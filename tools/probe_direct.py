@@ -146,6 +146,27 @@ def main():
             m = arr.mean(axis=0)
             print(f"      {name:8s} by block: first 8 {np.round(m[:8], 2).tolist()} last 8 {np.round(m[-8:], 2).tolist()} "
                   f"by XCD (b % 8) {np.round([m[x::8].mean() for x in range(8)], 2).tolist()}")
+    # per wave: its point evaluated, relative to the block's B2; the last
+    # arriver's trees stored (probe build, g_pwave)
+    if hasattr(lib, "viso_debug_probe_waves_direct"):
+        lib.viso_debug_probe_waves_direct.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        pw = np.zeros((512, 256, 16), np.uint64)
+        mw = lib.viso_debug_probe_waves_direct(pw.ctypes.data, 512)
+        pw = pw[:mw].astype(np.int64)
+        blk2 = blk[-mw:] if len(blk) >= mw else blk
+        for L in (3, 2, 1, 0):
+            sel = np.where(lv_b[-mw:] == L)[0]
+            if not len(sel):
+                continue
+            T = int(nt[-mw:][sel[0]])
+            b2 = blk2[sel, :T, 1][:, :, None]
+            rel = (pw[sel, :T, :] - b2) * us
+            valid = pw[sel, :T, :] > 0
+            row = []
+            for w in range(16):
+                v = rel[:, :, w][valid[:, :, w]]
+                row.append(f"{np.median(v):5.2f}" if len(v) else "    -")
+            print(f"L({L}) per wave, point(s) done after B2 (p50 us): " + " ".join(row[:15]) + f" | trees stored {row[15]}")
     per = [(entry[i + 1] - entry[i]) * us for i in range(n - 1) if (lvl[i], lvl[i + 1]) in [(3, 2), (2, 1), (1, 0), (0, 3)]]
     print(f"entry-to-entry per launch in the chain: {np.mean(per):.2f} us")
 

@@ -138,7 +138,9 @@ struct viso_ctx {
     viso::DevBuf kp1, kp2, kp1b, kp2b, track_success, n_track_dev;
     viso::FastScratch fast;
     viso::DevBuf fast_rows;
-    int n_track = 0;
+    int n_track = 0;             // < 0: on the device only (ntrack_pending)
+    bool ntrack_pending = false;  // a re-detection frame's count not read yet
+    int resolve_ntrack();
     bool success_valid = false;
     int frame_cnt = 0;
     double initR[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
@@ -179,6 +181,9 @@ struct viso_ctx {
     hipStream_t lk_stream = nullptr;
     hipEvent_t lk_ring[viso::kLkRing] = {};  // recorded after each lk_stream batch
     viso::HostStage stage;  // pinned staging of host-ingested frames (ingest_host)
+    // PoseEstimation2d2d's H path runs on lk_stream beside the E path (no LK
+    // alignment runs while initialising): fork / join events
+    hipEvent_t geo_fork = nullptr, geo_join = nullptr;
     int64_t lk_seq = 0;                      // lk_stream batches launched
     // The last tracking frame's final direct-pose solve (F) is deferred: it
     // runs fused into the next tracking frame's L(3), or alone when the
@@ -251,6 +256,8 @@ struct viso_ctx {
     bool bg_eligible();
     int bg_begin(const std::vector<int>& chunk);
     int bg_end(bool drain = true);
+    // the grid's buffer, event and kernel warm-up (context init)
+    int bg_prepare();
     // after a host sync: VISO_ERR_HIP if a background launch since the last
     // check timed out waiting for a pose (its LK outputs are then invalid)
     int bg_check();

@@ -63,6 +63,9 @@ __device__ unsigned long long g_pexit[kPRing];
 // per-block entry / exit stamps of the last kPRingB launches
 constexpr int kPRingB = 512;
 __device__ unsigned long long g_pblk[kPRingB][256][4];  // entry, after B2, wave 0's points done, exit
+// per block of the last kPRingB launches: [w] wave w's points evaluated
+// (w < 16), [15] the last arriver's tile trees stored
+__device__ unsigned long long g_pwave[kPRingB][256][16];
 #define PROBE_DECL()                                \
     __shared__ unsigned long long pst[kPSt];        \
     const unsigned long long probe_t0 = __builtin_amdgcn_s_memrealtime()
@@ -337,22 +340,27 @@ __device__ inline void point_quotients(const Intrinsics& K, const double* pose, 
     const double fx = K.fx * scale, fy = K.fy * scale;
     const double zz = z * z, xy = x * y;
     // numerator = c1 * c2 (c2 = 1.0 where the numerator is a single value:
-    // exact), denominator z or zz
-    double c1, c2 = 1.0, den = zz;
-    switch (lane < 12 ? lane : 0) {
-        case 0: c1 = x; den = z; break;
-        case 1: c1 = y; den = z; break;
-        case 2: c1 = fx; den = z; break;                 // J[0] = fx / z
-        case 3: c1 = -fx; c2 = x; break;                 // J[2] = -fx * x / zz
-        case 4: c1 = -fx; c2 = xy; break;                // J[3] = -fx * xy / zz
-        case 5: c1 = fx * x; c2 = x; break;              // J[4] = fx + fx * x * x / zz
-        case 6: c1 = -fx; c2 = y; den = z; break;        // J[5] = -fx * y / z
-        case 7: c1 = fy; den = z; break;                 // J[7] = fy / z
-        case 8: c1 = -fy; c2 = y; break;                 // J[8] = -fy * y / zz
-        case 9: c1 = fy * y; c2 = y; break;              // J[9] = -fy - fy * y * y / zz
-        case 10: c1 = fy; c2 = xy; break;                // J[10] = fy * xy / zz
-        default: c1 = fy; c2 = x; den = z; break;        // J[11] = fy * x / z
-    }
+    // exact), denominator z or zz, per lane:
+    //    0: x / z                1: y / z               2: fx / z      (J[0])
+    //    3: -fx * x / zz (J[2])  4: -fx * xy / zz (J[3]) 5: fx*x * x / zz (J[4])
+    //    6: -fx * y / z  (J[5])  7: fy / z   (J[7])      8: -fy * y / zz (J[8])
+    //    9: fy*y * y / zz (J[9]) 10: fy * xy / zz (J[10]) 11: fy * x / z (J[11])
+    // formed by lane-mask selects (v_cndmask), not a switch on the lane (a
+    // divergent switch runs every case's code under its own EXEC mask)
+    const double fxx = fx * x, fyy = fy * y;
+    double c1 = fy;
+    c1 = lane == 0 ? x : c1;
+    c1 = lane == 1 ? y : c1;
+    c1 = lane == 2 ? fx : c1;
+    c1 = (lane == 3 || lane == 4 || lane == 6) ? -fx : c1;
+    c1 = lane == 5 ? fxx : c1;
+    c1 = lane == 8 ? -fy : c1;
+    c1 = lane == 9 ? fyy : c1;
+    double c2 = 1.0;
+    c2 = (lane == 3 || lane == 5 || lane >= 11) ? x : c2;
+    c2 = (lane == 4 || lane == 10) ? xy : c2;
+    c2 = (lane == 6 || lane == 8 || lane == 9) ? y : c2;
+    const double den = (lane <= 2 || lane == 6 || lane == 7 || lane >= 11) ? z : zz;
     double q = (c1 * c2) / den;
     if (lane == 5) q = fx + q;
     if (lane == 9) q = -fy - q;
@@ -770,6 +778,8 @@ __device__ void direct_tile_pf(const DirectArgs& a, const LevelPair& fp, int lv,
     if (lane == 0 && good_cnt) atomicAdd(s_good, good_cnt);
 #ifdef VISO_PROBE
     if (threadIdx.x == 0 && blockIdx.x < 256) g_pblk[a.probe_seq & (kPRingB - 1)][blockIdx.x][2] = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0 && blockIdx.x < 256 && wave < 15)
+        g_pwave[a.probe_seq & (kPRingB - 1)][blockIdx.x][wave] = __builtin_amdgcn_s_memrealtime();
 #endif
     if (s_cnt && T <= 16) {
         const int nw = T < W ? T : W;  // waves that evaluated points
@@ -793,6 +803,10 @@ __device__ void direct_tile_pf(const DirectArgs& a, const LevelPair& fp, int lv,
             part[(size_t)lane * kMaxTiles + b] = r;  // k-major: [28][256]
         }
         if (lane == 0) good[b] = __hip_atomic_load(s_good, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#ifdef VISO_PROBE
+        if (lane == 0 && blockIdx.x < 256)
+            g_pwave[a.probe_seq & (kPRingB - 1)][blockIdx.x][15] = __builtin_amdgcn_s_memrealtime();
+#endif
         return;
     }
     __syncthreads();
@@ -1864,6 +1878,23 @@ extern "C" int viso_debug_probe_ring(unsigned long long* log, unsigned long long
         g_probe_host_seq = 0;
     }
     return 0;
+}
+
+// Per-block, per-wave tile stamps (g_pwave) of the last min(cap, n, 512)
+// launches, in launch order: out[i][b][16].
+extern "C" int viso_debug_probe_waves_direct(unsigned long long* out, int cap) {
+    using namespace viso;
+    static unsigned long long h[kPRingB][256][16];
+    if (hipDeviceSynchronize() != hipSuccess) return -2;
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_pwave), sizeof(h)) != hipSuccess) return -2;
+    const int n = (int)g_probe_host_seq;
+    const int m = std::min(std::min(cap, n), kPRingB);
+    for (int i = 0; i < m; ++i) {
+        const int s = (n - m + i) & (kPRingB - 1);
+        for (int b = 0; b < 256; ++b)
+            for (int k = 0; k < 16; ++k) out[((size_t)i * 256 + b) * 16 + k] = h[s][b][k];
+    }
+    return m;
 }
 
 // Per-block stamps of the last min(cap, n, 512) launches, in launch order:

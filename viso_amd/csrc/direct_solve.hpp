@@ -136,6 +136,10 @@ __device__ __attribute__((always_inline)) inline void solve_finish(SolveLds& L, 
 
 
 
+__device__ __attribute__((always_inline)) inline void solve_after_lu(SolveLds& L, const double* A, const int* tr,
+                                                                      double h, int iter, double* stats,
+                                                                      unsigned long long* stamps);
+
 // One GN step of one level on wave 0 (all 64 lanes): L.S -> update, the new
 // L.state and the loop decision L.cont (src/viso.cpp:731-753).
 __device__ __attribute__((always_inline)) inline void solve_wave0(SolveLds& L, int iter, double* stats,
@@ -194,6 +198,16 @@ __device__ __attribute__((always_inline)) inline void solve_wave0(SolveLds& L, i
             for (int c = k + 1; c < 6; ++c) A[6 * i + c] = A[6 * i + c] - A[6 * i + k] * A[6 * k + c];
     }
     SPROBE(0);
+    solve_after_lu(L, A, tr, h, iter, stats, stamps);
+}
+
+// The rest of the faithful step after the LU factors (A, unit L below the
+// diagonal, U on and above, replicated in every lane) and the row
+// transpositions tr: the inverse, update = H^-1 b, solve_finish.
+__device__ __attribute__((always_inline)) inline void solve_after_lu(SolveLds& L, const double* A, const int* tr,
+                                                                      double h, int iter, double* stats,
+                                                                      unsigned long long* stamps) {
+    const int lane = threadIdx.x & 63;
     // ---- inverse: lane c < 6 solves column c of X = P * I by forward (unit
     // L) and backward (U) substitution
     const int cc = lane < 6 ? lane : 0;

@@ -152,6 +152,17 @@ int viso_ctx::init() {
     if (rc) return rc;
     direct = direct_scratch_at(direct_buf.ptr);
     for (int i = 0; i < kLkRing; ++i) VISO_HIP_CHECK(hipEventCreateWithFlags(&lk_ring[i], hipEventDisableTiming));
+    // the background LK grid's resources and its kernel's first launch, here
+    // rather than in the first tracking chunk (a hipMalloc, the kernel's
+    // dynamic-LDS attribute and code-object load would otherwise land in that
+    // chunk: ~0.1 ms)
+    rc = bg_prepare();
+    if (rc) return rc;
+    VISO_HIP_CHECK(hipEventCreateWithFlags(&geo_fork, hipEventDisableTiming));
+    VISO_HIP_CHECK(hipEventCreateWithFlags(&geo_join, hipEventDisableTiming));
+    // the pose getter's pinned staging (viso_get_poses)
+    h_poses_cap = (size_t)std::min(std::max(p.max_poses, 1), 4096);
+    VISO_HIP_CHECK(hipHostMalloc((void**)&h_poses, 96 * h_poses_cap));
     VISO_HIP_CHECK(hipMemsetAsync(n_track_dev.ptr, 0, 256, stream));
     VISO_HIP_CHECK(hipStreamSynchronize(stream));
     return VISO_OK;
@@ -166,6 +177,10 @@ void viso_ctx::release() {
     }
     if (bg_done) (void)hipEventDestroy(bg_done);
     bg_done = nullptr;
+    for (hipEvent_t* e : {&geo_fork, &geo_join}) {
+        if (*e) (void)hipEventDestroy(*e);
+        *e = nullptr;
+    }
     if (lk_stream) (void)hipStreamDestroy(lk_stream);
     lk_stream = nullptr;
     DevBuf* bufs[] = {&scratch_a, &scratch_b, &scratch_c, &scratch_d, &slot_pool, &slot_pose,
@@ -399,24 +414,27 @@ bool viso_ctx::bg_eligible() {
            kf_interval <= 0 && !dpend && lk_pending.empty();
 }
 
+// ready flags [kLkBatch], eight heads on lines of their own, 32 spare words,
+// leftover list (cursor, count, ..., 4096 items); + 32 words past them: the
+// error word and the drain's item count, kept across chunks (sticky) until
+// bg_check reads and clears them
+static constexpr size_t kBgWords = kLkBatch + 8 * 32 + 32 + 32 + 4096;
+
+int viso_ctx::bg_prepare() {
+    VISO_HIP_CHECK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
+    VISO_HIP_CHECK(hipEventCreateWithFlags(&bg_done, hipEventDisableTiming));
+    int rc = bg_buf.ensure(sizeof(int) * (kBgWords + 32));
+    if (rc) return rc;
+    VISO_HIP_CHECK(hipMemsetAsync(bg_buf.ptr, 0, sizeof(int) * (kBgWords + 32), stream));
+    warm_lk_bg(stream);
+    VISO_HIP_CHECK(hipGetLastError());
+    return VISO_OK;
+}
+
 int viso_ctx::bg_begin(const std::vector<int>& chunk) {
     const int nb = (int)chunk.size();
     if (!bg_eligible() || nb < 1 || nb > kLkBatch) return VISO_OK;
-    if (!n_cu) {
-        VISO_HIP_CHECK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
-        VISO_HIP_CHECK(hipEventCreateWithFlags(&bg_done, hipEventDisableTiming));
-    }
-    // ready flags [kLkBatch], eight heads on lines of their own, error word,
-    // leftover list (cursor, count, 4096 items)
-    // + 32 words past them: the error word and the drain's item count, kept
-    // across chunks (sticky) until bg_check reads and clears them
-    const size_t bg_words = kLkBatch + 8 * 32 + 32 + 32 + 4096;
-    const bool fresh = bg_buf.ptr == nullptr;
-    int rc = bg_buf.ensure(sizeof(int) * (bg_words + 32));
-    if (!rc && fresh) rc = hipMemsetAsync((int*)bg_buf.ptr + bg_words, 0, 32 * sizeof(int), stream) == hipSuccess
-                               ? VISO_OK
-                               : VISO_ERR_HIP;
-    if (rc) return rc;
+    const size_t bg_words = kBgWords;
     LkAlignArgs a = lk_args();
     a.n_frames = nb;
     for (int f = 0; f < nb; ++f) {
@@ -671,17 +689,26 @@ int viso_ctx::on_new_frame(int cur) {
             }
             if (frame_cnt > 0 && frame_cnt <= p.reinitialize_after) {
                 stats[3] = -1;
+                // n_track < 0: the re-detection frame before this one left its
+                // count on the device only; the KLT and the compaction read it
+                // there (capped at max_features)
                 const int n = n_track;
-                if (n > 0) {
+                if (n != 0) {
                     TimedRegion t(timing, VISO_KERNEL_KLT, stream);
-                    launch_klt(frame(ref_slot), frame(cur), g, (const float2*)kp1.ptr,
-                               (float2*)kp2.ptr, (uint8_t*)track_success.ptr, n,
-                               p.photometric_error_thresh, stream);
+                    if (n > 0)
+                        launch_klt(frame(ref_slot), frame(cur), g, (const float2*)kp1.ptr,
+                                   (float2*)kp2.ptr, (uint8_t*)track_success.ptr, n,
+                                   p.photometric_error_thresh, stream);
+                    else
+                        launch_klt_dev(frame(ref_slot), frame(cur), g, (const float2*)kp1.ptr,
+                                       (float2*)kp2.ptr, (uint8_t*)track_success.ptr, (const int*)n_track_dev.ptr,
+                                       p.max_features, p.photometric_error_thresh, stream);
                 }
                 // erase failed tracks (src/viso.cpp:23-40)
                 launch_compact_tracks((const float2*)kp1.ptr, (const float2*)kp2.ptr,
-                                      (const uint8_t*)track_success.ptr, n, (float2*)kp1b.ptr,
-                                      (float2*)kp2b.ptr, (int*)n_track_dev.ptr, stream);
+                                      (const uint8_t*)track_success.ptr, n >= 0 ? n : -p.max_features,
+                                      (float2*)kp1b.ptr, (float2*)kp2b.ptr, (int*)n_track_dev.ptr, stream);
+                ntrack_pending = false;
                 std::swap(kp1, kp1b);
                 std::swap(kp2, kp2b);
                 success_valid = false;
@@ -703,7 +730,7 @@ int viso_ctx::on_new_frame(int cur) {
                 if (h_ctl->gate) {
                     {
                         TimedRegion t(timing, VISO_KERNEL_RANSAC, stream);
-                        launch_pose_2d2d_body(geo, stream);
+                        launch_pose_2d2d_body(geo, stream, lk_stream, geo_fork, geo_join);
                     }
                     VISO_HIP_CHECK(hipGetLastError());
                     VISO_HIP_CHECK(hipMemcpyAsync(h_ctl, geo.ctl, sizeof(GeoCtl), hipMemcpyDeviceToHost, stream));
@@ -763,18 +790,20 @@ int viso_ctx::on_new_frame(int cur) {
                                 stream);
                 }
                 VISO_HIP_CHECK(hipGetLastError());
-                VISO_HIP_CHECK(hipMemcpyAsync(h_int, n_track_dev.ptr, sizeof(int), hipMemcpyDeviceToHost, stream));
-                VISO_HIP_CHECK(hipStreamSynchronize(stream));
-                n_track = std::min(h_int[0], p.max_features);
-                h_int[1] = n_track;
-                VISO_HIP_CHECK(hipMemcpyAsync(n_track_dev.ptr, &h_int[1], sizeof(int), hipMemcpyHostToDevice, stream));
-                if (n_track > 0)
-                    VISO_HIP_CHECK(hipMemcpyAsync(kp2.ptr, kp1.ptr, sizeof(float2) * (size_t)n_track,
-                                                  hipMemcpyDeviceToDevice, stream));
+                // no host round trip: the count is capped and kp2 = kp1 on the
+                // device, the next frame's KLT reads the count there, and the
+                // host learns it lazily (resolve_ntrack: a getter, or the next
+                // frame's gate read)
+                launch_detect_finish((int*)n_track_dev.ptr, p.max_features, (const float2*)kp1.ptr,
+                                     (float2*)kp2.ptr, stream);
+                VISO_HIP_CHECK(hipGetLastError());
+                VISO_HIP_CHECK(hipMemcpyAsync(h_int + 3, n_track_dev.ptr, sizeof(int), hipMemcpyDeviceToHost, stream));
+                n_track = -1;
+                ntrack_pending = true;
                 success_valid = false;
                 set_role(ref_slot, cur);
                 frame_cnt = 0;
-                stats[1] = n_track;
+                stats[1] = -1;  // resolve_ntrack fills it in
             }
             if (counted) ++frame_cnt;
             break;
@@ -1035,10 +1064,22 @@ int viso_get_points(viso_ctx* c, double* xyz, size_t cap, size_t* n) {
     return VISO_OK;
 }
 
+// A re-detection frame's corner count, read lazily (on_new_frame leaves it
+// on the device and copies it to pinned h_int[3] behind the frame).
+int viso_ctx::resolve_ntrack() {
+    if (!ntrack_pending) return VISO_OK;
+    VISO_HIP_CHECK(hipStreamSynchronize(stream));
+    n_track = std::min(h_int[3], p.max_features);
+    if (stats[1] == -1) stats[1] = n_track;
+    ntrack_pending = false;
+    return VISO_OK;
+}
+
 int viso_get_init_tracks(viso_ctx* c, float* kp1, float* kp2, uint8_t* success, size_t cap,
                          size_t* n) {
     if (!c) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(c->device));
+    if (int rc = c->resolve_ntrack()) return rc;
     const size_t m = std::min(cap, (size_t)c->n_track);
     if (m > 0) {
         if (kp1) VISO_HIP_CHECK(hipMemcpyAsync(kp1, c->kp1.ptr, 8 * m, hipMemcpyDeviceToHost, c->stream));
@@ -1077,6 +1118,7 @@ int viso_get_alignment(viso_ctx* c, int32_t* pair_kf, uint8_t* success, double* 
 int viso_get_frame_stats(viso_ctx* c, double out[16]) {
     if (!c || !out) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(c->device));
+    if (int rc = c->resolve_ntrack()) return rc;
     std::memcpy(out, c->stats, sizeof(c->stats));
     if (c->state == VISO_STATE_RUNNING && c->stats[12] == 0 && c->ran_tracking) {
         // last frame was a tracking frame: level-0 direct stats + LK counts

@@ -170,6 +170,7 @@ __global__ __launch_bounds__(kNormThreads) void normalize_kernel(GeoArgs a) {
         c->disparity = d;
         c->gate = (n >= 10 && !(d < a.disparity_thresh)) ? 1 : 0;
         c->n_cand = 0;
+        c->e_ncand = c->h_ncand = 0;
         c->e_count = c->h_count = 0;
         c->e_best = c->h_best = -1;
         c->e_iters = c->h_iters = 0;
@@ -679,10 +680,10 @@ __global__ __launch_bounds__(64) void recover_pick_kernel(GeoArgs a) {
         pick = 2;
     else
         pick = 3;
-    double* cand = c->cand[c->n_cand];
+    double* cand = c->cand[0];  // the E path's slot
     for (int k = 0; k < 9; ++k) cand[k] = a.rp[9 * (pick & 1) + k];
     for (int k = 0; k < 3; ++k) cand[9 + k] = pick >= 2 ? -a.rp[18 + k] : a.rp[18 + k];
-    c->n_cand += 1;
+    c->e_ncand = 1;
 }
 
 // ---------------------------------------------------------------- H refine moments
@@ -872,10 +873,10 @@ __global__ __launch_bounds__(64) void h_refine_decompose_kernel(GeoArgs a) {
     double mx = 0;
     for (int k = 0; k < 9; ++k) mx = fmax(mx, fabs(S[k]));
     if (mx < 0.001) {
-        double* cand = c->cand[c->n_cand];
+        double* cand = c->cand[1];  // the H path's slots start at 1
         for (int k = 0; k < 9; ++k) cand[k] = Hn[k];
         cand[9] = cand[10] = cand[11] = 0;
-        c->n_cand += 1;
+        c->h_ncand = 1;
         return;
     }
     auto minor = [&](int row, int col) {
@@ -946,24 +947,28 @@ __global__ __launch_bounds__(64) void h_refine_decompose_kernel(GeoArgs a) {
     const double* ts[4] = {ta, ta, tb, tb};
     const double sg[4] = {1, -1, 1, -1};
     for (int m = 0; m < 4; ++m) {
-        double* cand = c->cand[c->n_cand];
+        double* cand = c->cand[1 + m];
         for (int k = 0; k < 9; ++k) cand[k] = Rs[m][k];
         for (int k = 0; k < 3; ++k) cand[9 + k] = sg[m] > 0 ? ts[m][k] : -ts[m][k];
-        c->n_cand += 1;
     }
+    c->h_ncand = 4;
 }
+
+// candidate mi of SelectMotion (the reference's order: recoverPose's, then
+// decomposeHomographyMat's) -> its slot
+__device__ inline int cand_slot(const GeoCtl* c, int mi) { return mi < c->e_ncand ? 0 : 1 + (mi - c->e_ncand); }
 
 // ---------------------------------------------------------------- SelectMotion
 __global__ __launch_bounds__(256) void select_points_kernel(GeoArgs a) {
     const GeoCtl* c = a.ctl;
     if (!c->gate) return;
-    const int n = c->n, m = c->n_cand;
+    const int n = c->n, m = c->e_ncand + c->h_ncand;
     const int gid = blockIdx.x * 256 + threadIdx.x;
     const int mi = gid / a.cap, i = gid - mi * a.cap;
     if (mi >= m || i >= n) return;
     const double kPi = 3.14159265358979323846;
-    const double* R = c->cand[mi];
-    const double* T = c->cand[mi] + 9;
+    const double* R = c->cand[cand_slot(c, mi)];
+    const double* T = c->cand[cand_slot(c, mi)] + 9;
     uint8_t* inl = a.sel_in + (size_t)mi * a.cap;
     double* pts = a.sel_pts + (size_t)mi * a.cap * 3;
     inl[i] = 0;
@@ -1006,7 +1011,7 @@ __global__ __launch_bounds__(256) void select_reduce_kernel(GeoArgs a) {
     __shared__ int s_best, s_bestn;
     GeoCtl* c = a.ctl;
     if (!c->gate) return;
-    const int n = c->n, m = c->n_cand;
+    const int n = c->n, m = c->e_ncand + c->h_ncand;
     if (threadIdx.x == 0) {
         s_best = -1;
         s_bestn = 0;
@@ -1035,11 +1040,12 @@ __global__ __launch_bounds__(256) void select_reduce_kernel(GeoArgs a) {
         mean = block_tree_sum(n, [&](int i) { return inl[i] ? pts[3 * i + 2] : 0.0; }, s_red);
     }
     if (threadIdx.x == 0) {
+        c->n_cand = m;
         c->nr_inliers = nr;
         c->best_motion = best;
         if (best >= 0) {
-            for (int k = 0; k < 9; ++k) c->R[k] = c->cand[best][k];
-            for (int k = 0; k < 3; ++k) c->T[k] = c->cand[best][9 + k];
+            for (int k = 0; k < 9; ++k) c->R[k] = c->cand[cand_slot(c, best)][k];
+            for (int k = 0; k < 3; ++k) c->T[k] = c->cand[cand_slot(c, best)][9 + k];
         }
         c->mean_depth = mean;
         c->mean_nonzero = mean != 0 ? 1 : 0;
@@ -1098,7 +1104,24 @@ void launch_pose_2d2d_gate(const GeoArgs& a, hipStream_t stream) {
     normalize_kernel<<<1, kNormThreads, 0, stream>>>(a);
 }
 
-void launch_pose_2d2d_body(const GeoArgs& a, hipStream_t stream) {
+void launch_pose_2d2d_body(const GeoArgs& a, hipStream_t stream, hipStream_t hs, hipEvent_t fork,
+                           hipEvent_t join) {
+    // the H path on hs (when given), concurrent with the E path on stream
+    const bool split = hs && fork && join && a.h_iters > 0;
+    hipStream_t sh = stream;
+    if (split) {
+        (void)hipEventRecord(fork, stream);
+        (void)hipStreamWaitEvent(hs, fork, 0);
+        sh = hs;
+    }
+    if (a.h_iters > 0) {
+        h_hyp_kernel<<<(a.h_iters + 3) / 4, 256, 0, sh>>>(a);
+        score_kernel<false><<<a.h_iters, 256, 0, sh>>>(a);
+        scan_kernel<false><<<1, 256, 0, sh>>>(a);
+        h_moment_leaves_kernel<<<(a.cap + 255) / 256, 256, 0, sh>>>(a);
+        h_moment_sums_kernel<<<45, 256, 0, sh>>>(a);
+        h_refine_decompose_kernel<<<1, 64, 0, sh>>>(a);
+    }
     if (a.e_iters > 0) {
         e_hyp_kernel<<<(a.e_iters + 3) / 4, 256, 0, stream>>>(a);
         score_kernel<true><<<a.e_iters, 256, 0, stream>>>(a);
@@ -1107,13 +1130,9 @@ void launch_pose_2d2d_body(const GeoArgs& a, hipStream_t stream) {
         recover_count_kernel<<<(4 * a.cap + 255) / 256, 256, 0, stream>>>(a);
         recover_pick_kernel<<<1, 64, 0, stream>>>(a);
     }
-    if (a.h_iters > 0) {
-        h_hyp_kernel<<<(a.h_iters + 3) / 4, 256, 0, stream>>>(a);
-        score_kernel<false><<<a.h_iters, 256, 0, stream>>>(a);
-        scan_kernel<false><<<1, 256, 0, stream>>>(a);
-        h_moment_leaves_kernel<<<(a.cap + 255) / 256, 256, 0, stream>>>(a);
-        h_moment_sums_kernel<<<45, 256, 0, stream>>>(a);
-        h_refine_decompose_kernel<<<1, 64, 0, stream>>>(a);
+    if (split) {
+        (void)hipEventRecord(join, hs);
+        (void)hipStreamWaitEvent(stream, join, 0);
     }
     const int total = 5 * a.cap;
     select_points_kernel<<<(total + 255) / 256, 256, 0, stream>>>(a);

@@ -19,6 +19,11 @@ struct GeoCtl {
     int e_count, e_best, e_iters;
     int h_count, h_best, h_iters;
     int n_cand;
+    // candidate slots: [0] recoverPose's (E path, e_ncand = 0 or 1), [1..4]
+    // decomposeHomographyMat's (H path, h_ncand of them) — fixed slots, so
+    // the two paths can run concurrently; SelectMotion walks them in the
+    // reference's order (E first, then H; src/viso.cpp:236-244)
+    int e_ncand, h_ncand;
     double cand[kMaxCandidates][12];
     double H[9];
     int nr_inliers, best_motion;
@@ -78,6 +83,10 @@ void launch_pose_2d2d(const GeoArgs& a, hipStream_t stream, Timing* timing);
 // returns at once when the gate is closed; a caller that has read the gate
 // on the host may skip the body.
 void launch_pose_2d2d_gate(const GeoArgs& a, hipStream_t stream);
-void launch_pose_2d2d_body(const GeoArgs& a, hipStream_t stream);
+// hs (optional): a second stream for the H path, forked from / joined to
+// `stream` by the events fork / join (the E and H RANSAC chains are
+// independent until SelectMotion)
+void launch_pose_2d2d_body(const GeoArgs& a, hipStream_t stream, hipStream_t hs = nullptr,
+                           hipEvent_t fork = nullptr, hipEvent_t join = nullptr);
 
 }  // namespace viso

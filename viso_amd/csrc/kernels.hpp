@@ -36,8 +36,15 @@ void launch_fast(const uint8_t* img, int w, int h, int thresh, FastScratch& s, f
 // OpticalFlowMultiLevel(inverse=true): kp2 in/out, success out (level 0).
 void launch_klt(const FrameDev& ref, const FrameDev& cur, const PyrGeom& g, const float2* kp1,
                 float2* kp2, uint8_t* success, int n, double thresh, hipStream_t stream);
+// the same with the track count in device memory (*n_dev, capped at cap)
+void launch_klt_dev(const FrameDev& ref, const FrameDev& cur, const PyrGeom& g, const float2* kp1,
+                    float2* kp2, uint8_t* success, const int* n_dev, int cap, double thresh, hipStream_t stream);
+// a re-detection frame's FAST count capped at cap and kp2 = kp1 over it, on
+// the device
+void launch_detect_finish(int* n_dev, int cap, const float2* kp1, float2* kp2, hipStream_t stream);
 // Order-preserving erase of failed tracks (src/viso.cpp:23-40):
-// kp1/kp2[0..n) with success -> out arrays; *n_out = survivors.
+// kp1/kp2[0..n) with success -> out arrays; *n_out = survivors.  n < 0:
+// the count is *n_out's input value, capped at -n.
 void launch_compact_tracks(const float2* kp1, const float2* kp2, const uint8_t* success, int n,
                            float2* kp1_out, float2* kp2_out, int* n_out, hipStream_t stream);
 
@@ -97,6 +104,8 @@ void launch_lk_bg(const LkAlignArgs& a, int grid, hipStream_t stream);
 // the items of a background launch it has not taken yet, at full occupancy
 // (after the chunk's last pose): grid workgroups pull from the same counter
 void launch_lk_drain(const LkAlignArgs& a, int grid, hipStream_t stream);
+// the background kernel's attribute and first launches (context init)
+void warm_lk_bg(hipStream_t stream);
 // Keyframe choice + per-level templates of every map point (once per map).
 void launch_lk_template(const LkAlignArgs& a, hipStream_t stream);
 

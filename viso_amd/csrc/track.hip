@@ -121,15 +121,26 @@ __device__ inline Window load_window(uint8_t* lds, const uint8_t* img, int w, in
     return window_commit(lds, window_issue(img, w, h, cx, cy));
 }
 
-// GetPixelValue's bilinear sample with its four taps read from the window
-__device__ inline double win_bilinear(const Window& win, double x, double y, int ix, int iy) {
-    const int o = (iy - win.y0) * kWinW + (ix - win.x0);
-    const double d0 = (double)ld_lds_u8(win.lds, o), d1 = (double)ld_lds_u8(win.lds, o + 1);
-    const double d2 = (double)ld_lds_u8(win.lds, o + kWinW);
-    const double d3 = (double)ld_lds_u8(win.lds, o + kWinW + 1);
+// GetPixelValue's bilinear expression on the four taps packed in t (bytes
+// d0 | d1 << 8 | d2 << 16 | d3 << 24)
+__device__ inline double bilerp_packed(double x, double y, uint32_t t) {
+    const double d0 = (double)(t & 0xff), d1 = (double)((t >> 8) & 0xff);
+    const double d2 = (double)((t >> 16) & 0xff), d3 = (double)(t >> 24);
     const double xx = x - floor(x);
     const double yy = y - floor(y);
     return double((1 - xx) * (1 - yy) * d0 + xx * (1 - yy) * d1 + (1 - xx) * yy * d2 + xx * yy * d3);
+}
+
+// the four window taps of base pixel (ix, iy), packed
+__device__ inline uint32_t win_taps(const Window& win, int ix, int iy) {
+    const int o = (iy - win.y0) * kWinW + (ix - win.x0);
+    return (uint32_t)ld_lds_u8(win.lds, o) | ((uint32_t)ld_lds_u8(win.lds, o + 1) << 8) |
+           ((uint32_t)ld_lds_u8(win.lds, o + kWinW) << 16) | ((uint32_t)ld_lds_u8(win.lds, o + kWinW + 1) << 24);
+}
+
+// GetPixelValue's bilinear sample with its four taps read from the window
+__device__ inline double win_bilinear(const Window& win, double x, double y, int ix, int iy) {
+    return bilerp_packed(x, y, win_taps(win, ix, iy));
 }
 
 // The GN iterations' window follows the point: once the wave's taps leave
@@ -198,6 +209,36 @@ __device__ inline double sample_win_follow(const uint8_t* __restrict__ img, int 
     return in ? win_bilinear(win, x, y, ix, iy) : sample_px(img, w, h, x, y);
 }
 
+// The GN loop's taps of the last window sample, per lane: base pixel (ix,
+// iy) and its four bytes.  A converging point's steps are mostly sub-pixel,
+// so its base pixels repeat; the taps are buffer bytes (the window mirrors the
+// level buffer), so reusing them gives sample_win_follow's value without the
+// LDS round trip on the iteration's dependency chain.
+struct TapCache {
+    int ix, iy;  // INT_MIN: empty
+    uint32_t t;
+};
+
+template <bool FINITE = false>
+__device__ inline double sample_win_cached(const uint8_t* __restrict__ img, int w, int h, double x, double y,
+                                           Window& win, TapCache& tc) {
+    if (!win.lds) return sample_px(img, w, h, x, y);  // wave-uniform (window_issue)
+    const bool finite = FINITE || (x > -1e9 && x < 1e9 && y > -1e9 && y < 1e9);
+    const int ix = finite ? (int)x : 0, iy = finite ? (int)y : 0;
+    if (__builtin_amdgcn_ballot_w64(finite && ix == tc.ix && iy == tc.iy) == ~0ull) return bilerp_packed(x, y, tc.t);
+    const bool in = finite && (unsigned)(ix - win.x0) < (unsigned)(kWinW - 1) &&
+                    (unsigned)(iy - win.y0) < (unsigned)(kWinH - 1);
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(in) == ~0ull, 1) ||
+        window_follow(img, w, h, ix, iy, finite, win)) {
+        tc.t = win_taps(win, ix, iy);
+        tc.ix = ix;
+        tc.iy = iy;
+        return bilerp_packed(x, y, tc.t);
+    }
+    tc.ix = INT_MIN;
+    return in ? win_bilinear(win, x, y, ix, iy) : sample_px(img, w, h, x, y);
+}
+
 // The per-level template of the inverse-compositional LK: this lane's
 // template value I1 and Jacobian (J0, J1) = -grad at ref, and the 2x2 inverse
 // of H = sum J J^T (canonical wave trees).  It depends only on the reference
@@ -262,6 +303,7 @@ __device__ inline LkResult lk_iterate(const LkTemplate& t, int w1, int h1,
     double cost = 0, lastCost = 0;
     bool succ = true;
     int iter = 0;
+    TapCache tc{INT_MIN, INT_MIN, 0u};
     for (; iter < MAXIT; ++iter) {
         // a point still iterating after boost_at steps (the background grid's
         // last frame, VISO_LK_BOOST): its wave outranks the short points'
@@ -277,7 +319,7 @@ __device__ inline LkResult lk_iterate(const LkTemplate& t, int w1, int h1,
             succ = false;
             break;
         }
-        const double e = t.I1 - sample_win_follow<!KLT_BOUNDS>(img2, w2, h2, cur_x + dx, cur_y + dy, win);
+        const double e = t.I1 - sample_win_cached<!KLT_BOUNDS>(img2, w2, h2, cur_x + dx, cur_y + dy, win, tc);
         double B0, B1;
         if (KLT_BOUNDS)
             wave_tree_sum3(-t.J0 * e, -t.J1 * e, e * e, B0, B1, cost);
@@ -365,17 +407,13 @@ __device__ inline LkResult lk_iterate_fast(float I1, float J0, float J1, const f
     return {dx, dy, succ, iter};
 }
 
-__global__ __launch_bounds__(256) void klt_kernel(FrameDev ref, FrameDev cur, PyrDev g,
-                                                  const float2* __restrict__ kp1,
-                                                  float2* __restrict__ kp2,
-                                                  uint8_t* __restrict__ success, int n,
-                                                  double thresh) {
-    __shared__ uint8_t s_win[4][kWinW * kWinH];
-    const int i = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-    if (i >= n) return;  // wave-uniform
+__device__ __attribute__((always_inline)) inline void klt_track_body(FrameDev ref, FrameDev cur, PyrDev g,
+                                                                     const float2* __restrict__ kp1,
+                                                                     float2* __restrict__ kp2,
+                                                                     uint8_t* __restrict__ success, int i,
+                                                                     double thresh, uint8_t* my_win) {
     const int lane = threadIdx.x & 63;
     const int px = (lane >> 3) - 4, py = (lane & 7) - 4;
-    uint8_t* my_win = s_win[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
     const float2 k1 = kp1[i];
     float2 k2 = kp2[i];
     // kp2[j].pt *= scales[3]  (saturate_cast<float>(x * 0.125))
@@ -409,6 +447,22 @@ __global__ __launch_bounds__(256) void klt_kernel(FrameDev ref, FrameDev cur, Py
         success[i] = succ ? 1 : 0;
     }
 }
+
+// n_dev (optional): the track count in device memory (after a re-detection
+// frame, whose FAST count the host has not read), capped at n; the waves then
+// stride over the tracks (grid waves apart)
+__global__ __launch_bounds__(256) void klt_kernel(FrameDev ref, FrameDev cur, PyrDev g,
+                                                  const float2* __restrict__ kp1,
+                                                  float2* __restrict__ kp2,
+                                                  uint8_t* __restrict__ success, int n,
+                                                  double thresh, const int* __restrict__ n_dev) {
+    __shared__ uint8_t s_win[4][kWinW * kWinH];
+    if (n_dev) n = min(__builtin_amdgcn_readfirstlane(*n_dev), n);
+    const int stride = __builtin_amdgcn_readfirstlane(gridDim.x * 4);
+    for (int i = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); i < n; i += stride)
+        klt_track_body(ref, cur, g, kp1, kp2, success, i, thresh, s_win[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)]);
+}
+
 
 // Keyframe choice of one map point (LKAlignment, src/viso.cpp:774-800):
 // the keyframe with the smallest viewing angle (Keyframe::ViewingAngle,
@@ -723,6 +777,7 @@ constexpr int kBgLeftCap = 4096;                           // leftover items (on
 constexpr int kBgClosed = 1 << 30;                          // bg_left[1]: the drain has read the count
 template <bool FAST>
 __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
+    if (a.n_frames <= 0) return;  // warm_lk_bg
     __shared__ uint8_t s_win[4][2][kWinW * kWinH];
     __shared__ double s_pose[4][12];  // the wave's current frame pose
     const LkAlignArgs* ka = (const LkAlignArgs*)__builtin_amdgcn_kernarg_segment_ptr();
@@ -1003,6 +1058,10 @@ __global__ __launch_bounds__(1024) void compact_tracks_kernel(const float2* __re
                                                               float2* __restrict__ o2,
                                                               int* __restrict__ n_out) {
     __shared__ int s_w[16];
+    // n < 0: the count is *n_out's input value, capped at -n (a re-detection
+    // frame's FAST count the host has not read)
+    if (n < 0) n = min(*n_out, -n);
+    __syncthreads();  // every thread has read *n_out before thread 1023 writes it
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int C = (n + 1023) / 1024;
     const int lo = min(t * C, n), hi = min(lo + C, n);
@@ -1027,7 +1086,21 @@ __global__ __launch_bounds__(1024) void compact_tracks_kernel(const float2* __re
     if (t == 1023) *n_out = off;
 }
 
+// After FAST on a re-detection frame (src/viso.cpp:100-108): the corner
+// count capped at cap, and kp2 = kp1 over it, on the device (no host read).
+__global__ __launch_bounds__(256) void detect_finish_kernel(int* __restrict__ n_dev, int cap,
+                                                             const float2* __restrict__ kp1,
+                                                             float2* __restrict__ kp2) {
+    const int n = min(*n_dev, cap);
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) kp2[i] = kp1[i];
+    if (blockIdx.x == 0 && threadIdx.x == 0) *n_dev = n;  // idempotent: every reader caps alike
+}
+
 }  // namespace
+
+void launch_detect_finish(int* n_dev, int cap, const float2* kp1, float2* kp2, hipStream_t stream) {
+    detect_finish_kernel<<<std::max(1, std::min((cap + 255) / 256, 64)), 256, 0, stream>>>(n_dev, cap, kp1, kp2);
+}
 
 void launch_compact_tracks(const float2* kp1, const float2* kp2, const uint8_t* success, int n,
                            float2* kp1_out, float2* kp2_out, int* n_out, hipStream_t stream) {
@@ -1038,7 +1111,15 @@ void launch_klt(const FrameDev& ref, const FrameDev& cur, const PyrGeom& g, cons
                 float2* kp2, uint8_t* success, int n, double thresh, hipStream_t stream) {
     if (n <= 0) return;
     klt_kernel<<<(n + 3) / 4, 256, 0, stream>>>(ref, cur, make_pyrdev(g), kp1, kp2, success, n,
-                                                 thresh);
+                                                 thresh, nullptr);
+}
+
+void launch_klt_dev(const FrameDev& ref, const FrameDev& cur, const PyrGeom& g, const float2* kp1,
+                    float2* kp2, uint8_t* success, const int* n_dev, int cap, double thresh, hipStream_t stream) {
+    if (cap <= 0) return;
+    // one wave per track up to 8,192 tracks, striding beyond
+    const int blocks = (std::min(cap, 8192) + 3) / 4;
+    klt_kernel<<<blocks, 256, 0, stream>>>(ref, cur, make_pyrdev(g), kp1, kp2, success, cap, thresh, n_dev);
 }
 
 void launch_lk_align(const LkAlignArgs& a, hipStream_t stream) {
@@ -1054,21 +1135,38 @@ void launch_lk_align(const LkAlignArgs& a, hipStream_t stream) {
 // two never share a CU (2 x 84 > 160 KB) while one leaves room for a 12-wave
 // direct-pose workgroup (84 + 68 <= 160 KB)
 constexpr size_t kBgLdsTotal = 84 * 1024;
-void launch_lk_bg(const LkAlignArgs& a, int grid, hipStream_t stream) {
-    if (a.n <= 0 || a.bg_items <= 0 || grid <= 0) return;
+// the resident grid's dynamic LDS (its request minus the static windows);
+// the kernel's attribute is raised to it once
+static size_t lk_bg_dyn_lds() {
     const size_t dyn = kBgLdsTotal - sizeof(uint8_t) * 4 * 2 * kWinW * kWinH;
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)lk_item_kernel<true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
-        (void)hipFuncSetAttribute((const void*)lk_item_kernel<false>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+        (void)hipFuncSetAttribute((const void*)lk_item_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)dyn);
+        (void)hipFuncSetAttribute((const void*)lk_item_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)dyn);
         attr = true;
     }
+    return dyn;
+}
+void launch_lk_bg(const LkAlignArgs& a, int grid, hipStream_t stream) {
+    if (a.n <= 0 || a.bg_items <= 0 || grid <= 0) return;
+    const size_t dyn = lk_bg_dyn_lds();
     if (a.fast)
         lk_item_kernel<true><<<grid, 256, dyn, stream>>>(a);
     else
         lk_item_kernel<false><<<grid, 256, dyn, stream>>>(a);
+}
+
+// The background kernel's one-time costs (its dynamic-LDS attribute, the
+// first launch of both precisions) at context init: a one-workgroup launch
+// with no frames returns at once.
+void warm_lk_bg(hipStream_t stream) {
+    (void)lk_bg_dyn_lds();
+    LkAlignArgs a{};
+    a.n_frames = 0;
+    lk_item_kernel<true><<<1, 256, 0, stream>>>(a);
+    lk_item_kernel<false><<<1, 256, 0, stream>>>(a);
 }
 
 void launch_lk_drain(const LkAlignArgs& a, int grid, hipStream_t stream) {
