@@ -1,5 +1,5 @@
 // Micro-benchmark of the direct-pose level solve (dev tool; not part of the
-// library): one workgroup runs solve_wave0 (viso_amd/csrc/direct_solve.hpp)
+// library): one workgroup runs a solve of viso_amd/csrc/direct_solve.hpp
 // REPS times on a fixed symmetric positive-definite H / b and reports the
 // mean s_memrealtime ticks (100 MHz) per solve, plus the result bits so that
 // variants can be checked for bit-identity.
@@ -23,64 +23,7 @@ __device__ unsigned long long g_probe[128];
 #define REPS 200
 #endif
 
-// Lane-per-element PartialPivLU: lane 6 r + c < 36 holds
-// A[r][c]; per step the pivot column is read by readlane (uniform, first
-// maximal |pivot| wins as in Eigen), the row swap and the rank-1 update's
-// operands move by ds_bpermute, the division and update are one element per
-// lane with the replicated form's operations.  The factors then go through
-// LDS into every lane's registers for solve_after_lu (same inverse / update /
-// finish), so the result bits must equal solve_wave0's.
-__device__ inline double bperm_f64(double v, int src) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_ds_bpermute(src * 4, (int)(b & 0xffffffffLL));
-    const int hi = __builtin_amdgcn_ds_bpermute(src * 4, (int)(b >> 32));
-    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-
-__device__ void solve_wave0_lanelu(SolveLds& L, int iter, double* stats, unsigned long long* stamps = nullptr) {
-    const int lane = threadIdx.x & 63;
-    const int r = lane / 6, c = lane - 6 * (lane / 6);
-    const bool in = lane < 36;
-    const int r0 = r < c ? r : c, c0 = r < c ? c : r;
-    const double h = in ? L.S[r0 * 6 - (r0 * (r0 - 1)) / 2 + (c0 - r0)] : 0.0;
-    double a = h;
-    int tr[6];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-        int p = k;
-        double best = fabs(readlane_f64(a, 7 * k));
-#pragma unroll
-        for (int i = k + 1; i < 6; ++i) {
-            const double s = fabs(readlane_f64(a, 6 * i + k));
-            if (s > best) {
-                best = s;
-                p = i;
-            }
-        }
-        p = __builtin_amdgcn_readfirstlane(p);
-        tr[k] = p;
-        if (__builtin_amdgcn_readfirstlane(best != 0.0 ? 1 : 0)) {
-            if (p != k) a = bperm_f64(a, r == k ? 6 * p + c : (r == p ? 6 * k + c : lane));
-            const double piv = readlane_f64(a, 7 * k);
-            if (in && r > k && c == k) a = a / piv;
-        }
-        if (k < 5) {
-            const double lk = bperm_f64(a, 6 * r + k), kc = bperm_f64(a, 6 * k + c);
-            if (in && r > k && c > k) a = a - lk * kc;
-        }
-    }
-    double* T = &L.red[0][0];
-    if (in) T[lane] = a;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    double A[36];
-#pragma unroll
-    for (int i = 0; i < 36; ++i) A[i] = T[i];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    SPROBE(0);
-    solve_after_lu(L, A, tr, h, iter, stats, stamps);
-}
-
-template <int MODE>  // 0 replicated LU, 1 LDL^T (fast mode), 2 lane-per-element LU
+template <int MODE>  // 0 replicated LU (round 4), 1 LDL^T (fast mode), 2 lane-per-element LU
 __global__ void bench(const double* S28, const double* st7, double* out, unsigned long long* ticks) {
     __shared__ SolveLds L;
     const int lane = threadIdx.x & 63;
@@ -103,16 +46,16 @@ __global__ void bench(const double* S28, const double* st7, double* out, unsigne
             if (MODE == 1)
                 solve_wave0_ldlt(L, 0, nullptr, stamps);
             else if (MODE == 2)
-                solve_wave0_lanelu(L, 0, nullptr, stamps);
+                solve_wave0_lane(L, 0, nullptr, stamps);
             else
-                solve_wave0(L, 0, nullptr, stamps);
+                solve_wave0_rep(L, 0, nullptr, stamps);
 #else
             if (MODE == 1)
                 solve_wave0_ldlt(L, 0, nullptr);
             else if (MODE == 2)
-                solve_wave0_lanelu(L, 0, nullptr);
+                solve_wave0_lane(L, 0, nullptr);
             else
-                solve_wave0(L, 0, nullptr);
+                solve_wave0_rep(L, 0, nullptr);
 #endif
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             acc += __builtin_amdgcn_s_memrealtime() - t0;

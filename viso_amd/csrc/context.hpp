@@ -264,6 +264,7 @@ struct viso_ctx {
     int bg_launch();
     bool bg_unchecked = false;
     bool bg_active = false;
+    bool bg_launched = false;  // bg_begin cleared the words; the grid is launched after frame 0
     int bg_mode = -1;        // VISO_LK_BG: 0 off, 1 on (read once; -1 unread)
     int bg_nb = 0;           // frames of the chunk
     int bg_cur = -1;         // chunk index of the frame on_new_frame is processing

@@ -347,6 +347,23 @@ __device__ inline void point_quotients(const Intrinsics& K, const double* pose, 
     //    9: fy*y * y / zz (J[9]) 10: fy * xy / zz (J[10]) 11: fy * x / z (J[11])
     // formed by lane-mask selects (v_cndmask), not a switch on the lane (a
     // divergent switch runs every case's code under its own EXEC mask)
+#ifdef VISO_QUOT_SWITCH  // dev A/B: the round-4 switch form
+    double c1, c2 = 1.0, den = zz;
+    switch (lane < 12 ? lane : 0) {
+        case 0: c1 = x; den = z; break;
+        case 1: c1 = y; den = z; break;
+        case 2: c1 = fx; den = z; break;
+        case 3: c1 = -fx; c2 = x; break;
+        case 4: c1 = -fx; c2 = xy; break;
+        case 5: c1 = fx * x; c2 = x; break;
+        case 6: c1 = -fx; c2 = y; den = z; break;
+        case 7: c1 = fy; den = z; break;
+        case 8: c1 = -fy; c2 = y; break;
+        case 9: c1 = fy * y; c2 = y; break;
+        case 10: c1 = fy; c2 = xy; break;
+        default: c1 = fy; c2 = x; den = z; break;
+    }
+#else
     const double fxx = fx * x, fyy = fy * y;
     double c1 = fy;
     c1 = lane == 0 ? x : c1;
@@ -361,6 +378,7 @@ __device__ inline void point_quotients(const Intrinsics& K, const double* pose, 
     c2 = (lane == 4 || lane == 10) ? xy : c2;
     c2 = (lane == 6 || lane == 8 || lane == 9) ? y : c2;
     const double den = (lane <= 2 || lane == 6 || lane == 7 || lane >= 11) ? z : zz;
+#endif
     double q = (c1 * c2) / den;
     if (lane == 5) q = fx + q;
     if (lane == 9) q = -fy - q;

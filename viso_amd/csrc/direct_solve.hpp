@@ -141,8 +141,10 @@ __device__ __attribute__((always_inline)) inline void solve_after_lu(SolveLds& L
                                                                       unsigned long long* stamps);
 
 // One GN step of one level on wave 0 (all 64 lanes): L.S -> update, the new
-// L.state and the loop decision L.cont (src/viso.cpp:731-753).
-__device__ __attribute__((always_inline)) inline void solve_wave0(SolveLds& L, int iter, double* stats,
+// L.state and the loop decision L.cont (src/viso.cpp:731-753), with the LU
+// replicated in every lane's registers (the
+// product's solve: solve_wave0 below).
+__device__ __attribute__((always_inline)) inline void solve_wave0_rep(SolveLds& L, int iter, double* stats,
                                    unsigned long long* stamps = nullptr) {
     const int lane = threadIdx.x & 63;
     const int row = lane / 6, col = lane - 6 * (lane / 6);
@@ -258,6 +260,80 @@ __device__ __attribute__((always_inline)) inline void solve_after_lu(SolveLds& L
     solve_finish(L, update, h, iter, stats, stamps);
 }
 
+
+// Lane-per-element PartialPivLU : lane 6 r + c < 36 holds
+// A[r][c]; per step the pivot column is read by readlane (uniform, first
+// maximal |pivot| wins as in Eigen), the row swap and the rank-1 update's
+// operands move by ds_bpermute, the division and update are one element per
+// lane with the replicated form's operations.  The factors then go through
+// LDS into every lane's registers for solve_after_lu (same inverse / update /
+// finish): the result bits equal solve_wave0_rep's (solve_bench checks the
+// hash).  Per step one division and one update per lane instead of up to
+// five divisions and 25 updates in every lane: 2.84 against 3.13 us per solve
+// alone (profiles/r05_solve_bench.log), but 0.1 us per level SLOWER inside
+// direct_level_kernel, where the other waves' prefetch shares the LDS pipe
+// with its ds_bpermute hops (profiles/r05_solve_ab.log): not the product's
+// (build with -DVISO_SOLVE_LANE to use it).
+__device__ inline double bperm_f64(double v, int src) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_ds_bpermute(src * 4, (int)(b & 0xffffffffLL));
+    const int hi = __builtin_amdgcn_ds_bpermute(src * 4, (int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+__device__ __attribute__((always_inline)) inline void solve_wave0_lane(SolveLds& L, int iter, double* stats,
+                                                                        unsigned long long* stamps = nullptr) {
+    const int lane = threadIdx.x & 63;
+    const int r = lane / 6, c = lane - 6 * (lane / 6);
+    const bool in = lane < 36;
+    const int r0 = r < c ? r : c, c0 = r < c ? c : r;
+    const double h = in ? L.S[r0 * 6 - (r0 * (r0 - 1)) / 2 + (c0 - r0)] : 0.0;
+    double a = h;
+    int tr[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        int p = k;
+        double best = fabs(readlane_f64(a, 7 * k));
+#pragma unroll
+        for (int i = k + 1; i < 6; ++i) {
+            const double s = fabs(readlane_f64(a, 6 * i + k));
+            if (s > best) {
+                best = s;
+                p = i;
+            }
+        }
+        p = __builtin_amdgcn_readfirstlane(p);
+        tr[k] = p;
+        if (__builtin_amdgcn_readfirstlane(best != 0.0 ? 1 : 0)) {
+            if (p != k) a = bperm_f64(a, r == k ? 6 * p + c : (r == p ? 6 * k + c : lane));
+            const double piv = readlane_f64(a, 7 * k);
+            if (in && r > k && c == k) a = a / piv;
+        }
+        if (k < 5) {
+            const double lk = bperm_f64(a, 6 * r + k), kc = bperm_f64(a, 6 * k + c);
+            if (in && r > k && c > k) a = a - lk * kc;
+        }
+    }
+    double* T = &L.red[0][0];
+    if (in) T[lane] = a;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    double A[36];
+#pragma unroll
+    for (int i = 0; i < 36; ++i) A[i] = T[i];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    SPROBE(0);
+    solve_after_lu(L, A, tr, h, iter, stats, stamps);
+}
+
+
+__device__ __attribute__((always_inline)) inline void solve_wave0(SolveLds& L, int iter, double* stats,
+                                                                   unsigned long long* stamps = nullptr) {
+#ifdef VISO_SOLVE_LANE
+    solve_wave0_lane(L, iter, stats, stamps);
+#else
+    solve_wave0_rep(L, iter, stats, stamps);
+#endif
+}
 
 // Tolerance mode (VISO_PRECISION_FAST): update = H^-1 b by an LDL^T
 // factorisation of the (symmetric positive semi-definite) H and two

@@ -156,10 +156,10 @@ int viso_ctx::init() {
     // rather than in the first tracking chunk (a hipMalloc, the kernel's
     // dynamic-LDS attribute and code-object load would otherwise land in that
     // chunk: ~0.1 ms)
-    rc = bg_prepare();
-    if (rc) return rc;
     VISO_HIP_CHECK(hipEventCreateWithFlags(&geo_fork, hipEventDisableTiming));
     VISO_HIP_CHECK(hipEventCreateWithFlags(&geo_join, hipEventDisableTiming));
+    rc = bg_prepare();
+    if (rc) return rc;
     // the pose getter's pinned staging (viso_get_poses)
     h_poses_cap = (size_t)std::min(std::max(p.max_poses, 1), 4096);
     VISO_HIP_CHECK(hipHostMalloc((void**)&h_poses, 96 * h_poses_cap));
@@ -427,6 +427,14 @@ int viso_ctx::bg_prepare() {
     if (rc) return rc;
     VISO_HIP_CHECK(hipMemsetAsync(bg_buf.ptr, 0, sizeof(int) * (kBgWords + 32), stream));
     warm_lk_bg(stream);
+    // lk_stream's first dispatch (its hardware queue is brought up then) and
+    // a cross-stream event hand-off, here rather than in the first chunk's
+    // background launch
+    VISO_HIP_CHECK(hipEventRecord(geo_fork, stream));
+    VISO_HIP_CHECK(hipStreamWaitEvent(lk_stream, geo_fork, 0));
+    warm_lk_bg(lk_stream);
+    VISO_HIP_CHECK(hipEventRecord(geo_join, lk_stream));
+    VISO_HIP_CHECK(hipStreamWaitEvent(stream, geo_join, 0));
     VISO_HIP_CHECK(hipGetLastError());
     return VISO_OK;
 }
@@ -459,18 +467,25 @@ int viso_ctx::bg_begin(const std::vector<int>& chunk) {
     }
     // flags, heads and leftovers cleared behind the chunk's pyramid; the grid
     // (on the side stream's own hardware queue, create_streams) starts behind
-    // them
+    // them.  The grid itself is launched once the chunk's first frame is
+    // enqueued (bg_launch): its host-side cost (the cross-stream wait, the
+    // launch on the masked queue, ~30 us) then overlaps that frame's chain
+    // instead of holding the chain's first launch back.
     VISO_HIP_CHECK(hipMemsetAsync(bg_buf.ptr, 0, sizeof(int) * bg_words, stream));
+    VISO_HIP_CHECK(hipEventRecord(bg_done, stream));
     bg_args = a;
     bg_active = true;
     bg_unchecked = true;
+    bg_launched = false;
     bg_nb = nb;
     bg_slots.clear();
-    return bg_launch();
+    return VISO_OK;
 }
 
+// (bg_done holds the memset of bg_begin until the grid's own record below)
 int viso_ctx::bg_launch() {
-    VISO_HIP_CHECK(hipEventRecord(bg_done, stream));
+    if (!bg_active || bg_launched) return VISO_OK;
+    bg_launched = true;
     VISO_HIP_CHECK(hipStreamWaitEvent(lk_stream, bg_done, 0));
     {
         TimedRegion t(timing, VISO_KERNEL_LKALIGN, lk_stream);
@@ -501,6 +516,13 @@ int viso_ctx::bg_check() {
 // outputs, the held frames), which is the latest LK batch of the flush_lk
 // bookkeeping.
 int viso_ctx::bg_end(bool drain) {
+    // a chunk whose first frame ended in an error before bg_launch (drain =
+    // false) has no grid: bg_done still marks the memset, so the waits below
+    // hold nothing back
+    if (drain) {
+        const int rc = bg_launch();
+        if (rc) return rc;
+    }
     // (drain = false: the error path of finish_call; the chunk's last pose was
     // not launched, so no drain runs: the resident grid's waves give their
     // items back and leave, and the context stream only waits for them)
@@ -730,7 +752,10 @@ int viso_ctx::on_new_frame(int cur) {
                 if (h_ctl->gate) {
                     {
                         TimedRegion t(timing, VISO_KERNEL_RANSAC, stream);
-                        launch_pose_2d2d_body(geo, stream, lk_stream, geo_fork, geo_join);
+                        // the H chain on lk_stream beside the E chain (dev: VISO_GEO_SPLIT=0 keeps
+                        // both on the context stream)
+                        static const bool split = !(getenv("VISO_GEO_SPLIT") && getenv("VISO_GEO_SPLIT")[0] == '0');
+                        launch_pose_2d2d_body(geo, stream, split ? lk_stream : nullptr, geo_fork, geo_join);
                     }
                     VISO_HIP_CHECK(hipGetLastError());
                     VISO_HIP_CHECK(hipMemcpyAsync(h_ctl, geo.ctl, sizeof(GeoCtl), hipMemcpyDeviceToHost, stream));
@@ -981,6 +1006,9 @@ int viso_process_frames_device(viso_ctx* c, const uint8_t* d_left, const uint8_t
             launch_pyramid_frames(c->geom, l0.data(), dst.data(), (int)l0.size(), c->stream);
         }
         VISO_HIP_CHECK(hipGetLastError());
+        // (the background words' memset stays behind the pyramid: issued
+        // ahead of it, the chain ran at half speed in 3 of 6 bench runs,
+        // profiles/r05_bg_order_ab.log)
         {
             const int rc = c->bg_begin(sl);
             if (rc) {
@@ -1012,6 +1040,10 @@ int viso_process_frames_device(viso_ctx* c, const uint8_t* d_left, const uint8_t
             const int rc = c->on_new_frame(sl[(size_t)i]);
             c->right_l0 = nullptr;
             if (rc) return end_chunk(rc);
+            if (i == 0) {
+                const int r2 = c->bg_launch();
+                if (r2) return end_chunk(r2);
+            }
         }
         // the last frame's final solve, then the chunk's LKAlignment batch
         // behind the chunk (the GPU is free then; beside the next chunk it

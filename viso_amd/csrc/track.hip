@@ -225,7 +225,9 @@ __device__ inline double sample_win_cached(const uint8_t* __restrict__ img, int 
     if (!win.lds) return sample_px(img, w, h, x, y);  // wave-uniform (window_issue)
     const bool finite = FINITE || (x > -1e9 && x < 1e9 && y > -1e9 && y < 1e9);
     const int ix = finite ? (int)x : 0, iy = finite ? (int)y : 0;
+#ifndef VISO_LK_NOTAPCACHE
     if (__builtin_amdgcn_ballot_w64(finite && ix == tc.ix && iy == tc.iy) == ~0ull) return bilerp_packed(x, y, tc.t);
+#endif
     const bool in = finite && (unsigned)(ix - win.x0) < (unsigned)(kWinW - 1) &&
                     (unsigned)(iy - win.y0) < (unsigned)(kWinH - 1);
     if (__builtin_expect(__builtin_amdgcn_ballot_w64(in) == ~0ull, 1) ||
@@ -319,7 +321,13 @@ __device__ inline LkResult lk_iterate(const LkTemplate& t, int w1, int h1,
             succ = false;
             break;
         }
-        const double e = t.I1 - sample_win_cached<!KLT_BOUNDS>(img2, w2, h2, cur_x + dx, cur_y + dy, win, tc);
+        // (KLT: ten iterations at most, its window path as it was)
+        double smp;
+        if constexpr (KLT_BOUNDS)
+            smp = sample_win_follow<false>(img2, w2, h2, cur_x + dx, cur_y + dy, win);
+        else
+            smp = sample_win_cached<true>(img2, w2, h2, cur_x + dx, cur_y + dy, win, tc);
+        const double e = t.I1 - smp;
         double B0, B1;
         if (KLT_BOUNDS)
             wave_tree_sum3(-t.J0 * e, -t.J1 * e, e * e, B0, B1, cost);
@@ -407,7 +415,7 @@ __device__ inline LkResult lk_iterate_fast(float I1, float J0, float J1, const f
     return {dx, dy, succ, iter};
 }
 
-__device__ __attribute__((always_inline)) inline void klt_track_body(FrameDev ref, FrameDev cur, PyrDev g,
+__device__ __attribute__((always_inline)) inline void klt_track_body(const FrameDev& ref, const FrameDev& cur, const PyrDev& g,
                                                                      const float2* __restrict__ kp1,
                                                                      float2* __restrict__ kp2,
                                                                      uint8_t* __restrict__ success, int i,
@@ -449,18 +457,20 @@ __device__ __attribute__((always_inline)) inline void klt_track_body(FrameDev re
 }
 
 // n_dev (optional): the track count in device memory (after a re-detection
-// frame, whose FAST count the host has not read), capped at n; the waves then
-// stride over the tracks (grid waves apart)
+// frame, whose FAST count the host has not read), capped at n; the grid then
+// covers n and waves past the count return at once.  (A grid-stride loop over
+// the tracks measured 40 % slower: the loop moved the window state into 16 KB
+// of promoted LDS and 110 VGPRs.)
 __global__ __launch_bounds__(256) void klt_kernel(FrameDev ref, FrameDev cur, PyrDev g,
                                                   const float2* __restrict__ kp1,
                                                   float2* __restrict__ kp2,
                                                   uint8_t* __restrict__ success, int n,
                                                   double thresh, const int* __restrict__ n_dev) {
     __shared__ uint8_t s_win[4][kWinW * kWinH];
+    const int i = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     if (n_dev) n = min(__builtin_amdgcn_readfirstlane(*n_dev), n);
-    const int stride = __builtin_amdgcn_readfirstlane(gridDim.x * 4);
-    for (int i = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); i < n; i += stride)
-        klt_track_body(ref, cur, g, kp1, kp2, success, i, thresh, s_win[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)]);
+    if (i >= n) return;  // wave-uniform
+    klt_track_body(ref, cur, g, kp1, kp2, success, i, thresh, s_win[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)]);
 }
 
 
