@@ -750,16 +750,17 @@ int viso_ctx::on_new_frame(int cur) {
                 VISO_HIP_CHECK(hipMemcpyAsync(h_ctl, geo.ctl, sizeof(GeoCtl), hipMemcpyDeviceToHost, stream));
                 VISO_HIP_CHECK(hipStreamSynchronize(stream));
                 if (h_ctl->gate) {
+                    hipStream_t bs = stream;
                     {
                         TimedRegion t(timing, VISO_KERNEL_RANSAC, stream);
-                        // the H chain on lk_stream beside the E chain (dev: VISO_GEO_SPLIT=0 keeps
-                        // both on the context stream)
-                        static const bool split = !(getenv("VISO_GEO_SPLIT") && getenv("VISO_GEO_SPLIT")[0] == '0');
-                        launch_pose_2d2d_body(geo, stream, split ? lk_stream : nullptr, geo_fork, geo_join);
+                        // the H chain and SelectMotion on lk_stream beside the E chain (the
+                        // gate's read above left both streams idle); the result is read
+                        // on the stream SelectMotion ran on
+                        bs = launch_pose_2d2d_body(geo, stream, lk_stream, geo_fork, geo_join);
                     }
                     VISO_HIP_CHECK(hipGetLastError());
-                    VISO_HIP_CHECK(hipMemcpyAsync(h_ctl, geo.ctl, sizeof(GeoCtl), hipMemcpyDeviceToHost, stream));
-                    VISO_HIP_CHECK(hipStreamSynchronize(stream));
+                    VISO_HIP_CHECK(hipMemcpyAsync(h_ctl, geo.ctl, sizeof(GeoCtl), hipMemcpyDeviceToHost, bs));
+                    VISO_HIP_CHECK(hipStreamSynchronize(bs));
                 }
                 const GeoCtl& c = *h_ctl;
                 n_track = c.n;
@@ -1226,7 +1227,8 @@ int viso_pose_2d2d(viso_ctx* c, const double* p1, const double* p2, int32_t n, d
         std::memcpy(T, g.T, sizeof(g.T));
     }
     if (candidates)
-        for (int m = 0; m < g.n_cand; ++m) std::memcpy(candidates + 12 * m, g.cand[m], 96);
+        for (int m = 0; m < g.n_cand; ++m)  // the E path's slot 0, the H path's from slot 1
+            std::memcpy(candidates + 12 * m, g.cand[m < g.e_ncand ? 0 : 1 + (m - g.e_ncand)], 96);
     if (n > 0 && (inliers || points3d)) {
         std::vector<uint8_t> in((size_t)n);
         VISO_HIP_CHECK(hipMemcpy(in.data(), a.inliers, (size_t)n, hipMemcpyDeviceToHost));

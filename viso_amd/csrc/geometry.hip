@@ -736,15 +736,14 @@ __device__ inline void wave_lds_sync() {
 
 // The eigenvector of the smallest eigenvalue of the symmetric 9 x 9 moment
 // matrix (the least-squares DLT refinement of the winning homography) by a
-// round-robin (parallel-ordered) cyclic Jacobi on one wave: per round the
-// four disjoint rotations are computed by lanes 0-4 from the round's A, then
-// lane per (pair, index) rotates the column pairs of A and V, then the row
-// pairs of A.  Restated step for step by oracle_linalg.hpp jacobi_eigen_rr
+// round-robin (parallel-ordered) cyclic Jacobi on one wave: per round each
+// (pair, index) lane forms its pair's rotation from the round's A, rotates
+// the column pairs of A and V, then the row pairs of A (two LDS hand-offs per
+// round; round 4 formed the rotations in lanes 0-4 and passed them on: three).  Restated step for step by oracle_linalg.hpp jacobi_eigen_rr
 // (sweep test, stop rule, descending selection sort).  All lanes return it.
 __device__ void smallest_eigvec9_rr(const double* __restrict__ Min, double* out) {
     constexpr int N = 9, M = 10, R = 9, P = 5;
-    __shared__ double sA[81], sV[81], sc[P], ss[P];
-    __shared__ int sact[P];
+    __shared__ double sA[81], sV[81];
     const int lane = threadIdx.x & 63;
     for (int k = lane; k < 81; k += 64) {
         sA[k] = Min[k];
@@ -762,56 +761,48 @@ __device__ void smallest_eigvec9_rr(const double* __restrict__ Min, double* out)
         diag = uniform_f64(diag);
         if (off <= 1e-30 * diag || off == 0.0) break;
         for (int r = 0; r < R; ++r) {
-            if (lane < P) {
-                // circle method: arr[0] = 0, arr[j] = 1 + (j - 1 + r) mod 9; pair i = (arr[i], arr[9 - i])
-                const int a0 = lane == 0 ? 0 : 1 + (lane - 1 + r) % (M - 1);
-                const int b0 = 1 + (M - 1 - lane - 1 + r) % (M - 1);
-                const int p = a0 < b0 ? a0 : b0, q = a0 < b0 ? b0 : a0;
-                const bool act = q < N && sA[N * p + q] != 0.0;
-                double cc = 0.0, sn = 0.0;
+            // lane (i, k) < 45: pair i's rotation, formed in the lane itself
+            // from the round's A (the same operations in all nine lanes of
+            // the pair: no hand-off through LDS), then its rotation of the
+            // column pairs (p, q) of A and of V at row k, then of A's row
+            // pairs at column k; (p, q) from the circle method: arr[0] = 0,
+            // arr[j] = 1 + (j - 1 + r) mod 9, pair i = (arr[i], arr[9 - i])
+            const int i = lane / N, k = lane - N * (lane / N);
+            const bool own = lane < P * N;
+            const int a0 = i == 0 ? 0 : 1 + (i - 1 + r) % (M - 1);
+            const int b0 = 1 + (M - 1 - i - 1 + r) % (M - 1);
+            const int p = a0 < b0 ? a0 : b0, q0 = a0 < b0 ? b0 : a0;
+            const int q = q0 < N ? q0 : p;  // the idle pair (q0 = 9) loads in bounds, stores nothing
+            double c = 0.0, sn = 0.0;
+            bool act = false;
+            if (own) {
+                const double apq = sA[N * p + q];
+                act = q0 < N && apq != 0.0;
                 if (act) {
-                    const double apq = sA[N * p + q];
                     const double theta = (sA[N * q + q] - sA[N * p + p]) / (2.0 * apq);
                     const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-                    cc = 1.0 / sqrt(t * t + 1.0);
-                    sn = t * cc;
+                    c = 1.0 / sqrt(t * t + 1.0);
+                    sn = t * c;
                 }
-                sact[lane] = act ? 1 : 0;
-                sc[lane] = cc;
-                ss[lane] = sn;
             }
+            double akp = 0, akq = 0, vkp = 0, vkq = 0;
+            if (own) {
+                akp = sA[N * k + p];
+                akq = sA[N * k + q];
+                vkp = sV[N * k + p];
+                vkq = sV[N * k + q];
+            }
+            // every lane of the wave has read the round's A before any lane writes
             wave_lds_sync();
-            // lane (i, k) < 45: pair i's rotation of column pairs (p, q) of A
-            // and of V at row k, then of A's row pairs at column k; (p, q)
-            // from the circle method in registers, so a lane's loads need
-            // one LDS round trip (rotation + operands together)
-            if (lane < P * N) {
-                const int i = lane / N, k = lane - N * (lane / N);
-                const int a0 = i == 0 ? 0 : 1 + (i - 1 + r) % (M - 1);
-                const int b0 = 1 + (M - 1 - i - 1 + r) % (M - 1);
-                const int p = a0 < b0 ? a0 : b0, q0 = a0 < b0 ? b0 : a0;
-                const int q = q0 < N ? q0 : p;  // the idle pair (q0 = 9) loads in bounds, stores nothing
-                const bool act = sact[i] != 0;
-                const double c = sc[i], sn = ss[i];
-                const double akp = sA[N * k + p], akq = sA[N * k + q];
-                const double vkp = sV[N * k + p], vkq = sV[N * k + q];
-                if (act) {
-                    sA[N * k + p] = c * akp - sn * akq;
-                    sA[N * k + q] = sn * akp + c * akq;
-                    sV[N * k + p] = c * vkp - sn * vkq;
-                    sV[N * k + q] = sn * vkp + c * vkq;
-                }
+            if (own && act) {
+                sA[N * k + p] = c * akp - sn * akq;
+                sA[N * k + q] = sn * akp + c * akq;
+                sV[N * k + p] = c * vkp - sn * vkq;
+                sV[N * k + q] = sn * vkp + c * vkq;
             }
             wave_lds_sync();
             // row pairs of A
-            if (lane < P * N) {
-                const int i = lane / N, k = lane - N * (lane / N);
-                const int a0 = i == 0 ? 0 : 1 + (i - 1 + r) % (M - 1);
-                const int b0 = 1 + (M - 1 - i - 1 + r) % (M - 1);
-                const int p = a0 < b0 ? a0 : b0, q0 = a0 < b0 ? b0 : a0;
-                const int q = q0 < N ? q0 : p;
-                const bool act = sact[i] != 0;
-                const double c = sc[i], sn = ss[i];
+            if (own) {
                 const double apk = sA[N * p + k], aqk = sA[N * q + k];
                 if (act) {
                     sA[N * p + k] = c * apk - sn * aqk;
@@ -1005,33 +996,49 @@ __global__ __launch_bounds__(256) void select_points_kernel(GeoArgs a) {
     pts[3 * i + 2] = P1[2];
 }
 
-__global__ __launch_bounds__(256) void select_reduce_kernel(GeoArgs a) {
+// SelectMotion's reduction and output in one single-workgroup launch
+// (src/viso.cpp:596-638): the candidates' inlier counts in one pass over the
+// flags (integers: any order), the first maximum, the mean depth of the
+// best candidate's points (block_tree_sum, the oracle's tree), then the
+// normalised inlier points in index order: thread t owns the contiguous
+// flags [t per, (t + 1) per), so one exclusive scan of the per-thread counts
+// places every point (round 4: one launch per step and three block barriers
+// per 256 flags, 31 us for ~2,000 tracks).
+__global__ __launch_bounds__(256) void select_finish_kernel(GeoArgs a) {
     __shared__ double s_red[4];
-    __shared__ int s_cnt[4];
+    __shared__ int s_cnt[4][kMaxCandidates];
+    __shared__ int s_wave[4];
     __shared__ int s_best, s_bestn;
     GeoCtl* c = a.ctl;
     if (!c->gate) return;
     const int n = c->n, m = c->e_ncand + c->h_ncand;
-    if (threadIdx.x == 0) {
-        s_best = -1;
-        s_bestn = 0;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    int cnt[kMaxCandidates];
+#pragma unroll
+    for (int k = 0; k < kMaxCandidates; ++k) cnt[k] = 0;
+    for (int i = t; i < n; i += 256)
+#pragma unroll
+        for (int k = 0; k < kMaxCandidates; ++k)
+            if (k < m) cnt[k] += a.sel_in[(size_t)k * a.cap + i];
+#pragma unroll
+    for (int k = 0; k < kMaxCandidates; ++k) {
+        const int w = wave_sum_int(cnt[k]);
+        if (lane == 0) s_cnt[wave][k] = w;
     }
     __syncthreads();
-    for (int mi = 0; mi < m; ++mi) {
-        int cnt = 0;
-        for (int i = threadIdx.x; i < n; i += 256) cnt += a.sel_in[(size_t)mi * a.cap + i];
-        cnt = wave_sum_int(cnt);
-        if ((threadIdx.x & 63) == 0) s_cnt[threadIdx.x >> 6] = cnt;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const int tot = (s_cnt[0] + s_cnt[1]) + (s_cnt[2] + s_cnt[3]);
-            if (tot > s_bestn) {  // strict: the first maximum wins (src/viso.cpp:605)
-                s_bestn = tot;
-                s_best = mi;
+    if (t == 0) {
+        int best = -1, bestn = 0;
+        for (int k = 0; k < m; ++k) {
+            const int tot = (s_cnt[0][k] + s_cnt[1][k]) + (s_cnt[2][k] + s_cnt[3][k]);
+            if (tot > bestn) {  // strict: the first maximum wins (src/viso.cpp:605)
+                bestn = tot;
+                best = k;
             }
         }
-        __syncthreads();
+        s_best = best;
+        s_bestn = bestn;
     }
+    __syncthreads();
     const int best = s_best, nr = s_bestn;
     double mean = 0.0;
     if (best >= 0) {
@@ -1039,7 +1046,10 @@ __global__ __launch_bounds__(256) void select_reduce_kernel(GeoArgs a) {
         const double* pts = a.sel_pts + (size_t)best * a.cap * 3;
         mean = block_tree_sum(n, [&](int i) { return inl[i] ? pts[3 * i + 2] : 0.0; }, s_red);
     }
-    if (threadIdx.x == 0) {
+    // every thread derives the ctl values it needs from the same operations
+    const bool nonzero = mean != 0;
+    const double md = nonzero ? mean / nr : mean;
+    if (t == 0) {
         c->n_cand = m;
         c->nr_inliers = nr;
         c->best_motion = best;
@@ -1047,42 +1057,36 @@ __global__ __launch_bounds__(256) void select_reduce_kernel(GeoArgs a) {
             for (int k = 0; k < 9; ++k) c->R[k] = c->cand[cand_slot(c, best)][k];
             for (int k = 0; k < 3; ++k) c->T[k] = c->cand[cand_slot(c, best)][9 + k];
         }
-        c->mean_depth = mean;
-        c->mean_nonzero = mean != 0 ? 1 : 0;
-        if (mean != 0) {
-            c->mean_depth = mean / nr;
-            for (int k = 0; k < 3; ++k) c->T[k] = c->T[k] / c->mean_depth;
-        }
+        c->mean_depth = md;
+        c->mean_nonzero = nonzero ? 1 : 0;
+        if (nonzero)
+            for (int k = 0; k < 3; ++k) c->T[k] = c->T[k] / md;
     }
-}
-
-// normalised inlier points in order (the reference's points3d after
-// SelectMotion's depth normalisation) -> map points; inlier flags -> mask
-__global__ __launch_bounds__(256) void select_output_kernel(GeoArgs a) {
-    __shared__ int s_wave[4];
-    __shared__ int s_base;
-    const GeoCtl* c = a.ctl;
-    if (!c->gate) return;
-    const int best = c->best_motion, n = c->n;
-    if (threadIdx.x == 0) s_base = 0;
+    // output: flags, and the inlier points in order
+    const int per = (n + 255) / 256;
+    const int i0 = min(t * per, n), i1 = min(i0 + per, n);
+    const uint8_t* inl = a.sel_in + (size_t)(best >= 0 ? best : 0) * a.cap;
+    int own = 0;
+    for (int i = i0; i < i1; ++i) own += (best >= 0 && inl[i]) ? 1 : 0;
+    // exclusive scan of `own` over the block
+    int incl = own;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+    }
+    if (lane == 63) s_wave[wave] = incl;
     __syncthreads();
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (int i0 = 0; i0 < n; i0 += 256) {
-        const int i = i0 + threadIdx.x;
-        bool in = false;
-        if (i < n && best >= 0) in = a.sel_in[(size_t)best * a.cap + i] != 0;
-        if (i < n) a.inliers[i] = in ? 1 : 0;
-        const unsigned long long msk = __ballot(in);
-        const int before = __popcll(msk & ((1ULL << lane) - 1ULL));
-        if (lane == 0) s_wave[wave] = __popcll(msk);
-        __syncthreads();
-        int off = s_base;
-        for (int k = 0; k < wave; ++k) off += s_wave[k];
+    int off = incl - own;
+    for (int k = 0; k < wave; ++k) off += s_wave[k];
+    const double* pts = a.sel_pts + (size_t)(best >= 0 ? best : 0) * a.cap * 3;
+    for (int i = i0; i < i1; ++i) {
+        const bool in = best >= 0 && inl[i] != 0;
+        a.inliers[i] = in ? 1 : 0;
         if (in) {
-            const double* P = a.sel_pts + ((size_t)best * a.cap + i) * 3;
-            const double md = c->mean_depth;
-            double* o = a.points_out + 3 * (size_t)(off + before);
-            if (c->mean_nonzero) {
+            const double* P = pts + 3 * (size_t)i;
+            double* o = a.points_out + 3 * (size_t)off;
+            if (nonzero) {
                 o[0] = P[0] / md;
                 o[1] = P[1] / md;
                 o[2] = P[2] / md;
@@ -1091,10 +1095,8 @@ __global__ __launch_bounds__(256) void select_output_kernel(GeoArgs a) {
                 o[1] = P[1];
                 o[2] = P[2];
             }
+            ++off;
         }
-        __syncthreads();
-        if (threadIdx.x == 0) s_base += (s_wave[0] + s_wave[1]) + (s_wave[2] + s_wave[3]);
-        __syncthreads();
     }
 }
 
@@ -1104,40 +1106,46 @@ void launch_pose_2d2d_gate(const GeoArgs& a, hipStream_t stream) {
     normalize_kernel<<<1, kNormThreads, 0, stream>>>(a);
 }
 
-void launch_pose_2d2d_body(const GeoArgs& a, hipStream_t stream, hipStream_t hs, hipEvent_t fork,
-                           hipEvent_t join) {
-    // the H path on hs (when given), concurrent with the E path on stream
-    const bool split = hs && fork && join && a.h_iters > 0;
-    hipStream_t sh = stream;
+hipStream_t launch_pose_2d2d_body(const GeoArgs& a, hipStream_t stream, hipStream_t hs, hipEvent_t e_done,
+                                  hipEvent_t join) {
+    const bool split = hs && e_done && join && a.h_iters > 0 && a.e_iters > 0;
+    const hipStream_t sh = split ? hs : stream;
+    // the H chain (the longer one) and the E chain, interleaved launch by
+    // launch so that neither waits for the other's host-side enqueue
+    for (int step = 0; step < 6; ++step) {
+        if (a.h_iters > 0) {
+            switch (step) {
+                case 0: h_hyp_kernel<<<(a.h_iters + 3) / 4, 256, 0, sh>>>(a); break;
+                case 1: score_kernel<false><<<a.h_iters, 256, 0, sh>>>(a); break;
+                case 2: scan_kernel<false><<<1, 256, 0, sh>>>(a); break;
+                case 3: h_moment_leaves_kernel<<<(a.cap + 255) / 256, 256, 0, sh>>>(a); break;
+                case 4: h_moment_sums_kernel<<<45, 256, 0, sh>>>(a); break;
+                default: h_refine_decompose_kernel<<<1, 64, 0, sh>>>(a); break;
+            }
+        }
+        if (a.e_iters > 0) {
+            switch (step) {
+                case 0: e_hyp_kernel<<<(a.e_iters + 3) / 4, 256, 0, stream>>>(a); break;
+                case 1: score_kernel<true><<<a.e_iters, 256, 0, stream>>>(a); break;
+                case 2: scan_kernel<true><<<1, 256, 0, stream>>>(a); break;
+                case 3: recover_setup_kernel<<<1, 64, 0, stream>>>(a); break;
+                case 4: recover_count_kernel<<<(4 * a.cap + 255) / 256, 256, 0, stream>>>(a); break;
+                default: recover_pick_kernel<<<1, 64, 0, stream>>>(a); break;
+            }
+        }
+    }
     if (split) {
-        (void)hipEventRecord(fork, stream);
-        (void)hipStreamWaitEvent(hs, fork, 0);
-        sh = hs;
-    }
-    if (a.h_iters > 0) {
-        h_hyp_kernel<<<(a.h_iters + 3) / 4, 256, 0, sh>>>(a);
-        score_kernel<false><<<a.h_iters, 256, 0, sh>>>(a);
-        scan_kernel<false><<<1, 256, 0, sh>>>(a);
-        h_moment_leaves_kernel<<<(a.cap + 255) / 256, 256, 0, sh>>>(a);
-        h_moment_sums_kernel<<<45, 256, 0, sh>>>(a);
-        h_refine_decompose_kernel<<<1, 64, 0, sh>>>(a);
-    }
-    if (a.e_iters > 0) {
-        e_hyp_kernel<<<(a.e_iters + 3) / 4, 256, 0, stream>>>(a);
-        score_kernel<true><<<a.e_iters, 256, 0, stream>>>(a);
-        scan_kernel<true><<<1, 256, 0, stream>>>(a);
-        recover_setup_kernel<<<1, 64, 0, stream>>>(a);
-        recover_count_kernel<<<(4 * a.cap + 255) / 256, 256, 0, stream>>>(a);
-        recover_pick_kernel<<<1, 64, 0, stream>>>(a);
-    }
-    if (split) {
-        (void)hipEventRecord(join, hs);
-        (void)hipStreamWaitEvent(stream, join, 0);
+        (void)hipEventRecord(e_done, stream);
+        (void)hipStreamWaitEvent(sh, e_done, 0);
     }
     const int total = 5 * a.cap;
-    select_points_kernel<<<(total + 255) / 256, 256, 0, stream>>>(a);
-    select_reduce_kernel<<<1, 256, 0, stream>>>(a);
-    select_output_kernel<<<1, 256, 0, stream>>>(a);
+    select_points_kernel<<<(total + 255) / 256, 256, 0, sh>>>(a);
+    select_finish_kernel<<<1, 256, 0, sh>>>(a);
+    if (split) {
+        (void)hipEventRecord(join, sh);
+        (void)hipStreamWaitEvent(stream, join, 0);
+    }
+    return sh;
 }
 
 void launch_pose_2d2d(const GeoArgs& a, hipStream_t stream, Timing* timing) {

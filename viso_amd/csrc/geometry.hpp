@@ -83,10 +83,13 @@ void launch_pose_2d2d(const GeoArgs& a, hipStream_t stream, Timing* timing);
 // returns at once when the gate is closed; a caller that has read the gate
 // on the host may skip the body.
 void launch_pose_2d2d_gate(const GeoArgs& a, hipStream_t stream);
-// hs (optional): a second stream for the H path, forked from / joined to
-// `stream` by the events fork / join (the E and H RANSAC chains are
-// independent until SelectMotion)
-void launch_pose_2d2d_body(const GeoArgs& a, hipStream_t stream, hipStream_t hs = nullptr,
-                           hipEvent_t fork = nullptr, hipEvent_t join = nullptr);
+// hs (optional): a second stream for the H path.  The caller has
+// synchronised `stream` behind the gate (both streams see its results); the
+// E and H chains are enqueued interleaved, SelectMotion runs on hs behind
+// the H chain once the E chain's event `e_done` is passed, and `join` (on
+// hs, behind SelectMotion) is waited for by `stream`.  Returns the stream
+// SelectMotion ran on (read the result there).
+hipStream_t launch_pose_2d2d_body(const GeoArgs& a, hipStream_t stream, hipStream_t hs = nullptr,
+                                  hipEvent_t e_done = nullptr, hipEvent_t join = nullptr);
 
 }  // namespace viso
