@@ -332,7 +332,7 @@ __device__ inline double sample_cw(const uint8_t* __restrict__ img, int w, int h
 //   0: x / z, 1: y / z (the projection)        -> Q[0], Q[1]
 //   2..11: J[0], J[2], J[3], J[4], J[5], J[7], J[8], J[9], J[10], J[11]
 __device__ inline void point_quotients(const Intrinsics& K, const double* pose, const double* P, double scale,
-                                       double* Q) {
+                                       double* Q, double* qt) {
     const int lane = threadIdx.x & 63;
     double Pc[3];
     mat3_vec(pose, P, Pc);
@@ -345,40 +345,51 @@ __device__ inline void point_quotients(const Intrinsics& K, const double* pose, 
     //    3: -fx * x / zz (J[2])  4: -fx * xy / zz (J[3]) 5: fx*x * x / zz (J[4])
     //    6: -fx * y / z  (J[5])  7: fy / z   (J[7])      8: -fy * y / zz (J[8])
     //    9: fy*y * y / zz (J[9]) 10: fy * xy / zz (J[10]) 11: fy * x / z (J[11])
-    // formed by lane-mask selects (v_cndmask), not a switch on the lane (a
-    // divergent switch runs every case's code under its own EXEC mask)
-#ifdef VISO_QUOT_SWITCH  // dev A/B: the round-4 switch form
-    double c1, c2 = 1.0, den = zz;
-    switch (lane < 12 ? lane : 0) {
-        case 0: c1 = x; den = z; break;
-        case 1: c1 = y; den = z; break;
-        case 2: c1 = fx; den = z; break;
-        case 3: c1 = -fx; c2 = x; break;
-        case 4: c1 = -fx; c2 = xy; break;
-        case 5: c1 = fx * x; c2 = x; break;
-        case 6: c1 = -fx; c2 = y; den = z; break;
-        case 7: c1 = fy; den = z; break;
-        case 8: c1 = -fy; c2 = y; break;
-        case 9: c1 = fy * y; c2 = y; break;
-        case 10: c1 = fy; c2 = xy; break;
-        default: c1 = fy; c2 = x; den = z; break;
-    }
-#else
+    // The operands come from a per-wave table of the twelve candidate values
+    // in LDS, each lane reading its three at fixed per-lane slots (qt given:
+    // the tile phase), or by lane-mask selects (26 v_cndmask: the tile phase
+    // is VALU-issue-bound, LDS reads are not VALU; -0.6 us per frame,
+    // profiles/r05_quotient_table_ab.log).  The twelve results go to every
+    // lane by readlane (passing J's ten back through the table measured the
+    // same).
     const double fxx = fx * x, fyy = fy * y;
-    double c1 = fy;
-    c1 = lane == 0 ? x : c1;
-    c1 = lane == 1 ? y : c1;
-    c1 = lane == 2 ? fx : c1;
-    c1 = (lane == 3 || lane == 4 || lane == 6) ? -fx : c1;
-    c1 = lane == 5 ? fxx : c1;
-    c1 = lane == 8 ? -fy : c1;
-    c1 = lane == 9 ? fyy : c1;
-    double c2 = 1.0;
-    c2 = (lane == 3 || lane == 5 || lane >= 11) ? x : c2;
-    c2 = (lane == 4 || lane == 10) ? xy : c2;
-    c2 = (lane == 6 || lane == 8 || lane == 9) ? y : c2;
-    const double den = (lane <= 2 || lane == 6 || lane == 7 || lane >= 11) ? z : zz;
-#endif
+    double c1, c2, den;
+    if (qt) {
+        // slots: 0 x, 1 y, 2 fx, 3 -fx, 4 fxx, 5 fy, 6 -fy, 7 fyy, 8 1.0, 9 xy, 10 z, 11 zz
+        if (lane == 0) {
+            double2* t2 = reinterpret_cast<double2*>(qt);
+            t2[0] = make_double2(x, y);
+            t2[1] = make_double2(fx, -fx);
+            t2[2] = make_double2(fxx, fy);
+            t2[3] = make_double2(-fy, fyy);
+            t2[4] = make_double2(1.0, xy);
+            t2[5] = make_double2(z, zz);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // per-lane slots, 4 bits each, lanes 0..11 (lanes >= 12 as lane 11)
+        constexpr unsigned long long kC1 = 0x557653433210ULL, kC2 = 0x091181090888ULL,
+                                     kDen = 0xABBBAABBBAAAULL;
+        const int l = lane < 12 ? lane : 11;
+        c1 = qt[(kC1 >> (4 * l)) & 15];
+        c2 = qt[(kC2 >> (4 * l)) & 15];
+        den = qt[(kDen >> (4 * l)) & 15];
+    } else {
+        c1 = fy;
+        c1 = lane == 0 ? x : c1;
+        c1 = lane == 1 ? y : c1;
+        c1 = lane == 2 ? fx : c1;
+        c1 = (lane == 3 || lane == 4 || lane == 6) ? -fx : c1;
+        c1 = lane == 5 ? fxx : c1;
+        c1 = lane == 8 ? -fy : c1;
+        c1 = lane == 9 ? fyy : c1;
+        c2 = 1.0;
+        c2 = (lane == 3 || lane == 5 || lane >= 11) ? x : c2;
+        c2 = (lane == 4 || lane == 10) ? xy : c2;
+        c2 = (lane == 6 || lane == 8 || lane == 9) ? y : c2;
+        den = (lane <= 2 || lane == 6 || lane == 7 || lane >= 11) ? z : zz;
+    }
     double q = (c1 * c2) / den;
     if (lane == 5) q = fx + q;
     if (lane == 9) q = -fy - q;
@@ -389,20 +400,19 @@ __device__ inline void point_quotients(const Intrinsics& K, const double* pose, 
 __device__ inline bool direct_point_rs(const DirectArgs& a, const LevelPair& fp, int lv,
                                        const double* cur_pose,
                                        const RefSample& r, const uint8_t* win, const CurWin& cw,
-                                       double* out, int* idx) {
+                                       double* out, int* idx, double* qt = nullptr) {
     const int lane = threadIdx.x & 63;
     const int px = (lane >> 3) - 4, py = (lane & 7) - 4;
     const double scale = kScale[lv];
     const int w = a.g.w[lv], h = a.g.h[lv];
     // project_px and d_pixel_d_xi (bit-identical; divisions lane-parallel)
     double Q[12];
-    point_quotients(a.K, cur_pose, r.P, scale, Q);
+    point_quotients(a.K, cur_pose, r.P, scale, Q, qt);
     const double uc = scale * (Q[0] * a.K.fx + a.K.cx);
     const double vc = scale * (Q[1] * a.K.fy + a.K.cy);
     const double hp = 4.0;
     const bool good = r.ok && inside_px(uc - hp, vc - hp, w, h) && inside_px(uc + hp, vc + hp, w, h);
     if (!good) return false;
-    const double Jp[12] = {Q[2], 0.0, Q[3], Q[4], Q[5], Q[6], 0.0, Q[7], Q[8], Q[9], Q[10], Q[11]};
     const uint8_t* C = fp.cur;
     const double x = uc + px, y = vc + py;
     double error, g0, g1;
@@ -425,8 +435,10 @@ __device__ inline bool direct_point_rs(const DirectArgs& a, const LevelPair& fp,
         if (__builtin_expect(one_binade, 1)) {
             const double xx = uc - floor(uc), yy = vc - floor(vc);
             const double w00 = (1 - xx) * (1 - yy), w10 = xx * (1 - yy), w01 = (1 - xx) * yy, w11 = xx * yy;
-            const int o = (fv + py - cw.y0) * kCW + (fu + px - cw.x0);  // tap (0, 0) of this lane
-            auto tap = [&](int dx, int dy) { return (double)ld_lds_u8(win, o + dy * kCW + dx); };
+            // tap (-1, -1) of this lane: every tap below is a non-negative
+            // immediate offset from it (one address, twelve ds_read_u8)
+            const uint8_t* wb = win + ((fv + py - 1 - cw.y0) * kCW + (fu + px - 1 - cw.x0));
+            auto tap = [&](int dx, int dy) { return (double)ld_lds_u8(wb, (dy + 1) * kCW + (dx + 1)); };
             const double tm0 = tap(-1, 0), t00 = tap(0, 0), t10 = tap(1, 0), t20 = tap(2, 0);
             const double tm1 = tap(-1, 1), t01 = tap(0, 1), t11 = tap(1, 1), t21 = tap(2, 1);
             const double t0m = tap(0, -1), t1m = tap(1, -1), t02 = tap(0, 2), t12 = tap(1, 2);
@@ -456,6 +468,7 @@ __device__ inline bool direct_point_rs(const DirectArgs& a, const LevelPair& fp,
         g0 = 0.5 * (sample_cw(C, w, h, x + 1, y, win, cw) - sample_cw(C, w, h, x - 1, y, win, cw));
         g1 = 0.5 * (sample_cw(C, w, h, x, y + 1, win, cw) - sample_cw(C, w, h, x, y - 1, win, cw));
     }
+    const double Jp[12] = {Q[2], 0.0, Q[3], Q[4], Q[5], Q[6], 0.0, Q[7], Q[8], Q[9], Q[10], Q[11]};
     double J[6];
 #pragma unroll
     for (int k = 0; k < 6; ++k) J[k] = -g0 * Jp[k] + -g1 * Jp[6 + k];
@@ -739,7 +752,7 @@ __device__ inline void merged_ref(const DirectArgs& a, const LevelPair& fp, int 
 template <bool FAST, bool LV16 = false, int W = kWaves>
 __device__ void direct_tile_pf(const DirectArgs& a, const LevelPair& fp, int lv, const double* cur_pose, int b,
                                const PfLds& pf, bool merged, double* part, int* good, double* s_pts,
-                               int* s_good, int* s_cnt = nullptr) {
+                               int* s_good, int* s_cnt = nullptr, double* s_qt = nullptr) {
     const int wave = wave_id(), lane = threadIdx.x & 63;
     int first, T;
     tile_range(a, b, &first, &T);
@@ -783,7 +796,8 @@ __device__ void direct_tile_pf(const DirectArgs& a, const LevelPair& fp, int lv,
                 }
                 f = (double)ff;
             } else {
-                ok = direct_point_rs(a, fp, lv, cur_pose, r, pf.win[local], cw, &f, &idx);
+                ok = direct_point_rs(a, fp, lv, cur_pose, r, pf.win[local], cw, &f, &idx,
+                                     s_qt ? s_qt + 12 * wave : nullptr);
             }
         }
         if (!ok) {
@@ -1001,6 +1015,13 @@ __global__ __launch_bounds__(kThreads, 4) void direct_level_kernel(const double*
     __shared__ int s_cnt;  // waves done with their points (last-arriver tile tree)
     __shared__ int s_arrive;
     __shared__ PfLds s_pf;
+#ifndef VISO_NO_QT
+    // the quotient operand tables of the tile phase (point_quotients)
+    __shared__ __attribute__((aligned(16))) double s_qt[FAST ? 2 : kWaves * 12];
+    double* const qt = FAST ? nullptr : s_qt;
+#else
+    double* const qt = nullptr;
+#endif
     const int lv = a.level;
     const bool merged = a.merged && lv == kLevels - 1;
     const int prev = lv + 1;
@@ -1167,7 +1188,7 @@ __global__ __launch_bounds__(kThreads, 4) void direct_level_kernel(const double*
 #pragma unroll
         for (int k = 0; k < 12; ++k) pose[k] = s_pose[k];
         direct_tile_pf<FAST>(a, fp, lv, pose, blockIdx.x, s_pf, merged, a.s.part + (size_t)lv * kMaxTiles * kSums,
-                       a.s.good + lv * kMaxTiles, s_pts, &s_good, &s_cnt);
+                       a.s.good + lv * kMaxTiles, s_pts, &s_good, &s_cnt, qt);
     }
 #ifdef VISO_PROBE
     // block 0 exit: its stamps to the launch's ring slot.  The exit stamp is
