@@ -155,6 +155,8 @@ struct viso_ctx {
     double* h_dbl = nullptr;        // pinned scratch doubles (64)
     double* h_poses = nullptr;      // pinned staging of the pose log (viso_get_poses)
     size_t h_poses_cap = 0;         // poses it holds
+    size_t poses_staged = 0;        // poses whose copy into h_poses is enqueued (finish_call)
+    int stage_poses();
 
     // ---------------- map (Map / MapPoint, include/map.h, map_point.h)
     viso::DevBuf map_pts;  // kMaxMapPoints x 3

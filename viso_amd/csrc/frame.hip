@@ -392,7 +392,22 @@ int viso_ctx::finish_call(hipStream_t ls) {
         rc = bg_end();
         if (rc) return rc;
     }
-    return flush_lk(ls);
+    rc = flush_lk(ls);
+    if (rc) return rc;
+    return stage_poses();
+}
+
+// Every pose of the log is final once a call has ended (the last frame's by
+// its final solve, launched above): the new ones are copied into the pinned
+// staging behind the call's work, so viso_get_poses after a synchronise reads
+// host memory instead of making its own device round trip.
+int viso_ctx::stage_poses() {
+    const size_t m = std::min((size_t)n_poses, (size_t)std::max(p.max_poses, 0));
+    if (m <= poses_staged || m > h_poses_cap || !h_poses) return VISO_OK;
+    VISO_HIP_CHECK(hipMemcpyAsync(h_poses + 12 * poses_staged, (const double*)pose_log.ptr + 12 * poses_staged,
+                                  96 * (m - poses_staged), hipMemcpyDeviceToHost, stream));
+    poses_staged = m;
+    return VISO_OK;
 }
 
 // Background LK alignment: eligible when the context is
@@ -1072,16 +1087,26 @@ int viso_get_poses(viso_ctx* c, double* Tcw12, size_t cap, size_t* n) {
     VISO_HIP_CHECK(hipSetDevice(c->device));
     // through a pinned staging buffer: one DMA and one stream sync (a
     // pageable destination is copied through the runtime's own staging)
+    if (c->poses_staged >= m) {
+        // staged behind the calls that produced them (stage_poses): the
+        // stream's sync makes the copy visible
+        VISO_HIP_CHECK(hipStreamSynchronize(c->stream));
+        std::memcpy(Tcw12, c->h_poses, 96 * m);
+        return VISO_OK;
+    }
     if (c->h_poses_cap < m) {
         const size_t want = std::max(m, (size_t)4096);
+        VISO_HIP_CHECK(hipStreamSynchronize(c->stream));  // no staged copy in flight into the old buffer
         if (c->h_poses) VISO_HIP_CHECK(hipHostFree(c->h_poses));
         c->h_poses = nullptr;
         c->h_poses_cap = 0;
+        c->poses_staged = 0;
         VISO_HIP_CHECK(hipHostMalloc((void**)&c->h_poses, 96 * want));
         c->h_poses_cap = want;
     }
     VISO_HIP_CHECK(hipMemcpyAsync(c->h_poses, c->pose_log.ptr, 96 * m, hipMemcpyDeviceToHost, c->stream));
     VISO_HIP_CHECK(hipStreamSynchronize(c->stream));
+    c->poses_staged = std::max(c->poses_staged, m);
     std::memcpy(Tcw12, c->h_poses, 96 * m);
     return VISO_OK;
 }

@@ -1019,11 +1019,17 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
                 break;
             }
             head = (xcc + h) & 7;
-            // a wave past its own head (and every drain wave) looks first: an
-            // exhausted head costs a load, not an atomic (thousands of waves
-            // walking the heads at the chunk's end would otherwise queue
-            // behind each other on eight words)
+            // a wave past its own head looks first: an exhausted head costs a
+            // load, not an atomic (thousands of waves walking the heads at the
+            // chunk's end would otherwise queue behind each other on eight
+            // words).  A drain wave at its own head does not: the head holds
+            // the last frame's points then, and a look ahead of every
+            // dequeue doubled the operations on those eight words.
+#ifdef VISO_DRAIN_PEEK_OWN
             if ((h > 0 || a.bg_drain) &&
+#else
+            if (h > 0 &&
+#endif
                 __builtin_amdgcn_readfirstlane(__hip_atomic_load(a.bg_next + 32 * head, __ATOMIC_RELAXED,
                                                                  __HIP_MEMORY_SCOPE_AGENT)) >= per_head) {
                 ++h;
@@ -1127,8 +1133,8 @@ void launch_klt(const FrameDev& ref, const FrameDev& cur, const PyrGeom& g, cons
 void launch_klt_dev(const FrameDev& ref, const FrameDev& cur, const PyrGeom& g, const float2* kp1,
                     float2* kp2, uint8_t* success, const int* n_dev, int cap, double thresh, hipStream_t stream) {
     if (cap <= 0) return;
-    // one wave per track up to 8,192 tracks, striding beyond
-    const int blocks = (std::min(cap, 8192) + 3) / 4;
+    // one wave per track of the capacity; waves past the device count return
+    const int blocks = (cap + 3) / 4;
     klt_kernel<<<blocks, 256, 0, stream>>>(ref, cur, make_pyrdev(g), kp1, kp2, success, cap, thresh, n_dev);
 }
 
@@ -1145,23 +1151,32 @@ void launch_lk_align(const LkAlignArgs& a, hipStream_t stream) {
 // two never share a CU (2 x 84 > 160 KB) while one leaves room for a 12-wave
 // direct-pose workgroup (84 + 68 <= 160 KB)
 constexpr size_t kBgLdsTotal = 84 * 1024;
-// the resident grid's dynamic LDS (its request minus the static windows);
-// the kernel's attribute is raised to it once
-static size_t lk_bg_dyn_lds() {
-    const size_t dyn = kBgLdsTotal - sizeof(uint8_t) * 4 * 2 * kWinW * kWinH;
+// the resident grid's dynamic LDS per precision: its request minus the
+// kernel's own static LDS (read from the code object, windows and per-wave
+// poses, rather than restated here); the kernels' attributes are raised to
+// it once.  (A round-5 variant that prefetched every level's template and
+// window into the wave's LDS at item start made the tail 105-126 us instead
+// of 81-84: spills at item start and fewer co-resident drain workgroups.)
+static size_t lk_bg_dyn_lds(bool fast) {
+    static size_t dyn[2] = {0, 0};
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)lk_item_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)dyn);
-        (void)hipFuncSetAttribute((const void*)lk_item_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)dyn);
+        const void* k[2] = {(const void*)lk_item_kernel<false>, (const void*)lk_item_kernel<true>};
+        for (int j = 0; j < 2; ++j) {
+            hipFuncAttributes fa{};
+            size_t st = 4 * 2 * kWinW * kWinH;
+            if (hipFuncGetAttributes(&fa, k[j]) == hipSuccess) st = fa.sharedSizeBytes;
+            dyn[j] = kBgLdsTotal > st ? kBgLdsTotal - st : 0;
+            (void)hipFuncSetAttribute(k[j], hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn[j]);
+        }
+        (void)hipGetLastError();
         attr = true;
     }
-    return dyn;
+    return dyn[fast ? 1 : 0];
 }
 void launch_lk_bg(const LkAlignArgs& a, int grid, hipStream_t stream) {
     if (a.n <= 0 || a.bg_items <= 0 || grid <= 0) return;
-    const size_t dyn = lk_bg_dyn_lds();
+    const size_t dyn = lk_bg_dyn_lds(a.fast);
     if (a.fast)
         lk_item_kernel<true><<<grid, 256, dyn, stream>>>(a);
     else
@@ -1172,7 +1187,7 @@ void launch_lk_bg(const LkAlignArgs& a, int grid, hipStream_t stream) {
 // first launch of both precisions) at context init: a one-workgroup launch
 // with no frames returns at once.
 void warm_lk_bg(hipStream_t stream) {
-    (void)lk_bg_dyn_lds();
+    (void)lk_bg_dyn_lds(false);
     LkAlignArgs a{};
     a.n_frames = 0;
     lk_item_kernel<true><<<1, 256, 0, stream>>>(a);
