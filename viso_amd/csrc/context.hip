@@ -129,6 +129,12 @@ int viso_destroy(viso_ctx* c) {
 
 int viso_synchronize(viso_ctx* c) {
     if (!c) return VISO_ERR_ARG;
+    // the pose log's new entries ride this sync into pinned memory, so a
+    // viso_get_poses after it makes no device round trip of its own
+    {
+        const int rc = c->stage_poses();
+        if (rc) return rc;
+    }
     VISO_HIP_CHECK(hipStreamSynchronize(c->stream));
     if (c->lk_stream) VISO_HIP_CHECK(hipStreamSynchronize(c->lk_stream));
     return c->bg_check();

@@ -392,15 +392,15 @@ int viso_ctx::finish_call(hipStream_t ls) {
         rc = bg_end();
         if (rc) return rc;
     }
-    rc = flush_lk(ls);
-    if (rc) return rc;
-    return stage_poses();
+    return flush_lk(ls);
 }
 
-// Every pose of the log is final once a call has ended (the last frame's by
-// its final solve, launched above): the new ones are copied into the pinned
-// staging behind the call's work, so viso_get_poses after a synchronise reads
-// host memory instead of making its own device round trip.
+// Every pose of the log is final once an ingest call has ended (the last
+// frame's by its final solve, launched in finish_call): viso_synchronize
+// copies the new ones into the pinned staging ahead of its stream sync, so a
+// viso_get_poses after it reads host memory instead of making its own device
+// round trip (enqueued per ingest call instead, the copy cost frame-by-frame
+// callers ~10 us per frame).
 int viso_ctx::stage_poses() {
     const size_t m = std::min((size_t)n_poses, (size_t)std::max(p.max_poses, 0));
     if (m <= poses_staged || m > h_poses_cap || !h_poses) return VISO_OK;
