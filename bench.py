@@ -1074,13 +1074,13 @@ def pmc_evidence(W, H, breakdown, stereo_vo, n_map=None):
         # the HEAD's rocprofv3 kernel trace of the same workload with the
         # background LK grid off (VISO_LK_BG=0; tools/gpu_evidence.sh): the
         # dominant kernel's average duration and the fp64 fraction it gives
-        st = rocprof_avg_us(os.path.join(ROOT, "profiles", "r05_kernel_stats_nobg.csv"),
+        st = rocprof_avg_us(os.path.join(ROOT, "profiles", "r05_direct_kernel_stats.csv"),
                             "direct_level_kernel<false>")
         if st and flop:
             avg_us, calls = st
             peak = d.get("fp64_peak_tflops") or 78.6
             gn.update({"rocprof_avg_us_per_launch": round(avg_us, 2), "rocprof_calls": calls,
-                       "rocprof_source": "profiles/r05_kernel_stats_nobg.csv (rocprofv3 --kernel-trace --stats, "
+                       "rocprof_source": "profiles/r05_direct_kernel_stats.csv (rocprofv3 --kernel-trace --stats, "
                                          "VISO_LK_BG=0, bench.py --steps 20 --warmup 5)",
                        "fp64_frac": round(flop / (avg_us * 1e-6) / 1e12 / peak, 4),
                        "fp64_frac_basis": "algorithmic flop per launch / rocprof average duration / "
