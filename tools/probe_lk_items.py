@@ -138,8 +138,14 @@ def main():
                 if R[j, 2 + k]:
                     gaps.append(f"{(R[j, 2 + k] - prev) * us:.1f}")
                     prev = R[j, 6 + k]
+            wl = ""
+            if R[j, 15]:  # VISO_PROBE_WIN: the slowest window load of the item (issue -> data, -> LDS)
+                w15 = int(R[j, 15])
+                t_iss = ((w15 >> 40) - (int(R[j, 1]) & 0xffffff)) % (1 << 24)
+                wl = (f" | window L{(w15 >> 32) & 3}: load {(w15 & 0xffff) * us:.1f} commit {((w15 >> 16) & 0xffff) * us:.1f}"
+                      f" issued at {start[j] + t_iss * us:.1f}")
             print(f"   {idx[j]:5d} {'drain' if drain[j] else 'res  '} {xcc[j]} {se[j]} {cu[j]:2d} {simd[j]} | "
-                  f"{deq[j]:6.1f} {start[j]:6.1f} {end[j]:6.1f} | {' '.join(lv)} | gaps {' '.join(gaps)}")
+                  f"{deq[j]:6.1f} {start[j]:6.1f} {end[j]:6.1f} | {' '.join(lv)} | gaps {' '.join(gaps)}{wl}")
         # by iterations: time per iteration of long items vs their kind
         tot = its.sum(1)
         sel = tot >= 40

@@ -656,8 +656,32 @@ __device__ __attribute__((always_inline)) inline void lk_point(const LkAlignArgs
                     if (level > 0) {
                         const double s1 = kScale[level - 1];
                         tmpl_load(level - 1, tn, tfn);
+#ifdef VISO_PROBE_WIN
+                        // (probe) the window's global loads: issue -> data in
+                        // registers -> committed to LDS, the slowest level's
+                        const unsigned long long pw0 = __builtin_amdgcn_s_memrealtime();
+                        const WinRegs wr = window_issue(level_ptr(cur, level - 1), a.g.w[level - 1],
+                                                        a.g.h[level - 1], cu * s1, cv * s1);
+                        int sum = 0;
+#pragma unroll
+                        for (int k = 0; k < kWinPer; ++k) sum += wr.v[k];
+                        __builtin_amdgcn_readfirstlane(sum);  // waits for the nine loads
+                        asm volatile("" ::"v"(sum));
+                        const unsigned long long pw1 = __builtin_amdgcn_s_memrealtime();
+                        win = window_commit((level & 1) ? my_win0 : my_win1, wr);
+                        const unsigned long long pw2 = __builtin_amdgcn_s_memrealtime();
+                        if (pr_slot >= 0 && lane == 0) {
+                            const unsigned long long ld = (pw1 - pw0) < 65535 ? (pw1 - pw0) : 65535;
+                            const unsigned long long st = (pw2 - pw1) < 65535 ? (pw2 - pw1) : 65535;
+                            const unsigned long long old = g_probe_items[pr_slot][15];
+                            if (ld > (old & 0xffff))
+                                g_probe_items[pr_slot][15] = ld | (st << 16) | ((unsigned long long)(level - 1) << 32) |
+                                                             ((pw0 & 0xffffffull) << 40);
+                        }
+#else
                         win = load_window((level & 1) ? my_win0 : my_win1, level_ptr(cur, level - 1),
                                           a.g.w[level - 1], a.g.h[level - 1], cu * s1, cv * s1);
+#endif
                     }
                 };
 #ifdef VISO_PROBE
