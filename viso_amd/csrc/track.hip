@@ -65,11 +65,24 @@ struct Window {
 // The window's bytes in flight (issued, not yet in LDS): lane l holds bytes
 // l + 64 k of the row-major window.
 constexpr int kWinPer = kWinW * kWinH / 64;  // 9
+#ifndef VISO_WIN_BYTES
+// The window's 24 rows of 24 bytes as 72 unaligned 8-byte loads (row e / 3,
+// bytes 8 (e % 3) ..): lanes 0..63 hold chunks 0..63, lanes 0..7 chunks
+// 64..71 — two load instructions per window instead of nine byte loads (the
+// window sits inside the image, so no byte needs a bounds test).
+constexpr int kWinChunks = kWinW * kWinH / 8;  // 72
+struct WinRegs {
+    uint64_t v[2];
+    int x0, y0;
+    bool on;
+};
+#else
 struct WinRegs {
     uint8_t v[kWinPer];
     int x0, y0;
     bool on;
 };
+#endif
 
 // (cx, cy) is the wave's patch centre (the same in every lane): the window's
 // placement is taken into SGPRs, so every window test downstream is a
@@ -84,17 +97,29 @@ __device__ inline WinRegs window_issue(const uint8_t* img, int w, int h, double 
     int y0 = (int)floor(cy) - kWinH / 2 + 1;
     x0 = __builtin_amdgcn_readfirstlane(min(max(x0, 0), w - kWinW));
     y0 = __builtin_amdgcn_readfirstlane(min(max(y0, 0), h - kWinH));
+    const int lane = threadIdx.x & 63;
+    const uint8_t* base = img + ((size_t)y0 * (size_t)w + (size_t)x0);
+#ifndef VISO_WIN_BYTES
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int e = lane + 64 * k;
+        const int rr = e / 3, c = e - 3 * (e / 3);
+        r.v[k] = 0;
+        if (e < kWinChunks)
+            r.v[k] = *reinterpret_cast<const __attribute__((address_space(1))) uint64_t*>(
+                (const __attribute__((address_space(1))) uint8_t*)base + (uint32_t)(rr * w + 8 * c));
+    }
+#else
     // byte e = lane + 64 k of the row-major window: row e / 24, column e % 24
     // (compile-time per k up to the lane), 32-bit offsets from the window's
     // first byte (a level is far below 2^31 bytes)
-    const int lane = threadIdx.x & 63;
-    const uint8_t* base = img + ((size_t)y0 * (size_t)w + (size_t)x0);
 #pragma unroll
     for (int k = 0; k < kWinPer; ++k) {
         const int e = lane + 64 * k;
         const int rr = e / kWinW, c = e - rr * kWinW;
         r.v[k] = ld_global_u8_off(base, (uint32_t)(rr * w + c));
     }
+#endif
     r.x0 = x0;
     r.y0 = y0;
     return r;
@@ -104,8 +129,18 @@ __device__ inline Window window_commit(uint8_t* lds, const WinRegs& r) {
     Window win{nullptr, 0, 0};
     if (!r.on) return win;
     const int lane = threadIdx.x & 63;
+#ifndef VISO_WIN_BYTES
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int e = lane + 64 * k;
+        if (e < kWinChunks)  // chunk e lands at byte 8 e of the row-major window (rows of 24 = 3 chunks)
+            *reinterpret_cast<__attribute__((address_space(3))) uint64_t*>(
+                (__attribute__((address_space(3))) uint8_t*)lds + 8 * e) = r.v[k];
+    }
+#else
 #pragma unroll
     for (int k = 0; k < kWinPer; ++k) st_lds_u8(lds, lane + 64 * k, r.v[k]);
+#endif
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -466,7 +501,7 @@ __global__ __launch_bounds__(256) void klt_kernel(FrameDev ref, FrameDev cur, Py
                                                   float2* __restrict__ kp2,
                                                   uint8_t* __restrict__ success, int n,
                                                   double thresh, const int* __restrict__ n_dev) {
-    __shared__ uint8_t s_win[4][kWinW * kWinH];
+    __shared__ __attribute__((aligned(16))) uint8_t s_win[4][kWinW * kWinH];
     const int i = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     if (n_dev) n = min(__builtin_amdgcn_readfirstlane(*n_dev), n);
     if (i >= n) return;  // wave-uniform
@@ -664,7 +699,7 @@ __device__ __attribute__((always_inline)) inline void lk_point(const LkAlignArgs
                                                         a.g.h[level - 1], cu * s1, cv * s1);
                         int sum = 0;
 #pragma unroll
-                        for (int k = 0; k < kWinPer; ++k) sum += wr.v[k];
+                        for (int k = 0; k < (int)(sizeof(wr.v) / sizeof(wr.v[0])); ++k) sum += (int)wr.v[k];
                         __builtin_amdgcn_readfirstlane(sum);  // waits for the nine loads
                         asm volatile("" ::"v"(sum));
                         const unsigned long long pw1 = __builtin_amdgcn_s_memrealtime();
@@ -763,7 +798,7 @@ __device__ __attribute__((always_inline)) inline void lk_point(const LkAlignArgs
 template <bool FAST>
 __global__ __launch_bounds__(256, FAST ? VISO_LK_MIN_WAVES_FAST : VISO_LK_MIN_WAVES) void lk_align_kernel(
     LkAlignArgs a) {
-    __shared__ uint8_t s_win[4][2][kWinW * kWinH];
+    __shared__ __attribute__((aligned(16))) uint8_t s_win[4][2][kWinW * kWinH];
     const int i = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     if (i >= a.n) return;
     // frame of the batch (blockIdx.y): its pyramid, pose and output rows
@@ -812,7 +847,7 @@ constexpr int kBgClosed = 1 << 30;                          // bg_left[1]: the d
 template <bool FAST>
 __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
     if (a.n_frames <= 0) return;  // warm_lk_bg
-    __shared__ uint8_t s_win[4][2][kWinW * kWinH];
+    __shared__ __attribute__((aligned(16))) uint8_t s_win[4][2][kWinW * kWinH];
     __shared__ double s_pose[4][12];  // the wave's current frame pose
     const LkAlignArgs* ka = (const LkAlignArgs*)__builtin_amdgcn_kernarg_segment_ptr();
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
