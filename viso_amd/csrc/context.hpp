@@ -140,6 +140,7 @@ struct viso_ctx {
     viso::DevBuf fast_rows;
     int n_track = 0;             // < 0: on the device only (ntrack_pending)
     bool ntrack_pending = false;  // a re-detection frame's count not read yet
+    hipEvent_t ntrack_evt = nullptr;  // behind that count's copy into h_int[3]
     int resolve_ntrack();
     bool success_valid = false;
     int frame_cnt = 0;

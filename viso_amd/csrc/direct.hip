@@ -1629,7 +1629,31 @@ __global__ void set_pose_kernel(double* dst, Pose12v p) {
     if (threadIdx.x < 12) dst[threadIdx.x] = p.v[threadIdx.x];
 }
 
+// Map creation (src/viso.cpp:79-96) in one launch: the current frame's pose
+// (by value), the map points (the 2D-2D result's inlier points), and the two
+// keyframe poses (the reference frame's, read on the device, and the new one).
+__global__ void map_create_kernel(double* __restrict__ cur_pose, Pose12v p, const double* __restrict__ pts_src,
+                                  double* __restrict__ pts_dst, int n_dbl, const double* __restrict__ ref_pose,
+                                  double* __restrict__ kf_poses) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    for (int i = t; i < n_dbl; i += gridDim.x * blockDim.x) pts_dst[i] = pts_src[i];
+    if (blockIdx.x == 0 && threadIdx.x < 12) {
+        cur_pose[threadIdx.x] = p.v[threadIdx.x];
+        kf_poses[threadIdx.x] = ref_pose[threadIdx.x];
+        kf_poses[12 + threadIdx.x] = p.v[threadIdx.x];
+    }
+}
+
 }  // namespace
+
+void launch_map_create(double* cur_pose, const double pose[12], const double* pts_src, double* pts_dst, int n_pts,
+                       const double* ref_pose, double* kf_poses, hipStream_t stream) {
+    Pose12v p;
+    for (int k = 0; k < 12; ++k) p.v[k] = pose[k];
+    const int n_dbl = 3 * n_pts;
+    const int blocks = std::max(1, std::min((n_dbl + 255) / 256, 64));
+    map_create_kernel<<<blocks, 256, 0, stream>>>(cur_pose, p, pts_src, pts_dst, n_dbl, ref_pose, kf_poses);
+}
 
 void launch_set_pose(double* dst, const double src[12], hipStream_t stream) {
     Pose12v p;

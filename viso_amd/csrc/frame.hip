@@ -158,6 +158,7 @@ int viso_ctx::init() {
     // chunk: ~0.1 ms)
     VISO_HIP_CHECK(hipEventCreateWithFlags(&geo_fork, hipEventDisableTiming));
     VISO_HIP_CHECK(hipEventCreateWithFlags(&geo_join, hipEventDisableTiming));
+    VISO_HIP_CHECK(hipEventCreateWithFlags(&ntrack_evt, hipEventDisableTiming));
     rc = bg_prepare();
     if (rc) return rc;
     // the pose getter's pinned staging (viso_get_poses)
@@ -177,7 +178,7 @@ void viso_ctx::release() {
     }
     if (bg_done) (void)hipEventDestroy(bg_done);
     bg_done = nullptr;
-    for (hipEvent_t* e : {&geo_fork, &geo_join}) {
+    for (hipEvent_t* e : {&geo_fork, &geo_join, &ntrack_evt}) {
         if (*e) (void)hipEventDestroy(*e);
         *e = nullptr;
     }
@@ -728,7 +729,15 @@ int viso_ctx::on_new_frame(int cur) {
                 stats[3] = -1;
                 // n_track < 0: the re-detection frame before this one left its
                 // count on the device only; the KLT and the compaction read it
-                // there (capped at max_features)
+                // there (capped at max_features) — unless its copy has landed
+                // already (a caller that synchronised in between): then the
+                // exact count, without waiting
+                if (ntrack_pending && hipEventQuery(ntrack_evt) == hipSuccess) {
+                    n_track = std::min(h_int[3], p.max_features);
+                    if (stats[1] == -1) stats[1] = n_track;
+                    ntrack_pending = false;
+                }
+                (void)hipGetLastError();  // (hipErrorNotReady from the query)
                 const int n = n_track;
                 if (n != 0) {
                     TimedRegion t(timing, VISO_KERNEL_KLT, stream);
@@ -805,14 +814,13 @@ int viso_ctx::on_new_frame(int cur) {
                     double pose[12];
                     std::memcpy(pose, initR, sizeof(initR));
                     std::memcpy(pose + 9, initT, sizeof(initT));
-                    launch_set_pose(pose_of(cur), pose, stream);
                     n_map = std::min(nr_inliers, kMaxMapPoints);
                     point_host.assign((size_t)n_map, 0);  // in keyframe 0's (ref) frame
-                    VISO_HIP_CHECK(hipMemcpyAsync(map_pts.ptr, geo.points_out, 24 * (size_t)n_map,
-                                                  hipMemcpyDeviceToDevice, stream));
-                    for (size_t j = 0; j < kf_slots.size(); ++j)
-                        VISO_HIP_CHECK(hipMemcpyAsync((char*)kf_poses.ptr + 96 * j, pose_of(kf_slots[j]),
-                                                      96, hipMemcpyDeviceToDevice, stream));
+                    // the frame's pose, the map points and the two keyframe
+                    // poses in one launch (round 4: a kernel and three copies)
+                    launch_map_create(pose_of(cur), pose, geo.points_out, (double*)map_pts.ptr, n_map,
+                                      pose_of(ref_slot), (double*)kf_poses.ptr, stream);
+                    VISO_HIP_CHECK(hipGetLastError());
                     // LK-alignment templates of the new map (constant while tracking)
                     {
                         const int rc = build_lk_templates();
@@ -839,6 +847,7 @@ int viso_ctx::on_new_frame(int cur) {
                                      (float2*)kp2.ptr, stream);
                 VISO_HIP_CHECK(hipGetLastError());
                 VISO_HIP_CHECK(hipMemcpyAsync(h_int + 3, n_track_dev.ptr, sizeof(int), hipMemcpyDeviceToHost, stream));
+                VISO_HIP_CHECK(hipEventRecord(ntrack_evt, stream));
                 n_track = -1;
                 ntrack_pending = true;
                 success_valid = false;

@@ -221,5 +221,9 @@ int launch_photometric_ba(const uint8_t* const* kf_l0, int n_kf, int w, int h, c
                           hipStream_t stream);
 // dst (12 doubles, device) <- src (host values, passed by value)
 void launch_set_pose(double* dst, const double src[12], hipStream_t stream);
+// map creation: cur_pose <- pose, pts_dst <- pts_src (n_pts x 3), kf_poses[0]
+// <- *ref_pose, kf_poses[1] <- pose (one launch)
+void launch_map_create(double* cur_pose, const double pose[12], const double* pts_src, double* pts_dst, int n_pts,
+                       const double* ref_pose, double* kf_poses, hipStream_t stream);
 
 }  // namespace viso
