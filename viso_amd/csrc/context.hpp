@@ -133,6 +133,10 @@ struct viso_ctx {
     std::deque<int> free_slots;  // FIFO: the longest-free slot is reused first
     int ref_slot = -1, last_slot = -1;  // init_.ref_frame, last_frame
     std::vector<int> kf_slots;          // Map::keyframes_
+    int ident_slot = -1;  // the ingest's pyramid wrote this frame's Keyframe-ctor pose (PyrOwn)
+    // the ingest's pyramid launch(es) with its last frame's PyrOwn (level 0
+    // owned, identity pose outside tracking)
+    void launch_ingest_pyramid(const uint8_t* const* l0, uint8_t* const* dst, const int* sl, int n);
 
     // ---------------- initialisation tracks (Viso::Initialization, include/viso.h:33-41)
     viso::DevBuf kp1, kp2, kp1b, kp2b, track_success, n_track_dev;
@@ -140,7 +144,7 @@ struct viso_ctx {
     viso::DevBuf fast_rows;
     int n_track = 0;             // < 0: on the device only (ntrack_pending)
     bool ntrack_pending = false;  // a re-detection frame's count not read yet
-    hipEvent_t ntrack_evt = nullptr;  // behind that count's copy into h_int[3]
+    hipEvent_t ntrack_evt = nullptr;  // behind the FAST frame's count store into h_int[3]
     int resolve_ntrack();
     bool success_valid = false;
     int frame_cnt = 0;
@@ -153,6 +157,10 @@ struct viso_ctx {
     viso::GeoArgs geo{};
     viso::GeoCtl* h_ctl = nullptr;  // pinned
     int* h_int = nullptr;           // pinned scratch ints
+    // their device-side addresses (kernels store the FAST frame's count and
+    // the 2D-2D control block there directly: no copy launch per frame)
+    int* h_int_dev = nullptr;
+    viso::GeoCtl* h_ctl_dev = nullptr;
     double* h_dbl = nullptr;        // pinned scratch doubles (64)
     double* h_poses = nullptr;      // pinned staging of the pose log (viso_get_poses)
     size_t h_poses_cap = 0;         // poses it holds

@@ -139,6 +139,9 @@ int viso_ctx::init() {
     VISO_HIP_CHECK(hipHostMalloc((void**)&h_ctl, sizeof(GeoCtl)));
     VISO_HIP_CHECK(hipHostMalloc((void**)&h_int, 64 * sizeof(int)));
     VISO_HIP_CHECK(hipHostMalloc((void**)&h_dbl, 256 * sizeof(double)));
+    VISO_HIP_CHECK(hipHostGetDevicePointer((void**)&h_int_dev, h_int, 0));
+    VISO_HIP_CHECK(hipHostGetDevicePointer((void**)&h_ctl_dev, h_ctl, 0));
+    geo.host_ctl = h_ctl_dev;
     // map + tracking
     if (!rc) rc = map_pts.ensure(24 * (size_t)kMaxMapPoints);
     if (!rc) rc = kf_poses.ensure(96 * (size_t)kMaxKeyframes);
@@ -283,6 +286,27 @@ int viso_ctx::own_level0(int s) {
     r.l0 = slot_base(s);
     r.borrowed = false;
     return VISO_OK;
+}
+
+// The ingest's pyramid.  Its last frame is last_frame when the call ends, so
+// its level 0 would be copied into its slot at the end anyway (own_level0):
+// the tail launch copies it instead (small chunks; a large one's bands would
+// serialise the copy), and outside tracking also writes that
+// frame's Keyframe-ctor pose (R = I, T = 0; on_new_frame skips its launch) —
+// a frame-by-frame caller pays two launches fewer per frame.
+void viso_ctx::launch_ingest_pyramid(const uint8_t* const* l0, uint8_t* const* dst, const int* sl, int n) {
+    const int s = sl[n - 1];
+    PyrOwn own{n - 1, state != VISO_STATE_RUNNING ? pose_of(s) : nullptr, false};
+    ident_slot = own.ident_pose ? s : -1;
+    {
+        TimedRegion t(timing, VISO_KERNEL_PYRAMID, stream);
+        launch_pyramid_frames(geom, l0, dst, n, stream, &own);
+    }
+    SlotRec& r = slots[(size_t)s];
+    if (r.borrowed && own.copied) {
+        r.l0 = slot_base(s);
+        r.borrowed = false;
+    }
 }
 
 int viso_ctx::ingest_host(const uint8_t* grey, int32_t w, int32_t h, int32_t stride, int* slot_out) {
@@ -714,7 +738,9 @@ int viso_ctx::on_new_frame(int cur) {
     } cur_ref{this, cur};
     for (int k = 0; k < 16; ++k) stats[k] = 0;
     // Keyframe ctor: R = I, T = 0 (a tracking frame overwrites it below)
-    if (state != VISO_STATE_RUNNING) launch_set_pose(pose_of(cur), kIdentityPose, stream);
+    // (written by the ingest's pyramid launch for its last frame, PyrOwn)
+    if (state != VISO_STATE_RUNNING && cur != ident_slot) launch_set_pose(pose_of(cur), kIdentityPose, stream);
+    if (cur == ident_slot) ident_slot = -1;
     const double K[4] = {p.fx, p.fy, p.cx, p.cy};
     bool counted = true;  // ++init_.frame_cnt at the end of kInitialization
     switch (state) {
@@ -771,7 +797,7 @@ int viso_ctx::on_new_frame(int cur) {
                     launch_pose_2d2d_gate(geo, stream);
                 }
                 VISO_HIP_CHECK(hipGetLastError());
-                VISO_HIP_CHECK(hipMemcpyAsync(h_ctl, geo.ctl, sizeof(GeoCtl), hipMemcpyDeviceToHost, stream));
+                // (the gate mirrors the control block into h_ctl itself)
                 VISO_HIP_CHECK(hipStreamSynchronize(stream));
                 if (h_ctl->gate) {
                     hipStream_t bs = stream;
@@ -783,7 +809,7 @@ int viso_ctx::on_new_frame(int cur) {
                         bs = launch_pose_2d2d_body(geo, stream, lk_stream, geo_fork, geo_join);
                     }
                     VISO_HIP_CHECK(hipGetLastError());
-                    VISO_HIP_CHECK(hipMemcpyAsync(h_ctl, geo.ctl, sizeof(GeoCtl), hipMemcpyDeviceToHost, bs));
+                    // (SelectMotion's last launch mirrors the block into h_ctl)
                     VISO_HIP_CHECK(hipStreamSynchronize(bs));
                 }
                 const GeoCtl& c = *h_ctl;
@@ -832,21 +858,19 @@ int viso_ctx::on_new_frame(int cur) {
                 }
             } else {
                 // re-detect (src/viso.cpp:100-108)
+                // no host round trip: the FAST launch caps the count and
+                // writes kp2 = kp1 on the device, the next frame's KLT reads
+                // the count there, and the host learns it lazily from the
+                // copy the same launch stores into h_int[3] (resolve_ntrack:
+                // a getter, or the next frame once ntrack_evt has passed)
                 {
                     TimedRegion t(timing, VISO_KERNEL_FAST, stream);
+                    const FastDetect det{(float2*)kp2.ptr, h_int_dev + 3};
                     launch_fast(frame(cur).l[0], g.w[0], g.h[0], p.fast_thresh, fast,
                                 (float2*)kp1.ptr, nullptr, p.max_features, (int*)n_track_dev.ptr,
-                                stream);
+                                stream, &det);
                 }
                 VISO_HIP_CHECK(hipGetLastError());
-                // no host round trip: the count is capped and kp2 = kp1 on the
-                // device, the next frame's KLT reads the count there, and the
-                // host learns it lazily (resolve_ntrack: a getter, or the next
-                // frame's gate read)
-                launch_detect_finish((int*)n_track_dev.ptr, p.max_features, (const float2*)kp1.ptr,
-                                     (float2*)kp2.ptr, stream);
-                VISO_HIP_CHECK(hipGetLastError());
-                VISO_HIP_CHECK(hipMemcpyAsync(h_int + 3, n_track_dev.ptr, sizeof(int), hipMemcpyDeviceToHost, stream));
                 VISO_HIP_CHECK(hipEventRecord(ntrack_evt, stream));
                 n_track = -1;
                 ntrack_pending = true;
@@ -953,10 +977,7 @@ int viso_process_frame(viso_ctx* c, const uint8_t* grey, int32_t width, int32_t 
     if (rc) return rc;
     uint8_t* slot = c->slot_base(s);
     const uint8_t* l0 = slot;
-    {
-        TimedRegion t(c->timing, VISO_KERNEL_PYRAMID, c->stream);
-        launch_pyramid_frames(c->geom, &l0, &slot, 1, c->stream);
-    }
+    c->launch_ingest_pyramid(&l0, &slot, &s, 1);
     VISO_HIP_CHECK(hipGetLastError());
     rc = c->on_new_frame(s);
     if (rc) return rc;
@@ -978,10 +999,7 @@ int viso_process_stereo(viso_ctx* c, const uint8_t* left, const uint8_t* right,
     }
     uint8_t* slot = c->slot_base(sl);
     const uint8_t* l0 = slot;
-    {
-        TimedRegion t(c->timing, VISO_KERNEL_PYRAMID, c->stream);
-        launch_pyramid_frames(c->geom, &l0, &slot, 1, c->stream);
-    }
+    c->launch_ingest_pyramid(&l0, &slot, &sl, 1);
     VISO_HIP_CHECK(hipGetLastError());
     // the right image feeds the stereo initialisation (viso_set_stereo), which
     // reads its level 0 only: no pyramid is built for it; the reference path
@@ -1026,10 +1044,7 @@ int viso_process_frames_device(viso_ctx* c, const uint8_t* d_left, const uint8_t
             l0.push_back(src);
             dst.push_back(c->slot_base(s));
         }
-        {
-            TimedRegion t(c->timing, VISO_KERNEL_PYRAMID, c->stream);
-            launch_pyramid_frames(c->geom, l0.data(), dst.data(), (int)l0.size(), c->stream);
-        }
+        c->launch_ingest_pyramid(l0.data(), dst.data(), sl.data(), (int)l0.size());
         VISO_HIP_CHECK(hipGetLastError());
         // (the background words' memset stays behind the pyramid: issued
         // ahead of it, the chain ran at half speed in 3 of 6 bench runs,
@@ -1238,7 +1253,7 @@ int viso_pose_2d2d(viso_ctx* c, const double* p1, const double* p2, int32_t n, d
         launch_pose_2d2d(a, c->stream, &c->timing);
     }
     VISO_HIP_CHECK(hipGetLastError());
-    VISO_HIP_CHECK(hipMemcpyAsync(c->h_ctl, a.ctl, sizeof(GeoCtl), hipMemcpyDeviceToHost, c->stream));
+    // (the gate and SelectMotion mirror the control block into h_ctl)
     VISO_HIP_CHECK(hipStreamSynchronize(c->stream));
     const GeoCtl& g = *c->h_ctl;
     for (int k = 0; k < 8; ++k) stats[k] = 0;

@@ -91,6 +91,18 @@ __device__ inline int pick_uniform(const int* v, int i) {
     return r;
 }
 
+// the control block into a.host_ctl (GeoArgs) by the block's first threads,
+// after a barrier that follows the block's last ctl write: system-scope
+// stores, visible to the host once the launch has completed
+__device__ inline void ctl_mirror(const GeoArgs& a) {
+    if (!a.host_ctl) return;
+    constexpr int kWords = (int)(sizeof(GeoCtl) / 8);
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(a.ctl);
+    uint64_t* dst = reinterpret_cast<uint64_t*>(a.host_ctl);
+    for (int k = threadIdx.x; k < kWords; k += blockDim.x)
+        __hip_atomic_store(dst + k, src[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // ---------------------------------------------------------------- normalise
 // p = K_inv * (x, y, 1) (src/viso.cpp:45-48); q = float-rounded (cv::Point2f,
 // :204-205); disparity = canonical tree of |p2 - p1|^2 (:199-211).
@@ -177,6 +189,8 @@ __global__ __launch_bounds__(kNormThreads) void normalize_kernel(GeoArgs a) {
         c->nr_inliers = 0;
         c->best_motion = -1;
     }
+    __syncthreads();
+    ctl_mirror(a);
 }
 
 // ---------------------------------------------------------------- E RANSAC
@@ -1062,6 +1076,8 @@ __global__ __launch_bounds__(256) void select_finish_kernel(GeoArgs a) {
         if (nonzero)
             for (int k = 0; k < 3; ++k) c->T[k] = c->T[k] / md;
     }
+    __syncthreads();
+    ctl_mirror(a);
     // output: flags, and the inlier points in order
     const int per = (n + 255) / 256;
     const int i0 = min(t * per, n), i1 = min(i0 + per, n);

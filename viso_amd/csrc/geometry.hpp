@@ -33,6 +33,8 @@ struct GeoCtl {
     int pad;
 };
 
+static_assert(sizeof(GeoCtl) % 8 == 0, "GeoCtl is mirrored in 8-byte words");
+
 struct GeoArgs {
     const int* n_dev;  // tracked point count (device)
     const float2* kp1;
@@ -46,6 +48,10 @@ struct GeoArgs {
     double* q1;  // cap x 2 (float-rounded)
     double* q2;
     GeoCtl* ctl;
+    // optional: the control block mirrored into pinned host memory (device
+    // address) by the gate and by SelectMotion's last launch, for the host
+    // to read after its stream sync without a copy launch
+    GeoCtl* host_ctl;
     double disparity_thresh;
     double proj_thresh;
     double parallax_thresh;

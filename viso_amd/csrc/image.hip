@@ -452,6 +452,7 @@ constexpr size_t kPfLdsMax = (size_t)160 * 1024 / (kPfSlots / 256);  // the CU's
 static_assert(kPfSlots % 256 == 0 && kPfSlots <= 1024, "pyramid tail: 1..4 workgroups per CU");
 
 typedef uint32_t pf_u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kPfOwnPer = 4;  // PyrOwn level-0 chunks per thread (16 bytes each)
 
 struct PyrTailArgs {
     uint8_t* slot[kPyrBatch];
@@ -460,6 +461,11 @@ struct PyrTailArgs {
     int n, nb, band, xcd_map;  // images, bands per image, level-3 rows per band, XCD map
     int s1, s2;                // LDS row strides of staged levels 1 / 2
     int lds1;                  // byte offset of the level-1 rows (level 2 below it)
+    // PyrOwn (kernels.hpp) for image own_img: own_len level-0 bytes from
+    // own_src into its slot (own_src null: none), its identity pose
+    const uint8_t* own_src;
+    double* ident_pose;
+    int own_img, own_len;
 };
 
 // own rows [o?a, o?b) and computed rows [c?a, c?b) of band b per level
@@ -581,6 +587,27 @@ __global__ __launch_bounds__(kPfThreads) void pyr_tail_kernel(PyrTailArgs a) {
     uint8_t* lds1 = s_pf + a.lds1;
     uint8_t* lds2 = s_pf;
     const int tid = (int)threadIdx.x;
+    // ---- PyrOwn: the identity pose; the image's bands split its level-0
+    // copy in 16-byte chunks (the source possibly unaligned: a caller's frame
+    // at f * w * h), at most kPfOwnPer per thread (the launcher's limit),
+    // loaded ahead of phase 1's loads and stored behind them, so that the
+    // two latencies overlap
+    if (img == a.own_img && a.ident_pose && band == 0 && tid < 12)
+        a.ident_pose[tid] = (tid == 0 || tid == 4 || tid == 8) ? 1.0 : 0.0;
+    const bool own_copy = img == a.own_img && a.own_src;
+    const int own_c16 = a.own_len >> 4;
+    const int own_lo = own_copy ? (int)((long long)own_c16 * band / a.nb) : 0;
+    const int own_hi = own_copy ? (int)((long long)own_c16 * (band + 1) / a.nb) : 0;
+    pf_u32x4 oq[kPfOwnPer];
+    if (own_copy) {
+#pragma unroll
+        for (int j = 0; j < kPfOwnPer; ++j) {
+            const int k = own_lo + tid + j * kPfThreads;
+            if (k < own_hi)
+                oq[j] = *reinterpret_cast<const __attribute__((address_space(1))) pf_u32x4*>(
+                    reinterpret_cast<uintptr_t>(a.own_src + 16 * (size_t)k));
+        }
+    }
     // ---- phase 1: level-1 rows [c1a, c1b) from HBM (a chunk past a row end
     // reads into the next row or level 2 of the slot)
     {
@@ -594,6 +621,18 @@ __global__ __launch_bounds__(kPfThreads) void pyr_tail_kernel(PyrTailArgs a) {
             if (i < rows)
                 q[k] = *reinterpret_cast<const __attribute__((address_space(1))) pf_u32x4*>(
                     reinterpret_cast<uintptr_t>(l1 + (size_t)(r.c1a + i) * a.w1 + 16 * c));
+        }
+        if (own_copy) {
+            uint8_t* dst = a.slot[img];
+#pragma unroll
+            for (int j = 0; j < kPfOwnPer; ++j) {
+                const int k = own_lo + tid + j * kPfThreads;
+                if (k < own_hi)
+                    *reinterpret_cast<__attribute__((address_space(1))) pf_u32x4*>(
+                        reinterpret_cast<uintptr_t>(dst + 16 * (size_t)k)) = oq[j];
+            }
+            if (band == a.nb - 1)
+                for (int i = 16 * own_c16 + tid; i < a.own_len; i += kPfThreads) dst[i] = a.own_src[i];
         }
 #pragma unroll
         for (int k = 0; k < kPfStage1; ++k)
@@ -873,7 +912,8 @@ __global__ __launch_bounds__(256) void fast_order_kernel(int h, int ntx, int nty
                                                          const int* __restrict__ tot,
                                                          const int* __restrict__ lst, int cap,
                                                          float2* __restrict__ kp_out,
-                                                         int4* __restrict__ raw_out, int* __restrict__ n_out) {
+                                                         int4* __restrict__ raw_out, int* __restrict__ n_out,
+                                                         float2* __restrict__ kp_copy, int* host_n, int cap_n) {
     __shared__ int s_off[kFtRows * kFtMaxTx + 1];
     __shared__ int s_w[4], s_b[4];
     const int ty = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = wave_id();
@@ -925,10 +965,17 @@ __global__ __launch_bounds__(256) void fast_order_kernel(int h, int ntx, int nty
             const int v = lst[((size_t)y * ntx + tx) * kFtCap + (i - s_off[lo])];
             const int x = v & 0xffff, sc = v >> 16;
             if (kp_out) kp_out[o] = make_float2((float)x, (float)y);
+            if (kp_copy) kp_copy[o] = make_float2((float)x, (float)y);
             if (raw_out) raw_out[o] = make_int4(x, y, sc, 0);
         }
     }
-    if (ty == nty - 1 && t == 0) *n_out = base + total;
+    if (ty == nty - 1 && t == 0) {
+        const int n = cap_n ? min(base + total, cap) : base + total;
+        *n_out = n;
+        // the pinned host copy: a system-scope store, visible to the host
+        // once the launch has completed (FastDetect)
+        if (host_n) __hip_atomic_store(host_n, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // Tail-launch plan for n images of a geometry; false (level 1 narrower than
@@ -1016,21 +1063,40 @@ void launch_pyr_level(const PyrGeom& g, int l, const uint8_t* const* l0, uint8_t
 }  // namespace
 
 void launch_pyramid_frames(const PyrGeom& g, const uint8_t* const* l0, uint8_t* const* slot,
-                           int n, hipStream_t stream) {
+                           int n, hipStream_t stream, PyrOwn* own) {
+    const size_t len0 = (size_t)g.w[0] * g.h[0];
     for (int b0 = 0; b0 < n; b0 += kPyrBatch) {
         const int nb = (n - b0) < kPyrBatch ? (n - b0) : kPyrBatch;
+        // this launch's image of `own`, or -1
+        const int oi = own && own->img >= b0 && own->img < b0 + nb ? own->img - b0 : -1;
+        bool copy = oi >= 0 && l0[b0 + oi] != slot[b0 + oi];
         launch_pyr_level(g, 1, l0 + b0, slot + b0, nb, stream);
         PyrTailArgs ta;
         size_t lds = 0;
         if (pf_plan(g, nb, ta, lds)) {
+            // the copy fits the image's bands' chunk slots (small batches:
+            // many bands per image), else it stays the caller's
+            copy = copy && (len0 >> 4) <= (size_t)ta.nb * kPfThreads * kPfOwnPer;
+            if (oi >= 0) own->copied = copy;
             for (int i = 0; i < nb; ++i) ta.slot[i] = slot[b0 + i];
             ta.n = nb;
             ta.xcd_map = nb >= 8;
+            ta.own_img = oi;
+            ta.own_src = copy ? l0[b0 + oi] : nullptr;
+            ta.own_len = (int)len0;
+            ta.ident_pose = oi >= 0 ? own->ident_pose : nullptr;
             const int grid = ta.xcd_map ? 8 * ta.nb * ((nb + 7) / 8) : ta.nb * nb;
             pyr_tail_kernel<<<grid, kPfThreads, lds, stream>>>(ta);
         } else {
             launch_pyr_level(g, 2, l0 + b0, slot + b0, nb, stream);
             launch_pyr_level(g, 3, l0 + b0, slot + b0, nb, stream);
+            if (oi >= 0 && own->ident_pose) {
+                const double ident[12] = {1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0};
+                launch_set_pose(own->ident_pose, ident, stream);
+            }
+            if (copy)
+                (void)hipMemcpyAsync(slot[b0 + oi], l0[b0 + oi], len0, hipMemcpyDeviceToDevice, stream);
+            if (oi >= 0) own->copied = copy;
         }
     }
 }
@@ -1070,12 +1136,14 @@ FastScratch fast_scratch_at(void* base, int w, int h) {
 }
 
 void launch_fast(const uint8_t* img, int w, int h, int thresh, FastScratch& s, float2* kp_out,
-                 int4* raw_out, int cap, int* n_out, hipStream_t stream) {
+                 int4* raw_out, int cap, int* n_out, hipStream_t stream, const FastDetect* det) {
     int ntx, nty;
     fast_dims(w, h, &ntx, &nty);
     thresh = thresh < 0 ? 0 : (thresh > 255 ? 255 : thresh);
     fast_tile_kernel<<<dim3(ntx, nty), 256, 0, stream>>>(img, w, h, thresh, ntx, s.cnt, s.tot, s.lst);
-    fast_order_kernel<<<nty, 256, 0, stream>>>(h, ntx, nty, s.cnt, s.tot, s.lst, cap, kp_out, raw_out, n_out);
+    fast_order_kernel<<<nty, 256, 0, stream>>>(h, ntx, nty, s.cnt, s.tot, s.lst, cap, kp_out, raw_out, n_out,
+                                               det ? det->kp_copy : nullptr, det ? det->host_n : nullptr,
+                                               det ? 1 : 0);
 }
 
 }  // namespace viso

@@ -15,8 +15,18 @@ void launch_pyramid(const PyrGeom& g, uint8_t* base, int n_images, size_t img_st
 // 1..3 go to slot[i] + g.off[l] (n <= kPyrBatch per launch; more are split).
 constexpr int kPyrBatch = 128;
 // Two launches: level 1 (streaming bands), levels 2-3 (pyr_tail_kernel).
+// own (optional): for frame img, its level 0 copied from l0[img] into
+// slot[img] (when they differ and the batch is small enough: copied says
+// whether it was) and, when ident_pose is set, the identity pose written
+// there — done by the tail launch (a frame-by-frame caller's copy and pose
+// launches folded into it).
+struct PyrOwn {
+    int img;
+    double* ident_pose;
+    bool copied;
+};
 void launch_pyramid_frames(const PyrGeom& g, const uint8_t* const* l0, uint8_t* const* slot,
-                           int n, hipStream_t stream);
+                           int n, hipStream_t stream, PyrOwn* own = nullptr);
 
 // FAST device scratch (image.hip): per (row, tile) keypoint counts and
 // slots, per-tile totals; carved from fast_scratch_bytes(w, h) bytes.
@@ -29,8 +39,15 @@ size_t fast_scratch_bytes(int w, int h);
 FastScratch fast_scratch_at(void* base, int w, int h);
 // FAST + NMS on a level-0 image; writes up to cap keypoints (float2 and/or
 // raw int4 {x, y, score, 0}) and the total count to *n_out (device).
+// det (a re-detection frame, src/viso.cpp:100-108): the count is stored
+// capped at cap, the keypoints also go to kp_copy (kp2 = kp1) and the capped
+// count also to host_n (pinned host memory, device-mapped; may be null).
+struct FastDetect {
+    float2* kp_copy;
+    int* host_n;
+};
 void launch_fast(const uint8_t* img, int w, int h, int thresh, FastScratch& s, float2* kp_out,
-                 int4* raw_out, int cap, int* n_out, hipStream_t stream);
+                 int4* raw_out, int cap, int* n_out, hipStream_t stream, const FastDetect* det = nullptr);
 
 // ---------------------------------------------------------------- tracking
 // OpticalFlowMultiLevel(inverse=true): kp2 in/out, success out (level 0).
@@ -39,9 +56,6 @@ void launch_klt(const FrameDev& ref, const FrameDev& cur, const PyrGeom& g, cons
 // the same with the track count in device memory (*n_dev, capped at cap)
 void launch_klt_dev(const FrameDev& ref, const FrameDev& cur, const PyrGeom& g, const float2* kp1,
                     float2* kp2, uint8_t* success, const int* n_dev, int cap, double thresh, hipStream_t stream);
-// a re-detection frame's FAST count capped at cap and kp2 = kp1 over it, on
-// the device
-void launch_detect_finish(int* n_dev, int cap, const float2* kp1, float2* kp2, hipStream_t stream);
 // Order-preserving erase of failed tracks (src/viso.cpp:23-40):
 // kp1/kp2[0..n) with success -> out arrays; *n_out = survivors.  n < 0:
 // the count is *n_out's input value, capped at -n.

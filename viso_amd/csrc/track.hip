@@ -1161,21 +1161,7 @@ __global__ __launch_bounds__(1024) void compact_tracks_kernel(const float2* __re
     if (t == 1023) *n_out = off;
 }
 
-// After FAST on a re-detection frame (src/viso.cpp:100-108): the corner
-// count capped at cap, and kp2 = kp1 over it, on the device (no host read).
-__global__ __launch_bounds__(256) void detect_finish_kernel(int* __restrict__ n_dev, int cap,
-                                                             const float2* __restrict__ kp1,
-                                                             float2* __restrict__ kp2) {
-    const int n = min(*n_dev, cap);
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) kp2[i] = kp1[i];
-    if (blockIdx.x == 0 && threadIdx.x == 0) *n_dev = n;  // idempotent: every reader caps alike
-}
-
 }  // namespace
-
-void launch_detect_finish(int* n_dev, int cap, const float2* kp1, float2* kp2, hipStream_t stream) {
-    detect_finish_kernel<<<std::max(1, std::min((cap + 255) / 256, 64)), 256, 0, stream>>>(n_dev, cap, kp1, kp2);
-}
 
 void launch_compact_tracks(const float2* kp1, const float2* kp2, const uint8_t* success, int n,
                            float2* kp1_out, float2* kp2_out, int* n_out, hipStream_t stream) {
