@@ -145,6 +145,12 @@ struct viso_ctx {
     int n_track = 0;             // < 0: on the device only (ntrack_pending)
     bool ntrack_pending = false;  // a re-detection frame's count not read yet
     hipEvent_t ntrack_evt = nullptr;  // behind the FAST frame's count store into h_int[3]
+    hipEvent_t gate_evt = nullptr;    // behind the 2D-2D gate (the host waits for it alone)
+    // the last 2D-2D gate read: its frame count since the reference frame
+    // (0: none since the last re-detection), open or not, its disparity
+    int gate_cnt = 0;
+    bool gate_open = false;
+    double gate_disp = 0.0;
     int resolve_ntrack();
     bool success_valid = false;
     int frame_cnt = 0;
@@ -192,7 +198,7 @@ struct viso_ctx {
     hipStream_t lk_stream = nullptr;
     hipEvent_t lk_ring[viso::kLkRing] = {};  // recorded after each lk_stream batch
     viso::HostStage stage;  // pinned staging of host-ingested frames (ingest_host)
-    // PoseEstimation2d2d's H path runs on lk_stream beside the E path (no LK
+    // PoseEstimation2d2d's E path runs on lk_stream beside the H path (no LK
     // alignment runs while initialising): fork / join events
     hipEvent_t geo_fork = nullptr, geo_join = nullptr;
     int64_t lk_seq = 0;                      // lk_stream batches launched

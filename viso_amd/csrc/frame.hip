@@ -162,6 +162,7 @@ int viso_ctx::init() {
     VISO_HIP_CHECK(hipEventCreateWithFlags(&geo_fork, hipEventDisableTiming));
     VISO_HIP_CHECK(hipEventCreateWithFlags(&geo_join, hipEventDisableTiming));
     VISO_HIP_CHECK(hipEventCreateWithFlags(&ntrack_evt, hipEventDisableTiming));
+    VISO_HIP_CHECK(hipEventCreateWithFlags(&gate_evt, hipEventDisableTiming));
     rc = bg_prepare();
     if (rc) return rc;
     // the pose getter's pinned staging (viso_get_poses)
@@ -181,7 +182,7 @@ void viso_ctx::release() {
     }
     if (bg_done) (void)hipEventDestroy(bg_done);
     bg_done = nullptr;
-    for (hipEvent_t* e : {&geo_fork, &geo_join, &ntrack_evt}) {
+    for (hipEvent_t* e : {&geo_fork, &geo_join, &ntrack_evt, &gate_evt}) {
         if (*e) (void)hipEventDestroy(*e);
         *e = nullptr;
     }
@@ -797,16 +798,41 @@ int viso_ctx::on_new_frame(int cur) {
                     launch_pose_2d2d_gate(geo, stream);
                 }
                 VISO_HIP_CHECK(hipGetLastError());
-                // (the gate mirrors the control block into h_ctl itself)
-                VISO_HIP_CHECK(hipStreamSynchronize(stream));
+                // the gate mirrors the control block into h_ctl itself.  When
+                // it is likely open, the H hypotheses go behind it before it
+                // is read (a closed gate returns them at once), so the host's
+                // round trip overlaps them: likely = the last frame's gate
+                // was open, or its disparity extrapolated to this frame (it
+                // grows about with the square of the frames since the
+                // reference one) comes within 25 % of the threshold.  A wrong
+                // guess costs time only (a no-op launch, or the round trip)
+                const int k = frame_cnt;
+                const bool spec = gate_cnt > 0 && gate_cnt == k - 1 &&
+                                  (gate_open || gate_disp * ((double)k * k) / ((double)(k - 1) * (k - 1)) * 1.25 >=
+                                                    p.disparity_squared_thresh);
+                if (spec) {
+                    VISO_HIP_CHECK(hipEventRecord(gate_evt, stream));
+                    {
+                        TimedRegion t(timing, VISO_KERNEL_RANSAC, stream);
+                        launch_pose_2d2d_spec(geo, stream);
+                    }
+                    VISO_HIP_CHECK(hipGetLastError());
+                    VISO_HIP_CHECK(hipEventSynchronize(gate_evt));
+                } else {
+                    VISO_HIP_CHECK(hipStreamSynchronize(stream));
+                }
+                gate_cnt = k;
+                gate_open = h_ctl->gate != 0;
+                gate_disp = h_ctl->disparity;
                 if (h_ctl->gate) {
                     hipStream_t bs = stream;
                     {
                         TimedRegion t(timing, VISO_KERNEL_RANSAC, stream);
-                        // the H chain and SelectMotion on lk_stream beside the E chain (the
-                        // gate's read above left both streams idle); the result is read
-                        // on the stream SelectMotion ran on
-                        bs = launch_pose_2d2d_body(geo, stream, lk_stream, geo_fork, geo_join);
+                        // the E and H chains on the two streams (lk_stream is
+                        // idle: nothing of this frame was enqueued there), the
+                        // H chain behind its speculative launch; the result is
+                        // read on the stream SelectMotion ran on
+                        bs = launch_pose_2d2d_body(geo, stream, lk_stream, geo_fork, geo_join, spec);
                     }
                     VISO_HIP_CHECK(hipGetLastError());
                     // (SelectMotion's last launch mirrors the block into h_ctl)
@@ -874,6 +900,7 @@ int viso_ctx::on_new_frame(int cur) {
                 VISO_HIP_CHECK(hipEventRecord(ntrack_evt, stream));
                 n_track = -1;
                 ntrack_pending = true;
+                gate_cnt = 0;
                 success_valid = false;
                 set_role(ref_slot, cur);
                 frame_cnt = 0;

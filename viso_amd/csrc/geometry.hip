@@ -1017,11 +1017,16 @@ __global__ __launch_bounds__(256) void select_points_kernel(GeoArgs a) {
 // normalised inlier points in index order: thread t owns the contiguous
 // flags [t per, (t + 1) per), so one exclusive scan of the per-thread counts
 // places every point (round 4: one launch per step and three block barriers
-// per 256 flags, 31 us for ~2,000 tracks).
-__global__ __launch_bounds__(256) void select_finish_kernel(GeoArgs a) {
-    __shared__ double s_red[4];
-    __shared__ int s_cnt[4][kMaxCandidates];
-    __shared__ int s_wave[4];
+// per 256 flags, 31 us for ~2,000 tracks).  1,024 threads: each thread's
+// serial share of flags, depth leaves and outputs (dependent global loads,
+// one latency each) is a quarter of a 256-thread block's.
+constexpr int kSelThreads = 1024;
+constexpr int kSelWaves = kSelThreads / 64;
+
+__global__ __launch_bounds__(kSelThreads) void select_finish_kernel(GeoArgs a) {
+    __shared__ double s_red[kSelWaves];
+    __shared__ int s_cnt[kSelWaves][kMaxCandidates];
+    __shared__ int s_wave[kSelWaves];
     __shared__ int s_best, s_bestn;
     GeoCtl* c = a.ctl;
     if (!c->gate) return;
@@ -1030,7 +1035,7 @@ __global__ __launch_bounds__(256) void select_finish_kernel(GeoArgs a) {
     int cnt[kMaxCandidates];
 #pragma unroll
     for (int k = 0; k < kMaxCandidates; ++k) cnt[k] = 0;
-    for (int i = t; i < n; i += 256)
+    for (int i = t; i < n; i += kSelThreads)
 #pragma unroll
         for (int k = 0; k < kMaxCandidates; ++k)
             if (k < m) cnt[k] += a.sel_in[(size_t)k * a.cap + i];
@@ -1043,7 +1048,8 @@ __global__ __launch_bounds__(256) void select_finish_kernel(GeoArgs a) {
     if (t == 0) {
         int best = -1, bestn = 0;
         for (int k = 0; k < m; ++k) {
-            const int tot = (s_cnt[0][k] + s_cnt[1][k]) + (s_cnt[2][k] + s_cnt[3][k]);
+            int tot = 0;
+            for (int w = 0; w < kSelWaves; ++w) tot += s_cnt[w][k];
             if (tot > bestn) {  // strict: the first maximum wins (src/viso.cpp:605)
                 bestn = tot;
                 best = k;
@@ -1058,7 +1064,12 @@ __global__ __launch_bounds__(256) void select_finish_kernel(GeoArgs a) {
     if (best >= 0) {
         const uint8_t* inl = a.sel_in + (size_t)best * a.cap;
         const double* pts = a.sel_pts + (size_t)best * a.cap * 3;
-        mean = block_tree_sum(n, [&](int i) { return inl[i] ? pts[3 * i + 2] : 0.0; }, s_red);
+        // (both loads issued together: the depth's load does not wait for
+        // the flag's)
+        mean = block_tree_sum<kSelThreads>(n, [&](int i) {
+            const double z = pts[3 * i + 2];
+            return inl[i] ? z : 0.0;
+        }, s_red);
     }
     // every thread derives the ctl values it needs from the same operations
     const bool nonzero = mean != 0;
@@ -1079,7 +1090,7 @@ __global__ __launch_bounds__(256) void select_finish_kernel(GeoArgs a) {
     __syncthreads();
     ctl_mirror(a);
     // output: flags, and the inlier points in order
-    const int per = (n + 255) / 256;
+    const int per = (n + kSelThreads - 1) / kSelThreads;
     const int i0 = min(t * per, n), i1 = min(i0 + per, n);
     const uint8_t* inl = a.sel_in + (size_t)(best >= 0 ? best : 0) * a.cap;
     int own = 0;
@@ -1122,16 +1133,23 @@ void launch_pose_2d2d_gate(const GeoArgs& a, hipStream_t stream) {
     normalize_kernel<<<1, kNormThreads, 0, stream>>>(a);
 }
 
+void launch_pose_2d2d_spec(const GeoArgs& a, hipStream_t stream) {
+    if (a.h_iters > 0) h_hyp_kernel<<<(a.h_iters + 3) / 4, 256, 0, stream>>>(a);
+}
+
 hipStream_t launch_pose_2d2d_body(const GeoArgs& a, hipStream_t stream, hipStream_t hs, hipEvent_t e_done,
-                                  hipEvent_t join) {
+                                  hipEvent_t join, bool h_spec) {
     const bool split = hs && e_done && join && a.h_iters > 0 && a.e_iters > 0;
-    const hipStream_t sh = split ? hs : stream;
-    // the H chain (the longer one) and the E chain, interleaved launch by
-    // launch so that neither waits for the other's host-side enqueue
+    // the H chain (the longer one) on `stream` behind its speculative first
+    // launch (h_spec) and the E chain on hs, or the H chain on hs
+    const hipStream_t sh = h_spec ? stream : (split ? hs : stream);
+    const hipStream_t se = h_spec ? (split ? hs : stream) : stream;
+    // the two chains interleaved launch by launch so that neither waits for
+    // the other's host-side enqueue
     for (int step = 0; step < 6; ++step) {
         if (a.h_iters > 0) {
             switch (step) {
-                case 0: h_hyp_kernel<<<(a.h_iters + 3) / 4, 256, 0, sh>>>(a); break;
+                case 0: if (!h_spec) h_hyp_kernel<<<(a.h_iters + 3) / 4, 256, 0, sh>>>(a); break;
                 case 1: score_kernel<false><<<a.h_iters, 256, 0, sh>>>(a); break;
                 case 2: scan_kernel<false><<<1, 256, 0, sh>>>(a); break;
                 case 3: h_moment_leaves_kernel<<<(a.cap + 255) / 256, 256, 0, sh>>>(a); break;
@@ -1141,23 +1159,24 @@ hipStream_t launch_pose_2d2d_body(const GeoArgs& a, hipStream_t stream, hipStrea
         }
         if (a.e_iters > 0) {
             switch (step) {
-                case 0: e_hyp_kernel<<<(a.e_iters + 3) / 4, 256, 0, stream>>>(a); break;
-                case 1: score_kernel<true><<<a.e_iters, 256, 0, stream>>>(a); break;
-                case 2: scan_kernel<true><<<1, 256, 0, stream>>>(a); break;
-                case 3: recover_setup_kernel<<<1, 64, 0, stream>>>(a); break;
-                case 4: recover_count_kernel<<<(4 * a.cap + 255) / 256, 256, 0, stream>>>(a); break;
-                default: recover_pick_kernel<<<1, 64, 0, stream>>>(a); break;
+                case 0: e_hyp_kernel<<<(a.e_iters + 3) / 4, 256, 0, se>>>(a); break;
+                case 1: score_kernel<true><<<a.e_iters, 256, 0, se>>>(a); break;
+                case 2: scan_kernel<true><<<1, 256, 0, se>>>(a); break;
+                case 3: recover_setup_kernel<<<1, 64, 0, se>>>(a); break;
+                case 4: recover_count_kernel<<<(4 * a.cap + 255) / 256, 256, 0, se>>>(a); break;
+                default: recover_pick_kernel<<<1, 64, 0, se>>>(a); break;
             }
         }
     }
+    // SelectMotion behind the H chain, once the E chain's event has passed
     if (split) {
-        (void)hipEventRecord(e_done, stream);
+        (void)hipEventRecord(e_done, se);
         (void)hipStreamWaitEvent(sh, e_done, 0);
     }
     const int total = 5 * a.cap;
     select_points_kernel<<<(total + 255) / 256, 256, 0, sh>>>(a);
-    select_finish_kernel<<<1, 256, 0, sh>>>(a);
-    if (split) {
+    select_finish_kernel<<<1, kSelThreads, 0, sh>>>(a);
+    if (split && sh != stream) {
         (void)hipEventRecord(join, sh);
         (void)hipStreamWaitEvent(stream, join, 0);
     }

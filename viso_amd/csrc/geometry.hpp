@@ -89,13 +89,19 @@ void launch_pose_2d2d(const GeoArgs& a, hipStream_t stream, Timing* timing);
 // returns at once when the gate is closed; a caller that has read the gate
 // on the host may skip the body.
 void launch_pose_2d2d_gate(const GeoArgs& a, hipStream_t stream);
-// hs (optional): a second stream for the H path.  The caller has
-// synchronised `stream` behind the gate (both streams see its results); the
-// E and H chains are enqueued interleaved, SelectMotion runs on hs behind
-// the H chain once the E chain's event `e_done` is passed, and `join` (on
-// hs, behind SelectMotion) is waited for by `stream`.  Returns the stream
-// SelectMotion ran on (read the result there).
+// The H chain's first launch (the hypotheses), enqueued on `stream` behind
+// the gate before the host has read it: a closed gate makes it return at
+// once, an open one lets the host's round trip on the gate overlap it.
+void launch_pose_2d2d_spec(const GeoArgs& a, hipStream_t stream);
+// hs (optional): a second stream.  The host has seen the gate's result (both
+// streams may read it); the E and H chains are enqueued interleaved, the
+// longer H chain on `stream` behind launch_pose_2d2d_spec's launch (h_spec)
+// and the E chain on hs — or, without h_spec, the H chain on hs and the E
+// chain on `stream`; SelectMotion runs behind the H chain once the E chain's
+// event `e_done` has passed, and when that is hs, `join` (behind
+// SelectMotion) is waited for by `stream`.  Returns the stream SelectMotion
+// ran on (read the result there).
 hipStream_t launch_pose_2d2d_body(const GeoArgs& a, hipStream_t stream, hipStream_t hs = nullptr,
-                                  hipEvent_t e_done = nullptr, hipEvent_t join = nullptr);
+                                  hipEvent_t e_done = nullptr, hipEvent_t join = nullptr, bool h_spec = false);
 
 }  // namespace viso

@@ -354,15 +354,19 @@ __device__ inline void triangulate_h(const double* R, const double* T, double x1
     null_vector_jacobi<4>(A, X);
 }
 
-// Block-wide (256 threads) canonical pairwise tree over n leaves: leaf(i)
-// for i < n, +0.0 beyond.  Each thread reduces an aligned chunk of
-// C = max(1, P/256) leaves with the binary-counter form of the same tree,
-// then lanes and waves combine in index order.  Result valid in thread 0.
-template <class F>
-__device__ inline double block_tree_sum(int n, F leaf, double* s_red4) {
+// Block-wide (T threads, a power of two >= 64) canonical pairwise tree over
+// n leaves: leaf(i) for i < n, +0.0 beyond.  Each thread reduces an aligned
+// chunk of C = max(1, P/T) leaves with the binary-counter form of the same
+// tree, then lanes and the T/64 waves combine pairwise in index order — the
+// same tree for any T (padding leaves are +0.0: exact).  s_red holds T/64
+// doubles.  Result valid in every thread.
+template <int T = 256, class F>
+__device__ inline double block_tree_sum(int n, F leaf, double* s_red) {
+    static_assert(T >= 64 && (T & (T - 1)) == 0, "block_tree_sum: power-of-two block");
+    constexpr int W = T / 64;
     int P = 1;
     while (P < n) P <<= 1;
-    const int C = P > 256 ? P / 256 : 1;
+    const int C = P > T ? P / T : 1;
     const int t = threadIdx.x;
     double stack[16];
     int sp = 0;
@@ -376,11 +380,17 @@ __device__ inline double block_tree_sum(int n, F leaf, double* s_red4) {
     v = wave_tree_sum(v);
     const int wave = t >> 6;
     __syncthreads();
-    if ((t & 63) == 0) s_red4[wave] = v;
+    if ((t & 63) == 0) s_red[wave] = v;
     __syncthreads();
-    const double r = (s_red4[0] + s_red4[1]) + (s_red4[2] + s_red4[3]);
+    double l[W];
+#pragma unroll
+    for (int k = 0; k < W; ++k) l[k] = s_red[k];
+#pragma unroll
+    for (int w = W; w > 1; w >>= 1)
+#pragma unroll
+        for (int k = 0; k < w / 2; ++k) l[k] = l[2 * k] + l[2 * k + 1];
     __syncthreads();
-    return r;
+    return l[0];
 }
 
 }  // namespace viso
