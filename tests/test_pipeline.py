@@ -138,6 +138,36 @@ def test_gpu_sequence_parity_frame_by_frame():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["0", "1"])
+def test_gpu_init_gate_speculation_paths_agree(mode, monkeypatch):
+    """The initialisation's 2D-2D gate read (frame.hip): the H hypotheses
+    launched behind the gate before the host reads it (H chain on the context
+    stream, E chain on lk_stream) or after it (H chain on lk_stream) — forced
+    never (0) / always (1) against the default prediction, which takes both
+    paths on this sequence: every frame's counts, the tracks, the map and the
+    poses bit for bit."""
+    import viso_amd
+    seq = seqdata.sequence(0)
+    n = d_init_frame() + 3
+
+    def run():
+        v = viso_amd.Viso(*seq.K, width=W, height=H, enable_tracking=1)
+        rows = []
+        for f in range(n):
+            v.OnNewFrame(seqdata.image(f))
+            st = v.stats()
+            rows.append((v.state, st[1], st[2], st[3], st[4], st[8], st[12]))
+        return rows, v.GetPoints(), v.poses
+
+    ref = run()
+    monkeypatch.setenv("VISO_GATE_SPEC", mode)
+    got = run()
+    assert got[0] == ref[0]
+    assert np.array_equal(got[1], ref[1]) and len(ref[1]) > 0
+    assert np.array_equal(got[2], ref[2]) and len(ref[2]) > 0
+
+
+@pytest.mark.gpu
 def test_gpu_as_shipped_mode():
     seq, gv, ov = _run_pair(0, enable_tracking=0)
     for f in range(d_init_frame() + 3):

@@ -151,6 +151,7 @@ struct viso_ctx {
     int gate_cnt = 0;
     bool gate_open = false;
     double gate_disp = 0.0;
+    int gate_spec_mode = -1;  // VISO_GATE_SPEC (tests): 0 never, 1 always, -1 predicted
     int resolve_ntrack();
     bool success_valid = false;
     int frame_cnt = 0;

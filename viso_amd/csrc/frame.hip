@@ -163,6 +163,7 @@ int viso_ctx::init() {
     VISO_HIP_CHECK(hipEventCreateWithFlags(&geo_join, hipEventDisableTiming));
     VISO_HIP_CHECK(hipEventCreateWithFlags(&ntrack_evt, hipEventDisableTiming));
     VISO_HIP_CHECK(hipEventCreateWithFlags(&gate_evt, hipEventDisableTiming));
+    if (const char* e = getenv("VISO_GATE_SPEC")) gate_spec_mode = e[0] == '1' ? 1 : 0;
     rc = bg_prepare();
     if (rc) return rc;
     // the pose getter's pinned staging (viso_get_poses)
@@ -806,10 +807,15 @@ int viso_ctx::on_new_frame(int cur) {
                 // grows about with the square of the frames since the
                 // reference one) comes within 25 % of the threshold.  A wrong
                 // guess costs time only (a no-op launch, or the round trip)
+                // (VISO_GATE_SPEC=0 / 1: never / always, for the tests of
+                // the three paths)
                 const int k = frame_cnt;
-                const bool spec = gate_cnt > 0 && gate_cnt == k - 1 &&
-                                  (gate_open || gate_disp * ((double)k * k) / ((double)(k - 1) * (k - 1)) * 1.25 >=
-                                                    p.disparity_squared_thresh);
+                const bool spec = gate_spec_mode >= 0
+                                      ? gate_spec_mode == 1
+                                      : gate_cnt > 0 && gate_cnt == k - 1 &&
+                                            (gate_open || gate_disp * ((double)k * k) / ((double)(k - 1) * (k - 1)) *
+                                                                  1.25 >=
+                                                              p.disparity_squared_thresh);
                 if (spec) {
                     VISO_HIP_CHECK(hipEventRecord(gate_evt, stream));
                     {
