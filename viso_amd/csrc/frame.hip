@@ -548,7 +548,8 @@ int viso_ctx::bg_check() {
     bg_unchecked = false;
     if (w[0] || w[1]) VISO_HIP_CHECK(hipMemsetAsync(bg_args.bg_err, 0, 2 * sizeof(int), stream));
     if (getenv("VISO_LK_BG_STATS"))  // dev: how much of the last chunk the drain carried
-        fprintf(stderr, "viso lk-bg: %d frames x %d points, drain ran %d items, error %d\n", bg_nb, n_map, w[1], w[0]);
+        fprintf(stderr, "viso lk-bg: %d frames x %d points, drain ran %d items (builds with VISO_DRAIN_COUNT), error %d\n",
+                bg_nb, n_map, w[1], w[0]);
     return w[0] ? VISO_ERR_HIP : VISO_OK;
 }
 

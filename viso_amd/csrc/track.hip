@@ -1115,7 +1115,11 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
             if (pend_head >= 0 && !give_back(pend_head, pend_k)) (void)run_item(pend_head, pend_k);
             return;
         }
-        if (a.bg_drain && lane == 0) atomicAdd(a.bg_err + 1, 1);  // items the drain ran (stats)
+#ifdef VISO_DRAIN_COUNT
+        // (dev) items the drain ran: one same-address atomic per item, ~1,500
+        // of them queued on one L2 channel in the chunk's tail
+        if (a.bg_drain && lane == 0) atomicAdd(a.bg_err + 1, 1);
+#endif
 #ifdef VISO_PROBE
         ++pr_items;
 #endif
