@@ -136,7 +136,8 @@ struct viso_ctx {
     int ident_slot = -1;  // the ingest's pyramid wrote this frame's Keyframe-ctor pose (PyrOwn)
     // the ingest's pyramid launch(es) with its last frame's PyrOwn (level 0
     // owned, identity pose outside tracking)
-    void launch_ingest_pyramid(const uint8_t* const* l0, uint8_t* const* dst, const int* sl, int n);
+    void launch_ingest_pyramid(const uint8_t* const* l0, uint8_t* const* dst, const int* sl, int n,
+                               bool bg_words = false);
 
     // ---------------- initialisation tracks (Viso::Initialization, include/viso.h:33-41)
     viso::DevBuf kp1, kp2, kp1b, kp2b, track_success, n_track_dev;
@@ -272,7 +273,8 @@ struct viso_ctx {
     // pyramid when the context is tracking (frames of the chunk: their slots),
     // bg_end once the chunk's last pose is launched
     bool bg_eligible();
-    int bg_begin(const std::vector<int>& chunk);
+    // (zeroed: the chunk's pyramid launch cleared the words)
+    int bg_begin(const std::vector<int>& chunk, bool zeroed = false);
     int bg_end(bool drain = true);
     // the grid's buffer, event and kernel warm-up (context init)
     int bg_prepare();

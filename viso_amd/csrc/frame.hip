@@ -290,15 +290,26 @@ int viso_ctx::own_level0(int s) {
     return VISO_OK;
 }
 
+// ready flags [kLkBatch], eight heads on lines of their own, 32 spare words,
+// leftover list (cursor, count, ..., 4096 items); + 32 words past them: the
+// error word and the drain's item count, kept across chunks (sticky) until
+// bg_check reads and clears them
+static constexpr size_t kBgWords = kLkBatch + 8 * 32 + 32 + 32 + 4096;
+
 // The ingest's pyramid.  Its last frame is last_frame when the call ends, so
 // its level 0 would be copied into its slot at the end anyway (own_level0):
 // the tail launch copies it instead (small chunks; a large one's bands would
 // serialise the copy), and outside tracking also writes that
 // frame's Keyframe-ctor pose (R = I, T = 0; on_new_frame skips its launch) —
 // a frame-by-frame caller pays two launches fewer per frame.
-void viso_ctx::launch_ingest_pyramid(const uint8_t* const* l0, uint8_t* const* dst, const int* sl, int n) {
+void viso_ctx::launch_ingest_pyramid(const uint8_t* const* l0, uint8_t* const* dst, const int* sl, int n,
+                                     bool bg_words) {
     const int s = sl[n - 1];
     PyrOwn own{n - 1, state != VISO_STATE_RUNNING ? pose_of(s) : nullptr, false};
+    if (bg_words) {  // the chunk's background-LK words (bg_begin), cleared by the tail launch
+        own.zero = (int*)bg_buf.ptr;
+        own.n_zero = (int)kBgWords;
+    }
     ident_slot = own.ident_pose ? s : -1;
     {
         TimedRegion t(timing, VISO_KERNEL_PYRAMID, stream);
@@ -456,11 +467,6 @@ bool viso_ctx::bg_eligible() {
            kf_interval <= 0 && !dpend && lk_pending.empty();
 }
 
-// ready flags [kLkBatch], eight heads on lines of their own, 32 spare words,
-// leftover list (cursor, count, ..., 4096 items); + 32 words past them: the
-// error word and the drain's item count, kept across chunks (sticky) until
-// bg_check reads and clears them
-static constexpr size_t kBgWords = kLkBatch + 8 * 32 + 32 + 32 + 4096;
 
 int viso_ctx::bg_prepare() {
     VISO_HIP_CHECK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
@@ -481,7 +487,7 @@ int viso_ctx::bg_prepare() {
     return VISO_OK;
 }
 
-int viso_ctx::bg_begin(const std::vector<int>& chunk) {
+int viso_ctx::bg_begin(const std::vector<int>& chunk, bool zeroed) {
     const int nb = (int)chunk.size();
     if (!bg_eligible() || nb < 1 || nb > kLkBatch) return VISO_OK;
     const size_t bg_words = kBgWords;
@@ -507,13 +513,15 @@ int viso_ctx::bg_begin(const std::vector<int>& chunk) {
         const long us = strtol(idle, nullptr, 10);
         if (us > 0 && us < 1000000) a.bg_idle = (unsigned int)(us * 100);
     }
-    // flags, heads and leftovers cleared behind the chunk's pyramid; the grid
+    // flags, heads and leftovers cleared by the chunk's pyramid tail launch
+    // (zeroed; else a memset behind it — round 5 measured the memset's
+    // launch and gaps at ~10 us of the chunk's start); the grid
     // (on the side stream's own hardware queue, create_streams) starts behind
     // them.  The grid itself is launched once the chunk's first frame is
     // enqueued (bg_launch): its host-side cost (the cross-stream wait, the
     // launch on the masked queue, ~30 us) then overlaps that frame's chain
     // instead of holding the chain's first launch back.
-    VISO_HIP_CHECK(hipMemsetAsync(bg_buf.ptr, 0, sizeof(int) * bg_words, stream));
+    if (!zeroed) VISO_HIP_CHECK(hipMemsetAsync(bg_buf.ptr, 0, sizeof(int) * bg_words, stream));
     VISO_HIP_CHECK(hipEventRecord(bg_done, stream));
     bg_args = a;
     bg_active = true;
@@ -1078,13 +1086,16 @@ int viso_process_frames_device(viso_ctx* c, const uint8_t* d_left, const uint8_t
             l0.push_back(src);
             dst.push_back(c->slot_base(s));
         }
-        c->launch_ingest_pyramid(l0.data(), dst.data(), sl.data(), (int)l0.size());
+        // a background-LK chunk's words are cleared by the pyramid's tail
+        // launch (bg_begin then makes no memset launch)
+        const bool bg = c->bg_eligible() && nb <= kLkBatch;
+        c->launch_ingest_pyramid(l0.data(), dst.data(), sl.data(), (int)l0.size(), bg);
         VISO_HIP_CHECK(hipGetLastError());
         // (the background words' memset stays behind the pyramid: issued
         // ahead of it, the chain ran at half speed in 3 of 6 bench runs,
         // profiles/r05_bg_order_ab.log)
         {
-            const int rc = c->bg_begin(sl);
+            const int rc = c->bg_begin(sl, bg);
             if (rc) {
                 for (int s : sl) c->drop(s);
                 return rc;

@@ -466,6 +466,8 @@ struct PyrTailArgs {
     const uint8_t* own_src;
     double* ident_pose;
     int own_img, own_len;
+    int* zero;  // PyrOwn::zero, n_zero ints cleared by the grid's threads
+    int n_zero;
 };
 
 // own rows [o?a, o?b) and computed rows [c?a, c?b) of band b per level
@@ -575,6 +577,8 @@ __global__ __launch_bounds__(kPfThreads) void pyr_tail_kernel(PyrTailArgs a) {
         band = (int)blockIdx.x % a.nb;
         img = (int)blockIdx.x / a.nb;
     }
+    for (int i = (int)(blockIdx.x * kPfThreads + threadIdx.x); i < a.n_zero; i += (int)(gridDim.x * kPfThreads))
+        a.zero[i] = 0;
     if (img >= a.n) return;  // block-uniform, before any barrier
 #ifdef VISO_PROBE
     const unsigned long long pr_t0 = __builtin_amdgcn_s_memrealtime();
@@ -1085,6 +1089,9 @@ void launch_pyramid_frames(const PyrGeom& g, const uint8_t* const* l0, uint8_t* 
             ta.own_src = copy ? l0[b0 + oi] : nullptr;
             ta.own_len = (int)len0;
             ta.ident_pose = oi >= 0 ? own->ident_pose : nullptr;
+            const bool last = b0 + nb >= n;  // the words: once, with the last launch
+            ta.zero = own && last ? own->zero : nullptr;
+            ta.n_zero = own && last && own->zero ? own->n_zero : 0;
             const int grid = ta.xcd_map ? 8 * ta.nb * ((nb + 7) / 8) : ta.nb * nb;
             pyr_tail_kernel<<<grid, kPfThreads, lds, stream>>>(ta);
         } else {
@@ -1097,6 +1104,8 @@ void launch_pyramid_frames(const PyrGeom& g, const uint8_t* const* l0, uint8_t* 
             if (copy)
                 (void)hipMemcpyAsync(slot[b0 + oi], l0[b0 + oi], len0, hipMemcpyDeviceToDevice, stream);
             if (oi >= 0) own->copied = copy;
+            if (own && own->zero && b0 + nb >= n)
+                (void)hipMemsetAsync(own->zero, 0, sizeof(int) * (size_t)own->n_zero, stream);
         }
     }
 }

@@ -20,10 +20,14 @@ constexpr int kPyrBatch = 128;
 // whether it was) and, when ident_pose is set, the identity pose written
 // there — done by the tail launch (a frame-by-frame caller's copy and pose
 // launches folded into it).
+// zero (optional): n_zero ints cleared by the same launch (the chunk's
+// background-LK words, bg_begin).
 struct PyrOwn {
     int img;
     double* ident_pose;
     bool copied;
+    int* zero = nullptr;
+    int n_zero = 0;
 };
 void launch_pyramid_frames(const PyrGeom& g, const uint8_t* const* l0, uint8_t* const* slot,
                            int n, hipStream_t stream, PyrOwn* own = nullptr);
