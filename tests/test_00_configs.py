@@ -140,6 +140,52 @@ def test_gpu_config1_bench_workload_matches_oracle(lk, monkeypatch):
     assert np.max(np.abs(ua - oua)) < 1e-6
 
 
+@pytest.mark.gpu
+def test_gpu_background_lk_error_reaches_host(monkeypatch):
+    """A background LK wait that fails sets the grid's error word and its
+    pinned host copy from the failing wave itself (no copy behind the chunk):
+    v.synchronize() raises it (VISO_ERR_HIP), once — the word is cleared, and
+    the next chunk, without the fault, synchronises cleanly with the poses of
+    an uninterrupted run.  The fault is injected (VISO_LK_BG_INJECT_FAIL: the
+    drain's first wave reports a failed wait)."""
+    import torch
+
+    import viso_amd
+    from viso_amd._lib import VisoError
+    _config1_oracle()  # (the sequence's frames)
+    seq, left, right = _C1["seq"], _C1["left"], _C1["right"]
+    W, H, warm, steps = _C1["W"], _C1["H"], _C1["warm"], _C1["steps"]
+    dl, dr = torch.from_numpy(left).cuda(), torch.from_numpy(right).cuda()
+    torch.cuda.synchronize()
+    fb = W * H
+    half = steps // 2
+
+    def run(inject):
+        v = viso_amd.Viso(*seq.K, width=W, height=H, enable_tracking=1, batch_frames=128)
+        v.set_stereo(seq.p.baseline, STEREO_MAX_DISP, 1)
+        v.process_device(dl.data_ptr(), dr.data_ptr(), warm, fb)
+        v.synchronize()
+        if inject:
+            monkeypatch.setenv("VISO_LK_BG_INJECT_FAIL", "1")
+        v.process_device(dl.data_ptr() + warm * fb, dr.data_ptr() + warm * fb, half, fb)
+        if inject:
+            with pytest.raises(VisoError) as e:
+                v.synchronize()
+            assert e.value.rc == -2  # VISO_ERR_HIP
+            monkeypatch.delenv("VISO_LK_BG_INJECT_FAIL")
+            v.synchronize()  # reported once
+        else:
+            v.synchronize()
+        f0 = warm + half
+        v.process_device(dl.data_ptr() + f0 * fb, dr.data_ptr() + f0 * fb, steps - half, fb)
+        v.synchronize()
+        return v.poses
+
+    ref = run(False)
+    got = run(True)
+    assert len(ref) == warm + steps - 1 and np.array_equal(got, ref)
+
+
 # ------------------------------------------------------------------ configs[2]
 @pytest.mark.gpu
 def test_gpu_config2_1080p_reference_init_and_tracking():

@@ -171,8 +171,12 @@ struct viso_ctx {
     viso::GeoCtl* h_ctl_dev = nullptr;
     double* h_dbl = nullptr;        // pinned scratch doubles (64)
     double* h_poses = nullptr;      // pinned staging of the pose log (viso_get_poses)
+    double* h_poses_dev = nullptr;  // its device address (the direct kernels log into it too)
     size_t h_poses_cap = 0;         // poses it holds
     size_t poses_staged = 0;        // poses whose copy into h_poses is enqueued (finish_call)
+    double* log_host(int index) const {  // the direct launch's log_host for a log index
+        return index >= 0 && (size_t)index < h_poses_cap ? h_poses_dev : nullptr;
+    }
     int stage_poses();
 
     // ---------------- map (Map / MapPoint, include/map.h, map_point.h)

@@ -148,6 +148,10 @@ struct DirectArgs {
     double* pose_out;  // result pose (12) or null
     double* log;
     int log_index;  // < 0: no log append
+    // the log's copy in the context's pinned staging (device address of the
+    // host buffer, same index) or null (log_pose)
+    double* log_host;
+    double* prev_log_host;
     // L(3) fused with the previous frame's final solve (merged != 0): the
     // prologue solves the previous frame's level 0, writes its pose (+ log),
     // and seeds T21 from it (it is this frame's `last` pose)
@@ -174,6 +178,18 @@ __device__ inline void store_frame_pose(double* dst, const double* pose, int* re
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_store(ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+}
+
+// A logged pose (one thread), and its copy in the context's pinned staging
+// when given: system-scope stores the host reads after its stream sync, so
+// viso_synchronize enqueues no copy of the poses (round 5: one copy launch
+// at the end of every ingest call).
+__device__ inline void log_pose(double* log, double* log_host, int index, const double* pose) {
+    if (!log || index < 0) return;
+    for (int k = 0; k < 12; ++k) log[12 * (size_t)index + k] = pose[k];
+    if (log_host)
+        for (int k = 0; k < 12; ++k)
+            __hip_atomic_store(log_host + 12 * (size_t)index + k, pose[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // The map points of workgroup (tile) b: [*first, *first + *cnt).
@@ -973,8 +989,7 @@ __device__ inline void after_solve(const DirectArgs& a, bool merged, SolveLds& L
         if (blockIdx.x == 0) {
             for (int k = 0; k < 7; ++k) a.s.state[kLevels * kStateStride + k] = L.state[k];
             if (a.prev_pose_out) store_frame_pose(a.prev_pose_out, s_last, a.prev_ready);
-            if (a.prev_log && a.prev_log_index >= 0)
-                for (int k = 0; k < 12; ++k) a.prev_log[12 * (size_t)a.prev_log_index + k] = s_last[k];
+            log_pose(a.prev_log, a.prev_log_host, a.prev_log_index, s_last);
         }
         // Sophus::SE3d(R, t) of last_frame (src/viso.cpp:114)
         double q[4];
@@ -1174,8 +1189,7 @@ __global__ __launch_bounds__(kThreads, 4) void direct_level_kernel(const double*
         for (int k = 0; k < 7; ++k) a.s.state[out * kStateStride + k] = L.state[k];
         if (lv < 0 && a.pose_out) {
             store_frame_pose(a.pose_out, s_pose, a.ready);
-            if (a.log && a.log_index >= 0)
-                for (int k = 0; k < 12; ++k) a.log[12 * (size_t)a.log_index + k] = s_pose[k];
+            log_pose(a.log, a.log_host, a.log_index, s_pose);
         }
     }
     if (blockIdx.x == 0 && t == 0 && merged)
@@ -1739,6 +1753,7 @@ void launch_direct_levels(const FrameDev& last_pyr, const FrameDev& cur_pyr, con
         a.prev_pose_out = merge->pose_out;
         a.prev_log = merge->log;
         a.prev_log_index = merge->log ? merge->log_index : -1;
+        a.prev_log_host = merge->log ? merge->log_host : nullptr;
         a.prev_ready = merge->ready;
     }
     const int grid = a.n_tiles > 0 ? a.n_tiles : 1;
@@ -1763,13 +1778,14 @@ void launch_direct_final(const FrameDev& last_pyr, const FrameDev& cur_pyr, cons
                          const double K[4], const double* points, int n,
                          const double* pose_last12, const DirectScratch& s, double* stats,
                          double* pose_out, double* log, int log_index, hipStream_t stream, int precision,
-                         int* ready) {
+                         int* ready, double* log_host) {
     DirectArgs a = direct_args(last_pyr, cur_pyr, g, K, points, n, pose_last12, pose_last12, s,
                                stats, precision == VISO_PRECISION_FAST);
     a.pose_out = pose_out;
     a.ready = ready;
     a.log = log;
     a.log_index = log ? log_index : -1;
+    a.log_host = log ? log_host : nullptr;
     a.level = -1;
     a.probe_seq = next_probe_seq();
     // F solves level 0

@@ -139,6 +139,7 @@ int viso_ctx::init() {
     VISO_HIP_CHECK(hipHostMalloc((void**)&h_ctl, sizeof(GeoCtl)));
     VISO_HIP_CHECK(hipHostMalloc((void**)&h_int, 64 * sizeof(int)));
     VISO_HIP_CHECK(hipHostMalloc((void**)&h_dbl, 256 * sizeof(double)));
+    std::memset(h_int, 0, 64 * sizeof(int));
     VISO_HIP_CHECK(hipHostGetDevicePointer((void**)&h_int_dev, h_int, 0));
     VISO_HIP_CHECK(hipHostGetDevicePointer((void**)&h_ctl_dev, h_ctl, 0));
     geo.host_ctl = h_ctl_dev;
@@ -169,6 +170,7 @@ int viso_ctx::init() {
     // the pose getter's pinned staging (viso_get_poses)
     h_poses_cap = (size_t)std::min(std::max(p.max_poses, 1), 4096);
     VISO_HIP_CHECK(hipHostMalloc((void**)&h_poses, 96 * h_poses_cap));
+    VISO_HIP_CHECK(hipHostGetDevicePointer((void**)&h_poses_dev, h_poses, 0));
     VISO_HIP_CHECK(hipMemsetAsync(n_track_dev.ptr, 0, 256, stream));
     VISO_HIP_CHECK(hipStreamSynchronize(stream));
     return VISO_OK;
@@ -204,6 +206,7 @@ void viso_ctx::release() {
     h_int = nullptr;
     h_dbl = nullptr;
     h_poses = nullptr;
+    h_poses_dev = nullptr;
     h_poses_cap = 0;
 }
 
@@ -410,7 +413,7 @@ int viso_ctx::resolve_direct() {
     launch_direct_final(frame(dpend_last), frame(dpend_cur), geom, K, (const double*)map_pts.ptr,
                         n_map, pose_of(dpend_last), direct, (double*)direct_stats.ptr,
                         pose_of(dpend_cur), dpend_log >= 0 ? (double*)pose_log.ptr : nullptr,
-                        dpend_log, stream, p.precision, bg_ready(dpend_bg));
+                        dpend_log, stream, p.precision, bg_ready(dpend_bg), log_host(dpend_log));
     VISO_HIP_CHECK(hipGetLastError());
     drop(dpend_cur);
     drop(dpend_last);
@@ -442,6 +445,12 @@ int viso_ctx::finish_call(hipStream_t ls) {
 int viso_ctx::stage_poses() {
     const size_t m = std::min((size_t)n_poses, (size_t)std::max(p.max_poses, 0));
     if (m <= poses_staged || m > h_poses_cap || !h_poses) return VISO_OK;
+    // the direct kernels logged every pose below h_poses_cap into h_poses
+    // too (log_host): nothing to copy
+    if (h_poses_dev) {
+        poses_staged = m;
+        return VISO_OK;
+    }
     VISO_HIP_CHECK(hipMemcpyAsync(h_poses + 12 * poses_staged, (const double*)pose_log.ptr + 12 * poses_staged,
                                   96 * (m - poses_staged), hipMemcpyDeviceToHost, stream));
     poses_staged = m;
@@ -506,9 +515,11 @@ int viso_ctx::bg_begin(const std::vector<int>& chunk, bool zeroed) {
     a.bg_next = a.bg_ready + kLkBatch;
     a.bg_left = a.bg_next + 8 * 32 + 32;
     a.bg_err = a.bg_ready + bg_words;
+    a.bg_err_host = h_int_dev + 32;
     a.bg_items = nb * n_map;
     // tests: VISO_LK_BG_IDLE_US shortens the resident waves' patience, so the
     // leftover list and the drain carry most items
+    if (const char* f = getenv("VISO_LK_BG_INJECT_FAIL")) a.bg_inject_fail = f[0] == '1';
     if (const char* idle = getenv("VISO_LK_BG_IDLE_US")) {
         const long us = strtol(idle, nullptr, 10);
         if (us > 0 && us < 1000000) a.bg_idle = (unsigned int)(us * 100);
@@ -548,13 +559,16 @@ int viso_ctx::bg_launch() {
 
 int viso_ctx::bg_check() {
     if (!bg_unchecked || !bg_buf.ptr) return VISO_OK;
-    // the words (error, items the drain ran) were copied into pinned memory
-    // behind the drain on the context stream (bg_end): they are final once
-    // that stream has passed the copy
+    // the error word is in pinned memory (bg_err_host; the drain's item
+    // count too in VISO_DRAIN_COUNT builds, copied behind the drain): final
+    // once the context stream has passed the drain and the grid (bg_end)
     VISO_HIP_CHECK(hipStreamSynchronize(stream));
     const int w[2] = {h_int[32], h_int[33]};
     bg_unchecked = false;
-    if (w[0] || w[1]) VISO_HIP_CHECK(hipMemsetAsync(bg_args.bg_err, 0, 2 * sizeof(int), stream));
+    if (w[0] || w[1]) {
+        VISO_HIP_CHECK(hipMemsetAsync(bg_args.bg_err, 0, 2 * sizeof(int), stream));
+        h_int[32] = h_int[33] = 0;
+    }
     if (getenv("VISO_LK_BG_STATS"))  // dev: how much of the last chunk the drain carried
         fprintf(stderr, "viso lk-bg: %d frames x %d points, drain ran %d items (builds with VISO_DRAIN_COUNT), error %d\n",
                 bg_nb, n_map, w[1], w[0]);
@@ -584,8 +598,11 @@ int viso_ctx::bg_end(bool drain) {
         VISO_HIP_CHECK(hipGetLastError());
     }
     VISO_HIP_CHECK(hipStreamWaitEvent(stream, bg_done, 0));
-    // the error / drain-count words, for bg_check (no blocking copy at sync)
+    // the error word reaches h_int[32] from the failing wave itself
+    // (bg_err_host); the drain's item count (dev builds) by a copy
+#ifdef VISO_DRAIN_COUNT
     VISO_HIP_CHECK(hipMemcpyAsync(h_int + 32, bg_args.bg_err, 2 * sizeof(int), hipMemcpyDeviceToHost, stream));
+#endif
     lk_last_rows = bg_nb;
     lk_last_pts = n_map;
     VISO_HIP_CHECK(hipEventRecord(lk_ring[lk_seq % kLkRing], lk_stream));
@@ -943,6 +960,7 @@ int viso_ctx::on_new_frame(int cur) {
                     m.log = dpend_log >= 0 ? (double*)pose_log.ptr : nullptr;
                     m.log_index = dpend_log;
                     m.ready = bg_ready(dpend_bg);
+                    m.log_host = log_host(dpend_log);
                 }
                 launch_direct_levels(frame(last_slot), frame(cur), g, K, (const double*)map_pts.ptr,
                                      n_map, pose_of(last_slot), pose_of(last_slot), direct,
@@ -1168,9 +1186,11 @@ int viso_get_poses(viso_ctx* c, double* Tcw12, size_t cap, size_t* n) {
         VISO_HIP_CHECK(hipStreamSynchronize(c->stream));  // no staged copy in flight into the old buffer
         if (c->h_poses) VISO_HIP_CHECK(hipHostFree(c->h_poses));
         c->h_poses = nullptr;
+        c->h_poses_dev = nullptr;
         c->h_poses_cap = 0;
         c->poses_staged = 0;
         VISO_HIP_CHECK(hipHostMalloc((void**)&c->h_poses, 96 * want));
+        VISO_HIP_CHECK(hipHostGetDevicePointer((void**)&c->h_poses_dev, c->h_poses, 0));
         c->h_poses_cap = want;
     }
     VISO_HIP_CHECK(hipMemcpyAsync(c->h_poses, c->pose_log.ptr, 96 * m, hipMemcpyDeviceToHost, c->stream));

@@ -107,6 +107,10 @@ struct LkAlignArgs {
     int* bg_ready = nullptr;
     int* bg_next = nullptr;
     int* bg_err = nullptr;
+    // the error word's pinned host copy (device address): set with bg_err[0]
+    // by the (rare) failing wave, so the end of a chunk copies nothing back
+    int* bg_err_host = nullptr;
+    int bg_inject_fail = 0;  // tests (VISO_LK_BG_INJECT_FAIL): the drain reports a failed wait
     int bg_items = 0;
     // leftovers: [0] drain cursor, [1] count, [32 ..] items (head * per_head + k)
     int* bg_left = nullptr;
@@ -181,6 +185,7 @@ struct DirectPrev {
     double* log;
     int log_index;
     int* ready = nullptr;  // background LK alignment's flag for that pose (or null)
+    double* log_host = nullptr;  // the log's pinned host copy (device address), same index
 };
 // true when a direct-pose workgroup leaves its CU room for the background LK
 // alignment's (12 waves of 128 VGPRs + <= 76 KB LDS beside 4 waves + 84 KB)
@@ -194,7 +199,8 @@ void launch_direct_final(const FrameDev& last, const FrameDev& cur, const PyrGeo
                          const double K[4], const double* points, int n,
                          const double* pose_last12, const DirectScratch& s, double* stats,
                          double* pose_out, double* log, int log_index, hipStream_t stream,
-                         int precision = VISO_PRECISION_FAITHFUL, int* ready = nullptr);
+                         int precision = VISO_PRECISION_FAITHFUL, int* ready = nullptr,
+                         double* log_host = nullptr);
 // ---------------------------------------------------------------- rig direct pose
 // Multi-camera photometric rig (the repo's own spec;
 // oracle/oracle_rig.cpp): levels 3..0 of one rig Gauss-Newton step each over

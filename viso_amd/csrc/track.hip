@@ -844,6 +844,13 @@ constexpr int kBgTake = VISO_LK_BG_TAKE;  // items per head dequeue (1 or 2)
 #endif
 constexpr int kBgLeftCap = 4096;                           // leftover items (one per resident wave at most)
 constexpr int kBgClosed = 1 << 30;                          // bg_left[1]: the drain has read the count
+// a background wait that failed: the sticky error word, and its pinned host
+// copy (viso_ctx::bg_check reads that after its stream sync)
+__device__ inline void bg_fail(const LkAlignArgs& a) {
+    atomicOr(a.bg_err, 1);
+    if (a.bg_err_host) __hip_atomic_store(a.bg_err_host, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 template <bool FAST>
 __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
     if (a.n_frames <= 0) return;  // warm_lk_bg
@@ -887,7 +894,7 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
                     break;
                 }
                 if (c >= kBgLeftCap) {  // (one slot per resident wave: unreachable)
-                    atomicOr(a.bg_err, 1);
+                    bg_fail(a);
                     break;
                 }
                 const int prev = atomicCAS(a.bg_left + 1, c, c + 1);
@@ -932,7 +939,7 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
                 t0 = __builtin_amdgcn_s_memrealtime();
             }
             if (must && dt > kBgWaitTicks) {
-                if (lane == 0) atomicOr(a.bg_err, 1);
+                if (lane == 0) bg_fail(a);
                 return false;
             }
             __builtin_amdgcn_s_sleep(VISO_LK_BG_POLL);
@@ -1003,6 +1010,7 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
     int n_left = 0;
     if (a.bg_drain) {
         if (blockIdx.x == 0 && wave == 0) {
+            if (lane == 0 && a.bg_inject_fail) bg_fail(a);  // (tests: the error path)
             if (lane == 0) {
                 n_left = atomicOr(a.bg_left + 1, kBgClosed) & ~kBgClosed;
                 __hip_atomic_store(a.bg_left + 2, n_left | kBgClosed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1015,7 +1023,7 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
                           __hip_atomic_load(a.bg_left + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) &
                      kBgClosed)) {
                 if (__builtin_amdgcn_s_memrealtime() - t0 > kBgWaitTicks) {
-                    if (lane == 0) atomicOr(a.bg_err, 1);
+                    if (lane == 0) bg_fail(a);
                     return;
                 }
                 __builtin_amdgcn_s_sleep(2);
@@ -1060,7 +1068,7 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
             while ((e = __builtin_amdgcn_readfirstlane(
                         __hip_atomic_load(a.bg_left + 32 + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) == 0) {
                 if (__builtin_amdgcn_s_memrealtime() - t0 > kBgWaitTicks) {
-                    if (lane == 0) atomicOr(a.bg_err, 1);
+                    if (lane == 0) bg_fail(a);
                     return;
                 }
                 __builtin_amdgcn_s_sleep(2);
