@@ -112,7 +112,9 @@ struct SlotRec {
     bool borrowed = false;
     int refs = 0;
     int64_t lk_use = -1;  // last lk_stream batch that reads it (lk_seq numbering)
+    int64_t free_epoch = -1;  // the ingest call (epoch) during which it was freed
 };
+constexpr int kEpochRing = 16;
 constexpr int kLkRing = 64;
 }  // namespace viso
 
@@ -204,6 +206,18 @@ struct viso_ctx {
     hipStream_t lk_stream = nullptr;
     hipEvent_t lk_ring[viso::kLkRing] = {};  // recorded after each lk_stream batch
     viso::HostStage stage;  // pinned staging of host-ingested frames (ingest_host)
+    // Host uploads run on their own stream (created at the first one, with a
+    // hardware queue of its own when a CU-masked stream can be made), so a
+    // frame's DMA overlaps the previous frame's chain.  A slot's last readers
+    // on the context stream were all enqueued by the end of the ingest call
+    // that freed it: every ingest call ends an epoch with an event there.
+    hipStream_t up_stream = nullptr;
+    int64_t epoch = 0;
+    hipEvent_t epoch_evt[viso::kEpochRing] = {};
+    hipEvent_t epoch_now = nullptr;  // a slot freed in the current call (rare)
+    int end_epoch();
+    int create_up_stream();
+    int upload_host(int s, const uint8_t* grey, int32_t w, int32_t h, int32_t stride);
     // PoseEstimation2d2d's E path runs on lk_stream beside the H path (no LK
     // alignment runs while initialising): fork / join events
     hipEvent_t geo_fork = nullptr, geo_join = nullptr;
@@ -250,7 +264,7 @@ struct viso_ctx {
     int init();
     void release();
     // frame pool
-    int acquire_slot();
+    int acquire_slot(hipStream_t lk_wait = nullptr);
     void hold(int slot);
     void drop(int slot);
     void set_role(int& role, int slot);

@@ -164,6 +164,8 @@ int viso_ctx::init() {
     VISO_HIP_CHECK(hipEventCreateWithFlags(&geo_join, hipEventDisableTiming));
     VISO_HIP_CHECK(hipEventCreateWithFlags(&ntrack_evt, hipEventDisableTiming));
     VISO_HIP_CHECK(hipEventCreateWithFlags(&gate_evt, hipEventDisableTiming));
+    for (auto& e : epoch_evt) VISO_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    VISO_HIP_CHECK(hipEventCreateWithFlags(&epoch_now, hipEventDisableTiming));
     if (const char* e = getenv("VISO_GATE_SPEC")) gate_spec_mode = e[0] == '1' ? 1 : 0;
     rc = bg_prepare();
     if (rc) return rc;
@@ -178,6 +180,7 @@ int viso_ctx::init() {
 
 void viso_ctx::release() {
     if (lk_stream) (void)hipStreamSynchronize(lk_stream);
+    if (up_stream) (void)hipStreamSynchronize(up_stream);
     timing.destroy();
     for (auto& e : lk_ring) {
         if (e) (void)hipEventDestroy(e);
@@ -191,6 +194,12 @@ void viso_ctx::release() {
     }
     if (lk_stream) (void)hipStreamDestroy(lk_stream);
     lk_stream = nullptr;
+    for (auto& e : epoch_evt) {
+        if (e) (void)hipEventDestroy(e);
+        e = nullptr;
+    }
+    if (epoch_now) (void)hipEventDestroy(epoch_now);
+    epoch_now = nullptr;
     DevBuf* bufs[] = {&scratch_a, &scratch_b, &scratch_c, &scratch_d, &slot_pool, &slot_pose,
                       &kp1, &kp2, &kp1b, &kp2b, &track_success, &n_track_dev, &fast_rows,
                       &geo_buf, &map_pts, &kf_poses, &direct_buf, &direct_stats,
@@ -202,6 +211,8 @@ void viso_ctx::release() {
     if (h_dbl) (void)hipHostFree(h_dbl);
     if (h_poses) (void)hipHostFree(h_poses);
     stage.release();
+    if (up_stream) (void)hipStreamDestroy(up_stream);
+    up_stream = nullptr;
     h_ctl = nullptr;
     h_int = nullptr;
     h_dbl = nullptr;
@@ -236,22 +247,74 @@ int viso_ctx::create_streams() {
     return VISO_OK;
 }
 
+// The upload stream (host ingest), with a hardware queue of its own when a
+// CU-masked stream can be made (a plain stream may share the context
+// stream's queue, behind the chain it should overlap: still correct).
+int viso_ctx::create_up_stream() {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0) {
+        std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
+        for (int c = 0; c < cus; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
+        if (hipExtStreamCreateWithCUMask(&up_stream, (uint32_t)mask.size(), mask.data()) != hipSuccess)
+            up_stream = nullptr;
+    }
+    if (!up_stream) {
+        (void)hipGetLastError();
+        if (hipStreamCreateWithFlags(&up_stream, hipStreamNonBlocking) != hipSuccess) return VISO_ERR_HIP;
+    }
+    return VISO_OK;
+}
+
 // ------------------------------------------------------------------ frame pool
-int viso_ctx::acquire_slot() {
+int viso_ctx::acquire_slot(hipStream_t lk_wait) {
     if (free_slots.empty()) return -1;
     int s = free_slots.front();
     free_slots.pop_front();
     // lk_stream may still read this slot's previous frame: order the reuse
-    // behind that batch (a no-op wait in steady state; a later batch on the
-    // same stream also implies completion)
+    // (on the stream that writes it first: the context stream, or the upload
+    // stream) behind that batch (a no-op wait in steady state; a later batch
+    // on the same stream also implies completion)
     const int64_t use = slots[(size_t)s].lk_use;
     if (use >= 0 && lk_seq > use) {
         const int64_t e = (lk_seq - use <= kLkRing) ? use : lk_seq - 1;
-        (void)hipStreamWaitEvent(stream, lk_ring[e % kLkRing], 0);
+        (void)hipStreamWaitEvent(lk_wait ? lk_wait : stream, lk_ring[e % kLkRing], 0);
     }
+    const int64_t fe = slots[(size_t)s].free_epoch;
     slots[(size_t)s] = SlotRec{};
     slots[(size_t)s].l0 = slot_base(s);
+    slots[(size_t)s].free_epoch = fe;
     return s;
+}
+
+// The end of an ingest call: an event behind its work on the context stream
+// (the reuse of a slot it freed is ordered behind it on the upload stream).
+int viso_ctx::end_epoch() {
+    VISO_HIP_CHECK(hipEventRecord(epoch_evt[epoch % kEpochRing], stream));
+    ++epoch;
+    return VISO_OK;
+}
+
+// Host frame -> slot s's level 0 through the pinned staging, on the upload
+// stream: behind the slot's last readers (its lk_stream batch: acquire_slot;
+// the context stream's: the epoch that freed it), and the context stream
+// waits for the DMA before the frame's pyramid.
+int viso_ctx::upload_host(int s, const uint8_t* grey, int32_t w, int32_t h, int32_t stride) {
+    const int64_t fe = slots[(size_t)s].free_epoch;
+    if (fe >= 0) {
+        if (fe < epoch) {
+            const int64_t e = (epoch - fe <= kEpochRing) ? fe : epoch - 1;
+            VISO_HIP_CHECK(hipStreamWaitEvent(up_stream, epoch_evt[e % kEpochRing], 0));
+        } else {  // freed during this call: behind everything enqueued so far
+            VISO_HIP_CHECK(hipEventRecord(epoch_now, stream));
+            VISO_HIP_CHECK(hipStreamWaitEvent(up_stream, epoch_now, 0));
+        }
+    }
+    {
+        TimedRegion t(timing, VISO_KERNEL_UPLOAD, up_stream);
+        VISO_HIP_CHECK(stage.upload(slot_base(s), grey, w, h, stride, up_stream));
+    }
+    VISO_HIP_CHECK(hipStreamWaitEvent(stream, stage.last, 0));
+    return VISO_OK;
 }
 
 void viso_ctx::hold(int s) {
@@ -261,7 +324,10 @@ void viso_ctx::hold(int s) {
 void viso_ctx::drop(int s) {
     if (s < 0) return;
     SlotRec& r = slots[(size_t)s];
-    if (--r.refs == 0) free_slots.push_back(s);
+    if (--r.refs == 0) {
+        r.free_epoch = epoch;
+        free_slots.push_back(s);
+    }
 }
 
 void viso_ctx::set_role(int& role, int s) {
@@ -327,13 +393,19 @@ void viso_ctx::launch_ingest_pyramid(const uint8_t* const* l0, uint8_t* const* d
 
 int viso_ctx::ingest_host(const uint8_t* grey, int32_t w, int32_t h, int32_t stride, int* slot_out) {
     if (w != p.width || h != p.height || stride < w || !grey) return VISO_ERR_ARG;
-    int s = acquire_slot();
+    if (!up_stream) {
+        int rc = create_up_stream();
+        if (rc) return rc;
+    }
+    int s = acquire_slot(up_stream);
     if (s < 0) return VISO_ERR_CAPACITY;
     // through pinned staging (staging.hpp: a pageable hipMemcpy2DAsync
-    // measured 3.25 ms per 1242x375 frame)
-    {
-        TimedRegion t(timing, VISO_KERNEL_UPLOAD, stream);
-        VISO_HIP_CHECK(stage.upload(slot_base(s), grey, w, h, stride, stream));
+    // measured 3.25 ms per 1242x375 frame), on the upload stream
+    const int rc = upload_host(s, grey, w, h, stride);
+    if (rc) {
+        hold(s);
+        drop(s);
+        return rc;
     }
     *slot_out = s;
     return VISO_OK;
@@ -1041,7 +1113,9 @@ int viso_process_frame(viso_ctx* c, const uint8_t* grey, int32_t width, int32_t 
     VISO_HIP_CHECK(hipGetLastError());
     rc = c->on_new_frame(s);
     if (rc) return rc;
-    return c->finish_call(c->lk_stream);
+    rc = c->finish_call(c->lk_stream);
+    const int re = c->end_epoch();
+    return rc ? rc : re;
 }
 
 int viso_process_stereo(viso_ctx* c, const uint8_t* left, const uint8_t* right,
@@ -1070,7 +1144,9 @@ int viso_process_stereo(viso_ctx* c, const uint8_t* left, const uint8_t* right,
     c->right_l0 = nullptr;
     c->drop(sr);
     if (rc) return rc;
-    return c->finish_call(c->lk_stream);
+    rc = c->finish_call(c->lk_stream);
+    const int re = c->end_epoch();
+    return rc ? rc : re;
 }
 
 int viso_process_frames_device(viso_ctx* c, const uint8_t* d_left, const uint8_t* d_right,
@@ -1154,7 +1230,7 @@ int viso_process_frames_device(viso_ctx* c, const uint8_t* d_left, const uint8_t
         const int rc = end_chunk(VISO_OK);
         if (rc) return rc;
     }
-    return VISO_OK;
+    return c->end_epoch();
 }
 
 int viso_get_state(viso_ctx* c, int32_t* state) {

@@ -23,6 +23,7 @@ struct HostStage {
     hipEvent_t ev[kRing] = {};
     bool used[kRing] = {};
     int next = 0;
+    hipEvent_t last = nullptr;  // the latest upload's event (behind its DMA on s)
 
     // rows [0, h) of w bytes at src (row pitch stride) -> dst (packed), on s
     hipError_t upload(uint8_t* dst, const uint8_t* src, int w, int h, int stride, hipStream_t s) {
@@ -46,6 +47,7 @@ struct HostStage {
         if ((e = hipMemcpyAsync(dst, buf[k], bytes, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
         if ((e = hipEventRecord(ev[k], s)) != hipSuccess) return e;
         used[k] = true;
+        last = ev[k];
         return hipSuccess;
     }
 
@@ -61,6 +63,7 @@ struct HostStage {
             cap[k] = 0;
             used[k] = false;
         }
+        last = nullptr;
     }
 };
 
