@@ -876,10 +876,16 @@ int viso_ctx::on_new_frame(int cur) {
                                        (float2*)kp2.ptr, (uint8_t*)track_success.ptr, (const int*)n_track_dev.ptr,
                                        p.max_features, p.photometric_error_thresh, stream);
                 }
-                // erase failed tracks (src/viso.cpp:23-40)
-                launch_compact_tracks((const float2*)kp1.ptr, (const float2*)kp2.ptr,
-                                      (const uint8_t*)track_success.ptr, n >= 0 ? n : -p.max_features,
-                                      (float2*)kp1b.ptr, (float2*)kp2b.ptr, (int*)n_track_dev.ptr, stream);
+                // erase failed tracks (src/viso.cpp:23-40) into the other
+                // track buffers, which become kp1 / kp2 — in the gate's launch
+                CompactIn ci;
+                ci.in1 = (const float2*)kp1.ptr;
+                ci.in2 = (const float2*)kp2.ptr;
+                ci.success = (const uint8_t*)track_success.ptr;
+                ci.n = n >= 0 ? n : -p.max_features;
+                ci.out1 = (float2*)kp1b.ptr;
+                ci.out2 = (float2*)kp2b.ptr;
+                ci.n_out = (int*)n_track_dev.ptr;
                 ntrack_pending = false;
                 std::swap(kp1, kp1b);
                 std::swap(kp2, kp2b);
@@ -894,7 +900,7 @@ int viso_ctx::on_new_frame(int cur) {
                 // host round trip
                 {
                     TimedRegion t(timing, VISO_KERNEL_RANSAC, stream);
-                    launch_pose_2d2d_gate(geo, stream);
+                    launch_compact_gate(ci, geo, stream);
                 }
                 VISO_HIP_CHECK(hipGetLastError());
                 // the gate mirrors the control block into h_ctl itself.  When

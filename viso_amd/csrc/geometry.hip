@@ -116,9 +116,49 @@ __device__ inline void ctl_mirror(const GeoArgs& a) {
 constexpr int kNormThreads = 1024;
 constexpr int kNormMaxC = 64;
 
-__global__ __launch_bounds__(kNormThreads) void normalize_kernel(GeoArgs a) {
+// With ci.success (launch_compact_gate) the same workgroup first erases the
+// failed tracks (src/viso.cpp:23-40, order kept): thread t owns the
+// ceil(n / 1024) consecutive tracks [t C, t C + C), counts its survivors, one
+// block-wide exclusive scan places them, and each thread copies its own in
+// order into ci.out1 / ci.out2 (= a.kp1 / a.kp2); the count goes to
+// ci.n_out (= a.n_dev) and, through LDS, to the normalisation below.
+// ci.n < 0: the input count is *ci.n_out's value capped at -n (a
+// re-detection frame's FAST count the host has not read).
+__global__ __launch_bounds__(kNormThreads) void normalize_kernel(GeoArgs a, CompactIn ci) {
     __shared__ double s_w[kNormThreads / 64];
-    const int n = *a.n_dev;
+    __shared__ int s_c[kNormThreads / 64];
+    __shared__ int s_n;
+    if (ci.success) {
+        int m = ci.n;
+        if (m < 0) m = min(*ci.n_out, -m);
+        const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+        const int Cc = (m + kNormThreads - 1) / kNormThreads;
+        const int lo = min(t * Cc, m), hi = min(lo + Cc, m);
+        int cnt = 0;
+        for (int i = lo; i < hi; ++i) cnt += ci.success[i] != 0;
+        int incl = cnt;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int o = __shfl_up(incl, d);
+            if (lane >= d) incl += o;
+        }
+        if (lane == 63) s_c[wave] = incl;
+        __syncthreads();  // (also: every thread has read *ci.n_out)
+        int off = incl - cnt;
+        for (int k = 0; k < wave; ++k) off += s_c[k];
+        for (int i = lo; i < hi; ++i)
+            if (ci.success[i]) {
+                ci.out1[off] = ci.in1[i];
+                ci.out2[off] = ci.in2[i];
+                ++off;
+            }
+        if (t == kNormThreads - 1) {
+            *ci.n_out = off;
+            s_n = off;
+        }
+        __syncthreads();  // the compacted tracks (global, this workgroup's) and their count
+    }
+    const int n = ci.success ? s_n : *a.n_dev;
     const double* Ki = a.Kinv;
     int P = 1;
     while (P < n) P <<= 1;
@@ -1130,7 +1170,11 @@ __global__ __launch_bounds__(kSelThreads) void select_finish_kernel(GeoArgs a) {
 }  // namespace
 
 void launch_pose_2d2d_gate(const GeoArgs& a, hipStream_t stream) {
-    normalize_kernel<<<1, kNormThreads, 0, stream>>>(a);
+    normalize_kernel<<<1, kNormThreads, 0, stream>>>(a, CompactIn{});
+}
+
+void launch_compact_gate(const CompactIn& ci, const GeoArgs& a, hipStream_t stream) {
+    normalize_kernel<<<1, kNormThreads, 0, stream>>>(a, ci);
 }
 
 void launch_pose_2d2d_spec(const GeoArgs& a, hipStream_t stream) {

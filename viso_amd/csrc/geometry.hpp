@@ -89,6 +89,20 @@ void launch_pose_2d2d(const GeoArgs& a, hipStream_t stream, Timing* timing);
 // returns at once when the gate is closed; a caller that has read the gate
 // on the host may skip the body.
 void launch_pose_2d2d_gate(const GeoArgs& a, hipStream_t stream);
+// The erase of failed tracks (src/viso.cpp:23-40) and the gate in one
+// launch: in1 / in2 [0, n) with success -> out1 / out2 (which must be a.kp1 /
+// a.kp2), the count -> *n_out (which must be a.n_dev); n < 0: the count is
+// *n_out's input value capped at -n.
+struct CompactIn {
+    const float2* in1 = nullptr;
+    const float2* in2 = nullptr;
+    const uint8_t* success = nullptr;
+    int n = 0;
+    float2* out1 = nullptr;
+    float2* out2 = nullptr;
+    int* n_out = nullptr;
+};
+void launch_compact_gate(const CompactIn& ci, const GeoArgs& a, hipStream_t stream);
 // The H chain's first launch (the hypotheses), enqueued on `stream` behind
 // the gate before the host has read it: a closed gate makes it return at
 // once, an open one lets the host's round trip on the gate overlap it.

@@ -60,11 +60,6 @@ void launch_klt(const FrameDev& ref, const FrameDev& cur, const PyrGeom& g, cons
 // the same with the track count in device memory (*n_dev, capped at cap)
 void launch_klt_dev(const FrameDev& ref, const FrameDev& cur, const PyrGeom& g, const float2* kp1,
                     float2* kp2, uint8_t* success, const int* n_dev, int cap, double thresh, hipStream_t stream);
-// Order-preserving erase of failed tracks (src/viso.cpp:23-40):
-// kp1/kp2[0..n) with success -> out arrays; *n_out = survivors.  n < 0:
-// the count is *n_out's input value, capped at -n.
-void launch_compact_tracks(const float2* kp1, const float2* kp2, const uint8_t* success, int n,
-                           float2* kp1_out, float2* kp2_out, int* n_out, hipStream_t stream);
 
 constexpr int kMaxKeyframes = 8;
 // One frame of a batched LKAlignment launch: its pyramid and pose (device).

@@ -1134,51 +1134,7 @@ __global__ __launch_bounds__(256, 4) void lk_item_kernel(LkAlignArgs a) {
     }
 }
 
-// One 1,024-thread workgroup: thread t owns the ceil(n / 1024) consecutive
-// tracks [t C, t C + C), counts its survivors, one block-wide exclusive scan
-// places them, and each thread copies its own in order (src/viso.cpp:23-40
-// erase, order kept).
-__global__ __launch_bounds__(1024) void compact_tracks_kernel(const float2* __restrict__ kp1,
-                                                              const float2* __restrict__ kp2,
-                                                              const uint8_t* __restrict__ success,
-                                                              int n, float2* __restrict__ o1,
-                                                              float2* __restrict__ o2,
-                                                              int* __restrict__ n_out) {
-    __shared__ int s_w[16];
-    // n < 0: the count is *n_out's input value, capped at -n (a re-detection
-    // frame's FAST count the host has not read)
-    if (n < 0) n = min(*n_out, -n);
-    __syncthreads();  // every thread has read *n_out before thread 1023 writes it
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int C = (n + 1023) / 1024;
-    const int lo = min(t * C, n), hi = min(lo + C, n);
-    int cnt = 0;
-    for (int i = lo; i < hi; ++i) cnt += success[i] != 0;
-    int incl = cnt;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int o = __shfl_up(incl, d);
-        if (lane >= d) incl += o;
-    }
-    if (lane == 63) s_w[wave] = incl;
-    __syncthreads();
-    int off = incl - cnt;
-    for (int k = 0; k < wave; ++k) off += s_w[k];
-    for (int i = lo; i < hi; ++i)
-        if (success[i]) {
-            o1[off] = kp1[i];
-            o2[off] = kp2[i];
-            ++off;
-        }
-    if (t == 1023) *n_out = off;
-}
-
 }  // namespace
-
-void launch_compact_tracks(const float2* kp1, const float2* kp2, const uint8_t* success, int n,
-                           float2* kp1_out, float2* kp2_out, int* n_out, hipStream_t stream) {
-    compact_tracks_kernel<<<1, 1024, 0, stream>>>(kp1, kp2, success, n, kp1_out, kp2_out, n_out);
-}
 
 void launch_klt(const FrameDev& ref, const FrameDev& cur, const PyrGeom& g, const float2* kp1,
                 float2* kp2, uint8_t* success, int n, double thresh, hipStream_t stream) {
