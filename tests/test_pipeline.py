@@ -168,6 +168,33 @@ def test_gpu_init_gate_speculation_paths_agree(mode, monkeypatch):
 
 
 @pytest.mark.gpu
+def test_gpu_host_ingest_slot_reuse():
+    """Host frames go up on their own stream (frame.hip upload_host): a
+    slot's reuse waits for the ingest call that freed it (its epoch event)
+    and for its LK batch.  With batch_frames=1 the pool has 10 slots, so
+    slots are reused every few frames — the poses, the map and the last LK
+    alignment equal a run whose pool never wraps (batch_frames=128), bit for
+    bit."""
+    import viso_amd
+    seq = seqdata.sequence(0)
+    n = d_init_frame() + 30
+
+    def run(batch):
+        v = viso_amd.Viso(*seq.K, width=W, height=H, enable_tracking=1, batch_frames=batch)
+        for f in range(n):
+            v.OnNewFrame(seqdata.image(f))
+        v.synchronize()
+        return v.poses, v.GetPoints(), v.alignment()
+
+    ref = run(128)
+    got = run(1)
+    assert len(ref[0]) >= 25 and np.array_equal(got[0], ref[0])
+    assert np.array_equal(got[1], ref[1])
+    for a, b in zip(got[2], ref[2]):
+        assert np.array_equal(a, b)
+
+
+@pytest.mark.gpu
 def test_gpu_as_shipped_mode():
     seq, gv, ov = _run_pair(0, enable_tracking=0)
     for f in range(d_init_frame() + 3):
