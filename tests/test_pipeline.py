@@ -207,7 +207,12 @@ def test_gpu_as_shipped_mode():
 
 
 @pytest.mark.gpu
-def test_gpu_batched_device_ingest_matches_per_frame():
+@pytest.mark.parametrize("batch", [5, 2])
+def test_gpu_batched_device_ingest_matches_per_frame(batch):
+    """viso_process_frames_device in chunks of `batch` frames equals
+    frame-by-frame host ingest; batch 2 makes a 12-slot pool that wraps
+    within the 14 frames (slot reuse behind the pyramid's own level-0 copy of
+    each chunk's last frame, PyrOwn)."""
     import torch
 
     import viso_amd
@@ -221,7 +226,7 @@ def test_gpu_batched_device_ingest_matches_per_frame():
     dl = torch.from_numpy(frames).cuda()
     dr = torch.from_numpy(rights).cuda()
     torch.cuda.synchronize()
-    bat = viso_amd.Viso(*seq.K, width=W, height=H, enable_tracking=1, batch_frames=5)
+    bat = viso_amd.Viso(*seq.K, width=W, height=H, enable_tracking=1, batch_frames=batch)
     bat.process_device(dl.data_ptr(), dr.data_ptr(), n, W * H)
     bat.synchronize()
     assert bat.state == ref.state
