@@ -61,8 +61,15 @@ def main():
     v.synchronize()
     assert lib.viso_debug_probe_ring(log.ctypes.data, exits.ctypes.data, cap, ctypes.byref(nl), 1) == 0
     lib.viso_debug_probe_lk(lkbuf, 1)
+    wm = (ctypes.c_ulonglong * 4)()
+    has_wm = hasattr(lib, "viso_debug_probe_window_misses")
+    if has_wm:
+        lib.viso_debug_probe_window_misses(wm, 1)
     run(warm, steps)
     v.synchronize()
+    if has_wm:
+        lib.viso_debug_probe_window_misses(wm, 0)
+        print("current-image samples outside their LDS window, per level (L0..L3): " + ", ".join(str(x) for x in wm))
     print(f"map points {len(v.GetPoints())}, state {v.state}")
     assert lib.viso_debug_probe_ring(log.ctypes.data, exits.ctypes.data, cap, ctypes.byref(nl), 0) == 0
     n = min(nl.value, cap)

@@ -320,6 +320,11 @@ __device__ inline void win_store(uint8_t* lds, const CurWin& c) {
     }
 }
 
+#ifdef VISO_PROBE
+// (probe) current-image samples that missed their LDS window, per level
+__device__ unsigned long long g_pfb[4];
+#endif
+
 // sample_px with the taps served from the window when all four lie in it
 __device__ inline double sample_cw(const uint8_t* __restrict__ img, int w, int h, double x,
                                    double y, const uint8_t* win, const CurWin& c) {
@@ -335,7 +340,24 @@ __device__ inline double sample_cw(const uint8_t* __restrict__ img, int w, int h
             return double((1 - xx) * (1 - yy) * d0 + xx * (1 - yy) * d1 + (1 - xx) * yy * d2 +
                           xx * yy * d3);
         }
+        // a sample on the image's last row: its lower taps lie past the
+        // level buffer and read 0 (sample_px's rule), the upper two come from
+        // the window (clamped to the bottom edge, it holds that row) — the
+        // points near the bottom edge, ~10 % of them at level 3, no longer
+        // wait for global loads
+        if (iy == h - 1 && ix >= c.x0 && ix + 1 < c.x0 + kCW && iy >= c.y0 && iy < c.y0 + kCW) {
+            const int o = (iy - c.y0) * kCW + (ix - c.x0);
+            const double d0 = (double)ld_lds_u8(win, o), d1 = (double)ld_lds_u8(win, o + 1);
+            const double d2 = 0.0, d3 = 0.0;
+            const double xx = x - floor(x);
+            const double yy = y - floor(y);
+            return double((1 - xx) * (1 - yy) * d0 + xx * (1 - yy) * d1 + (1 - xx) * yy * d2 +
+                          xx * yy * d3);
+        }
     }
+#ifdef VISO_PROBE
+    atomicAdd(&g_pfb[w >= 1000 ? 0 : w >= 500 ? 1 : w >= 250 ? 2 : 3], 1ull);
+#endif
     return sample_px(img, w, h, x, y);
 }
 
@@ -1956,6 +1978,18 @@ extern "C" int viso_debug_probe_ring(unsigned long long* log, unsigned long long
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_plog), z1, sizeof(z1)) != hipSuccess) return -2;
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_pexit), z2, sizeof(z2)) != hipSuccess) return -2;
         g_probe_host_seq = 0;
+    }
+    return 0;
+}
+
+// (probe) window misses per level since the last reset: out[4]
+extern "C" int viso_debug_probe_window_misses(unsigned long long* out, int reset) {
+    using namespace viso;
+    if (hipDeviceSynchronize() != hipSuccess) return -2;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pfb), 4 * sizeof(unsigned long long)) != hipSuccess) return -2;
+    if (reset) {
+        static const unsigned long long z[4] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_pfb), z, sizeof(z)) != hipSuccess) return -2;
     }
     return 0;
 }
