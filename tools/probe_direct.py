@@ -61,7 +61,7 @@ def main():
     v.synchronize()
     assert lib.viso_debug_probe_ring(log.ctypes.data, exits.ctypes.data, cap, ctypes.byref(nl), 1) == 0
     lib.viso_debug_probe_lk(lkbuf, 1)
-    wm = (ctypes.c_ulonglong * 4)()
+    wm = (ctypes.c_ulonglong * 8)()
     has_wm = hasattr(lib, "viso_debug_probe_window_misses")
     if has_wm:
         lib.viso_debug_probe_window_misses(wm, 1)
@@ -69,7 +69,9 @@ def main():
     v.synchronize()
     if has_wm:
         lib.viso_debug_probe_window_misses(wm, 0)
-        print("current-image samples outside their LDS window, per level (L0..L3): " + ", ".join(str(x) for x in wm))
+        print("current-image samples outside their LDS window, per level (L0..L3): " +
+              ", ".join(str(x) for x in list(wm)[:4]))
+        print(f"merged L(3) points with a lane re-loading its `last` taps: {wm[4]} of {wm[5]}")
     print(f"map points {len(v.GetPoints())}, state {v.state}")
     assert lib.viso_debug_probe_ring(log.ctypes.data, exits.ctypes.data, cap, ctypes.byref(nl), 0) == 0
     n = min(nl.value, cap)

@@ -322,7 +322,9 @@ __device__ inline void win_store(uint8_t* lds, const CurWin& c) {
 
 #ifdef VISO_PROBE
 // (probe) current-image samples that missed their LDS window, per level
-__device__ unsigned long long g_pfb[4];
+// [0..3]; merged L(3) points whose `last` taps some lane reloaded [4], and
+// all merged L(3) points [5]
+__device__ unsigned long long g_pfb[8];
 #endif
 
 // sample_px with the taps served from the window when all four lie in it
@@ -760,6 +762,15 @@ __device__ inline void merged_ref(const DirectArgs& a, const LevelPair& fp, int 
     const long long base = (long long)(int)y * (long long)w + (long long)(int)x;
     const double xp = pf.ur[j] + px, yp = pf.vr[j] + py;
     const long long bp = pf.ok[j] ? (long long)(int)yp * (long long)w + (long long)(int)xp : -(1LL << 40);
+#ifdef VISO_PROBE
+    {
+        const unsigned long long rl = __ballot(base != bp);
+        if (lane == 0) {
+            atomicAdd(&g_pfb[5], 1ull);
+            if (rl) atomicAdd(&g_pfb[4], 1ull);
+        }
+    }
+#endif
     if (__builtin_expect(base == bp, 1)) {
         const uint32_t t = pf.taps[j][lane];
         r.t0 = (int)(t & 0xff);
@@ -1982,13 +1993,13 @@ extern "C" int viso_debug_probe_ring(unsigned long long* log, unsigned long long
     return 0;
 }
 
-// (probe) window misses per level since the last reset: out[4]
+// (probe) window misses per level since the last reset: out[8] (g_pfb)
 extern "C" int viso_debug_probe_window_misses(unsigned long long* out, int reset) {
     using namespace viso;
     if (hipDeviceSynchronize() != hipSuccess) return -2;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pfb), 4 * sizeof(unsigned long long)) != hipSuccess) return -2;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pfb), 8 * sizeof(unsigned long long)) != hipSuccess) return -2;
     if (reset) {
-        static const unsigned long long z[4] = {};
+        static const unsigned long long z[8] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_pfb), z, sizeof(z)) != hipSuccess) return -2;
     }
     return 0;
