@@ -129,6 +129,9 @@ int viso_destroy(viso_ctx* c) {
 
 int viso_synchronize(viso_ctx* c) {
     if (!c) return VISO_ERR_ARG;
+    VISO_HIP_CHECK(hipSetDevice(c->device));
+    // what host-frame calls left pending (their last final solve, queued LK)
+    if (int rc = c->settle()) return rc;
     // the pose log's new entries ride this sync into pinned memory, so a
     // viso_get_poses after it makes no device round trip of its own
     {
@@ -165,6 +168,7 @@ int viso_timing_get(viso_ctx* c, int32_t kernel, int64_t* launches, double* tota
 int viso_pyramid(viso_ctx* c, const uint8_t* images, int32_t n, int32_t width, int32_t height,
                  uint8_t* out) {
     if (!c || !images || !out || n <= 0 || width < 8 || height < 8) return VISO_ERR_ARG;
+    if (int rc = c->settle()) return rc;  // (host-frame work left pending)
     VISO_HIP_CHECK(hipSetDevice(c->device));
     PyrGeom g = make_geom(width, height);
     int rc = c->scratch_a.ensure(g.slot * (size_t)n);
@@ -189,6 +193,7 @@ int viso_pyramid(viso_ctx* c, const uint8_t* images, int32_t n, int32_t width, i
 int viso_fast(viso_ctx* c, const uint8_t* image, int32_t width, int32_t height, int32_t thresh,
               int32_t* xs, int32_t* ys, int32_t* scores, size_t cap, size_t* n) {
     if (!c || !image || width < 8 || height < 8 || width > kMaxWidth) return VISO_ERR_ARG;
+    if (int rc = c->settle()) return rc;  // (host-frame work left pending)
     VISO_HIP_CHECK(hipSetDevice(c->device));
     const size_t npx = (size_t)width * height;
     const size_t kcap = std::max<size_t>(cap, 1);
@@ -232,6 +237,7 @@ extern "C" {
 int viso_klt(viso_ctx* c, const uint8_t* ref_pyr, const uint8_t* cur_pyr, int32_t width,
              int32_t height, const float* kp1, float* kp2, uint8_t* success, int32_t n) {
     if (!c || !ref_pyr || !cur_pyr || n < 0 || width < 16 || height < 16) return VISO_ERR_ARG;
+    if (int rc = c->settle()) return rc;  // (host-frame work left pending)
     if (n == 0) return VISO_OK;
     if (!kp1 || !kp2 || !success) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(c->device));
@@ -265,6 +271,7 @@ int viso_direct_pose(viso_ctx* c, const uint8_t* last_pyr, const uint8_t* cur_py
                      double pose_io[12]) {
     if (!c || !last_pyr || !cur_pyr || !pose_last || !pose_io || n < 0 || n > kMaxMapPoints)
         return VISO_ERR_ARG;
+    if (int rc = c->settle()) return rc;  // (host-frame work left pending)
     if (n > 0 && !points) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(c->device));
     PyrGeom g = make_geom(width, height);
@@ -302,6 +309,7 @@ int viso_lk_align(viso_ctx* c, const uint8_t* kf_pyrs, const double* kf_poses, i
     if (!c || !kf_pyrs || !kf_poses || n_kf <= 0 || n_kf > kMaxKeyframes || !cur_pyr || !cur_pose ||
         n < 0)
         return VISO_ERR_ARG;
+    if (int rc = c->settle()) return rc;  // (host-frame work left pending)
     if (n == 0) return VISO_OK;
     if (!points || !pair_kf || !success || !uv_before || !uv_after) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(c->device));
@@ -361,6 +369,7 @@ int viso_lk_align(viso_ctx* c, const uint8_t* kf_pyrs, const double* kf_poses, i
 extern "C" int viso_set_stereo(viso_ctx* c, double baseline, int32_t max_disp, int32_t min_disp) {
     if (!c || !(baseline >= 0) || (baseline > 0 && (max_disp < 2 || min_disp < 1 || min_disp >= max_disp)))
         return VISO_ERR_ARG;
+    if (int rc = c->settle()) return rc;  // (host-frame work left pending)
     c->stereo_base = baseline;
     c->stereo_max_disp = max_disp;
     c->stereo_min_disp = min_disp;
@@ -369,6 +378,7 @@ extern "C" int viso_set_stereo(viso_ctx* c, double baseline, int32_t max_disp, i
 
 extern "C" int viso_set_keyframes(viso_ctx* c, int32_t interval, int32_t ngood_permille) {
     if (!c || interval < 0 || ngood_permille < 0 || ngood_permille > 1000) return VISO_ERR_ARG;
+    if (int rc = c->settle()) return rc;  // (host-frame work left pending)
     c->kf_interval = interval;
     c->kf_permille = ngood_permille;
     return VISO_OK;
@@ -376,6 +386,7 @@ extern "C" int viso_set_keyframes(viso_ctx* c, int32_t interval, int32_t ngood_p
 
 extern "C" int viso_set_bundle_adjust(viso_ctx* c, int32_t iterations) {
     if (!c || iterations < 0 || iterations > 100) return VISO_ERR_ARG;
+    if (int rc = c->settle()) return rc;  // (host-frame work left pending)
     c->ba_iterations = iterations;
     return VISO_OK;
 }
@@ -384,6 +395,7 @@ extern "C" int viso_photometric_ba(viso_ctx* c, const uint8_t* const* kf_images,
                                    double* points, const int32_t* host, int32_t n, int32_t iterations,
                                    double* report) {
     if (!c || !kf_images || !kf_poses || !points || !host) return VISO_ERR_ARG;
+    if (int rc = c->settle()) return rc;  // (host-frame work left pending)
     // n bounded as the pipeline's map (the block trees' stack depth and the
     // launch grids are sized for kMaxMapPoints)
     if (n_kf < 2 || n_kf > kMaxKeyframes || n < 1 || n > kMaxMapPoints || iterations < 1 || iterations > 100)
@@ -428,6 +440,7 @@ extern "C" int viso_stereo_match(viso_ctx* c, const uint8_t* left, const uint8_t
                                  int32_t* disparity, int32_t* sad) {
     if (!c || !left || !right || width < 8 || height < 8 || n < 0 || max_disp < 0)
         return VISO_ERR_ARG;
+    if (int rc = c->settle()) return rc;  // (host-frame work left pending)
     if (n == 0) return VISO_OK;
     if (!xs || !ys || !disparity || !sad) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(c->device));

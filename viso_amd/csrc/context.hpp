@@ -286,6 +286,17 @@ struct viso_ctx {
     int resolve_direct();
     // end of an ingest call: pending final solve, then the LK batch on `s`
     int finish_call(hipStream_t s);
+    // end of a host-frame call (viso_process_frame / _stereo) while
+    // tracking: the final solve stays pending (the next frame's L(3) runs
+    // it, as inside a device chunk) and the LK alignment of every queued
+    // frame but the last goes out in batches; settle() launches what is
+    // pending before anything reads it or changes what it depends on
+    // (getters, viso_synchronize, setters, stage calls, device ingest)
+    int finish_host_call();
+    int settle();
+    int host_lk_batch() const;
+    // LK batch of lk_pending on `s` (all but the last frame: keep_last)
+    int flush_lk_frames(hipStream_t s, bool keep_last);
     // LK alignment of a device-ingest chunk in the background of its
     // direct-pose chain (track.hip lk_item_kernel): bg_begin after the chunk's
     // pyramid when the context is tracking (frames of the chunk: their slots),

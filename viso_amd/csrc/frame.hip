@@ -438,8 +438,15 @@ LkAlignArgs viso_ctx::lk_args() {
     return a;
 }
 
-int viso_ctx::flush_lk(hipStream_t ls) {
-    if (lk_pending.empty()) return VISO_OK;
+int viso_ctx::flush_lk(hipStream_t ls) { return flush_lk_frames(ls, false); }
+
+int viso_ctx::flush_lk_frames(hipStream_t ls, bool keep_last) {
+    if (lk_pending.empty() || (keep_last && lk_pending.size() < 2)) return VISO_OK;
+    int kept = -1;
+    if (keep_last) {
+        kept = lk_pending.back();
+        lk_pending.pop_back();
+    }
     LkAlignArgs a = lk_args();
     a.n_frames = (int)lk_pending.size();
     for (int f = 0; f < a.n_frames; ++f) {
@@ -476,7 +483,32 @@ int viso_ctx::flush_lk(hipStream_t ls) {
     }
     for (int s : lk_pending) drop(s);
     lk_pending.clear();
+    if (kept >= 0) lk_pending.push_back(kept);
     return VISO_OK;
+}
+
+// Frames of LK alignment a host-frame caller may leave queued: each holds its
+// slot, so the pool keeps room for the roles (ref, last, keyframes) and the
+// next frames.
+int viso_ctx::host_lk_batch() const {
+    const int room = (n_slots - (int)kf_slots.size() - 6) / 2;
+    return std::max(1, std::min(8, room));
+}
+
+int viso_ctx::finish_host_call() {
+    // outside tracking, and with keyframe insertion (its decision reads the
+    // frame's nGood at once), as every other call
+    if (state != VISO_STATE_RUNNING || kf_interval > 0 || bg_active) return finish_call(lk_stream);
+    // the queued frames but the last have their final poses on the context
+    // stream by now (each one's final solve ran in its successor's L(3))
+    if ((int)lk_pending.size() > host_lk_batch()) return flush_lk_frames(lk_stream, true);
+    return VISO_OK;
+}
+
+int viso_ctx::settle() {
+    if (!dpend && lk_pending.empty()) return VISO_OK;
+    VISO_HIP_CHECK(hipSetDevice(device));
+    return finish_call(lk_stream);
 }
 
 int viso_ctx::resolve_direct() {
@@ -1119,7 +1151,7 @@ int viso_process_frame(viso_ctx* c, const uint8_t* grey, int32_t width, int32_t 
     VISO_HIP_CHECK(hipGetLastError());
     rc = c->on_new_frame(s);
     if (rc) return rc;
-    rc = c->finish_call(c->lk_stream);
+    rc = c->finish_host_call();
     const int re = c->end_epoch();
     return rc ? rc : re;
 }
@@ -1150,7 +1182,7 @@ int viso_process_stereo(viso_ctx* c, const uint8_t* left, const uint8_t* right,
     c->right_l0 = nullptr;
     c->drop(sr);
     if (rc) return rc;
-    rc = c->finish_call(c->lk_stream);
+    rc = c->finish_host_call();
     const int re = c->end_epoch();
     return rc ? rc : re;
 }
@@ -1158,6 +1190,7 @@ int viso_process_stereo(viso_ctx* c, const uint8_t* left, const uint8_t* right,
 int viso_process_frames_device(viso_ctx* c, const uint8_t* d_left, const uint8_t* d_right,
                                int32_t n, size_t frame_stride) {
     if (!c || !d_left || n < 0) return VISO_ERR_ARG;
+    if (int rc = c->settle()) return rc;  // (host-frame work left pending)
     if (frame_stride < (size_t)c->geom.w[0] * c->geom.h[0]) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(c->device));
     const int B = c->p.batch_frames;
@@ -1247,6 +1280,7 @@ int viso_get_state(viso_ctx* c, int32_t* state) {
 
 int viso_get_poses(viso_ctx* c, double* Tcw12, size_t cap, size_t* n) {
     if (!c) return VISO_ERR_ARG;
+    if (int rc = c->settle()) return rc;  // (host-frame work left pending)
     // the count is host state (one pose per launched tracking frame): asking
     // for it alone needs no device round trip
     if (n) *n = (size_t)c->n_poses;
@@ -1284,6 +1318,7 @@ int viso_get_poses(viso_ctx* c, double* Tcw12, size_t cap, size_t* n) {
 
 int viso_get_points(viso_ctx* c, double* xyz, size_t cap, size_t* n) {
     if (!c) return VISO_ERR_ARG;
+    if (int rc = c->settle()) return rc;  // (host-frame work left pending)
     VISO_HIP_CHECK(hipSetDevice(c->device));
     const size_t m = std::min(cap, (size_t)c->n_map);
     if (m > 0 && xyz)
@@ -1328,6 +1363,7 @@ int viso_get_init_tracks(viso_ctx* c, float* kp1, float* kp2, uint8_t* success, 
 int viso_get_alignment(viso_ctx* c, int32_t* pair_kf, uint8_t* success, double* uv_before,
                        double* uv_after, size_t cap, size_t* n) {
     if (!c) return VISO_ERR_ARG;
+    if (int rc = c->settle()) return rc;  // (host-frame work left pending)
     VISO_HIP_CHECK(hipSetDevice(c->device));
     VISO_HIP_CHECK(hipStreamSynchronize(c->lk_stream));
     if (int rc = c->bg_check()) return rc;
@@ -1346,6 +1382,7 @@ int viso_get_alignment(viso_ctx* c, int32_t* pair_kf, uint8_t* success, double* 
 
 int viso_get_frame_stats(viso_ctx* c, double out[16]) {
     if (!c || !out) return VISO_ERR_ARG;
+    if (int rc = c->settle()) return rc;  // (host-frame work left pending)
     VISO_HIP_CHECK(hipSetDevice(c->device));
     if (int rc = c->resolve_ntrack()) return rc;
     std::memcpy(out, c->stats, sizeof(c->stats));
@@ -1380,6 +1417,7 @@ int viso_pose_2d2d(viso_ctx* c, const double* p1, const double* p2, int32_t n, d
                    double T[3], uint8_t* inliers, double* points3d, double* candidates,
                    double stats[8]) {
     if (!c || n < 0 || n > c->p.max_features || !R || !T || !stats) return VISO_ERR_ARG;
+    if (int rc = c->settle()) return rc;  // (host-frame work left pending)
     if (n > 0 && (!p1 || !p2)) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(c->device));
     int rc = c->scratch_d.ensure(48 * (size_t)std::max(n, 1) + 512);
