@@ -84,8 +84,13 @@ int viso_destroy(viso_ctx* ctx);
 
 /* FrameSequence::FrameHandler::OnNewFrame(Keyframe::Ptr)
  * (include/frame_sequence.h:13-16, implemented by Viso::OnNewFrame,
- * src/viso.cpp:7-145).  `grey`: width x height u8 rows, `stride` bytes apart.
- * Builds the 4-level pyramid (Keyframe ctor, include/keyframe.h:28-46). */
+ * src/viso.cpp:7-145).  `grey`: width x height u8 rows, `stride` bytes apart
+ * (copied before the call returns).  Builds the 4-level pyramid (Keyframe
+ * ctor, include/keyframe.h:28-46).  Asynchronous: while tracking, the
+ * frame's last pose step and its LK alignment may still be queued when the
+ * call returns; every other call on the context (getters,
+ * viso_synchronize, setters, stage calls, device ingest) launches them
+ * first, so results read through the API are always complete. */
 int viso_process_frame(viso_ctx* ctx, const uint8_t* grey, int32_t width, int32_t height,
                        int32_t stride);
 
