@@ -139,7 +139,7 @@ struct viso_ctx {
     // the ingest's pyramid launch(es) with its last frame's PyrOwn (level 0
     // owned, identity pose outside tracking)
     void launch_ingest_pyramid(const uint8_t* const* l0, uint8_t* const* dst, const int* sl, int n,
-                               bool bg_words = false);
+                               bool bg_words = false, hipStream_t st = nullptr);
 
     // ---------------- initialisation tracks (Viso::Initialization, include/viso.h:33-41)
     viso::DevBuf kp1, kp2, kp1b, kp2b, track_success, n_track_dev;
@@ -217,7 +217,8 @@ struct viso_ctx {
     hipEvent_t epoch_now = nullptr;  // a slot freed in the current call (rare)
     int end_epoch();
     int create_up_stream();
-    int upload_host(int s, const uint8_t* grey, int32_t w, int32_t h, int32_t stride);
+    int upload_host(int s, const uint8_t* grey, int32_t w, int32_t h, int32_t stride, bool pyramid);
+    hipEvent_t up_done = nullptr;  // behind a host frame's upload + pyramid
     // PoseEstimation2d2d's E path runs on lk_stream beside the H path (no LK
     // alignment runs while initialising): fork / join events
     hipEvent_t geo_fork = nullptr, geo_join = nullptr;
@@ -279,7 +280,8 @@ struct viso_ctx {
     int build_lk_templates();
     // OnNewFrame on a frame whose pyramid is already built in `slot`
     int on_new_frame(int slot);
-    int ingest_host(const uint8_t* grey, int32_t w, int32_t h, int32_t stride, int* slot_out);
+    // (pyramid: the frame's pyramid too, on the upload stream)
+    int ingest_host(const uint8_t* grey, int32_t w, int32_t h, int32_t stride, int* slot_out, bool pyramid = false);
     // launch LKAlignment of every pending tracking frame (on `s`)
     int flush_lk(hipStream_t s);
     // launch the pending final solve, if any

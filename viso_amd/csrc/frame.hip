@@ -166,6 +166,7 @@ int viso_ctx::init() {
     VISO_HIP_CHECK(hipEventCreateWithFlags(&gate_evt, hipEventDisableTiming));
     for (auto& e : epoch_evt) VISO_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     VISO_HIP_CHECK(hipEventCreateWithFlags(&epoch_now, hipEventDisableTiming));
+    VISO_HIP_CHECK(hipEventCreateWithFlags(&up_done, hipEventDisableTiming));
     if (const char* e = getenv("VISO_GATE_SPEC")) gate_spec_mode = e[0] == '1' ? 1 : 0;
     rc = bg_prepare();
     if (rc) return rc;
@@ -200,6 +201,8 @@ void viso_ctx::release() {
     }
     if (epoch_now) (void)hipEventDestroy(epoch_now);
     epoch_now = nullptr;
+    if (up_done) (void)hipEventDestroy(up_done);
+    up_done = nullptr;
     DevBuf* bufs[] = {&scratch_a, &scratch_b, &scratch_c, &scratch_d, &slot_pool, &slot_pose,
                       &kp1, &kp2, &kp1b, &kp2b, &track_success, &n_track_dev, &fast_rows,
                       &geo_buf, &map_pts, &kf_poses, &direct_buf, &direct_stats,
@@ -298,7 +301,7 @@ int viso_ctx::end_epoch() {
 // stream: behind the slot's last readers (its lk_stream batch: acquire_slot;
 // the context stream's: the epoch that freed it), and the context stream
 // waits for the DMA before the frame's pyramid.
-int viso_ctx::upload_host(int s, const uint8_t* grey, int32_t w, int32_t h, int32_t stride) {
+int viso_ctx::upload_host(int s, const uint8_t* grey, int32_t w, int32_t h, int32_t stride, bool pyramid) {
     const int64_t fe = slots[(size_t)s].free_epoch;
     if (fe >= 0) {
         if (fe < epoch) {
@@ -313,7 +316,18 @@ int viso_ctx::upload_host(int s, const uint8_t* grey, int32_t w, int32_t h, int3
         TimedRegion t(timing, VISO_KERNEL_UPLOAD, up_stream);
         VISO_HIP_CHECK(stage.upload(slot_base(s), grey, w, h, stride, up_stream));
     }
-    VISO_HIP_CHECK(hipStreamWaitEvent(stream, stage.last, 0));
+    if (!pyramid) {
+        VISO_HIP_CHECK(hipStreamWaitEvent(stream, stage.last, 0));
+        return VISO_OK;
+    }
+    // the frame's pyramid behind its upload, on the same stream: both beside
+    // the previous frame's chain
+    uint8_t* slot = slot_base(s);
+    const uint8_t* l0 = slot;
+    launch_ingest_pyramid(&l0, &slot, &s, 1, false, up_stream);
+    VISO_HIP_CHECK(hipGetLastError());
+    VISO_HIP_CHECK(hipEventRecord(up_done, up_stream));
+    VISO_HIP_CHECK(hipStreamWaitEvent(stream, up_done, 0));
     return VISO_OK;
 }
 
@@ -372,7 +386,8 @@ static constexpr size_t kBgWords = kLkBatch + 8 * 32 + 32 + 32 + 4096;
 // frame's Keyframe-ctor pose (R = I, T = 0; on_new_frame skips its launch) —
 // a frame-by-frame caller pays two launches fewer per frame.
 void viso_ctx::launch_ingest_pyramid(const uint8_t* const* l0, uint8_t* const* dst, const int* sl, int n,
-                                     bool bg_words) {
+                                     bool bg_words, hipStream_t st) {
+    if (!st) st = stream;
     const int s = sl[n - 1];
     PyrOwn own{n - 1, state != VISO_STATE_RUNNING ? pose_of(s) : nullptr, false};
     if (bg_words) {  // the chunk's background-LK words (bg_begin), cleared by the tail launch
@@ -381,8 +396,8 @@ void viso_ctx::launch_ingest_pyramid(const uint8_t* const* l0, uint8_t* const* d
     }
     ident_slot = own.ident_pose ? s : -1;
     {
-        TimedRegion t(timing, VISO_KERNEL_PYRAMID, stream);
-        launch_pyramid_frames(geom, l0, dst, n, stream, &own);
+        TimedRegion t(timing, VISO_KERNEL_PYRAMID, st);
+        launch_pyramid_frames(geom, l0, dst, n, st, &own);
     }
     SlotRec& r = slots[(size_t)s];
     if (r.borrowed && own.copied) {
@@ -391,7 +406,7 @@ void viso_ctx::launch_ingest_pyramid(const uint8_t* const* l0, uint8_t* const* d
     }
 }
 
-int viso_ctx::ingest_host(const uint8_t* grey, int32_t w, int32_t h, int32_t stride, int* slot_out) {
+int viso_ctx::ingest_host(const uint8_t* grey, int32_t w, int32_t h, int32_t stride, int* slot_out, bool pyramid) {
     if (w != p.width || h != p.height || stride < w || !grey) return VISO_ERR_ARG;
     if (!up_stream) {
         int rc = create_up_stream();
@@ -401,7 +416,7 @@ int viso_ctx::ingest_host(const uint8_t* grey, int32_t w, int32_t h, int32_t str
     if (s < 0) return VISO_ERR_CAPACITY;
     // through pinned staging (staging.hpp: a pageable hipMemcpy2DAsync
     // measured 3.25 ms per 1242x375 frame), on the upload stream
-    const int rc = upload_host(s, grey, w, h, stride);
+    const int rc = upload_host(s, grey, w, h, stride, pyramid);
     if (rc) {
         hold(s);
         drop(s);
@@ -1143,12 +1158,9 @@ int viso_process_frame(viso_ctx* c, const uint8_t* grey, int32_t width, int32_t 
     if (!c) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(c->device));
     int s = -1;
-    int rc = c->ingest_host(grey, width, height, stride, &s);
+    // upload and pyramid on the upload stream (ingest_host)
+    int rc = c->ingest_host(grey, width, height, stride, &s, true);
     if (rc) return rc;
-    uint8_t* slot = c->slot_base(s);
-    const uint8_t* l0 = slot;
-    c->launch_ingest_pyramid(&l0, &slot, &s, 1);
-    VISO_HIP_CHECK(hipGetLastError());
     rc = c->on_new_frame(s);
     if (rc) return rc;
     rc = c->finish_host_call();
@@ -1161,18 +1173,14 @@ int viso_process_stereo(viso_ctx* c, const uint8_t* left, const uint8_t* right,
     if (!c || !left || !right || !dims) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(c->device));
     int sl = -1, sr = -1;
-    int rc = c->ingest_host(left, dims[0], dims[1], dims[2], &sl);
+    int rc = c->ingest_host(left, dims[0], dims[1], dims[2], &sl, true);
     if (rc) return rc;
-    rc = c->ingest_host(right, dims[0], dims[1], dims[2], &sr);
+    rc = c->ingest_host(right, dims[0], dims[1], dims[2], &sr, false);
     if (rc) {
         c->hold(sl);
         c->drop(sl);
         return rc;
     }
-    uint8_t* slot = c->slot_base(sl);
-    const uint8_t* l0 = slot;
-    c->launch_ingest_pyramid(&l0, &slot, &sl, 1);
-    VISO_HIP_CHECK(hipGetLastError());
     // the right image feeds the stereo initialisation (viso_set_stereo), which
     // reads its level 0 only: no pyramid is built for it; the reference path
     // runs on the left image only
