@@ -1054,7 +1054,9 @@ __global__ __launch_bounds__(kThreads, 4) void direct_level_kernel(const double*
                                                                  const int* __restrict__ pre_good, int pre_hdr,
                                                                  DirectArgs a) {
     PROBE_DECL();
-    if (pre_hdr & kHdrBg) __builtin_amdgcn_s_setprio(1);
+    // the chain's waves outrank co-resident LK alignment waves (the
+    // background grid, or a host-frame call's LK batch on the side stream)
+    __builtin_amdgcn_s_setprio(1);
     __shared__ SolveLds L;
     __shared__ double s_pose[12];
     __shared__ double s_last[12];  // merged L(3): this frame's `last` pose
@@ -1182,10 +1184,7 @@ __global__ __launch_bounds__(kThreads, 4) void direct_level_kernel(const double*
             solve_wave0(L, 0, stp);
 #endif
         PST(7);
-        if (pre_hdr & kHdrBg)
-            __builtin_amdgcn_s_setprio(1);
-        else
-            __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_setprio(1);
     }
     if (!solve && wave == 0 && lane == 0) {
         // seeded level: no solve, T21 is the seed (thread 256 wrote it)
