@@ -830,7 +830,9 @@ def main():
         traffic, tsrc = pyramid_traffic(W, H, imgs_per_launch)
         roofline = {"kernel": "image pass of one ingest chunk: pyr_down_sk (level 1) + pyr_tail (levels 2-3) "
                               "(algorithmic bytes = "
-                              "L0 read + L1..L3 write per image)", "bound": "hbm",
+                              "L0 read + L1..L3 write per image; not counted: the tail launch of a chunk of "
+                              "<= 32 frames also copies the chunk's last level 0 into its slot, which the "
+                              "library keeps as last_frame, and clears the background-LK words)", "bound": "hbm",
                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "traffic_source": tsrc,
