@@ -492,9 +492,11 @@ def measure_host_ingest(args, seq, W, H, left, right, log, n=32, warm=4):
            "host_enqueue_us_per_frame": round(1e6 * (t1 - t0) / n, 1),
            "split_us_per_frame": split,
            "split_note": "pass 2 (frames %d-%d) with HIP events around each group; direct = the frame's four level "
-                         "launches plus its final solve (a single-frame call ends with a standalone F launch); "
-                         "lkalign = the frame's LK batch on the side stream; final sync host time in sync_us"
+                         "launches, the previous frame's final solve merged into its L(3) (a frame's own final "
+                         "solve stays pending until the next call); lkalign = side-stream batches of up to "
+                         "host_lk_batch() (<= 8) queued frames; final sync host time in sync_us"
                          % (f0 + n, f0 + 2 * n - 1),
+           "frames_total": f0 + 2 * n,
            "sync_us": round(1e6 * (t4 - t3), 1),
            "_poses": poses}
     log(f"[host_ingest] {out['value']} frames/s ({out['us_per_frame']} us per frame)")
@@ -535,7 +537,16 @@ def measure_config2(args, log):
     fb = W * H
     # (1) reference path: init + tracking
     vk, _, _, _ = run_reference_init(seq, W, H, d_left, 6, 2, n_track)  # warm-up (kernel breakdown)
-    v, per, n_init, dt = run_reference_init(seq, W, H, d_left, 6, n_track, n_track, timing=False)
+    # three clocked passes, the median reported (one round-6 run showed a
+    # single 8 ms stall in this leg that two A/B reruns did not reproduce,
+    # gpurun_out/r06b)
+    passes = []
+    for _ in range(3):
+        passes.append(run_reference_init(seq, W, H, d_left, 6, n_track, n_track, timing=False))
+    order = sorted(range(3), key=lambda i: passes[i][3] if passes[i][3] else float("inf"))
+    for i in order[:1] + order[2:]:
+        passes[i][0].close()
+    v, per, n_init, dt = passes[order[1]]
     out = {"workload": "configs[2]: synthetic 1920x1080 grey sequence, ~8k FAST@50 corners per frame, "
                        "reference path (monocular init with E-1000 / H-2000 RANSAC, then direct pose + LK "
                        "alignment), frames resident in HBM",
@@ -545,6 +556,7 @@ def measure_config2(args, log):
            "init_frame_us": round(float(np.mean(per[1:])), 1) if len(per) > 1 else None,
            "tracking_frames": n_track if dt else 0,
            "tracking_frames_per_s": round(n_track / dt, 1) if dt else None,
+           "tracking_frames_per_s_passes": [round(n_track / p[3], 1) if p[3] else None for p in passes],
            "map_points": int(len(v.GetPoints())),
            "init_kernels": init_kernels(vk)}
     log(f"[config2] init {out['init_frame_us']} us/frame, tracking {out['tracking_frames_per_s']} frames/s")
@@ -926,7 +938,12 @@ def main():
                       "rmse_translation": float(np.sqrt(np.mean(np.sum((gP[:m, 9:] - oP[:m, 9:]) ** 2, 1))))}
         if host_ingest is not None:
             # the oracle's frames 0.. (stereo initialisation at frame 0, then
-            # tracking; the right image only feeds the initialisation)
+            # tracking; the right image only feeds the initialisation),
+            # continued untimed past the CPU sample so every frame the leg ran
+            # is compared
+            for f in range(warm + n_cpu, min(host_ingest["frames_total"], len(left))):
+                ov.on_new_stereo(left[f], right[f])
+            oP = ov.poses()
             hP = host_ingest["_poses"]
             mh = min(len(oP), len(hP))
             if mh:

@@ -90,7 +90,9 @@ int viso_destroy(viso_ctx* ctx);
  * frame's last pose step and its LK alignment may still be queued when the
  * call returns; every other call on the context (getters,
  * viso_synchronize, setters, stage calls, device ingest) launches them
- * first, so results read through the API are always complete. */
+ * first, so results read through the API are always complete.  An error of
+ * that deferred work (frame k's final solve or LK batch) is returned by the
+ * call that launches it — the next call on the context — not by frame k's. */
 int viso_process_frame(viso_ctx* ctx, const uint8_t* grey, int32_t width, int32_t height,
                        int32_t stride);
 
@@ -141,6 +143,29 @@ int viso_get_alignment(viso_ctx* ctx, int32_t* pair_kf, uint8_t* success, double
  * (level 0), [10] direct-pose cost (level 0), [11] frames processed,
  * [12] init succeeded on this frame, [13..15] reserved. */
 int viso_get_frame_stats(viso_ctx* ctx, double stats[16]);
+/* Per-frame log (structured per-frame statistics, every tracking frame
+ * rather than the last one; no reference counterpart — the reference prints
+ * nGood / cost per level, src/viso.cpp:755-757).  enable != 0 allocates
+ * max_poses rows of 4 doubles on the device: for the tracking frame with
+ * pose index k (the k-th entry of viso_get_poses), row k = {level-0 nGood,
+ * level-0 cost (as viso_get_frame_stats [9], [10]), LK alignment pairs,
+ * LK alignment successes (as [6], [7])}, written by the kernels themselves
+ * (the direct pose's logging thread; one counting launch per LK batch);
+ * rows of frames processed while it was off read NaN.  enable = 0 frees it. */
+int viso_set_frame_log(viso_ctx* ctx, int32_t enable);
+/* The context's execution resources (no reference counterpart), 8 ints:
+ * [0] LK alignment of device-ingest chunks in the background of the direct
+ *     chain (1) or batched after it (0: VISO_LK_BG=0, serialised kernels, or
+ *     no side queue of its own could be made),
+ * [1] the LK side stream has a hardware queue of its own (CU-masked stream),
+ * [2] the host-upload stream likewise (-1: not created yet, it is made by the
+ *     first host frame),
+ * [3] frame slots in the pool, [4] per-frame log on, [5] batch_frames,
+ * [6..7] reserved (0).  See INTEGRATION.md §4 for the queue budget. */
+int viso_get_config(viso_ctx* ctx, int32_t info[8]);
+/* The first min(cap, poses) rows (4 doubles each) of the per-frame log; *n =
+ * the pose count.  VISO_ERR_STATE when the log is off. */
+int viso_get_frame_log(viso_ctx* ctx, double* rows, size_t cap, size_t* n);
 
 /* Kernel timing (HIP events on the context stream) for roofline accounting.
  * kernel ids: see VISO_KERNEL_*.  When enabled, every launch of the kernel
@@ -156,6 +181,9 @@ int viso_get_frame_stats(viso_ctx* ctx, double stats[16]);
 #define VISO_KERNEL_STEREO 7
 #define VISO_KERNEL_UPLOAD 8 /* host -> device copy of a frame (viso_process_frame / _stereo) */
 #define VISO_KERNEL_COUNT 9
+/* (timing_get first launches what host-frame calls left pending, as the
+ * getters do; an error of a frame's deferred work — its final solve or LK
+ * batch — is returned by the next call on the context that launches it) */
 int viso_timing_enable(viso_ctx* ctx, int32_t enable);
 /* Restrict timing to the kernels whose bit (1 << VISO_KERNEL_*) is set
  * (default: all).  Each timed region records two events on its stream. */

@@ -64,6 +64,81 @@ def _oracle_stereo_poses(seed, n, W=1242, H=375):
 # ------------------------------------------------------------------ configs[1]
 _C1 = dict(W=1242, H=375, warm=5, steps=20)
 
+# bench.py's default line: --warmup 20 (one call; frame 0's stereo pair
+# creates the map), then --steps 256 in --batch 128 calls
+_C1L = dict(W=1242, H=375, warm=20, steps=256, batch=128)
+
+
+@pytest.mark.gpu
+def test_gpu_config1_200_frames_faithful():
+    """configs[1] at (beyond) its stated length, "first 200 stereo pairs": the
+    bench's default workload frame for frame — 20 warm-up frames in one call
+    (stereo initialisation at frame 0, then 19 tracking frames whose LK
+    alignment runs batched after the chain), then 256 tracking frames in two
+    128-frame calls, each cut into 64-frame chunks with the chunk-resident
+    background LK grid; 276 frames through a pool of 2 x 128 + 8 = 264 slots,
+    so slots are reused.  The reference loop (src/viso.cpp:113-138) against
+    the oracle, faithful: every pose <= 1e-10 rel (north star: 1e-4), the map
+    exact, and per frame (viso_set_frame_log) the level-0 direct-pose nGood
+    and cost, LK pairs and LK successes exactly as the oracle's per-frame
+    stats; the last frame's alignment exact; the background grid's error word
+    clear (synchronize raises it otherwise)."""
+    import torch
+
+    import viso_amd
+    from viso_amd.shard import sequence_seed
+    from viso_amd.synth import Sequence
+    W, H, warm, steps, B = _C1L["W"], _C1L["H"], _C1L["warm"], _C1L["steps"], _C1L["batch"]
+    n = warm + steps
+    seq = Sequence(W, H, seed=sequence_seed(0))
+    left = np.stack([seq.image(f, 0) for f in range(n)])
+    right = np.stack([seq.image(f, 1) for f in range(warm)])
+    # the GPU first (the oracle's 276 frames follow on the host)
+    dl, dr = torch.from_numpy(left).cuda(), torch.from_numpy(right).cuda()
+    torch.cuda.synchronize()
+    fb = W * H
+    v = viso_amd.Viso(*seq.K, width=W, height=H, enable_tracking=1, batch_frames=B, max_poses=1024)
+    v.set_stereo(seq.p.baseline, STEREO_MAX_DISP, 1)
+    v.set_frame_log(True)
+    assert v.config()["slots"] == 2 * B + 8 < n
+    v.process_device(dl.data_ptr(), dr.data_ptr(), warm, fb)
+    v.synchronize()
+    assert v.state == 1
+    f = warm
+    while f < n:
+        m = min(B, n - f)
+        v.process_device(dl.data_ptr() + f * fb, None, m, fb)
+        f += m
+    v.synchronize()
+    gP, gp, glog, gal = v.poses, v.GetPoints(), v.frame_log(), v.alignment()
+    assert v.config()["background_lk"] == 1
+    v.close()
+    # the oracle, frame by frame
+    ov = oracle_lib.Viso(seq.K, W, H, enable_tracking=1)
+    ov.set_stereo(seq.p.baseline, STEREO_MAX_DISP, 1)
+    ov.on_new_stereo(left[0], right[0])
+    olog = []
+    for f in range(1, n):
+        ov.on_new_frame(left[f])
+        s = ov.stats()
+        olog.append((s[9], s[10], s[6], s[7]))
+    olog = np.array(olog)
+    assert ov.state == 1
+    op, oP = ov.points(), ov.poses()
+    assert len(op) > 2000 and np.array_equal(gp, op)
+    assert gP.shape == oP.shape == (n - 1, 12)
+    assert _rel_rows(gP, oP).max() <= 1e-10
+    assert glog.shape == olog.shape == (n - 1, 4)
+    assert np.array_equal(glog[:, 0], olog[:, 0]), np.nonzero(glog[:, 0] != olog[:, 0])
+    assert np.array_equal(glog[:, 2], olog[:, 2]), np.nonzero(glog[:, 2] != olog[:, 2])
+    assert np.array_equal(glog[:, 3], olog[:, 3]), np.nonzero(glog[:, 3] != olog[:, 3])
+    assert (np.abs(glog[:, 1] - olog[:, 1]) <= 1e-10 * np.abs(olog[:, 1])).all()
+    assert (olog[:, 2] > 0).all()  # every tracking frame aligned points
+    pk, sc, ub, ua = gal
+    opk, osc, oub, oua = ov.alignment()
+    assert np.array_equal(pk, opk) and np.array_equal(sc, osc)
+    assert np.max(np.abs(ua - oua)) < 1e-6
+
 
 def _config1_oracle():
     """The oracle's run of the config-1 workload (cached: the LK-mode variants

@@ -64,6 +64,9 @@ SIGNATURES = {
     "viso_get_init_tracks": [_vp, _vp, _vp, _vp, _sz, _vp],
     "viso_get_alignment": [_vp, _vp, _vp, _vp, _vp, _sz, _vp],
     "viso_get_frame_stats": [_vp, _vp],
+    "viso_set_frame_log": [_vp, _i32],
+    "viso_get_config": [_vp, _vp],
+    "viso_get_frame_log": [_vp, _vp, _sz, _vp],
     "viso_timing_enable": [_vp, _i32],
     "viso_timing_select": [_vp, ctypes.c_uint32],
     "viso_timing_get": [_vp, _i32, _vp, _vp],

@@ -157,6 +157,9 @@ int viso_timing_select(viso_ctx* c, uint32_t kernel_mask) {
 
 int viso_timing_get(viso_ctx* c, int32_t kernel, int64_t* launches, double* total_ms) {
     if (!c || kernel < 0 || kernel >= VISO_KERNEL_COUNT) return VISO_ERR_ARG;
+    // what host-frame calls left pending (the last frame's final solve and
+    // LK batch) is launched and timed first
+    if (int r = c->settle()) return r;
     int rc = c->timing.collect();
     if (rc != VISO_OK) return rc;
     if (launches) *launches = c->timing.launches[kernel];

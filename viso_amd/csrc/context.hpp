@@ -113,6 +113,7 @@ struct SlotRec {
     int refs = 0;
     int64_t lk_use = -1;  // last lk_stream batch that reads it (lk_seq numbering)
     int64_t free_epoch = -1;  // the ingest call (epoch) during which it was freed
+    int log_index = -1;       // a tracking frame's pose-log index (< 0: not logged)
 };
 constexpr int kEpochRing = 16;
 constexpr int kLkRing = 64;
@@ -175,7 +176,12 @@ struct viso_ctx {
     double* h_poses = nullptr;      // pinned staging of the pose log (viso_get_poses)
     double* h_poses_dev = nullptr;  // its device address (the direct kernels log into it too)
     size_t h_poses_cap = 0;         // poses it holds
-    size_t poses_staged = 0;        // poses whose copy into h_poses is enqueued (finish_call)
+    // poses of h_poses that are final once the context stream has passed the
+    // calls that produced them: advanced by stage_poses (viso_synchronize)
+    // and viso_get_poses.  Entries below h_poses_cap are written into h_poses
+    // by the direct kernels themselves (log_host); the buffer grows
+    // geometrically in viso_get_poses (up to max_poses)
+    size_t poses_staged = 0;
     double* log_host(int index) const {  // the direct launch's log_host for a log index
         return index >= 0 && (size_t)index < h_poses_cap ? h_poses_dev : nullptr;
     }
@@ -230,6 +236,13 @@ struct viso_ctx {
     int dpend_cur = -1, dpend_last = -1, dpend_log = -1;
     viso::DevBuf pose_log;  // max_poses x 12
     int n_poses = 0;
+    // the per-frame log (viso_set_frame_log): max_poses x 4 doubles {level-0
+    // nGood, level-0 cost, LK pairs, LK successes} per logged tracking frame;
+    // null when off
+    viso::DevBuf frame_log;
+    double* flog() const { return (double*)frame_log.ptr; }
+    // the LK columns of the frames in batch rows 0.. (their slots), on `s`
+    int count_lk(const std::vector<int>& row_slots, hipStream_t s);
 
     // ---------------- stereo initialisation (viso_set_stereo; the repo's own
     // replacement of the 2D-2D init, no reference counterpart)
@@ -304,6 +317,8 @@ struct viso_ctx {
     // pyramid when the context is tracking (frames of the chunk: their slots),
     // bg_end once the chunk's last pose is launched
     bool bg_eligible();
+    bool bg_on();  // the background mode itself (VISO_LK_BG, serialised kernels, the side queue)
+    bool lk_dedicated = false, up_dedicated = false;  // lk_stream / up_stream CU-masked (queue of their own)
     // (zeroed: the chunk's pyramid launch cleared the words)
     int bg_begin(const std::vector<int>& chunk, bool zeroed = false);
     int bg_end(bool drain = true);

@@ -165,6 +165,10 @@ struct DirectArgs {
     // once the frame pose (pose_out / prev_pose_out) is stored; may be null
     int* ready;
     int* prev_ready;
+    // the per-frame log (viso_set_frame_log; may be null): [log index][4]
+    // doubles, the level-0 solve's nGood and cost written here beside the
+    // pose log entry (LK pair / success counts by lk_count_kernel)
+    double* flog;
 };
 
 // The frame pose of a direct-pose launch: 12 agent-scope (sc1) stores by one
@@ -190,6 +194,14 @@ __device__ inline void log_pose(double* log, double* log_host, int index, const 
     if (log_host)
         for (int k = 0; k < 12; ++k)
             __hip_atomic_store(log_host + 12 * (size_t)index + k, pose[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// A logged frame's level-0 nGood and cost (the solve's, the values
+// viso_get_frame_stats reports as [9] and [10]); one thread, beside log_pose.
+__device__ inline void log_frame(double* flog, int index, const SolveLds& L) {
+    if (!flog || index < 0) return;
+    flog[4 * (size_t)index + 0] = (double)L.ngood;
+    flog[4 * (size_t)index + 1] = L.cost;
 }
 
 // The map points of workgroup (tile) b: [*first, *first + *cnt).
@@ -1023,6 +1035,7 @@ __device__ inline void after_solve(const DirectArgs& a, bool merged, SolveLds& L
             for (int k = 0; k < 7; ++k) a.s.state[kLevels * kStateStride + k] = L.state[k];
             if (a.prev_pose_out) store_frame_pose(a.prev_pose_out, s_last, a.prev_ready);
             log_pose(a.prev_log, a.prev_log_host, a.prev_log_index, s_last);
+            log_frame(a.flog, a.prev_log_index, L);
         }
         // Sophus::SE3d(R, t) of last_frame (src/viso.cpp:114)
         double q[4];
@@ -1222,6 +1235,7 @@ __global__ __launch_bounds__(kThreads, 4) void direct_level_kernel(const double*
         if (lv < 0 && a.pose_out) {
             store_frame_pose(a.pose_out, s_pose, a.ready);
             log_pose(a.log, a.log_host, a.log_index, s_pose);
+            log_frame(a.flog, a.log_index, L);
         }
     }
     if (blockIdx.x == 0 && t == 0 && merged)
@@ -1787,6 +1801,7 @@ void launch_direct_levels(const FrameDev& last_pyr, const FrameDev& cur_pyr, con
         a.prev_log_index = merge->log ? merge->log_index : -1;
         a.prev_log_host = merge->log ? merge->log_host : nullptr;
         a.prev_ready = merge->ready;
+        a.flog = merge->log ? merge->flog : nullptr;
     }
     const int grid = a.n_tiles > 0 ? a.n_tiles : 1;
     for (int level = kLevels - 1; level >= 0; --level) {
@@ -1810,7 +1825,7 @@ void launch_direct_final(const FrameDev& last_pyr, const FrameDev& cur_pyr, cons
                          const double K[4], const double* points, int n,
                          const double* pose_last12, const DirectScratch& s, double* stats,
                          double* pose_out, double* log, int log_index, hipStream_t stream, int precision,
-                         int* ready, double* log_host) {
+                         int* ready, double* log_host, double* flog) {
     DirectArgs a = direct_args(last_pyr, cur_pyr, g, K, points, n, pose_last12, pose_last12, s,
                                stats, precision == VISO_PRECISION_FAST);
     a.pose_out = pose_out;
@@ -1818,6 +1833,7 @@ void launch_direct_final(const FrameDev& last_pyr, const FrameDev& cur_pyr, cons
     a.log = log;
     a.log_index = log ? log_index : -1;
     a.log_host = log ? log_host : nullptr;
+    a.flog = log ? flog : nullptr;
     a.level = -1;
     a.probe_seq = next_probe_seq();
     // F solves level 0

@@ -207,7 +207,7 @@ void viso_ctx::release() {
                       &kp1, &kp2, &kp1b, &kp2b, &track_success, &n_track_dev, &fast_rows,
                       &geo_buf, &map_pts, &kf_poses, &direct_buf, &direct_stats,
                       &bg_buf, &lk_pair, &lk_succ, &lk_before, &lk_after, &lk_tmpl, &lk_tmpl_h,
-                      &lk_tmpl_kf, &lk_tmpl_uv, &pose_log};
+                      &lk_tmpl_kf, &lk_tmpl_uv, &pose_log, &frame_log};
     for (DevBuf* b : bufs) b->release();
     if (h_ctl) (void)hipHostFree(h_ctl);
     if (h_int) (void)hipHostFree(h_int);
@@ -241,6 +241,7 @@ int viso_ctx::create_streams() {
         for (int c = 0; c < cus; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
         if (hipExtStreamCreateWithCUMask(&lk_stream, (uint32_t)mask.size(), mask.data()) != hipSuccess)
             lk_stream = nullptr;
+        lk_dedicated = lk_stream != nullptr;
     }
     if (!lk_stream) {
         (void)hipGetLastError();
@@ -260,6 +261,7 @@ int viso_ctx::create_up_stream() {
         for (int c = 0; c < cus; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
         if (hipExtStreamCreateWithCUMask(&up_stream, (uint32_t)mask.size(), mask.data()) != hipSuccess)
             up_stream = nullptr;
+        up_dedicated = up_stream != nullptr;
     }
     if (!up_stream) {
         (void)hipGetLastError();
@@ -488,6 +490,7 @@ int viso_ctx::flush_lk_frames(hipStream_t ls, bool keep_last) {
         launch_lk_align(a, ls);
     }
     VISO_HIP_CHECK(hipGetLastError());
+    if (int rc = count_lk(lk_pending, ls)) return rc;
     lk_last_rows = a.n_frames;
     lk_last_pts = n_map;  // a later keyframe insertion grows n_map, not these rows
     if (side) {
@@ -532,7 +535,7 @@ int viso_ctx::resolve_direct() {
     launch_direct_final(frame(dpend_last), frame(dpend_cur), geom, K, (const double*)map_pts.ptr,
                         n_map, pose_of(dpend_last), direct, (double*)direct_stats.ptr,
                         pose_of(dpend_cur), dpend_log >= 0 ? (double*)pose_log.ptr : nullptr,
-                        dpend_log, stream, p.precision, bg_ready(dpend_bg), log_host(dpend_log));
+                        dpend_log, stream, p.precision, bg_ready(dpend_bg), log_host(dpend_log), flog());
     VISO_HIP_CHECK(hipGetLastError());
     drop(dpend_cur);
     drop(dpend_last);
@@ -582,7 +585,10 @@ int viso_ctx::stage_poses() {
 // leaves a CU room for the background one (direct_fits_background).  Every
 // frame of such a chunk is a tracking frame, so every ready flag is raised:
 // frame f's by frame f+1's merged level-3 launch, the last by the final solve.
-bool viso_ctx::bg_eligible() {
+bool viso_ctx::bg_eligible() { return bg_on() && direct_fits_background() && state == VISO_STATE_RUNNING && n_map > 0 &&
+                                      lk_tmpl.ptr && kf_interval <= 0 && !dpend && lk_pending.empty(); }
+
+bool viso_ctx::bg_on() {
     if (bg_mode < 0) {
         // off on request, and when kernels are serialised (the resident grid
         // would wait out its flag timeouts behind the chain it waits for)
@@ -591,8 +597,7 @@ bool viso_ctx::bg_eligible() {
         const char* blk = getenv("HIP_LAUNCH_BLOCKING");
         bg_mode = (e && e[0] == '0') || (ser && ser[0] && ser[0] != '0') || (blk && blk[0] && blk[0] != '0') ? 0 : 1;
     }
-    return bg_mode && direct_fits_background() && state == VISO_STATE_RUNNING && n_map > 0 && lk_tmpl.ptr &&
-           kf_interval <= 0 && !dpend && lk_pending.empty();
+    return bg_mode != 0;
 }
 
 
@@ -717,6 +722,9 @@ int viso_ctx::bg_end(bool drain) {
         VISO_HIP_CHECK(hipGetLastError());
     }
     VISO_HIP_CHECK(hipStreamWaitEvent(stream, bg_done, 0));
+    if (drain) {
+        if (int rc = count_lk(bg_slots, stream)) return rc;
+    }
     // the error word reaches h_int[32] from the failing wave itself
     // (bg_err_host); the drain's item count (dev builds) by a copy
 #ifdef VISO_DRAIN_COUNT
@@ -732,6 +740,17 @@ int viso_ctx::bg_end(bool drain) {
     bg_slots.clear();
     bg_active = false;
     dpend_bg = -1;
+    return VISO_OK;
+}
+
+int viso_ctx::count_lk(const std::vector<int>& row_slots, hipStream_t s) {
+    if (!flog() || row_slots.empty()) return VISO_OK;
+    LkCountArgs rows{};
+    const int n = std::min((int)row_slots.size(), kLkBatch);
+    for (int f = 0; f < n; ++f) rows.idx[f] = slots[(size_t)row_slots[(size_t)f]].log_index;
+    launch_lk_count((const int32_t*)lk_pair.ptr, (const uint8_t*)lk_succ.ptr, kMaxMapPoints, n_map, n, rows, flog(),
+                    s);
+    VISO_HIP_CHECK(hipGetLastError());
     return VISO_OK;
 }
 
@@ -905,12 +924,18 @@ int viso_ctx::on_new_frame(int cur) {
                 // there (capped at max_features) — unless its copy has landed
                 // already (a caller that synchronised in between): then the
                 // exact count, without waiting
-                if (ntrack_pending && hipEventQuery(ntrack_evt) == hipSuccess) {
-                    n_track = std::min(h_int[3], p.max_features);
-                    if (stats[1] == -1) stats[1] = n_track;
-                    ntrack_pending = false;
+                if (ntrack_pending) {
+                    const hipError_t q = hipEventQuery(ntrack_evt);
+                    if (q == hipSuccess) {
+                        n_track = std::min(h_int[3], p.max_features);
+                        if (stats[1] == -1) stats[1] = n_track;
+                        ntrack_pending = false;
+                    } else if (q == hipErrorNotReady) {
+                        (void)hipGetLastError();  // (only the query's own status)
+                    } else {
+                        return VISO_ERR_HIP;
+                    }
                 }
-                (void)hipGetLastError();  // (hipErrorNotReady from the query)
                 const int n = n_track;
                 if (n != 0) {
                     TimedRegion t(timing, VISO_KERNEL_KLT, stream);
@@ -1086,6 +1111,7 @@ int viso_ctx::on_new_frame(int cur) {
                     m.log_index = dpend_log;
                     m.ready = bg_ready(dpend_bg);
                     m.log_host = log_host(dpend_log);
+                    m.flog = flog();
                 }
                 launch_direct_levels(frame(last_slot), frame(cur), g, K, (const double*)map_pts.ptr,
                                      n_map, pose_of(last_slot), pose_of(last_slot), direct,
@@ -1102,6 +1128,7 @@ int viso_ctx::on_new_frame(int cur) {
             hold(cur);
             hold(last_slot);
             dpend_log = log ? n_poses : -1;
+            slots[(size_t)cur].log_index = dpend_log;
             dpend_bg = bg_active ? bg_cur : -1;
             if (log) ++n_poses;
             // LKAlignment (src/viso.cpp:121, 768-843): run by the chunk's
@@ -1306,7 +1333,12 @@ int viso_get_poses(viso_ctx* c, double* Tcw12, size_t cap, size_t* n) {
         return VISO_OK;
     }
     if (c->h_poses_cap < m) {
-        const size_t want = std::max(m, (size_t)4096);
+        // geometric growth (up to max_poses): the kernels then mirror the
+        // poses logged after this call into the new buffer (log_host), and
+        // stage_poses keeps the staged path, instead of a reallocation and
+        // full copy on every later read
+        const size_t cap_max = (size_t)std::max(c->p.max_poses, 1);
+        const size_t want = std::min(cap_max, std::max(m, std::max((size_t)4096, 2 * c->h_poses_cap)));
         VISO_HIP_CHECK(hipStreamSynchronize(c->stream));  // no staged copy in flight into the old buffer
         if (c->h_poses) VISO_HIP_CHECK(hipHostFree(c->h_poses));
         c->h_poses = nullptr;
@@ -1419,6 +1451,52 @@ int viso_get_frame_stats(viso_ctx* c, double out[16]) {
         out[10] = c->h_dbl[1];
     }
     return VISO_OK;
+}
+
+int viso_get_config(viso_ctx* c, int32_t info[8]) {
+    if (!c || !info) return VISO_ERR_ARG;
+    for (int k = 0; k < 8; ++k) info[k] = 0;
+    info[0] = c->bg_on() && direct_fits_background() ? 1 : 0;
+    info[1] = c->lk_dedicated ? 1 : 0;
+    info[2] = c->up_stream ? (c->up_dedicated ? 1 : 0) : -1;
+    info[3] = c->n_slots;
+    info[4] = c->flog() ? 1 : 0;
+    info[5] = c->p.batch_frames;
+    return VISO_OK;
+}
+
+int viso_set_frame_log(viso_ctx* c, int32_t enable) {
+    if (!c) return VISO_ERR_ARG;
+    if (int rc = c->settle()) return rc;  // (host-frame work left pending)
+    VISO_HIP_CHECK(hipSetDevice(c->device));
+    if (!enable) {
+        VISO_HIP_CHECK(hipStreamSynchronize(c->stream));
+        if (c->lk_stream) VISO_HIP_CHECK(hipStreamSynchronize(c->lk_stream));
+        c->frame_log.release();
+        return VISO_OK;
+    }
+    if (c->flog()) return VISO_OK;
+    const size_t bytes = 32 * (size_t)std::max(c->p.max_poses, 1);
+    if (int rc = c->frame_log.ensure(bytes)) return rc;
+    // NaN until a frame's entry is written (frames logged before the log was on)
+    VISO_HIP_CHECK(hipMemsetAsync(c->frame_log.ptr, 0xff, bytes, c->stream));
+    return VISO_OK;
+}
+
+int viso_get_frame_log(viso_ctx* c, double* rows, size_t cap, size_t* n) {
+    if (!c) return VISO_ERR_ARG;
+    if (!c->flog()) return VISO_ERR_STATE;
+    if (int rc = c->settle()) return rc;  // (host-frame work left pending)
+    VISO_HIP_CHECK(hipSetDevice(c->device));
+    const size_t total = std::min((size_t)c->n_poses, (size_t)std::max(c->p.max_poses, 0));
+    if (n) *n = total;
+    // the LK columns of a side-stream batch are written on lk_stream
+    if (c->lk_stream) VISO_HIP_CHECK(hipStreamSynchronize(c->lk_stream));
+    const size_t m = std::min(cap, total);
+    if (m > 0 && rows)
+        VISO_HIP_CHECK(hipMemcpyAsync(rows, c->frame_log.ptr, 32 * m, hipMemcpyDeviceToHost, c->stream));
+    VISO_HIP_CHECK(hipStreamSynchronize(c->stream));
+    return c->bg_check();
 }
 
 int viso_pose_2d2d(viso_ctx* c, const double* p1, const double* p2, int32_t n, double R[9],

@@ -125,6 +125,14 @@ void launch_lk_drain(const LkAlignArgs& a, int grid, hipStream_t stream);
 void warm_lk_bg(hipStream_t stream);
 // Keyframe choice + per-level templates of every map point (once per map).
 void launch_lk_template(const LkAlignArgs& a, hipStream_t stream);
+// The per-frame log's LK columns (viso_set_frame_log): for batch row f with
+// log index idx[f] >= 0, flog[4 idx + 2] = points paired with a keyframe
+// (pair_kf >= 0), flog[4 idx + 3] = successes, over the row's n points.
+struct LkCountArgs {
+    int idx[kLkBatch];
+};
+void launch_lk_count(const int32_t* pair_kf, const uint8_t* success, size_t stride, int n, int n_rows,
+                     const LkCountArgs& rows, double* flog, hipStream_t stream);
 
 // ---------------------------------------------------------------- stereo (north star)
 // stereo initialisation (stereo.hip): per keypoint flag / camera point, then
@@ -181,6 +189,7 @@ struct DirectPrev {
     int log_index;
     int* ready = nullptr;  // background LK alignment's flag for that pose (or null)
     double* log_host = nullptr;  // the log's pinned host copy (device address), same index
+    double* flog = nullptr;      // the per-frame log (viso_set_frame_log), same index, or null
 };
 // true when a direct-pose workgroup leaves its CU room for the background LK
 // alignment's (12 waves of 128 VGPRs + <= 76 KB LDS beside 4 waves + 84 KB)
@@ -195,7 +204,7 @@ void launch_direct_final(const FrameDev& last, const FrameDev& cur, const PyrGeo
                          const double* pose_last12, const DirectScratch& s, double* stats,
                          double* pose_out, double* log, int log_index, hipStream_t stream,
                          int precision = VISO_PRECISION_FAITHFUL, int* ready = nullptr,
-                         double* log_host = nullptr);
+                         double* log_host = nullptr, double* flog = nullptr);
 // ---------------------------------------------------------------- rig direct pose
 // Multi-camera photometric rig (the repo's own spec;
 // oracle/oracle_rig.cpp): levels 3..0 of one rig Gauss-Newton step each over

@@ -1171,21 +1171,24 @@ constexpr size_t kBgLdsTotal = 84 * 1024;
 // window into the wave's LDS at item start made the tail 105-126 us instead
 // of 81-84: spills at item start and fewer co-resident drain workgroups.)
 static size_t lk_bg_dyn_lds(bool fast) {
-    static size_t dyn[2] = {0, 0};
-    static bool attr = false;
-    if (!attr) {
-        const void* k[2] = {(const void*)lk_item_kernel<false>, (const void*)lk_item_kernel<true>};
-        for (int j = 0; j < 2; ++j) {
-            hipFuncAttributes fa{};
-            size_t st = 4 * 2 * kWinW * kWinH;
-            if (hipFuncGetAttributes(&fa, k[j]) == hipSuccess) st = fa.sharedSizeBytes;
-            dyn[j] = kBgLdsTotal > st ? kBgLdsTotal - st : 0;
-            (void)hipFuncSetAttribute(k[j], hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn[j]);
+    // (a function-local static's initialiser runs once, thread-safely:
+    // contexts may be created from several host threads)
+    struct Dyn {
+        size_t v[2] = {0, 0};
+        Dyn() {
+            const void* k[2] = {(const void*)lk_item_kernel<false>, (const void*)lk_item_kernel<true>};
+            for (int j = 0; j < 2; ++j) {
+                hipFuncAttributes fa{};
+                size_t st = 4 * 2 * kWinW * kWinH;
+                if (hipFuncGetAttributes(&fa, k[j]) == hipSuccess) st = fa.sharedSizeBytes;
+                v[j] = kBgLdsTotal > st ? kBgLdsTotal - st : 0;
+                (void)hipFuncSetAttribute(k[j], hipFuncAttributeMaxDynamicSharedMemorySize, (int)v[j]);
+            }
+            (void)hipGetLastError();
         }
-        (void)hipGetLastError();
-        attr = true;
-    }
-    return dyn[fast ? 1 : 0];
+    };
+    static const Dyn dyn;
+    return dyn.v[fast ? 1 : 0];
 }
 void launch_lk_bg(const LkAlignArgs& a, int grid, hipStream_t stream) {
     if (a.n <= 0 || a.bg_items <= 0 || grid <= 0) return;
@@ -1218,6 +1221,46 @@ void launch_lk_drain(const LkAlignArgs& a, int grid, hipStream_t stream) {
 void launch_lk_template(const LkAlignArgs& a, hipStream_t stream) {
     if (a.n <= 0) return;
     lk_template_kernel<<<(a.n + 3) / 4, 256, 0, stream>>>(a);
+}
+
+namespace {
+// One workgroup per batch row: the row's pair / success counts (integer
+// sums, order-free) into the per-frame log.  Off the product path unless
+// the caller enabled the log (viso_set_frame_log).
+__global__ __launch_bounds__(256) void lk_count_kernel(const int32_t* __restrict__ pair_kf,
+                                                       const uint8_t* __restrict__ success, size_t stride, int n,
+                                                       LkCountArgs rows, double* __restrict__ flog) {
+    const int idx = rows.idx[blockIdx.x];
+    if (idx < 0) return;
+    const int32_t* pk = pair_kf + stride * blockIdx.x;
+    const uint8_t* sc = success + stride * blockIdx.x;
+    int pairs = 0, succ = 0;
+    for (int i = threadIdx.x; i < n; i += 256) {
+        pairs += pk[i] >= 0;
+        succ += sc[i] != 0;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        pairs += __shfl_xor(pairs, o);
+        succ += __shfl_xor(succ, o);
+    }
+    __shared__ int s[2][4];
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        s[0][w] = pairs;
+        s[1][w] = succ;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        flog[4 * (size_t)idx + 2] = (double)((s[0][0] + s[0][1]) + (s[0][2] + s[0][3]));
+        flog[4 * (size_t)idx + 3] = (double)((s[1][0] + s[1][1]) + (s[1][2] + s[1][3]));
+    }
+}
+}  // namespace
+
+void launch_lk_count(const int32_t* pair_kf, const uint8_t* success, size_t stride, int n, int n_rows,
+                     const LkCountArgs& rows, double* flog, hipStream_t stream) {
+    if (!flog || n_rows <= 0 || n_rows > kLkBatch) return;
+    lk_count_kernel<<<n_rows, 256, 0, stream>>>(pair_kf, success, stride, n < 0 ? 0 : n, rows, flog);
 }
 
 }  // namespace viso

@@ -130,6 +130,29 @@ class Viso(FrameHandler):
         _lib.call("viso_get_frame_stats", self.ctx.h, out.ctypes.data)
         return out
 
+    def config(self) -> dict:
+        """viso_get_config: background LK, dedicated queues, pool size."""
+        info = np.zeros(8, np.int32)
+        _lib.call("viso_get_config", self.ctx.h, info.ctypes.data)
+        return {"background_lk": int(info[0]), "lk_queue_dedicated": int(info[1]),
+                "upload_queue_dedicated": int(info[2]), "slots": int(info[3]), "frame_log": int(info[4]),
+                "batch_frames": int(info[5])}
+
+    def set_frame_log(self, on: bool = True) -> None:
+        """Per-frame log (viso_set_frame_log): every tracking frame's level-0
+        nGood / cost and LK pair / success counts, kept on the device."""
+        _lib.call("viso_set_frame_log", self.ctx.h, 1 if on else 0)
+
+    def frame_log(self) -> np.ndarray:
+        """(poses, 4): level-0 nGood, level-0 cost, LK pairs, LK successes per
+        tracking frame (row k = pose k); NaN for frames run with the log off."""
+        n = ctypes.c_size_t(0)
+        _lib.call("viso_get_frame_log", self.ctx.h, None, 0, ctypes.byref(n))
+        out = np.zeros((n.value, 4), np.float64)
+        if n.value:
+            _lib.call("viso_get_frame_log", self.ctx.h, out.ctypes.data, n.value, ctypes.byref(n))
+        return out
+
     def tracks(self):
         """init_.kp1, init_.kp2 (float32 (n,2)) and init_.success."""
         n = ctypes.c_size_t(0)
