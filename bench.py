@@ -51,6 +51,9 @@ sys.path.insert(0, ROOT)
 
 METRIC = "stereo frames/sec at 1242x375 grey, 1/2/4/8 GPUs; pose RMSE vs reference"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# 32-bit VALU lane-ops per second: 256 CUs x 4 SIMDs x 32 lanes per cycle
+# (a wave64 instruction issues over 2 cycles, MI355X_MICROARCH.md) x 2.4 GHz
+VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9
 STEREO_MAX_DISP = 128
 
 
@@ -808,6 +811,9 @@ def main():
                   "frames_per_rank": [int(g.shape[0]) for g in gathered],
                   "own_log_exact": bool(np.array_equal(gathered[rank], poses[n_pose_before:]))}
     frames_by_state = {"initialization": steps - tracking_timed, "running": tracking_timed}
+    # what the last timed chunk's pyramid tail launch did beside levels 2-3
+    # (host state: viso_get_config [6], [7])
+    tail_cfg = v.config()
 
     # ---------------------------------------------------------- kernel timing
     timing = {}
@@ -839,16 +845,26 @@ def main():
         imgs_per_launch = steps / timing["pyramid"]["launches"]
         bytes_per_launch = algo_bytes_img * imgs_per_launch
         achieved = bytes_per_launch / (timing["pyramid"]["avg_ms"] * 1e-3) / 1e9
-        traffic, tsrc = pyramid_traffic(W, H, imgs_per_launch)
+        traffic, tsrc = pyramid_traffic(W, H, imgs_per_launch, _lib.built_hash())
+        # the tail launch's work beside the levels, not algorithmic bytes of
+        # the pyramid: the chunk's last level 0 copied into the pool (read +
+        # write; the library keeps that frame as last_frame) and the chunk's
+        # background-LK words cleared
+        extra = 2 * tail_cfg["tail_copy_bytes"] + 4 * tail_cfg["tail_zero_ints"]
         roofline = {"kernel": "image pass of one ingest chunk: pyr_down_sk (level 1) + pyr_tail (levels 2-3) "
-                              "(algorithmic bytes = "
-                              "L0 read + L1..L3 write per image; not counted: the tail launch of a chunk of "
-                              "<= 32 frames also copies the chunk's last level 0 into its slot, which the "
-                              "library keeps as last_frame, and clears the background-LK words)", "bound": "hbm",
+                              "(algorithmic bytes = L0 read + L1..L3 write per image; extra_bytes: the tail "
+                              "launch's level-0 copy of the chunk's last frame and its clear of the "
+                              "background-LK words, not counted in achieved)", "bound": "hbm",
                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "traffic_source": tsrc,
                     "algorithmic_bytes_per_launch": int(bytes_per_launch),
+                    "extra_bytes": int(extra),
+                    "extra_bytes_basis": {"level0_copy_read_plus_write": 2 * tail_cfg["tail_copy_bytes"],
+                                          "background_words_cleared": 4 * tail_cfg["tail_zero_ints"]},
+                    "achieved_incl_extra": round((bytes_per_launch + extra) /
+                                                 (timing["pyramid"]["avg_ms"] * 1e-3) / 1e9, 1),
+                    "traffic_over_algorithmic": round(traffic / bytes_per_launch, 3) if traffic else None,
                     "images_per_launch": imgs_per_launch}
     st = v.stats()
     n_map = len(v.GetPoints())
@@ -1022,19 +1038,43 @@ def host_info():
     return {"nproc": os.cpu_count(), "cpu_model": model}
 
 
-def pyramid_traffic(W, H, imgs_per_launch):
+def pyramid_traffic(W, H, imgs_per_launch, src):
     """HBM bytes per image-pass launch from the committed rocprofv3 --pmc
-    FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.py), only for an entry
-    profiled at exactly this frame size and chunk (no scaling)."""
+    FETCH_SIZE / WRITE_SIZE passes (tools/gpu_pyr_pmc.sh -> tools/pmc_traffic.py),
+    only for an entry profiled at exactly this frame size and chunk (no
+    scaling) with the library this run loaded (its source hash `src`)."""
     f = os.path.join(ROOT, "profiles", "pyramid_traffic.json")
     if not os.path.exists(f):
         return None, None
     with open(f) as fh:
         t = json.load(fh)
+    stale = None
     for e in t.get("entries", []):
         if (e["width"], e["height"]) == (W, H) and e["images_per_launch"] == imgs_per_launch:
-            return int(e["traffic_bytes_per_launch"]), f"profiles/pyramid_traffic.json ({e['source']})"
+            if e.get("src") != src:
+                stale = e.get("src") or "unstamped"
+                continue
+            return int(e["traffic_bytes_per_launch"]), f"profiles/pyramid_traffic.json ({e['source']}; src:{src})"
+    if stale:
+        return None, f"profiles/pyramid_traffic.json entry is from library src:{stale}, not this one (src:{src})"
     return None, None
+
+
+def newest_profile(pattern):
+    """The newest round's committed profile: profiles/rNN_<pattern>, NN highest."""
+    import glob
+    fs = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r[0-9][0-9]_{pattern}")))
+    return os.path.relpath(fs[-1], ROOT) if fs else None
+
+
+def svo_algorithmic_ops():
+    """The stereo-VO kernels' algorithmic work on tools/bench_svo.py's 100-pair
+    batch (profiles/svo_algorithmic_ops.json, tools/svo_ops.py: the CPU spec)."""
+    f = os.path.join(ROOT, "profiles", "svo_algorithmic_ops.json")
+    if not os.path.exists(f):
+        return None
+    with open(f) as fh:
+        return json.load(fh)
 
 
 def rocprof_avg_us(path, kernel):
@@ -1058,9 +1098,7 @@ def pmc_evidence(W, H, breakdown, stereo_vo, n_map=None):
     and HBM traffic of the matching pass (svo_circle_kernel).  Live durations
     come from this run's HIP events where the bench has them."""
     # the newest committed pass
-    rel = next((r for r in ("profiles/r05_gn_svo_pmc.json", "profiles/r04_gn_svo_pmc.json",
-                            "profiles/r03_gn_svo_pmc.json")
-                if os.path.exists(os.path.join(ROOT, r))), None)
+    rel = newest_profile("gn_svo_pmc.json")
     if (W, H) != (1242, 375) or rel is None:
         return None, None
     f = os.path.join(ROOT, rel)
@@ -1100,13 +1138,18 @@ def pmc_evidence(W, H, breakdown, stereo_vo, n_map=None):
         # the HEAD's rocprofv3 kernel trace of the same workload with the
         # background LK grid off (VISO_LK_BG=0; tools/gpu_evidence.sh): the
         # dominant kernel's average duration and the fp64 fraction it gives
-        st = rocprof_avg_us(os.path.join(ROOT, "profiles", "r05_direct_kernel_stats.csv"),
-                            "direct_level_kernel<false>")
+        stats_rel = newest_profile("direct_kernel_stats.csv")
+        st = rocprof_avg_us(os.path.join(ROOT, stats_rel), "direct_level_kernel<false>") if stats_rel else None
+        src_rel = newest_profile("evidence_src.txt")
+        ev_src = open(os.path.join(ROOT, src_rel)).read().strip() if src_rel else None
+        from viso_amd import _lib as vlib
+        gn.update({"evidence_src": ev_src, "pmc_src": t.get("src") or None,
+                   "evidence_matches_library": ev_src == vlib.built_hash() if ev_src else None})
         if st and flop:
             avg_us, calls = st
             peak = d.get("fp64_peak_tflops") or 78.6
             gn.update({"rocprof_avg_us_per_launch": round(avg_us, 2), "rocprof_calls": calls,
-                       "rocprof_source": "profiles/r05_direct_kernel_stats.csv (rocprofv3 --kernel-trace --stats, "
+                       "rocprof_source": f"{stats_rel} (rocprofv3 --kernel-trace --stats, "
                                          "VISO_LK_BG=0, bench.py --steps 20 --warmup 5)",
                        "fp64_frac": round(flop / (avg_us * 1e-6) / 1e12 / peak, 4),
                        "fp64_frac_basis": "algorithmic flop per launch / rocprof average duration / "
@@ -1122,6 +1165,31 @@ def pmc_evidence(W, H, breakdown, stereo_vo, n_map=None):
               "bound": "latency / VALU (four dependent best-SAD searches per feature over a cache-resident "
                        "descriptor set), not HBM",
               "source": f"{rel} (FETCH_SIZE x2 + WRITE_SIZE)"}
+        ops = svo_algorithmic_ops()
+        if ops:
+            # the kernel's algorithmic work against its actual roof (VALU:
+            # v_sad_u8 takes 4 byte differences per lane-op), and HBM traffic
+            # against the bytes the pass must read
+            sad_lane_ops = ops["sad_bytes"] / 4
+            mp.update({"valu_frac": round(sad_lane_ops / (us * 1e-6) / VALU_PEAK_LANE_OPS, 4),
+                       "valu_frac_basis": f"{ops['sad_candidates']} SAD candidates x 32 B / 4 B per v_sad_u8 "
+                                          f"lane-op / {us} us / {VALU_PEAK_LANE_OPS / 1e12:.1f} T lane-ops/s "
+                                          "(256 CUs x 4 SIMDs x 32 lanes/cycle x 2.4 GHz); "
+                                          "profiles/svo_algorithmic_ops.json (tools/svo_ops.py)",
+                       "algorithmic_bytes": ops["circle_input_bytes"],
+                       "traffic_over_algorithmic": round(c["traffic_bytes"] / ops["circle_input_bytes"], 3)})
+            dk = t.get("svo", {}).get("svo_detect_kernel")
+            if dk and dk.get("sq_duration_us"):
+                dus = dk["sq_duration_us"]
+                mp["detect"] = {"kernel": "svo_detect_kernel (blob / corner filters + 4-class NMS, 100 pairs)",
+                                "duration_us": dus, "valu_busy": dk.get("valu_busy"),
+                                "valu_frac": round(ops["detect_ops"] / (dus * 1e-6) / VALU_PEAK_LANE_OPS, 4),
+                                "valu_frac_basis": f"{ops['detect_ops']} integer ops ({ops['detect_basis']}) / "
+                                                   f"{dus} us / {VALU_PEAK_LANE_OPS / 1e12:.1f} T lane-ops/s",
+                                "traffic_bytes": dk.get("traffic_bytes"),
+                                "algorithmic_bytes": 2 * 1242 * 375 * ops["pairs"],
+                                "traffic_over_algorithmic": round(dk["traffic_bytes"] / (2 * 1242 * 375 * ops["pairs"]), 3)
+                                if dk.get("traffic_bytes") else None}
         if c.get("valu_busy") is not None:
             mp.update({"valu_busy": c["valu_busy"], "valu_insts": c["valu_insts"],
                        "valu_insts_per_us": c["valu_insts_per_us"],

@@ -161,7 +161,10 @@ int viso_set_frame_log(viso_ctx* ctx, int32_t enable);
  * [2] the host-upload stream likewise (-1: not created yet, it is made by the
  *     first host frame),
  * [3] frame slots in the pool, [4] per-frame log on, [5] batch_frames,
- * [6..7] reserved (0).  See INTEGRATION.md §4 for the queue budget. */
+ * [6] level-0 bytes the last ingest's pyramid tail launch copied into the
+ *     pool beside levels 2-3 (its last frame, kept as last_frame: 0 or
+ *     width x height), [7] background-LK words (int32) it cleared.
+ * See INTEGRATION.md §4 for the queue budget. */
 int viso_get_config(viso_ctx* ctx, int32_t info[8]);
 /* The first min(cap, poses) rows (4 doubles each) of the per-frame log; *n =
  * the pose count.  VISO_ERR_STATE when the log is off. */

@@ -135,6 +135,11 @@ struct FeatSet {
     }
 };
 
+// candidates whose SAD the spec evaluates (the matching pass's algorithmic
+// work: 32 byte differences each; oracle_svo_sad_evals, for the bench's
+// VALU-fraction figure of svo_circle_kernel)
+unsigned long long g_sad_evals = 0;
+
 // best candidate of `dst` for a query (u, v, class, descriptor): rows
 // [v - dv, v + dv], u - du_hi <= u' <= u - du_lo; min SAD, ties -> lowest index
 int best_match(const FeatSet& dst, int h, int u, int v, int c, const uint8_t* d, int du_lo,
@@ -146,6 +151,7 @@ int best_match(const FeatSet& dst, int h, int u, int v, int c, const uint8_t* d,
             const int dd = u - dst.u[j];
             if (dd < du_lo || dd > du_hi) continue;
             const int s = sad32(d, dst.d + (size_t)j * VISO_SVO_DESC_BYTES);
+            ++g_sad_evals;
             if (s < best_sad || (s == best_sad && j < best)) {
                 best_sad = s;
                 best = j;
@@ -561,6 +567,13 @@ int oracle_svo_estimate(const int32_t* uv8, int n, int64_t frame, const viso_svo
 int oracle_svo_rig_estimate(const int32_t* uv8, const int32_t* cams, int n, int64_t frame,
                             const viso_svo_params* p, const double* extr, double* motion12, uint8_t* inlier) {
     return estimate(uv8, n, frame, *p, motion12, inlier, cams, extr);
+}
+
+// SAD evaluations of the matching so far (reset: zero the count after reading).
+unsigned long long oracle_svo_sad_evals(int reset) {
+    const unsigned long long n = g_sad_evals;
+    if (reset) g_sad_evals = 0;
+    return n;
 }
 
 }  // extern "C"

@@ -85,6 +85,7 @@ SIG = {
     "oracle_svo_bucket": ([_vp, _i, _i, _i, _vp, _vp], _i),
     "oracle_svo_estimate": ([_vp, _i, ctypes.c_int64, _vp, _vp, _vp], _i),
     "oracle_svo_rig_estimate": ([_vp, _vp, _i, ctypes.c_int64, _vp, _vp, _vp, _vp], _i),
+    "oracle_svo_sad_evals": ([_i], ctypes.c_uint64),
 }
 
 _lib = None

@@ -4,7 +4,8 @@
 #   rocprofv3 kernel trace of the bench with the background LK grid OFF
 #   (VISO_LK_BG=0: clean direct_level_kernel durations; with the grid on, the
 #   trace's serialised bookkeeping distorts the chain) and one with it on,
-#   then the PMC passes (tools/gpu_pmc.sh, grid off), and, when the probe
+#   then the PMC passes (tools/gpu_pmc.sh, grid off; tools/gpu_pyr_pmc.sh, the
+#   image pass's HBM traffic over bench.py), and, when the probe
 #   build is present (VISO_VARIANT=probe VISO_DEFS=-DVISO_PROBE_LIGHT), the
 #   direct chain's per-level phases with the grid on and off
 #   (tools/probe_direct.py) and the LK tail (tools/probe_lk_items.py).
@@ -15,7 +16,8 @@ TAG=${1:-evidence}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest_gpu.log; exit 1; }
+timeout -k 10 60 python -c "import viso_amd._lib as l; print(l.built_hash())" > $OUT/src.txt || { echo "library hash failed"; exit 1; }
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest_gpu.log; exit 1; }
 tail -1 $OUT/pytest_gpu.log
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo "smoke failed"; tail -30 $OUT/smoke.log; exit 1; }
 tail -1 $OUT/smoke.log
@@ -29,6 +31,7 @@ python tools/db2stats.py $(find $OUT/prof_nobg -name '*results.db' | head -1) $O
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python -u bench.py --no-cpu --svo-cpu-pairs 0 --no-host-ingest > $OUT/bench_rocprof.json 2> $OUT/bench_rocprof.err || { echo "rocprof failed"; tail -30 $OUT/bench_rocprof.err; exit 1; }
 python tools/db2stats.py $(find $OUT/prof -name '*results.db' | head -1) $OUT/kernel_stats.csv && echo "kernel stats: $OUT/kernel_stats.csv"
 VISO_LK_BG=0 bash tools/gpu_pmc.sh ${TAG}_pmc | tail -3
+bash tools/gpu_pyr_pmc.sh ${TAG}_pyr | tail -3
 if [ -f viso_amd/libviso_amd_probe.so ]; then
   VISO_LIB=$PWD/viso_amd/libviso_amd_probe.so timeout -k 10 200 python -u tools/probe_direct.py > $OUT/direct_probe_bg.log 2>&1 || { echo "direct probe failed"; tail -20 $OUT/direct_probe_bg.log; exit 1; }
   VISO_LK_BG=0 VISO_LIB=$PWD/viso_amd/libviso_amd_probe.so timeout -k 10 200 python -u tools/probe_direct.py > $OUT/direct_probe_nobg.log 2>&1 || { echo "direct probe (grid off) failed"; tail -20 $OUT/direct_probe_nobg.log; exit 1; }

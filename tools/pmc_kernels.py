@@ -61,7 +61,9 @@ def main():
     sf, sw = load(os.path.join(run, "svo_f")), load(os.path.join(run, "svo_w"))
     sq = load(os.path.join(run, "svo_sq"))
     res = {"source": f"rocprofv3 --pmc passes of tools/gpu_pmc.sh ({os.path.basename(run.rstrip('/'))})",
-           "cus": CUS, "clock_ghz": CLK_GHZ, "gn": {}, "svo": {}}
+           "cus": CUS, "clock_ghz": CLK_GHZ, "gn": {}, "svo": {},
+           # the library the passes ran (viso_version "src:"), when given
+           "src": os.environ.get("SRC_HASH", "")}
     for k in ("direct_level_kernel", "lk_align_kernel", "pyr_down_sk_kernel"):
         if k not in occ:
             continue

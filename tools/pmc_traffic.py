@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes for the image pass.
 
-Usage: [IMAGES=n SOURCE=...] tools/pmc_traffic.py FETCH_DIR WRITE_DIR [OUT_JSON]
+Usage: [IMAGES=n SOURCE=... SRC_HASH=...] tools/pmc_traffic.py FETCH_DIR WRITE_DIR [OUT_JSON]
 (OUT_JSON is a table of entries keyed by frame size and images per launch,
 profiles/pyramid_traffic.json for bench.py)
 
@@ -31,7 +31,10 @@ import sys
 def per_dispatch(path, counter):
     vals = collections.defaultdict(float)
     grid = {}
-    for r in csv.DictReader(open(os.path.join(path, "run_counter_collection.csv"))):
+    f = os.path.join(path, "run_counter_collection.csv")
+    if not os.path.exists(f):
+        f = next(os.path.join(d, x) for d, _, xs in os.walk(path) for x in xs if x.endswith("counter_collection.csv"))
+    for r in csv.DictReader(open(f)):
         if ("pyr_down_" not in r["Kernel_Name"] and "pyr_tail_" not in r["Kernel_Name"]) or \
                 r["Counter_Name"] != counter:
             continue
@@ -79,14 +82,18 @@ def main():
            "fetch_scale": scale,
            "note": f"FETCH_SIZE x fetch_scale + WRITE_SIZE (KB -> bytes) summed over the {LAUNCHES} "
                    f"image-pass launches of one {imgs}-image chunk (tools/pmc_traffic.py)",
-           "raw_fetch_kb_per_launch": per_level(f, fg), "raw_write_kb_per_launch": per_level(w, wg)}
+           "raw_fetch_kb_per_launch": per_level(f, fg), "raw_write_kb_per_launch": per_level(w, wg),
+           # the library the passes ran (viso_version "src:"): bench.py uses
+           # an entry only for the library it loads
+           "src": os.environ.get("SRC_HASH", "")}
     print(json.dumps(res, indent=1))
     if out:
         # a table of entries (bench.py pyramid_traffic looks up its own size
         # and chunk): replace the entry of this size / chunk, keep the others
         table = {"entries": []}
-        if os.path.exists(out):
-            old = json.load(open(out))
+        base = os.environ.get("BASE_TABLE", out)
+        if os.path.exists(base):
+            old = json.load(open(base))
             table = old if "entries" in old else table
         table["entries"] = [e for e in table["entries"]
                             if (e["width"], e["height"], e["images_per_launch"]) !=

@@ -5,6 +5,7 @@
 // Viso::OnNewFrame (src/viso.cpp:7-145); every pixel/point loop runs in the
 // gfx950 kernels of image.hip / track.hip / direct.hip / geometry.hip.
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -103,6 +104,8 @@ int viso_create(const viso_params* p, int device, viso_ctx** out) {
     if (!c) return VISO_ERR_ARG;
     c->p = *p;
     c->device = device;
+    if (const char* e = getenv("VISO_HOST_TIMES")) c->host_times.on = c->stage.timed = e[0] == '1';
+    if (const char* e = getenv("VISO_HOST_TIMELINE")) c->dev_tl.on = e[0] == '1';
     c->geom = make_geom(p->width, p->height);
     if (c->create_streams() != VISO_OK) {
         delete c;
@@ -120,6 +123,32 @@ int viso_create(const viso_params* p, int device, viso_ctx** out) {
 int viso_destroy(viso_ctx* c) {
     if (!c) return VISO_ERR_ARG;
     (void)hipSetDevice(c->device);
+    if (c->dev_tl.on && !c->dev_tl.marks.empty()) {
+        (void)hipDeviceSynchronize();
+        const hipEvent_t e0 = c->dev_tl.marks[0].e;
+        int64_t fr = -1;
+        fprintf(stderr, "viso device timeline (us from the first mark): frame: upload start / end, pyramid end, "
+                        "chain start / end\n");
+        for (auto& m : c->dev_tl.marks) {
+            float ms = 0.f;
+            (void)hipEventElapsedTime(&ms, e0, m.e);
+            if (m.frame != fr) {
+                fprintf(stderr, "%s%lld:", fr >= 0 ? "\n" : "", (long long)m.frame);
+                fr = m.frame;
+            }
+            fprintf(stderr, " %d@%.1f", m.kind, 1e3 * ms);
+        }
+        fprintf(stderr, "\n");
+        for (auto& m : c->dev_tl.marks) (void)hipEventDestroy(m.e);
+        c->dev_tl.marks.clear();
+    }
+    if (c->host_times.on && c->host_times.calls > 0) {
+        const double n = (double)c->host_times.calls;
+        fprintf(stderr, "viso host times: %lld frame calls, us per call: ingest %.1f (pinned copy %.1f), "
+                        "OnNewFrame %.1f, end %.1f\n",
+                (long long)c->host_times.calls, c->host_times.us[0] / n, c->stage.copy_us / n,
+                c->host_times.us[1] / n, c->host_times.us[2] / n);
+    }
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     c->release();
     if (c->stream) (void)hipStreamDestroy(c->stream);

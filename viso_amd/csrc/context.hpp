@@ -1,6 +1,7 @@
 // viso_amd — context object behind the C ABI.
 #pragma once
 
+#include <chrono>
 #include <deque>
 #include <vector>
 
@@ -102,6 +103,52 @@ struct TimedRegion {
     }
 };
 
+// (dev, VISO_HOST_TIMES=1) host time of viso_process_frame by phase: 0
+// ingest (the pinned copy inside it is HostStage::copy_us), 1 OnNewFrame's
+// launches, 2 the call's end (LK batching, epoch); printed at destroy
+struct HostTimes {
+    bool on = false;
+    double us[3] = {0, 0, 0};
+    int64_t calls = 0;
+    struct Clock {
+        HostTimes& h;
+        std::chrono::steady_clock::time_point t;
+        explicit Clock(HostTimes& h_) : h(h_) {
+            if (h.on) {
+                t = std::chrono::steady_clock::now();
+                ++h.calls;
+            }
+        }
+        void lap(int k) {
+            if (!h.on) return;
+            const auto n = std::chrono::steady_clock::now();
+            h.us[k] += std::chrono::duration<double, std::micro>(n - t).count();
+            t = n;
+        }
+    };
+};
+
+// (dev, VISO_HOST_TIMELINE=1) device timestamps of the host-frame path: per
+// mark (frame, kind) an event recorded on the mark's stream; printed at
+// destroy relative to the first (kinds: 0 upload start, 1 upload end, 2
+// pyramid end, 3 chain start, 4 chain end)
+struct DevTimeline {
+    bool on = false;
+    struct Mark {
+        int64_t frame;
+        int kind;
+        hipEvent_t e;
+    };
+    std::vector<Mark> marks;
+    void mark(int64_t frame, int kind, hipStream_t s) {
+        if (!on || marks.size() > 20000) return;
+        hipEvent_t e = nullptr;
+        if (hipEventCreate(&e) != hipSuccess) return;
+        (void)hipEventRecord(e, s);
+        marks.push_back({frame, kind, e});
+    }
+};
+
 }  // namespace viso
 
 namespace viso {
@@ -136,6 +183,9 @@ struct viso_ctx {
     std::deque<int> free_slots;  // FIFO: the longest-free slot is reused first
     int ref_slot = -1, last_slot = -1;  // init_.ref_frame, last_frame
     std::vector<int> kf_slots;          // Map::keyframes_
+    // the last ingest pyramid's tail launch: level-0 bytes it copied into the
+    // pool (PyrOwn; 0 or w x h) and background-LK words it cleared
+    int tail_copy_bytes = 0, tail_zero_ints = 0;
     int ident_slot = -1;  // the ingest's pyramid wrote this frame's Keyframe-ctor pose (PyrOwn)
     // the ingest's pyramid launch(es) with its last frame's PyrOwn (level 0
     // owned, identity pose outside tracking)
@@ -212,6 +262,8 @@ struct viso_ctx {
     hipStream_t lk_stream = nullptr;
     hipEvent_t lk_ring[viso::kLkRing] = {};  // recorded after each lk_stream batch
     viso::HostStage stage;  // pinned staging of host-ingested frames (ingest_host)
+    viso::HostTimes host_times;
+    viso::DevTimeline dev_tl;
     // Host uploads run on their own stream (created at the first one, with a
     // hardware queue of its own when a CU-masked stream can be made), so a
     // frame's DMA overlaps the previous frame's chain.  A slot's last readers
@@ -225,6 +277,13 @@ struct viso_ctx {
     int create_up_stream();
     int upload_host(int s, const uint8_t* grey, int32_t w, int32_t h, int32_t stride, bool pyramid);
     hipEvent_t up_done = nullptr;  // behind a host frame's upload + pyramid
+    // VISO_HOST_PYR=split: a host frame's pyramid on a stream of its own
+    // behind its DMA (up_dma), so one frame's pyramid overlaps the next DMA
+    hipStream_t pyr_stream = nullptr;
+    hipEvent_t up_dma = nullptr;
+    int host_pyr_mode = -1;
+    bool host_pyr_split();
+    int create_masked_stream(hipStream_t* out);
     // PoseEstimation2d2d's E path runs on lk_stream beside the H path (no LK
     // alignment runs while initialising): fork / join events
     hipEvent_t geo_fork = nullptr, geo_join = nullptr;
@@ -310,6 +369,11 @@ struct viso_ctx {
     int finish_host_call();
     int settle();
     int host_lk_batch() const;
+    // host batches in the background-grid geometry (VISO_HOST_LK; -1 unread)
+    int host_lk_mode = -1;
+    bool host_lk_grid();
+    viso::DevBuf hbg_buf;  // their words (ready flags up, heads, leftover header, error)
+    int host_grid_args(viso::LkAlignArgs& a, hipStream_t s);
     // LK batch of lk_pending on `s` (all but the last frame: keep_last)
     int flush_lk_frames(hipStream_t s, bool keep_last);
     // LK alignment of a device-ingest chunk in the background of its

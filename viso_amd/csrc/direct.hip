@@ -335,7 +335,16 @@ __device__ inline void win_store(uint8_t* lds, const CurWin& c) {
 #ifdef VISO_PROBE
 // (probe) current-image samples that missed their LDS window, per level
 // [0..3]; merged L(3) points whose `last` taps some lane reloaded [4], and
-// all merged L(3) points [5]
+// all merged L(3) points [5].  Counted only in VISO_PROBE_PFB builds: they
+// are same-address device atomics (one per missed sample, one or two per
+// merged-L(3) point: ~4,900 per merged launch serialised on one L2 channel),
+// and in the plain probe build they stretched every merged L(3) launch from
+// ~14 to ~34 us — the probe measured itself
+#ifdef VISO_PROBE_PFB
+#define PFB_ADD(k) atomicAdd(&g_pfb[(k)], 1ull)
+#else
+#define PFB_ADD(k) ((void)0)
+#endif
 __device__ unsigned long long g_pfb[8];
 #endif
 
@@ -370,7 +379,7 @@ __device__ inline double sample_cw(const uint8_t* __restrict__ img, int w, int h
         }
     }
 #ifdef VISO_PROBE
-    atomicAdd(&g_pfb[w >= 1000 ? 0 : w >= 500 ? 1 : w >= 250 ? 2 : 3], 1ull);
+    PFB_ADD(w >= 1000 ? 0 : w >= 500 ? 1 : w >= 250 ? 2 : 3);
 #endif
     return sample_px(img, w, h, x, y);
 }
@@ -774,12 +783,12 @@ __device__ inline void merged_ref(const DirectArgs& a, const LevelPair& fp, int 
     const long long base = (long long)(int)y * (long long)w + (long long)(int)x;
     const double xp = pf.ur[j] + px, yp = pf.vr[j] + py;
     const long long bp = pf.ok[j] ? (long long)(int)yp * (long long)w + (long long)(int)xp : -(1LL << 40);
-#ifdef VISO_PROBE
+#ifdef VISO_PROBE_PFB
     {
         const unsigned long long rl = __ballot(base != bp);
         if (lane == 0) {
-            atomicAdd(&g_pfb[5], 1ull);
-            if (rl) atomicAdd(&g_pfb[4], 1ull);
+            PFB_ADD(5);
+            if (rl) PFB_ADD(4);
         }
     }
 #endif

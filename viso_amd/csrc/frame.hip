@@ -207,7 +207,7 @@ void viso_ctx::release() {
                       &kp1, &kp2, &kp1b, &kp2b, &track_success, &n_track_dev, &fast_rows,
                       &geo_buf, &map_pts, &kf_poses, &direct_buf, &direct_stats,
                       &bg_buf, &lk_pair, &lk_succ, &lk_before, &lk_after, &lk_tmpl, &lk_tmpl_h,
-                      &lk_tmpl_kf, &lk_tmpl_uv, &pose_log, &frame_log};
+                      &lk_tmpl_kf, &lk_tmpl_uv, &pose_log, &frame_log, &hbg_buf};
     for (DevBuf* b : bufs) b->release();
     if (h_ctl) (void)hipHostFree(h_ctl);
     if (h_int) (void)hipHostFree(h_int);
@@ -216,6 +216,13 @@ void viso_ctx::release() {
     stage.release();
     if (up_stream) (void)hipStreamDestroy(up_stream);
     up_stream = nullptr;
+    if (pyr_stream) {
+        (void)hipStreamSynchronize(pyr_stream);
+        (void)hipStreamDestroy(pyr_stream);
+    }
+    pyr_stream = nullptr;
+    if (up_dma) (void)hipEventDestroy(up_dma);
+    up_dma = nullptr;
     h_ctl = nullptr;
     h_int = nullptr;
     h_dbl = nullptr;
@@ -247,6 +254,31 @@ int viso_ctx::create_streams() {
         (void)hipGetLastError();
         if (!(q && q[0] == 's')) bg_mode = 0;
         if (hipStreamCreateWithFlags(&lk_stream, hipStreamNonBlocking) != hipSuccess) return VISO_ERR_HIP;
+    }
+    return VISO_OK;
+}
+
+bool viso_ctx::host_pyr_split() {
+    if (host_pyr_mode < 0) {
+        const char* e = getenv("VISO_HOST_PYR");
+        host_pyr_mode = (e && e[0] == 's') ? 1 : 0;
+    }
+    return host_pyr_mode != 0;
+}
+
+// A stream with a hardware queue of its own when a CU-masked stream (every
+// CU) can be made, else a plain one.
+int viso_ctx::create_masked_stream(hipStream_t* out) {
+    int cus = 0;
+    *out = nullptr;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0) {
+        std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
+        for (int c = 0; c < cus; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
+        if (hipExtStreamCreateWithCUMask(out, (uint32_t)mask.size(), mask.data()) != hipSuccess) *out = nullptr;
+    }
+    if (!*out) {
+        (void)hipGetLastError();
+        if (hipStreamCreateWithFlags(out, hipStreamNonBlocking) != hipSuccess) return VISO_ERR_HIP;
     }
     return VISO_OK;
 }
@@ -316,19 +348,33 @@ int viso_ctx::upload_host(int s, const uint8_t* grey, int32_t w, int32_t h, int3
     }
     {
         TimedRegion t(timing, VISO_KERNEL_UPLOAD, up_stream);
+        dev_tl.mark(frames, 0, up_stream);
         VISO_HIP_CHECK(stage.upload(slot_base(s), grey, w, h, stride, up_stream));
+        dev_tl.mark(frames, 1, up_stream);
     }
     if (!pyramid) {
         VISO_HIP_CHECK(hipStreamWaitEvent(stream, stage.last, 0));
         return VISO_OK;
     }
     // the frame's pyramid behind its upload, on the same stream: both beside
-    // the previous frame's chain
+    // the previous frame's chain (VISO_HOST_PYR=split: on a stream of its
+    // own behind the DMA, so frame f's pyramid overlaps frame f+1's DMA)
     uint8_t* slot = slot_base(s);
     const uint8_t* l0 = slot;
-    launch_ingest_pyramid(&l0, &slot, &s, 1, false, up_stream);
+    hipStream_t ps = up_stream;
+    if (host_pyr_split()) {
+        if (!pyr_stream) {
+            if (int rc = create_masked_stream(&pyr_stream)) return rc;
+            VISO_HIP_CHECK(hipEventCreateWithFlags(&up_dma, hipEventDisableTiming));
+        }
+        VISO_HIP_CHECK(hipEventRecord(up_dma, up_stream));
+        VISO_HIP_CHECK(hipStreamWaitEvent(pyr_stream, up_dma, 0));
+        ps = pyr_stream;
+    }
+    launch_ingest_pyramid(&l0, &slot, &s, 1, false, ps);
     VISO_HIP_CHECK(hipGetLastError());
-    VISO_HIP_CHECK(hipEventRecord(up_done, up_stream));
+    dev_tl.mark(frames, 2, ps);
+    VISO_HIP_CHECK(hipEventRecord(up_done, ps));
     VISO_HIP_CHECK(hipStreamWaitEvent(stream, up_done, 0));
     return VISO_OK;
 }
@@ -401,6 +447,9 @@ void viso_ctx::launch_ingest_pyramid(const uint8_t* const* l0, uint8_t* const* d
         TimedRegion t(timing, VISO_KERNEL_PYRAMID, st);
         launch_pyramid_frames(geom, l0, dst, n, st, &own);
     }
+    // (viso_get_config [6], [7]: what the tail launch did beside the levels)
+    tail_copy_bytes = own.copied ? (int)((size_t)geom.w[0] * geom.h[0]) : 0;
+    tail_zero_ints = own.n_zero;
     SlotRec& r = slots[(size_t)s];
     if (r.borrowed && own.copied) {
         r.l0 = slot_base(s);
@@ -485,9 +534,22 @@ int viso_ctx::flush_lk_frames(hipStream_t ls, bool keep_last) {
         // order behind the last side batch
         VISO_HIP_CHECK(hipStreamWaitEvent(stream, lk_ring[(lk_seq - 1) % kLkRing], 0));
     }
+    // A host-frame caller's batch (side stream, beside the next frames'
+    // chains): the chunk-resident grid's geometry — one workgroup per CU in
+    // each CU's spare wave slots, below the chain's priority — with every
+    // frame's ready flag already up (their poses are final), instead of a
+    // full-occupancy launch whose workgroups hold the CUs the next frame's
+    // direct launches need (VISO_HOST_LK=batch: the latter).
+    const bool grid = side && host_lk_grid();
+    if (grid) {
+        if (int rc = host_grid_args(a, ls)) return rc;
+    }
     {
         TimedRegion t(timing, VISO_KERNEL_LKALIGN, ls);
-        launch_lk_align(a, ls);
+        if (grid)
+            launch_lk_bg(a, n_cu, ls);
+        else
+            launch_lk_align(a, ls);
     }
     VISO_HIP_CHECK(hipGetLastError());
     if (int rc = count_lk(lk_pending, ls)) return rc;
@@ -502,6 +564,40 @@ int viso_ctx::flush_lk_frames(hipStream_t ls, bool keep_last) {
     for (int s : lk_pending) drop(s);
     lk_pending.clear();
     if (kept >= 0) lk_pending.push_back(kept);
+    return VISO_OK;
+}
+
+bool viso_ctx::host_lk_grid() {
+    if (host_lk_mode < 0) {
+        const char* e = getenv("VISO_HOST_LK");
+        host_lk_mode = (e && e[0] == 'b') ? 0 : 1;
+    }
+    return host_lk_mode && bg_on() && direct_fits_background() && lk_tmpl.ptr;
+}
+
+// The words of a host batch's resident grid (their own buffer: a device-
+// ingest chunk's words are cleared on the context stream while this grid may
+// still run on the side stream): ready flags all up (set once), the heads and
+// the leftover header cleared per batch on the batch's stream; at most two
+// such batches outstanding (the grid shares the chain's CUs, so a caller far
+// ahead of it would otherwise hold ever more frame slots).
+int viso_ctx::host_grid_args(LkAlignArgs& a, hipStream_t ls) {
+    constexpr size_t kHdr = 8 * 32 + 32 + 32;  // heads + leftover header
+    if (!hbg_buf.ptr) {
+        if (int rc = hbg_buf.ensure(sizeof(int) * (kBgWords + 32))) return rc;
+        VISO_HIP_CHECK(hipMemsetAsync(hbg_buf.ptr, 0, sizeof(int) * (kBgWords + 32), ls));
+        VISO_HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)hbg_buf.ptr, 1, kLkBatch, ls));
+    }
+    if (lk_seq >= 2) VISO_HIP_CHECK(hipEventSynchronize(lk_ring[(lk_seq - 2) % kLkRing]));
+    int* w = (int*)hbg_buf.ptr;
+    VISO_HIP_CHECK(hipMemsetAsync(w + kLkBatch, 0, sizeof(int) * kHdr, ls));
+    a.bg_ready = w;
+    a.bg_next = w + kLkBatch;
+    a.bg_left = a.bg_next + 8 * 32 + 32;
+    a.bg_err = w + kBgWords;
+    a.bg_err_host = h_int_dev + 32;
+    a.bg_items = a.n_frames * n_map;
+    bg_unchecked = true;
     return VISO_OK;
 }
 
@@ -1113,10 +1209,12 @@ int viso_ctx::on_new_frame(int cur) {
                     m.log_host = log_host(dpend_log);
                     m.flog = flog();
                 }
+                dev_tl.mark(frames, 3, stream);
                 launch_direct_levels(frame(last_slot), frame(cur), g, K, (const double*)map_pts.ptr,
                                      n_map, pose_of(last_slot), pose_of(last_slot), direct,
                                      (double*)direct_stats.ptr, dpend ? &m : nullptr, stream, p.precision,
                                      bg_active);
+                dev_tl.mark(frames, 4, stream);
             }
             if (dpend) {
                 drop(dpend_cur);
@@ -1184,14 +1282,18 @@ int viso_process_frame(viso_ctx* c, const uint8_t* grey, int32_t width, int32_t 
                        int32_t stride) {
     if (!c) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(c->device));
+    HostTimes::Clock ht(c->host_times);
     int s = -1;
     // upload and pyramid on the upload stream (ingest_host)
     int rc = c->ingest_host(grey, width, height, stride, &s, true);
+    ht.lap(0);
     if (rc) return rc;
     rc = c->on_new_frame(s);
+    ht.lap(1);
     if (rc) return rc;
     rc = c->finish_host_call();
     const int re = c->end_epoch();
+    ht.lap(2);
     return rc ? rc : re;
 }
 
@@ -1462,6 +1564,8 @@ int viso_get_config(viso_ctx* c, int32_t info[8]) {
     info[3] = c->n_slots;
     info[4] = c->flog() ? 1 : 0;
     info[5] = c->p.batch_frames;
+    info[6] = c->tail_copy_bytes;
+    info[7] = c->tail_zero_ints;
     return VISO_OK;
 }
 

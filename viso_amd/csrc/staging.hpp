@@ -11,6 +11,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdint>
 #include <cstring>
 
@@ -24,6 +25,8 @@ struct HostStage {
     bool used[kRing] = {};
     int next = 0;
     hipEvent_t last = nullptr;  // the latest upload's event (behind its DMA on s)
+    double copy_us = 0.0;       // (VISO_HOST_TIMES) host time in the row copies
+    bool timed = false;
 
     // rows [0, h) of w bytes at src (row pitch stride) -> dst (packed), on s
     hipError_t upload(uint8_t* dst, const uint8_t* src, int w, int h, int stride, hipStream_t s) {
@@ -40,10 +43,13 @@ struct HostStage {
             cap[k] = bytes;
         }
         if (!ev[k] && (e = hipEventCreateWithFlags(&ev[k], hipEventDisableTiming)) != hipSuccess) return e;
+        const auto t0 = timed ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point{};
         if (stride == w)
             std::memcpy(buf[k], src, bytes);
         else
             for (int y = 0; y < h; ++y) std::memcpy(buf[k] + (size_t)y * w, src + (size_t)y * stride, (size_t)w);
+        if (timed)
+            copy_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
         if ((e = hipMemcpyAsync(dst, buf[k], bytes, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
         if ((e = hipEventRecord(ev[k], s)) != hipSuccess) return e;
         used[k] = true;

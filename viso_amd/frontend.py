@@ -136,7 +136,7 @@ class Viso(FrameHandler):
         _lib.call("viso_get_config", self.ctx.h, info.ctypes.data)
         return {"background_lk": int(info[0]), "lk_queue_dedicated": int(info[1]),
                 "upload_queue_dedicated": int(info[2]), "slots": int(info[3]), "frame_log": int(info[4]),
-                "batch_frames": int(info[5])}
+                "batch_frames": int(info[5]), "tail_copy_bytes": int(info[6]), "tail_zero_ints": int(info[7])}
 
     def set_frame_log(self, on: bool = True) -> None:
         """Per-frame log (viso_set_frame_log): every tracking frame's level-0
