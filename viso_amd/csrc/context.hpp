@@ -163,6 +163,7 @@ struct SlotRec {
     int log_index = -1;       // a tracking frame's pose-log index (< 0: not logged)
 };
 constexpr int kEpochRing = 16;
+constexpr int kEpochStride = 8;  // calls per epoch record (end_epoch)
 constexpr int kLkRing = 64;
 }  // namespace viso
 
@@ -272,22 +273,21 @@ struct viso_ctx {
     hipStream_t up_stream = nullptr;
     int64_t epoch = 0;
     hipEvent_t epoch_evt[viso::kEpochRing] = {};
+    int64_t epoch_rec_call[viso::kEpochRing] = {};  // the call (epoch) each record was made at
+    int64_t epoch_nrec = 0;                         // records made
+    int64_t epoch_last_rec = -(1LL << 40);          // the call of the latest record
+    int wait_freed(int64_t fe, hipStream_t st);
     hipEvent_t epoch_now = nullptr;  // a slot freed in the current call (rare)
     int end_epoch();
     int create_up_stream();
     int upload_host(int s, const uint8_t* grey, int32_t w, int32_t h, int32_t stride, bool pyramid);
-    hipEvent_t up_done = nullptr;  // behind a host frame's upload + pyramid
-    // VISO_HOST_PYR=split: a host frame's pyramid on a stream of its own
-    // behind its DMA (up_dma), so one frame's pyramid overlaps the next DMA
-    hipStream_t pyr_stream = nullptr;
-    hipEvent_t up_dma = nullptr;
-    int host_pyr_mode = -1;
-    bool host_pyr_split();
-    int create_masked_stream(hipStream_t* out);
     // PoseEstimation2d2d's E path runs on lk_stream beside the H path (no LK
     // alignment runs while initialising): fork / join events
     hipEvent_t geo_fork = nullptr, geo_join = nullptr;
     int64_t lk_seq = 0;                      // lk_stream batches launched
+    int64_t lk_done = 0;                     // batches the host has seen complete (all < lk_done)
+    int64_t lk_waited_ctx = 0, lk_waited_up = 0;  // batches the context / upload stream already wait for
+    int order_after_lk(int64_t use, hipStream_t st);
     // The last tracking frame's final direct-pose solve (F) is deferred: it
     // runs fused into the next tracking frame's L(3), or alone when the
     // ingest call ends (resolve_direct).  Its frame and `last` slots are held.
@@ -395,6 +395,10 @@ struct viso_ctx {
     bool bg_unchecked = false;
     bool bg_active = false;
     bool bg_launched = false;  // bg_begin cleared the words; the grid is launched after frame 0
+    // the last chunk's resident grid (lk_stream batch bg_grid_seq) may still
+    // read its words: the next clearing of them orders behind it first
+    bool bg_grid_pending = false;
+    int64_t bg_grid_seq = -1;
     int bg_mode = -1;        // VISO_LK_BG: 0 off, 1 on (read once; -1 unread)
     int bg_nb = 0;           // frames of the chunk
     int bg_cur = -1;         // chunk index of the frame on_new_frame is processing

@@ -48,6 +48,24 @@ const double kIdentityPose[12] = {1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0};
 
 }  // namespace
 
+// Flags of the events that only order GPU work against GPU work (cross-
+// stream waits; the host never reads memory behind them): no timing, and
+// (VISO_EVENT_FENCE=device / none) a device-scope release or no system-
+// scope fence instead of the default system-scope fence, whose cache
+// writeback and invalidation sit on the waiting stream (hip_runtime_api.h
+// hipEventDisableSystemFence).  Events the host waits on before reading what
+// kernels stored into pinned memory (ntrack_evt, gate_evt) keep the default.
+static unsigned gpu_event_flags() {
+    static const unsigned f = [] {
+        const char* e = getenv("VISO_EVENT_FENCE");
+        unsigned x = hipEventDisableTiming;
+        if (e && e[0] == 'd') x |= hipEventReleaseToDevice;
+        if (e && e[0] == 'n') x |= hipEventDisableSystemFence;
+        return x;
+    }();
+    return f;
+}
+
 // ------------------------------------------------------------------ lifecycle
 int viso_ctx::init() {
     const PyrGeom& g = geom;
@@ -155,18 +173,17 @@ int viso_ctx::init() {
     if (!rc) rc = pose_log.ensure(96 * (size_t)std::max(p.max_poses, 1));
     if (rc) return rc;
     direct = direct_scratch_at(direct_buf.ptr);
-    for (int i = 0; i < kLkRing; ++i) VISO_HIP_CHECK(hipEventCreateWithFlags(&lk_ring[i], hipEventDisableTiming));
+    for (int i = 0; i < kLkRing; ++i) VISO_HIP_CHECK(hipEventCreateWithFlags(&lk_ring[i], gpu_event_flags()));
     // the background LK grid's resources and its kernel's first launch, here
     // rather than in the first tracking chunk (a hipMalloc, the kernel's
     // dynamic-LDS attribute and code-object load would otherwise land in that
     // chunk: ~0.1 ms)
-    VISO_HIP_CHECK(hipEventCreateWithFlags(&geo_fork, hipEventDisableTiming));
-    VISO_HIP_CHECK(hipEventCreateWithFlags(&geo_join, hipEventDisableTiming));
+    VISO_HIP_CHECK(hipEventCreateWithFlags(&geo_fork, gpu_event_flags()));
+    VISO_HIP_CHECK(hipEventCreateWithFlags(&geo_join, gpu_event_flags()));
     VISO_HIP_CHECK(hipEventCreateWithFlags(&ntrack_evt, hipEventDisableTiming));
     VISO_HIP_CHECK(hipEventCreateWithFlags(&gate_evt, hipEventDisableTiming));
-    for (auto& e : epoch_evt) VISO_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    VISO_HIP_CHECK(hipEventCreateWithFlags(&epoch_now, hipEventDisableTiming));
-    VISO_HIP_CHECK(hipEventCreateWithFlags(&up_done, hipEventDisableTiming));
+    for (auto& e : epoch_evt) VISO_HIP_CHECK(hipEventCreateWithFlags(&e, gpu_event_flags()));
+    VISO_HIP_CHECK(hipEventCreateWithFlags(&epoch_now, gpu_event_flags()));
     if (const char* e = getenv("VISO_GATE_SPEC")) gate_spec_mode = e[0] == '1' ? 1 : 0;
     rc = bg_prepare();
     if (rc) return rc;
@@ -201,8 +218,6 @@ void viso_ctx::release() {
     }
     if (epoch_now) (void)hipEventDestroy(epoch_now);
     epoch_now = nullptr;
-    if (up_done) (void)hipEventDestroy(up_done);
-    up_done = nullptr;
     DevBuf* bufs[] = {&scratch_a, &scratch_b, &scratch_c, &scratch_d, &slot_pool, &slot_pose,
                       &kp1, &kp2, &kp1b, &kp2b, &track_success, &n_track_dev, &fast_rows,
                       &geo_buf, &map_pts, &kf_poses, &direct_buf, &direct_stats,
@@ -216,13 +231,6 @@ void viso_ctx::release() {
     stage.release();
     if (up_stream) (void)hipStreamDestroy(up_stream);
     up_stream = nullptr;
-    if (pyr_stream) {
-        (void)hipStreamSynchronize(pyr_stream);
-        (void)hipStreamDestroy(pyr_stream);
-    }
-    pyr_stream = nullptr;
-    if (up_dma) (void)hipEventDestroy(up_dma);
-    up_dma = nullptr;
     h_ctl = nullptr;
     h_int = nullptr;
     h_dbl = nullptr;
@@ -258,31 +266,6 @@ int viso_ctx::create_streams() {
     return VISO_OK;
 }
 
-bool viso_ctx::host_pyr_split() {
-    if (host_pyr_mode < 0) {
-        const char* e = getenv("VISO_HOST_PYR");
-        host_pyr_mode = (e && e[0] == 's') ? 1 : 0;
-    }
-    return host_pyr_mode != 0;
-}
-
-// A stream with a hardware queue of its own when a CU-masked stream (every
-// CU) can be made, else a plain one.
-int viso_ctx::create_masked_stream(hipStream_t* out) {
-    int cus = 0;
-    *out = nullptr;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0) {
-        std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
-        for (int c = 0; c < cus; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
-        if (hipExtStreamCreateWithCUMask(out, (uint32_t)mask.size(), mask.data()) != hipSuccess) *out = nullptr;
-    }
-    if (!*out) {
-        (void)hipGetLastError();
-        if (hipStreamCreateWithFlags(out, hipStreamNonBlocking) != hipSuccess) return VISO_ERR_HIP;
-    }
-    return VISO_OK;
-}
-
 // The upload stream (host ingest), with a hardware queue of its own when a
 // CU-masked stream can be made (a plain stream may share the context
 // stream's queue, behind the chain it should overlap: still correct).
@@ -311,10 +294,9 @@ int viso_ctx::acquire_slot(hipStream_t lk_wait) {
     // (on the stream that writes it first: the context stream, or the upload
     // stream) behind that batch (a no-op wait in steady state; a later batch
     // on the same stream also implies completion)
-    const int64_t use = slots[(size_t)s].lk_use;
-    if (use >= 0 && lk_seq > use) {
-        const int64_t e = (lk_seq - use <= kLkRing) ? use : lk_seq - 1;
-        (void)hipStreamWaitEvent(lk_wait ? lk_wait : stream, lk_ring[e % kLkRing], 0);
+    if (order_after_lk(slots[(size_t)s].lk_use, lk_wait ? lk_wait : stream)) {
+        free_slots.push_front(s);
+        return -1;
     }
     const int64_t fe = slots[(size_t)s].free_epoch;
     slots[(size_t)s] = SlotRec{};
@@ -323,11 +305,70 @@ int viso_ctx::acquire_slot(hipStream_t lk_wait) {
     return s;
 }
 
+// Order `st` behind lk_stream batch `use` — unless the host already knows it
+// is complete (a query of its event, or of a later one) or `st` already waits
+// for it or a later batch.  A cross-queue wait is a barrier packet costing the
+// waiting queue ~6-10 us even when its event completed long ago (round 6),
+// and a device-ingest caller past the pool's first lap reuses a slot per
+// frame.  Batches older than the event ring are covered by its oldest event
+// (lk_stream runs them in order).
+int viso_ctx::order_after_lk(int64_t use, hipStream_t st) {
+    if (use < 0 || use >= lk_seq || use < lk_done) return VISO_OK;
+    int64_t* waited = st == stream ? &lk_waited_ctx : st == up_stream ? &lk_waited_up : nullptr;
+    if (waited && use < *waited) return VISO_OK;
+    const int64_t e = (lk_seq - use <= kLkRing) ? use : lk_seq - kLkRing;
+    const hipError_t q = hipEventQuery(lk_ring[e % kLkRing]);
+    if (q == hipSuccess) {
+        lk_done = std::max(lk_done, e + 1);
+        return VISO_OK;
+    }
+    if (q != hipErrorNotReady) return VISO_ERR_HIP;
+    (void)hipGetLastError();  // (the query's own status)
+    VISO_HIP_CHECK(hipStreamWaitEvent(st, lk_ring[e % kLkRing], 0));
+    if (waited) *waited = e + 1;
+    return VISO_OK;
+}
+
 // The end of an ingest call: an event behind its work on the context stream
 // (the reuse of a slot it freed is ordered behind it on the upload stream).
+// Every event record on the context stream costs it a marker packet (~6-10
+// us of the queue's time on MI355X, gpurun_out/r06h: a host-frame caller paid
+// one per frame), so an epoch is recorded only every kEpochStride calls; a
+// slot's reuse waits for the oldest record made at or after the call that
+// freed it (wait_freed).
 int viso_ctx::end_epoch() {
-    VISO_HIP_CHECK(hipEventRecord(epoch_evt[epoch % kEpochRing], stream));
+    if (epoch - epoch_last_rec >= kEpochStride) {
+        const int k = (int)(epoch_nrec % kEpochRing);
+        VISO_HIP_CHECK(hipEventRecord(epoch_evt[k], stream));
+        epoch_rec_call[k] = epoch;
+        epoch_last_rec = epoch;
+        ++epoch_nrec;
+    }
     ++epoch;
+    return VISO_OK;
+}
+
+// Order work on `st` behind the context-stream work of call fe (the call
+// that freed a slot): the oldest epoch record made at or after it (records
+// are in call order on the in-order context stream), else — freed after the
+// last record — a record now, behind everything enqueued so far.
+int viso_ctx::wait_freed(int64_t fe, hipStream_t st) {
+    if (fe < 0) return VISO_OK;
+    const int64_t m = std::min<int64_t>(epoch_nrec, kEpochRing);
+    for (int64_t j = epoch_nrec - m; j < epoch_nrec; ++j) {
+        const int k = (int)(j % kEpochRing);
+        if (epoch_rec_call[k] >= fe) {
+            // (no barrier packet when the host sees the record complete)
+            const hipError_t q = hipEventQuery(epoch_evt[k]);
+            if (q == hipSuccess) return VISO_OK;
+            if (q != hipErrorNotReady) return VISO_ERR_HIP;
+            (void)hipGetLastError();
+            VISO_HIP_CHECK(hipStreamWaitEvent(st, epoch_evt[k], 0));
+            return VISO_OK;
+        }
+    }
+    VISO_HIP_CHECK(hipEventRecord(epoch_now, stream));
+    VISO_HIP_CHECK(hipStreamWaitEvent(st, epoch_now, 0));
     return VISO_OK;
 }
 
@@ -336,46 +377,29 @@ int viso_ctx::end_epoch() {
 // the context stream's: the epoch that freed it), and the context stream
 // waits for the DMA before the frame's pyramid.
 int viso_ctx::upload_host(int s, const uint8_t* grey, int32_t w, int32_t h, int32_t stride, bool pyramid) {
-    const int64_t fe = slots[(size_t)s].free_epoch;
-    if (fe >= 0) {
-        if (fe < epoch) {
-            const int64_t e = (epoch - fe <= kEpochRing) ? fe : epoch - 1;
-            VISO_HIP_CHECK(hipStreamWaitEvent(up_stream, epoch_evt[e % kEpochRing], 0));
-        } else {  // freed during this call: behind everything enqueued so far
-            VISO_HIP_CHECK(hipEventRecord(epoch_now, stream));
-            VISO_HIP_CHECK(hipStreamWaitEvent(up_stream, epoch_now, 0));
-        }
-    }
+    if (int rc = wait_freed(slots[(size_t)s].free_epoch, up_stream)) return rc;
     {
         TimedRegion t(timing, VISO_KERNEL_UPLOAD, up_stream);
         dev_tl.mark(frames, 0, up_stream);
-        VISO_HIP_CHECK(stage.upload(slot_base(s), grey, w, h, stride, up_stream));
+        VISO_HIP_CHECK(stage.upload(slot_base(s), grey, w, h, stride, up_stream, true));
         dev_tl.mark(frames, 1, up_stream);
     }
-    if (!pyramid) {
-        VISO_HIP_CHECK(hipStreamWaitEvent(stream, stage.last, 0));
-        return VISO_OK;
+    if (pyramid) {
+        // the frame's pyramid behind its upload, on the same stream: both
+        // beside the previous frame's chain
+        uint8_t* slot = slot_base(s);
+        const uint8_t* l0 = slot;
+        launch_ingest_pyramid(&l0, &slot, &s, 1, false, up_stream);
+        VISO_HIP_CHECK(hipGetLastError());
+        dev_tl.mark(frames, 2, up_stream);
     }
-    // the frame's pyramid behind its upload, on the same stream: both beside
-    // the previous frame's chain (VISO_HOST_PYR=split: on a stream of its
-    // own behind the DMA, so frame f's pyramid overlaps frame f+1's DMA)
-    uint8_t* slot = slot_base(s);
-    const uint8_t* l0 = slot;
-    hipStream_t ps = up_stream;
-    if (host_pyr_split()) {
-        if (!pyr_stream) {
-            if (int rc = create_masked_stream(&pyr_stream)) return rc;
-            VISO_HIP_CHECK(hipEventCreateWithFlags(&up_dma, hipEventDisableTiming));
-        }
-        VISO_HIP_CHECK(hipEventRecord(up_dma, up_stream));
-        VISO_HIP_CHECK(hipStreamWaitEvent(pyr_stream, up_dma, 0));
-        ps = pyr_stream;
-    }
-    launch_ingest_pyramid(&l0, &slot, &s, 1, false, ps);
-    VISO_HIP_CHECK(hipGetLastError());
-    dev_tl.mark(frames, 2, ps);
-    VISO_HIP_CHECK(hipEventRecord(up_done, ps));
-    VISO_HIP_CHECK(hipStreamWaitEvent(stream, up_done, 0));
+    // one event behind the DMA (and the pyramid): the staging buffer's reuse
+    // and the context stream's wait share it — each record is a marker packet
+    // on its queue and each cross-queue wait a barrier packet (round 6: ~6-10
+    // us of a queue's time each, gpurun_out/r06h), and this path pays them per
+    // frame
+    VISO_HIP_CHECK(stage.commit(up_stream));
+    VISO_HIP_CHECK(hipStreamWaitEvent(stream, stage.last, 0));
     return VISO_OK;
 }
 
@@ -439,6 +463,12 @@ void viso_ctx::launch_ingest_pyramid(const uint8_t* const* l0, uint8_t* const* d
     const int s = sl[n - 1];
     PyrOwn own{n - 1, state != VISO_STATE_RUNNING ? pose_of(s) : nullptr, false};
     if (bg_words) {  // the chunk's background-LK words (bg_begin), cleared by the tail launch
+        // (behind the previous chunk's resident grid, which still reads them:
+        // bg_end leaves that wait to the next clearing, order_after_lk)
+        if (bg_grid_pending) {
+            (void)order_after_lk(bg_grid_seq, st);
+            bg_grid_pending = false;
+        }
         own.zero = (int*)bg_buf.ptr;
         own.n_zero = (int)kBgWords;
     }
@@ -532,7 +562,7 @@ int viso_ctx::flush_lk_frames(hipStream_t ls, bool keep_last) {
     } else if (lk_seq > 0) {
         // the outputs may still be read by the last side batch's getters:
         // order behind the last side batch
-        VISO_HIP_CHECK(hipStreamWaitEvent(stream, lk_ring[(lk_seq - 1) % kLkRing], 0));
+        if (int rc = order_after_lk(lk_seq - 1, stream)) return rc;
     }
     // A host-frame caller's batch (side stream, beside the next frames'
     // chains): the chunk-resident grid's geometry — one workgroup per CU in
@@ -699,7 +729,7 @@ bool viso_ctx::bg_on() {
 
 int viso_ctx::bg_prepare() {
     VISO_HIP_CHECK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
-    VISO_HIP_CHECK(hipEventCreateWithFlags(&bg_done, hipEventDisableTiming));
+    VISO_HIP_CHECK(hipEventCreateWithFlags(&bg_done, gpu_event_flags()));
     int rc = bg_buf.ensure(sizeof(int) * (kBgWords + 32));
     if (rc) return rc;
     VISO_HIP_CHECK(hipMemsetAsync(bg_buf.ptr, 0, sizeof(int) * (kBgWords + 32), stream));
@@ -752,7 +782,13 @@ int viso_ctx::bg_begin(const std::vector<int>& chunk, bool zeroed) {
     // enqueued (bg_launch): its host-side cost (the cross-stream wait, the
     // launch on the masked queue, ~30 us) then overlaps that frame's chain
     // instead of holding the chain's first launch back.
-    if (!zeroed) VISO_HIP_CHECK(hipMemsetAsync(bg_buf.ptr, 0, sizeof(int) * bg_words, stream));
+    if (!zeroed) {
+        if (bg_grid_pending) {
+            if (int rc = order_after_lk(bg_grid_seq, stream)) return rc;
+            bg_grid_pending = false;
+        }
+        VISO_HIP_CHECK(hipMemsetAsync(bg_buf.ptr, 0, sizeof(int) * bg_words, stream));
+    }
     VISO_HIP_CHECK(hipEventRecord(bg_done, stream));
     bg_args = a;
     bg_active = true;
@@ -817,9 +853,18 @@ int viso_ctx::bg_end(bool drain) {
         launch_lk_drain(d, 3 * n_cu, stream);
         VISO_HIP_CHECK(hipGetLastError());
     }
-    VISO_HIP_CHECK(hipStreamWaitEvent(stream, bg_done, 0));
-    if (drain) {
+    // The context stream does not wait for the resident grid here (a
+    // barrier packet at every chunk's end, on the chain's queue): what it
+    // protects — the grid's words, cleared by the next chunk's pyramid tail —
+    // is ordered there (bg_grid_pending); slot reuse and the batched LK
+    // launch by their own lk_use / lk_seq ordering (order_after_lk); the
+    // getters synchronise lk_stream.  The per-frame log's count reads the
+    // rows on the context stream, so it keeps the wait.
+    if (drain && flog()) {
+        VISO_HIP_CHECK(hipStreamWaitEvent(stream, bg_done, 0));
         if (int rc = count_lk(bg_slots, stream)) return rc;
+    } else if (!drain) {
+        VISO_HIP_CHECK(hipStreamWaitEvent(stream, bg_done, 0));
     }
     // the error word reaches h_int[32] from the failing wave itself
     // (bg_err_host); the drain's item count (dev builds) by a copy
@@ -831,6 +876,8 @@ int viso_ctx::bg_end(bool drain) {
     VISO_HIP_CHECK(hipEventRecord(lk_ring[lk_seq % kLkRing], lk_stream));
     for (int s : bg_slots) slots[(size_t)s].lk_use = lk_seq;
     for (int s : kf_slots) slots[(size_t)s].lk_use = lk_seq;
+    bg_grid_pending = true;
+    bg_grid_seq = lk_seq;
     ++lk_seq;
     for (int s : bg_slots) drop(s);
     bg_slots.clear();

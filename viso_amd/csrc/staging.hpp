@@ -28,8 +28,25 @@ struct HostStage {
     double copy_us = 0.0;       // (VISO_HOST_TIMES) host time in the row copies
     bool timed = false;
 
-    // rows [0, h) of w bytes at src (row pitch stride) -> dst (packed), on s
-    hipError_t upload(uint8_t* dst, const uint8_t* src, int w, int h, int stride, hipStream_t s) {
+    int pending = -1;  // a buffer whose reuse event the caller records (upload(defer))
+
+    // The buffer's reuse event, recorded by the caller on `s` behind work that
+    // follows the DMA on the same stream (its pyramid): one marker per frame
+    // on that stream instead of two (each record is a marker packet).
+    hipError_t commit(hipStream_t s) {
+        if (pending < 0) return hipSuccess;
+        const int k = pending;
+        pending = -1;
+        hipError_t e = hipEventRecord(ev[k], s);
+        if (e != hipSuccess) return e;
+        used[k] = true;
+        last = ev[k];
+        return hipSuccess;
+    }
+
+    // rows [0, h) of w bytes at src (row pitch stride) -> dst (packed), on s;
+    // defer: the reuse event is left to commit()
+    hipError_t upload(uint8_t* dst, const uint8_t* src, int w, int h, int stride, hipStream_t s, bool defer = false) {
         const size_t bytes = (size_t)w * (size_t)h;
         const int k = next;
         next = (next + 1) % kRing;
@@ -51,6 +68,10 @@ struct HostStage {
         if (timed)
             copy_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
         if ((e = hipMemcpyAsync(dst, buf[k], bytes, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+        if (defer) {
+            pending = k;
+            return hipSuccess;
+        }
         if ((e = hipEventRecord(ev[k], s)) != hipSuccess) return e;
         used[k] = true;
         last = ev[k];
