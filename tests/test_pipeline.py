@@ -194,6 +194,62 @@ def test_gpu_host_ingest_slot_reuse():
         assert np.array_equal(a, b)
 
 
+_HQ = {}
+
+
+def _host_queue_oracle(n):
+    """The oracle over the bench sequence (stereo init at frame 0, n - 1
+    tracking frames): per-frame (nGood, cost, LK pairs, LK successes)."""
+    if n not in _HQ:
+        from viso_amd.synth import Sequence
+        seq = Sequence(1242, 375, seed=0)
+        left = [seq.image(f, 0) for f in range(n)]
+        right0 = seq.image(0, 1)
+        ov = oracle_lib.Viso(seq.K, 1242, 375, enable_tracking=1)
+        ov.set_stereo(seq.p.baseline, 128, 1)
+        ov.on_new_stereo(left[0], right0)
+        log = []
+        for f in range(1, n):
+            ov.on_new_frame(left[f])
+            s = ov.stats()
+            log.append((s[9], s[10], s[6], s[7]))
+        _HQ[n] = (seq, left, right0, ov.poses(), ov.points(), np.array(log), ov.alignment())
+    return _HQ[n]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chunk", ["16", "3", "0"])
+def test_gpu_host_frames_queued_match_oracle(chunk, monkeypatch):
+    """The drop-in's calling pattern (FrameSequence::RunOnce -> OnNewFrame,
+    include/frame_sequence.h:25-38) in a burst: frame 0's stereo pair, then
+    40 viso_process_frame calls with nothing read in between, so tracking
+    frames queue and run as chunks of up to VISO_HOST_CHUNK frames (16, the
+    default; 3; 0 = the frame-by-frame path).  Poses, the map, the per-frame
+    log (level-0 nGood / cost, LK pairs / successes of every frame) and the
+    last alignment equal the oracle's."""
+    import viso_amd
+    monkeypatch.setenv("VISO_HOST_CHUNK", chunk)
+    n = 41
+    seq, left, right0, oP, op, olog, oal = _host_queue_oracle(n)
+    v = viso_amd.Viso(*seq.K, width=1242, height=375, enable_tracking=1)
+    v.set_stereo(seq.p.baseline, 128, 1)
+    v.set_frame_log(True)
+    v.process(left[0], right0)
+    for f in range(1, n):
+        v.OnNewFrame(left[f])
+    v.synchronize()
+    gP, glog = v.poses, v.frame_log()
+    assert gP.shape == oP.shape == (n - 1, 12)
+    assert np.linalg.norm(gP - oP, axis=1).max() <= 1e-10 * np.linalg.norm(oP, axis=1).max()
+    assert np.array_equal(v.GetPoints(), op)
+    assert np.array_equal(glog[:, [0, 2, 3]], olog[:, [0, 2, 3]])
+    assert (np.abs(glog[:, 1] - olog[:, 1]) <= 1e-10 * np.abs(olog[:, 1])).all()
+    pk, sc, ub, ua = v.alignment()
+    assert np.array_equal(pk, oal[0]) and np.array_equal(sc, oal[1])
+    assert np.max(np.abs(ua - oal[3])) < 1e-6
+    v.close()
+
+
 @pytest.mark.gpu
 def test_gpu_as_shipped_mode():
     seq, gv, ov = _run_pair(0, enable_tracking=0)

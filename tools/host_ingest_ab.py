@@ -28,7 +28,8 @@ def main():
         variants.append((name, dict(kv.split("=", 1) for kv in env.split(",") if kv)))
     W, H = 1242, 375
     seq = Sequence(W, H, seed=0)
-    n = 1 + 4 + 2 * 32
+    per = int(os.environ.get("FRAMES", "32"))
+    n = 1 + 4 + 2 * per
     left = np.stack([seq.image(f, 0) for f in range(n)])
     right = np.stack([seq.image(f, 1) for f in range(n)])
     # the copy floor: numpy -> pinned
@@ -51,7 +52,7 @@ def main():
             old = {k: os.environ.get(k) for k in env}
             os.environ.update(env)
             try:
-                out = bench.measure_host_ingest(args, seq, W, H, left, right, lambda *a: None)
+                out = bench.measure_host_ingest(args, seq, W, H, left, right, lambda *a: None, n=per)
             finally:
                 for k, v in old.items():
                     if v is None:

@@ -352,6 +352,9 @@ struct viso_ctx {
     int build_lk_templates();
     // OnNewFrame on a frame whose pyramid is already built in `slot`
     int on_new_frame(int slot);
+    // one ingest chunk (viso_process_frames_device; queued host frames)
+    int ingest_chunk(const std::vector<int>& sl, const std::vector<const uint8_t*>& l0,
+                     const std::vector<const uint8_t*>& right, bool overlap_tail = false);
     // (pyramid: the frame's pyramid too, on the upload stream)
     int ingest_host(const uint8_t* grey, int32_t w, int32_t h, int32_t stride, int* slot_out, bool pyramid = false);
     // launch LKAlignment of every pending tracking frame (on `s`)
@@ -359,7 +362,8 @@ struct viso_ctx {
     // launch the pending final solve, if any
     int resolve_direct();
     // end of an ingest call: pending final solve, then the LK batch on `s`
-    int finish_call(hipStream_t s);
+    // (overlap: a chunk follows — its drain runs on lk_stream, bg_end)
+    int finish_call(hipStream_t s, bool overlap = false);
     // end of a host-frame call (viso_process_frame / _stereo) while
     // tracking: the final solve stays pending (the next frame's L(3) runs
     // it, as inside a device chunk) and the LK alignment of every queued
@@ -368,6 +372,12 @@ struct viso_ctx {
     // (getters, viso_synchronize, setters, stage calls, device ingest)
     int finish_host_call();
     int settle();
+    // host frames queued while tracking (slots, uploaded, held), run as chunks
+    std::vector<int> host_q;
+    int host_chunk = -1;  // frames per queued chunk (VISO_HOST_CHUNK; 0 off; -1 unread)
+    bool host_queue_eligible();
+    int queue_host_frame(const uint8_t* grey, int32_t w, int32_t h, int32_t stride);
+    int flush_host_q();
     int host_lk_batch() const;
     // host batches in the background-grid geometry (VISO_HOST_LK; -1 unread)
     int host_lk_mode = -1;
@@ -385,7 +395,7 @@ struct viso_ctx {
     bool lk_dedicated = false, up_dedicated = false;  // lk_stream / up_stream CU-masked (queue of their own)
     // (zeroed: the chunk's pyramid launch cleared the words)
     int bg_begin(const std::vector<int>& chunk, bool zeroed = false);
-    int bg_end(bool drain = true);
+    int bg_end(bool drain = true, bool overlap = false);
     // the grid's buffer, event and kernel warm-up (context init)
     int bg_prepare();
     // after a host sync: VISO_ERR_HIP if a background launch since the last
@@ -395,10 +405,14 @@ struct viso_ctx {
     bool bg_unchecked = false;
     bool bg_active = false;
     bool bg_launched = false;  // bg_begin cleared the words; the grid is launched after frame 0
-    // the last chunk's resident grid (lk_stream batch bg_grid_seq) may still
-    // read its words: the next clearing of them orders behind it first
-    bool bg_grid_pending = false;
-    int64_t bg_grid_seq = -1;
+    // two sets of the grid's words, alternating chunks (the previous chunk's
+    // grid and, when overlapped, its drain still read theirs on lk_stream);
+    // bg_set_seq: the lk_stream batch that last read each set (-1: none)
+    int bg_set = 1;
+    int64_t bg_set_seq[2] = {-1, -1};
+    int* bg_words_of(int set) const;
+    int tail_mode = -1;  // VISO_LK_TAIL (read once)
+    bool tail_overlap_on();
     int bg_mode = -1;        // VISO_LK_BG: 0 off, 1 on (read once; -1 unread)
     int bg_nb = 0;           // frames of the chunk
     int bg_cur = -1;         // chunk index of the frame on_new_frame is processing
@@ -409,7 +423,7 @@ struct viso_ctx {
     hipEvent_t bg_done = nullptr;
     viso::LkAlignArgs bg_args{};  // the chunk's launch (the drain reuses it)
     int* bg_ready(int idx) const {
-        return (bg_active && idx >= 0) ? (int*)bg_buf.ptr + idx : nullptr;
+        return (bg_active && idx >= 0) ? bg_args.bg_ready + idx : nullptr;  // (the chunk's word set)
     }
     // LKAlignment arguments common to the template and alignment launches
     viso::LkAlignArgs lk_args();

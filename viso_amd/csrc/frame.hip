@@ -463,13 +463,12 @@ void viso_ctx::launch_ingest_pyramid(const uint8_t* const* l0, uint8_t* const* d
     const int s = sl[n - 1];
     PyrOwn own{n - 1, state != VISO_STATE_RUNNING ? pose_of(s) : nullptr, false};
     if (bg_words) {  // the chunk's background-LK words (bg_begin), cleared by the tail launch
-        // (behind the previous chunk's resident grid, which still reads them:
-        // bg_end leaves that wait to the next clearing, order_after_lk)
-        if (bg_grid_pending) {
-            (void)order_after_lk(bg_grid_seq, st);
-            bg_grid_pending = false;
-        }
-        own.zero = (int*)bg_buf.ptr;
+        // (the set the next chunk uses: two sets alternate, so the previous
+        // chunk's grid and drain, which may still run on lk_stream, read the
+        // other; this one's last readers, two chunks back, are ordered first)
+        const int set = bg_set ^ 1;
+        (void)order_after_lk(bg_set_seq[set], st);
+        own.zero = bg_words_of(set);
         own.n_zero = (int)kBgWords;
     }
     ident_slot = own.ident_pose ? s : -1;
@@ -650,9 +649,92 @@ int viso_ctx::finish_host_call() {
 }
 
 int viso_ctx::settle() {
+    if (!host_q.empty()) {
+        VISO_HIP_CHECK(hipSetDevice(device));
+        if (int rc = flush_host_q()) return rc;
+    }
     if (!dpend && lk_pending.empty()) return VISO_OK;
     VISO_HIP_CHECK(hipSetDevice(device));
     return finish_call(lk_stream);
+}
+
+// Host frames while tracking (viso_process_frame): each call only uploads its
+// frame (the DMA on the upload stream) and queues it; queued frames run as a
+// device-ingest chunk (ingest_chunk: one batched pyramid launch, the
+// background LK grid, one cross-queue wait for the DMAs) once host_chunk are
+// queued, or at once when the context's previous chunk has finished (so a
+// caller slower than the GPU gets each frame started right away), and
+// whenever anything else is called (settle).  Per frame that leaves the
+// chain and the DMA; per chunk the pyramid launch pair, the grid and its end.
+// VISO_HOST_CHUNK=0 turns it off (the frame-by-frame path below).
+bool viso_ctx::host_queue_eligible() {
+    if (host_chunk < 0) {
+        const char* e = getenv("VISO_HOST_CHUNK");
+        host_chunk = e ? std::max(0, std::min(kLkBatch, atoi(e))) : 16;
+    }
+    return host_chunk > 0 && state == VISO_STATE_RUNNING && kf_interval <= 0 && bg_on() &&
+           direct_fits_background() && n_map > 0 && lk_tmpl.ptr;
+}
+
+int viso_ctx::queue_host_frame(const uint8_t* grey, int32_t w, int32_t h, int32_t stride) {
+    if (w != p.width || h != p.height || stride < w || !grey) return VISO_ERR_ARG;
+    // per-frame work left by the frame-by-frame path first (in order)
+    if (dpend || !lk_pending.empty()) {
+        if (int rc = finish_call(lk_stream)) return rc;
+    }
+    if (!up_stream) {
+        if (int rc = create_up_stream()) return rc;
+    }
+    int s = acquire_slot(up_stream);
+    if (s < 0 && !host_q.empty()) {  // the queue holds the pool's last slots
+        if (int rc = flush_host_q()) return rc;
+        s = acquire_slot(up_stream);
+    }
+    if (s < 0) return VISO_ERR_CAPACITY;
+    if (int rc = wait_freed(slots[(size_t)s].free_epoch, up_stream)) {
+        hold(s);
+        drop(s);
+        return rc;
+    }
+    {
+        TimedRegion t(timing, VISO_KERNEL_UPLOAD, up_stream);
+        const hipError_t e = stage.upload(slot_base(s), grey, w, h, stride, up_stream);
+        if (e != hipSuccess) {
+            hold(s);
+            drop(s);
+            return VISO_ERR_HIP;
+        }
+    }
+    hold(s);  // queued
+    host_q.push_back(s);
+    bool idle = true;
+    if (lk_seq > 0) {
+        // the previous chunk's end: its grid's event (lk_stream), recorded after
+        // the chunk's last pose
+        const hipError_t q = hipEventQuery(lk_ring[(lk_seq - 1) % kLkRing]);
+        if (q == hipErrorNotReady) {
+            (void)hipGetLastError();
+            idle = false;
+        } else if (q != hipSuccess) {
+            return VISO_ERR_HIP;
+        }
+    }
+    if ((int)host_q.size() >= host_chunk || idle) return flush_host_q();
+    return VISO_OK;
+}
+
+int viso_ctx::flush_host_q() {
+    if (host_q.empty()) return VISO_OK;
+    std::vector<int> sl;
+    sl.swap(host_q);
+    // the chunk's DMAs (the upload stream is in order: its last one)
+    if (hipStreamWaitEvent(stream, stage.last, 0) != hipSuccess) {
+        for (int s : sl) drop(s);
+        return VISO_ERR_HIP;
+    }
+    std::vector<const uint8_t*> l0;
+    for (int s : sl) l0.push_back(slot_base(s));
+    return ingest_chunk(sl, l0, {}, tail_overlap_on());
 }
 
 int viso_ctx::resolve_direct() {
@@ -669,7 +751,7 @@ int viso_ctx::resolve_direct() {
     return VISO_OK;
 }
 
-int viso_ctx::finish_call(hipStream_t ls) {
+int viso_ctx::finish_call(hipStream_t ls, bool overlap) {
     int rc = resolve_direct();
     if (rc) {
         // still tear the background state down (its held frames, the pending
@@ -678,7 +760,7 @@ int viso_ctx::finish_call(hipStream_t ls) {
         return rc;
     }
     if (bg_active) {
-        rc = bg_end();
+        rc = bg_end(true, overlap);
         if (rc) return rc;
     }
     return flush_lk(ls);
@@ -714,6 +796,17 @@ int viso_ctx::stage_poses() {
 bool viso_ctx::bg_eligible() { return bg_on() && direct_fits_background() && state == VISO_STATE_RUNNING && n_map > 0 &&
                                       lk_tmpl.ptr && kf_interval <= 0 && !dpend && lk_pending.empty(); }
 
+// (VISO_LK_TAIL=0: every chunk's drain on the context stream, as round 5)
+bool viso_ctx::tail_overlap_on() {
+    if (tail_mode < 0) {
+        const char* e = getenv("VISO_LK_TAIL");
+        tail_mode = (e && e[0] == '0') ? 0 : 1;
+    }
+    return tail_mode != 0;
+}
+
+int* viso_ctx::bg_words_of(int set) const { return (int*)bg_buf.ptr + (size_t)set * kBgWords; }
+
 bool viso_ctx::bg_on() {
     if (bg_mode < 0) {
         // off on request, and when kernels are serialised (the resident grid
@@ -730,9 +823,10 @@ bool viso_ctx::bg_on() {
 int viso_ctx::bg_prepare() {
     VISO_HIP_CHECK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
     VISO_HIP_CHECK(hipEventCreateWithFlags(&bg_done, gpu_event_flags()));
-    int rc = bg_buf.ensure(sizeof(int) * (kBgWords + 32));
+    // two word sets (alternating chunks) + the sticky error words
+    int rc = bg_buf.ensure(sizeof(int) * (2 * kBgWords + 32));
     if (rc) return rc;
-    VISO_HIP_CHECK(hipMemsetAsync(bg_buf.ptr, 0, sizeof(int) * (kBgWords + 32), stream));
+    VISO_HIP_CHECK(hipMemsetAsync(bg_buf.ptr, 0, sizeof(int) * (2 * kBgWords + 32), stream));
     warm_lk_bg(stream);
     // lk_stream's first dispatch (its hardware queue is brought up then) and
     // a cross-stream event hand-off, here rather than in the first chunk's
@@ -761,10 +855,11 @@ int viso_ctx::bg_begin(const std::vector<int>& chunk, bool zeroed) {
     a.success = (uint8_t*)lk_succ.ptr;
     a.uv_before = (double*)lk_before.ptr;
     a.uv_after = (double*)lk_after.ptr;
-    a.bg_ready = (int*)bg_buf.ptr;
+    const int set = bg_set ^ 1;  // (the set the pyramid tail cleared)
+    a.bg_ready = bg_words_of(set);
     a.bg_next = a.bg_ready + kLkBatch;
     a.bg_left = a.bg_next + 8 * 32 + 32;
-    a.bg_err = a.bg_ready + bg_words;
+    a.bg_err = (int*)bg_buf.ptr + 2 * bg_words;
     a.bg_err_host = h_int_dev + 32;
     a.bg_items = nb * n_map;
     // tests: VISO_LK_BG_IDLE_US shortens the resident waves' patience, so the
@@ -783,13 +878,11 @@ int viso_ctx::bg_begin(const std::vector<int>& chunk, bool zeroed) {
     // launch on the masked queue, ~30 us) then overlaps that frame's chain
     // instead of holding the chain's first launch back.
     if (!zeroed) {
-        if (bg_grid_pending) {
-            if (int rc = order_after_lk(bg_grid_seq, stream)) return rc;
-            bg_grid_pending = false;
-        }
-        VISO_HIP_CHECK(hipMemsetAsync(bg_buf.ptr, 0, sizeof(int) * bg_words, stream));
+        if (int rc = order_after_lk(bg_set_seq[set], stream)) return rc;
+        VISO_HIP_CHECK(hipMemsetAsync(a.bg_ready, 0, sizeof(int) * bg_words, stream));
     }
     VISO_HIP_CHECK(hipEventRecord(bg_done, stream));
+    bg_set = set;
     bg_args = a;
     bg_active = true;
     bg_unchecked = true;
@@ -836,7 +929,7 @@ int viso_ctx::bg_check() {
 // context stream), then the context stream waits for the resident grid (its
 // outputs, the held frames), which is the latest LK batch of the flush_lk
 // bookkeeping.
-int viso_ctx::bg_end(bool drain) {
+int viso_ctx::bg_end(bool drain, bool overlap) {
     // a chunk whose first frame ended in an error before bg_launch (drain =
     // false) has no grid: bg_done still marks the memset, so the waits below
     // hold nothing back
@@ -847,7 +940,18 @@ int viso_ctx::bg_end(bool drain) {
     // (drain = false: the error path of finish_call; the chunk's last pose was
     // not launched, so no drain runs: the resident grid's waves give their
     // items back and leave, and the context stream only waits for them)
-    if (drain) {
+    if (drain && overlap) {
+        // a chunk another one follows: the drain goes on lk_stream behind the
+        // resident grid, in the grid's geometry (one workgroup per CU beside
+        // the chain's), so the chunk's LK tail (its last frame's points, whose
+        // pose the final solve gives) overlaps the next chunk's pyramid and
+        // chain instead of holding the context stream ~60-70 us
+        LkAlignArgs d = bg_args;
+        d.bg_drain = 1;
+        launch_lk_bg(d, n_cu, lk_stream);
+        VISO_HIP_CHECK(hipGetLastError());
+        VISO_HIP_CHECK(hipEventRecord(bg_done, lk_stream));
+    } else if (drain) {
         LkAlignArgs d = bg_args;
         d.bg_drain = 1;
         launch_lk_drain(d, 3 * n_cu, stream);
@@ -876,8 +980,10 @@ int viso_ctx::bg_end(bool drain) {
     VISO_HIP_CHECK(hipEventRecord(lk_ring[lk_seq % kLkRing], lk_stream));
     for (int s : bg_slots) slots[(size_t)s].lk_use = lk_seq;
     for (int s : kf_slots) slots[(size_t)s].lk_use = lk_seq;
-    bg_grid_pending = true;
-    bg_grid_seq = lk_seq;
+    // (the words' last readers: this batch's grid, and its drain when it ran
+    // on lk_stream; a drain on the context stream precedes any later clearing
+    // there)
+    bg_set_seq[bg_set] = lk_seq;
     ++lk_seq;
     for (int s : bg_slots) drop(s);
     bg_slots.clear();
@@ -1322,6 +1428,66 @@ int viso_ctx::on_new_frame(int cur) {
     return VISO_OK;
 }
 
+// One ingest chunk (the frames' slots, held by the caller's hold; their level
+// 0 at l0[i] — borrowed from the caller's device buffer, or already in the
+// slot; right[i] the right image or null): the chunk's pyramids in one
+// batched launch, the background LK grid when eligible, OnNewFrame per frame,
+// then the chunk's end.  Releases the chunk's holds, also on an error.
+int viso_ctx::ingest_chunk(const std::vector<int>& sl, const std::vector<const uint8_t*>& l0,
+                           const std::vector<const uint8_t*>& right, bool overlap_tail) {
+    const int nb = (int)sl.size();
+    std::vector<uint8_t*> dst;
+    for (int s : sl) dst.push_back(slot_base(s));
+    // a background-LK chunk's words are cleared by the pyramid's tail
+    // launch (bg_begin then makes no memset launch)
+    const bool bg = bg_eligible() && nb <= kLkBatch;
+    launch_ingest_pyramid(l0.data(), dst.data(), sl.data(), nb, bg);
+    if (hipGetLastError() != hipSuccess) {
+        for (int s : sl) drop(s);
+        return VISO_ERR_HIP;
+    }
+    // (the background words' memset stays behind the pyramid: issued
+    // ahead of it, the chain ran at half speed in 3 of 6 bench runs,
+    // profiles/r05_bg_order_ab.log)
+    if (const int rc = bg_begin(sl, bg)) {
+        for (int s : sl) drop(s);
+        return rc;
+    }
+    // end of the chunk, also on an error: launch what still reads the
+    // chunk's borrowed frames (the pending final solve, the LK batch),
+    // give retained frames their own level 0, release the chunk's holds
+    auto end_chunk = [&](int rc) -> int {
+        const int r1 = finish_call(stream, overlap_tail && !rc);
+        if (!rc) rc = r1;
+        const int roles[2] = {ref_slot, last_slot};
+        for (int r : roles) {
+            const int r2 = own_level0(r);
+            if (!rc) rc = r2;
+        }
+        for (int s : kf_slots) {
+            const int r2 = own_level0(s);
+            if (!rc) rc = r2;
+        }
+        for (int s : sl) drop(s);
+        return rc;
+    };
+    for (int i = 0; i < nb; ++i) {
+        right_l0 = right.empty() ? nullptr : right[(size_t)i];
+        bg_cur = i;
+        const int rc = on_new_frame(sl[(size_t)i]);
+        right_l0 = nullptr;
+        if (rc) return end_chunk(rc);
+        if (i == 0) {
+            const int r2 = bg_launch();
+            if (r2) return end_chunk(r2);
+        }
+    }
+    // the last frame's final solve, then the chunk's LKAlignment batch
+    // behind the chunk (the GPU is free then; beside the next chunk it
+    // would take the CU resources the latency-bound direct chain needs)
+    return end_chunk(VISO_OK);
+}
+
 // ------------------------------------------------------------------ C ABI
 extern "C" {
 
@@ -1330,6 +1496,14 @@ int viso_process_frame(viso_ctx* c, const uint8_t* grey, int32_t width, int32_t 
     if (!c) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(c->device));
     HostTimes::Clock ht(c->host_times);
+    if (c->host_queue_eligible()) {
+        // tracking: queue the frame (its DMA), run queued frames as chunks
+        int rc = c->queue_host_frame(grey, width, height, stride);
+        ht.lap(0);
+        const int re = c->end_epoch();
+        return rc ? rc : re;
+    }
+    if (int rc = c->flush_host_q()) return rc;  // (frames queued before: in order)
     int s = -1;
     // upload and pyramid on the upload stream (ingest_host)
     int rc = c->ingest_host(grey, width, height, stride, &s, true);
@@ -1348,6 +1522,7 @@ int viso_process_stereo(viso_ctx* c, const uint8_t* left, const uint8_t* right,
                         const int32_t dims[3]) {
     if (!c || !left || !right || !dims) return VISO_ERR_ARG;
     VISO_HIP_CHECK(hipSetDevice(c->device));
+    if (int rc = c->flush_host_q()) return rc;  // (frames queued before: in order)
     int sl = -1, sr = -1;
     int rc = c->ingest_host(left, dims[0], dims[1], dims[2], &sl, true);
     if (rc) return rc;
@@ -1384,8 +1559,7 @@ int viso_process_frames_device(viso_ctx* c, const uint8_t* d_left, const uint8_t
         // which covers at most kLkBatch frames: chunks are cut to that
         nb = std::min(c->bg_eligible() ? std::min(B, kLkBatch) : B, n - f0);
         std::vector<int> sl;
-        std::vector<const uint8_t*> l0;
-        std::vector<uint8_t*> dst;
+        std::vector<const uint8_t*> l0, right;
         // left images only: the right image is read at level 0, in place, by
         // the stereo initialisation (no stage consumes a right pyramid)
         for (int i = 0; i < nb; ++i) {
@@ -1401,57 +1575,9 @@ int viso_process_frames_device(viso_ctx* c, const uint8_t* d_left, const uint8_t
             c->hold(s);  // pending in this chunk
             sl.push_back(s);
             l0.push_back(src);
-            dst.push_back(c->slot_base(s));
+            right.push_back(d_right ? d_right + frame_stride * (size_t)f : nullptr);
         }
-        // a background-LK chunk's words are cleared by the pyramid's tail
-        // launch (bg_begin then makes no memset launch)
-        const bool bg = c->bg_eligible() && nb <= kLkBatch;
-        c->launch_ingest_pyramid(l0.data(), dst.data(), sl.data(), (int)l0.size(), bg);
-        VISO_HIP_CHECK(hipGetLastError());
-        // (the background words' memset stays behind the pyramid: issued
-        // ahead of it, the chain ran at half speed in 3 of 6 bench runs,
-        // profiles/r05_bg_order_ab.log)
-        {
-            const int rc = c->bg_begin(sl, bg);
-            if (rc) {
-                for (int s : sl) c->drop(s);
-                return rc;
-            }
-        }
-        // end of the chunk, also on an error: launch what still reads the
-        // chunk's borrowed frames (the pending final solve, the LK batch),
-        // give retained frames their own level 0, release the chunk's holds
-        auto end_chunk = [&](int rc) -> int {
-            const int r1 = c->finish_call(c->stream);
-            if (!rc) rc = r1;
-            const int roles[2] = {c->ref_slot, c->last_slot};
-            for (int r : roles) {
-                const int r2 = c->own_level0(r);
-                if (!rc) rc = r2;
-            }
-            for (int s : c->kf_slots) {
-                const int r2 = c->own_level0(s);
-                if (!rc) rc = r2;
-            }
-            for (int s : sl) c->drop(s);
-            return rc;
-        };
-        for (int i = 0; i < nb; ++i) {
-            c->right_l0 = d_right ? d_right + frame_stride * (size_t)(f0 + i) : nullptr;
-            c->bg_cur = i;
-            const int rc = c->on_new_frame(sl[(size_t)i]);
-            c->right_l0 = nullptr;
-            if (rc) return end_chunk(rc);
-            if (i == 0) {
-                const int r2 = c->bg_launch();
-                if (r2) return end_chunk(r2);
-            }
-        }
-        // the last frame's final solve, then the chunk's LKAlignment batch
-        // behind the chunk (the GPU is free then; beside the next chunk it
-        // would take the CU resources the latency-bound direct chain needs)
-        const int rc = end_chunk(VISO_OK);
-        if (rc) return rc;
+        if (int rc = c->ingest_chunk(sl, l0, right, f0 + nb < n && c->tail_overlap_on())) return rc;
     }
     return c->end_epoch();
 }
