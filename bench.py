@@ -445,7 +445,7 @@ def cpu_oracle_run(seq, W, H, left, right, warm, n, copies=False):
     return dt, ov
 
 
-def measure_host_ingest(args, seq, W, H, left, right, log, n=32, warm=4):
+def measure_host_ingest(args, seq, W, H, left, right, log, n=96, warm=4):
     """host_ingest: the drop-in's own calling pattern —
     FrameSequence::RunOnce decoding one image and calling
     FrameHandler::OnNewFrame with it (include/frame_sequence.h:25-38;
@@ -457,7 +457,11 @@ def measure_host_ingest(args, seq, W, H, left, right, log, n=32, warm=4):
     sync.  Pass 2 (the next n frames): the library's HIP-event groups per frame
     (upload, pyramid, direct chain, LK alignment on the side stream) and the
     host time of the final sync.  The poses are compared with the oracle's
-    after the CPU leg (parity_vs_oracle)."""
+    after the CPU leg (parity_vs_oracle).  n = 96 (round 6; 32 before): while
+    tracking, host frames queue and run as chunks that grow while the caller
+    is ahead of the GPU (viso_process_frame, VISO_HOST_CHUNK), so the first
+    frames of a burst carry the startup and 96 frames measure the steady
+    state."""
     import viso_amd
     v = viso_amd.Viso(*seq.K, width=W, height=H, enable_tracking=1)
     v.set_stereo(seq.p.baseline, STEREO_MAX_DISP, 1)
@@ -494,11 +498,12 @@ def measure_host_ingest(args, seq, W, H, left, right, log, n=32, warm=4):
            "us_per_frame": round(1e6 * (t2 - t0) / n, 1),
            "host_enqueue_us_per_frame": round(1e6 * (t1 - t0) / n, 1),
            "split_us_per_frame": split,
-           "split_note": "pass 2 (frames %d-%d) with HIP events around each group; direct = the frame's four level "
-                         "launches, the previous frame's final solve merged into its L(3) (a frame's own final "
-                         "solve stays pending until the next call); lkalign = side-stream batches of up to "
-                         "host_lk_batch() (<= 8) queued frames; final sync host time in sync_us"
-                         % (f0 + n, f0 + 2 * n - 1),
+           "split_note": "pass 2 (frames %d-%d) with HIP events around each group, per frame: upload = the "
+                         "frame's DMA from the pinned staging (upload stream); tracking frames queue and run "
+                         "as device-ingest chunks of up to 16 (viso_process_frame), so pyramid = the chunks' "
+                         "batched pyramid launches, direct = the frame's four level launches, lkalign = the "
+                         "chunks' background LK grids over their lifetime beside the chains; final sync host "
+                         "time in sync_us" % (f0 + n, f0 + 2 * n - 1),
            "frames_total": f0 + 2 * n,
            "sync_us": round(1e6 * (t4 - t3), 1),
            "_poses": poses}
@@ -882,7 +887,7 @@ def main():
     if rank == 0 and not args.no_init:
         init_leg = measure_init_frames(args, seq, W, H, d_left, left, log)
     host_ingest = None
-    if rank == 0 and not args.no_host_ingest and len(left) >= 1 + 4 + 2 * 32:
+    if rank == 0 and not args.no_host_ingest and len(left) >= 1 + 4 + 2 * 96:
         host_ingest = measure_host_ingest(args, seq, W, H, left, right, log)
     other = other_poses = None
     if rank == 0 and not args.no_other:
