@@ -107,11 +107,23 @@ void d_pixel_d_xi(const double K[4], const double* R, const double* T, const dou
 }
 
 // Per-map-point partial sums of one DirectPoseEstimationSingleLayer
-// iteration (28 = 21 upper-triangle H + 6 b + 1 cost, all tree sums over the
-// 64 patch pixels).  Returns false if the point is not "good" (:704-715).
-// With `running` (literal order) the pixel terms are instead added straight
-// into the level's running sums, x outer / y inner, as H += J J^T,
-// b += -error J, cost += error^2 do at src/viso.cpp:722-729.
+// iteration (28 = 21 upper-triangle H + 6 b + 1 cost).  Returns false if the
+// point is not "good" (:704-715).
+// Canonical (tree) form, factored (round 6): the reference's per-pixel
+// J = -J_img_pixel^T J_pixel_xi (:725) has J_pixel_xi computed once per point
+// (:718), so over the patch
+//   sum_p J J^T  = Jp^T G Jp,  G = sum_p g g^T  (g = J_img_pixel)
+//   sum_p -e J   = Jp^T (sum_p e g)
+// i.e. six pixel sums (g0 g0, g0 g1, g1 g1, e g0, e g1, e e; each the
+// descending pairwise tree tree_sum_desc64, the device's reduce_scatter_6_desc)
+// and then, per H entry (a, b), (G00 (Jp0a Jp0b) + G01 (Jp0a Jp1b + Jp1a Jp0b))
+// + G11 (Jp1a Jp1b), per b entry (e g0) Jp0a + (e g1) Jp1a, and the cost
+// sum e e — the same real-number sums as the reference's, rounded
+// differently; tests/test_literal_drift.py bounds what that does to the
+// poses against the literal form below.
+// With `running` (literal order) the pixel terms are instead formed per pixel
+// and added straight into the level's running sums, x outer / y inner, as
+// H += J J^T, b += -error J, cost += error^2 do at src/viso.cpp:722-729.
 bool direct_point_partials(const PyrView& last, const PyrView& cur, const Pose& last_pose,
                            const Pose& cur_pose, const double K[4], const double* P, int level,
                            double out[28], double* running = nullptr) {
@@ -126,7 +138,7 @@ bool direct_point_partials(const PyrView& last, const PyrView& cur, const Pose& 
     if (!good) return false;
     double Jpx[12];
     d_pixel_d_xi(K, cur_pose.R, cur_pose.t, P, kScales[level], Jpx);
-    static thread_local double leaf[28][64];
+    static thread_local double leaf[6][64];
     const uint8_t* L = last.level(level);
     const uint8_t* C = cur.level(level);
     for (int x = -4; x < 4; ++x)
@@ -136,18 +148,37 @@ bool direct_point_partials(const PyrView& last, const PyrView& cur, const Pose& 
                                  sample(C, cur.w[level], cur.h[level], u_cur + x, v_cur + y);
             double g0, g1;
             gradient(C, cur.w[level], cur.h[level], u_cur + x, v_cur + y, g0, g1);
-            double J[6];
-            for (int k = 0; k < 6; ++k) J[k] = -g0 * Jpx[k] + -g1 * Jpx[6 + k];
-            int idx = 0;
-            for (int a = 0; a < 6; ++a)
-                for (int b = a; b < 6; ++b) leaf[idx++][p] = J[a] * J[b];
-            for (int k = 0; k < 6; ++k) leaf[21 + k][p] = -error * J[k];
-            leaf[27][p] = error * error;
-            if (running)
-                for (int k = 0; k < 28; ++k) running[k] = running[k] + leaf[k][p];
+            if (running) {
+                double J[6];
+                for (int k = 0; k < 6; ++k) J[k] = -g0 * Jpx[k] + -g1 * Jpx[6 + k];
+                int idx = 0;
+                for (int a = 0; a < 6; ++a)
+                    for (int b = a; b < 6; ++b) {
+                        running[idx] = running[idx] + J[a] * J[b];
+                        ++idx;
+                    }
+                for (int k = 0; k < 6; ++k) running[21 + k] = running[21 + k] + -error * J[k];
+                running[27] = running[27] + error * error;
+                continue;
+            }
+            leaf[0][p] = g0 * g0;
+            leaf[1][p] = g0 * g1;
+            leaf[2][p] = g1 * g1;
+            leaf[3][p] = error * g0;
+            leaf[4][p] = error * g1;
+            leaf[5][p] = error * error;
         }
-    if (!running)
-        for (int k = 0; k < 28; ++k) out[k] = tree_sum_desc64(leaf[k]);  // device reduce_scatter_28_desc
+    if (running) return true;
+    double G[6];
+    for (int k = 0; k < 6; ++k) G[k] = tree_sum_desc64(leaf[k]);  // device reduce_scatter_6_desc
+    const double* J0 = Jpx;      // dPixel/dXi row 0 (u)
+    const double* J1 = Jpx + 6;  // row 1 (v)
+    int idx = 0;
+    for (int a = 0; a < 6; ++a)
+        for (int b = a; b < 6; ++b)
+            out[idx++] = (G[0] * (J0[a] * J0[b]) + G[1] * (J0[a] * J1[b] + J1[a] * J0[b])) + G[2] * (J1[a] * J1[b]);
+    for (int a = 0; a < 6; ++a) out[21 + a] = G[3] * J0[a] + G[4] * J1[a];
+    out[27] = G[5];
     return true;
 }
 

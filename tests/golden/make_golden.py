@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Generate tests/golden/golden_v1.npz: frozen input/output vectors of the
+"""Generate tests/golden/golden_v2.npz: frozen input/output vectors of the
 per-frame path, written by the CPU oracle (oracle/, compiled in this
 container).
 
@@ -12,7 +12,13 @@ regenerated from a seed at test time, except the synthetic sequence frames:
 they are re-rendered by viso_amd.synth and checked against stored SHA-256
 hashes before use.
 
-    python tests/golden/make_golden.py      # rewrites golden_v1.npz
+    python tests/golden/make_golden.py      # rewrites golden_v2.npz
+
+golden_v2 (round 6) is golden_v1 (rounds 1-5) regenerated after the direct
+pose's per-point sums took the factored form (oracle_track.cpp
+direct_point_partials); only the sequence's fp64 outputs moved, in their last
+bits (tests/test_golden.py::test_factored_sums_vs_golden_v1 keeps v1 as the
+per-pixel form's frozen outputs).
 """
 from __future__ import annotations
 
@@ -26,7 +32,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 
-OUT = os.path.join(HERE, "golden_v1.npz")
+OUT = os.path.join(HERE, "golden_v2.npz")
 SEQ_FRAMES = 10  # synthetic seq (seed 0) initialises at frame 5, then tracks
 
 

@@ -1,5 +1,7 @@
-"""Golden vectors (tests/golden/golden_v1.npz, written by
-tests/golden/make_golden.py from the CPU oracle).
+"""Golden vectors (tests/golden/golden_v2.npz, written by
+tests/golden/make_golden.py from the CPU oracle; golden_v1.npz holds the
+same vectors from before the direct pose's factored per-point sums, kept as
+the per-pixel form's frozen outputs).
 
 The reference ships no fixtures and cannot be built here, so parity with the
 reference itself is unpinned. These vectors freeze the
@@ -19,7 +21,8 @@ import pytest
 
 from tests import oracle_lib
 
-GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "golden_v1.npz")
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "golden_v2.npz")
+GOLDEN_V1 = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "golden_v1.npz")
 W, H = 1242, 375
 
 
@@ -101,7 +104,7 @@ def test_oracle_sequence_golden():
     for f, img in enumerate(frames):
         v.on_new_frame(img)
         assert v.state == g["seq_states"][f], f
-        # stats[15] (keyframe count) postdates golden_v1, which holds 0 there
+        # stats[15] (keyframe count) postdates the golden files, which hold 0 there
         st = v.stats()
         assert np.array_equal(st[:15], g["seq_stats"][f][:15]), f
     assert np.array_equal(v.poses(), g["seq_poses"])
@@ -110,6 +113,31 @@ def test_oracle_sequence_golden():
     pk, sc, _, ua = v.alignment()
     assert np.array_equal(pk, g["seq_lk_pair"]) and np.array_equal(sc, g["seq_lk_success"])
     assert np.array_equal(ua, g["seq_lk_after"])
+
+
+def test_factored_sums_vs_golden_v1():
+    """The direct pose's per-point sums in the factored form (round 6:
+    Jp^T G Jp from six pixel sums, oracle_track.cpp direct_point_partials)
+    against golden_v1, frozen while the oracle formed the 28 products per
+    pixel: every discrete output equal (states, counts, decisions, LK pairs
+    and success flags), fp64 outputs equal to within their last bits (poses
+    measured 2.4e-17 rel, map points equal, LK positions 1.6e-17)."""
+    with np.load(GOLDEN_V1, allow_pickle=False) as z:
+        g1 = {k: z[k] for k in z.files}
+    g = golden()
+    for k in g1:
+        if g1[k].dtype.kind in "iub":
+            assert np.array_equal(g[k], g1[k]), k
+    assert np.array_equal(g["seq_states"], g1["seq_states"])
+    for f in range(len(g1["seq_stats"])):
+        for k in (0, 1, 2, 3, 4, 5, 6, 7, 9, 12):  # state, counts and decisions
+            assert g["seq_stats"][f][k] == g1["seq_stats"][f][k], (f, k)
+    assert _rel(g["seq_stats"], g1["seq_stats"]) < 1e-13
+    assert _rel(g["seq_poses"], g1["seq_poses"]) < 1e-15
+    assert np.array_equal(g["seq_points"], g1["seq_points"])
+    assert np.array_equal(g["seq_lk_pair"], g1["seq_lk_pair"])
+    assert np.array_equal(g["seq_lk_success"], g1["seq_lk_success"])
+    assert np.max(np.abs(g["seq_lk_after"] - g1["seq_lk_after"])) < 1e-9
 
 
 # ------------------------------------------------------------------ GPU vs golden

@@ -102,7 +102,7 @@ def main():
     entry = log[:, 0]
     print(f"{n} launches; tiles per launch {int(np.median(tiles))}")
     names = ["partials reduced (w0)", "solver starts", "LU", "inverse", "update", "SE3 exp", "solve done",
-             "after B2", "prefetch done (last wave)", "-", "block 0 exit"]
+             "after B2", "prefetch done (last wave)", "-", "block 0 exit", "first LU pass (VISO_LU_TWICE)"]
     print("phase (us from block 0 entry; mean over launches)      " +
           "  ".join(f"{x:>7s}" for x in ["F", "L0", "L1", "L2", "L3m", "L3"]))
     kinds = [(lvl == -1), (lvl == 0), (lvl == 1), (lvl == 2), (lvl == 3) & (merged == 1), (lvl == 3) & (merged == 0)]

@@ -384,16 +384,15 @@ __device__ inline double sample_cw(const uint8_t* __restrict__ img, int w, int h
     return sample_px(img, w, h, x, y);
 }
 
-// The 28 sums of one map point by reduce-scatter: returns good; a lane with
-// *idx >= 0 holds sum *idx in *out (reduce_scatter_28_desc).
 // The twelve quotients of one map point's projection (project_px) and
 // dPixel/dXi (d_pixel_d_xi), each with those functions' exact operations,
 // one per lane (lane k < 12) so that a single division sequence serves all
-// of them; every lane gets the results by readlane (wave-uniform values).
+// of them; the projection's two go to every lane by readlane (Q), J's ten
+// stay in their lanes (the return value; 0 in lanes >= 12).
 //   0: x / z, 1: y / z (the projection)        -> Q[0], Q[1]
 //   2..11: J[0], J[2], J[3], J[4], J[5], J[7], J[8], J[9], J[10], J[11]
-__device__ inline void point_quotients(const Intrinsics& K, const double* pose, const double* P, double scale,
-                                       double* Q, double* qt) {
+__device__ inline double point_quotients(const Intrinsics& K, const double* pose, const double* P, double scale,
+                                         double* Q, double* qt) {
     const int lane = threadIdx.x & 63;
     double Pc[3];
     mat3_vec(pose, P, Pc);
@@ -454,21 +453,80 @@ __device__ inline void point_quotients(const Intrinsics& K, const double* pose, 
     double q = (c1 * c2) / den;
     if (lane == 5) q = fx + q;
     if (lane == 9) q = -fy - q;
-#pragma unroll
-    for (int k = 0; k < 12; ++k) Q[k] = readlane_f64(q, k);
+    // the projection to every lane; J's ten stay in lanes 2..11 (the factored
+    // sums fetch them per lane, direct_point_rs), lanes >= 12 hold J's zeros
+    Q[0] = readlane_f64(q, 0);
+    Q[1] = readlane_f64(q, 1);
+    return lane < 12 ? q : 0.0;
 }
 
+// Source lanes of the four J entries lane k needs for sum k of the factored
+// form (point_sums_factored): J[a], J[6 + a], J[b], J[6 + b] with (a, b) the
+// k-th upper-triangle pair (k < 21) or a = k - 21 (b sums, k < 27).  J[j]
+// sits in lane 2 (j = 0), j + 1 (j = 2..5) or j (j = 7..11) of
+// point_quotients' result; J[1] = J[6] = 0 read lane 12.  Byte addresses for
+// ds_bpermute, packed 8 bits each.  Per wave, once.
+__device__ inline unsigned factored_sources() {
+    const int k = threadIdx.x & 31;  // (lanes >= 28 unused)
+    // per source s, 4 bits per lane: lanes 0-15 in lo[s], 16-27 in hi[s]
+    constexpr unsigned long long lo[4] = {0x43333ccccc222222ULL, 0x9888877777ccccccULL, 0x465436543c6543c2ULL,
+                                          0x9ba98ba987ba987cULL};
+    constexpr unsigned long long hi[4] = {0x26543c265544ULL, 0xcba987cbaa99ULL, 0xccccccc66565ULL,
+                                          0x7777777bbabaULL};
+    unsigned r = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        r |= (unsigned)((k < 16 ? lo[q] >> (4 * k) : hi[q] >> (4 * (k - 16))) & 15) << (8 * q);
+    return r;
+}
+
+// The six patch sums of the factored form by reduce-scatter in DESCENDING
+// xor order (partner lane ^ 32, ^ 16, ..., ^ 1: the pairwise tree of
+// oracle_common.hpp tree_sum_desc64 for each value).  xor 32: the halves keep
+// values 0-2 / 3-5 (v_permlane32_swap); xor 16: even rows keep the first,
+// odd rows the third of their three, both rows the second (v_permlane16_swap);
+// xor 8: lanes with bit 3 clear keep the row's first, the others the second
+// (DPP row_ror:8 is the xor-8 partner); then one value per lane: xor 4 by
+// row_shr / row_shl 4 + select, xor 2 / 1 by quad_perm.  Lane l ends with
+// value 3 * b5 + (b3 ? 1 : b4 ? 2 : 0): value v in lanes 0, 8, 16, 32, 40, 48.
+// Requires EXEC = all lanes.
+__device__ inline double reduce_scatter_6_desc(const double* v) {
+    const int lane = threadIdx.x & 63;
+    const bool b2 = lane & 4, b3 = lane & 8;
+    double a[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        double ra, rb;
+        permlane32_swap_f64(v[k], v[3 + k], ra, rb);
+        a[k] = ra + rb;
+    }
+    double ra, rb;
+    permlane16_swap_f64(a[0], a[2], ra, rb);
+    const double c0 = ra + rb;
+    permlane16_swap_f64(a[1], a[1], ra, rb);
+    const double c1 = ra + rb;
+    double d = dsel(b3, c1, c0) + dpp_f64<0x128>(dsel(b3, c0, c1));
+    const double r4 = dpp_f64<0x114>(d), l4 = dpp_f64<0x104>(d);  // row_shr / row_shl by 4
+    d = d + dsel(b2, r4, l4);
+    d = d + dpp_f64<0x4E>(d);  // lane ^ 2
+    d = d + dpp_f64<0xB1>(d);  // lane ^ 1
+    return d;
+}
+
+// The 28 sums of one map point (factored form, oracle direct_point_partials):
+// returns good; lane k < 28 holds sum k in *out (*idx = k, -1 elsewhere).
+// src_lanes: factored_sources() of this lane.
 __device__ inline bool direct_point_rs(const DirectArgs& a, const LevelPair& fp, int lv,
                                        const double* cur_pose,
                                        const RefSample& r, const uint8_t* win, const CurWin& cw,
-                                       double* out, int* idx, double* qt = nullptr) {
+                                       double* out, int* idx, unsigned src_lanes, double* qt = nullptr) {
     const int lane = threadIdx.x & 63;
     const int px = (lane >> 3) - 4, py = (lane & 7) - 4;
     const double scale = kScale[lv];
     const int w = a.g.w[lv], h = a.g.h[lv];
     // project_px and d_pixel_d_xi (bit-identical; divisions lane-parallel)
-    double Q[12];
-    point_quotients(a.K, cur_pose, r.P, scale, Q, qt);
+    double Q[2];
+    const double jq = point_quotients(a.K, cur_pose, r.P, scale, Q, qt);
     const double uc = scale * (Q[0] * a.K.fx + a.K.cx);
     const double vc = scale * (Q[1] * a.K.fy + a.K.cy);
     const double hp = 4.0;
@@ -529,20 +587,27 @@ __device__ inline bool direct_point_rs(const DirectArgs& a, const LevelPair& fp,
         g0 = 0.5 * (sample_cw(C, w, h, x + 1, y, win, cw) - sample_cw(C, w, h, x - 1, y, win, cw));
         g1 = 0.5 * (sample_cw(C, w, h, x, y + 1, win, cw) - sample_cw(C, w, h, x, y - 1, win, cw));
     }
-    const double Jp[12] = {Q[2], 0.0, Q[3], Q[4], Q[5], Q[6], 0.0, Q[7], Q[8], Q[9], Q[10], Q[11]};
-    double J[6];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) J[k] = -g0 * Jp[k] + -g1 * Jp[6 + k];
-    double leaf[kSums];
-    int e = 0;
-#pragma unroll
-    for (int rr = 0; rr < 6; ++rr)
-#pragma unroll
-        for (int c = rr; c < 6; ++c) leaf[e++] = J[rr] * J[c];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) leaf[21 + k] = -error * J[k];
-    leaf[27] = error * error;
-    *out = reduce_scatter_28_desc(leaf, idx);  // descending-xor pixel tree (oracle tree_sum_desc64)
+    // The factored sums (oracle direct_point_partials): J = -g^T Jp with Jp =
+    // dPixel/dXi constant over the patch, so sum_p J J^T = Jp^T G Jp and
+    // sum_p -e J = Jp^T (sum_p e g) with G = sum_p g g^T: six pixel sums
+    // (descending-xor trees, oracle tree_sum_desc64) instead of 28
+    const double leaf[6] = {g0 * g0, g0 * g1, g1 * g1, error * g0, error * g1, error * error};
+    const double s = reduce_scatter_6_desc(leaf);
+    // lane k < 28 forms sum k from the six and its four J entries
+    const unsigned sa = src_lanes;
+    const double p0a = bperm_f64(jq, (int)(sa & 0xff)), p1a = bperm_f64(jq, (int)((sa >> 8) & 0xff));
+    const double p0b = bperm_f64(jq, (int)((sa >> 16) & 0xff)), p1b = bperm_f64(jq, (int)(sa >> 24));
+    const double S0 = readlane_f64(s, 0), S1 = readlane_f64(s, 8), S2 = readlane_f64(s, 16);
+    const double S3 = readlane_f64(s, 32), S4 = readlane_f64(s, 40), S5 = readlane_f64(s, 48);
+    double o;
+    if (lane < 21)
+        o = (S0 * (p0a * p0b) + S1 * (p0a * p1b + p1a * p0b)) + S2 * (p1a * p1b);
+    else if (lane < 27)
+        o = S3 * p0a + S4 * p1a;
+    else
+        o = S5;
+    *out = o;
+    *idx = lane < kSums ? lane : -1;
     return true;
 }
 
@@ -819,14 +884,18 @@ __device__ inline void merged_ref(const DirectArgs& a, const LevelPair& fp, int 
 // wave_tree_sum_dpp on T slots) and stores them; the other waves are done.
 // `last_arriver` = false (the continuation, which reuses s_pts in a loop)
 // keeps the block-barrier form.
+constexpr unsigned kSrcHere = 0xffffffffu;  // direct_tile_pf: factored_sources() computed there
+
 template <bool FAST, bool LV16 = false, int W = kWaves>
 __device__ void direct_tile_pf(const DirectArgs& a, const LevelPair& fp, int lv, const double* cur_pose, int b,
                                const PfLds& pf, bool merged, double* part, int* good, double* s_pts,
-                               int* s_good, int* s_cnt = nullptr, double* s_qt = nullptr) {
+                               int* s_good, int* s_cnt = nullptr, double* s_qt = nullptr,
+                               unsigned src_in = kSrcHere) {
     const int wave = wave_id(), lane = threadIdx.x & 63;
     int first, T;
     tile_range(a, b, &first, &T);
     int good_cnt = 0;
+    const unsigned src_lanes = FAST ? 0u : src_in != kSrcHere ? src_in : factored_sources();
     for (int local = wave; local < T; local += W) {
         const int i = first + local;
         double f = 0.0;
@@ -866,7 +935,7 @@ __device__ void direct_tile_pf(const DirectArgs& a, const LevelPair& fp, int lv,
                 }
                 f = (double)ff;
             } else {
-                ok = direct_point_rs(a, fp, lv, cur_pose, r, pf.win[local], cw, &f, &idx,
+                ok = direct_point_rs(a, fp, lv, cur_pose, r, pf.win[local], cw, &f, &idx, src_lanes,
                                      s_qt ? s_qt + 12 * wave : nullptr);
             }
         }
@@ -1192,13 +1261,14 @@ __global__ __launch_bounds__(kThreads, 4) void direct_level_kernel(const double*
         PST(2);
         double* stp = (a.stats && blockIdx.x == 0) ? a.stats + (size_t)kStats * sl : nullptr;
 #ifdef VISO_PROBE
-        unsigned long long stamps[4] = {probe_t0, probe_t0, probe_t0, probe_t0};
+        unsigned long long stamps[5] = {probe_t0, probe_t0, probe_t0, probe_t0, probe_t0};
         if (FAST)
             solve_wave0_ldlt(L, 0, stp, stamps);
         else
             solve_wave0(L, 0, stp, stamps);
         if (blockIdx.x == 0 && lane == 0)
             for (int k = 0; k < 4; ++k) pst[3 + k] = stamps[k];
+        if (blockIdx.x == 0 && lane == 0) pst[12] = stamps[4];
 #else
         if (FAST)
             solve_wave0_ldlt(L, 0, stp);
@@ -1214,6 +1284,8 @@ __global__ __launch_bounds__(kThreads, 4) void direct_level_kernel(const double*
             __builtin_amdgcn_s_sleep(1);
     }
     if (wave == 0 && lane == 0 && !L.cont) after_solve(a, merged, L, s_last, s_pose);
+    // the factored sums' per-lane J sources (direct_point_rs), ahead of B2
+    const unsigned src_lanes = FAST ? 0u : factored_sources();
     __syncthreads();  // B2
     if (__builtin_expect(solve && L.cont, 0)) {
         // the continuation needs every thread; it leaves s_good dirty
@@ -1257,7 +1329,7 @@ __global__ __launch_bounds__(kThreads, 4) void direct_level_kernel(const double*
 #pragma unroll
         for (int k = 0; k < 12; ++k) pose[k] = s_pose[k];
         direct_tile_pf<FAST>(a, fp, lv, pose, blockIdx.x, s_pf, merged, a.s.part + (size_t)lv * kMaxTiles * kSums,
-                       a.s.good + lv * kMaxTiles, s_pts, &s_good, &s_cnt, qt);
+                       a.s.good + lv * kMaxTiles, s_pts, &s_good, &s_cnt, qt, src_lanes);
     }
 #ifdef VISO_PROBE
     // block 0 exit: its stamps to the launch's ring slot.  The exit stamp is

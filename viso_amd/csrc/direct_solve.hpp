@@ -156,6 +156,14 @@ __device__ __attribute__((always_inline)) inline void solve_wave0_rep(SolveLds& 
     // registers of every lane: no cross-lane traffic on the serial chain; the
     // pivot row is wave-uniform, so a row swap is a scalar branch + moves.
     double A[36];
+    int tr[6];
+#ifdef VISO_LU_TWICE
+    // probe experiment: the LU runs twice (the same instructions), the first
+    // pass's end stamped in stamps[4] -- a second pass faster than the first
+    // means the first waited on instruction fetch
+#pragma clang loop unroll(disable)
+    for (int rep = 0; rep < 2; ++rep) {
+#endif
 #pragma unroll
     for (int r = 0; r < 6; ++r)
 #pragma unroll
@@ -163,7 +171,6 @@ __device__ __attribute__((always_inline)) inline void solve_wave0_rep(SolveLds& 
             const int r1 = r < c ? r : c, c1 = r < c ? c : r;
             A[6 * r + c] = L.S[r1 * 6 - (r1 * (r1 - 1)) / 2 + (c1 - r1)];
         }
-    int tr[6];
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
         int p = k;
@@ -199,6 +206,13 @@ __device__ __attribute__((always_inline)) inline void solve_wave0_rep(SolveLds& 
 #pragma unroll
             for (int c = k + 1; c < 6; ++c) A[6 * i + c] = A[6 * i + c] - A[6 * i + k] * A[6 * k + c];
     }
+#ifdef VISO_LU_TWICE
+    if (rep == 0) {
+        asm volatile("" ::"v"(A[35]), "v"(A[0]));
+        if (stamps) stamps[4] = __builtin_amdgcn_s_memrealtime();
+    }
+    }
+#endif
     SPROBE(0);
     solve_after_lu(L, A, tr, h, iter, stats, stamps);
 }
