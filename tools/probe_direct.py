@@ -176,6 +176,28 @@ def main():
                 v = rel[:, :, w][valid[:, :, w]]
                 row.append(f"{np.median(v):5.2f}" if len(v) else "    -")
             print(f"L({L}) per wave, point(s) done after B2 (p50 us): " + " ".join(row[:15]) + f" | trees stored {row[15]}")
+    # per wave, its point's phases (VISO_PROBE_PT builds): start after B2,
+    # then quotients / samples / six sums / 28 sums, blocks < 32
+    if hasattr(lib, "viso_debug_probe_points"):
+        lib.viso_debug_probe_points.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        pp = np.zeros((128, 32, 16, 5), np.uint64)
+        mp = lib.viso_debug_probe_points(pp.ctypes.data, 128)
+        pp = pp[:mp].astype(np.int64)
+        blk3 = blk[-mp:]
+        for L in (3, 2, 1, 0):
+            sel = np.where(lv_b[-mp:] == L)[0]
+            if not len(sel):
+                continue
+            b2 = blk3[sel, :32, 1][:, :, None]
+            st = pp[sel]  # launches x 32 x 16 x 5
+            print(f"L({L}) per wave (blocks < 32, p50 us): start after B2 | quotients | samples | six sums | 28 sums")
+            for w in range(12):
+                ok = st[:, :, w, 0] > 0
+                if not ok.any():
+                    continue
+                s0 = (st[:, :, w, 0] - b2[:, :, 0])[ok] * us
+                d = [np.median((st[:, :, w, k] - st[:, :, w, k - 1])[ok]) * us for k in range(1, 5)]
+                print(f"   wave {w:2d}: {np.median(s0):5.2f} | " + " | ".join(f"{x:5.2f}" for x in d))
     per = [(entry[i + 1] - entry[i]) * us for i in range(n - 1) if (lvl[i], lvl[i + 1]) in [(3, 2), (2, 1), (1, 0), (0, 3)]]
     print(f"entry-to-entry per launch in the chain: {np.mean(per):.2f} us")
 

@@ -39,6 +39,7 @@
 // whose photometric cost is exactly 0) is executed faithfully by each
 // workgroup on its own, re-evaluating every tile into private scratch.
 #include <algorithm>
+#include <cstring>
 
 #include "device_math.hpp"
 #include "direct_solve.hpp"
@@ -66,6 +67,18 @@ __device__ unsigned long long g_pblk[kPRingB][256][4];  // entry, after B2, wave
 // per block of the last kPRingB launches: [w] wave w's points evaluated
 // (w < 16), [15] the last arriver's tile trees stored
 __device__ unsigned long long g_pwave[kPRingB][256][16];
+#ifdef VISO_PROBE_PT
+// (probe) phases of each wave's point in blocks < 32 of the last 128
+// launches: entry, quotients, samples, six sums reduced, 28 sums formed
+constexpr int kPtRing = 128, kPtBlocks = 32, kPtStamps = 5;
+__device__ unsigned long long g_ppt[kPtRing][kPtBlocks][16][kPtStamps];
+#define PPT(k)                                                                                       \
+    do {                                                                                             \
+        if (blockIdx.x < kPtBlocks && (threadIdx.x & 63) == 0)                                       \
+            g_ppt[a.probe_seq & (kPtRing - 1)][blockIdx.x][threadIdx.x >> 6][(k)] =                  \
+                __builtin_amdgcn_s_memrealtime();                                                    \
+    } while (0)
+#endif
 #define PROBE_DECL()                                \
     __shared__ unsigned long long pst[kPSt];        \
     const unsigned long long probe_t0 = __builtin_amdgcn_s_memrealtime()
@@ -77,6 +90,9 @@ __device__ unsigned long long g_pwave[kPRingB][256][16];
 #else
 #define PROBE_DECL()
 #define PST(k)
+#endif
+#ifndef VISO_PROBE_PT
+#define PPT(k) ((void)0)
 #endif
 
 namespace viso {
@@ -525,8 +541,10 @@ __device__ inline bool direct_point_rs(const DirectArgs& a, const LevelPair& fp,
     const double scale = kScale[lv];
     const int w = a.g.w[lv], h = a.g.h[lv];
     // project_px and d_pixel_d_xi (bit-identical; divisions lane-parallel)
+    PPT(0);
     double Q[2];
     const double jq = point_quotients(a.K, cur_pose, r.P, scale, Q, qt);
+    PPT(1);
     const double uc = scale * (Q[0] * a.K.fx + a.K.cx);
     const double vc = scale * (Q[1] * a.K.fy + a.K.cy);
     const double hp = 4.0;
@@ -591,8 +609,10 @@ __device__ inline bool direct_point_rs(const DirectArgs& a, const LevelPair& fp,
     // dPixel/dXi constant over the patch, so sum_p J J^T = Jp^T G Jp and
     // sum_p -e J = Jp^T (sum_p e g) with G = sum_p g g^T: six pixel sums
     // (descending-xor trees, oracle tree_sum_desc64) instead of 28
+    PPT(2);
     const double leaf[6] = {g0 * g0, g0 * g1, g1 * g1, error * g0, error * g1, error * error};
     const double s = reduce_scatter_6_desc(leaf);
+    PPT(3);
     // lane k < 28 forms sum k from the six and its four J entries
     const unsigned sa = src_lanes;
     const double p0a = bperm_f64(jq, (int)(sa & 0xff)), p1a = bperm_f64(jq, (int)((sa >> 8) & 0xff));
@@ -608,6 +628,7 @@ __device__ inline bool direct_point_rs(const DirectArgs& a, const LevelPair& fp,
         o = S5;
     *out = o;
     *idx = lane < kSums ? lane : -1;
+    PPT(4);
     return true;
 }
 
@@ -2088,6 +2109,24 @@ extern "C" int viso_debug_probe_ring(unsigned long long* log, unsigned long long
     }
     return 0;
 }
+
+#ifdef VISO_PROBE_PT
+// (probe) per-point phase stamps (g_ppt) of the last min(cap, n, 128)
+// launches, in launch order: out[i][b < 32][wave < 16][5]
+extern "C" int viso_debug_probe_points(unsigned long long* out, int cap) {
+    using namespace viso;
+    static unsigned long long h[kPtRing][kPtBlocks][16][kPtStamps];
+    if (hipDeviceSynchronize() != hipSuccess) return -2;
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_ppt), sizeof(h)) != hipSuccess) return -2;
+    const int n = (int)g_probe_host_seq;
+    const int m = std::min(std::min(cap, n), kPtRing);
+    for (int i = 0; i < m; ++i) {
+        const int s = (n - m + i) & (kPtRing - 1);
+        std::memcpy(out + (size_t)i * kPtBlocks * 16 * kPtStamps, &h[s][0][0][0], sizeof(h[s]));
+    }
+    return m;
+}
+#endif
 
 // (probe) window misses per level since the last reset: out[8] (g_pfb)
 extern "C" int viso_debug_probe_window_misses(unsigned long long* out, int reset) {
