@@ -692,7 +692,16 @@ def main():
     # path on a one-GPU box (tests/test_multi.py); the product path is RCCL
     backend = os.environ.get("VISO_DIST_BACKEND", "nccl")
     if distributed:
-        local = local % max(torch.cuda.device_count(), 1)
+        n_dev = max(torch.cuda.device_count(), 1)
+        if world > n_dev and os.environ.get("VISO_LK_BG") is None:
+            # ranks sharing a GPU (the gloo rehearsal on a one-GPU box): LK
+            # alignment batched after each chunk's chain, not as a
+            # chunk-resident grid -- two processes' resident grids and chains
+            # on the same CUs can hold each other back past the grid's bounded
+            # waits; one GPU per rank keeps the default
+            os.environ["VISO_LK_BG"] = "0"
+            log(f"[rank {rank}] {world} ranks on {n_dev} GPU(s): background LK alignment off (VISO_LK_BG=0)")
+        local = local % n_dev
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
