@@ -196,6 +196,10 @@ struct viso_ctx {
     // ---------------- initialisation tracks (Viso::Initialization, include/viso.h:33-41)
     viso::DevBuf kp1, kp2, kp1b, kp2b, track_success, n_track_dev;
     viso::FastScratch fast;
+    // the detection frame's FAST tiles fused into its one-image ingest's
+    // level-1 launch (FastPre; fast_pre_slot: that frame's slot, or -1)
+    viso::FastPre fast_pre;
+    int fast_pre_slot = -1;
     viso::DevBuf fast_rows;
     int n_track = 0;             // < 0: on the device only (ntrack_pending)
     bool ntrack_pending = false;  // a re-detection frame's count not read yet

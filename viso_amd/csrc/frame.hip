@@ -462,6 +462,7 @@ void viso_ctx::launch_ingest_pyramid(const uint8_t* const* l0, uint8_t* const* d
     if (!st) st = stream;
     const int s = sl[n - 1];
     PyrOwn own{n - 1, state != VISO_STATE_RUNNING ? pose_of(s) : nullptr, false};
+    if (n == 1 && st == stream && fast_pre_slot == s && fast_pre.img) own.fast = &fast_pre;
     if (bg_words) {  // the chunk's background-LK words (bg_begin), cleared by the tail launch
         // (the set the next chunk uses: two sets alternate, so the previous
         // chunk's grid and drain, which may still run on lk_stream, read the
@@ -1323,9 +1324,13 @@ int viso_ctx::on_new_frame(int cur) {
                 {
                     TimedRegion t(timing, VISO_KERNEL_FAST, stream);
                     const FastDetect det{(float2*)kp2.ptr, h_int_dev + 3};
+                    // (tiles already run by the ingest's level-1 launch: FastPre)
+                    const bool pre = fast_pre.done && fast_pre_slot == cur;
                     launch_fast(frame(cur).l[0], g.w[0], g.h[0], p.fast_thresh, fast,
                                 (float2*)kp1.ptr, nullptr, p.max_features, (int*)n_track_dev.ptr,
-                                stream, &det);
+                                stream, &det, pre);
+                    fast_pre = FastPre{};
+                    fast_pre_slot = -1;
                 }
                 VISO_HIP_CHECK(hipGetLastError());
                 VISO_HIP_CHECK(hipEventRecord(ntrack_evt, stream));
@@ -1441,6 +1446,21 @@ int viso_ctx::ingest_chunk(const std::vector<int>& sl, const std::vector<const u
     // a background-LK chunk's words are cleared by the pyramid's tail
     // launch (bg_begin then makes no memset launch)
     const bool bg = bg_eligible() && nb <= kLkBatch;
+    // a one-frame chunk whose frame starts with FAST (the monocular
+    // initialisation's detection frame, src/viso.cpp:100-108: no reference
+    // keypoints to track yet) runs the FAST tiles in the pyramid's level-1
+    // launch (FastPre); on_new_frame then only orders them
+    fast_pre = FastPre{};
+    fast_pre_slot = -1;
+    if (nb == 1 && state == VISO_STATE_INITIALIZATION && !(stereo_base > 0 && !right.empty() && right[0]) &&
+        !(frame_cnt > 0 && frame_cnt <= p.reinitialize_after)) {
+        fast_pre.img = l0[0];
+        fast_pre.w = geom.w[0];
+        fast_pre.h = geom.h[0];
+        fast_pre.thresh = p.fast_thresh;
+        fast_pre.s = fast;
+        fast_pre_slot = sl[0];
+    }
     launch_ingest_pyramid(l0.data(), dst.data(), sl.data(), nb, bg);
     if (hipGetLastError() != hipSuccess) {
         for (int s : sl) drop(s);
@@ -1457,6 +1477,8 @@ int viso_ctx::ingest_chunk(const std::vector<int>& sl, const std::vector<const u
     // chunk's borrowed frames (the pending final solve, the LK batch),
     // give retained frames their own level 0, release the chunk's holds
     auto end_chunk = [&](int rc) -> int {
+        fast_pre = FastPre{};  // (consumed by its frame's FAST, or unused)
+        fast_pre_slot = -1;
         const int r1 = finish_call(stream, overlap_tail && !rc);
         if (!rc) rc = r1;
         const int roles[2] = {ref_slot, last_slot};

@@ -342,15 +342,17 @@ __device__ inline void sk_band(const SkBand& b, const PkEdge& e, int lane) {
     }
 }
 
+// (the body of pyr_down_sk_kernel for workgroup (bx, by); pyr1_fast_kernel
+// runs it for its first workgroups)
 template <int BH, int D>
-__global__ __launch_bounds__(256) void pyr_down_sk_kernel(PyrLevelArgs a) {
+__device__ __forceinline__ void pyr_down_sk_body(const PyrLevelArgs& a, int bx, int by) {
     const int lane = threadIdx.x & 63;
     // everything that depends only on the wave's unit is wave-uniform: keep
     // it in SGPRs (readfirstlane) so the VALU only does the per-lane work
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    int img = (int)blockIdx.y, blk = (int)blockIdx.x;
+    int img = by, blk = bx;
     if (a.xcd_per > 0) {
-        const int w = ((int)blockIdx.x & 7) * a.xcd_per + ((int)blockIdx.x >> 3);
+        const int w = (bx & 7) * a.xcd_per + (bx >> 3);
         img = w / a.bpi;
         blk = w - img * a.bpi;
         if (img >= a.n_img) return;  // block-uniform (no barrier in this kernel)
@@ -418,6 +420,11 @@ __global__ __launch_bounds__(256) void pyr_down_sk_kernel(PyrLevelArgs a) {
         }
     }
 #endif
+}
+
+template <int BH, int D>
+__global__ __launch_bounds__(256) void pyr_down_sk_kernel(PyrLevelArgs a) {
+    pyr_down_sk_body<BH, D>(a, (int)blockIdx.x, (int)blockIdx.y);
 }
 
 // ---------------------------------------------------------------- pyramid tail
@@ -785,15 +792,16 @@ __device__ inline u16x2 ft_run9(u16x2 m) {
     return a3 & ft_rot<8>(m);
 }
 
-__global__ __launch_bounds__(256) void fast_tile_kernel(const uint8_t* __restrict__ img, int w, int h,
-                                                        int thresh, int ntx, int* __restrict__ cnt,
-                                                        int* __restrict__ tot, int* __restrict__ lst) {
+// (the body of fast_tile_kernel for tile (tx, ty); pyr1_fast_kernel runs it
+// for its workgroups past the level-1 ones)
+__device__ __forceinline__ void fast_tile_body(const uint8_t* __restrict__ img, int w, int h, int thresh, int ntx,
+                                               int* __restrict__ cnt, int* __restrict__ tot,
+                                               int* __restrict__ lst, const int tx, const int ty) {
     __shared__ __attribute__((aligned(16))) uint8_t s_pa[kFtPRows][kFtPStride];  // pixel index i at i
     __shared__ __attribute__((aligned(16))) uint8_t s_pb[kFtPRows][kFtPStride];  // pixel index i at i - 2
     __shared__ __attribute__((aligned(16))) uint8_t s_sc[kFtSRows][128];
     __shared__ uint16_t s_list[4][kFtList];
     __shared__ int s_tot;
-    const int tx = blockIdx.x, ty = blockIdx.y;
     // output columns [ox, ox + 126), rows [oy, oy + kFtRows); score column j
     // is x = ox - 1 + j, score row r is y = oy - 1 + r; pixel index i is
     // x = ox - 4 + i, pixel row q is y = oy - 4 + q
@@ -912,6 +920,36 @@ __global__ __launch_bounds__(256) void fast_tile_kernel(const uint8_t* __restric
     if (t == 0) tot[(size_t)ty * ntx + tx] = s_tot;
 }
 
+__global__ __launch_bounds__(256) void fast_tile_kernel(const uint8_t* __restrict__ img, int w, int h,
+                                                        int thresh, int ntx, int* __restrict__ cnt,
+                                                        int* __restrict__ tot, int* __restrict__ lst) {
+    fast_tile_body(img, w, h, thresh, ntx, cnt, tot, lst, (int)blockIdx.x, (int)blockIdx.y);
+}
+
+// A one-image level-1 launch with the image's FAST tiles as extra
+// workgroups (FastPre): workgroups [0, n_pyr) are pyr_down_sk_kernel's (its
+// XCD-dealt 1-D form: n_pyr = 8 xcd_per), the rest FAST tiles in row-major
+// order.  The two share nothing but the launch: level 1 and the tiles both
+// only read level 0.
+struct FastTileArgs {
+    const uint8_t* img;
+    int w, h, thresh, ntx;
+    int* cnt;
+    int* tot;
+    int* lst;
+};
+
+template <int BH, int D>
+__global__ __launch_bounds__(256) void pyr1_fast_kernel(PyrLevelArgs a, int n_pyr, FastTileArgs f) {
+    const int b = (int)blockIdx.x;
+    if (b < n_pyr) {
+        pyr_down_sk_body<BH, D>(a, b, 0);
+        return;
+    }
+    const int t = b - n_pyr;
+    fast_tile_body(f.img, f.w, f.h, f.thresh, f.ntx, f.cnt, f.tot, f.lst, t % f.ntx, t / f.ntx);
+}
+
 __global__ __launch_bounds__(256) void fast_order_kernel(int h, int ntx, int nty, const int* __restrict__ cnt,
                                                          const int* __restrict__ tot,
                                                          const int* __restrict__ lst, int cap,
@@ -1026,8 +1064,13 @@ bool pf_plan(const PyrGeom& g, int n, PyrTailArgs& a, size_t& lds) {
 // one per-level launch (level l from level l-1) over nb images: the
 // register-only streaming form for level 1 at least 8 columns wide, the
 // LDS-staged form for the tiny levels of images the tail does not take
+void fast_dims(int w, int h, int* ntx, int* nty) {
+    *ntx = (w + kFtCols - 1) / kFtCols;
+    *nty = (h + kFtRows - 1) / kFtRows;
+}
+
 void launch_pyr_level(const PyrGeom& g, int l, const uint8_t* const* l0, uint8_t* const* slot, int nb,
-                      hipStream_t stream) {
+                      hipStream_t stream, FastPre* fp = nullptr) {
     PyrLevelArgs a;
     for (int i = 0; i < nb; ++i) {
         a.src[i] = l == 1 ? l0[i] : slot[i] + g.off[l - 1];
@@ -1045,6 +1088,15 @@ void launch_pyr_level(const PyrGeom& g, int l, const uint8_t* const* l0, uint8_t
         a.bpi = (a.units + 3) / 4;
         a.n_img = nb;
         a.xcd_per = (a.bpi * nb + 7) / 8;
+        if (fp && nb == 1 && small) {
+            FastTileArgs f{fp->img, fp->w, fp->h, fp->thresh < 0 ? 0 : (fp->thresh > 255 ? 255 : fp->thresh), 0,
+                           fp->s.cnt, fp->s.tot, fp->s.lst};
+            int nty;
+            fast_dims(fp->w, fp->h, &f.ntx, &nty);
+            pyr1_fast_kernel<kSkBHs, kSkRings><<<8 * a.xcd_per + f.ntx * nty, 256, 0, stream>>>(a, 8 * a.xcd_per, f);
+            fp->done = true;
+            return;
+        }
         if (small)
             pyr_down_sk_kernel<kSkBHs, kSkRings><<<8 * a.xcd_per, 256, 0, stream>>>(a);
         else
@@ -1074,7 +1126,7 @@ void launch_pyramid_frames(const PyrGeom& g, const uint8_t* const* l0, uint8_t* 
         // this launch's image of `own`, or -1
         const int oi = own && own->img >= b0 && own->img < b0 + nb ? own->img - b0 : -1;
         bool copy = oi >= 0 && l0[b0 + oi] != slot[b0 + oi];
-        launch_pyr_level(g, 1, l0 + b0, slot + b0, nb, stream);
+        launch_pyr_level(g, 1, l0 + b0, slot + b0, nb, stream, own && n == 1 ? own->fast : nullptr);
         PyrTailArgs ta;
         size_t lds = 0;
         if (pf_plan(g, nb, ta, lds)) {
@@ -1121,10 +1173,6 @@ void launch_pyramid(const PyrGeom& g, uint8_t* base, int n_images, size_t img_st
     launch_pyramid_frames(g, l0.data(), slot.data(), n_images, stream);
 }
 
-static void fast_dims(int w, int h, int* ntx, int* nty) {
-    *ntx = (w + kFtCols - 1) / kFtCols;
-    *nty = (h + kFtRows - 1) / kFtRows;
-}
 
 size_t fast_scratch_bytes(int w, int h) {
     int ntx, nty;
@@ -1145,11 +1193,13 @@ FastScratch fast_scratch_at(void* base, int w, int h) {
 }
 
 void launch_fast(const uint8_t* img, int w, int h, int thresh, FastScratch& s, float2* kp_out,
-                 int4* raw_out, int cap, int* n_out, hipStream_t stream, const FastDetect* det) {
+                 int4* raw_out, int cap, int* n_out, hipStream_t stream, const FastDetect* det, bool tiles_done) {
     int ntx, nty;
     fast_dims(w, h, &ntx, &nty);
     thresh = thresh < 0 ? 0 : (thresh > 255 ? 255 : thresh);
-    fast_tile_kernel<<<dim3(ntx, nty), 256, 0, stream>>>(img, w, h, thresh, ntx, s.cnt, s.tot, s.lst);
+    // (tiles_done: the ingest's level-1 launch ran them, FastPre)
+    if (!tiles_done)
+        fast_tile_kernel<<<dim3(ntx, nty), 256, 0, stream>>>(img, w, h, thresh, ntx, s.cnt, s.tot, s.lst);
     fast_order_kernel<<<nty, 256, 0, stream>>>(h, ntx, nty, s.cnt, s.tot, s.lst, cap, kp_out, raw_out, n_out,
                                                det ? det->kp_copy : nullptr, det ? det->host_n : nullptr,
                                                det ? 1 : 0);

@@ -22,16 +22,6 @@ constexpr int kPyrBatch = 128;
 // launches folded into it).
 // zero (optional): n_zero ints cleared by the same launch (the chunk's
 // background-LK words, bg_begin).
-struct PyrOwn {
-    int img;
-    double* ident_pose;
-    bool copied;
-    int* zero = nullptr;
-    int n_zero = 0;
-};
-void launch_pyramid_frames(const PyrGeom& g, const uint8_t* const* l0, uint8_t* const* slot,
-                           int n, hipStream_t stream, PyrOwn* own = nullptr);
-
 // FAST device scratch (image.hip): per (row, tile) keypoint counts and
 // slots, per-tile totals; carved from fast_scratch_bytes(w, h) bytes.
 struct FastScratch {
@@ -39,6 +29,29 @@ struct FastScratch {
     int* tot = nullptr;  // [bands][tiles across]
     int* lst = nullptr;  // [h][tiles across][64]
 };
+
+// A one-image ingest whose frame starts with FAST (the initialisation's
+// detection frame): the FAST tiles of `img` (the frame's level 0) run as
+// extra workgroups of the level-1 launch (pyr1_fast_kernel) instead of a
+// launch of their own behind the pyramid; done = they were launched, so the
+// frame's launch_fast only orders them (tiles_done).
+struct FastPre {
+    const uint8_t* img = nullptr;
+    int w = 0, h = 0, thresh = 0;
+    FastScratch s;
+    bool done = false;
+};
+
+struct PyrOwn {
+    int img;
+    double* ident_pose;
+    bool copied;
+    int* zero = nullptr;
+    int n_zero = 0;
+    FastPre* fast = nullptr;
+};
+void launch_pyramid_frames(const PyrGeom& g, const uint8_t* const* l0, uint8_t* const* slot,
+                           int n, hipStream_t stream, PyrOwn* own = nullptr);
 size_t fast_scratch_bytes(int w, int h);
 FastScratch fast_scratch_at(void* base, int w, int h);
 // FAST + NMS on a level-0 image; writes up to cap keypoints (float2 and/or
@@ -51,7 +64,8 @@ struct FastDetect {
     int* host_n;
 };
 void launch_fast(const uint8_t* img, int w, int h, int thresh, FastScratch& s, float2* kp_out,
-                 int4* raw_out, int cap, int* n_out, hipStream_t stream, const FastDetect* det = nullptr);
+                 int4* raw_out, int cap, int* n_out, hipStream_t stream, const FastDetect* det = nullptr,
+                 bool tiles_done = false);
 
 // ---------------------------------------------------------------- tracking
 // OpticalFlowMultiLevel(inverse=true): kp2 in/out, success out (level 0).
