@@ -170,6 +170,12 @@ int viso_ctx::init() {
     if (!rc) rc = lk_succ.ensure((size_t)kMaxMapPoints * kLkBatch);
     if (!rc) rc = lk_before.ensure(16 * (size_t)kMaxMapPoints * kLkBatch);
     if (!rc) rc = lk_after.ensure(16 * (size_t)kMaxMapPoints * kLkBatch);
+    // the LK-alignment templates at their largest map (96 MiB): a map's
+    // creation (an initialisation frame, timed as one) then allocates nothing
+    if (!rc) rc = lk_tmpl.ensure((size_t)kMaxMapPoints * kLevels * 192 * 8);
+    if (!rc) rc = lk_tmpl_h.ensure((size_t)kMaxMapPoints * kLevels * 4 * 8);
+    if (!rc) rc = lk_tmpl_kf.ensure((size_t)kMaxMapPoints * 4);
+    if (!rc) rc = lk_tmpl_uv.ensure((size_t)kMaxMapPoints * 16);
     if (!rc) rc = pose_log.ensure(96 * (size_t)std::max(p.max_poses, 1));
     if (rc) return rc;
     direct = direct_scratch_at(direct_buf.ptr);
